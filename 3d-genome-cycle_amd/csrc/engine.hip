@@ -1,0 +1,1105 @@
+// engine.hip -- host side of the gcs engine and its C ABI (include/gcs.h).
+//
+// The engine owns all device memory of one simulated system on one HIP device/stream.  Force fields are
+// registered like md::system::add_forcefield (returning a handle that gcs_remove_forcefield accepts) and
+// compiled lazily into flat device tables (bonded CSR, bending table, tethers, point sources, walls)
+// before the next launch.  gcs_engine_run replaces md::simulate_brownian_dynamics: the per-step callback's
+// state updates run on the device (k_tail), and chunks of steps are replayed from a captured hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gcs.h"
+#include "engine_internal.hpp"
+
+using namespace gcs;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+#define HIPCHK(call)                                                                                        \
+    do {                                                                                                    \
+        hipError_t e_ = (call);                                                                             \
+        if (e_ != hipSuccess) return fail(GCS_EHIP, std::string(#call) + ": " + hipGetErrorString(e_));     \
+    } while (0)
+
+enum FieldKind { F_SOFTCORE = 1, F_SOFTWELL, F_BONDED, F_BENDING, F_WALL_IN, F_WALL_OUT, F_POINT, F_KFIBER };
+
+struct FieldRec {
+    int kind = 0;
+    int handle = 0;
+    gcs_softcore_params sc{};
+    gcs_softwell_params sw{};
+    gcs_bond_params bond{};
+    gcs_wall_params wall{};
+    gcs_point_source_params point{};
+    double spring = 0, energy = 0;
+    double center[3] = {0, 0, 0};
+    double pole[3] = {0, 0, 0};
+    std::vector<int64_t> idx;
+    std::vector<gcs_kinetochore_spec> specs;
+};
+
+template <class T>
+int dalloc(T** p, size_t count)
+{
+    *p = nullptr;
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+    if (e != hipSuccess) return fail(GCS_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return GCS_OK;
+}
+
+template <class T>
+void dfree(T*& p)
+{
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+}  // namespace
+
+struct gcs_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int n = 0;
+    std::vector<double> mu, ab;
+    std::vector<FieldRec> fields;
+    int next_handle = 1;
+    bool dirty = true;
+    int topo_version = 0;
+    int ncell_max = 0;
+
+    // device state
+    float4* pos[2] = {nullptr, nullptr};
+    float4* kmu = nullptr;
+    float4* spos = nullptr;
+    float* sb = nullptr;
+    int *sidx = nullptr, *scell = nullptr, *cell_of = nullptr, *slot = nullptr, *tmp = nullptr;
+    int *count = nullptr, *cstart = nullptr;
+    DevCtx* ctx = nullptr;
+    double* dsched = nullptr;
+    float* part_force = nullptr;
+    float* part_bbox = nullptr;
+    double* part_energy = nullptr;
+    float4* force_out = nullptr;
+    // topology tables
+    int* boff = nullptr;
+    int2* bent = nullptr;
+    BondParam* bpar = nullptr;
+    float* bend_eps = nullptr;
+    int* toff = nullptr;
+    Tether* tent = nullptr;
+    // injected noise
+    float* noise = nullptr;
+    int64_t noise_steps = 0;
+    int64_t noise_cursor = 0;  // host mirror
+    // search scratch
+    int search_cap = 0;
+    float4 *s_pts = nullptr, *s_spos = nullptr;
+    float* s_sb = nullptr;
+    int *s_sidx = nullptr, *s_scell = nullptr, *s_cell_of = nullptr, *s_slot = nullptr, *s_tmp = nullptr;
+    int *s_count = nullptr, *s_cstart = nullptr, *s_counts = nullptr, *s_offsets = nullptr, *s_total = nullptr;
+    int s_ncell_max = 0;
+    DevCtx* s_ctx = nullptr;
+    unsigned long long *s_keys = nullptr, *s_keys2 = nullptr;
+    void* s_sort_temp = nullptr;
+    size_t s_sort_bytes = 0;
+    int64_t s_key_cap = 0;
+
+    ForceArgs fa{};
+    gcs_schedule sched{};
+    int sched_flags = 0;
+    int parity = 0;  // host mirror of ctx->parity
+
+    // options / graph cache
+    int graph_steps = 32;
+    int waves = 4;
+    hipGraphExec_t gexec = nullptr;
+    hipGraph_t graph = nullptr;
+    int g_steps = 0, g_waves = 0, g_version = -1, g_spacestep = -1;
+    gcs_bd_config g_cfg{};
+    int g_sched_flags = -1;
+};
+
+namespace {
+
+void drop_graph(gcs_engine* e)
+{
+    if (e->gexec) (void)hipGraphExecDestroy(e->gexec);
+    if (e->graph) (void)hipGraphDestroy(e->graph);
+    e->gexec = nullptr;
+    e->graph = nullptr;
+}
+
+FieldRec* new_field(gcs_engine* e, int kind)
+{
+    e->fields.emplace_back();
+    FieldRec& f = e->fields.back();
+    f.kind = kind;
+    f.handle = e->next_handle++;
+    e->dirty = true;
+    return &f;
+}
+
+bool valid_index(const gcs_engine* e, int64_t i) { return i >= 0 && i < e->n; }
+
+// Flatten the registered fields into device tables (DESIGN.md "device layout").
+int compile(gcs_engine* e)
+{
+    if (!e->dirty) return GCS_OK;
+    const int n = e->n;
+    ForceArgs& a = e->fa;
+    a.has_pair = 0;
+    a.has_bonds = 0;
+    a.has_bend = 0;
+    a.has_tether = 0;
+    a.n_point = 0;
+    a.has_wall_in = 0;
+    a.has_wall_out = 0;
+
+    std::vector<std::vector<int2>> blist(n);
+    std::vector<BondParam> params;
+    std::vector<float> bend(n, 0.f);
+    std::vector<std::vector<Tether>> tlist(n);
+    int pair_mix = 1;
+
+    for (const FieldRec& f : e->fields) {
+        switch (f.kind) {
+        case F_SOFTCORE:
+            if (a.has_pair) return fail(GCS_EINVAL, "only one neighbor soft-core field may be active");
+            a.has_pair = 1;
+            a.pair_mix = f.sc.mix ? 1 : 0;
+            pair_mix = a.pair_mix;
+            a.pair_scaled = f.sc.scaled ? 1 : 0;
+            a.pa_eps = (float)f.sc.a_energy;
+            a.pa_sig = (float)f.sc.a_diameter;
+            a.pb_eps = (float)f.sc.b_energy;
+            a.pb_sig = (float)(f.sc.b_diameter > 0 ? f.sc.b_diameter : 1.0);
+            if (!f.sc.mix) a.pb_eps = 0.f;
+            a.pair_dist = (float)f.sc.neighbor_distance;
+            break;
+        case F_SOFTWELL: {
+            BondParam bp{};
+            bp.type = kSoftwell;
+            bp.ka = (float)f.sw.energy;
+            bp.kb = (float)(1.0 / (f.sw.decay_distance * f.sw.decay_distance));
+            bp.la = (float)(f.sw.cutoff * f.sw.cutoff);
+            const int pid = (int)params.size();
+            params.push_back(bp);
+            for (size_t p = 0; p < f.idx.size(); ++p)
+                for (size_t q = 0; q < f.idx.size(); ++q)
+                    if (p != q && f.idx[p] != f.idx[q]) blist[f.idx[p]].push_back(make_int2((int)f.idx[q], pid));
+            break;
+        }
+        case F_BONDED: {
+            // a field whose spring constants are all zero contributes exactly nothing (the reference's
+            // i,i+2 loop field with a/b_core_2nd_bond_spring = 0, simulation_driver_forcefield.cpp:99-136)
+            if (f.bond.a_spring == 0 && f.bond.b_spring == 0) break;
+            BondParam bp{};
+            bp.type = f.bond.potential == GCS_POT_HARMONIC ? kHarmonic
+                      : (f.bond.potential == GCS_POT_SPRING ? kSpring : kSemispring);
+            bp.mix = f.bond.mix ? 1 : 0;
+            bp.scaled = f.bond.scaled ? 1 : 0;
+            bp.ka = (float)f.bond.a_spring;
+            bp.kb = (float)f.bond.b_spring;
+            bp.la = (float)f.bond.a_length;
+            bp.lb = (float)f.bond.b_length;
+            const int pid = (int)params.size();
+            params.push_back(bp);
+            for (size_t q = 0; q + 1 < f.idx.size(); q += 2) {
+                const int i = (int)f.idx[q], j = (int)f.idx[q + 1];
+                blist[i].push_back(make_int2(j, pid));
+                blist[j].push_back(make_int2(i, pid));
+            }
+            break;
+        }
+        case F_BENDING:
+            for (int64_t k : f.idx) bend[k] += (float)f.energy;
+            break;
+        case F_WALL_IN:
+            if (a.has_wall_in) return fail(GCS_EINVAL, "only one ellipsoid inward field may be active");
+            a.has_wall_in = 1;
+            a.win.a_eps = (float)f.wall.a_energy;
+            a.win.a_sig = (float)f.wall.a_diameter;
+            a.win.b_eps = (float)f.wall.b_energy;
+            a.win.b_sig = (float)(f.wall.b_diameter > 0 ? f.wall.b_diameter : 1.0);
+            a.win.wall_a = (float)f.wall.wall_a;
+            a.win.wall_b = (float)f.wall.wall_b;
+            a.win.cx = (float)f.wall.center[0];
+            a.win.cy = (float)f.wall.center[1];
+            a.win.cz = (float)f.wall.center[2];
+            a.win.mix = f.wall.mix ? 1 : 0;
+            a.win.scaled = f.wall.scaled ? 1 : 0;
+            if (!f.wall.mix) a.win.b_eps = 0.f;
+            break;
+        case F_WALL_OUT:
+            if (a.has_wall_out) return fail(GCS_EINVAL, "only one ellipsoid outward field may be active");
+            a.has_wall_out = 1;
+            a.wout_k = (float)f.spring;
+            a.wout_cx = (float)f.center[0];
+            a.wout_cy = (float)f.center[1];
+            a.wout_cz = (float)f.center[2];
+            break;
+        case F_POINT: {
+            if (a.n_point >= kMaxPointSources) return fail(GCS_EINVAL, "too many point-source fields (max 4)");
+            PointSrc& p = a.point[a.n_point++];
+            p.type = f.point.potential;
+            p.px = (float)f.point.point[0];
+            p.py = (float)f.point.point[1];
+            p.pz = (float)f.point.point[2];
+            p.k = (float)f.point.spring;
+            p.l = (float)f.point.length;
+            p.f = (float)f.point.force;
+            p.b = (float)f.point.reactive_distance;
+            break;
+        }
+        case F_KFIBER:
+            for (const gcs_kinetochore_spec& sp : f.specs) {
+                Tether t{};
+                t.px = (float)f.pole[0];
+                t.py = (float)f.pole[1];
+                t.pz = (float)f.pole[2];
+                t.k = (float)(sp.decay_rate / sp.mobility);  // kinetochore_fiber_forcefield.cpp:46-53
+                t.l = (float)sp.stationary_length;
+                tlist[sp.particle_index].push_back(t);
+            }
+            break;
+        }
+    }
+    if (a.has_wall_in && a.has_wall_out) {
+        if (a.win.cx != a.wout_cx || a.win.cy != a.wout_cy || a.win.cz != a.wout_cz)
+            return fail(GCS_EINVAL, "inward and outward ellipsoid fields must share the centre");
+    }
+
+    // per-particle constants {mu, a, b, 0}
+    std::vector<float4> hk(n);
+    for (int i = 0; i < n; ++i) hk[i] = make_float4((float)e->mu[i], (float)e->ab[2 * i], (float)e->ab[2 * i + 1], 0.f);
+    HIPCHK(hipMemcpyAsync(e->kmu, hk.data(), n * sizeof(float4), hipMemcpyHostToDevice, e->stream));
+    (void)pair_mix;
+
+    dfree(e->boff);
+    dfree(e->bent);
+    dfree(e->bpar);
+    dfree(e->bend_eps);
+    dfree(e->toff);
+    dfree(e->tent);
+
+    size_t nb = 0;
+    for (auto& l : blist) nb += l.size();
+    if (nb > 0) {
+        std::vector<int> off(n + 1, 0);
+        std::vector<int2> ent;
+        ent.reserve(nb);
+        for (int i = 0; i < n; ++i) {
+            off[i] = (int)ent.size();
+            ent.insert(ent.end(), blist[i].begin(), blist[i].end());
+        }
+        off[n] = (int)ent.size();
+        int rc;
+        if ((rc = dalloc(&e->boff, n + 1))) return rc;
+        if ((rc = dalloc(&e->bent, ent.size()))) return rc;
+        if ((rc = dalloc(&e->bpar, params.size()))) return rc;
+        HIPCHK(hipMemcpyAsync(e->boff, off.data(), (n + 1) * sizeof(int), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipMemcpyAsync(e->bent, ent.data(), ent.size() * sizeof(int2), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipMemcpyAsync(e->bpar, params.data(), params.size() * sizeof(BondParam), hipMemcpyHostToDevice, e->stream));
+        a.has_bonds = 1;
+    }
+    bool any_bend = false;
+    for (float v : bend) any_bend |= (v != 0.f);
+    if (any_bend) {
+        int rc;
+        if ((rc = dalloc(&e->bend_eps, n))) return rc;
+        HIPCHK(hipMemcpyAsync(e->bend_eps, bend.data(), n * sizeof(float), hipMemcpyHostToDevice, e->stream));
+        a.has_bend = 1;
+    }
+    size_t nt = 0;
+    for (auto& l : tlist) nt += l.size();
+    if (nt > 0) {
+        std::vector<int> off(n + 1, 0);
+        std::vector<Tether> ent;
+        for (int i = 0; i < n; ++i) {
+            off[i] = (int)ent.size();
+            ent.insert(ent.end(), tlist[i].begin(), tlist[i].end());
+        }
+        off[n] = (int)ent.size();
+        int rc;
+        if ((rc = dalloc(&e->toff, n + 1))) return rc;
+        if ((rc = dalloc(&e->tent, ent.size()))) return rc;
+        HIPCHK(hipMemcpyAsync(e->toff, off.data(), (n + 1) * sizeof(int), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipMemcpyAsync(e->tent, ent.data(), ent.size() * sizeof(Tether), hipMemcpyHostToDevice, e->stream));
+        a.has_tether = 1;
+    }
+    a.boff = e->boff;
+    a.bent = e->bent;
+    a.bpar = e->bpar;
+    a.bend_eps = e->bend_eps;
+    a.toff = e->toff;
+    a.tent = e->tent;
+    HIPCHK(hipStreamSynchronize(e->stream));  // host vectors die here
+    e->dirty = false;
+    e->topo_version++;
+    drop_graph(e);
+    return GCS_OK;
+}
+
+void fill_state_args(gcs_engine* e)
+{
+    ForceArgs& a = e->fa;
+    a.n = e->n;
+    a.pos0 = e->pos[0];
+    a.pos1 = e->pos[1];
+    a.kmu = e->kmu;
+    a.spos = e->spos;
+    a.sb = e->sb;
+    a.sidx = e->sidx;
+    a.scell = e->scell;
+    a.cstart = e->cstart;
+    a.part_force = e->part_force;
+    a.part_bbox = e->part_bbox;
+    a.part_energy = e->part_energy;
+    a.force_out = e->force_out;
+    a.noise = e->noise;
+    a.noise_steps = e->noise_steps;
+}
+
+void enqueue_cells(gcs_engine* e)
+{
+    const int n = e->n;
+    launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count);
+    launch_cell_scan(e->stream, e->ctx, n, e->count, e->cstart);
+    launch_cell_scatter(e->stream, n, e->cell_of, e->slot, e->cstart, e->tmp);
+    launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, n, e->tmp, e->cell_of, e->cstart, e->sidx,
+                     e->scell, e->spos, e->sb, e->fa.has_pair ? e->fa.pair_mix : 1);
+}
+
+void enqueue_step(gcs_engine* e, bool spacestep, float spacestep_v, float timestep)
+{
+    const int fb = force_blocks(e->n);
+    enqueue_cells(e);
+    if (!spacestep) {
+        launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa);
+        launch_tail(e->stream, e->ctx, e->fa, fb, fb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
+    } else {
+        launch_force(e->stream, kModeForce, e->waves, e->ctx, e->fa);
+        launch_adapt(e->stream, e->ctx, e->fa, fb, spacestep_v, timestep);
+        launch_update(e->stream, e->ctx, e->fa);
+        launch_tail(e->stream, e->ctx, e->fa, fb, update_blocks(e->n), 1, e->sched_flags != 0, e->ncell_max, e->dsched);
+    }
+}
+
+int upload_sched(gcs_engine* e)
+{
+    double h[kSchedCount] = {0};
+    const gcs_schedule& s = e->sched;
+    e->sched_flags = (s.update_time ? 1 : 0) | (s.update_scales ? 2 : 0) | (s.update_wall ? 4 : 0);
+    h[kSchedFlags] = e->sched_flags;
+    h[kSchedDt] = s.timestep;
+    h[kSchedCs0] = s.core_scale_init;
+    h[kSchedCsTau] = s.core_scale_tau;
+    h[kSchedBs0] = s.bond_scale_init;
+    h[kSchedBsTau] = s.bond_scale_tau;
+    for (int k = 0; k < 3; ++k) h[kSchedK0 + k] = s.wall_semiaxes_spring[k];
+    h[kSchedMuW] = s.wall_mobility;
+    HIPCHK(hipMemcpyAsync(e->dsched, h, sizeof(h), hipMemcpyHostToDevice, e->stream));
+    return GCS_OK;
+}
+
+int set_ctx_field(gcs_engine* e, size_t offset, const void* src, size_t bytes)
+{
+    HIPCHK(hipMemcpyAsync((char*)e->ctx + offset, src, bytes, hipMemcpyHostToDevice, e->stream));
+    return GCS_OK;
+}
+
+int prepare(gcs_engine* e)
+{
+    HIPCHK(hipSetDevice(e->device));
+    int rc = compile(e);
+    if (rc) return rc;
+    fill_state_args(e);
+    return GCS_OK;
+}
+
+// compile, load the BD parameters into the kernel arguments, set the step counter, build the first grid
+int begin_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
+{
+    int rc = prepare(e);
+    if (rc) return rc;
+    ForceArgs& a = e->fa;
+    a.temperature = (float)cfg->temperature;
+    a.timestep = (float)cfg->timestep;
+    a.seed_lo = (unsigned)cfg->seed;
+    a.seed_hi = (unsigned)(cfg->seed >> 32);
+    a.noise_mode = cfg->noise;
+    long long st = first_step;
+    if ((rc = set_ctx_field(e, offsetof(DevCtx, step), &st, sizeof(st)))) return rc;
+    double dt = cfg->timestep;
+    if ((rc = set_ctx_field(e, offsetof(DevCtx, dt_used), &dt, sizeof(dt)))) return rc;
+    launch_prime(e->stream, e->ctx, a, 0.f, e->ncell_max);
+    HIPCHK(hipGetLastError());
+    return GCS_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------------
+// C ABI
+
+extern "C" {
+
+const char* gcs_last_error(void) { return g_last_error.c_str(); }
+
+int gcs_abi_version(void) { return GCS_ABI_VERSION; }
+
+int gcs_device_count(int32_t* count)
+{
+    int c = 0;
+    HIPCHK(hipGetDeviceCount(&c));
+    *count = c;
+    return GCS_OK;
+}
+
+int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
+{
+    if (!d || !out) return fail(GCS_EINVAL, "null argument");
+    *out = nullptr;
+    if (d->particle_count <= 0 || d->particle_count > (int64_t)1 << 30)
+        return fail(GCS_EINVAL, "particle_count must be in [1, 2^30]");
+    gcs_engine* e = new gcs_engine();
+    e->device = d->device;
+    e->n = (int)d->particle_count;
+    const int n = e->n;
+    e->mu.assign(n, 1.0);
+    e->ab.assign(2 * (size_t)n, 0.0);
+    for (int i = 0; i < n; ++i) {
+        if (d->mobilities) e->mu[i] = d->mobilities[i];
+        if (d->ab_factors) {
+            e->ab[2 * i] = d->ab_factors[2 * i];
+            e->ab[2 * i + 1] = d->ab_factors[2 * i + 1];
+        }
+    }
+    auto bail = [&](int rc) {
+        gcs_engine_destroy(e);
+        return rc;
+    };
+    hipError_t he = hipSetDevice(e->device);
+    if (he != hipSuccess) return bail(fail(GCS_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(he)));
+    he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (he != hipSuccess) return bail(fail(GCS_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(he)));
+    e->ncell_max = std::min(1 << 21, std::max(4096, 4 * n));
+    int rc = 0;
+    const int fb = force_blocks(n), ub = update_blocks(n);
+    if ((rc = dalloc(&e->pos[0], n)) || (rc = dalloc(&e->pos[1], n)) || (rc = dalloc(&e->kmu, n)) ||
+        (rc = dalloc(&e->spos, n)) || (rc = dalloc(&e->sb, n)) || (rc = dalloc(&e->sidx, n)) ||
+        (rc = dalloc(&e->scell, n)) || (rc = dalloc(&e->cell_of, n)) || (rc = dalloc(&e->slot, n)) ||
+        (rc = dalloc(&e->tmp, n)) || (rc = dalloc(&e->count, e->ncell_max + 2)) ||
+        (rc = dalloc(&e->cstart, e->ncell_max + 2)) || (rc = dalloc(&e->ctx, 1)) || (rc = dalloc(&e->dsched, kSchedCount)) ||
+        (rc = dalloc(&e->part_force, (size_t)std::max(fb, ub) * kForcePartials)) ||
+        (rc = dalloc(&e->part_bbox, (size_t)std::max(fb, ub) * kBBoxPartials)) ||
+        (rc = dalloc(&e->part_energy, (size_t)fb * kEnergyKinds)) || (rc = dalloc(&e->force_out, n)))
+        return bail(rc);
+    he = hipMemsetAsync(e->count, 0, (e->ncell_max + 2) * sizeof(int), e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->pos[0], 0, n * sizeof(float4), e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->pos[1], 0, n * sizeof(float4), e->stream);
+    DevCtx c{};
+    c.cs = 1.0;
+    c.bs = 1.0;
+    if (he == hipSuccess) he = hipMemcpyAsync(e->ctx, &c, sizeof(c), hipMemcpyHostToDevice, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    if (he != hipSuccess) return bail(fail(GCS_EHIP, std::string("engine init: ") + hipGetErrorString(he)));
+    if ((rc = upload_sched(e))) return bail(rc);
+    *out = e;
+    return GCS_OK;
+}
+
+int gcs_engine_destroy(gcs_engine* e)
+{
+    if (!e) return GCS_OK;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    drop_graph(e);
+    dfree(e->pos[0]);
+    dfree(e->pos[1]);
+    dfree(e->kmu);
+    dfree(e->spos);
+    dfree(e->sb);
+    dfree(e->sidx);
+    dfree(e->scell);
+    dfree(e->cell_of);
+    dfree(e->slot);
+    dfree(e->tmp);
+    dfree(e->count);
+    dfree(e->cstart);
+    dfree(e->ctx);
+    dfree(e->dsched);
+    dfree(e->part_force);
+    dfree(e->part_bbox);
+    dfree(e->part_energy);
+    dfree(e->force_out);
+    dfree(e->boff);
+    dfree(e->bent);
+    dfree(e->bpar);
+    dfree(e->bend_eps);
+    dfree(e->toff);
+    dfree(e->tent);
+    dfree(e->noise);
+    dfree(e->s_pts);
+    dfree(e->s_spos);
+    dfree(e->s_sb);
+    dfree(e->s_sidx);
+    dfree(e->s_scell);
+    dfree(e->s_cell_of);
+    dfree(e->s_slot);
+    dfree(e->s_tmp);
+    dfree(e->s_count);
+    dfree(e->s_cstart);
+    dfree(e->s_counts);
+    dfree(e->s_offsets);
+    dfree(e->s_total);
+    dfree(e->s_ctx);
+    dfree(e->s_keys);
+    dfree(e->s_keys2);
+    if (e->s_sort_temp) (void)hipFree(e->s_sort_temp);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return GCS_OK;
+}
+
+int gcs_engine_particle_count(const gcs_engine* e, int64_t* count)
+{
+    if (!e || !count) return fail(GCS_EINVAL, "null argument");
+    *count = e->n;
+    return GCS_OK;
+}
+
+int gcs_add_neighbor_softcore(gcs_engine* e, const gcs_softcore_params* p, int32_t* handle)
+{
+    if (!e || !p) return fail(GCS_EINVAL, "null argument");
+    if (!(p->a_diameter > 0) || !(p->neighbor_distance > 0) || (p->mix && !(p->b_diameter > 0)))
+        return fail(GCS_EINVAL, "soft-core diameters and neighbor distance must be positive");
+    FieldRec* f = new_field(e, F_SOFTCORE);
+    f->sc = *p;
+    if (handle) *handle = f->handle;
+    return GCS_OK;
+}
+
+int gcs_add_neighbor_softwell(gcs_engine* e, const gcs_softwell_params* p, const int64_t* targets, int64_t n_targets,
+                              int32_t* handle)
+{
+    if (!e || !p || (n_targets > 0 && !targets)) return fail(GCS_EINVAL, "null argument");
+    if (p->exponent != 6) return fail(GCS_EINVAL, "softwell exponent must be 6");
+    if (!(p->decay_distance > 0)) return fail(GCS_EINVAL, "softwell decay distance must be positive");
+    for (int64_t k = 0; k < n_targets; ++k)
+        if (!valid_index(e, targets[k])) return fail(GCS_EINVAL, "softwell target out of range");
+    FieldRec* f = new_field(e, F_SOFTWELL);
+    f->sw = *p;
+    f->idx.assign(targets, targets + n_targets);
+    if (handle) *handle = f->handle;
+    return GCS_OK;
+}
+
+int gcs_add_bonded_pairwise(gcs_engine* e, const gcs_bond_params* p, const int64_t* ranges, int64_t n_ranges,
+                            int32_t stride, const int64_t* pairs, int64_t n_pairs, int32_t* handle)
+{
+    if (!e || !p) return fail(GCS_EINVAL, "null argument");
+    if ((n_ranges > 0 && !ranges) || (n_pairs > 0 && !pairs)) return fail(GCS_EINVAL, "null topology array");
+    if (n_ranges > 0 && stride < 1) return fail(GCS_EINVAL, "range stride must be >= 1");
+    if (p->potential != GCS_POT_SEMISPRING && p->potential != GCS_POT_HARMONIC && p->potential != GCS_POT_SPRING)
+        return fail(GCS_EINVAL, "bond potential must be semispring, harmonic or spring");
+    std::vector<int64_t> idx;
+    for (int64_t r = 0; r < n_ranges; ++r) {
+        const int64_t b = ranges[2 * r], en = ranges[2 * r + 1];
+        if (b < 0 || en > e->n || b > en) return fail(GCS_EINVAL, "bonded range out of bounds");
+        for (int64_t k = b; k + stride < en; ++k) {
+            idx.push_back(k);
+            idx.push_back(k + stride);
+        }
+    }
+    for (int64_t q = 0; q < n_pairs; ++q) {
+        if (!valid_index(e, pairs[2 * q]) || !valid_index(e, pairs[2 * q + 1]))
+            return fail(GCS_EINVAL, "bonded pair out of range");
+        if (pairs[2 * q] == pairs[2 * q + 1]) return fail(GCS_EINVAL, "bonded pair joins a particle to itself");
+        idx.push_back(pairs[2 * q]);
+        idx.push_back(pairs[2 * q + 1]);
+    }
+    FieldRec* f = new_field(e, F_BONDED);
+    f->bond = *p;
+    f->idx = std::move(idx);
+    if (handle) *handle = f->handle;
+    return GCS_OK;
+}
+
+int gcs_add_bonded_triplewise(gcs_engine* e, double bending_energy, const int64_t* ranges, int64_t n_ranges,
+                              int32_t* handle)
+{
+    if (!e || (n_ranges > 0 && !ranges)) return fail(GCS_EINVAL, "null argument");
+    std::vector<int64_t> idx;
+    for (int64_t r = 0; r < n_ranges; ++r) {
+        const int64_t b = ranges[2 * r], en = ranges[2 * r + 1];
+        if (b < 0 || en > e->n || b > en) return fail(GCS_EINVAL, "bending range out of bounds");
+        for (int64_t k = b; k + 2 < en; ++k) idx.push_back(k);
+    }
+    FieldRec* f = new_field(e, F_BENDING);
+    f->energy = bending_energy;
+    f->idx = std::move(idx);
+    if (handle) *handle = f->handle;
+    return GCS_OK;
+}
+
+int gcs_add_ellipsoid_inward(gcs_engine* e, const gcs_wall_params* p, int32_t* handle)
+{
+    if (!e || !p) return fail(GCS_EINVAL, "null argument");
+    if (!(p->a_diameter > 0) || (p->mix && !(p->b_diameter > 0))) return fail(GCS_EINVAL, "wall diameters must be positive");
+    FieldRec* f = new_field(e, F_WALL_IN);
+    f->wall = *p;
+    if (handle) *handle = f->handle;
+    return GCS_OK;
+}
+
+int gcs_add_ellipsoid_outward(gcs_engine* e, double spring, const double center[3], int32_t* handle)
+{
+    if (!e) return fail(GCS_EINVAL, "null argument");
+    FieldRec* f = new_field(e, F_WALL_OUT);
+    f->spring = spring;
+    for (int k = 0; k < 3; ++k) f->center[k] = center ? center[k] : 0.0;
+    if (handle) *handle = f->handle;
+    return GCS_OK;
+}
+
+int gcs_add_point_source(gcs_engine* e, const gcs_point_source_params* p, int32_t* handle)
+{
+    if (!e || !p) return fail(GCS_EINVAL, "null argument");
+    if (p->potential < GCS_POT_SEMISPRING || p->potential > GCS_POT_FORCE_FLUX)
+        return fail(GCS_EINVAL, "unknown point-source potential");
+    FieldRec* f = new_field(e, F_POINT);
+    f->point = *p;
+    if (handle) *handle = f->handle;
+    return GCS_OK;
+}
+
+int gcs_add_kinetochore_fiber(gcs_engine* e, const double pole[3], const gcs_kinetochore_spec* specs, int64_t n_specs,
+                              int32_t* handle)
+{
+    if (!e || !pole || (n_specs > 0 && !specs)) return fail(GCS_EINVAL, "null argument");
+    for (int64_t q = 0; q < n_specs; ++q) {
+        if (!valid_index(e, specs[q].particle_index)) return fail(GCS_EINVAL, "kinetochore particle out of range");
+        if (!(specs[q].mobility > 0)) return fail(GCS_EINVAL, "kinetochore mobility must be positive");
+    }
+    FieldRec* f = new_field(e, F_KFIBER);
+    for (int k = 0; k < 3; ++k) f->pole[k] = pole[k];
+    f->specs.assign(specs, specs + n_specs);
+    if (handle) *handle = f->handle;
+    return GCS_OK;
+}
+
+int gcs_remove_forcefield(gcs_engine* e, int32_t handle)
+{
+    if (!e) return fail(GCS_EINVAL, "null argument");
+    for (size_t k = 0; k < e->fields.size(); ++k)
+        if (e->fields[k].handle == handle) {
+            e->fields.erase(e->fields.begin() + (long)k);
+            e->dirty = true;
+            return GCS_OK;
+        }
+    return fail(GCS_EINVAL, "no force field with that handle");
+}
+
+int gcs_engine_set_positions(gcs_engine* e, const double* xyz, int64_t n)
+{
+    if (!e || !xyz) return fail(GCS_EINVAL, "null argument");
+    if (n != e->n) return fail(GCS_EINVAL, "position count does not match the particle count");
+    HIPCHK(hipSetDevice(e->device));
+    std::vector<float4> h(n);
+    for (int64_t i = 0; i < n; ++i)
+        h[i] = make_float4((float)xyz[3 * i], (float)xyz[3 * i + 1], (float)xyz[3 * i + 2], 0.f);
+    HIPCHK(hipMemcpyAsync(e->pos[e->parity], h.data(), n * sizeof(float4), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return GCS_OK;
+}
+
+int gcs_engine_get_positions(gcs_engine* e, double* xyz, int64_t n)
+{
+    if (!e || !xyz) return fail(GCS_EINVAL, "null argument");
+    if (n != e->n) return fail(GCS_EINVAL, "position count does not match the particle count");
+    HIPCHK(hipSetDevice(e->device));
+    std::vector<float4> h(n);
+    HIPCHK(hipMemcpyAsync(h.data(), e->pos[e->parity], n * sizeof(float4), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    for (int64_t i = 0; i < n; ++i) {
+        xyz[3 * i] = h[i].x;
+        xyz[3 * i + 1] = h[i].y;
+        xyz[3 * i + 2] = h[i].z;
+    }
+    return GCS_OK;
+}
+
+int gcs_engine_get_context(gcs_engine* e, gcs_context* c)
+{
+    if (!e || !c) return fail(GCS_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(e->device));
+    DevCtx d;
+    HIPCHK(hipMemcpyAsync(&d, e->ctx, sizeof(d), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    c->step = d.step;
+    c->time = d.time;
+    c->core_scale = d.cs;
+    c->bond_scale = d.bs;
+    for (int k = 0; k < 3; ++k) {
+        c->wall_semiaxes[k] = d.wall[k];
+        c->inward_reaction[k] = d.react_in[k];
+        c->outward_reaction[k] = d.react_out[k];
+    }
+    c->last_timestep = d.dt_used;
+    return GCS_OK;
+}
+
+int gcs_engine_set_context(gcs_engine* e, const gcs_context* c)
+{
+    if (!e || !c) return fail(GCS_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(e->device));
+    DevCtx d;
+    HIPCHK(hipMemcpyAsync(&d, e->ctx, sizeof(d), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    d.step = c->step;
+    d.time = c->time;
+    d.cs = c->core_scale;
+    d.bs = c->bond_scale;
+    for (int k = 0; k < 3; ++k) {
+        d.wall[k] = c->wall_semiaxes[k];
+        d.react_in[k] = c->inward_reaction[k];
+        d.react_out[k] = c->outward_reaction[k];
+    }
+    d.dt_used = c->last_timestep;
+    HIPCHK(hipMemcpyAsync(e->ctx, &d, sizeof(d), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return GCS_OK;
+}
+
+int gcs_engine_set_schedule(gcs_engine* e, const gcs_schedule* s)
+{
+    if (!e || !s) return fail(GCS_EINVAL, "null argument");
+    if ((s->update_scales && (!(s->core_scale_tau > 0) || !(s->bond_scale_tau > 0))))
+        return fail(GCS_EINVAL, "scale time constants must be positive");
+    HIPCHK(hipSetDevice(e->device));
+    e->sched = *s;
+    int rc = upload_sched(e);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return GCS_OK;
+}
+
+int gcs_engine_apply_schedule(gcs_engine* e, int64_t step)
+{
+    if (!e) return fail(GCS_EINVAL, "null argument");
+    int rc = prepare(e);
+    if (rc) return rc;
+    long long st = step;
+    if ((rc = set_ctx_field(e, offsetof(DevCtx, step), &st, sizeof(st)))) return rc;
+    launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max);
+    launch_tail(e->stream, e->ctx, e->fa, 0, 0, 0, 1, e->ncell_max, e->dsched);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return GCS_OK;
+}
+
+int gcs_engine_set_noise(gcs_engine* e, const double* normals, int64_t steps)
+{
+    if (!e || (steps > 0 && !normals)) return fail(GCS_EINVAL, "null argument");
+    if (steps < 0) return fail(GCS_EINVAL, "negative step count");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    dfree(e->noise);
+    const size_t cnt = (size_t)steps * (size_t)e->n * 3;
+    std::vector<float> h(cnt);
+    for (size_t k = 0; k < cnt; ++k) h[k] = (float)normals[k];
+    int rc = dalloc(&e->noise, cnt);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(e->noise, h.data(), cnt * sizeof(float), hipMemcpyHostToDevice, e->stream));
+    long long zero = 0;
+    if ((rc = set_ctx_field(e, offsetof(DevCtx, noise_cursor), &zero, sizeof(zero)))) return rc;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->noise_steps = steps;
+    e->noise_cursor = 0;
+    drop_graph(e);
+    return GCS_OK;
+}
+
+int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps)
+{
+    if (!e || !cfg) return fail(GCS_EINVAL, "null argument");
+    if (steps < 0) return fail(GCS_EINVAL, "negative step count");
+    if (!(cfg->timestep > 0)) return fail(GCS_EINVAL, "timestep must be positive");
+    if (cfg->noise < GCS_NOISE_PHILOX || cfg->noise > GCS_NOISE_NONE) return fail(GCS_EINVAL, "unknown noise mode");
+    if (cfg->noise == GCS_NOISE_INJECTED && e->noise_cursor + steps > e->noise_steps)
+        return fail(GCS_ESTATE, "not enough injected noise for the requested steps");
+    if (steps == 0) return prepare(e);
+    int rc = begin_run(e, cfg, first_step);
+    if (rc) return rc;
+    const bool spacestep = cfg->spacestep > 0;
+
+    const int G = e->graph_steps;
+    int64_t done = 0;
+    if (G > 0 && steps >= G) {
+        const bool same = e->gexec && e->g_steps == G && e->g_waves == e->waves && e->g_version == e->topo_version &&
+                          e->g_spacestep == (int)spacestep && e->g_sched_flags == e->sched_flags &&
+                          std::memcmp(&e->g_cfg, cfg, sizeof(*cfg)) == 0;
+        if (!same) {
+            drop_graph(e);
+            HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+            for (int k = 0; k < G; ++k) enqueue_step(e, spacestep, (float)cfg->spacestep, (float)cfg->timestep);
+            HIPCHK(hipStreamEndCapture(e->stream, &e->graph));
+            HIPCHK(hipGraphInstantiate(&e->gexec, e->graph, nullptr, nullptr, 0));
+            e->g_steps = G;
+            e->g_waves = e->waves;
+            e->g_version = e->topo_version;
+            e->g_spacestep = (int)spacestep;
+            e->g_sched_flags = e->sched_flags;
+            e->g_cfg = *cfg;
+        }
+        for (; done + G <= steps; done += G) HIPCHK(hipGraphLaunch(e->gexec, e->stream));
+    }
+    for (; done < steps; ++done) enqueue_step(e, spacestep, (float)cfg->spacestep, (float)cfg->timestep);
+    HIPCHK(hipGetLastError());
+    if (steps & 1) e->parity ^= 1;
+    if (cfg->noise == GCS_NOISE_INJECTED) e->noise_cursor += steps;
+    return GCS_OK;
+}
+
+int gcs_engine_synchronize(gcs_engine* e)
+{
+    if (!e) return fail(GCS_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return GCS_OK;
+}
+
+int gcs_engine_compute_forces(gcs_engine* e, double* forces, int64_t n)
+{
+    if (!e || !forces) return fail(GCS_EINVAL, "null argument");
+    if (n != e->n) return fail(GCS_EINVAL, "force array size does not match the particle count");
+    int rc = prepare(e);
+    if (rc) return rc;
+    launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max);
+    enqueue_cells(e);
+    launch_force(e->stream, kModeForce, e->waves, e->ctx, e->fa);
+    launch_tail(e->stream, e->ctx, e->fa, force_blocks(e->n), 0, 0, 0, e->ncell_max, e->dsched);
+    HIPCHK(hipGetLastError());
+    std::vector<float4> h(n);
+    HIPCHK(hipMemcpyAsync(h.data(), e->force_out, n * sizeof(float4), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    for (int64_t i = 0; i < n; ++i) {
+        forces[3 * i] = h[i].x;
+        forces[3 * i + 1] = h[i].y;
+        forces[3 * i + 2] = h[i].z;
+    }
+    return GCS_OK;
+}
+
+int gcs_engine_compute_energy(gcs_engine* e, double* total, double* per_kind)
+{
+    if (!e || !total) return fail(GCS_EINVAL, "null argument");
+    int rc = prepare(e);
+    if (rc) return rc;
+    launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max);
+    enqueue_cells(e);
+    launch_force(e->stream, kModeEnergy, e->waves, e->ctx, e->fa);
+    HIPCHK(hipGetLastError());
+    const int fb = force_blocks(e->n);
+    std::vector<double> h((size_t)fb * kEnergyKinds);
+    HIPCHK(hipMemcpyAsync(h.data(), e->part_energy, h.size() * sizeof(double), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    double pk[kEnergyKinds] = {0};
+    for (int b = 0; b < fb; ++b)
+        for (int k = 0; k < kEnergyKinds; ++k) pk[k] += h[(size_t)b * kEnergyKinds + k];
+    double t = 0;
+    for (int k = 0; k < kEnergyKinds; ++k) t += pk[k];
+    *total = t;
+    if (per_kind)
+        for (int k = 0; k < kEnergyKinds; ++k) per_kind[k] = pk[k];
+    return GCS_OK;
+}
+
+int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, double distance, uint32_t* pairs,
+                                int64_t capacity, int64_t* count)
+{
+    if (!e || !count || (capacity > 0 && !pairs)) return fail(GCS_EINVAL, "null argument");
+    if (!(distance > 0)) return fail(GCS_EINVAL, "search distance must be positive");
+    if (!points && n != e->n) return fail(GCS_EINVAL, "point count does not match the particle count");
+    if (n < 0 || n > (int64_t)1 << 30) return fail(GCS_EINVAL, "bad point count");
+    *count = 0;
+    if (n < 2) return GCS_OK;
+    HIPCHK(hipSetDevice(e->device));
+    int rc;
+    if (n > e->search_cap) {
+        dfree(e->s_pts);
+        dfree(e->s_spos);
+        dfree(e->s_sb);
+        dfree(e->s_sidx);
+        dfree(e->s_scell);
+        dfree(e->s_cell_of);
+        dfree(e->s_slot);
+        dfree(e->s_tmp);
+        dfree(e->s_count);
+        dfree(e->s_cstart);
+        dfree(e->s_counts);
+        dfree(e->s_offsets);
+        dfree(e->s_total);
+        dfree(e->s_ctx);
+        e->search_cap = 0;
+        const int cap = (int)n;
+        const int ncm = std::min(1 << 21, std::max(4096, 4 * cap));
+        if ((rc = dalloc(&e->s_pts, cap)) || (rc = dalloc(&e->s_spos, cap)) || (rc = dalloc(&e->s_sb, cap)) ||
+            (rc = dalloc(&e->s_sidx, cap)) || (rc = dalloc(&e->s_scell, cap)) || (rc = dalloc(&e->s_cell_of, cap)) ||
+            (rc = dalloc(&e->s_slot, cap)) || (rc = dalloc(&e->s_tmp, cap)) || (rc = dalloc(&e->s_count, ncm + 2)) ||
+            (rc = dalloc(&e->s_cstart, ncm + 2)) || (rc = dalloc(&e->s_counts, cap)) ||
+            (rc = dalloc(&e->s_offsets, cap)) || (rc = dalloc(&e->s_total, 1)) || (rc = dalloc(&e->s_ctx, 1)))
+            return rc;
+        HIPCHK(hipMemsetAsync(e->s_count, 0, (ncm + 2) * sizeof(int), e->stream));
+        e->search_cap = cap;
+        e->s_ncell_max = ncm;
+    }
+    const int ni = (int)n;
+    const float4* src = e->s_pts;
+    if (points) {
+        std::vector<float4> h(n);
+        for (int64_t i = 0; i < n; ++i)
+            h[i] = make_float4((float)points[3 * i], (float)points[3 * i + 1], (float)points[3 * i + 2], 0.f);
+        HIPCHK(hipMemcpyAsync(e->s_pts, h.data(), n * sizeof(float4), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+    } else {
+        src = e->pos[e->parity];
+    }
+    DevCtx c{};
+    c.cs = 1.0;
+    c.bs = 1.0;
+    HIPCHK(hipMemcpyAsync(e->s_ctx, &c, sizeof(c), hipMemcpyHostToDevice, e->stream));
+    ForceArgs sa{};
+    sa.n = ni;
+    sa.pos0 = const_cast<float4*>(src);
+    sa.pos1 = const_cast<float4*>(src);
+    launch_prime(e->stream, e->s_ctx, sa, (float)distance, e->s_ncell_max);
+    launch_cell_count(e->stream, e->s_ctx, src, src, ni, e->s_cell_of, e->s_slot, e->s_count);
+    launch_cell_scan(e->stream, e->s_ctx, ni, e->s_count, e->s_cstart);
+    launch_cell_scatter(e->stream, ni, e->s_cell_of, e->s_slot, e->s_cstart, e->s_tmp);
+    launch_cell_sort(e->stream, e->s_ctx, src, src, nullptr, ni, e->s_tmp, e->s_cell_of, e->s_cstart, e->s_sidx,
+                     e->s_scell, e->s_spos, e->s_sb, 1);
+    launch_search_count(e->stream, e->s_ctx, ni, e->s_spos, e->s_sidx, e->s_scell, e->s_cstart, e->s_counts);
+    launch_exclusive_scan_small(e->stream, e->s_counts, e->s_offsets, ni, e->s_total);
+    HIPCHK(hipGetLastError());
+    int total = 0;
+    HIPCHK(hipMemcpyAsync(&total, e->s_total, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    *count = total;
+    if (total > capacity) return fail(GCS_ECAPACITY, "pair buffer too small; *count holds the required size");
+    if (total == 0) return GCS_OK;
+    if (total > e->s_key_cap) {
+        dfree(e->s_keys);
+        dfree(e->s_keys2);
+        if (e->s_sort_temp) (void)hipFree(e->s_sort_temp);
+        e->s_sort_temp = nullptr;
+        e->s_key_cap = 0;
+        if ((rc = dalloc(&e->s_keys, total)) || (rc = dalloc(&e->s_keys2, total))) return rc;
+        e->s_sort_bytes = sort_u64_temp_bytes(total);
+        HIPCHK(hipMalloc(&e->s_sort_temp, std::max<size_t>(e->s_sort_bytes, 16)));
+        e->s_key_cap = total;
+    }
+    launch_search_emit(e->stream, e->s_ctx, ni, e->s_spos, e->s_sidx, e->s_scell, e->s_cstart, e->s_offsets, e->s_keys);
+    size_t bytes = sort_u64_temp_bytes(total);
+    if (bytes > e->s_sort_bytes) {
+        (void)hipFree(e->s_sort_temp);
+        HIPCHK(hipMalloc(&e->s_sort_temp, bytes));
+        e->s_sort_bytes = bytes;
+    }
+    sort_u64_keys(e->stream, e->s_keys, e->s_keys2, total, e->s_sort_temp, e->s_sort_bytes);
+    HIPCHK(hipGetLastError());
+    std::vector<unsigned long long> h(total);
+    HIPCHK(hipMemcpyAsync(h.data(), e->s_keys2, total * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    for (int k = 0; k < total; ++k) {
+        pairs[2 * k] = (uint32_t)(h[k] >> 32);
+        pairs[2 * k + 1] = (uint32_t)h[k];
+    }
+    return GCS_OK;
+}
+
+int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps, gcs_profile* out)
+{
+    if (!e || !cfg || !out) return fail(GCS_EINVAL, "null argument");
+    if (steps <= 0) return fail(GCS_EINVAL, "profile needs at least one step");
+    if (cfg->spacestep > 0) return fail(GCS_EINVAL, "profile covers the fixed-timestep path only");
+    if (cfg->noise == GCS_NOISE_INJECTED && e->noise_cursor + steps > e->noise_steps)
+        return fail(GCS_ESTATE, "not enough injected noise for the requested steps");
+    int rc = begin_run(e, cfg, first_step);
+    if (rc) return rc;
+    std::vector<hipEvent_t> ev((size_t)steps * 4 + 2, nullptr);
+    for (auto& x : ev) HIPCHK(hipEventCreate(&x));
+    const int fb = force_blocks(e->n);
+    HIPCHK(hipEventRecord(ev[0], e->stream));
+    for (int64_t k = 0; k < steps; ++k) {
+        HIPCHK(hipEventRecord(ev[1 + 4 * k], e->stream));
+        enqueue_cells(e);
+        HIPCHK(hipEventRecord(ev[2 + 4 * k], e->stream));
+        launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa);
+        HIPCHK(hipEventRecord(ev[3 + 4 * k], e->stream));
+        launch_tail(e->stream, e->ctx, e->fa, fb, fb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
+        HIPCHK(hipEventRecord(ev[4 + 4 * k], e->stream));
+    }
+    HIPCHK(hipEventRecord(ev[ev.size() - 1], e->stream));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));
+    double cell = 0, force = 0, tail = 0;
+    for (int64_t k = 0; k < steps; ++k) {
+        float a = 0, b = 0, c = 0;
+        HIPCHK(hipEventElapsedTime(&a, ev[1 + 4 * k], ev[2 + 4 * k]));
+        HIPCHK(hipEventElapsedTime(&b, ev[2 + 4 * k], ev[3 + 4 * k]));
+        HIPCHK(hipEventElapsedTime(&c, ev[3 + 4 * k], ev[4 + 4 * k]));
+        cell += a;
+        force += b;
+        tail += c;
+    }
+    float tot = 0;
+    HIPCHK(hipEventElapsedTime(&tot, ev[0], ev[ev.size() - 1]));
+    for (auto& x : ev) (void)hipEventDestroy(x);
+    if (steps & 1) e->parity ^= 1;
+    if (cfg->noise == GCS_NOISE_INJECTED) e->noise_cursor += steps;
+    DevCtx d;
+    HIPCHK(hipMemcpy(&d, e->ctx, sizeof(d), hipMemcpyDeviceToHost));
+    out->steps = steps;
+    out->total_ms = tot;
+    out->force_ms = force / (double)steps;
+    out->cell_ms = cell / (double)steps;
+    out->tail_ms = tail / (double)steps;
+    out->mean_neighbors = d.neighbors;
+    return GCS_OK;
+}
+
+int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
+{
+    if (!e) return fail(GCS_EINVAL, "null argument");
+    if (option == GCS_OPT_GRAPH_STEPS) {
+        if (value < 0 || value > 4096) return fail(GCS_EINVAL, "graph steps must be in [0, 4096]");
+        e->graph_steps = (int)value;
+        drop_graph(e);
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_WAVES_PER_TILE) {
+        if (value != 1 && value != 2 && value != 4 && value != 8) return fail(GCS_EINVAL, "waves per tile must be 1, 2, 4 or 8");
+        e->waves = (int)value;
+        drop_graph(e);
+        return GCS_OK;
+    }
+    return fail(GCS_EINVAL, "unknown option");
+}
+
+}  // extern "C"

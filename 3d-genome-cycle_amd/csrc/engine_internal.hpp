@@ -1,0 +1,178 @@
+// engine_internal.hpp -- device-side data layout and kernel interfaces of the gcs engine (gfx950).
+//
+// HBM layout (fp32, 16-B aligned rows so every particle access is one dwordx4):
+//   pos[2][N]   float4 {x, y, z, 0}      double-buffered particle positions, particle order
+//   kmu[N]      float4 {mu, a, b, 0}     per-particle constants (mobility, A/B factors)
+//   spos[N]     float4 {x, y, z, a}      positions re-ordered by cell (rebuilt every step)
+//   sb[N], sidx[N], scell[N]             b factor, particle index and cell of each sorted slot
+//   cstart[ncell+1]                      first sorted slot of each cell (cell = x + nx (y + ny z))
+//   bonded CSR (boff/bent/bpar), bend_eps[N], tether CSR (toff/tent)   topology, particle order
+//   DevCtx                               device-resident driver context + the current cell grid
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gcs {
+
+constexpr int kTile = 64;          // particles per tile of the pair loop = one wave's lanes
+constexpr int kMaxPointSources = 4;
+constexpr int kForcePartials = 8;  // per force block: reaction in[3], out[3], max mu|F|, neighbours
+constexpr int kBBoxPartials = 6;   // per block: bbox lo[3], hi[3]
+constexpr int kEnergyKinds = 8;
+
+struct Grid {
+    float lo[3];
+    float inv[3];
+    int n[3];
+    int ncell;
+    float rc;   // pair cutoff of this step
+    float rc2;
+};
+
+struct DevCtx {
+    double time, cs, bs;
+    double wall[3];
+    double react_in[3], react_out[3];
+    double dt_used;
+    double max_drift;      // max_i mu_i |F_i| of the last force evaluation (spacestep)
+    double neighbors;      // mean neighbours within the cutoff per particle (last force evaluation)
+    long long step;        // last completed step
+    long long noise_cursor;
+    int parity;            // index of the current position buffer
+    int pad0;
+    float bbox_lo[3], bbox_hi[3];
+    Grid grid;
+};
+
+enum BondType : int { kSemispring = 0, kHarmonic = 1, kSpring = 2, kSoftwell = 3 };
+
+struct BondParam {
+    int type, mix, scaled, pad;
+    float ka, kb, la, lb;  // softwell: ka = energy, kb = 1/decay^2, la = cutoff^2
+};
+
+struct Tether {  // kinetochore fiber spring to a fixed pole
+    float px, py, pz, k, l, pad0, pad1, pad2;
+};
+
+struct PointSrc {
+    int type;      // GCS_POT_*
+    float px, py, pz, k, l, f, b;
+};
+
+struct WallIn {
+    float a_eps, a_sig, b_eps, b_sig, wall_a, wall_b, cx, cy, cz;
+    int mix, scaled;
+};
+
+enum Mode : int { kModeStep = 0, kModeForce = 1, kModeEnergy = 2 };
+
+struct ForceArgs {
+    int n;
+    // state
+    float4* pos0;
+    float4* pos1;
+    const float4* kmu;
+    const float4* spos;
+    const float* sb;
+    const int* sidx;
+    const int* scell;
+    const int* cstart;
+    // neighbor soft-core pair field
+    int has_pair, pair_mix, pair_scaled, pad0;
+    float pa_eps, pa_sig, pb_eps, pb_sig, pair_dist;
+    // bonded CSR (particle order)
+    int has_bonds;
+    const int* boff;
+    const int2* bent;
+    const BondParam* bpar;
+    // bending
+    int has_bend;
+    const float* bend_eps;
+    // kinetochore fibers
+    int has_tether;
+    const int* toff;
+    const Tether* tent;
+    // point sources
+    int n_point;
+    PointSrc point[kMaxPointSources];
+    // ellipsoid walls
+    int has_wall_in, has_wall_out;
+    WallIn win;
+    float wout_k, wout_cx, wout_cy, wout_cz;
+    // Brownian dynamics
+    float temperature, timestep;
+    unsigned seed_lo, seed_hi;
+    int noise_mode;
+    const float* noise;
+    long long noise_steps;
+    // outputs
+    float* part_force;    // [blocks][kForcePartials]
+    float* part_bbox;     // [blocks][kBBoxPartials]
+    double* part_energy;  // [blocks][kEnergyKinds]
+    float4* force_out;    // [N] (kModeForce)
+};
+
+// ---- Philox4x32-10 + Box-Muller: the production noise stream (identical on host for the oracle) ----
+__host__ __device__ inline void philox4x32_10(unsigned c[4], unsigned k0, unsigned k1)
+{
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        unsigned long long p0 = (unsigned long long)0xD2511F53u * c[0];
+        unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c[2];
+        unsigned n0 = (unsigned)(p1 >> 32) ^ c[1] ^ k0;
+        unsigned n1 = (unsigned)p1;
+        unsigned n2 = (unsigned)(p0 >> 32) ^ c[3] ^ k1;
+        unsigned n3 = (unsigned)p0;
+        c[0] = n0;
+        c[1] = n1;
+        c[2] = n2;
+        c[3] = n3;
+    }
+}
+
+// launch wrappers (kernels.hip)
+void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed, int ncell_max);
+void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n,
+                       int* cell_of, int* slot, int* count);
+void launch_cell_scan(hipStream_t s, const DevCtx* ctx, int n, int* count, int* cstart);
+void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* slot, const int* cstart, int* tmp);
+void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, const float4* kmu,
+                      int n, const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell,
+                      float4* spos, float* sb, int pair_mix);
+void launch_force(hipStream_t s, int mode, int waves, const DevCtx* ctx, const ForceArgs& a);
+void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a);
+void launch_adapt(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force_blocks, float spacestep, float timestep);
+void launch_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force_blocks, int bbox_blocks, int advance,
+                 int apply_sched, int ncell_max, const double* sched /* device: gcs_schedule mirror */);
+void launch_search_count(hipStream_t s, const DevCtx* ctx, int n, const float4* spos, const int* sidx,
+                         const int* scell, const int* cstart, int* counts);
+void launch_search_emit(hipStream_t s, const DevCtx* ctx, int n, const float4* spos, const int* sidx,
+                        const int* scell, const int* cstart, const int* offsets, unsigned long long* keys);
+void launch_exclusive_scan_small(hipStream_t s, const int* in, int* out, int n, int* total);
+void sort_u64_keys(hipStream_t s, unsigned long long* keys, unsigned long long* tmp, int n, void* temp, size_t temp_bytes);
+size_t sort_u64_temp_bytes(int n);
+
+inline int force_blocks(int n) { return (n + kTile - 1) / kTile; }
+constexpr int kUpdateBlock = 256;
+inline int update_blocks(int n) { return (n + kUpdateBlock - 1) / kUpdateBlock; }
+
+// device schedule mirror (double[16]): layout used by launch_tail
+enum SchedIdx {
+    kSchedFlags = 0,  // bit0 time, bit1 scales, bit2 wall
+    kSchedDt = 1,
+    kSchedCs0 = 2,
+    kSchedCsTau = 3,
+    kSchedBs0 = 4,
+    kSchedBsTau = 5,
+    kSchedK0 = 6,
+    kSchedMuW = 9,
+    kSchedCount = 16,
+};
+
+}  // namespace gcs

@@ -1,0 +1,937 @@
+// kernels.hip -- CDNA4 (gfx950, wave64) kernels of the gcs engine.
+//
+// One Brownian-dynamics step = 6 launches on one stream (captured into a hipGraph by the host):
+//   cell_count   per particle: cell of its position, slot = atomicAdd(count[cell])
+//   cell_scan    1 block: exclusive scan count -> cstart, re-zero count
+//   cell_scatter per particle: tmp[cstart[cell] + slot] = particle
+//   cell_sort    per sorted slot: rank inside the cell by particle index (deterministic order),
+//                write the cell-sorted copies spos/sb/sidx/scell
+//   force        per 64-particle tile (WAVES waves): gather-form pair loop over the tile's stencil rows
+//                (wave-uniform neighbour reads -> scalar loads), + bonded/bending/tether/point/wall terms,
+//                + the Euler-Maruyama update; per-block reaction / bbox partials; no atomics
+//   tail         1 block: reduce the partials in a fixed order (fp64), apply the interphase schedule
+//                (time, core/bond scale, wall ODE), build the next step's cell grid
+// Replaces: md::simulate_brownian_dynamics's force+integrator loop as driven from
+// stage_interphase/simulation_driver_interphase.cpp:57-63 (force fields: simulation_driver_forcefield.cpp:9-244).
+#include "engine_internal.hpp"
+
+#include <hipcub/hipcub.hpp>
+
+#include "../../include/gcs.h"
+
+namespace gcs {
+
+namespace {
+
+__device__ inline float wave_sum(float v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ inline double wave_sum_d(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ inline float wave_max(float v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ inline float wave_min(float v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    return v;
+}
+
+__device__ inline int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ inline int cell_index(const Grid& g, float x, float y, float z)
+{
+    int cx = (int)((x - g.lo[0]) * g.inv[0]);
+    int cy = (int)((y - g.lo[1]) * g.inv[1]);
+    int cz = (int)((z - g.lo[2]) * g.inv[2]);
+    cx = min(max(cx, 0), g.n[0] - 1);
+    cy = min(max(cy, 0), g.n[1] - 1);
+    cz = min(max(cz, 0), g.n[2] - 1);
+    return cx + g.n[0] * (cy + g.n[1] * cz);
+}
+
+// Cell grid over the current bounding box; cell edge >= rc (1e-4 margin) so any pair closer than rc lies
+// in the same or an adjacent cell (particles outside the box are clamped into the border cells, which
+// keeps that property because clamping never increases a per-axis cell distance).
+__device__ void compute_grid(DevCtx* ctx, float rc, int ncell_max)
+{
+    Grid g;
+    int n[3];
+    float ext[3];
+    long long total = 1;
+    for (int k = 0; k < 3; ++k) {
+        float e = ctx->bbox_hi[k] - ctx->bbox_lo[k];
+        if (!(e > 0.f) || !(e < 3.0e38f)) e = 0.f;
+        ext[k] = e;
+        float q = (rc > 0.f) ? e / (rc * 1.0001f) : 0.f;
+        int m = (q >= 1.f) ? (int)fminf(q, 1024.f) : 1;
+        n[k] = m;
+        total *= m;
+    }
+    while (total > ncell_max) {
+        int kk = 0;
+        for (int k = 1; k < 3; ++k)
+            if (n[k] > n[kk]) kk = k;
+        total /= n[kk];
+        n[kk] = max(1, n[kk] / 2);
+        total *= n[kk];
+    }
+    for (int k = 0; k < 3; ++k) {
+        g.lo[k] = ctx->bbox_lo[k];
+        g.n[k] = n[k];
+        g.inv[k] = ext[k] > 0.f ? (float)n[k] / ext[k] : 0.f;
+    }
+    g.ncell = (int)total;
+    g.rc = rc;
+    g.rc2 = rc * rc;
+    ctx->grid = g;
+}
+
+__device__ inline float pair_cutoff(const ForceArgs& a, double cs)
+{
+    if (!a.has_pair) return 1.f;
+    return a.pair_dist * (a.pair_scaled ? (float)cs : 1.f);
+}
+
+// ----------------------------------------------------------------------------------------------------
+// cell list
+
+__global__ __launch_bounds__(1024) void k_prime(DevCtx* ctx, ForceArgs a, float rc_fixed, int ncell_max)
+{
+    __shared__ float red[6][16];
+    const float4* pos = ctx->parity ? a.pos1 : a.pos0;
+    float lo[3] = {3.0e38f, 3.0e38f, 3.0e38f}, hi[3] = {-3.0e38f, -3.0e38f, -3.0e38f};
+    for (int i = threadIdx.x; i < a.n; i += blockDim.x) {
+        float4 p = pos[i];
+        lo[0] = fminf(lo[0], p.x);
+        lo[1] = fminf(lo[1], p.y);
+        lo[2] = fminf(lo[2], p.z);
+        hi[0] = fmaxf(hi[0], p.x);
+        hi[1] = fmaxf(hi[1], p.y);
+        hi[2] = fmaxf(hi[2], p.z);
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int k = 0; k < 3; ++k) {
+        float l = wave_min(lo[k]), h = wave_max(hi[k]);
+        if (lane == 0) {
+            red[k][wave] = l;
+            red[3 + k][wave] = h;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int nw = blockDim.x / 64;
+        for (int k = 0; k < 3; ++k) {
+            float l = red[k][0], h = red[3 + k][0];
+            for (int w = 1; w < nw; ++w) {
+                l = fminf(l, red[k][w]);
+                h = fmaxf(h, red[3 + k][w]);
+            }
+            ctx->bbox_lo[k] = l;
+            ctx->bbox_hi[k] = h;
+        }
+        float rc = rc_fixed > 0.f ? rc_fixed : pair_cutoff(a, ctx->cs);
+        compute_grid(ctx, rc, ncell_max);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_cell_count(const DevCtx* __restrict__ ctx, const float4* __restrict__ p0,
+                                                    const float4* __restrict__ p1, int n, int* __restrict__ cell_of,
+                                                    int* __restrict__ slot, int* __restrict__ count)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4* pos = ctx->parity ? p1 : p0;
+    const Grid g = ctx->grid;
+    const float4 p = pos[i];
+    const int c = cell_index(g, p.x, p.y, p.z);
+    cell_of[i] = c;
+    slot[i] = atomicAdd(&count[c], 1);
+}
+
+// exclusive scan of the wave (64 lanes), returns the inclusive value
+__device__ inline int wave_incl_scan(int v, int lane)
+{
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(1024) void k_cell_scan(const DevCtx* __restrict__ ctx, int n, int* __restrict__ count,
+                                                    int* __restrict__ cstart)
+{
+    __shared__ int wtot[16];
+    const int nc = ctx->grid.ncell;
+    const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int per = (nc + T - 1) / T;
+    const int b = min(nc, tid * per), e = min(nc, b + per);
+    int sum = 0;
+    for (int k = b; k < e; ++k) sum += count[k];
+    int incl = wave_incl_scan(sum, lane);
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    if (wave == 0) {
+        int v = (lane < T / 64) ? wtot[lane] : 0;
+        int vi = wave_incl_scan(v, lane);
+        if (lane < T / 64) wtot[lane] = vi - v;
+    }
+    __syncthreads();
+    int run = wtot[wave] + incl - sum;
+    for (int k = b; k < e; ++k) {
+        int c = count[k];
+        cstart[k] = run;
+        run += c;
+        count[k] = 0;
+    }
+    if (tid == 0) cstart[nc] = n;
+}
+
+__global__ __launch_bounds__(256) void k_cell_scatter(int n, const int* __restrict__ cell_of, const int* __restrict__ slot,
+                                                      const int* __restrict__ cstart, int* __restrict__ tmp)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    tmp[cstart[cell_of[i]] + slot[i]] = i;
+}
+
+__global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ctx, const float4* __restrict__ p0,
+                                                   const float4* __restrict__ p1, const float4* __restrict__ kmu, int n,
+                                                   const int* __restrict__ tmp, const int* __restrict__ cell_of,
+                                                   const int* __restrict__ cstart, int* __restrict__ sidx,
+                                                   int* __restrict__ scell, float4* __restrict__ spos,
+                                                   float* __restrict__ sb, int pair_mix)
+{
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const float4* pos = ctx->parity ? p1 : p0;
+    const int i = tmp[s];
+    const int c = cell_of[i];
+    const int b = cstart[c], e = cstart[c + 1];
+    int r = 0;
+    for (int t = b; t < e; ++t) r += (tmp[t] < i) ? 1 : 0;
+    const int d = b + r;
+    const float4 p = pos[i];
+    const float4 k = kmu ? kmu[i] : make_float4(1.f, 1.f, 0.f, 0.f);
+    sidx[d] = i;
+    scell[d] = c;
+    // the pair field's factors: (a, b) when it mixes A/B (interphase), (1, 0) for plain softcore<2,3>
+    spos[d] = make_float4(p.x, p.y, p.z, pair_mix ? k.y : 1.f);
+    sb[d] = pair_mix ? k.z : 0.f;
+}
+
+// ----------------------------------------------------------------------------------------------------
+// Brownian step helpers
+
+__device__ inline void philox_normal3(unsigned seed_lo, unsigned seed_hi, long long step, int i, float& n0, float& n1,
+                                      float& n2)
+{
+    unsigned c[4] = {(unsigned)i, (unsigned)(unsigned long long)step, (unsigned)((unsigned long long)step >> 32),
+                     0x47435331u};
+    philox4x32_10(c, seed_lo, seed_hi);
+    const float k24 = 1.0f / 16777216.0f;
+    float u0 = ((float)(c[0] >> 8) + 0.5f) * k24;
+    float u1 = ((float)(c[1] >> 8) + 0.5f) * k24;
+    float u2 = ((float)(c[2] >> 8) + 0.5f) * k24;
+    float u3 = ((float)(c[3] >> 8) + 0.5f) * k24;
+    float r1 = sqrtf(-2.0f * logf(u0));
+    float r2 = sqrtf(-2.0f * logf(u2));
+    float s1, c1, s2, c2;
+    sincospif(2.0f * u1, &s1, &c1);
+    sincospif(2.0f * u3, &s2, &c2);
+    n0 = r1 * c1;
+    n1 = r1 * s1;
+    n2 = r2 * c2;
+}
+
+__device__ inline void noise3(const ForceArgs& a, const DevCtx* ctx, int i, float& n0, float& n1, float& n2)
+{
+    if (a.noise_mode == GCS_NOISE_PHILOX) {
+        philox_normal3(a.seed_lo, a.seed_hi, ctx->step + 1, i, n0, n1, n2);
+    } else if (a.noise_mode == GCS_NOISE_INJECTED) {
+        long long cur = ctx->noise_cursor;
+        if (cur >= a.noise_steps) cur = a.noise_steps - 1;  // host checks the budget before launching
+        const float* p = a.noise + (cur * (long long)a.n + i) * 3;
+        n0 = p[0];
+        n1 = p[1];
+        n2 = p[2];
+    } else {
+        n0 = n1 = n2 = 0.f;
+    }
+}
+
+// spring-type potential at separation vector r (|r|^2 = r2): returns force coefficient c (F = c r) and U
+__device__ inline float spring_coef(int type, float K, float l, float r2, float& U)
+{
+    if (type == kHarmonic) {
+        U = 0.5f * K * r2;
+        return -K;
+    }
+    float d = sqrtf(r2);
+    if ((type == kSemispring && d <= l) || d <= 0.f) {
+        U = (type == kSpring && d <= 0.f) ? 0.5f * K * l * l : 0.f;
+        return 0.f;
+    }
+    float dl = d - l;
+    U = 0.5f * K * dl * dl;
+    return -K * dl / d;
+}
+
+// ----------------------------------------------------------------------------------------------------
+// force / step kernel
+
+template <int MODE, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__ ctx, ForceArgs a)
+{
+    __shared__ float red[WAVES > 1 ? WAVES : 1][4][64];
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    const int n = a.n;
+    const int s0 = blockIdx.x * kTile;
+    const int s = s0 + lane;
+    const bool valid = s < n;
+    const int sl = valid ? s : n - 1;
+    const float4 pi = a.spos[sl];
+    const float bi = a.sb[sl];
+    const float cs = (float)ctx->cs;
+
+    float fx = 0.f, fy = 0.f, fz = 0.f, acc = 0.f;  // acc: pair energy (ENERGY) or neighbour count
+
+    if (a.has_pair) {
+        const Grid g = ctx->grid;
+        const float scale = a.pair_scaled ? cs : 1.f;
+        const float sa = a.pa_sig * scale, sbb = a.pb_sig * scale;
+        const float k2a = 1.f / (sa * sa), k2b = 1.f / (sbb * sbb);
+        // F = coef * (x_i - x_j):  A * 6 eps_a k2a ga^2  +  B * 24 eps_b k2b gb^2 t^3   (A, B = pair means)
+        const float ca = 0.5f * 6.f * a.pa_eps * k2a;
+        const float cb = 0.5f * 24.f * a.pb_eps * k2b;
+        const float ea = 0.25f * a.pa_eps;  // energy: 1/2 (mean) x 1/2 (each pair seen from both ends)
+        const float eb = 0.25f * a.pb_eps;
+        const float rc2 = g.rc2;
+        const int nx = g.n[0], ny = g.n[1], nz = g.n[2];
+        const int slast = min(n, s0 + kTile) - 1;
+        const int c0 = uniform(a.scell[s0]), c1 = uniform(a.scell[slast]);
+        const int x0 = c0 % nx, y0 = (c0 / nx) % ny, z0 = c0 / (nx * ny);
+        const int x1 = c1 % nx, y1 = (c1 / nx) % ny, z1 = c1 / (nx * ny);
+        int xlo, xhi, ylo, yhi, zlo, zhi;
+        if (z0 == z1 && y0 == y1) {  // the tile lies in one row of cells: 3x3 rows, x-range padded by 1
+            xlo = x0 - 1; xhi = x1 + 1; ylo = y0 - 1; yhi = y0 + 1; zlo = z0 - 1; zhi = z0 + 1;
+        } else if (z0 == z1) {
+            xlo = 0; xhi = nx - 1; ylo = y0 - 1; yhi = y1 + 1; zlo = z0 - 1; zhi = z0 + 1;
+        } else {
+            xlo = 0; xhi = nx - 1; ylo = 0; yhi = ny - 1; zlo = z0 - 1; zhi = z1 + 1;
+        }
+        xlo = max(xlo, 0); xhi = min(xhi, nx - 1);
+        ylo = max(ylo, 0); yhi = min(yhi, ny - 1);
+        zlo = max(zlo, 0); zhi = min(zhi, nz - 1);
+
+        // total candidates over the stencil rows; wave w takes the w-th contiguous share
+        int total = 0;
+        for (int z = zlo; z <= zhi; ++z)
+            for (int y = ylo; y <= yhi; ++y) {
+                const int base = (z * ny + y) * nx;
+                total += a.cstart[base + xhi + 1] - a.cstart[base + xlo];
+            }
+        total = uniform(total);
+        const int wlo = (int)(((long long)total * wave) / WAVES);
+        const int whi = (int)(((long long)total * (wave + 1)) / WAVES);
+        const float ahi = pi.w, bhi = bi;
+        int v = 0;
+        for (int z = zlo; z <= zhi && v < whi; ++z)
+            for (int y = ylo; y <= yhi && v < whi; ++y) {
+                const int base = (z * ny + y) * nx;
+                const int jb = uniform(a.cstart[base + xlo]);
+                const int je = uniform(a.cstart[base + xhi + 1]);
+                const int len = je - jb;
+                const int lo = max(v, wlo), hi = min(v + len, whi);
+                const int off = jb - v;
+                for (int k = lo; k < hi; ++k) {
+                    const int j = k + off;
+                    const float4 pj = a.spos[j];
+                    const float bj = a.sb[j];
+                    const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+                    const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                    const bool in = (r2 < rc2) && (j != s);
+                    const float A = ahi + pj.w, B = bhi + bj;
+                    const float ua = r2 * k2a;
+                    const float ga = 1.f - ua;
+                    const float t = r2 * k2b;
+                    const float t2 = t * t;
+                    const float gb = 1.f - t2 * t2;
+                    const float gb2 = gb * gb;
+                    const bool ina = in && (ua < 1.f);
+                    const bool inb = in && (t < 1.f);
+                    if (MODE == kModeEnergy) {
+                        const float ua3 = ga * ga * ga, ub3 = gb2 * gb;
+                        acc += (ina ? A * ea * ua3 : 0.f) + (inb ? B * eb * ub3 : 0.f);
+                    } else {
+                        const float fa = ina ? ga * ga : 0.f;
+                        const float fb = inb ? gb2 * t2 * t : 0.f;
+                        const float coef = fmaf(A * ca, fa, B * cb * fb);
+                        fx = fmaf(coef, dx, fx);
+                        fy = fmaf(coef, dy, fy);
+                        fz = fmaf(coef, dz, fz);
+                        acc += in ? 1.f : 0.f;
+                    }
+                }
+                v += len;
+            }
+    }
+
+    if (WAVES > 1) {
+        red[wave][0][lane] = fx;
+        red[wave][1][lane] = fy;
+        red[wave][2][lane] = fz;
+        red[wave][3][lane] = acc;
+        __syncthreads();
+        if (wave != 0) return;
+        fx = red[0][0][lane];
+        fy = red[0][1][lane];
+        fz = red[0][2][lane];
+        acc = red[0][3][lane];
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) {
+            fx += red[w][0][lane];
+            fy += red[w][1][lane];
+            fz += red[w][2][lane];
+            acc += red[w][3][lane];
+        }
+    }
+
+    // ---- particle-local terms (wave 0) ----
+    const int i = a.sidx[sl];
+    const int par = ctx->parity;
+    const float4* __restrict__ posc = par ? a.pos1 : a.pos0;
+    float4* __restrict__ posn = par ? a.pos0 : a.pos1;
+    const float4 km = a.kmu[i];
+    const float xi = pi.x, yi = pi.y, zi = pi.z;
+    const float bs = (float)ctx->bs;
+    float e_sw = 0.f, e_bond = 0.f, e_bend = 0.f, e_win = 0.f, e_wout = 0.f, e_pt = 0.f, e_kf = 0.f;
+    float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
+
+    if (a.has_bonds) {
+        const int eb = a.boff[i], ee = a.boff[i + 1];
+        for (int q = eb; q < ee; ++q) {
+            const int2 en = a.bent[q];
+            const BondParam bp = a.bpar[en.y];
+            const float4 pj = posc[en.x];
+            const float rx = xi - pj.x, ry = yi - pj.y, rz = zi - pj.z;
+            const float r2 = fmaf(rz, rz, fmaf(ry, ry, rx * rx));
+            float c = 0.f, U = 0.f;
+            if (bp.type == kSoftwell) {
+                if (r2 < bp.la) {
+                    const float u = r2 * bp.kb;
+                    const float den = 1.f + u * u * u;
+                    c = -6.f * bp.ka * u * u * bp.kb / (den * den);
+                    e_sw += -0.5f * bp.ka / den;
+                }
+            } else {
+                float K = bp.ka, l = bp.la;
+                if (bp.mix) {
+                    const float4 kj = a.kmu[en.x];
+                    const float A = 0.5f * (km.y + kj.y), B = 0.5f * (km.z + kj.z);
+                    K = A * bp.ka + B * bp.kb;
+                    l = A * bp.la + B * bp.lb;
+                }
+                if (bp.scaled) {
+                    K = K * (1.f / (bs * bs));
+                    l = l * bs;
+                }
+                c = spring_coef(bp.type, K, l, r2, U);
+                e_bond += 0.5f * U;
+            }
+            fx = fmaf(c, rx, fx);
+            fy = fmaf(c, ry, fy);
+            fz = fmaf(c, rz, fz);
+        }
+    }
+
+    if (a.has_bend) {
+        for (int role = 0; role < 3; ++role) {
+            const int k0 = i - role;
+            if (k0 < 0 || k0 + 2 >= n) continue;
+            const float eps = a.bend_eps[k0];
+            if (eps == 0.f) continue;
+            float4 q0 = (role == 0) ? make_float4(xi, yi, zi, 0.f) : posc[k0];
+            float4 q1 = (role == 1) ? make_float4(xi, yi, zi, 0.f) : posc[k0 + 1];
+            float4 q2 = (role == 2) ? make_float4(xi, yi, zi, 0.f) : posc[k0 + 2];
+            const float r1x = q1.x - q0.x, r1y = q1.y - q0.y, r1z = q1.z - q0.z;
+            const float r2x = q2.x - q1.x, r2y = q2.y - q1.y, r2z = q2.z - q1.z;
+            const float n1 = r1x * r1x + r1y * r1y + r1z * r1z;
+            const float n2 = r2x * r2x + r2y * r2y + r2z * r2z;
+            if (!(n1 > 0.f) || !(n2 > 0.f)) continue;
+            const float inv12 = rsqrtf(n1 * n2);
+            const float cv = (r1x * r2x + r1y * r2y + r1z * r2z) * inv12;
+            const float i1 = cv / n1, i2 = cv / n2;
+            const float d1x = r2x * inv12 - i1 * r1x, d1y = r2y * inv12 - i1 * r1y, d1z = r2z * inv12 - i1 * r1z;
+            const float d2x = r1x * inv12 - i2 * r2x, d2y = r1y * inv12 - i2 * r2y, d2z = r1z * inv12 - i2 * r2z;
+            if (role == 0) {
+                fx -= eps * d1x; fy -= eps * d1y; fz -= eps * d1z;
+                e_bend += eps * (1.f - cv);
+            } else if (role == 2) {
+                fx += eps * d2x; fy += eps * d2y; fz += eps * d2z;
+            } else {
+                fx += eps * (d1x - d2x); fy += eps * (d1y - d2y); fz += eps * (d1z - d2z);
+            }
+        }
+    }
+
+    if (a.has_tether) {
+        const int tb = a.toff[i], te = a.toff[i + 1];
+        for (int q = tb; q < te; ++q) {
+            const Tether t = a.tent[q];
+            const float rx = xi - t.px, ry = yi - t.py, rz = zi - t.pz;
+            float U;
+            const float c = spring_coef(kSpring, t.k, t.l, rx * rx + ry * ry + rz * rz, U);
+            e_kf += U;
+            fx = fmaf(c, rx, fx);
+            fy = fmaf(c, ry, fy);
+            fz = fmaf(c, rz, fz);
+        }
+    }
+
+    for (int q = 0; q < a.n_point; ++q) {
+        const PointSrc& p = a.point[q];
+        const float rx = xi - p.px, ry = yi - p.py, rz = zi - p.pz;
+        const float r2 = rx * rx + ry * ry + rz * rz;
+        float c, U;
+        if (p.type == GCS_POT_FORCE_FLUX) {
+            // common/potentials/force_flux_potential.hpp:24-37
+            const float r1 = sqrtf(r2), b2 = p.b * p.b;
+            c = (r1 > 0.f) ? p.f * b2 / (b2 * r1 + r1 * r2) : 0.f;
+            U = p.f * p.b * atan2f(p.b, r1);
+        } else {
+            c = spring_coef(p.type == GCS_POT_SEMISPRING ? kSemispring : (p.type == GCS_POT_HARMONIC ? kHarmonic : kSpring),
+                            p.k, p.l, r2, U);
+        }
+        e_pt += U;
+        fx = fmaf(c, rx, fx);
+        fy = fmaf(c, ry, fy);
+        fz = fmaf(c, rz, fz);
+    }
+
+    if (a.has_wall_in || a.has_wall_out) {
+        // Sampson distance to the ellipsoid (DESIGN.md "ellipsoid wall"): rho = |r o 1/ax|,
+        // g = r o 1/ax^2, d = |1 - rho| rho / |g|, normal n = g / |g|
+        const float ax = (float)ctx->wall[0], ay = (float)ctx->wall[1], az = (float)ctx->wall[2];
+        const float cx = a.has_wall_in ? a.win.cx : a.wout_cx;
+        const float cy = a.has_wall_in ? a.win.cy : a.wout_cy;
+        const float cz = a.has_wall_in ? a.win.cz : a.wout_cz;
+        const float rx = xi - cx, ry = yi - cy, rz = zi - cz;
+        const float qx = rx / ax, qy = ry / ay, qz = rz / az;
+        const float gx = qx / ax, gy = qy / ay, gz = qz / az;
+        const float g2 = gx * gx + gy * gy + gz * gz;
+        if (g2 > 0.f) {
+            const float rho = sqrtf(qx * qx + qy * qy + qz * qz);
+            const float ginv = rsqrtf(g2);
+            const float d = fabsf(1.f - rho) * rho * ginv;
+            const float nx_ = gx * ginv, ny_ = gy * ginv, nz_ = gz * ginv;
+            if (a.has_wall_in && rho < 1.f) {
+                const WallIn& w = a.win;
+                const float sc = w.scaled ? cs : 1.f;
+                const float A = w.mix ? 0.5f * (km.y + w.wall_a) : 1.f;
+                const float B = w.mix ? 0.5f * (km.z + w.wall_b) : 0.f;
+                const float d2 = d * d;
+                const float sa = w.a_sig * sc, sbw = w.b_sig * sc;
+                const float k2a = 1.f / (sa * sa), k2b = 1.f / (sbw * sbw);
+                const float ua = d2 * k2a, t = d2 * k2b;
+                float coef = 0.f, U = 0.f;
+                if (ua < 1.f) {
+                    const float ga = 1.f - ua;
+                    coef += A * 6.f * w.a_eps * k2a * ga * ga;
+                    U += A * w.a_eps * ga * ga * ga;
+                }
+                if (t < 1.f && B != 0.f) {
+                    const float t2 = t * t;
+                    const float gb = 1.f - t2 * t2;
+                    coef += B * 24.f * w.b_eps * k2b * gb * gb * t2 * t;
+                    U += B * w.b_eps * gb * gb * gb;
+                }
+                const float wx = -coef * d * nx_, wy = -coef * d * ny_, wz = -coef * d * nz_;
+                fx += wx; fy += wy; fz += wz;
+                rin[0] = fabsf(wx); rin[1] = fabsf(wy); rin[2] = fabsf(wz);
+                e_win += U;
+            }
+            if (a.has_wall_out && rho > 1.f) {
+                const float wx = -a.wout_k * d * nx_, wy = -a.wout_k * d * ny_, wz = -a.wout_k * d * nz_;
+                fx += wx; fy += wy; fz += wz;
+                rout[0] = fabsf(wx); rout[1] = fabsf(wy); rout[2] = fabsf(wz);
+                e_wout += 0.5f * a.wout_k * d * d;
+            }
+        }
+    }
+
+    if (MODE == kModeEnergy) {
+        const double vals[kEnergyKinds] = {valid ? (double)acc : 0.0,  valid ? (double)e_sw : 0.0,
+                                           valid ? (double)e_bond : 0.0, valid ? (double)e_bend : 0.0,
+                                           valid ? (double)e_win : 0.0,  valid ? (double)e_wout : 0.0,
+                                           valid ? (double)e_pt : 0.0,   valid ? (double)e_kf : 0.0};
+        for (int k = 0; k < kEnergyKinds; ++k) {
+            const double t = wave_sum_d(vals[k]);
+            if (lane == 0) a.part_energy[blockIdx.x * kEnergyKinds + k] = t;
+        }
+        return;
+    }
+
+    // reaction / neighbour partials
+    {
+        float vals[kForcePartials];
+        vals[0] = valid ? rin[0] : 0.f;
+        vals[1] = valid ? rin[1] : 0.f;
+        vals[2] = valid ? rin[2] : 0.f;
+        vals[3] = valid ? rout[0] : 0.f;
+        vals[4] = valid ? rout[1] : 0.f;
+        vals[5] = valid ? rout[2] : 0.f;
+        const float drift = valid ? km.x * sqrtf(fx * fx + fy * fy + fz * fz) : 0.f;
+        vals[7] = valid ? acc : 0.f;
+        float outv[kForcePartials];
+        for (int k = 0; k < kForcePartials; ++k) outv[k] = (k == 6) ? wave_max(drift) : wave_sum(vals[k]);
+        if (lane == 0)
+            for (int k = 0; k < kForcePartials; ++k) a.part_force[blockIdx.x * kForcePartials + k] = outv[k];
+    }
+
+    if (MODE == kModeForce) {
+        if (valid) a.force_out[i] = make_float4(fx, fy, fz, 0.f);
+        return;
+    }
+
+    // ---- Euler-Maruyama update: x += mu dt F + sqrt(2 T mu dt) xi ----
+    const float mu = km.x;
+    const float dt = a.timestep;
+    float n0, n1, n2;
+    noise3(a, ctx, i, n0, n1, n2);
+    const float amp = sqrtf(2.f * a.temperature * mu * dt);
+    const float mdt = mu * dt;
+    const float nxp = xi + mdt * fx + amp * n0;
+    const float nyp = yi + mdt * fy + amp * n1;
+    const float nzp = zi + mdt * fz + amp * n2;
+    if (valid) posn[i] = make_float4(nxp, nyp, nzp, 0.f);
+    {
+        const float big = 3.0e38f;
+        const float l0 = wave_min(valid ? nxp : big), l1 = wave_min(valid ? nyp : big), l2 = wave_min(valid ? nzp : big);
+        const float h0 = wave_max(valid ? nxp : -big), h1 = wave_max(valid ? nyp : -big), h2 = wave_max(valid ? nzp : -big);
+        if (lane == 0) {
+            float* pb = a.part_bbox + blockIdx.x * kBBoxPartials;
+            pb[0] = l0; pb[1] = l1; pb[2] = l2; pb[3] = h0; pb[4] = h1; pb[5] = h2;
+        }
+    }
+}
+
+// spacestep path: update from stored forces with the adapted timestep (ctx->dt_used)
+__global__ __launch_bounds__(kUpdateBlock) void k_update(const DevCtx* __restrict__ ctx, ForceArgs a)
+{
+    __shared__ float red[6][kUpdateBlock / 64];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = i < a.n;
+    const int il = valid ? i : a.n - 1;
+    const int par = ctx->parity;
+    const float4* posc = par ? a.pos1 : a.pos0;
+    float4* posn = par ? a.pos0 : a.pos1;
+    const float4 p = posc[il];
+    const float4 f = a.force_out[il];
+    const float mu = a.kmu[il].x;
+    const float dt = (float)ctx->dt_used;
+    float n0, n1, n2;
+    noise3(a, ctx, il, n0, n1, n2);
+    const float amp = sqrtf(2.f * a.temperature * mu * dt);
+    const float mdt = mu * dt;
+    const float x = p.x + mdt * f.x + amp * n0;
+    const float y = p.y + mdt * f.y + amp * n1;
+    const float z = p.z + mdt * f.z + amp * n2;
+    if (valid) posn[i] = make_float4(x, y, z, 0.f);
+    const float big = 3.0e38f;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float v[6] = {wave_min(valid ? x : big),  wave_min(valid ? y : big),  wave_min(valid ? z : big),
+                  wave_max(valid ? x : -big), wave_max(valid ? y : -big), wave_max(valid ? z : -big)};
+    if (lane == 0)
+        for (int k = 0; k < 6; ++k) red[k][wave] = v[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float* pb = a.part_bbox + blockIdx.x * kBBoxPartials;
+        for (int k = 0; k < 6; ++k) {
+            float r = red[k][0];
+            for (int w = 1; w < kUpdateBlock / 64; ++w) r = (k < 3) ? fminf(r, red[k][w]) : fmaxf(r, red[k][w]);
+            pb[k] = r;
+        }
+    }
+}
+
+// spacestep: dt_used = min(dt, spacestep / max_i mu_i |F_i|)   (INFERRED semantics)
+__global__ __launch_bounds__(256) void k_adapt(DevCtx* ctx, ForceArgs a, int blocks, float spacestep, float timestep)
+{
+    __shared__ float red[4];
+    float m = 0.f;
+    for (int b = threadIdx.x; b < blocks; b += blockDim.x) m = fmaxf(m, a.part_force[b * kForcePartials + 6]);
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float mm = red[0];
+        for (int w = 1; w < (int)(blockDim.x / 64); ++w) mm = fmaxf(mm, red[w]);
+        double dt = timestep;
+        if (spacestep > 0.f && (double)mm * dt > (double)spacestep) dt = (double)spacestep / (double)mm;
+        ctx->dt_used = dt;
+        ctx->max_drift = mm;
+    }
+}
+
+// fixed-order reduction of the per-block partials + the device-resident interphase schedule
+__global__ __launch_bounds__(256) void k_tail(DevCtx* ctx, ForceArgs a, int fblocks, int bblocks, int advance,
+                                              int apply_sched, int ncell_max, const double* __restrict__ sched)
+{
+    __shared__ double sred[8][256];
+    __shared__ float bred[6][256];
+    const int tid = threadIdx.x;
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int b = tid; b < fblocks; b += 256)
+        for (int k = 0; k < 8; ++k) {
+            const float v = a.part_force[b * kForcePartials + k];
+            if (k == 6)
+                acc[6] = fmax(acc[6], (double)v);
+            else
+                acc[k] += (double)v;
+        }
+    float bb[6] = {3.0e38f, 3.0e38f, 3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
+    for (int b = tid; b < bblocks; b += 256)
+        for (int k = 0; k < 6; ++k) {
+            const float v = a.part_bbox[b * kBBoxPartials + k];
+            bb[k] = (k < 3) ? fminf(bb[k], v) : fmaxf(bb[k], v);
+        }
+    for (int k = 0; k < 8; ++k) sred[k][tid] = acc[k];
+    for (int k = 0; k < 6; ++k) bred[k][tid] = bb[k];
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (tid < w) {
+            for (int k = 0; k < 8; ++k)
+                sred[k][tid] = (k == 6) ? fmax(sred[k][tid], sred[k][tid + w]) : sred[k][tid] + sred[k][tid + w];
+            for (int k = 0; k < 6; ++k)
+                bred[k][tid] = (k < 3) ? fminf(bred[k][tid], bred[k][tid + w]) : fmaxf(bred[k][tid], bred[k][tid + w]);
+        }
+        __syncthreads();
+    }
+    if (tid != 0) return;
+    if (fblocks > 0) {
+        for (int k = 0; k < 3; ++k) {
+            ctx->react_in[k] = sred[k][0];
+            ctx->react_out[k] = sred[3 + k][0];
+        }
+        ctx->max_drift = sred[6][0];
+        ctx->neighbors = sred[7][0] / (double)a.n;
+    }
+    if (bblocks > 0)
+        for (int k = 0; k < 3; ++k) {
+            ctx->bbox_lo[k] = bred[k][0];
+            ctx->bbox_hi[k] = bred[3 + k][0];
+        }
+    if (advance) {
+        ctx->step += 1;
+        ctx->parity ^= 1;
+        if (a.noise_mode == GCS_NOISE_INJECTED) ctx->noise_cursor += 1;
+    }
+    if (apply_sched) {
+        // stage_interphase/simulation_driver_interphase.cpp:17 (time), :67-76 (scales), :79-90 (wall)
+        const int flags = (int)sched[kSchedFlags];
+        const double dt = sched[kSchedDt];
+        if (flags & 1) ctx->time = (double)ctx->step * dt;
+        if (flags & 2) {
+            ctx->cs = 1.0 - (1.0 - sched[kSchedCs0]) * exp(-(ctx->time / sched[kSchedCsTau]));
+            ctx->bs = 1.0 - (1.0 - sched[kSchedBs0]) * exp(-(ctx->time / sched[kSchedBsTau]));
+        }
+        if (flags & 4)
+            for (int k = 0; k < 3; ++k) {
+                double net = 0.0;
+                net += ctx->react_in[k] + ctx->react_out[k];
+                net -= sched[kSchedK0 + k] * ctx->wall[k];
+                ctx->wall[k] += dt * sched[kSchedMuW] * net;
+            }
+    }
+    compute_grid(ctx, pair_cutoff(a, ctx->cs), ncell_max);
+}
+
+// ----------------------------------------------------------------------------------------------------
+// neighbor search (contact map / md::neighbor_searcher): strict fp32 predicate, pairs i < j
+
+__device__ inline bool strict_pair(float4 p, float4 q, float rc2)
+{
+    const float dx = __fsub_rn(p.x, q.x), dy = __fsub_rn(p.y, q.y), dz = __fsub_rn(p.z, q.z);
+    const float r2 = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
+    return r2 < rc2;
+}
+
+template <bool EMIT>
+__global__ __launch_bounds__(256) void k_search(const DevCtx* __restrict__ ctx, int n, const float4* __restrict__ spos,
+                                                const int* __restrict__ sidx, const int* __restrict__ scell,
+                                                const int* __restrict__ cstart, int* __restrict__ counts,
+                                                const int* __restrict__ offsets, unsigned long long* __restrict__ keys)
+{
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const Grid g = ctx->grid;
+    const float rc2 = __fmul_rn(g.rc, g.rc);
+    const int i = sidx[s];
+    const float4 p = spos[s];
+    const int c = scell[s];
+    const int nx = g.n[0], ny = g.n[1], nz = g.n[2];
+    const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
+    int cnt = 0;
+    long long o = EMIT ? offsets[s] : 0;
+    for (int z = max(cz - 1, 0); z <= min(cz + 1, nz - 1); ++z)
+        for (int y = max(cy - 1, 0); y <= min(cy + 1, ny - 1); ++y) {
+            const int base = (z * ny + y) * nx;
+            const int jb = cstart[base + max(cx - 1, 0)], je = cstart[base + min(cx + 1, nx - 1) + 1];
+            for (int t = jb; t < je; ++t) {
+                const int j = sidx[t];
+                if (j <= i) continue;
+                if (!strict_pair(p, spos[t], rc2)) continue;
+                if (EMIT) keys[o++] = ((unsigned long long)(unsigned)i << 32) | (unsigned)j;
+                cnt++;
+            }
+        }
+    if (!EMIT) counts[s] = cnt;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_small(const int* __restrict__ in, int* __restrict__ out, int n,
+                                                     int* __restrict__ total)
+{
+    __shared__ int wtot[16];
+    const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int per = (n + T - 1) / T;
+    const int b = min(n, tid * per), e = min(n, b + per);
+    int sum = 0;
+    for (int k = b; k < e; ++k) sum += in[k];
+    int incl = wave_incl_scan(sum, lane);
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    if (wave == 0) {
+        int v = (lane < T / 64) ? wtot[lane] : 0;
+        int vi = wave_incl_scan(v, lane);
+        if (lane < T / 64) wtot[lane] = vi - v;
+        if (lane == T / 64 - 1) *total = vi;
+    }
+    __syncthreads();
+    int run = wtot[wave] + incl - sum;
+    for (int k = b; k < e; ++k) {
+        int c = in[k];
+        out[k] = run;
+        run += c;
+    }
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------------------------------------------
+// launch wrappers
+
+void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed, int ncell_max)
+{
+    hipLaunchKernelGGL(k_prime, dim3(1), dim3(1024), 0, s, ctx, a, rc_fixed, ncell_max);
+}
+
+void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n, int* cell_of,
+                       int* slot, int* count)
+{
+    hipLaunchKernelGGL(k_cell_count, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, n, cell_of, slot, count);
+}
+
+void launch_cell_scan(hipStream_t s, const DevCtx* ctx, int n, int* count, int* cstart)
+{
+    hipLaunchKernelGGL(k_cell_scan, dim3(1), dim3(1024), 0, s, ctx, n, count, cstart);
+}
+
+void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* slot, const int* cstart, int* tmp)
+{
+    hipLaunchKernelGGL(k_cell_scatter, dim3((n + 255) / 256), dim3(256), 0, s, n, cell_of, slot, cstart, tmp);
+}
+
+void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, const float4* kmu, int n,
+                      const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell, float4* spos,
+                      float* sb, int pair_mix)
+{
+    hipLaunchKernelGGL(k_cell_sort, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, kmu, n, tmp, cell_of,
+                       cstart, sidx, scell, spos, sb, pair_mix);
+}
+
+template <int MODE>
+static void launch_force_mode(hipStream_t s, int waves, const DevCtx* ctx, const ForceArgs& a)
+{
+    const dim3 grid(force_blocks(a.n));
+    switch (waves) {
+    case 1: hipLaunchKernelGGL((k_force<MODE, 1>), grid, dim3(64), 0, s, ctx, a); break;
+    case 2: hipLaunchKernelGGL((k_force<MODE, 2>), grid, dim3(128), 0, s, ctx, a); break;
+    case 8: hipLaunchKernelGGL((k_force<MODE, 8>), grid, dim3(512), 0, s, ctx, a); break;
+    default: hipLaunchKernelGGL((k_force<MODE, 4>), grid, dim3(256), 0, s, ctx, a); break;
+    }
+}
+
+void launch_force(hipStream_t s, int mode, int waves, const DevCtx* ctx, const ForceArgs& a)
+{
+    if (mode == kModeStep)
+        launch_force_mode<kModeStep>(s, waves, ctx, a);
+    else if (mode == kModeForce)
+        launch_force_mode<kModeForce>(s, waves, ctx, a);
+    else
+        launch_force_mode<kModeEnergy>(s, waves, ctx, a);
+}
+
+void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a)
+{
+    hipLaunchKernelGGL(k_update, dim3(update_blocks(a.n)), dim3(kUpdateBlock), 0, s, ctx, a);
+}
+
+void launch_adapt(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int fblocks, float spacestep, float timestep)
+{
+    hipLaunchKernelGGL(k_adapt, dim3(1), dim3(256), 0, s, ctx, a, fblocks, spacestep, timestep);
+}
+
+void launch_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance, int apply_sched,
+                 int ncell_max, const double* sched)
+{
+    hipLaunchKernelGGL(k_tail, dim3(1), dim3(256), 0, s, ctx, a, fblocks, bblocks, advance, apply_sched, ncell_max,
+                       sched);
+}
+
+void launch_search_count(hipStream_t s, const DevCtx* ctx, int n, const float4* spos, const int* sidx, const int* scell,
+                         const int* cstart, int* counts)
+{
+    hipLaunchKernelGGL((k_search<false>), dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, spos, sidx, scell, cstart,
+                       counts, (const int*)nullptr, (unsigned long long*)nullptr);
+}
+
+void launch_search_emit(hipStream_t s, const DevCtx* ctx, int n, const float4* spos, const int* sidx, const int* scell,
+                        const int* cstart, const int* offsets, unsigned long long* keys)
+{
+    hipLaunchKernelGGL((k_search<true>), dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, spos, sidx, scell, cstart,
+                       (int*)nullptr, offsets, keys);
+}
+
+void launch_exclusive_scan_small(hipStream_t s, const int* in, int* out, int n, int* total)
+{
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, s, in, out, n, total);
+}
+
+size_t sort_u64_temp_bytes(int n)
+{
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr, n);
+    return bytes;
+}
+
+void sort_u64_keys(hipStream_t s, unsigned long long* keys, unsigned long long* tmp, int n, void* temp, size_t temp_bytes)
+{
+    (void)hipcub::DeviceRadixSort::SortKeys(temp, temp_bytes, keys, tmp, n, 0, 64, s);
+}
+
+}  // namespace gcs

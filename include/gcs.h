@@ -1,0 +1,276 @@
+/*
+ * gcs.h -- C ABI of the MI355X-native overdamped-Langevin chromosome-polymer engine.
+ *
+ * Drop-in boundary for the hot path of snsinfu/3d-genome-cycle: the force/integrator loop that the
+ * stage drivers run through the (un-vendored, header-only) micromd library `md::`.  Every entry point
+ * below replaces one micromd call site used by the reference drivers; the replaced interface is cited
+ * as reference file:line (paths relative to src/simulation/ of the reference).
+ *
+ *   md::system{add_particle, view_mobilities, add_attribute}   -> gcs_engine_create
+ *       stage_interphase/simulation_driver_particles.cpp:9-35, stage_anatelophase/simulation_driver.cpp:57-64
+ *   md::make_neighbor_pairwise_forcefield(a*softcore<2,3> + b*softcore<8,3>)
+ *                                                              -> gcs_add_neighbor_softcore
+ *       stage_interphase/simulation_driver_forcefield.cpp:21-53; stage_anatelophase/simulation_driver.cpp:123-137;
+ *       stage_prometaphase/simulation_driver.cpp:99-111
+ *   md::make_neighbor_pairwise_forcefield(apply_cutoff(softwell<6>)).set_neighbor_targets
+ *                                                              -> gcs_add_neighbor_softwell
+ *       stage_interphase/simulation_driver_forcefield.cpp:168-185
+ *   md::make_bonded_pairwise_forcefield + add_bonded_range / add_bonded_pair
+ *                                                              -> gcs_add_bonded_pairwise
+ *       stage_interphase/simulation_driver_forcefield.cpp:56-160; stage_anatelophase/simulation_driver.cpp:145-163;
+ *       stage_prometaphase/simulation_driver.cpp:114-166
+ *   md::make_bonded_triplewise_forcefield(cosine_bending_potential) -> gcs_add_bonded_triplewise
+ *       stage_anatelophase/simulation_driver.cpp:165-187; stage_prometaphase/simulation_driver.cpp:126-144
+ *   md::make_ellipsoid_inward_forcefield / make_ellipsoid_outward_forcefield (+ stats.axial_reaction)
+ *                                                              -> gcs_add_ellipsoid_inward / _outward
+ *       stage_interphase/simulation_driver_forcefield.cpp:189-244
+ *   md::make_point_source_forcefield(semispring | force_flux_potential) -> gcs_add_point_source
+ *       stage_anatelophase/simulation_driver.cpp:221-235; stage_prometaphase/simulation_driver.cpp:210-230;
+ *       common/potentials/force_flux_potential.hpp:19-37
+ *   kinetochore_fiber_forcefield (custom md::forcefield)       -> gcs_add_kinetochore_fiber
+ *       common/forcefield/kinetochore_fiber_forcefield.{hpp:8-30, cpp:9-84}
+ *   md::system::remove_forcefield                             -> gcs_remove_forcefield
+ *       stage_anatelophase/simulation_driver.cpp:277-285 (anaphase -> telophase swap)
+ *   md::system::view_positions (read/write)                    -> gcs_engine_set_positions / _get_positions
+ *       stage_interphase/simulation_driver_relaxation.cpp:14-23; simulation_driver_interphase.cpp:34
+ *   md::system::compute_energy / compute_potential_energy      -> gcs_engine_compute_energy
+ *       stage_interphase/simulation_driver_interphase.cpp:24-27; stage_prometaphase/simulation_driver.cpp:299
+ *   md::simulate_brownian_dynamics(system, {T, dt, spacestep, steps, seed, callback})
+ *                                                              -> gcs_engine_run (+ gcs_engine_set_schedule)
+ *       stage_interphase/simulation_driver_interphase.cpp:57-63; simulation_driver_relaxation.cpp:48-55;
+ *       stage_anatelophase/simulation_driver.cpp:308-314, 349-355; stage_prometaphase/simulation_driver.cpp:278-284
+ *     The per-step callback's force-field mutations (update_core_scale, update_wall_semiaxes,
+ *     stage_interphase/simulation_driver_interphase.cpp:67-90) run ON DEVICE via gcs_schedule; the host
+ *     regains control only at interval boundaries (logging / sampling / contact map).
+ *   md::neighbor_searcher<md::open_box>(box, dist).set_points().search() -> gcs_engine_search_neighbors
+ *       stage_interphase/contact_map.cpp:60-62
+ *
+ * Conventions: every function returns 0 (GCS_OK) on success or a positive GCS_E* code; the message of
+ * the most recent failure on the calling thread is returned by gcs_last_error().  All arrays crossing
+ * the boundary are plain host pointers owned by the caller and copied; device memory is engine-owned.
+ * Positions are fp64 at the boundary (md::point is double) and fp32 on the device.  One engine per host
+ * thread, bound to one HIP device and one stream; engines are not internally locked.
+ */
+#ifndef GCS_H
+#define GCS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GCS_ABI_VERSION 1
+
+/* status codes */
+#define GCS_OK 0
+#define GCS_EINVAL 1    /* bad argument */
+#define GCS_EHIP 2      /* HIP runtime failure (message names the call) */
+#define GCS_ESTATE 3    /* call not valid in the engine's current state */
+#define GCS_ENOMEM 4    /* allocation failure */
+#define GCS_ECAPACITY 5 /* output buffer too small; the required count is still returned */
+
+/* pair potentials (micromd names) */
+#define GCS_POT_SEMISPRING 0 /* U = K/2 (r-l)^2 for r > l, else 0 */
+#define GCS_POT_HARMONIC 1   /* U = K/2 r^2 */
+#define GCS_POT_SPRING 2     /* U = K/2 (r-l)^2 */
+#define GCS_POT_FORCE_FLUX 3 /* U = b f atan2(b, r)   (common/potentials/force_flux_potential.hpp:24-37) */
+
+/* noise sources for gcs_engine_run */
+#define GCS_NOISE_PHILOX 0   /* counter-based Philox4x32-10 keyed by (seed, step, particle): production */
+#define GCS_NOISE_INJECTED 1 /* normals uploaded with gcs_engine_set_noise (reference-order parity mode) */
+#define GCS_NOISE_NONE 2     /* deterministic drift only */
+
+typedef struct gcs_engine gcs_engine;
+
+/* md::system construction: particle count, per-particle mobility and the interphase particle_data
+ * attribute {a_factor, b_factor} (common/particle_data.hpp:6-13). */
+typedef struct gcs_system_desc {
+    int64_t particle_count;
+    const double* mobilities; /* [N]; NULL -> 1 (micromd default mobility) */
+    const double* ab_factors; /* [N][2]; NULL -> (0, 0) */
+    int32_t device;           /* HIP device ordinal */
+    int32_t reserved;
+} gcs_system_desc;
+
+/* Neighbor-pairwise soft-core repulsion: U_ij = a_ij*SC<2,3>(r) + b_ij*SC<8,3>(r),
+ * SC<p,q>(r) = eps (1 - (r/sigma)^p)^q for r < sigma.
+ * mix = 1: a_ij = (a_i + a_j)/2, b_ij = (b_i + b_j)/2 (simulation_driver_forcefield.cpp:34-35);
+ * mix = 0: a_ij = 1, b_ij = 0 (plain softcore<2,3>, mitotic stages).
+ * scaled = 1: both diameters and neighbor_distance are multiplied by the context core_scale
+ * (simulation_driver_forcefield.cpp:39-43, 49-51). */
+typedef struct gcs_softcore_params {
+    double a_energy, a_diameter;
+    double b_energy, b_diameter;
+    double neighbor_distance;
+    int32_t mix;
+    int32_t scaled;
+} gcs_softcore_params;
+
+/* Bonded pairwise potential. mix = 1: K = a*a_spring + b*b_spring, l = a*a_length + b*b_length with
+ * a, b the pair means of the ab factors (simulation_driver_forcefield.cpp:65-76); mix = 0: K = a_spring,
+ * l = a_length.  scaled = 1: K /= s^2 and l *= s with s the context bond_scale (:81-83, :147-149). */
+typedef struct gcs_bond_params {
+    int32_t potential; /* GCS_POT_SEMISPRING | GCS_POT_HARMONIC | GCS_POT_SPRING */
+    int32_t mix;
+    int32_t scaled;
+    int32_t reserved;
+    double a_spring, b_spring;
+    double a_length, b_length;
+} gcs_bond_params;
+
+/* Droplet attraction among a target subset: apply_cutoff(softwell<exponent>{energy, decay}, cutoff),
+ * U = -energy / (1 + (r/decay)^exponent) for r < cutoff (simulation_driver_forcefield.cpp:173-185). */
+typedef struct gcs_softwell_params {
+    double energy;
+    double decay_distance;
+    double cutoff;
+    int32_t exponent; /* only 6 is used by the reference */
+    int32_t reserved;
+} gcs_softwell_params;
+
+/* Ellipsoid wall inward field: per-particle a = (a_i + wall_a)/2, b = (b_i + wall_b)/2 and
+ * a*SC<2,3>(a_energy, a_diameter) + b*SC<8,3>(b_energy, b_diameter) of the distance to the wall
+ * (simulation_driver_forcefield.cpp:203-225). Diameters are passed already halved (the reference
+ * uses a_core_diameter / 2); scaled multiplies them by core_scale.  The ellipsoid is centred at
+ * `center` with semiaxes taken from the context (:194-201). */
+typedef struct gcs_wall_params {
+    double a_energy, a_diameter;
+    double b_energy, b_diameter;
+    double wall_a, wall_b;
+    double center[3];
+    int32_t mix;
+    int32_t scaled;
+} gcs_wall_params;
+
+/* Point source field U(x - point) (make_point_source_forcefield). */
+typedef struct gcs_point_source_params {
+    int32_t potential; /* GCS_POT_SEMISPRING | GCS_POT_HARMONIC | GCS_POT_SPRING | GCS_POT_FORCE_FLUX */
+    int32_t reserved;
+    double point[3];
+    double spring, length;             /* spring-type potentials */
+    double force, reactive_distance;   /* force_flux_potential {constant_force, reactive_distance} */
+} gcs_point_source_params;
+
+/* kinetochore_fiber_forcefield::kinetochore_spec (common/forcefield/kinetochore_fiber_forcefield.hpp:14-20) */
+typedef struct gcs_kinetochore_spec {
+    int64_t particle_index;
+    double mobility;
+    double decay_rate;
+    double stationary_length;
+} gcs_kinetochore_spec;
+
+/* Driver context (common/simulation_context.hpp:7-18) plus the last force evaluation's statistics. */
+typedef struct gcs_context {
+    int64_t step;              /* last completed step */
+    double time;
+    double core_scale;
+    double bond_scale;
+    double wall_semiaxes[3];
+    double inward_reaction[3]; /* ellipsoid_inward stats.axial_reaction of the last force evaluation */
+    double outward_reaction[3];
+    double last_timestep;      /* timestep actually used by the last step (spacestep may shrink it) */
+} gcs_context;
+
+/* Device-resident replacement of the per-step callback's state updates
+ * (stage_interphase/simulation_driver_interphase.cpp:16-17, 51-52, 67-90). */
+typedef struct gcs_schedule {
+    int32_t update_time;   /* time = step * timestep */
+    int32_t update_scales; /* core/bond scale = 1 - (1 - init) exp(-time / tau) */
+    int32_t update_wall;   /* semiaxes += timestep * wall_mobility * (R_in + R_out - spring o semiaxes) */
+    int32_t reserved;
+    double timestep;
+    double core_scale_init, core_scale_tau;
+    double bond_scale_init, bond_scale_tau;
+    double wall_semiaxes_spring[3];
+    double wall_mobility;
+} gcs_schedule;
+
+/* md::brownian_dynamics_config {temperature, timestep, spacestep, steps, seed} */
+typedef struct gcs_bd_config {
+    double temperature;
+    double timestep;
+    double spacestep; /* > 0: the step's timestep is reduced so that max_i |mu_i F_i| dt <= spacestep */
+    uint64_t seed;
+    int32_t noise;    /* GCS_NOISE_* */
+    int32_t reserved;
+} gcs_bd_config;
+
+/* Per-kernel timing probe (HIP events on the engine stream around every launch of each kernel). */
+typedef struct gcs_profile {
+    int64_t steps;
+    double total_ms;          /* wall time of the probed steps (events around the whole loop) */
+    double force_ms;          /* average duration of one force/integrate launch */
+    double cell_ms;           /* average duration of the cell-list build (count + scan + scatter + sort) */
+    double tail_ms;           /* average duration of the schedule tail launch */
+    double mean_neighbors;    /* mean number of neighbours within the cutoff per particle (last step) */
+} gcs_profile;
+
+const char* gcs_last_error(void);
+int gcs_abi_version(void);
+int gcs_device_count(int32_t* count);
+
+int gcs_engine_create(const gcs_system_desc* desc, gcs_engine** out);
+int gcs_engine_destroy(gcs_engine* engine);
+int gcs_engine_particle_count(const gcs_engine* engine, int64_t* count);
+
+/* force fields; *handle receives an id usable with gcs_remove_forcefield */
+int gcs_add_neighbor_softcore(gcs_engine* e, const gcs_softcore_params* p, int32_t* handle);
+int gcs_add_neighbor_softwell(gcs_engine* e, const gcs_softwell_params* p,
+                              const int64_t* targets, int64_t n_targets, int32_t* handle);
+/* bonds: for each range [begin, end) the pairs (k, k + stride) with begin <= k, k + stride < end,
+ * plus the explicit pairs. stride 1 = add_bonded_range; stride 2 = the i, i+2 loop bonds. */
+int gcs_add_bonded_pairwise(gcs_engine* e, const gcs_bond_params* p,
+                            const int64_t* ranges, int64_t n_ranges, int32_t stride,
+                            const int64_t* pairs, int64_t n_pairs, int32_t* handle);
+/* cosine bending U = energy (1 - cos theta) over the triples (k, k+1, k+2) inside each range */
+int gcs_add_bonded_triplewise(gcs_engine* e, double bending_energy,
+                              const int64_t* ranges, int64_t n_ranges, int32_t* handle);
+int gcs_add_ellipsoid_inward(gcs_engine* e, const gcs_wall_params* p, int32_t* handle);
+int gcs_add_ellipsoid_outward(gcs_engine* e, double spring, const double center[3], int32_t* handle);
+int gcs_add_point_source(gcs_engine* e, const gcs_point_source_params* p, int32_t* handle);
+int gcs_add_kinetochore_fiber(gcs_engine* e, const double pole[3],
+                              const gcs_kinetochore_spec* specs, int64_t n_specs, int32_t* handle);
+int gcs_remove_forcefield(gcs_engine* e, int32_t handle);
+
+int gcs_engine_set_positions(gcs_engine* e, const double* xyz, int64_t n);
+int gcs_engine_get_positions(gcs_engine* e, double* xyz, int64_t n);
+int gcs_engine_set_context(gcs_engine* e, const gcs_context* ctx);
+int gcs_engine_get_context(gcs_engine* e, gcs_context* ctx);
+int gcs_engine_set_schedule(gcs_engine* e, const gcs_schedule* s);
+/* Apply the schedule once for `step` with the current reaction statistics (the driver's callback(0)). */
+int gcs_engine_apply_schedule(gcs_engine* e, int64_t step);
+
+/* Injected normals, [steps][N][3] in the order the reference integrator draws them; consumed by
+ * subsequent GCS_NOISE_INJECTED runs. */
+int gcs_engine_set_noise(gcs_engine* e, const double* normals, int64_t steps);
+
+/* Advance steps first_step+1 .. first_step+steps.  After each step the schedule is applied with that
+ * step's index (the reference callback order).  Asynchronous w.r.t. the host until a get_* call. */
+int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps);
+int gcs_engine_synchronize(gcs_engine* e);
+
+/* Total potential energy (md::system::compute_energy) and, if per_kind != NULL, a breakdown
+ * [pair, softwell, bonds, bending, wall_in, wall_out, point_source, kinetochore_fiber]. */
+int gcs_engine_compute_energy(gcs_engine* e, double* total, double* per_kind);
+/* Forces on every particle at the current positions/context ([N][3]); refreshes reaction stats. */
+int gcs_engine_compute_forces(gcs_engine* e, double* forces, int64_t n);
+
+/* Pairs (i < j) of `points` closer than `distance` (strict fp32 predicate), sorted by
+ * (i, j).  points == NULL searches the engine's current positions. pairs receives [count][2]. */
+int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, double distance,
+                                uint32_t* pairs, int64_t capacity, int64_t* count);
+
+int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps,
+                       gcs_profile* out);
+
+/* tuning knobs */
+#define GCS_OPT_GRAPH_STEPS 1   /* steps captured per hipGraph replay (0 = eager launches) */
+#define GCS_OPT_WAVES_PER_TILE 2 /* waves sharing one 64-particle tile of the pair loop: 1, 2, 4 or 8 */
+int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GCS_H */

@@ -1,0 +1,309 @@
+"""GPU parity: the HIP engine (libgcs.so, through the C ABI) against the fp64 CPU oracle.
+
+Tolerances (fp32 device arithmetic vs the fp64 restatement, stated per test):
+  forces        |dF| <= 1e-4 * max|F| + 1e-3 per component
+  energies      relative 1e-5 per kind (absolute 1e-4 for kinds near zero)
+  trajectories  |dx| <= 2e-5 after <= 50 steps with identical noise (injected or Philox)
+  neighbor sets bit-exact (strict fp32 predicate on both sides)
+"""
+import numpy as np
+import pytest
+
+from gcs import _abi as A
+from gcs import interphase, synthetic
+from gcs.config import InterphaseConfig
+from gcs.engine import Engine
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def both(design, cfg):
+    e, _ = interphase.build_interphase(Engine, design, cfg)
+    o, _ = interphase.build_interphase(oracle.OracleSystem, design, cfg)
+    return e, o
+
+
+def assert_forces_close(fe, fo):
+    scale = np.abs(fo).max()
+    err = np.abs(fe - fo).max()
+    assert err <= 1e-4 * scale + 1e-3, (err, scale)
+
+
+@pytest.fixture(scope="module")
+def c2_design():
+    return synthetic.make_c2()
+
+
+def test_forces_c1(c1_design, interphase_cfg):
+    e, o = both(c1_design, interphase_cfg)
+    assert_forces_close(e.compute_forces(), o.compute_forces())
+    ce, co = e.get_context(), o.get_context()
+    assert np.allclose(ce["inward_reaction"], co["inward_reaction"], rtol=1e-4, atol=1e-3)
+
+
+def test_forces_c1_full_scale(c1_design, interphase_cfg):
+    e, o = both(c1_design, interphase_cfg)
+    ctx = {"core_scale": 1.0, "bond_scale": 1.0, "wall_semiaxes": [1.55, 1.6, 1.5]}
+    e.set_context(ctx)
+    o.set_context(ctx)
+    assert_forces_close(e.compute_forces(), o.compute_forces())
+    ce, co = e.get_context(), o.get_context()
+    for k in ("inward_reaction", "outward_reaction"):
+        assert np.allclose(ce[k], co[k], rtol=1e-4, atol=1e-2), (k, ce[k], co[k])
+    assert max(co["inward_reaction"]) > 0 and max(co["outward_reaction"]) > 0
+
+
+def test_energy_c1(c1_design, interphase_cfg):
+    e, o = both(c1_design, interphase_cfg)
+    te, pe = e.compute_energy()
+    to, po = o.compute_energy()
+    assert te == pytest.approx(to, rel=1e-5)
+    assert np.allclose(pe, po, rtol=1e-5, atol=1e-4), (pe, po)
+
+
+def test_forces_c2(c2_design, interphase_cfg):
+    e, o = both(c2_design, interphase_cfg)
+    assert_forces_close(e.compute_forces(), o.compute_forces())
+    ctx = {"core_scale": 1.0, "bond_scale": 1.0, "wall_semiaxes": [1.9, 1.9, 1.9]}
+    e.set_context(ctx)
+    o.set_context(ctx)
+    assert_forces_close(e.compute_forces(), o.compute_forces())
+    te, pe = e.compute_energy()
+    to, po = o.compute_energy()
+    assert te == pytest.approx(to, rel=1e-5)
+
+
+def test_trajectory_injected_reference_noise(c1_design, interphase_cfg):
+    """Reference-order normals (std::mt19937_64 + libstdc++ normal_distribution, particle-major x,y,z)
+    injected into both: the engine reproduces the reference integrator's noise stream exactly."""
+    cfg = interphase_cfg
+    e, o = both(c1_design, cfg)
+    steps = 20
+    xi = oracle.reference_normals(123, steps * c1_design.n * 3).reshape(steps, c1_design.n, 3)
+    for s in (e, o):
+        s.set_schedule(**interphase.interphase_schedule(cfg))
+        s.apply_schedule(0)
+        s.set_noise(xi)
+        s.run(steps, temperature=cfg.temperature, timestep=cfg.timestep, noise=A.NOISE_INJECTED)
+    xe, xo = e.get_positions(), o.get_positions()
+    assert np.abs(xe - xo).max() <= 2e-5
+    ce, co = e.get_context(), o.get_context()
+    assert ce["step"] == co["step"] == steps
+    assert ce["core_scale"] == pytest.approx(co["core_scale"], rel=1e-12)
+    assert np.allclose(ce["wall_semiaxes"], co["wall_semiaxes"], rtol=1e-9)
+
+
+def test_trajectory_philox_c1(c1_design, interphase_cfg):
+    cfg = interphase_cfg
+    e, o = both(c1_design, cfg)
+    for s in (e, o):
+        s.set_schedule(**interphase.interphase_schedule(cfg))
+        s.apply_schedule(0)
+        s.run(50, temperature=cfg.temperature, timestep=cfg.timestep, seed=987654321)
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= 2e-5
+
+
+def test_trajectory_philox_c1_wall_contact(c1_design, interphase_cfg):
+    """Late-schedule window with the wall in contact: reactions drive the wall ODE on both sides."""
+    cfg = interphase_cfg
+    e, o = both(c1_design, cfg)
+    ctx = {"step": 200000, "time": 2.0, "core_scale": 0.99, "bond_scale": 0.99, "wall_semiaxes": [1.5, 1.55, 1.6]}
+    for s in (e, o):
+        s.set_context(ctx)
+        s.set_schedule(**interphase.interphase_schedule(cfg))
+        s.run(40, first_step=200000, temperature=cfg.temperature, timestep=cfg.timestep, seed=5)
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= 2e-5
+    ce, co = e.get_context(), o.get_context()
+    assert np.allclose(ce["wall_semiaxes"], co["wall_semiaxes"], rtol=1e-7)
+    assert np.allclose(ce["inward_reaction"], co["inward_reaction"], rtol=1e-3, atol=1e-2)
+    assert ce["step"] == 200040
+
+
+def test_relaxation_spacestep(c1_design, interphase_cfg):
+    cfg = interphase_cfg
+    e, o = both(c1_design, cfg)
+    steps = 10
+    xi = oracle.reference_normals(7, steps * c1_design.n * 3).reshape(steps, c1_design.n, 3)
+    for s in (e, o):
+        s.set_noise(xi)
+        s.run(steps, temperature=cfg.temperature, timestep=cfg.timestep, spacestep=cfg.relaxation_spacestep,
+              noise=A.NOISE_INJECTED)
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= 2e-5
+    assert e.get_context()["last_timestep"] == pytest.approx(o.get_context()["last_timestep"], rel=1e-4)
+
+
+def test_graph_and_eager_bitwise_identical(c1_design, interphase_cfg):
+    cfg = interphase_cfg
+    runs = []
+    for g in (0, 8, 32):
+        e, _ = interphase.build_interphase(Engine, c1_design, cfg)
+        e.set_option(A.OPT_GRAPH_STEPS, g)
+        e.set_schedule(**interphase.interphase_schedule(cfg))
+        e.apply_schedule(0)
+        e.run(70, seed=11)
+        runs.append((e.get_positions(), e.get_context()))
+    for x, c in runs[1:]:
+        assert np.array_equal(x, runs[0][0])
+        assert c == runs[0][1]
+
+
+@pytest.mark.parametrize("waves", [1, 2, 4, 8])
+def test_waves_per_tile_equivalent(c1_design, interphase_cfg, waves):
+    e, o = both(c1_design, interphase_cfg)
+    e.set_option(A.OPT_WAVES_PER_TILE, waves)
+    assert_forces_close(e.compute_forces(), o.compute_forces())
+
+
+def test_chunked_runs_equal_one_run(c1_design, interphase_cfg):
+    """The Philox counter is the absolute step: 3 chunks == 1 run, bit for bit."""
+    cfg = interphase_cfg
+    a, _ = interphase.build_interphase(Engine, c1_design, cfg)
+    b, _ = interphase.build_interphase(Engine, c1_design, cfg)
+    for s in (a, b):
+        s.set_schedule(**interphase.interphase_schedule(cfg))
+        s.apply_schedule(0)
+    a.run(60, seed=3)
+    b.run(25, first_step=0, seed=3)
+    b.run(20, first_step=25, seed=3)
+    b.run(15, first_step=45, seed=3)
+    assert np.array_equal(a.get_positions(), b.get_positions())
+
+
+def test_neighbor_search_bitexact_c1(c1_design):
+    e = Engine(c1_design.n)
+    e.set_positions(c1_design.positions)
+    for d in (0.12, 0.24, 0.3, 0.5):
+        assert np.array_equal(e.search_neighbors(d), oracle.search_neighbors(c1_design.positions, d))
+
+
+def test_neighbor_search_bitexact_c2(c2_design):
+    e = Engine(16)
+    for d in (0.12, 0.24):
+        got = e.search_neighbors(d, points=c2_design.positions)
+        exp = oracle.search_neighbors(c2_design.positions, d)
+        assert got.shape == exp.shape and np.array_equal(got, exp)
+
+
+def test_neighbor_search_edge_cases():
+    e = Engine(4)
+    pts = np.array([[0, 0, 0], [0, 0, 0], [0.25, 0, 0], [0.5, 0, 0], [5.0, 0, 0]], dtype=float)
+    assert e.search_neighbors(0.25, points=pts).tolist() == oracle.search_neighbors(pts, 0.25).tolist()
+    assert e.search_neighbors(0.2500001, points=pts).tolist() == oracle.search_neighbors(pts, 0.2500001).tolist()
+    assert e.search_neighbors(0.3, points=np.zeros((1, 3))).shape == (0, 2)
+    # all points coincident (degenerate bounding box)
+    same = np.zeros((70, 3))
+    got = e.search_neighbors(0.1, points=same)
+    assert got.shape == (70 * 69 // 2, 2)
+    assert np.array_equal(got, oracle.search_neighbors(same, 0.1))
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 200])
+def test_small_and_ragged_sizes(n):
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-0.5, 0.5, size=(n, 3))
+    ab = rng.choice([0.0, 0.5, 1.0], size=(n, 2))
+    mu = rng.uniform(0.5, 1.5, size=n)
+    sysd = {}
+    for name, cls in (("e", Engine), ("o", oracle.OracleSystem)):
+        s = cls(n, mobilities=mu, ab_factors=ab)
+        s.add_neighbor_softcore(2.5, 0.3, 2.5, 0.24, 0.3, mix=True, scaled=True)
+        if n > 1:
+            s.add_bonded_pairwise(A.POT_SEMISPRING, a_spring=100.0, b_spring=50.0, mix=True, scaled=True,
+                                  ranges=[(0, n)])
+        s.set_context({"core_scale": 0.8, "bond_scale": 0.7, "wall_semiaxes": [1, 1, 1]})
+        s.set_positions(x)
+        sysd[name] = s
+    assert_forces_close(sysd["e"].compute_forces(), sysd["o"].compute_forces())
+    for s in sysd.values():
+        s.run(5, seed=1, timestep=1e-4)
+    assert np.abs(sysd["e"].get_positions() - sysd["o"].get_positions()).max() <= 2e-5
+
+
+def test_particles_far_outside_and_coincident():
+    n = 130
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-1, 1, size=(n, 3))
+    x[:10] = 0.0          # coincident
+    x[10:15] += 50.0      # far away cluster
+    x[15] = [-80, 3, 3]   # isolated
+    res = []
+    for cls in (Engine, oracle.OracleSystem):
+        s = cls(n, ab_factors=np.tile([1.0, 0.0], (n, 1)))
+        s.add_neighbor_softcore(2.0, 0.3, neighbor_distance=0.3, mix=False)
+        s.set_positions(x)
+        res.append(s.compute_forces())
+    assert_forces_close(res[0], res[1])
+
+
+def test_mitotic_fields_parity():
+    rng = np.random.default_rng(7)
+    n = 120
+    x = np.cumsum(rng.normal(scale=0.15, size=(n, 3)), axis=0)
+    mu = np.full(n, 0.1)
+    out = []
+    for cls in (Engine, oracle.OracleSystem):
+        s = cls(n, mobilities=mu)
+        s.add_neighbor_softcore(a_energy=2.0, a_diameter=0.3, neighbor_distance=0.3, mix=False)
+        s.add_bonded_pairwise(A.POT_SEMISPRING, a_spring=1000.0, a_length=0.3, ranges=[(0, 60), (60, 120)])
+        s.add_bonded_triplewise(1.0, ranges=[(0, 20), (21, 60), (60, 80), (81, 120)])
+        s.add_bonded_pairwise(A.POT_SEMISPRING, a_spring=1000.0, a_length=0.3, pairs=[(20, 80)])
+        s.add_kinetochore_fiber([0.0, -5.0, 0.0], [(20, 0.1 / 60, 1.0, 0.0)])
+        s.add_kinetochore_fiber([0.0, 5.0, 0.0], [(80, 0.1 / 60, 1.0, 0.2)])
+        s.add_point_source(A.POT_FORCE_FLUX, [0.0, -5.0, 0.0], force=0.5, reactive_distance=0.3)
+        s.add_point_source(A.POT_FORCE_FLUX, [0.0, 5.0, 0.0], force=0.5, reactive_distance=0.3)
+        s.add_point_source(A.POT_SEMISPRING, [0.0, 0.0, 0.0], spring=100.0, length=1.5)
+        s.set_positions(x)
+        f = s.compute_forces()
+        en = s.compute_energy()
+        xi = oracle.reference_normals(99, 10 * n * 3).reshape(10, n, 3)
+        s.set_noise(xi)
+        s.run(10, timestep=1e-4, noise=A.NOISE_INJECTED)
+        out.append((f, en, s.get_positions()))
+    assert_forces_close(out[0][0], out[1][0])
+    assert out[0][1][0] == pytest.approx(out[1][1][0], rel=1e-5)
+    assert np.allclose(out[0][1][1], out[1][1][1], rtol=1e-5, atol=1e-4)
+    assert np.abs(out[0][2] - out[1][2]).max() <= 2e-5
+
+
+def test_remove_forcefield_swaps_like_anatelophase():
+    """stage_anatelophase/simulation_driver.cpp:277-285: remove the anaphase bonds/bending, add telophase ones"""
+    n = 90
+    rng = np.random.default_rng(3)
+    x = np.cumsum(rng.normal(scale=0.2, size=(n, 3)), axis=0)
+    res = []
+    for cls in (Engine, oracle.OracleSystem):
+        s = cls(n, mobilities=np.full(n, 0.1))
+        s.add_neighbor_softcore(2.0, 0.3, neighbor_distance=0.3, mix=False)
+        hb = s.add_bonded_pairwise(A.POT_SEMISPRING, a_spring=1000.0, a_length=0.3, ranges=[(0, 90)])
+        hk = s.add_bonded_triplewise(1.0, ranges=[(0, 90)])
+        s.set_positions(x)
+        s.run(5, timestep=1e-4, seed=4)
+        s.remove_forcefield(hb)
+        s.remove_forcefield(hk)
+        s.add_bonded_pairwise(A.POT_SEMISPRING, a_spring=500.0, a_length=0.3, ranges=[(0, 90)])
+        s.add_bonded_triplewise(3.0, ranges=[(0, 90)])
+        s.add_point_source(A.POT_SEMISPRING, [0, 0, 0], spring=100.0, length=1.5)
+        s.run(5, first_step=5, timestep=1e-4, seed=4)
+        res.append((s.get_positions(), s.compute_forces()))
+    assert np.abs(res[0][0] - res[1][0]).max() <= 2e-5
+    assert_forces_close(res[0][1], res[1][1])
+
+
+def test_c2_window_properties(c2_design, interphase_cfg):
+    """Full C2 size: a production window stays finite, the schedule advances and the step is deterministic."""
+    cfg = interphase_cfg
+    e1, _ = interphase.build_interphase(Engine, c2_design, cfg)
+    e2, _ = interphase.build_interphase(Engine, c2_design, cfg)
+    for s in (e1, e2):
+        s.set_schedule(**interphase.interphase_schedule(cfg))
+        s.apply_schedule(0)
+        s.run(64, seed=17)
+    x1, x2 = e1.get_positions(), e2.get_positions()
+    assert np.isfinite(x1).all()
+    assert np.array_equal(x1, x2)
+    c = e1.get_context()
+    assert c["step"] == 64 and c["time"] == pytest.approx(64 * cfg.timestep)
+    disp = np.linalg.norm(x1 - c2_design.positions, axis=1)
+    assert disp.mean() < 0.2
