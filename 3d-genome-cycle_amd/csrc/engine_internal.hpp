@@ -16,6 +16,8 @@
 namespace gcs {
 
 constexpr int kTile = 64;          // particles per tile of the pair loop = one wave's lanes
+constexpr int kMaxRows = 64;       // stencil rows per batch of the pair loop's row table
+constexpr int kPairFx = 2;         // x subdivision of the pair cell grid
 constexpr int kMaxPointSources = 4;
 constexpr int kForcePartials = 8;  // per force block: reaction in[3], out[3], max mu|F|, neighbours
 constexpr int kBBoxPartials = 6;   // per block: bbox lo[3], hi[3]
@@ -26,6 +28,7 @@ struct Grid {
     float inv[3];
     int n[3];
     int ncell;
+    int fx;     // x cell edge = rc / fx (the pair stencil spans +-fx cells in x, +-1 in y and z)
     float rc;   // pair cutoff of this step
     float rc2;
 };

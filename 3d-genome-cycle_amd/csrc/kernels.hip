@@ -64,7 +64,7 @@ __device__ inline int cell_index(const Grid& g, float x, float y, float z)
 // Cell grid over the current bounding box; cell edge >= rc (1e-4 margin) so any pair closer than rc lies
 // in the same or an adjacent cell (particles outside the box are clamped into the border cells, which
 // keeps that property because clamping never increases a per-axis cell distance).
-__device__ void compute_grid(DevCtx* ctx, float rc, int ncell_max)
+__device__ void compute_grid(DevCtx* ctx, float rc, int ncell_max, int fx)
 {
     Grid g;
     int n[3];
@@ -74,7 +74,8 @@ __device__ void compute_grid(DevCtx* ctx, float rc, int ncell_max)
         float e = ctx->bbox_hi[k] - ctx->bbox_lo[k];
         if (!(e > 0.f) || !(e < 3.0e38f)) e = 0.f;
         ext[k] = e;
-        float q = (rc > 0.f) ? e / (rc * 1.0001f) : 0.f;
+        const float edge = (k == 0) ? rc / (float)fx : rc;  // x cells are rc / fx wide
+        float q = (rc > 0.f) ? e / (edge * 1.0001f) : 0.f;
         int m = (q >= 1.f) ? (int)fminf(q, 1024.f) : 1;
         n[k] = m;
         total *= m;
@@ -93,6 +94,7 @@ __device__ void compute_grid(DevCtx* ctx, float rc, int ncell_max)
         g.inv[k] = ext[k] > 0.f ? (float)n[k] / ext[k] : 0.f;
     }
     g.ncell = (int)total;
+    g.fx = (n[0] > 1) ? fx : 1;
     g.rc = rc;
     g.rc2 = rc * rc;
     ctx->grid = g;
@@ -142,7 +144,7 @@ __global__ __launch_bounds__(1024) void k_prime(DevCtx* ctx, ForceArgs a, float 
             ctx->bbox_hi[k] = h;
         }
         float rc = rc_fixed > 0.f ? rc_fixed : pair_cutoff(a, ctx->cs);
-        compute_grid(ctx, rc, ncell_max);
+        compute_grid(ctx, rc, ncell_max, rc_fixed > 0.f ? 1 : kPairFx);
     }
 }
 
@@ -297,6 +299,11 @@ template <int MODE, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__ ctx, ForceArgs a)
 {
     __shared__ float red[WAVES > 1 ? WAVES : 1][4][64];
+    __shared__ int s_rowV[kMaxRows + 1];
+    __shared__ int s_rowJ[kMaxRows];
+    __shared__ float4 s_cand[WAVES][kTile];
+    __shared__ float s_candb[WAVES][kTile];
+    __shared__ int s_candj[MODE == kModeEnergy ? WAVES : 1][kTile];
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     const int n = a.n;
@@ -321,50 +328,89 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
         const float ea = 0.25f * a.pa_eps;  // energy: 1/2 (mean) x 1/2 (each pair seen from both ends)
         const float eb = 0.25f * a.pb_eps;
         const float rc2 = g.rc2;
-        const int nx = g.n[0], ny = g.n[1], nz = g.n[2];
+        const int nx = g.n[0], ny = g.n[1], nz = g.n[2], gfx = g.fx;
+        // The tile covers the contiguous cell-id interval [c0, c1] (x fastest).  Its stencil rows are all
+        // rows (y', z') next to a covered row; each gets the union of the covered x-ranges padded by fx
+        // cells (the x edge is rc / fx), so every particle within rc of a tile particle is a candidate.
         const int slast = min(n, s0 + kTile) - 1;
         const int c0 = uniform(a.scell[s0]), c1 = uniform(a.scell[slast]);
-        const int x0 = c0 % nx, y0 = (c0 / nx) % ny, z0 = c0 / (nx * ny);
-        const int x1 = c1 % nx, y1 = (c1 / nx) % ny, z1 = c1 / (nx * ny);
-        int xlo, xhi, ylo, yhi, zlo, zhi;
-        if (z0 == z1 && y0 == y1) {  // the tile lies in one row of cells: 3x3 rows, x-range padded by 1
-            xlo = x0 - 1; xhi = x1 + 1; ylo = y0 - 1; yhi = y0 + 1; zlo = z0 - 1; zhi = z0 + 1;
-        } else if (z0 == z1) {
-            xlo = 0; xhi = nx - 1; ylo = y0 - 1; yhi = y1 + 1; zlo = z0 - 1; zhi = z0 + 1;
-        } else {
-            xlo = 0; xhi = nx - 1; ylo = 0; yhi = ny - 1; zlo = z0 - 1; zhi = z1 + 1;
+        const int x0 = c0 % nx, r0 = c0 / nx, x1 = c1 % nx, r1 = c1 / nx;
+        const int y0 = r0 % ny, z0 = r0 / ny, y1 = r1 % ny, z1 = r1 / ny;
+        int ylo = 0, yhi = ny - 1;
+        if (z0 == z1) {
+            ylo = max(y0 - 1, 0);
+            yhi = min(y1 + 1, ny - 1);
         }
-        xlo = max(xlo, 0); xhi = min(xhi, nx - 1);
-        ylo = max(ylo, 0); yhi = min(yhi, ny - 1);
-        zlo = max(zlo, 0); zhi = min(zhi, nz - 1);
-
-        // total candidates over the stencil rows; wave w takes the w-th contiguous share
-        int total = 0;
-        for (int z = zlo; z <= zhi; ++z)
-            for (int y = ylo; y <= yhi; ++y) {
-                const int base = (z * ny + y) * nx;
-                total += a.cstart[base + xhi + 1] - a.cstart[base + xlo];
-            }
-        total = uniform(total);
-        const int wlo = (int)(((long long)total * wave) / WAVES);
-        const int whi = (int)(((long long)total * (wave + 1)) / WAVES);
+        const int zlo = max(z0 - 1, 0), zhi = min(z1 + 1, nz - 1);
+        const int nyb = yhi - ylo + 1;
+        const int nbox = nyb * (zhi - zlo + 1);
         const float ahi = pi.w, bhi = bi;
-        int v = 0;
-        for (int z = zlo; z <= zhi && v < whi; ++z)
-            for (int y = ylo; y <= yhi && v < whi; ++y) {
-                const int base = (z * ny + y) * nx;
-                const int jb = uniform(a.cstart[base + xlo]);
-                const int je = uniform(a.cstart[base + xhi + 1]);
-                const int len = je - jb;
-                const int lo = max(v, wlo), hi = min(v + len, whi);
-                const int off = jb - v;
-                for (int k = lo; k < hi; ++k) {
-                    const int j = k + off;
-                    const float4 pj = a.spos[j];
-                    const float bj = a.sb[j];
+        for (int rb = 0; rb < nbox; rb += kMaxRows) {
+            if (wave == 0) {  // row table of this batch: lane q builds stencil row rb + q
+                const int q = rb + lane;
+                int len = 0, jb = 0;
+                if (q < nbox) {
+                    const int yq = ylo + q % nyb, zq = zlo + q / nyb;
+                    int ulo = nx, uhi = -1;
+                    for (int dz = -1; dz <= 1; ++dz)
+                        for (int dy = -1; dy <= 1; ++dy) {
+                            const int y = yq + dy, z = zq + dz;
+                            if (y < 0 || y >= ny || z < 0 || z >= nz) continue;
+                            const int rr = z * ny + y;
+                            if (rr < r0 || rr > r1) continue;
+                            ulo = min(ulo, (rr == r0 ? x0 : 0) - gfx);
+                            uhi = max(uhi, (rr == r1 ? x1 : nx - 1) + gfx);
+                        }
+                    ulo = max(ulo, 0);
+                    uhi = min(uhi, nx - 1);
+                    if (ulo <= uhi) {
+                        const int base = (zq * ny + yq) * nx;
+                        jb = a.cstart[base + ulo];
+                        len = a.cstart[base + uhi + 1] - jb;
+                    }
+                }
+                const int incl = wave_incl_scan(len, lane);
+                s_rowV[lane] = incl - len;
+                s_rowJ[lane] = jb;
+                if (lane == kMaxRows - 1) s_rowV[kMaxRows] = incl;
+            }
+            __syncthreads();
+            const int total = uniform(s_rowV[kMaxRows]);
+            const int wlo = (int)(((long long)total * wave) / WAVES);
+            const int whi = (int)(((long long)total * (wave + 1)) / WAVES);
+            for (int base = wlo; base < whi; base += kTile) {
+                const int cnt = uniform(min(kTile, whi - base));
+                const int cnt8 = (cnt + 7) & ~7;  // padded with far-away sentinels -> unrolled by 8
+                if (lane >= cnt && lane < cnt8) {
+                    s_cand[wave][lane] = make_float4(1e18f, 1e18f, 1e18f, 0.f);
+                    s_candb[wave][lane] = 0.f;
+                    if (MODE == kModeEnergy) s_candj[MODE == kModeEnergy ? wave : 0][lane] = -1;
+                }
+                if (lane < cnt) {  // stage candidate base + lane: binary search of its stencil row
+                    const int v = base + lane;
+                    int lo = 0, hi = kMaxRows - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (s_rowV[mid] <= v)
+                            lo = mid;
+                        else
+                            hi = mid - 1;
+                    }
+                    const int j = s_rowJ[lo] + (v - s_rowV[lo]);
+                    s_cand[wave][lane] = a.spos[j];
+                    s_candb[wave][lane] = a.sb[j];
+                    if (MODE == kModeEnergy) s_candj[MODE == kModeEnergy ? wave : 0][lane] = j;
+                }
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll 8
+                for (int k = 0; k < cnt8; ++k) {
+                    const float4 pj = s_cand[wave][k];
+                    const float bj = s_candb[wave][k];
                     const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
                     const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                    const bool in = (r2 < rc2) && (j != s);
+                    // the self pair contributes exactly zero force (F is proportional to x_i - x_j)
+                    const bool in = (MODE == kModeEnergy) ? ((r2 < rc2) && (s_candj[MODE == kModeEnergy ? wave : 0][k] != s))
+                                                          : (r2 < rc2);
                     const float A = ahi + pj.w, B = bhi + bj;
                     const float ua = r2 * k2a;
                     const float ga = 1.f - ua;
@@ -384,11 +430,13 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
                         fx = fmaf(coef, dx, fx);
                         fy = fmaf(coef, dy, fy);
                         fz = fmaf(coef, dz, fz);
-                        acc += in ? 1.f : 0.f;
+                        acc += (in && r2 > 0.f) ? 1.f : 0.f;
                     }
                 }
-                v += len;
+                __builtin_amdgcn_wave_barrier();
             }
+            __syncthreads();
+        }
     }
 
     if (WAVES > 1) {
@@ -758,7 +806,7 @@ __global__ __launch_bounds__(256) void k_tail(DevCtx* ctx, ForceArgs a, int fblo
                 ctx->wall[k] += dt * sched[kSchedMuW] * net;
             }
     }
-    compute_grid(ctx, pair_cutoff(a, ctx->cs), ncell_max);
+    compute_grid(ctx, pair_cutoff(a, ctx->cs), ncell_max, kPairFx);
 }
 
 // ----------------------------------------------------------------------------------------------------
@@ -791,7 +839,7 @@ __global__ __launch_bounds__(256) void k_search(const DevCtx* __restrict__ ctx, 
     for (int z = max(cz - 1, 0); z <= min(cz + 1, nz - 1); ++z)
         for (int y = max(cy - 1, 0); y <= min(cy + 1, ny - 1); ++y) {
             const int base = (z * ny + y) * nx;
-            const int jb = cstart[base + max(cx - 1, 0)], je = cstart[base + min(cx + 1, nx - 1) + 1];
+            const int jb = cstart[base + max(cx - g.fx, 0)], je = cstart[base + min(cx + g.fx, nx - 1) + 1];
             for (int t = jb; t < je; ++t) {
                 const int j = sidx[t];
                 if (j <= i) continue;

@@ -45,7 +45,7 @@ def test_forces_c1(c1_design, interphase_cfg):
 
 def test_forces_c1_full_scale(c1_design, interphase_cfg):
     e, o = both(c1_design, interphase_cfg)
-    ctx = {"core_scale": 1.0, "bond_scale": 1.0, "wall_semiaxes": [1.55, 1.6, 1.5]}
+    ctx = {"core_scale": 1.0, "bond_scale": 1.0, "wall_semiaxes": [1.25, 1.3, 1.2]}
     e.set_context(ctx)
     o.set_context(ctx)
     assert_forces_close(e.compute_forces(), o.compute_forces())
