@@ -50,6 +50,15 @@ __device__ inline float wave_min(float v)
 
 __device__ inline int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+__device__ inline int wave_max_int(int v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
+constexpr int kHitStride = 68;  // bytes per lane of the hit lists (pads the LDS banks)
+
 __device__ inline int cell_index(const Grid& g, float x, float y, float z)
 {
     int cx = (int)((x - g.lo[0]) * g.inv[0]);
@@ -304,6 +313,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
     __shared__ float4 s_cand[WAVES][kTile];
     __shared__ float s_candb[WAVES][kTile];
     __shared__ int s_candj[MODE == kModeEnergy ? WAVES : 1][kTile];
+    __shared__ unsigned char s_hit[WAVES][kTile * kHitStride];
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     const int n = a.n;
@@ -402,37 +412,53 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
                     if (MODE == kModeEnergy) s_candj[MODE == kModeEnergy ? wave : 0][lane] = j;
                 }
                 __builtin_amdgcn_wave_barrier();
+                // phase 1: distance filter over the chunk; each lane records the indices of its hits
+                unsigned char* hits = &s_hit[wave][lane * kHitStride];
+                int nh = 0;
 #pragma unroll 8
                 for (int k = 0; k < cnt8; ++k) {
+                    const float4 pj = s_cand[wave][k];
+                    const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+                    const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                    // the self pair contributes exactly zero force (F is proportional to x_i - x_j), so the
+                    // force path keeps it (one wasted slot) instead of paying a second compare per candidate
+                    const bool in = (MODE == kModeEnergy)
+                                        ? ((r2 < rc2) && (s_candj[MODE == kModeEnergy ? wave : 0][k] != s))
+                                        : (r2 < rc2);
+                    hits[nh] = (unsigned char)k;  // unconditional store; the slot advances on a hit only
+                    nh += in ? 1 : 0;
+                }
+                // phase 2: the potential on the hits only (iterations = the wave's largest hit count)
+                const int mh = uniform(wave_max_int(nh));
+                for (int t = 0; t < mh; ++t) {
+                    const bool act = t < nh;
+                    const int k = hits[t];
                     const float4 pj = s_cand[wave][k];
                     const float bj = s_candb[wave][k];
                     const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
                     const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                    // the self pair contributes exactly zero force (F is proportional to x_i - x_j)
-                    const bool in = (MODE == kModeEnergy) ? ((r2 < rc2) && (s_candj[MODE == kModeEnergy ? wave : 0][k] != s))
-                                                          : (r2 < rc2);
                     const float A = ahi + pj.w, B = bhi + bj;
                     const float ua = r2 * k2a;
                     const float ga = 1.f - ua;
-                    const float t = r2 * k2b;
-                    const float t2 = t * t;
+                    const float tt = r2 * k2b;
+                    const float t2 = tt * tt;
                     const float gb = 1.f - t2 * t2;
                     const float gb2 = gb * gb;
-                    const bool ina = in && (ua < 1.f);
-                    const bool inb = in && (t < 1.f);
+                    const bool ina = act && (ua < 1.f);
+                    const bool inb = act && (tt < 1.f);
                     if (MODE == kModeEnergy) {
                         const float ua3 = ga * ga * ga, ub3 = gb2 * gb;
                         acc += (ina ? A * ea * ua3 : 0.f) + (inb ? B * eb * ub3 : 0.f);
                     } else {
                         const float fa = ina ? ga * ga : 0.f;
-                        const float fb = inb ? gb2 * t2 * t : 0.f;
+                        const float fb = inb ? gb2 * t2 * tt : 0.f;
                         const float coef = fmaf(A * ca, fa, B * cb * fb);
                         fx = fmaf(coef, dx, fx);
                         fy = fmaf(coef, dy, fy);
                         fz = fmaf(coef, dz, fz);
-                        acc += (in && r2 > 0.f) ? 1.f : 0.f;
                     }
                 }
+                if (MODE != kModeEnergy) acc += (float)nh;
                 __builtin_amdgcn_wave_barrier();
             }
             __syncthreads();
@@ -644,7 +670,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
         vals[4] = valid ? rout[1] : 0.f;
         vals[5] = valid ? rout[2] : 0.f;
         const float drift = valid ? km.x * sqrtf(fx * fx + fy * fy + fz * fz) : 0.f;
-        vals[7] = valid ? acc : 0.f;
+        vals[7] = valid ? acc - (a.has_pair ? 1.f : 0.f) : 0.f;  // the pair loop counted the particle itself
         float outv[kForcePartials];
         for (int k = 0; k < kForcePartials; ++k) outv[k] = (k == 6) ? wave_max(drift) : wave_sum(vals[k]);
         if (lane == 0)
