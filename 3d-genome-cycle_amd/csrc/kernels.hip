@@ -432,7 +432,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
                 const int mh = uniform(wave_max_int(nh));
                 for (int t = 0; t < mh; ++t) {
                     const bool act = t < nh;
-                    const int k = hits[t];
+                    const int k = act ? (int)hits[t] : 0;  // inactive lanes read a valid staged slot (no NaN)
                     const float4 pj = s_cand[wave][k];
                     const float bj = s_candb[wave][k];
                     const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
