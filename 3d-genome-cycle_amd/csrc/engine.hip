@@ -503,13 +503,13 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
     if ((rc = dalloc(&e->pos[0], n)) || (rc = dalloc(&e->pos[1], n)) || (rc = dalloc(&e->kmu, n)) ||
         (rc = dalloc(&e->spos, n)) || (rc = dalloc(&e->sb, n)) || (rc = dalloc(&e->sidx, n)) ||
         (rc = dalloc(&e->scell, n)) || (rc = dalloc(&e->cell_of, n)) || (rc = dalloc(&e->slot, n)) ||
-        (rc = dalloc(&e->tmp, n)) || (rc = dalloc(&e->count, e->ncell_max + 2)) ||
-        (rc = dalloc(&e->cstart, e->ncell_max + 2)) || (rc = dalloc(&e->ctx, 1)) || (rc = dalloc(&e->dsched, kSchedCount)) ||
+        (rc = dalloc(&e->tmp, n)) || (rc = dalloc(&e->count, e->ncell_max + kScanPad)) ||
+        (rc = dalloc(&e->cstart, e->ncell_max + kScanPad)) || (rc = dalloc(&e->ctx, 1)) || (rc = dalloc(&e->dsched, kSchedCount)) ||
         (rc = dalloc(&e->part_force, (size_t)std::max(fb, ub) * kForcePartials)) ||
         (rc = dalloc(&e->part_bbox, (size_t)std::max(fb, ub) * kBBoxPartials)) ||
         (rc = dalloc(&e->part_energy, (size_t)fb * kEnergyKinds)) || (rc = dalloc(&e->force_out, n)))
         return bail(rc);
-    he = hipMemsetAsync(e->count, 0, (e->ncell_max + 2) * sizeof(int), e->stream);
+    he = hipMemsetAsync(e->count, 0, (e->ncell_max + kScanPad) * sizeof(int), e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->pos[0], 0, n * sizeof(float4), e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->pos[1], 0, n * sizeof(float4), e->stream);
     DevCtx c{};
@@ -961,11 +961,11 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
         const int ncm = std::min(1 << 21, std::max(4096, 4 * cap));
         if ((rc = dalloc(&e->s_pts, cap)) || (rc = dalloc(&e->s_spos, cap)) || (rc = dalloc(&e->s_sb, cap)) ||
             (rc = dalloc(&e->s_sidx, cap)) || (rc = dalloc(&e->s_scell, cap)) || (rc = dalloc(&e->s_cell_of, cap)) ||
-            (rc = dalloc(&e->s_slot, cap)) || (rc = dalloc(&e->s_tmp, cap)) || (rc = dalloc(&e->s_count, ncm + 2)) ||
-            (rc = dalloc(&e->s_cstart, ncm + 2)) || (rc = dalloc(&e->s_counts, cap)) ||
+            (rc = dalloc(&e->s_slot, cap)) || (rc = dalloc(&e->s_tmp, cap)) || (rc = dalloc(&e->s_count, ncm + kScanPad)) ||
+            (rc = dalloc(&e->s_cstart, ncm + kScanPad)) || (rc = dalloc(&e->s_counts, cap)) ||
             (rc = dalloc(&e->s_offsets, cap)) || (rc = dalloc(&e->s_total, 1)) || (rc = dalloc(&e->s_ctx, 1)))
             return rc;
-        HIPCHK(hipMemsetAsync(e->s_count, 0, (ncm + 2) * sizeof(int), e->stream));
+        HIPCHK(hipMemsetAsync(e->s_count, 0, (ncm + kScanPad) * sizeof(int), e->stream));
         e->search_cap = cap;
         e->s_ncell_max = ncm;
     }

@@ -18,6 +18,7 @@ namespace gcs {
 constexpr int kTile = 64;          // particles per tile of the pair loop = one wave's lanes
 constexpr int kMaxRows = 64;       // stencil rows per batch of the pair loop's row table
 constexpr int kPairFx = 2;         // x subdivision of the pair cell grid
+constexpr int kScanPad = 4096 + 8; // count/cstart padding: k_cell_scan works in whole 4096-cell tiles
 constexpr int kMaxPointSources = 4;
 constexpr int kForcePartials = 8;  // per force block: reaction in[3], out[3], max mu|F|, neighbours
 constexpr int kBBoxPartials = 6;   // per block: bbox lo[3], hi[3]

@@ -182,31 +182,36 @@ __device__ inline int wave_incl_scan(int v, int lane)
     return v;
 }
 
+// Exclusive scan count -> cstart over the grid's cells in coalesced 4096-cell tiles (int4 per thread) with a
+// running carry; re-zeroes count for the next step.  count/cstart are padded by kScanPad so whole tiles may be
+// touched; entries past ncell are zero by invariant.
 __global__ __launch_bounds__(1024) void k_cell_scan(const DevCtx* __restrict__ ctx, int n, int* __restrict__ count,
                                                     int* __restrict__ cstart)
 {
     __shared__ int wtot[16];
+    __shared__ int tile_total;
     const int nc = ctx->grid.ncell;
-    const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int per = (nc + T - 1) / T;
-    const int b = min(nc, tid * per), e = min(nc, b + per);
-    int sum = 0;
-    for (int k = b; k < e; ++k) sum += count[k];
-    int incl = wave_incl_scan(sum, lane);
-    if (lane == 63) wtot[wave] = incl;
-    __syncthreads();
-    if (wave == 0) {
-        int v = (lane < T / 64) ? wtot[lane] : 0;
-        int vi = wave_incl_scan(v, lane);
-        if (lane < T / 64) wtot[lane] = vi - v;
-    }
-    __syncthreads();
-    int run = wtot[wave] + incl - sum;
-    for (int k = b; k < e; ++k) {
-        int c = count[k];
-        cstart[k] = run;
-        run += c;
-        count[k] = 0;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int carry = 0;
+    for (int base = 0; base < nc; base += 4096) {
+        const int i0 = base + 4 * tid;
+        const int4 c = *reinterpret_cast<const int4*>(count + i0);
+        const int sum = c.x + c.y + c.z + c.w;
+        const int incl = wave_incl_scan(sum, lane);
+        if (lane == 63) wtot[wave] = incl;
+        __syncthreads();
+        if (wave == 0) {
+            const int w = lane < 16 ? wtot[lane] : 0;
+            const int wi = wave_incl_scan(w, lane);
+            if (lane < 16) wtot[lane] = wi - w;
+            if (lane == 15) tile_total = wi;
+        }
+        __syncthreads();
+        const int run = carry + wtot[wave] + incl - sum;
+        *reinterpret_cast<int4*>(cstart + i0) = make_int4(run, run + c.x, run + c.x + c.y, run + c.x + c.y + c.z);
+        *reinterpret_cast<int4*>(count + i0) = make_int4(0, 0, 0, 0);
+        carry += tile_total;
+        __syncthreads();
     }
     if (tid == 0) cstart[nc] = n;
 }
@@ -388,17 +393,15 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
             const int total = uniform(s_rowV[kMaxRows]);
             const int wlo = (int)(((long long)total * wave) / WAVES);
             const int whi = (int)(((long long)total * (wave + 1)) / WAVES);
-            for (int base = wlo; base < whi; base += kTile) {
-                const int cnt = uniform(min(kTile, whi - base));
-                const int cnt8 = (cnt + 7) & ~7;  // padded with far-away sentinels -> unrolled by 8
-                if (lane >= cnt && lane < cnt8) {
-                    s_cand[wave][lane] = make_float4(1e18f, 1e18f, 1e18f, 0.f);
-                    s_candb[wave][lane] = 0.f;
-                    if (MODE == kModeEnergy) s_candj[MODE == kModeEnergy ? wave : 0][lane] = -1;
-                }
-                if (lane < cnt) {  // stage candidate base + lane: binary search of its stencil row
-                    const int v = base + lane;
-                    int lo = 0, hi = kMaxRows - 1;
+            // software pipeline: chunk c+1's candidates (row lookup + global loads) are in flight while
+            // chunk c is filtered and evaluated from LDS
+            auto fetch = [&](int base, float4& p, float& b, int& jj) {
+                const int v = base + lane;
+                p = make_float4(1e18f, 1e18f, 1e18f, 0.f);  // far-away sentinel: never a hit
+                b = 0.f;
+                jj = -1;
+                if (v < whi) {
+                    int lo = 0, hi = kMaxRows - 1;  // last stencil row starting at or before v
                     while (lo < hi) {
                         const int mid = (lo + hi + 1) >> 1;
                         if (s_rowV[mid] <= v)
@@ -406,12 +409,23 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
                         else
                             hi = mid - 1;
                     }
-                    const int j = s_rowJ[lo] + (v - s_rowV[lo]);
-                    s_cand[wave][lane] = a.spos[j];
-                    s_candb[wave][lane] = a.sb[j];
-                    if (MODE == kModeEnergy) s_candj[MODE == kModeEnergy ? wave : 0][lane] = j;
+                    jj = s_rowJ[lo] + (v - s_rowV[lo]);
+                    p = a.spos[jj];
+                    b = a.sb[jj];
                 }
+            };
+            float4 npj;
+            float nbj;
+            int njj;
+            fetch(wlo, npj, nbj, njj);
+            for (int base = wlo; base < whi; base += kTile) {
+                const int cnt = uniform(min(kTile, whi - base));
+                const int cnt8 = (cnt + 7) & ~7;  // sentinel-padded to a multiple of 8 -> unrolled by 8
+                s_cand[wave][lane] = npj;
+                s_candb[wave][lane] = nbj;
+                if (MODE == kModeEnergy) s_candj[MODE == kModeEnergy ? wave : 0][lane] = njj;
                 __builtin_amdgcn_wave_barrier();
+                if (base + kTile < whi) fetch(base + kTile, npj, nbj, njj);
                 // phase 1: distance filter over the chunk; each lane records the indices of its hits
                 unsigned char* hits = &s_hit[wave][lane * kHitStride];
                 int nh = 0;

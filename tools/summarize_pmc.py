@@ -8,7 +8,7 @@ from collections import defaultdict
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "").replace("gcs::(anonymous namespace)::", "")
+    return name.replace("void ", "").replace("gcs::(anonymous namespace)::", "").split("(")[0]
 
 
 def main(d):
