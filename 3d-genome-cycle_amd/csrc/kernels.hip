@@ -442,34 +442,39 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
                     hits[nh] = (unsigned char)k;  // unconditional store; the slot advances on a hit only
                     nh += in ? 1 : 0;
                 }
-                // phase 2: the potential on the hits only (iterations = the wave's largest hit count)
+                // phase 2: the potential on the hits only (iterations = the wave's largest hit count), four
+                // independent hits per iteration so their LDS gathers overlap (one dword = 4 hit indices)
                 const int mh = uniform(wave_max_int(nh));
-                for (int t = 0; t < mh; ++t) {
-                    const bool act = t < nh;
-                    const int k = act ? (int)hits[t] : 0;  // inactive lanes read a valid staged slot (no NaN)
-                    const float4 pj = s_cand[wave][k];
-                    const float bj = s_candb[wave][k];
-                    const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
-                    const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                    const float A = ahi + pj.w, B = bhi + bj;
-                    const float ua = r2 * k2a;
-                    const float ga = 1.f - ua;
-                    const float tt = r2 * k2b;
-                    const float t2 = tt * tt;
-                    const float gb = 1.f - t2 * t2;
-                    const float gb2 = gb * gb;
-                    const bool ina = act && (ua < 1.f);
-                    const bool inb = act && (tt < 1.f);
-                    if (MODE == kModeEnergy) {
-                        const float ua3 = ga * ga * ga, ub3 = gb2 * gb;
-                        acc += (ina ? A * ea * ua3 : 0.f) + (inb ? B * eb * ub3 : 0.f);
-                    } else {
-                        const float fa = ina ? ga * ga : 0.f;
-                        const float fb = inb ? gb2 * t2 * tt : 0.f;
-                        const float coef = fmaf(A * ca, fa, B * cb * fb);
-                        fx = fmaf(coef, dx, fx);
-                        fy = fmaf(coef, dy, fy);
-                        fz = fmaf(coef, dz, fz);
+                for (int t = 0; t < mh; t += 4) {
+                    const unsigned kk = *reinterpret_cast<const unsigned*>(hits + t);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const bool act = t + u < nh;
+                        const int k = act ? (int)((kk >> (8 * u)) & 0xffu) : 0;  // inactive: a valid slot, no NaN
+                        const float4 pj = s_cand[wave][k];
+                        const float bj = s_candb[wave][k];
+                        const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+                        const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                        const float A = ahi + pj.w, B = bhi + bj;
+                        const float ua = r2 * k2a;
+                        const float ga = 1.f - ua;
+                        const float tt = r2 * k2b;
+                        const float t2 = tt * tt;
+                        const float gb = 1.f - t2 * t2;
+                        const float gb2 = gb * gb;
+                        const bool ina = act && (ua < 1.f);
+                        const bool inb = act && (tt < 1.f);
+                        if (MODE == kModeEnergy) {
+                            const float ua3 = ga * ga * ga, ub3 = gb2 * gb;
+                            acc += (ina ? A * ea * ua3 : 0.f) + (inb ? B * eb * ub3 : 0.f);
+                        } else {
+                            const float fa = ina ? ga * ga : 0.f;
+                            const float fb = inb ? gb2 * t2 * tt : 0.f;
+                            const float coef = fmaf(A * ca, fa, B * cb * fb);
+                            fx = fmaf(coef, dx, fx);
+                            fy = fmaf(coef, dy, fy);
+                            fz = fmaf(coef, dz, fz);
+                        }
                     }
                 }
                 if (MODE != kModeEnergy) acc += (float)nh;
