@@ -57,7 +57,6 @@ __device__ inline int wave_max_int(int v)
     return v;
 }
 
-constexpr int kHitStride = 68;  // bytes per lane of the hit lists (pads the LDS banks)
 
 __device__ inline int cell_index(const Grid& g, float x, float y, float z)
 {
@@ -318,7 +317,6 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
     __shared__ float4 s_cand[WAVES][kTile];
     __shared__ float s_candb[WAVES][kTile];
     __shared__ int s_candj[MODE == kModeEnergy ? WAVES : 1][kTile];
-    __shared__ unsigned char s_hit[WAVES][kTile * kHitStride];
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     const int n = a.n;
@@ -426,31 +424,48 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
                 if (MODE == kModeEnergy) s_candj[MODE == kModeEnergy ? wave : 0][lane] = njj;
                 __builtin_amdgcn_wave_barrier();
                 if (base + kTile < whi) fetch(base + kTile, npj, nbj, njj);
-                // phase 1: distance filter over the chunk; each lane records the indices of its hits
-                unsigned char* hits = &s_hit[wave][lane * kHitStride];
-                int nh = 0;
-#pragma unroll 8
-                for (int k = 0; k < cnt8; ++k) {
-                    const float4 pj = s_cand[wave][k];
-                    const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
-                    const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                    // the self pair contributes exactly zero force (F is proportional to x_i - x_j), so the
-                    // force path keeps it (one wasted slot) instead of paying a second compare per candidate
-                    const bool in = (MODE == kModeEnergy)
-                                        ? ((r2 < rc2) && (s_candj[MODE == kModeEnergy ? wave : 0][k] != s))
-                                        : (r2 < rc2);
-                    hits[nh] = (unsigned char)k;  // unconditional store; the slot advances on a hit only
-                    nh += in ? 1 : 0;
+                // phase 1: distance filter over the chunk; each lane keeps a 64-bit mask of its hits
+                unsigned mlo = 0u, mhi = 0u;
+                for (int k0 = 0; k0 < cnt8; k0 += 8) {
+                    unsigned byte = 0u;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const float4 pj = s_cand[wave][k0 + u];
+                        const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+                        const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                        // the self pair contributes exactly zero force (F is proportional to x_i - x_j), so
+                        // the force path keeps it (one wasted slot) instead of a second compare per candidate
+                        const bool in = (MODE == kModeEnergy)
+                                            ? ((r2 < rc2) && (s_candj[MODE == kModeEnergy ? wave : 0][k0 + u] != s))
+                                            : (r2 < rc2);
+                        byte |= in ? (1u << u) : 0u;
+                    }
+                    if (k0 < 32)
+                        mlo |= byte << k0;
+                    else
+                        mhi |= byte << (k0 - 32);
                 }
+                const int nh = __popc(mlo) + __popc(mhi);
                 // phase 2: the potential on the hits only (iterations = the wave's largest hit count), four
-                // independent hits per iteration so their LDS gathers overlap (one dword = 4 hit indices)
+                // independent hits per iteration so their LDS gathers overlap
                 const int mh = uniform(wave_max_int(nh));
                 for (int t = 0; t < mh; t += 4) {
-                    const unsigned kk = *reinterpret_cast<const unsigned*>(hits + t);
+                    int kk[4];
+                    bool av[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {  // pop the lowest set bits
+                        av[u] = (mlo | mhi) != 0u;
+                        const int klo = __ffs(mlo) - 1, khi = __ffs(mhi) + 31;
+                        kk[u] = av[u] ? (mlo ? klo : khi) : 0;  // inactive: a valid slot, no NaN
+                        if (mlo)
+                            mlo &= mlo - 1u;
+                        else
+                            mhi &= mhi - 1u;
+                    }
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
-                        const bool act = t + u < nh;
-                        const int k = act ? (int)((kk >> (8 * u)) & 0xffu) : 0;  // inactive: a valid slot, no NaN
+                        const bool act = av[u];
+                        const int k = kk[u];
                         const float4 pj = s_cand[wave][k];
                         const float bj = s_candb[wave][k];
                         const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;

@@ -119,6 +119,7 @@ def main():
     ap.add_argument("--waves", type=int, default=4)
     ap.add_argument("--profile-steps", type=int, default=50)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline work (0 = skip)")
+    ap.add_argument("--no-start-window", action="store_true", help="skip the secondary step-0 window")
     args = ap.parse_args()
 
     world, rank, local, dist = dist_setup()
@@ -155,7 +156,7 @@ def main():
 
     # secondary: the production start window (step 0, core_scale 0.5, ~7x fewer neighbours)
     start_rate = None
-    if rank == 0:
+    if rank == 0 and not args.no_start_window:
         e0 = make_engine(design, cfg, local, 0)
         e0.set_option(A.OPT_GRAPH_STEPS, args.graph_steps)
         e0.run(64, first_step=0, seed=seed)
