@@ -87,7 +87,7 @@ struct gcs_engine {
     float4* spos = nullptr;
     float* sb = nullptr;
     int *sidx = nullptr, *scell = nullptr, *cell_of = nullptr, *slot = nullptr, *tmp = nullptr;
-    int *count = nullptr, *cstart = nullptr;
+    int *count = nullptr, *cstart = nullptr, *tile_start = nullptr;
     DevCtx* ctx = nullptr;
     double* dsched = nullptr;
     float* part_force = nullptr;
@@ -111,6 +111,7 @@ struct gcs_engine {
     float* s_sb = nullptr;
     int *s_sidx = nullptr, *s_scell = nullptr, *s_cell_of = nullptr, *s_slot = nullptr, *s_tmp = nullptr;
     int *s_count = nullptr, *s_cstart = nullptr, *s_counts = nullptr, *s_offsets = nullptr, *s_total = nullptr;
+    int* s_tile = nullptr;
     int s_ncell_max = 0;
     DevCtx* s_ctx = nullptr;
     unsigned long long *s_keys = nullptr, *s_keys2 = nullptr;
@@ -366,6 +367,7 @@ void fill_state_args(gcs_engine* e)
     a.sidx = e->sidx;
     a.scell = e->scell;
     a.cstart = e->cstart;
+    a.tile_start = e->tile_start;
     a.part_force = e->part_force;
     a.part_bbox = e->part_bbox;
     a.part_energy = e->part_energy;
@@ -378,7 +380,7 @@ void enqueue_cells(gcs_engine* e)
 {
     const int n = e->n;
     launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count);
-    launch_cell_scan(e->stream, e->ctx, n, e->count, e->cstart);
+    launch_cell_scan(e->stream, e->ctx, n, e->count, e->cstart, e->tile_start);
     launch_cell_scatter(e->stream, n, e->cell_of, e->slot, e->cstart, e->tmp);
     launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, n, e->tmp, e->cell_of, e->cstart, e->sidx,
                      e->scell, e->spos, e->sb, e->fa.has_pair ? e->fa.pair_mix : 1);
@@ -386,7 +388,7 @@ void enqueue_cells(gcs_engine* e)
 
 void enqueue_step(gcs_engine* e, bool spacestep, float spacestep_v, float timestep)
 {
-    const int fb = force_blocks(e->n);
+    const int fb = force_grid(e->n);
     enqueue_cells(e);
     if (!spacestep) {
         launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa);
@@ -499,12 +501,13 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
     if (he != hipSuccess) return bail(fail(GCS_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(he)));
     e->ncell_max = std::min(1 << 21, std::max(4096, 4 * n));
     int rc = 0;
-    const int fb = force_blocks(n), ub = update_blocks(n);
+    const int fb = force_grid(n), ub = update_blocks(n);
     if ((rc = dalloc(&e->pos[0], n)) || (rc = dalloc(&e->pos[1], n)) || (rc = dalloc(&e->kmu, n)) ||
         (rc = dalloc(&e->spos, n)) || (rc = dalloc(&e->sb, n)) || (rc = dalloc(&e->sidx, n)) ||
         (rc = dalloc(&e->scell, n)) || (rc = dalloc(&e->cell_of, n)) || (rc = dalloc(&e->slot, n)) ||
         (rc = dalloc(&e->tmp, n)) || (rc = dalloc(&e->count, e->ncell_max + kScanPad)) ||
-        (rc = dalloc(&e->cstart, e->ncell_max + kScanPad)) || (rc = dalloc(&e->ctx, 1)) || (rc = dalloc(&e->dsched, kSchedCount)) ||
+        (rc = dalloc(&e->cstart, e->ncell_max + kScanPad)) || (rc = dalloc(&e->tile_start, e->ncell_max + 2)) ||
+        (rc = dalloc(&e->ctx, 1)) || (rc = dalloc(&e->dsched, kSchedCount)) ||
         (rc = dalloc(&e->part_force, (size_t)std::max(fb, ub) * kForcePartials)) ||
         (rc = dalloc(&e->part_bbox, (size_t)std::max(fb, ub) * kBBoxPartials)) ||
         (rc = dalloc(&e->part_energy, (size_t)fb * kEnergyKinds)) || (rc = dalloc(&e->force_out, n)))
@@ -541,6 +544,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->tmp);
     dfree(e->count);
     dfree(e->cstart);
+    dfree(e->tile_start);
     dfree(e->ctx);
     dfree(e->dsched);
     dfree(e->part_force);
@@ -564,6 +568,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->s_tmp);
     dfree(e->s_count);
     dfree(e->s_cstart);
+    dfree(e->s_tile);
     dfree(e->s_counts);
     dfree(e->s_offsets);
     dfree(e->s_total);
@@ -893,7 +898,7 @@ int gcs_engine_compute_forces(gcs_engine* e, double* forces, int64_t n)
     launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max);
     enqueue_cells(e);
     launch_force(e->stream, kModeForce, e->waves, e->ctx, e->fa);
-    launch_tail(e->stream, e->ctx, e->fa, force_blocks(e->n), 0, 0, 0, e->ncell_max, e->dsched);
+    launch_tail(e->stream, e->ctx, e->fa, force_grid(e->n), 0, 0, 0, e->ncell_max, e->dsched);
     HIPCHK(hipGetLastError());
     std::vector<float4> h(n);
     HIPCHK(hipMemcpyAsync(h.data(), e->force_out, n * sizeof(float4), hipMemcpyDeviceToHost, e->stream));
@@ -915,7 +920,7 @@ int gcs_engine_compute_energy(gcs_engine* e, double* total, double* per_kind)
     enqueue_cells(e);
     launch_force(e->stream, kModeEnergy, e->waves, e->ctx, e->fa);
     HIPCHK(hipGetLastError());
-    const int fb = force_blocks(e->n);
+    const int fb = force_grid(e->n);
     std::vector<double> h((size_t)fb * kEnergyKinds);
     HIPCHK(hipMemcpyAsync(h.data(), e->part_energy, h.size() * sizeof(double), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
@@ -952,6 +957,7 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
         dfree(e->s_tmp);
         dfree(e->s_count);
         dfree(e->s_cstart);
+        dfree(e->s_tile);
         dfree(e->s_counts);
         dfree(e->s_offsets);
         dfree(e->s_total);
@@ -963,6 +969,7 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
             (rc = dalloc(&e->s_sidx, cap)) || (rc = dalloc(&e->s_scell, cap)) || (rc = dalloc(&e->s_cell_of, cap)) ||
             (rc = dalloc(&e->s_slot, cap)) || (rc = dalloc(&e->s_tmp, cap)) || (rc = dalloc(&e->s_count, ncm + kScanPad)) ||
             (rc = dalloc(&e->s_cstart, ncm + kScanPad)) || (rc = dalloc(&e->s_counts, cap)) ||
+            (rc = dalloc(&e->s_tile, ncm + 2)) ||
             (rc = dalloc(&e->s_offsets, cap)) || (rc = dalloc(&e->s_total, 1)) || (rc = dalloc(&e->s_ctx, 1)))
             return rc;
         HIPCHK(hipMemsetAsync(e->s_count, 0, (ncm + kScanPad) * sizeof(int), e->stream));
@@ -990,7 +997,7 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
     sa.pos1 = const_cast<float4*>(src);
     launch_prime(e->stream, e->s_ctx, sa, (float)distance, e->s_ncell_max);
     launch_cell_count(e->stream, e->s_ctx, src, src, ni, e->s_cell_of, e->s_slot, e->s_count);
-    launch_cell_scan(e->stream, e->s_ctx, ni, e->s_count, e->s_cstart);
+    launch_cell_scan(e->stream, e->s_ctx, ni, e->s_count, e->s_cstart, e->s_tile);
     launch_cell_scatter(e->stream, ni, e->s_cell_of, e->s_slot, e->s_cstart, e->s_tmp);
     launch_cell_sort(e->stream, e->s_ctx, src, src, nullptr, ni, e->s_tmp, e->s_cell_of, e->s_cstart, e->s_sidx,
                      e->s_scell, e->s_spos, e->s_sb, 1);
@@ -1044,7 +1051,7 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     if (rc) return rc;
     std::vector<hipEvent_t> ev((size_t)steps * 4 + 2, nullptr);
     for (auto& x : ev) HIPCHK(hipEventCreate(&x));
-    const int fb = force_blocks(e->n);
+    const int fb = force_grid(e->n);
     HIPCHK(hipEventRecord(ev[0], e->stream));
     for (int64_t k = 0; k < steps; ++k) {
         HIPCHK(hipEventRecord(ev[1 + 4 * k], e->stream));

@@ -44,7 +44,7 @@ struct DevCtx {
     long long step;        // last completed step
     long long noise_cursor;
     int parity;            // index of the current position buffer
-    int pad0;
+    int ntiles;            // k_force tiles of the current cell list (k_cell_scan)
     float bbox_lo[3], bbox_hi[3];
     Grid grid;
 };
@@ -83,6 +83,7 @@ struct ForceArgs {
     const int* sidx;
     const int* scell;
     const int* cstart;
+    const int* tile_start;  // [rows + 1] first tile of each cell row (k_cell_scan)
     // neighbor soft-core pair field
     int has_pair, pair_mix, pair_scaled, pad0;
     float pa_eps, pa_sig, pb_eps, pb_sig, pair_dist;
@@ -144,7 +145,7 @@ __host__ __device__ inline void philox4x32_10(unsigned c[4], unsigned k0, unsign
 void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed, int ncell_max);
 void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n,
                        int* cell_of, int* slot, int* count);
-void launch_cell_scan(hipStream_t s, const DevCtx* ctx, int n, int* count, int* cstart);
+void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start);
 void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* slot, const int* cstart, int* tmp);
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, const float4* kmu,
                       int n, const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell,
@@ -163,6 +164,9 @@ void sort_u64_keys(hipStream_t s, unsigned long long* keys, unsigned long long* 
 size_t sort_u64_temp_bytes(int n);
 
 inline int force_blocks(int n) { return (n + kTile - 1) / kTile; }
+// k_force launch size: tiles never cross a cell row, so there are up to (rows) more tiles than force_blocks;
+// blocks walk the tiles grid-stride, any launch size is correct
+inline int force_grid(int n) { return force_blocks(n) + force_blocks(n) / 4 + 64; }
 constexpr int kUpdateBlock = 256;
 inline int update_blocks(int n) { return (n + kUpdateBlock - 1) / kUpdateBlock; }
 

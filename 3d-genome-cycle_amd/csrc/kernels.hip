@@ -50,6 +50,9 @@ __device__ inline float wave_min(float v)
 
 __device__ inline int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// keeps a value "used" so a float4 LDS read stays one ds_read_b128
+__device__ inline void keep_live(float v) { asm volatile("" ::"v"(v)); }
+
 __device__ inline int wave_max_int(int v)
 {
 #pragma unroll
@@ -184,8 +187,8 @@ __device__ inline int wave_incl_scan(int v, int lane)
 // Exclusive scan count -> cstart over the grid's cells in coalesced 4096-cell tiles (int4 per thread) with a
 // running carry; re-zeroes count for the next step.  count/cstart are padded by kScanPad so whole tiles may be
 // touched; entries past ncell are zero by invariant.
-__global__ __launch_bounds__(1024) void k_cell_scan(const DevCtx* __restrict__ ctx, int n, int* __restrict__ count,
-                                                    int* __restrict__ cstart)
+__global__ __launch_bounds__(1024) void k_cell_scan(DevCtx* __restrict__ ctx, int n, int* __restrict__ count,
+                                                    int* __restrict__ cstart, int* __restrict__ tile_start)
 {
     __shared__ int wtot[16];
     __shared__ int tile_total;
@@ -213,6 +216,43 @@ __global__ __launch_bounds__(1024) void k_cell_scan(const DevCtx* __restrict__ c
         __syncthreads();
     }
     if (tid == 0) cstart[nc] = n;
+    __syncthreads();
+    // per-row tile prefix for k_force: row r = (y, z) holds ceil(particles / 64) tiles
+    const int nx = ctx->grid.n[0], nrows = ctx->grid.n[1] * ctx->grid.n[2];
+    carry = 0;
+    for (int base = 0; base < nrows; base += 4096) {
+        int c[4];
+        int sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = base + 4 * tid + q;
+            c[q] = (r < nrows) ? (cstart[(r + 1) * nx] - cstart[r * nx] + kTile - 1) / kTile : 0;
+            sum += c[q];
+        }
+        const int incl = wave_incl_scan(sum, lane);
+        if (lane == 63) wtot[wave] = incl;
+        __syncthreads();
+        if (wave == 0) {
+            const int w = lane < 16 ? wtot[lane] : 0;
+            const int wi = wave_incl_scan(w, lane);
+            if (lane < 16) wtot[lane] = wi - w;
+            if (lane == 15) tile_total = wi;
+        }
+        __syncthreads();
+        int run = carry + wtot[wave] + incl - sum;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = base + 4 * tid + q;
+            if (r < nrows) tile_start[r] = run;
+            run += c[q];
+        }
+        carry += tile_total;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        tile_start[nrows] = carry;
+        ctx->ntiles = carry;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_cell_scatter(int n, const int* __restrict__ cell_of, const int* __restrict__ slot,
@@ -308,228 +348,18 @@ __device__ inline float spring_coef(int type, float K, float l, float r2, float&
 // ----------------------------------------------------------------------------------------------------
 // force / step kernel
 
-template <int MODE, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__ ctx, ForceArgs a)
+// Particle-local terms of particle i at (xi, yi, zi): bonded CSR (chain/loop/nucleolar bonds, droplet),
+// cosine bending, kinetochore fibers, point sources and the ellipsoid walls (+ their reactions).
+template <int MODE>
+__device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceArgs& a, int i, float xi, float yi,
+                                   float zi, float4 km, float& fx, float& fy, float& fz, float* en, float* rin,
+                                   float* rout)
 {
-    __shared__ float red[WAVES > 1 ? WAVES : 1][4][64];
-    __shared__ int s_rowV[kMaxRows + 1];
-    __shared__ int s_rowJ[kMaxRows];
-    __shared__ float4 s_cand[WAVES][kTile];
-    __shared__ float s_candb[WAVES][kTile];
-    __shared__ int s_candj[MODE == kModeEnergy ? WAVES : 1][kTile];
-    const int lane = threadIdx.x & 63;
-    const int wave = uniform(threadIdx.x >> 6);
     const int n = a.n;
-    const int s0 = blockIdx.x * kTile;
-    const int s = s0 + lane;
-    const bool valid = s < n;
-    const int sl = valid ? s : n - 1;
-    const float4 pi = a.spos[sl];
-    const float bi = a.sb[sl];
+    const float4* __restrict__ posc = ctx->parity ? a.pos1 : a.pos0;
     const float cs = (float)ctx->cs;
-
-    float fx = 0.f, fy = 0.f, fz = 0.f, acc = 0.f;  // acc: pair energy (ENERGY) or neighbour count
-
-    if (a.has_pair) {
-        const Grid g = ctx->grid;
-        const float scale = a.pair_scaled ? cs : 1.f;
-        const float sa = a.pa_sig * scale, sbb = a.pb_sig * scale;
-        const float k2a = 1.f / (sa * sa), k2b = 1.f / (sbb * sbb);
-        // F = coef * (x_i - x_j):  A * 6 eps_a k2a ga^2  +  B * 24 eps_b k2b gb^2 t^3   (A, B = pair means)
-        const float ca = 0.5f * 6.f * a.pa_eps * k2a;
-        const float cb = 0.5f * 24.f * a.pb_eps * k2b;
-        const float ea = 0.25f * a.pa_eps;  // energy: 1/2 (mean) x 1/2 (each pair seen from both ends)
-        const float eb = 0.25f * a.pb_eps;
-        const float rc2 = g.rc2;
-        const int nx = g.n[0], ny = g.n[1], nz = g.n[2], gfx = g.fx;
-        // The tile covers the contiguous cell-id interval [c0, c1] (x fastest).  Its stencil rows are all
-        // rows (y', z') next to a covered row; each gets the union of the covered x-ranges padded by fx
-        // cells (the x edge is rc / fx), so every particle within rc of a tile particle is a candidate.
-        const int slast = min(n, s0 + kTile) - 1;
-        const int c0 = uniform(a.scell[s0]), c1 = uniform(a.scell[slast]);
-        const int x0 = c0 % nx, r0 = c0 / nx, x1 = c1 % nx, r1 = c1 / nx;
-        const int y0 = r0 % ny, z0 = r0 / ny, y1 = r1 % ny, z1 = r1 / ny;
-        int ylo = 0, yhi = ny - 1;
-        if (z0 == z1) {
-            ylo = max(y0 - 1, 0);
-            yhi = min(y1 + 1, ny - 1);
-        }
-        const int zlo = max(z0 - 1, 0), zhi = min(z1 + 1, nz - 1);
-        const int nyb = yhi - ylo + 1;
-        const int nbox = nyb * (zhi - zlo + 1);
-        const float ahi = pi.w, bhi = bi;
-        for (int rb = 0; rb < nbox; rb += kMaxRows) {
-            if (wave == 0) {  // row table of this batch: lane q builds stencil row rb + q
-                const int q = rb + lane;
-                int len = 0, jb = 0;
-                if (q < nbox) {
-                    const int yq = ylo + q % nyb, zq = zlo + q / nyb;
-                    int ulo = nx, uhi = -1;
-                    for (int dz = -1; dz <= 1; ++dz)
-                        for (int dy = -1; dy <= 1; ++dy) {
-                            const int y = yq + dy, z = zq + dz;
-                            if (y < 0 || y >= ny || z < 0 || z >= nz) continue;
-                            const int rr = z * ny + y;
-                            if (rr < r0 || rr > r1) continue;
-                            ulo = min(ulo, (rr == r0 ? x0 : 0) - gfx);
-                            uhi = max(uhi, (rr == r1 ? x1 : nx - 1) + gfx);
-                        }
-                    ulo = max(ulo, 0);
-                    uhi = min(uhi, nx - 1);
-                    if (ulo <= uhi) {
-                        const int base = (zq * ny + yq) * nx;
-                        jb = a.cstart[base + ulo];
-                        len = a.cstart[base + uhi + 1] - jb;
-                    }
-                }
-                const int incl = wave_incl_scan(len, lane);
-                s_rowV[lane] = incl - len;
-                s_rowJ[lane] = jb;
-                if (lane == kMaxRows - 1) s_rowV[kMaxRows] = incl;
-            }
-            __syncthreads();
-            const int total = uniform(s_rowV[kMaxRows]);
-            const int wlo = (int)(((long long)total * wave) / WAVES);
-            const int whi = (int)(((long long)total * (wave + 1)) / WAVES);
-            // software pipeline: chunk c+1's candidates (row lookup + global loads) are in flight while
-            // chunk c is filtered and evaluated from LDS
-            auto fetch = [&](int base, float4& p, float& b, int& jj) {
-                const int v = base + lane;
-                p = make_float4(1e18f, 1e18f, 1e18f, 0.f);  // far-away sentinel: never a hit
-                b = 0.f;
-                jj = -1;
-                if (v < whi) {
-                    int lo = 0, hi = kMaxRows - 1;  // last stencil row starting at or before v
-                    while (lo < hi) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (s_rowV[mid] <= v)
-                            lo = mid;
-                        else
-                            hi = mid - 1;
-                    }
-                    jj = s_rowJ[lo] + (v - s_rowV[lo]);
-                    p = a.spos[jj];
-                    b = a.sb[jj];
-                }
-            };
-            float4 npj;
-            float nbj;
-            int njj;
-            fetch(wlo, npj, nbj, njj);
-            for (int base = wlo; base < whi; base += kTile) {
-                const int cnt = uniform(min(kTile, whi - base));
-                const int cnt8 = (cnt + 7) & ~7;  // sentinel-padded to a multiple of 8 -> unrolled by 8
-                s_cand[wave][lane] = npj;
-                s_candb[wave][lane] = nbj;
-                if (MODE == kModeEnergy) s_candj[MODE == kModeEnergy ? wave : 0][lane] = njj;
-                __builtin_amdgcn_wave_barrier();
-                if (base + kTile < whi) fetch(base + kTile, npj, nbj, njj);
-                // phase 1: distance filter over the chunk; each lane keeps a 64-bit mask of its hits
-                unsigned mlo = 0u, mhi = 0u;
-                for (int k0 = 0; k0 < cnt8; k0 += 8) {
-                    unsigned byte = 0u;
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const float4 pj = s_cand[wave][k0 + u];
-                        const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
-                        const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                        // the self pair contributes exactly zero force (F is proportional to x_i - x_j), so
-                        // the force path keeps it (one wasted slot) instead of a second compare per candidate
-                        const bool in = (MODE == kModeEnergy)
-                                            ? ((r2 < rc2) && (s_candj[MODE == kModeEnergy ? wave : 0][k0 + u] != s))
-                                            : (r2 < rc2);
-                        byte |= in ? (1u << u) : 0u;
-                    }
-                    if (k0 < 32)
-                        mlo |= byte << k0;
-                    else
-                        mhi |= byte << (k0 - 32);
-                }
-                const int nh = __popc(mlo) + __popc(mhi);
-                // phase 2: the potential on the hits only (iterations = the wave's largest hit count), four
-                // independent hits per iteration so their LDS gathers overlap
-                const int mh = uniform(wave_max_int(nh));
-                for (int t = 0; t < mh; t += 4) {
-                    int kk[4];
-                    bool av[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {  // pop the lowest set bits
-                        av[u] = (mlo | mhi) != 0u;
-                        const int klo = __ffs(mlo) - 1, khi = __ffs(mhi) + 31;
-                        kk[u] = av[u] ? (mlo ? klo : khi) : 0;  // inactive: a valid slot, no NaN
-                        if (mlo)
-                            mlo &= mlo - 1u;
-                        else
-                            mhi &= mhi - 1u;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const bool act = av[u];
-                        const int k = kk[u];
-                        const float4 pj = s_cand[wave][k];
-                        const float bj = s_candb[wave][k];
-                        const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
-                        const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                        const float A = ahi + pj.w, B = bhi + bj;
-                        const float ua = r2 * k2a;
-                        const float ga = 1.f - ua;
-                        const float tt = r2 * k2b;
-                        const float t2 = tt * tt;
-                        const float gb = 1.f - t2 * t2;
-                        const float gb2 = gb * gb;
-                        const bool ina = act && (ua < 1.f);
-                        const bool inb = act && (tt < 1.f);
-                        if (MODE == kModeEnergy) {
-                            const float ua3 = ga * ga * ga, ub3 = gb2 * gb;
-                            acc += (ina ? A * ea * ua3 : 0.f) + (inb ? B * eb * ub3 : 0.f);
-                        } else {
-                            const float fa = ina ? ga * ga : 0.f;
-                            const float fb = inb ? gb2 * t2 * tt : 0.f;
-                            const float coef = fmaf(A * ca, fa, B * cb * fb);
-                            fx = fmaf(coef, dx, fx);
-                            fy = fmaf(coef, dy, fy);
-                            fz = fmaf(coef, dz, fz);
-                        }
-                    }
-                }
-                if (MODE != kModeEnergy) acc += (float)nh;
-                __builtin_amdgcn_wave_barrier();
-            }
-            __syncthreads();
-        }
-    }
-
-    if (WAVES > 1) {
-        red[wave][0][lane] = fx;
-        red[wave][1][lane] = fy;
-        red[wave][2][lane] = fz;
-        red[wave][3][lane] = acc;
-        __syncthreads();
-        if (wave != 0) return;
-        fx = red[0][0][lane];
-        fy = red[0][1][lane];
-        fz = red[0][2][lane];
-        acc = red[0][3][lane];
-#pragma unroll
-        for (int w = 1; w < WAVES; ++w) {
-            fx += red[w][0][lane];
-            fy += red[w][1][lane];
-            fz += red[w][2][lane];
-            acc += red[w][3][lane];
-        }
-    }
-
-    // ---- particle-local terms (wave 0) ----
-    const int i = a.sidx[sl];
-    const int par = ctx->parity;
-    const float4* __restrict__ posc = par ? a.pos1 : a.pos0;
-    float4* __restrict__ posn = par ? a.pos0 : a.pos1;
-    const float4 km = a.kmu[i];
-    const float xi = pi.x, yi = pi.y, zi = pi.z;
     const float bs = (float)ctx->bs;
     float e_sw = 0.f, e_bond = 0.f, e_bend = 0.f, e_win = 0.f, e_wout = 0.f, e_pt = 0.f, e_kf = 0.f;
-    float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
-
     if (a.has_bonds) {
         const int eb = a.boff[i], ee = a.boff[i + 1];
         for (int q = eb; q < ee; ++q) {
@@ -611,7 +441,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
         }
     }
 
-    for (int q = 0; q < a.n_point; ++q) {
+#pragma unroll
+    for (int q = 0; q < kMaxPointSources; ++q) {
+        if (q >= a.n_point) break;
         const PointSrc& p = a.point[q];
         const float rx = xi - p.px, ry = yi - p.py, rz = zi - p.pz;
         const float r2 = rx * rx + ry * ry + rz * rz;
@@ -682,58 +514,308 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
         }
     }
 
-    if (MODE == kModeEnergy) {
-        const double vals[kEnergyKinds] = {valid ? (double)acc : 0.0,  valid ? (double)e_sw : 0.0,
-                                           valid ? (double)e_bond : 0.0, valid ? (double)e_bend : 0.0,
-                                           valid ? (double)e_win : 0.0,  valid ? (double)e_wout : 0.0,
-                                           valid ? (double)e_pt : 0.0,   valid ? (double)e_kf : 0.0};
-        for (int k = 0; k < kEnergyKinds; ++k) {
-            const double t = wave_sum_d(vals[k]);
-            if (lane == 0) a.part_energy[blockIdx.x * kEnergyKinds + k] = t;
+    en[1] = e_sw;
+    en[2] = e_bond;
+    en[3] = e_bend;
+    en[4] = e_win;
+    en[5] = e_wout;
+    en[6] = e_pt;
+    en[7] = e_kf;
+}
+
+// Gather-form pair forces on the 64 particles of one tile [s_begin, s_end) (one row of cells, lane = particle)
+// from this wave's share of the tile's stencil candidates.  Stencil: the 3x3 neighbouring cell rows, x-range
+// [x_first - fx, x_last + fx] (x cells are rc / fx wide).  Candidates are staged 64 at a time in LDS
+// (software-pipelined), filtered in fp32 into a per-lane 64-bit hit mask, and the soft-core potential is
+// evaluated for the hits only.
+template <int MODE, int WAVES>
+__device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceArgs& a, int wave, int lane, int s,
+                                   int s_begin, int s_end, float4 pi, float bi, float& fx, float& fy, float& fz,
+                                   float& acc, int* s_rowV, int* s_rowJ, float4* s_cand, float* s_candb, int* s_candj)
+{
+    const Grid g = ctx->grid;
+    const float cs = (float)ctx->cs;
+    const float scale = a.pair_scaled ? cs : 1.f;
+    const float sa = a.pa_sig * scale, sbb = a.pb_sig * scale;
+    const float k2a = 1.f / (sa * sa), k2b = 1.f / (sbb * sbb);
+    // F = coef * (x_i - x_j):  A * 6 eps_a k2a ga^2  +  B * 24 eps_b k2b gb^2 t^3   (A, B = pair means)
+    const float ca = 0.5f * 6.f * a.pa_eps * k2a;
+    const float cb = 0.5f * 24.f * a.pb_eps * k2b;
+    const float ea = 0.25f * a.pa_eps;  // energy: 1/2 (mean) x 1/2 (each pair seen from both ends)
+    const float eb = 0.25f * a.pb_eps;
+    const float rc2 = g.rc2;
+    const int nx = g.n[0], ny = g.n[1], nz = g.n[2], gfx = g.fx;
+    const int c0 = uniform(a.scell[s_begin]), c1 = uniform(a.scell[s_end - 1]);
+    const int x0 = c0 % nx, x1 = c1 % nx, r0 = c0 / nx;
+    const int y0 = r0 % ny, z0 = r0 / ny;
+    const int xlo = max(x0 - gfx, 0), xhi = min(x1 + gfx, nx - 1);
+
+    // wave-private row table: lane q < 9 holds stencil row (y0 + q%3 - 1, z0 + q/3 - 1)
+    {
+        int len = 0, jb = 0;
+        if (lane < 9) {
+            const int y = y0 + lane % 3 - 1, z = z0 + lane / 3 - 1;
+            if (y >= 0 && y < ny && z >= 0 && z < nz) {
+                const int base = (z * ny + y) * nx;
+                jb = a.cstart[base + xlo];
+                len = a.cstart[base + xhi + 1] - jb;
+            }
         }
-        return;
+        const int incl = wave_incl_scan(len, lane);
+        if (lane < 16) {
+            s_rowV[lane] = incl - len;
+            s_rowJ[lane] = jb;
+        }
+        if (lane == 15) s_rowV[16] = incl;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int total = uniform(s_rowV[16]);
+    const int wlo = (int)(((long long)total * wave) / WAVES);
+    const int whi = (int)(((long long)total * (wave + 1)) / WAVES);
+    const float ahi = pi.w, bhi = bi;
+
+    auto fetch = [&](int base, float4& p, float& b, int& jj) {
+        const int v = base + lane;
+        p = make_float4(1e18f, 1e18f, 1e18f, 0.f);  // far-away sentinel: never a hit
+        b = 0.f;
+        jj = -1;
+        if (v < whi) {
+            int lo = 0;  // last stencil row starting at or before v (rows 9..15 start at `total`)
+#pragma unroll
+            for (int step = 8; step > 0; step >>= 1)
+                if (s_rowV[lo + step] <= v) lo += step;
+            jj = s_rowJ[lo] + (v - s_rowV[lo]);
+            p = a.spos[jj];
+            b = a.sb[jj];
+        }
+    };
+    float4 npj;
+    float nbj;
+    int njj;
+    fetch(wlo, npj, nbj, njj);
+    for (int base = wlo; base < whi; base += kTile) {
+        const int cnt = uniform(min(kTile, whi - base));
+        const int cnt8 = (cnt + 7) & ~7;  // sentinel-padded to a multiple of 8
+        s_cand[lane] = npj;
+        s_candb[lane] = nbj;
+        if (MODE == kModeEnergy) s_candj[lane] = njj;
+        __builtin_amdgcn_wave_barrier();
+        if (base + kTile < whi) fetch(base + kTile, npj, nbj, njj);  // next chunk in flight
+
+        // phase 1: distance filter over the chunk; each lane keeps a 64-bit mask of its hits
+        unsigned mlo = 0u, mhi = 0u;
+        for (int k0 = 0; k0 < cnt8; k0 += 8) {
+            unsigned byte = 0u;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const float4 pj = s_cand[k0 + u];
+                keep_live(pj.w);  // one ds_read_b128 (4 LDS cycles) instead of a ds_read_b96 (8)
+                const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+                const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                // the self pair contributes exactly zero force (F is proportional to x_i - x_j), so the force
+                // path keeps it (one wasted slot) instead of paying a second compare per candidate
+                const bool in = (MODE == kModeEnergy) ? ((r2 < rc2) && (s_candj[k0 + u] != s)) : (r2 < rc2);
+                byte |= in ? (1u << u) : 0u;
+            }
+            if (k0 < 32)
+                mlo |= byte << k0;
+            else
+                mhi |= byte << (k0 - 32);
+        }
+        const int nh = __popc(mlo) + __popc(mhi);
+        if (MODE != kModeEnergy) acc += (float)nh;
+        // phase 2: the potential on the hits only (iterations = the wave's largest hit count), four
+        // independent hits per iteration so their LDS gathers overlap
+        const int mh = uniform(wave_max_int(nh));
+        for (int t = 0; t < mh; t += 4) {
+            int kk[4];
+            bool av[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {  // pop the lowest set bits
+                av[u] = (mlo | mhi) != 0u;
+                const int klo = __ffs(mlo) - 1, khi = __ffs(mhi) + 31;
+                kk[u] = av[u] ? (mlo ? klo : khi) : 0;  // inactive: a valid slot, no NaN
+                if (mlo)
+                    mlo &= mlo - 1u;
+                else
+                    mhi &= mhi - 1u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const bool act = av[u];
+                const float4 pj = s_cand[kk[u]];
+                const float bj = s_candb[kk[u]];
+                const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+                const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                const float A = ahi + pj.w, B = bhi + bj;
+                const float ua = r2 * k2a;
+                const float ga = 1.f - ua;
+                const float tt = r2 * k2b;
+                const float t2 = tt * tt;
+                const float gb = 1.f - t2 * t2;
+                const float gb2 = gb * gb;
+                const bool ina = act && (ua < 1.f);
+                const bool inb = act && (tt < 1.f);
+                if (MODE == kModeEnergy) {
+                    const float ua3 = ga * ga * ga, ub3 = gb2 * gb;
+                    acc += (ina ? A * ea * ua3 : 0.f) + (inb ? B * eb * ub3 : 0.f);
+                } else {
+                    const float fa = ina ? ga * ga : 0.f;
+                    const float fb = inb ? gb2 * t2 * tt : 0.f;
+                    const float coef = fmaf(A * ca, fa, B * cb * fb);
+                    fx = fmaf(coef, dx, fx);
+                    fy = fmaf(coef, dy, fy);
+                    fz = fmaf(coef, dz, fz);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// One launch = one force evaluation (+ the Euler-Maruyama update in kModeStep).  Blocks walk the tiles of the
+// current cell list (grid-stride); a tile is <= 64 consecutive sorted particles of ONE row of cells
+// (k_cell_scan builds the per-row tile prefix).  The WAVES waves split the tile's candidates; wave 0 then
+// adds the particle-local terms and integrates.  Per-block partials (reactions, bbox, drift, neighbours,
+// energies) are reduced in a fixed order by k_tail / the host: no atomics, bitwise reproducible.
+template <int MODE, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__ ctx, ForceArgs a)
+{
+    __shared__ float red[WAVES > 1 ? WAVES : 1][4][64];
+    __shared__ int s_rowV[WAVES][17];
+    __shared__ int s_rowJ[WAVES][16];
+    __shared__ float4 s_cand[WAVES][kTile];
+    __shared__ float s_candb[WAVES][kTile];
+    __shared__ int s_candj[MODE == kModeEnergy ? WAVES : 1][kTile];
+    __shared__ float s_pr[kForcePartials + kBBoxPartials];  // per-block accumulators (lane 0 of wave 0)
+    __shared__ double s_pe[kEnergyKinds];
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    const int ntiles = ctx->ntiles;
+    const int nrows = ctx->grid.n[1] * ctx->grid.n[2];
+    const int nx = ctx->grid.n[0];
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < kForcePartials; ++k) s_pr[k] = 0.f;
+        for (int k = 0; k < 3; ++k) {
+            s_pr[kForcePartials + k] = 3.0e38f;
+            s_pr[kForcePartials + 3 + k] = -3.0e38f;
+        }
+        for (int k = 0; k < kEnergyKinds; ++k) s_pe[k] = 0.0;
     }
 
-    // reaction / neighbour partials
-    {
-        float vals[kForcePartials];
-        vals[0] = valid ? rin[0] : 0.f;
-        vals[1] = valid ? rin[1] : 0.f;
-        vals[2] = valid ? rin[2] : 0.f;
-        vals[3] = valid ? rout[0] : 0.f;
-        vals[4] = valid ? rout[1] : 0.f;
-        vals[5] = valid ? rout[2] : 0.f;
-        const float drift = valid ? km.x * sqrtf(fx * fx + fy * fy + fz * fz) : 0.f;
-        vals[7] = valid ? acc - (a.has_pair ? 1.f : 0.f) : 0.f;  // the pair loop counted the particle itself
-        float outv[kForcePartials];
-        for (int k = 0; k < kForcePartials; ++k) outv[k] = (k == 6) ? wave_max(drift) : wave_sum(vals[k]);
-        if (lane == 0)
-            for (int k = 0; k < kForcePartials; ++k) a.part_force[blockIdx.x * kForcePartials + k] = outv[k];
-    }
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        int s_begin, s_end;
+        {  // the row holding this tile: last row whose tile prefix is <= tile
+            int lo = 0, hi = nrows - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (a.tile_start[mid] <= tile)
+                    lo = mid;
+                else
+                    hi = mid - 1;
+            }
+            const int row_begin = a.cstart[lo * nx], row_end = a.cstart[(lo + 1) * nx];
+            s_begin = uniform(row_begin + (tile - a.tile_start[lo]) * kTile);
+            s_end = uniform(min(row_end, s_begin + kTile));
+        }
+        const int s = s_begin + lane;
+        const bool valid = s < s_end;
+        const int sl = valid ? s : s_end - 1;
+        const float4 pi = a.spos[sl];
+        const float bi = a.sb[sl];
 
-    if (MODE == kModeForce) {
-        if (valid) a.force_out[i] = make_float4(fx, fy, fz, 0.f);
-        return;
+        float fx = 0.f, fy = 0.f, fz = 0.f, acc = 0.f;  // acc: pair energy (ENERGY) or neighbour count
+        if (a.has_pair)
+            pair_forces<MODE, WAVES>(ctx, a, wave, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
+                                     s_rowJ[wave], s_cand[wave], s_candb[wave], s_candj[MODE == kModeEnergy ? wave : 0]);
+        if (WAVES > 1) {
+            red[wave][0][lane] = fx;
+            red[wave][1][lane] = fy;
+            red[wave][2][lane] = fz;
+            red[wave][3][lane] = acc;
+            __syncthreads();
+            if (wave == 0) {
+                fx = red[0][0][lane];
+                fy = red[0][1][lane];
+                fz = red[0][2][lane];
+                acc = red[0][3][lane];
+#pragma unroll
+                for (int w = 1; w < WAVES; ++w) {
+                    fx += red[w][0][lane];
+                    fy += red[w][1][lane];
+                    fz += red[w][2][lane];
+                    acc += red[w][3][lane];
+                }
+            }
+        }
+        if (wave == 0) {
+            const int i = a.sidx[sl];
+            const float4 km = a.kmu[i];
+            float en[kEnergyKinds];
+            float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
+            local_terms<MODE>(ctx, a, i, pi.x, pi.y, pi.z, km, fx, fy, fz, en, rin, rout);
+            en[0] = acc;
+            if (MODE == kModeEnergy) {
+                for (int k = 0; k < kEnergyKinds; ++k) {
+                    const double t = wave_sum_d(valid ? (double)en[k] : 0.0);
+                    if (lane == 0) s_pe[k] += t;
+                }
+            } else {
+                float v[kForcePartials];
+                v[0] = wave_sum(valid ? rin[0] : 0.f);
+                v[1] = wave_sum(valid ? rin[1] : 0.f);
+                v[2] = wave_sum(valid ? rin[2] : 0.f);
+                v[3] = wave_sum(valid ? rout[0] : 0.f);
+                v[4] = wave_sum(valid ? rout[1] : 0.f);
+                v[5] = wave_sum(valid ? rout[2] : 0.f);
+                v[6] = wave_max(valid ? km.x * sqrtf(fx * fx + fy * fy + fz * fz) : 0.f);
+                // the pair loop counted the particle itself
+                v[7] = wave_sum(valid ? acc - (a.has_pair ? 1.f : 0.f) : 0.f);
+                if (lane == 0)
+                    for (int k = 0; k < kForcePartials; ++k) s_pr[k] = (k == 6) ? fmaxf(s_pr[k], v[k]) : s_pr[k] + v[k];
+                if (MODE == kModeForce) {
+                    if (valid) a.force_out[i] = make_float4(fx, fy, fz, 0.f);
+                } else {
+                    // Euler-Maruyama: x += mu dt F + sqrt(2 T mu dt) xi
+                    float4* __restrict__ posn = ctx->parity ? a.pos0 : a.pos1;
+                    const float mu = km.x;
+                    const float dt = a.timestep;
+                    float n0, n1, n2;
+                    noise3(a, ctx, i, n0, n1, n2);
+                    const float amp = sqrtf(2.f * a.temperature * mu * dt);
+                    const float mdt = mu * dt;
+                    const float nxp = pi.x + mdt * fx + amp * n0;
+                    const float nyp = pi.y + mdt * fy + amp * n1;
+                    const float nzp = pi.z + mdt * fz + amp * n2;
+                    if (valid) posn[i] = make_float4(nxp, nyp, nzp, 0.f);
+                    const float big = 3.0e38f;
+                    const float l0 = wave_min(valid ? nxp : big), l1 = wave_min(valid ? nyp : big),
+                                l2 = wave_min(valid ? nzp : big);
+                    const float h0 = wave_max(valid ? nxp : -big), h1 = wave_max(valid ? nyp : -big),
+                                h2 = wave_max(valid ? nzp : -big);
+                    if (lane == 0) {
+                        float* b = s_pr + kForcePartials;
+                        b[0] = fminf(b[0], l0);
+                        b[1] = fminf(b[1], l1);
+                        b[2] = fminf(b[2], l2);
+                        b[3] = fmaxf(b[3], h0);
+                        b[4] = fmaxf(b[4], h1);
+                        b[5] = fmaxf(b[5], h2);
+                    }
+                }
+            }
+        }
+        if (WAVES > 1) __syncthreads();  // `red` is reused by the next tile
     }
-
-    // ---- Euler-Maruyama update: x += mu dt F + sqrt(2 T mu dt) xi ----
-    const float mu = km.x;
-    const float dt = a.timestep;
-    float n0, n1, n2;
-    noise3(a, ctx, i, n0, n1, n2);
-    const float amp = sqrtf(2.f * a.temperature * mu * dt);
-    const float mdt = mu * dt;
-    const float nxp = xi + mdt * fx + amp * n0;
-    const float nyp = yi + mdt * fy + amp * n1;
-    const float nzp = zi + mdt * fz + amp * n2;
-    if (valid) posn[i] = make_float4(nxp, nyp, nzp, 0.f);
-    {
-        const float big = 3.0e38f;
-        const float l0 = wave_min(valid ? nxp : big), l1 = wave_min(valid ? nyp : big), l2 = wave_min(valid ? nzp : big);
-        const float h0 = wave_max(valid ? nxp : -big), h1 = wave_max(valid ? nyp : -big), h2 = wave_max(valid ? nzp : -big);
-        if (lane == 0) {
-            float* pb = a.part_bbox + blockIdx.x * kBBoxPartials;
-            pb[0] = l0; pb[1] = l1; pb[2] = l2; pb[3] = h0; pb[4] = h1; pb[5] = h2;
+    if (WAVES == 1) __syncthreads();  // (WAVES > 1 synchronised at the end of every tile)
+    if (threadIdx.x == 0) {
+        if (MODE == kModeEnergy) {
+            for (int k = 0; k < kEnergyKinds; ++k) a.part_energy[blockIdx.x * kEnergyKinds + k] = s_pe[k];
+        } else {
+            for (int k = 0; k < kForcePartials; ++k) a.part_force[blockIdx.x * kForcePartials + k] = s_pr[k];
+            if (MODE == kModeStep)
+                for (int k = 0; k < kBBoxPartials; ++k)
+                    a.part_bbox[blockIdx.x * kBBoxPartials + k] = s_pr[kForcePartials + k];
         }
     }
 }
@@ -954,9 +1036,9 @@ void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, con
     hipLaunchKernelGGL(k_cell_count, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, n, cell_of, slot, count);
 }
 
-void launch_cell_scan(hipStream_t s, const DevCtx* ctx, int n, int* count, int* cstart)
+void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start)
 {
-    hipLaunchKernelGGL(k_cell_scan, dim3(1), dim3(1024), 0, s, ctx, n, count, cstart);
+    hipLaunchKernelGGL(k_cell_scan, dim3(1), dim3(1024), 0, s, ctx, n, count, cstart, tile_start);
 }
 
 void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* slot, const int* cstart, int* tmp)
@@ -975,7 +1057,7 @@ void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, cons
 template <int MODE>
 static void launch_force_mode(hipStream_t s, int waves, const DevCtx* ctx, const ForceArgs& a)
 {
-    const dim3 grid(force_blocks(a.n));
+    const dim3 grid(force_grid(a.n));
     switch (waves) {
     case 1: hipLaunchKernelGGL((k_force<MODE, 1>), grid, dim3(64), 0, s, ctx, a); break;
     case 2: hipLaunchKernelGGL((k_force<MODE, 2>), grid, dim3(128), 0, s, ctx, a); break;
