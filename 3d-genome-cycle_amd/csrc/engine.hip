@@ -88,6 +88,7 @@ struct gcs_engine {
     float* sb = nullptr;
     int *sidx = nullptr, *scell = nullptr, *cell_of = nullptr, *slot = nullptr, *tmp = nullptr;
     int *count = nullptr, *cstart = nullptr, *tile_start = nullptr;
+    int2* tile_range = nullptr;
     DevCtx* ctx = nullptr;
     double* dsched = nullptr;
     float* part_force = nullptr;
@@ -112,6 +113,7 @@ struct gcs_engine {
     int *s_sidx = nullptr, *s_scell = nullptr, *s_cell_of = nullptr, *s_slot = nullptr, *s_tmp = nullptr;
     int *s_count = nullptr, *s_cstart = nullptr, *s_counts = nullptr, *s_offsets = nullptr, *s_total = nullptr;
     int* s_tile = nullptr;
+    int2* s_tile_range = nullptr;
     int s_ncell_max = 0;
     DevCtx* s_ctx = nullptr;
     unsigned long long *s_keys = nullptr, *s_keys2 = nullptr;
@@ -367,7 +369,7 @@ void fill_state_args(gcs_engine* e)
     a.sidx = e->sidx;
     a.scell = e->scell;
     a.cstart = e->cstart;
-    a.tile_start = e->tile_start;
+    a.tile_range = e->tile_range;
     a.part_force = e->part_force;
     a.part_bbox = e->part_bbox;
     a.part_energy = e->part_energy;
@@ -380,7 +382,7 @@ void enqueue_cells(gcs_engine* e)
 {
     const int n = e->n;
     launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count);
-    launch_cell_scan(e->stream, e->ctx, n, e->count, e->cstart, e->tile_start);
+    launch_cell_scan(e->stream, e->ctx, n, e->count, e->cstart, e->tile_start, e->tile_range);
     launch_cell_scatter(e->stream, n, e->cell_of, e->slot, e->cstart, e->tmp);
     launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, n, e->tmp, e->cell_of, e->cstart, e->sidx,
                      e->scell, e->spos, e->sb, e->fa.has_pair ? e->fa.pair_mix : 1);
@@ -507,6 +509,7 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
         (rc = dalloc(&e->scell, n)) || (rc = dalloc(&e->cell_of, n)) || (rc = dalloc(&e->slot, n)) ||
         (rc = dalloc(&e->tmp, n)) || (rc = dalloc(&e->count, e->ncell_max + kScanPad)) ||
         (rc = dalloc(&e->cstart, e->ncell_max + kScanPad)) || (rc = dalloc(&e->tile_start, e->ncell_max + 2)) ||
+        (rc = dalloc(&e->tile_range, (size_t)force_blocks(n) + e->ncell_max + 2)) ||
         (rc = dalloc(&e->ctx, 1)) || (rc = dalloc(&e->dsched, kSchedCount)) ||
         (rc = dalloc(&e->part_force, (size_t)std::max(fb, ub) * kForcePartials)) ||
         (rc = dalloc(&e->part_bbox, (size_t)std::max(fb, ub) * kBBoxPartials)) ||
@@ -545,6 +548,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->count);
     dfree(e->cstart);
     dfree(e->tile_start);
+    dfree(e->tile_range);
     dfree(e->ctx);
     dfree(e->dsched);
     dfree(e->part_force);
@@ -569,6 +573,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->s_count);
     dfree(e->s_cstart);
     dfree(e->s_tile);
+    dfree(e->s_tile_range);
     dfree(e->s_counts);
     dfree(e->s_offsets);
     dfree(e->s_total);
@@ -958,6 +963,7 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
         dfree(e->s_count);
         dfree(e->s_cstart);
         dfree(e->s_tile);
+        dfree(e->s_tile_range);
         dfree(e->s_counts);
         dfree(e->s_offsets);
         dfree(e->s_total);
@@ -969,7 +975,7 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
             (rc = dalloc(&e->s_sidx, cap)) || (rc = dalloc(&e->s_scell, cap)) || (rc = dalloc(&e->s_cell_of, cap)) ||
             (rc = dalloc(&e->s_slot, cap)) || (rc = dalloc(&e->s_tmp, cap)) || (rc = dalloc(&e->s_count, ncm + kScanPad)) ||
             (rc = dalloc(&e->s_cstart, ncm + kScanPad)) || (rc = dalloc(&e->s_counts, cap)) ||
-            (rc = dalloc(&e->s_tile, ncm + 2)) ||
+            (rc = dalloc(&e->s_tile, ncm + 2)) || (rc = dalloc(&e->s_tile_range, (size_t)force_blocks(cap) + ncm + 2)) ||
             (rc = dalloc(&e->s_offsets, cap)) || (rc = dalloc(&e->s_total, 1)) || (rc = dalloc(&e->s_ctx, 1)))
             return rc;
         HIPCHK(hipMemsetAsync(e->s_count, 0, (ncm + kScanPad) * sizeof(int), e->stream));
@@ -997,7 +1003,7 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
     sa.pos1 = const_cast<float4*>(src);
     launch_prime(e->stream, e->s_ctx, sa, (float)distance, e->s_ncell_max);
     launch_cell_count(e->stream, e->s_ctx, src, src, ni, e->s_cell_of, e->s_slot, e->s_count);
-    launch_cell_scan(e->stream, e->s_ctx, ni, e->s_count, e->s_cstart, e->s_tile);
+    launch_cell_scan(e->stream, e->s_ctx, ni, e->s_count, e->s_cstart, e->s_tile, e->s_tile_range);
     launch_cell_scatter(e->stream, ni, e->s_cell_of, e->s_slot, e->s_cstart, e->s_tmp);
     launch_cell_sort(e->stream, e->s_ctx, src, src, nullptr, ni, e->s_tmp, e->s_cell_of, e->s_cstart, e->s_sidx,
                      e->s_scell, e->s_spos, e->s_sb, 1);
@@ -1097,6 +1103,12 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
     if (option == GCS_OPT_GRAPH_STEPS) {
         if (value < 0 || value > 4096) return fail(GCS_EINVAL, "graph steps must be in [0, 4096]");
         e->graph_steps = (int)value;
+        drop_graph(e);
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_CHUNK_ORDER) {
+        if (value != 0 && value != 1) return fail(GCS_EINVAL, "chunk order must be 0 (contiguous) or 1 (strided)");
+        e->fa.chunk_mode = (int)value;
         drop_graph(e);
         return GCS_OK;
     }

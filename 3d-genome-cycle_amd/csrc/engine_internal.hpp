@@ -83,9 +83,9 @@ struct ForceArgs {
     const int* sidx;
     const int* scell;
     const int* cstart;
-    const int* tile_start;  // [rows + 1] first tile of each cell row (k_cell_scan)
+    const int2* tile_range; // [tiles] sorted-slot range [begin, end) of each k_force tile (k_cell_scan)
     // neighbor soft-core pair field
-    int has_pair, pair_mix, pair_scaled, pad0;
+    int has_pair, pair_mix, pair_scaled, chunk_mode;
     float pa_eps, pa_sig, pb_eps, pb_sig, pair_dist;
     // bonded CSR (particle order)
     int has_bonds;
@@ -145,7 +145,7 @@ __host__ __device__ inline void philox4x32_10(unsigned c[4], unsigned k0, unsign
 void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed, int ncell_max);
 void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n,
                        int* cell_of, int* slot, int* count);
-void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start);
+void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start, int2* tile_range);
 void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* slot, const int* cstart, int* tmp);
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, const float4* kmu,
                       int n, const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell,

@@ -188,7 +188,8 @@ __device__ inline int wave_incl_scan(int v, int lane)
 // running carry; re-zeroes count for the next step.  count/cstart are padded by kScanPad so whole tiles may be
 // touched; entries past ncell are zero by invariant.
 __global__ __launch_bounds__(1024) void k_cell_scan(DevCtx* __restrict__ ctx, int n, int* __restrict__ count,
-                                                    int* __restrict__ cstart, int* __restrict__ tile_start)
+                                                    int* __restrict__ cstart, int* __restrict__ tile_start,
+                                                    int2* __restrict__ tile_range)
 {
     __shared__ int wtot[16];
     __shared__ int tile_total;
@@ -243,7 +244,12 @@ __global__ __launch_bounds__(1024) void k_cell_scan(DevCtx* __restrict__ ctx, in
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int r = base + 4 * tid + q;
-            if (r < nrows) tile_start[r] = run;
+            if (r < nrows) {
+                tile_start[r] = run;
+                const int rb = cstart[r * nx], re = cstart[(r + 1) * nx];
+                for (int k = 0; k < c[q]; ++k)
+                    tile_range[run + k] = make_int2(rb + k * kTile, min(re, rb + (k + 1) * kTile));
+            }
             run += c[q];
         }
         carry += tile_total;
@@ -570,16 +576,30 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
     }
     __builtin_amdgcn_wave_barrier();
     const int total = uniform(s_rowV[16]);
+    const float ahi = pi.w, bhi = bi;
+    // Chunk c of this wave holds candidates v = first(c) + stride * lane, lane < count(c).
+    //   contiguous (chunk_mode 0): the wave's share [wlo, whi) in runs of 64
+    //   strided    (chunk_mode 1): chunk g of G = ceil(total / 64) takes v = g + G * lane; wave w owns the
+    //   chunks g = w (mod WAVES).  Every chunk then samples all stencil rows, which evens the hit counts
+    //   across lanes (phase 2 runs as long as the lane with the most hits).
+    const bool strided = a.chunk_mode != 0;
+    const int G = (total + kTile - 1) / kTile;
     const int wlo = (int)(((long long)total * wave) / WAVES);
     const int whi = (int)(((long long)total * (wave + 1)) / WAVES);
-    const float ahi = pi.w, bhi = bi;
+    const int nchunk = strided ? (G > wave ? (G - wave + WAVES - 1) / WAVES : 0) : (whi - wlo + kTile - 1) / kTile;
+    const int stride = strided ? G : 1;
+    auto first = [&](int c) { return strided ? wave + c * WAVES : wlo + c * kTile; };
+    auto count = [&](int c) {
+        const int f = first(c);
+        return strided ? min(kTile, (total - f + G - 1) / G) : min(kTile, whi - f);
+    };
 
-    auto fetch = [&](int base, float4& p, float& b, int& jj) {
-        const int v = base + lane;
+    auto fetch = [&](int c, float4& p, float& b, int& jj) {
+        const int v = first(c) + stride * lane;
         p = make_float4(1e18f, 1e18f, 1e18f, 0.f);  // far-away sentinel: never a hit
         b = 0.f;
         jj = -1;
-        if (v < whi) {
+        if (lane < count(c)) {
             int lo = 0;  // last stencil row starting at or before v (rows 9..15 start at `total`)
 #pragma unroll
             for (int step = 8; step > 0; step >>= 1)
@@ -592,17 +612,19 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
     float4 npj;
     float nbj;
     int njj;
-    fetch(wlo, npj, nbj, njj);
-    for (int base = wlo; base < whi; base += kTile) {
-        const int cnt = uniform(min(kTile, whi - base));
+    if (nchunk > 0) fetch(0, npj, nbj, njj);
+    for (int c = 0; c < nchunk; ++c) {
+        const int cnt = uniform(count(c));
         const int cnt8 = (cnt + 7) & ~7;  // sentinel-padded to a multiple of 8
         s_cand[lane] = npj;
         s_candb[lane] = nbj;
         if (MODE == kModeEnergy) s_candj[lane] = njj;
         __builtin_amdgcn_wave_barrier();
-        if (base + kTile < whi) fetch(base + kTile, npj, nbj, njj);  // next chunk in flight
+        if (c + 1 < nchunk) fetch(c + 1, npj, nbj, njj);  // next chunk in flight
 
-        // phase 1: distance filter over the chunk; each lane keeps a 64-bit mask of its hits
+        // phase 1: distance filter over the chunk; each lane keeps a 64-bit mask of its hits.  Within a group
+        // of 8 candidates the mask byte is built as byte = 2 byte + hit (v_cmp + v_addc: 2 VALU per test), so
+        // candidate k0 + u lands on bit k0 + 7 - u (decoded by k = bit ^ 7).
         unsigned mlo = 0u, mhi = 0u;
         for (int k0 = 0; k0 < cnt8; k0 += 8) {
             unsigned byte = 0u;
@@ -612,10 +634,17 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
                 keep_live(pj.w);  // one ds_read_b128 (4 LDS cycles) instead of a ds_read_b96 (8)
                 const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
                 const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                // the self pair contributes exactly zero force (F is proportional to x_i - x_j), so the force
-                // path keeps it (one wasted slot) instead of paying a second compare per candidate
-                const bool in = (MODE == kModeEnergy) ? ((r2 < rc2) && (s_candj[k0 + u] != s)) : (r2 < rc2);
-                byte |= in ? (1u << u) : 0u;
+                if (MODE == kModeEnergy) {
+                    const bool in = (r2 < rc2) && (s_candj[k0 + u] != s);
+                    byte = 2u * byte + (in ? 1u : 0u);
+                } else {
+                    // the self pair contributes exactly zero force (F is proportional to x_i - x_j), so the force
+                    // path keeps it (one wasted slot) instead of paying a second compare per candidate
+                    asm("v_cmp_gt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+                        : "+v"(byte)
+                        : "v"(rc2), "v"(r2)
+                        : "vcc");
+                }
             }
             if (k0 < 32)
                 mlo |= byte << k0;
@@ -634,7 +663,7 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
             for (int u = 0; u < 4; ++u) {  // pop the lowest set bits
                 av[u] = (mlo | mhi) != 0u;
                 const int klo = __ffs(mlo) - 1, khi = __ffs(mhi) + 31;
-                kk[u] = av[u] ? (mlo ? klo : khi) : 0;  // inactive: a valid slot, no NaN
+                kk[u] = av[u] ? ((mlo ? klo : khi) ^ 7) : 0;  // bit -> candidate; inactive: a valid slot, no NaN
                 if (mlo)
                     mlo &= mlo - 1u;
                 else
@@ -692,8 +721,6 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     const int ntiles = ctx->ntiles;
-    const int nrows = ctx->grid.n[1] * ctx->grid.n[2];
-    const int nx = ctx->grid.n[0];
     if (threadIdx.x == 0) {
         for (int k = 0; k < kForcePartials; ++k) s_pr[k] = 0.f;
         for (int k = 0; k < 3; ++k) {
@@ -704,20 +731,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
     }
 
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        int s_begin, s_end;
-        {  // the row holding this tile: last row whose tile prefix is <= tile
-            int lo = 0, hi = nrows - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (a.tile_start[mid] <= tile)
-                    lo = mid;
-                else
-                    hi = mid - 1;
-            }
-            const int row_begin = a.cstart[lo * nx], row_end = a.cstart[(lo + 1) * nx];
-            s_begin = uniform(row_begin + (tile - a.tile_start[lo]) * kTile);
-            s_end = uniform(min(row_end, s_begin + kTile));
-        }
+        const int2 tr = a.tile_range[tile];
+        const int s_begin = uniform(tr.x), s_end = uniform(tr.y);
         const int s = s_begin + lane;
         const bool valid = s < s_end;
         const int sl = valid ? s : s_end - 1;
@@ -1036,9 +1051,9 @@ void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, con
     hipLaunchKernelGGL(k_cell_count, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, n, cell_of, slot, count);
 }
 
-void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start)
+void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start, int2* tile_range)
 {
-    hipLaunchKernelGGL(k_cell_scan, dim3(1), dim3(1024), 0, s, ctx, n, count, cstart, tile_start);
+    hipLaunchKernelGGL(k_cell_scan, dim3(1), dim3(1024), 0, s, ctx, n, count, cstart, tile_start, tile_range);
 }
 
 void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* slot, const int* cstart, int* tmp)

@@ -150,10 +150,15 @@ def test_graph_and_eager_bitwise_identical(c1_design, interphase_cfg):
 
 
 @pytest.mark.parametrize("waves", [1, 2, 4, 8])
-def test_waves_per_tile_equivalent(c1_design, interphase_cfg, waves):
+@pytest.mark.parametrize("order", [0, 1])
+def test_waves_per_tile_equivalent(c1_design, interphase_cfg, waves, order):
     e, o = both(c1_design, interphase_cfg)
     e.set_option(A.OPT_WAVES_PER_TILE, waves)
+    e.set_option(A.OPT_CHUNK_ORDER, order)
     assert_forces_close(e.compute_forces(), o.compute_forces())
+    te, pe = e.compute_energy()
+    to, po = o.compute_energy()
+    assert te == pytest.approx(to, rel=1e-5)
 
 
 def test_chunked_runs_equal_one_run(c1_design, interphase_cfg):
