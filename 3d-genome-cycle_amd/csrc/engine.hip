@@ -129,11 +129,13 @@ struct gcs_engine {
     // options / graph cache
     int graph_steps = 32;
     int waves = 4;
+    bool fused = true;
     hipGraphExec_t gexec = nullptr;
     hipGraph_t graph = nullptr;
     int g_steps = 0, g_waves = 0, g_version = -1, g_spacestep = -1;
     gcs_bd_config g_cfg{};
     int g_sched_flags = -1;
+    int g_fused = -1, g_chunk = -1;
 };
 
 namespace {
@@ -376,27 +378,59 @@ void fill_state_args(gcs_engine* e)
     a.force_out = e->force_out;
     a.noise = e->noise;
     a.noise_steps = e->noise_steps;
+    a.cell_of = e->cell_of;
+    a.slot = e->slot;
+    a.count = e->count;
+    a.cstart_w = e->cstart;
+    a.tile_start_w = e->tile_start;
+    a.tile_range_w = e->tile_range;
+    a.sched = e->dsched;
+    a.ncell_max = e->ncell_max;
+    a.apply_sched = e->sched_flags != 0;
 }
 
-void enqueue_cells(gcs_engine* e)
+// bin the current positions into ctx->grid: per-cell counts + slots, scan, tile table
+void enqueue_bin(gcs_engine* e)
 {
     const int n = e->n;
     launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count);
     launch_cell_scan(e->stream, e->ctx, n, e->count, e->cstart, e->tile_start, e->tile_range);
+}
+
+// scatter into the cells and order each cell by particle index: the cell-sorted copies the pair loop reads
+void enqueue_sort(gcs_engine* e)
+{
+    const int n = e->n;
     launch_cell_scatter(e->stream, n, e->cell_of, e->slot, e->cstart, e->tmp);
     launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, n, e->tmp, e->cell_of, e->cstart, e->sidx,
                      e->scell, e->spos, e->sb, e->fa.has_pair ? e->fa.pair_mix : 1);
 }
 
+void enqueue_cells(gcs_engine* e)
+{
+    enqueue_bin(e);
+    enqueue_sort(e);
+}
+
+bool fused_path(const gcs_engine* e, bool spacestep) { return e->fused && !spacestep; }
+
+// One BD step.  Fused (fixed timestep): scatter, sort, force (which bins the new positions and whose last block
+// runs the tail + the cell scan); begin_run binned the first positions.  Otherwise (spacestep, or fusion off):
+// count, scan, scatter, sort, force, [adapt, update], tail.
 void enqueue_step(gcs_engine* e, bool spacestep, float spacestep_v, float timestep)
 {
     const int fb = force_grid(e->n);
+    if (fused_path(e, spacestep)) {
+        enqueue_sort(e);
+        launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, true);
+        return;
+    }
     enqueue_cells(e);
     if (!spacestep) {
-        launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa);
+        launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, false);
         launch_tail(e->stream, e->ctx, e->fa, fb, fb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
     } else {
-        launch_force(e->stream, kModeForce, e->waves, e->ctx, e->fa);
+        launch_force(e->stream, kModeForce, e->waves, e->ctx, e->fa, false);
         launch_adapt(e->stream, e->ctx, e->fa, fb, spacestep_v, timestep);
         launch_update(e->stream, e->ctx, e->fa);
         launch_tail(e->stream, e->ctx, e->fa, fb, update_blocks(e->n), 1, e->sched_flags != 0, e->ncell_max, e->dsched);
@@ -450,7 +484,8 @@ int begin_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
     if ((rc = set_ctx_field(e, offsetof(DevCtx, step), &st, sizeof(st)))) return rc;
     double dt = cfg->timestep;
     if ((rc = set_ctx_field(e, offsetof(DevCtx, dt_used), &dt, sizeof(dt)))) return rc;
-    launch_prime(e->stream, e->ctx, a, 0.f, e->ncell_max);
+    launch_prime(e->stream, e->ctx, a, 0.f, e->ncell_max, e->dsched);
+    if (fused_path(e, cfg->spacestep > 0)) enqueue_bin(e);
     HIPCHK(hipGetLastError());
     return GCS_OK;
 }
@@ -816,7 +851,7 @@ int gcs_engine_apply_schedule(gcs_engine* e, int64_t step)
     if (rc) return rc;
     long long st = step;
     if ((rc = set_ctx_field(e, offsetof(DevCtx, step), &st, sizeof(st)))) return rc;
-    launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max);
+    launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max, e->dsched);
     launch_tail(e->stream, e->ctx, e->fa, 0, 0, 0, 1, e->ncell_max, e->dsched);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->stream));
@@ -862,6 +897,7 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
     int64_t done = 0;
     if (G > 0 && steps >= G) {
         const bool same = e->gexec && e->g_steps == G && e->g_waves == e->waves && e->g_version == e->topo_version &&
+                          e->g_fused == (int)e->fused && e->g_chunk == e->fa.chunk_mode &&
                           e->g_spacestep == (int)spacestep && e->g_sched_flags == e->sched_flags &&
                           std::memcmp(&e->g_cfg, cfg, sizeof(*cfg)) == 0;
         if (!same) {
@@ -875,6 +911,8 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
             e->g_version = e->topo_version;
             e->g_spacestep = (int)spacestep;
             e->g_sched_flags = e->sched_flags;
+            e->g_fused = (int)e->fused;
+            e->g_chunk = e->fa.chunk_mode;
             e->g_cfg = *cfg;
         }
         for (; done + G <= steps; done += G) HIPCHK(hipGraphLaunch(e->gexec, e->stream));
@@ -900,9 +938,9 @@ int gcs_engine_compute_forces(gcs_engine* e, double* forces, int64_t n)
     if (n != e->n) return fail(GCS_EINVAL, "force array size does not match the particle count");
     int rc = prepare(e);
     if (rc) return rc;
-    launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max);
+    launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max, e->dsched);
     enqueue_cells(e);
-    launch_force(e->stream, kModeForce, e->waves, e->ctx, e->fa);
+    launch_force(e->stream, kModeForce, e->waves, e->ctx, e->fa, false);
     launch_tail(e->stream, e->ctx, e->fa, force_grid(e->n), 0, 0, 0, e->ncell_max, e->dsched);
     HIPCHK(hipGetLastError());
     std::vector<float4> h(n);
@@ -921,9 +959,9 @@ int gcs_engine_compute_energy(gcs_engine* e, double* total, double* per_kind)
     if (!e || !total) return fail(GCS_EINVAL, "null argument");
     int rc = prepare(e);
     if (rc) return rc;
-    launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max);
+    launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max, e->dsched);
     enqueue_cells(e);
-    launch_force(e->stream, kModeEnergy, e->waves, e->ctx, e->fa);
+    launch_force(e->stream, kModeEnergy, e->waves, e->ctx, e->fa, false);
     HIPCHK(hipGetLastError());
     const int fb = force_grid(e->n);
     std::vector<double> h((size_t)fb * kEnergyKinds);
@@ -1001,7 +1039,7 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
     sa.n = ni;
     sa.pos0 = const_cast<float4*>(src);
     sa.pos1 = const_cast<float4*>(src);
-    launch_prime(e->stream, e->s_ctx, sa, (float)distance, e->s_ncell_max);
+    launch_prime(e->stream, e->s_ctx, sa, (float)distance, e->s_ncell_max, nullptr);
     launch_cell_count(e->stream, e->s_ctx, src, src, ni, e->s_cell_of, e->s_slot, e->s_count);
     launch_cell_scan(e->stream, e->s_ctx, ni, e->s_count, e->s_cstart, e->s_tile, e->s_tile_range);
     launch_cell_scatter(e->stream, ni, e->s_cell_of, e->s_slot, e->s_cstart, e->s_tmp);
@@ -1059,13 +1097,17 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     for (auto& x : ev) HIPCHK(hipEventCreate(&x));
     const int fb = force_grid(e->n);
     HIPCHK(hipEventRecord(ev[0], e->stream));
+    const bool fused = fused_path(e, false);
     for (int64_t k = 0; k < steps; ++k) {
         HIPCHK(hipEventRecord(ev[1 + 4 * k], e->stream));
-        enqueue_cells(e);
+        if (fused)
+            enqueue_sort(e);
+        else
+            enqueue_cells(e);
         HIPCHK(hipEventRecord(ev[2 + 4 * k], e->stream));
-        launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa);
+        launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, fused);
         HIPCHK(hipEventRecord(ev[3 + 4 * k], e->stream));
-        launch_tail(e->stream, e->ctx, e->fa, fb, fb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
+        if (!fused) launch_tail(e->stream, e->ctx, e->fa, fb, fb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
         HIPCHK(hipEventRecord(ev[4 + 4 * k], e->stream));
     }
     HIPCHK(hipEventRecord(ev[ev.size() - 1], e->stream));
@@ -1103,6 +1145,11 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
     if (option == GCS_OPT_GRAPH_STEPS) {
         if (value < 0 || value > 4096) return fail(GCS_EINVAL, "graph steps must be in [0, 4096]");
         e->graph_steps = (int)value;
+        drop_graph(e);
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_FUSED_STEP) {
+        e->fused = value != 0;
         drop_graph(e);
         return GCS_OK;
     }

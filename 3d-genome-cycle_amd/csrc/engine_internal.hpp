@@ -46,7 +46,10 @@ struct DevCtx {
     int parity;            // index of the current position buffer
     int ntiles;            // k_force tiles of the current cell list (k_cell_scan)
     float bbox_lo[3], bbox_hi[3];
-    Grid grid;
+    Grid grid;             // bins the current positions (the next force evaluation's stencil)
+    Grid grid_next;        // bins the positions the next step produces (fused path)
+    unsigned ticket;       // arrival counter of the fused force kernel's blocks (0 between launches)
+    int pad1;
 };
 
 enum BondType : int { kSemispring = 0, kHarmonic = 1, kSpring = 2, kSoftwell = 3 };
@@ -117,6 +120,16 @@ struct ForceArgs {
     float* part_bbox;     // [blocks][kBBoxPartials]
     double* part_energy;  // [blocks][kEnergyKinds]
     float4* force_out;    // [N] (kModeForce)
+    // fused step (kModeStep, FUSED): binning of the new positions + last-block tail and cell scan
+    int* cell_of;
+    int* slot;
+    int* count;
+    int* cstart_w;
+    int* tile_start_w;
+    int2* tile_range_w;
+    const double* sched;
+    int ncell_max;
+    int apply_sched;
 };
 
 // ---- Philox4x32-10 + Box-Muller: the production noise stream (identical on host for the oracle) ----
@@ -142,7 +155,7 @@ __host__ __device__ inline void philox4x32_10(unsigned c[4], unsigned k0, unsign
 }
 
 // launch wrappers (kernels.hip)
-void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed, int ncell_max);
+void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed, int ncell_max, const double* sched);
 void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n,
                        int* cell_of, int* slot, int* count);
 void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start, int2* tile_range);
@@ -150,7 +163,7 @@ void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* sl
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, const float4* kmu,
                       int n, const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell,
                       float4* spos, float* sb, int pair_mix);
-void launch_force(hipStream_t s, int mode, int waves, const DevCtx* ctx, const ForceArgs& a);
+void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceArgs& a, bool fused);
 void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a);
 void launch_adapt(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force_blocks, float spacestep, float timestep);
 void launch_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force_blocks, int bbox_blocks, int advance,

@@ -72,20 +72,20 @@ __device__ inline int cell_index(const Grid& g, float x, float y, float z)
     return cx + g.n[0] * (cy + g.n[1] * cz);
 }
 
-// Cell grid over the current bounding box; cell edge >= rc (1e-4 margin) so any pair closer than rc lies
-// in the same or an adjacent cell (particles outside the box are clamped into the border cells, which
-// keeps that property because clamping never increases a per-axis cell distance).
-__device__ void compute_grid(DevCtx* ctx, float rc, int ncell_max, int fx)
+// Cell grid over the box [lo, hi]; cell edge >= rc (1e-4 margin; x edge rc / fx) so any pair closer than rc lies
+// in the same or an adjacent cell (+-fx in x).  Particles outside the box are clamped into the border cells,
+// which keeps that property because clamping never increases a per-axis cell distance.
+__device__ Grid make_grid(const float* lo, const float* hi, float rc, int ncell_max, int fx)
 {
     Grid g;
     int n[3];
     float ext[3];
     long long total = 1;
     for (int k = 0; k < 3; ++k) {
-        float e = ctx->bbox_hi[k] - ctx->bbox_lo[k];
+        float e = hi[k] - lo[k];
         if (!(e > 0.f) || !(e < 3.0e38f)) e = 0.f;
         ext[k] = e;
-        const float edge = (k == 0) ? rc / (float)fx : rc;  // x cells are rc / fx wide
+        const float edge = (k == 0) ? rc / (float)fx : rc;
         float q = (rc > 0.f) ? e / (edge * 1.0001f) : 0.f;
         int m = (q >= 1.f) ? (int)fminf(q, 1024.f) : 1;
         n[k] = m;
@@ -100,7 +100,7 @@ __device__ void compute_grid(DevCtx* ctx, float rc, int ncell_max, int fx)
         total *= n[kk];
     }
     for (int k = 0; k < 3; ++k) {
-        g.lo[k] = ctx->bbox_lo[k];
+        g.lo[k] = (ext[k] > 0.f) ? lo[k] : 0.f;
         g.n[k] = n[k];
         g.inv[k] = ext[k] > 0.f ? (float)n[k] / ext[k] : 0.f;
     }
@@ -108,7 +108,33 @@ __device__ void compute_grid(DevCtx* ctx, float rc, int ncell_max, int fx)
     g.fx = (n[0] > 1) ? fx : 1;
     g.rc = rc;
     g.rc2 = rc * rc;
-    ctx->grid = g;
+    return g;
+}
+
+__device__ void compute_grid(DevCtx* ctx, float rc, int ncell_max, int fx)
+{
+    ctx->grid = make_grid(ctx->bbox_lo, ctx->bbox_hi, rc, ncell_max, fx);
+}
+
+// The grid that bins the positions produced by the NEXT step: the current bbox padded by 2 % + 0.01 (particles
+// move far less per step; any that leave are clamped, which is still exact) and the pair cutoff that step
+// will use, i.e. with the core scale the schedule sets after step `step` (closed form of update_core_scale).
+__device__ Grid next_grid(const DevCtx* ctx, const ForceArgs& a, const double* sched, long long step, int ncell_max)
+{
+    float lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) {
+        const float pad = 0.02f * fmaxf(ctx->bbox_hi[k] - ctx->bbox_lo[k], 0.f) + 0.01f;
+        lo[k] = ctx->bbox_lo[k] - pad;
+        hi[k] = ctx->bbox_hi[k] + pad;
+    }
+    double cs = ctx->cs;
+    const int flags = (int)sched[kSchedFlags];
+    if (flags & 2) {
+        const double t = (flags & 1) ? (double)step * sched[kSchedDt] : ctx->time;
+        cs = 1.0 - (1.0 - sched[kSchedCs0]) * exp(-(t / sched[kSchedCsTau]));
+    }
+    const float rc = a.has_pair ? a.pair_dist * (a.pair_scaled ? (float)fmax(cs, ctx->cs) : 1.f) : 1.f;
+    return make_grid(lo, hi, rc, ncell_max, kPairFx);
 }
 
 __device__ inline float pair_cutoff(const ForceArgs& a, double cs)
@@ -120,7 +146,8 @@ __device__ inline float pair_cutoff(const ForceArgs& a, double cs)
 // ----------------------------------------------------------------------------------------------------
 // cell list
 
-__global__ __launch_bounds__(1024) void k_prime(DevCtx* ctx, ForceArgs a, float rc_fixed, int ncell_max)
+__global__ __launch_bounds__(1024) void k_prime(DevCtx* ctx, ForceArgs a, float rc_fixed, int ncell_max,
+                                                const double* __restrict__ sched)
 {
     __shared__ float red[6][16];
     const float4* pos = ctx->parity ? a.pos1 : a.pos0;
@@ -156,6 +183,8 @@ __global__ __launch_bounds__(1024) void k_prime(DevCtx* ctx, ForceArgs a, float 
         }
         float rc = rc_fixed > 0.f ? rc_fixed : pair_cutoff(a, ctx->cs);
         compute_grid(ctx, rc, ncell_max, rc_fixed > 0.f ? 1 : kPairFx);
+        if (sched) ctx->grid_next = next_grid(ctx, a, sched, ctx->step + 1, ncell_max);
+        ctx->ticket = 0u;
     }
 }
 
@@ -184,19 +213,20 @@ __device__ inline int wave_incl_scan(int v, int lane)
     return v;
 }
 
-// Exclusive scan count -> cstart over the grid's cells in coalesced 4096-cell tiles (int4 per thread) with a
-// running carry; re-zeroes count for the next step.  count/cstart are padded by kScanPad so whole tiles may be
-// touched; entries past ncell are zero by invariant.
-__global__ __launch_bounds__(1024) void k_cell_scan(DevCtx* __restrict__ ctx, int n, int* __restrict__ count,
-                                                    int* __restrict__ cstart, int* __restrict__ tile_start,
-                                                    int2* __restrict__ tile_range)
+// Exclusive scan count -> cstart over the grid's cells in coalesced tiles of 4 cells per thread (int4) with a
+// running carry, re-zeroing count for the next step; then the per-row tile table of k_force (a tile is <= 64
+// consecutive sorted particles of ONE row of cells).  count/cstart are padded by kScanPad so whole tiles may be
+// touched; entries past ncell are zero by invariant.  Any block size that is a multiple of 64 (<= 1024).
+__device__ void scan_cells_body(DevCtx* __restrict__ ctx, int n, int* __restrict__ count, int* __restrict__ cstart,
+                                int* __restrict__ tile_start, int2* __restrict__ tile_range)
 {
     __shared__ int wtot[16];
     __shared__ int tile_total;
     const int nc = ctx->grid.ncell;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const int span = 4 * blockDim.x;
     int carry = 0;
-    for (int base = 0; base < nc; base += 4096) {
+    for (int base = 0; base < nc; base += span) {
         const int i0 = base + 4 * tid;
         const int4 c = *reinterpret_cast<const int4*>(count + i0);
         const int sum = c.x + c.y + c.z + c.w;
@@ -204,10 +234,10 @@ __global__ __launch_bounds__(1024) void k_cell_scan(DevCtx* __restrict__ ctx, in
         if (lane == 63) wtot[wave] = incl;
         __syncthreads();
         if (wave == 0) {
-            const int w = lane < 16 ? wtot[lane] : 0;
+            const int w = lane < nw ? wtot[lane] : 0;
             const int wi = wave_incl_scan(w, lane);
-            if (lane < 16) wtot[lane] = wi - w;
-            if (lane == 15) tile_total = wi;
+            if (lane < nw) wtot[lane] = wi - w;
+            if (lane == nw - 1) tile_total = wi;
         }
         __syncthreads();
         const int run = carry + wtot[wave] + incl - sum;
@@ -218,10 +248,9 @@ __global__ __launch_bounds__(1024) void k_cell_scan(DevCtx* __restrict__ ctx, in
     }
     if (tid == 0) cstart[nc] = n;
     __syncthreads();
-    // per-row tile prefix for k_force: row r = (y, z) holds ceil(particles / 64) tiles
     const int nx = ctx->grid.n[0], nrows = ctx->grid.n[1] * ctx->grid.n[2];
     carry = 0;
-    for (int base = 0; base < nrows; base += 4096) {
+    for (int base = 0; base < nrows; base += span) {
         int c[4];
         int sum = 0;
 #pragma unroll
@@ -234,10 +263,10 @@ __global__ __launch_bounds__(1024) void k_cell_scan(DevCtx* __restrict__ ctx, in
         if (lane == 63) wtot[wave] = incl;
         __syncthreads();
         if (wave == 0) {
-            const int w = lane < 16 ? wtot[lane] : 0;
+            const int w = lane < nw ? wtot[lane] : 0;
             const int wi = wave_incl_scan(w, lane);
-            if (lane < 16) wtot[lane] = wi - w;
-            if (lane == 15) tile_total = wi;
+            if (lane < nw) wtot[lane] = wi - w;
+            if (lane == nw - 1) tile_total = wi;
         }
         __syncthreads();
         int run = carry + wtot[wave] + incl - sum;
@@ -259,6 +288,13 @@ __global__ __launch_bounds__(1024) void k_cell_scan(DevCtx* __restrict__ ctx, in
         tile_start[nrows] = carry;
         ctx->ntiles = carry;
     }
+}
+
+__global__ __launch_bounds__(1024) void k_cell_scan(DevCtx* __restrict__ ctx, int n, int* __restrict__ count,
+                                                    int* __restrict__ cstart, int* __restrict__ tile_start,
+                                                    int2* __restrict__ tile_range)
+{
+    scan_cells_body(ctx, n, count, cstart, tile_start, tile_range);
 }
 
 __global__ __launch_bounds__(256) void k_cell_scatter(int n, const int* __restrict__ cell_of, const int* __restrict__ slot,
@@ -707,8 +743,14 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
 // (k_cell_scan builds the per-row tile prefix).  The WAVES waves split the tile's candidates; wave 0 then
 // adds the particle-local terms and integrates.  Per-block partials (reactions, bbox, drift, neighbours,
 // energies) are reduced in a fixed order by k_tail / the host: no atomics, bitwise reproducible.
-template <int MODE, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__ ctx, ForceArgs a)
+__device__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance, int apply_sched,
+                          int ncell_max, const double* __restrict__ sched, bool fused);
+
+// FUSED (kModeStep only): the new positions are also binned into ctx->grid_next (count atomics), and the last
+// block to finish (arrival ticket, agent-scope release/acquire: cdna_hip_programming.md G16) runs the schedule
+// tail and the cell scan for the next step, so a step is three launches: scatter, sort, force.
+template <int MODE, int WAVES, bool FUSED>
+__global__ __launch_bounds__(64 * WAVES) void k_force(DevCtx* __restrict__ ctx, ForceArgs a)
 {
     __shared__ float red[WAVES > 1 ? WAVES : 1][4][64];
     __shared__ int s_rowV[WAVES][17];
@@ -803,6 +845,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
                     const float nyp = pi.y + mdt * fy + amp * n1;
                     const float nzp = pi.z + mdt * fz + amp * n2;
                     if (valid) posn[i] = make_float4(nxp, nyp, nzp, 0.f);
+                    if (FUSED && valid) {
+                        const int c = cell_index(ctx->grid_next, nxp, nyp, nzp);
+                        a.cell_of[i] = c;
+                        a.slot[i] = atomicAdd(&a.count[c], 1);
+                    }
                     const float big = 3.0e38f;
                     const float l0 = wave_min(valid ? nxp : big), l1 = wave_min(valid ? nyp : big),
                                 l2 = wave_min(valid ? nzp : big);
@@ -831,6 +878,28 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(const DevCtx* __restrict__
             if (MODE == kModeStep)
                 for (int k = 0; k < kBBoxPartials; ++k)
                     a.part_bbox[blockIdx.x * kBBoxPartials + k] = s_pr[kForcePartials + k];
+        }
+    }
+    if (FUSED) {
+        __shared__ int s_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains (partials, cells, slots)
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned prev = atomicAdd(&ctx->ticket, 1u);
+            s_last = (prev == gridDim.x - 1) ? 1 : 0;
+            if (s_last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        __syncthreads();
+        if (s_last) {
+            const int nb = gridDim.x;
+            tail_body(ctx, a, nb, nb, 1, a.apply_sched, a.ncell_max, a.sched, true);
+            scan_cells_body(ctx, a.n, a.count, a.cstart_w, a.tile_start_w, a.tile_range_w);
+            if (threadIdx.x == 0) ctx->ticket = 0u;
         }
     }
 }
@@ -893,77 +962,96 @@ __global__ __launch_bounds__(256) void k_adapt(DevCtx* ctx, ForceArgs a, int blo
     }
 }
 
-// fixed-order reduction of the per-block partials + the device-resident interphase schedule
-__global__ __launch_bounds__(256) void k_tail(DevCtx* ctx, ForceArgs a, int fblocks, int bblocks, int advance,
-                                              int apply_sched, int ncell_max, const double* __restrict__ sched)
+__device__ inline double wave_max_d(double v)
 {
-    __shared__ double sred[8][256];
-    __shared__ float bred[6][256];
-    const int tid = threadIdx.x;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+
+// Fixed-order reduction of the per-block partials (per thread strided, wave butterflies, waves in index order:
+// bitwise reproducible) + the device-resident interphase schedule + the next cell grid.  Any block size that
+// is a multiple of 64.  fused: the step's force kernel already binned the new positions with grid_next, which
+// becomes the current grid, and the grid for the following step is prepared.
+__device__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance, int apply_sched,
+                          int ncell_max, const double* __restrict__ sched, bool fused)
+{
+    __shared__ double s_red[16][8];
+    __shared__ float s_bb[16][6];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int b = tid; b < fblocks; b += 256)
+    for (int b = tid; b < fblocks; b += blockDim.x)
         for (int k = 0; k < 8; ++k) {
-            const float v = a.part_force[b * kForcePartials + k];
-            if (k == 6)
-                acc[6] = fmax(acc[6], (double)v);
-            else
-                acc[k] += (double)v;
+            const double v = a.part_force[b * kForcePartials + k];
+            acc[k] = (k == 6) ? fmax(acc[k], v) : acc[k] + v;
         }
     float bb[6] = {3.0e38f, 3.0e38f, 3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
-    for (int b = tid; b < bblocks; b += 256)
+    for (int b = tid; b < bblocks; b += blockDim.x)
         for (int k = 0; k < 6; ++k) {
             const float v = a.part_bbox[b * kBBoxPartials + k];
             bb[k] = (k < 3) ? fminf(bb[k], v) : fmaxf(bb[k], v);
         }
-    for (int k = 0; k < 8; ++k) sred[k][tid] = acc[k];
-    for (int k = 0; k < 6; ++k) bred[k][tid] = bb[k];
+    for (int k = 0; k < 8; ++k) acc[k] = (k == 6) ? wave_max_d(acc[k]) : wave_sum_d(acc[k]);
+    for (int k = 0; k < 6; ++k) bb[k] = (k < 3) ? wave_min(bb[k]) : wave_max(bb[k]);
+    if (lane == 0) {
+        for (int k = 0; k < 8; ++k) s_red[wave][k] = acc[k];
+        for (int k = 0; k < 6; ++k) s_bb[wave][k] = bb[k];
+    }
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if (tid < w) {
-            for (int k = 0; k < 8; ++k)
-                sred[k][tid] = (k == 6) ? fmax(sred[k][tid], sred[k][tid + w]) : sred[k][tid] + sred[k][tid + w];
-            for (int k = 0; k < 6; ++k)
-                bred[k][tid] = (k < 3) ? fminf(bred[k][tid], bred[k][tid + w]) : fmaxf(bred[k][tid], bred[k][tid + w]);
+    if (tid == 0) {
+        for (int w = 1; w < nw; ++w) {
+            for (int k = 0; k < 8; ++k) acc[k] = (k == 6) ? fmax(acc[k], s_red[w][k]) : acc[k] + s_red[w][k];
+            for (int k = 0; k < 6; ++k) bb[k] = (k < 3) ? fminf(bb[k], s_bb[w][k]) : fmaxf(bb[k], s_bb[w][k]);
         }
-        __syncthreads();
-    }
-    if (tid != 0) return;
-    if (fblocks > 0) {
-        for (int k = 0; k < 3; ++k) {
-            ctx->react_in[k] = sred[k][0];
-            ctx->react_out[k] = sred[3 + k][0];
-        }
-        ctx->max_drift = sred[6][0];
-        ctx->neighbors = sred[7][0] / (double)a.n;
-    }
-    if (bblocks > 0)
-        for (int k = 0; k < 3; ++k) {
-            ctx->bbox_lo[k] = bred[k][0];
-            ctx->bbox_hi[k] = bred[3 + k][0];
-        }
-    if (advance) {
-        ctx->step += 1;
-        ctx->parity ^= 1;
-        if (a.noise_mode == GCS_NOISE_INJECTED) ctx->noise_cursor += 1;
-    }
-    if (apply_sched) {
-        // stage_interphase/simulation_driver_interphase.cpp:17 (time), :67-76 (scales), :79-90 (wall)
-        const int flags = (int)sched[kSchedFlags];
-        const double dt = sched[kSchedDt];
-        if (flags & 1) ctx->time = (double)ctx->step * dt;
-        if (flags & 2) {
-            ctx->cs = 1.0 - (1.0 - sched[kSchedCs0]) * exp(-(ctx->time / sched[kSchedCsTau]));
-            ctx->bs = 1.0 - (1.0 - sched[kSchedBs0]) * exp(-(ctx->time / sched[kSchedBsTau]));
-        }
-        if (flags & 4)
+        if (fblocks > 0) {
             for (int k = 0; k < 3; ++k) {
-                double net = 0.0;
-                net += ctx->react_in[k] + ctx->react_out[k];
-                net -= sched[kSchedK0 + k] * ctx->wall[k];
-                ctx->wall[k] += dt * sched[kSchedMuW] * net;
+                ctx->react_in[k] = acc[k];
+                ctx->react_out[k] = acc[3 + k];
             }
+            ctx->max_drift = acc[6];
+            ctx->neighbors = acc[7] / (double)a.n;
+        }
+        if (bblocks > 0)
+            for (int k = 0; k < 3; ++k) {
+                ctx->bbox_lo[k] = bb[k];
+                ctx->bbox_hi[k] = bb[3 + k];
+            }
+        if (advance) {
+            ctx->step += 1;
+            ctx->parity ^= 1;
+            if (a.noise_mode == GCS_NOISE_INJECTED) ctx->noise_cursor += 1;
+        }
+        if (apply_sched) {
+            // stage_interphase/simulation_driver_interphase.cpp:17 (time), :67-76 (scales), :79-90 (wall)
+            const int flags = (int)sched[kSchedFlags];
+            const double dt = sched[kSchedDt];
+            if (flags & 1) ctx->time = (double)ctx->step * dt;
+            if (flags & 2) {
+                ctx->cs = 1.0 - (1.0 - sched[kSchedCs0]) * exp(-(ctx->time / sched[kSchedCsTau]));
+                ctx->bs = 1.0 - (1.0 - sched[kSchedBs0]) * exp(-(ctx->time / sched[kSchedBsTau]));
+            }
+            if (flags & 4)
+                for (int k = 0; k < 3; ++k) {
+                    double net = 0.0;
+                    net += ctx->react_in[k] + ctx->react_out[k];
+                    net -= sched[kSchedK0 + k] * ctx->wall[k];
+                    ctx->wall[k] += dt * sched[kSchedMuW] * net;
+                }
+        }
+        if (fused) {
+            ctx->grid = ctx->grid_next;
+            ctx->grid_next = next_grid(ctx, a, sched, ctx->step + 1, ncell_max);
+        } else {
+            compute_grid(ctx, pair_cutoff(a, ctx->cs), ncell_max, kPairFx);
+        }
     }
-    compute_grid(ctx, pair_cutoff(a, ctx->cs), ncell_max, kPairFx);
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_tail(DevCtx* ctx, ForceArgs a, int fblocks, int bblocks, int advance,
+                                              int apply_sched, int ncell_max, const double* __restrict__ sched)
+{
+    tail_body(ctx, a, fblocks, bblocks, advance, apply_sched, ncell_max, sched, false);
 }
 
 // ----------------------------------------------------------------------------------------------------
@@ -1040,9 +1128,9 @@ __global__ __launch_bounds__(1024) void k_scan_small(const int* __restrict__ in,
 // ----------------------------------------------------------------------------------------------------
 // launch wrappers
 
-void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed, int ncell_max)
+void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed, int ncell_max, const double* sched)
 {
-    hipLaunchKernelGGL(k_prime, dim3(1), dim3(1024), 0, s, ctx, a, rc_fixed, ncell_max);
+    hipLaunchKernelGGL(k_prime, dim3(1), dim3(1024), 0, s, ctx, a, rc_fixed, ncell_max, sched);
 }
 
 void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n, int* cell_of,
@@ -1069,26 +1157,30 @@ void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, cons
                        cstart, sidx, scell, spos, sb, pair_mix);
 }
 
-template <int MODE>
-static void launch_force_mode(hipStream_t s, int waves, const DevCtx* ctx, const ForceArgs& a)
+template <int MODE, bool FUSED>
+static void launch_force_mode(hipStream_t s, int waves, DevCtx* ctx, const ForceArgs& a)
 {
     const dim3 grid(force_grid(a.n));
     switch (waves) {
-    case 1: hipLaunchKernelGGL((k_force<MODE, 1>), grid, dim3(64), 0, s, ctx, a); break;
-    case 2: hipLaunchKernelGGL((k_force<MODE, 2>), grid, dim3(128), 0, s, ctx, a); break;
-    case 8: hipLaunchKernelGGL((k_force<MODE, 8>), grid, dim3(512), 0, s, ctx, a); break;
-    default: hipLaunchKernelGGL((k_force<MODE, 4>), grid, dim3(256), 0, s, ctx, a); break;
+    case 1: hipLaunchKernelGGL((k_force<MODE, 1, FUSED>), grid, dim3(64), 0, s, ctx, a); break;
+    case 2: hipLaunchKernelGGL((k_force<MODE, 2, FUSED>), grid, dim3(128), 0, s, ctx, a); break;
+    case 8: hipLaunchKernelGGL((k_force<MODE, 8, FUSED>), grid, dim3(512), 0, s, ctx, a); break;
+    default: hipLaunchKernelGGL((k_force<MODE, 4, FUSED>), grid, dim3(256), 0, s, ctx, a); break;
     }
 }
 
-void launch_force(hipStream_t s, int mode, int waves, const DevCtx* ctx, const ForceArgs& a)
+void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceArgs& a, bool fused)
 {
-    if (mode == kModeStep)
-        launch_force_mode<kModeStep>(s, waves, ctx, a);
-    else if (mode == kModeForce)
-        launch_force_mode<kModeForce>(s, waves, ctx, a);
-    else
-        launch_force_mode<kModeEnergy>(s, waves, ctx, a);
+    if (mode == kModeStep) {
+        if (fused)
+            launch_force_mode<kModeStep, true>(s, waves, ctx, a);
+        else
+            launch_force_mode<kModeStep, false>(s, waves, ctx, a);
+    } else if (mode == kModeForce) {
+        launch_force_mode<kModeForce, false>(s, waves, ctx, a);
+    } else {
+        launch_force_mode<kModeEnergy, false>(s, waves, ctx, a);
+    }
 }
 
 void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a)

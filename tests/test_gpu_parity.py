@@ -312,3 +312,36 @@ def test_c2_window_properties(c2_design, interphase_cfg):
     assert c["step"] == 64 and c["time"] == pytest.approx(64 * cfg.timestep)
     disp = np.linalg.norm(x1 - c2_design.positions, axis=1)
     assert disp.mean() < 0.2
+
+
+def test_fused_and_unfused_steps_agree(c1_design, interphase_cfg):
+    """The fused step (binning + tail + scan inside the force kernel) and the 6-launch step give the same
+    trajectory within fp32 tolerance (their cell grids, hence summation orders, differ)."""
+    cfg = interphase_cfg
+    out = []
+    for fused in (0, 1):
+        e, _ = interphase.build_interphase(Engine, c1_design, cfg)
+        e.set_option(A.OPT_FUSED_STEP, fused)
+        e.set_schedule(**interphase.interphase_schedule(cfg))
+        e.apply_schedule(0)
+        e.run(50, seed=21)
+        out.append((e.get_positions(), e.get_context()))
+    assert np.abs(out[0][0] - out[1][0]).max() <= 2e-5
+    assert out[0][1]["step"] == out[1][1]["step"] == 50
+    assert np.allclose(out[0][1]["wall_semiaxes"], out[1][1]["wall_semiaxes"], rtol=1e-9)
+
+
+def test_fused_c2_matches_oracle_forces_after_run(c2_design, interphase_cfg):
+    """After a fused run the engine's cell list must still describe its positions: forces at the final state
+    match the oracle's on the same positions/context."""
+    cfg = interphase_cfg
+    e, _ = interphase.build_interphase(Engine, c2_design, cfg)
+    e.set_schedule(**interphase.interphase_schedule(cfg))
+    e.set_context({"step": 300000, "time": 3.0, "core_scale": 0.9988, "bond_scale": 0.9988,
+                   "wall_semiaxes": [2.0, 2.0, 2.0]})
+    e.run(96, first_step=300000, seed=8)
+    o, _ = interphase.build_interphase(oracle.OracleSystem, c2_design, cfg)
+    o.set_positions(e.get_positions())
+    ctx = e.get_context()
+    o.set_context(ctx)
+    assert_forces_close(e.compute_forces(), o.compute_forces())
