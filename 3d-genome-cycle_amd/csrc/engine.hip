@@ -9,6 +9,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -129,13 +131,20 @@ struct gcs_engine {
     // options / graph cache
     int graph_steps = 32;
     int waves = 4;
-    bool fused = true;
+    bool fused = false;  // GCS_OPT_FUSED_STEP (3-launch step); off: the 6-launch step measured faster
     hipGraphExec_t gexec = nullptr;
     hipGraph_t graph = nullptr;
     int g_steps = 0, g_waves = 0, g_version = -1, g_spacestep = -1;
     gcs_bd_config g_cfg{};
     int g_sched_flags = -1;
     int g_fused = -1, g_chunk = -1;
+
+    // fused-step continuity: after a fused run the cells of the next positions are already binned with the
+    // grid the next step expects, so a run that continues at chain_step skips re-priming (bitwise identical
+    // to one longer run).  Anything that touches positions, context, schedule or cells clears it.
+    bool chain_valid = false;
+    int64_t chain_step = 0;
+    int chain_version = -1;
 };
 
 namespace {
@@ -484,10 +493,23 @@ int begin_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
     if ((rc = set_ctx_field(e, offsetof(DevCtx, step), &st, sizeof(st)))) return rc;
     double dt = cfg->timestep;
     if ((rc = set_ctx_field(e, offsetof(DevCtx, dt_used), &dt, sizeof(dt)))) return rc;
-    launch_prime(e->stream, e->ctx, a, 0.f, e->ncell_max, e->dsched);
-    if (fused_path(e, cfg->spacestep > 0)) enqueue_bin(e);
+    const bool fused = fused_path(e, cfg->spacestep > 0);
+    const bool cont = fused && e->chain_valid && e->chain_step == first_step && e->chain_version == e->topo_version;
+    e->chain_valid = false;
+    if (!cont) {
+        launch_prime(e->stream, e->ctx, a, 0.f, e->ncell_max, e->dsched);
+        if (fused) enqueue_bin(e);
+    }
     HIPCHK(hipGetLastError());
     return GCS_OK;
+}
+
+// after a run's steps were enqueued
+void end_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps)
+{
+    e->chain_valid = fused_path(e, cfg->spacestep > 0);
+    e->chain_step = first_step + steps;
+    e->chain_version = e->topo_version;
 }
 
 }  // namespace
@@ -518,6 +540,8 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
     gcs_engine* e = new gcs_engine();
     e->device = d->device;
     e->n = (int)d->particle_count;
+    e->fa.chunk_mode = 1;  // strided candidate chunks (GCS_OPT_CHUNK_ORDER)
+    e->fa.xcd_tiles = 0;   // XCD-contiguous tile runs (GCS_OPT_XCD_TILES): slower, the slabs are unevenly dense
     const int n = e->n;
     e->mu.assign(n, 1.0);
     e->ab.assign(2 * (size_t)n, 0.0);
@@ -547,7 +571,7 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
         (rc = dalloc(&e->tile_range, (size_t)force_blocks(n) + e->ncell_max + 2)) ||
         (rc = dalloc(&e->ctx, 1)) || (rc = dalloc(&e->dsched, kSchedCount)) ||
         (rc = dalloc(&e->part_force, (size_t)std::max(fb, ub) * kForcePartials)) ||
-        (rc = dalloc(&e->part_bbox, (size_t)std::max(fb, ub) * kBBoxPartials)) ||
+        (rc = dalloc(&e->part_bbox, (size_t)std::max(fb, ub) * kBBoxStride)) ||
         (rc = dalloc(&e->part_energy, (size_t)fb * kEnergyKinds)) || (rc = dalloc(&e->force_out, n)))
         return bail(rc);
     he = hipMemsetAsync(e->count, 0, (e->ncell_max + kScanPad) * sizeof(int), e->stream);
@@ -763,6 +787,7 @@ int gcs_remove_forcefield(gcs_engine* e, int32_t handle)
 int gcs_engine_set_positions(gcs_engine* e, const double* xyz, int64_t n)
 {
     if (!e || !xyz) return fail(GCS_EINVAL, "null argument");
+    e->chain_valid = false;
     if (n != e->n) return fail(GCS_EINVAL, "position count does not match the particle count");
     HIPCHK(hipSetDevice(e->device));
     std::vector<float4> h(n);
@@ -812,6 +837,7 @@ int gcs_engine_get_context(gcs_engine* e, gcs_context* c)
 int gcs_engine_set_context(gcs_engine* e, const gcs_context* c)
 {
     if (!e || !c) return fail(GCS_EINVAL, "null argument");
+    e->chain_valid = false;
     HIPCHK(hipSetDevice(e->device));
     DevCtx d;
     HIPCHK(hipMemcpyAsync(&d, e->ctx, sizeof(d), hipMemcpyDeviceToHost, e->stream));
@@ -834,6 +860,7 @@ int gcs_engine_set_context(gcs_engine* e, const gcs_context* c)
 int gcs_engine_set_schedule(gcs_engine* e, const gcs_schedule* s)
 {
     if (!e || !s) return fail(GCS_EINVAL, "null argument");
+    e->chain_valid = false;
     if ((s->update_scales && (!(s->core_scale_tau > 0) || !(s->bond_scale_tau > 0))))
         return fail(GCS_EINVAL, "scale time constants must be positive");
     HIPCHK(hipSetDevice(e->device));
@@ -847,6 +874,7 @@ int gcs_engine_set_schedule(gcs_engine* e, const gcs_schedule* s)
 int gcs_engine_apply_schedule(gcs_engine* e, int64_t step)
 {
     if (!e) return fail(GCS_EINVAL, "null argument");
+    e->chain_valid = false;
     int rc = prepare(e);
     if (rc) return rc;
     long long st = step;
@@ -919,6 +947,7 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
     }
     for (; done < steps; ++done) enqueue_step(e, spacestep, (float)cfg->spacestep, (float)cfg->timestep);
     HIPCHK(hipGetLastError());
+    end_run(e, cfg, first_step, steps);
     if (steps & 1) e->parity ^= 1;
     if (cfg->noise == GCS_NOISE_INJECTED) e->noise_cursor += steps;
     return GCS_OK;
@@ -936,6 +965,7 @@ int gcs_engine_compute_forces(gcs_engine* e, double* forces, int64_t n)
 {
     if (!e || !forces) return fail(GCS_EINVAL, "null argument");
     if (n != e->n) return fail(GCS_EINVAL, "force array size does not match the particle count");
+    e->chain_valid = false;
     int rc = prepare(e);
     if (rc) return rc;
     launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max, e->dsched);
@@ -957,6 +987,7 @@ int gcs_engine_compute_forces(gcs_engine* e, double* forces, int64_t n)
 int gcs_engine_compute_energy(gcs_engine* e, double* total, double* per_kind)
 {
     if (!e || !total) return fail(GCS_EINVAL, "null argument");
+    e->chain_valid = false;
     int rc = prepare(e);
     if (rc) return rc;
     launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max, e->dsched);
@@ -983,6 +1014,7 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
 {
     if (!e || !count || (capacity > 0 && !pairs)) return fail(GCS_EINVAL, "null argument");
     if (!(distance > 0)) return fail(GCS_EINVAL, "search distance must be positive");
+    e->chain_valid = false;
     if (!points && n != e->n) return fail(GCS_EINVAL, "point count does not match the particle count");
     if (n < 0 || n > (int64_t)1 << 30) return fail(GCS_EINVAL, "bad point count");
     *count = 0;
@@ -1094,6 +1126,11 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     int rc = begin_run(e, cfg, first_step);
     if (rc) return rc;
     std::vector<hipEvent_t> ev((size_t)steps * 4 + 2, nullptr);
+    // GCS_DEBUG_TIMES=<file>: per-block {start, end, smid, tile size} of the last profiled force launch
+    const char* dbg_path = std::getenv("GCS_DEBUG_TIMES");
+    unsigned long long* dbg = nullptr;
+    const size_t dbg_n = (size_t)force_grid(e->n) * 4;
+    if (dbg_path) HIPCHK(hipMalloc(&dbg, dbg_n * sizeof(unsigned long long)));
     for (auto& x : ev) HIPCHK(hipEventCreate(&x));
     const int fb = force_grid(e->n);
     HIPCHK(hipEventRecord(ev[0], e->stream));
@@ -1105,13 +1142,16 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
         else
             enqueue_cells(e);
         HIPCHK(hipEventRecord(ev[2 + 4 * k], e->stream));
+        if (dbg && k == steps - 1) e->fa.dbg_times = dbg;
         launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, fused);
+        e->fa.dbg_times = nullptr;
         HIPCHK(hipEventRecord(ev[3 + 4 * k], e->stream));
         if (!fused) launch_tail(e->stream, e->ctx, e->fa, fb, fb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
         HIPCHK(hipEventRecord(ev[4 + 4 * k], e->stream));
     }
     HIPCHK(hipEventRecord(ev[ev.size() - 1], e->stream));
     HIPCHK(hipGetLastError());
+    end_run(e, cfg, first_step, steps);
     HIPCHK(hipStreamSynchronize(e->stream));
     double cell = 0, force = 0, tail = 0;
     for (int64_t k = 0; k < steps; ++k) {
@@ -1125,6 +1165,15 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     }
     float tot = 0;
     HIPCHK(hipEventElapsedTime(&tot, ev[0], ev[ev.size() - 1]));
+    if (dbg) {
+        std::vector<unsigned long long> h(dbg_n);
+        HIPCHK(hipMemcpy(h.data(), dbg, dbg_n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        (void)hipFree(dbg);
+        if (FILE* f = std::fopen(dbg_path, "wb")) {
+            std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+            std::fclose(f);
+        }
+    }
     for (auto& x : ev) (void)hipEventDestroy(x);
     if (steps & 1) e->parity ^= 1;
     if (cfg->noise == GCS_NOISE_INJECTED) e->noise_cursor += steps;
@@ -1135,6 +1184,16 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     out->force_ms = force / (double)steps;
     out->cell_ms = cell / (double)steps;
     out->tail_ms = tail / (double)steps;
+    if (fused) {  // the tail runs inside the force launch: report its last-block section (last step)
+        int khz = 0;
+        HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, e->device));
+        out->tail_ms = khz > 0 ? (double)(d.t_last[3] - d.t_last[0]) / (double)khz : 0.0;
+        if (std::getenv("GCS_DEBUG") && khz > 0)
+            std::fprintf(stderr, "gcs: grid %d x %d x %d (%d cells), ntiles %d; last block: tail %.2f us, scan %.2f us, "
+                         "rows %.2f us\n", d.grid.n[0], d.grid.n[1], d.grid.n[2], d.grid.ncell, d.ntiles,
+                         1e3 * (d.t_last[1] - d.t_last[0]) / khz, 1e3 * (d.t_last[2] - d.t_last[1]) / khz,
+                         1e3 * (d.t_last[3] - d.t_last[2]) / khz);
+    }
     out->mean_neighbors = d.neighbors;
     return GCS_OK;
 }
@@ -1142,6 +1201,7 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
 {
     if (!e) return fail(GCS_EINVAL, "null argument");
+    e->chain_valid = false;
     if (option == GCS_OPT_GRAPH_STEPS) {
         if (value < 0 || value > 4096) return fail(GCS_EINVAL, "graph steps must be in [0, 4096]");
         e->graph_steps = (int)value;
@@ -1156,6 +1216,12 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
     if (option == GCS_OPT_CHUNK_ORDER) {
         if (value != 0 && value != 1) return fail(GCS_EINVAL, "chunk order must be 0 (contiguous) or 1 (strided)");
         e->fa.chunk_mode = (int)value;
+        drop_graph(e);
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_XCD_TILES) {
+        if (value != 0 && value != 1) return fail(GCS_EINVAL, "xcd tiles must be 0 or 1");
+        e->fa.xcd_tiles = (int)value;
         drop_graph(e);
         return GCS_OK;
     }

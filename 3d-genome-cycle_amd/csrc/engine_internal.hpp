@@ -18,10 +18,12 @@ namespace gcs {
 constexpr int kTile = 64;          // particles per tile of the pair loop = one wave's lanes
 constexpr int kMaxRows = 64;       // stencil rows per batch of the pair loop's row table
 constexpr int kPairFx = 2;         // x subdivision of the pair cell grid
-constexpr int kScanPad = 4096 + 8; // count/cstart padding: k_cell_scan works in whole 4096-cell tiles
+constexpr int kScanSeg = 16;        // cells per thread per iteration of the cell scan
+constexpr int kScanPad = kScanSeg * 1024 + 8;  // count/cstart padding: the scan touches whole iterations (<= 1024 threads)
 constexpr int kMaxPointSources = 4;
 constexpr int kForcePartials = 8;  // per force block: reaction in[3], out[3], max mu|F|, neighbours
 constexpr int kBBoxPartials = 6;   // per block: bbox lo[3], hi[3]
+constexpr int kBBoxStride = 8;     // row stride of the bbox partials (rows of 8: one component per lane & 7)
 constexpr int kEnergyKinds = 8;
 
 struct Grid {
@@ -50,6 +52,7 @@ struct DevCtx {
     Grid grid_next;        // bins the positions the next step produces (fused path)
     unsigned ticket;       // arrival counter of the fused force kernel's blocks (0 between launches)
     int pad1;
+    unsigned long long t_last[4];  // wall clock: fused last-block section start, after tail, after scan, end
 };
 
 enum BondType : int { kSemispring = 0, kHarmonic = 1, kSpring = 2, kSoftwell = 3 };
@@ -117,7 +120,7 @@ struct ForceArgs {
     long long noise_steps;
     // outputs
     float* part_force;    // [blocks][kForcePartials]
-    float* part_bbox;     // [blocks][kBBoxPartials]
+    float* part_bbox;     // [blocks][kBBoxStride] (kBBoxPartials used)
     double* part_energy;  // [blocks][kEnergyKinds]
     float4* force_out;    // [N] (kModeForce)
     // fused step (kModeStep, FUSED): binning of the new positions + last-block tail and cell scan
@@ -130,6 +133,8 @@ struct ForceArgs {
     const double* sched;
     int ncell_max;
     int apply_sched;
+    int xcd_tiles;  // 1: each XCD takes one contiguous run of tiles (GCS_OPT_XCD_TILES)
+    unsigned long long* dbg_times;  // optional (GCS_DEBUG_TIMES): per block {start, end, tiles, candidates} wall clock
 };
 
 // ---- Philox4x32-10 + Box-Muller: the production noise stream (identical on host for the oracle) ----
@@ -179,7 +184,7 @@ size_t sort_u64_temp_bytes(int n);
 inline int force_blocks(int n) { return (n + kTile - 1) / kTile; }
 // k_force launch size: tiles never cross a cell row, so there are up to (rows) more tiles than force_blocks;
 // blocks walk the tiles grid-stride, any launch size is correct
-inline int force_grid(int n) { return force_blocks(n) + force_blocks(n) / 4 + 64; }
+inline int force_grid(int n) { return ((force_blocks(n) + force_blocks(n) / 4 + 64) + 7) & ~7; }  // multiple of 8 (XCDs)
 constexpr int kUpdateBlock = 256;
 inline int update_blocks(int n) { return (n + kUpdateBlock - 1) / kUpdateBlock; }
 

@@ -23,6 +23,35 @@ namespace gcs {
 
 namespace {
 
+// Write-through (sc1) stores and L1-bypassing (sc1) loads: the cross-workgroup hand-off of the fused step
+// (per-block partials and cell counts -> the last block) without a release fence (MI355X_MICROARCH.md
+// "Valid forms", first row: sc1 stores drained by s_waitcnt, one agent-scope ticket add per block, sc1 loads).
+__device__ __forceinline__ void st_sc1(float* p, float v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16-B sc1 load through a buffer descriptor (out-of-range offsets read 0)
+__device__ __forceinline__ float4 ld_sc1_f4(__amdgpu_buffer_rsrc_t r, int byte_off)
+{
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
+    float4 f;
+    __builtin_memcpy(&f, &v, 16);
+    return f;
+}
+__device__ __forceinline__ int4 ld_sc1_i4(__amdgpu_buffer_rsrc_t r, int byte_off)
+{
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
+    int4 f;
+    __builtin_memcpy(&f, &v, 16);
+    return f;
+}
+__device__ inline double wave_max_d(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+
 __device__ inline float wave_sum(float v)
 {
 #pragma unroll
@@ -75,7 +104,7 @@ __device__ inline int cell_index(const Grid& g, float x, float y, float z)
 // Cell grid over the box [lo, hi]; cell edge >= rc (1e-4 margin; x edge rc / fx) so any pair closer than rc lies
 // in the same or an adjacent cell (+-fx in x).  Particles outside the box are clamped into the border cells,
 // which keeps that property because clamping never increases a per-axis cell distance.
-__device__ Grid make_grid(const float* lo, const float* hi, float rc, int ncell_max, int fx)
+__device__ __forceinline__ Grid make_grid(const float* lo, const float* hi, float rc, int ncell_max, int fx)
 {
     Grid g;
     int n[3];
@@ -91,13 +120,14 @@ __device__ Grid make_grid(const float* lo, const float* hi, float rc, int ncell_
         n[k] = m;
         total *= m;
     }
-    while (total > ncell_max) {
-        int kk = 0;
-        for (int k = 1; k < 3; ++k)
-            if (n[k] > n[kk]) kk = k;
-        total /= n[kk];
-        n[kk] = max(1, n[kk] / 2);
-        total *= n[kk];
+    while (total > ncell_max) {  // halve the longest axis (no dynamic array indexing: keeps it in registers)
+        if (n[0] >= n[1] && n[0] >= n[2])
+            n[0] = max(1, n[0] / 2);
+        else if (n[1] >= n[2])
+            n[1] = max(1, n[1] / 2);
+        else
+            n[2] = max(1, n[2] / 2);
+        total = (long long)n[0] * n[1] * n[2];
     }
     for (int k = 0; k < 3; ++k) {
         g.lo[k] = (ext[k] > 0.f) ? lo[k] : 0.f;
@@ -111,7 +141,7 @@ __device__ Grid make_grid(const float* lo, const float* hi, float rc, int ncell_
     return g;
 }
 
-__device__ void compute_grid(DevCtx* ctx, float rc, int ncell_max, int fx)
+__device__ __forceinline__ void compute_grid(DevCtx* ctx, float rc, int ncell_max, int fx)
 {
     ctx->grid = make_grid(ctx->bbox_lo, ctx->bbox_hi, rc, ncell_max, fx);
 }
@@ -119,7 +149,7 @@ __device__ void compute_grid(DevCtx* ctx, float rc, int ncell_max, int fx)
 // The grid that bins the positions produced by the NEXT step: the current bbox padded by 2 % + 0.01 (particles
 // move far less per step; any that leave are clamped, which is still exact) and the pair cutoff that step
 // will use, i.e. with the core scale the schedule sets after step `step` (closed form of update_core_scale).
-__device__ Grid next_grid(const DevCtx* ctx, const ForceArgs& a, const double* sched, long long step, int ncell_max)
+__device__ __forceinline__ Grid next_grid(const DevCtx* ctx, const ForceArgs& a, const double* sched, long long step, int ncell_max)
 {
     float lo[3], hi[3];
     for (int k = 0; k < 3; ++k) {
@@ -217,39 +247,68 @@ __device__ inline int wave_incl_scan(int v, int lane)
 // running carry, re-zeroing count for the next step; then the per-row tile table of k_force (a tile is <= 64
 // consecutive sorted particles of ONE row of cells).  count/cstart are padded by kScanPad so whole tiles may be
 // touched; entries past ncell are zero by invariant.  Any block size that is a multiple of 64 (<= 1024).
-__device__ void scan_cells_body(DevCtx* __restrict__ ctx, int n, int* __restrict__ count, int* __restrict__ cstart,
-                                int* __restrict__ tile_start, int2* __restrict__ tile_range)
+__device__ __forceinline__ void scan_cells_body(DevCtx* __restrict__ ctx, int n, int* __restrict__ count,
+                                                int* __restrict__ cstart, int* __restrict__ tile_start,
+                                                int2* __restrict__ tile_range)
 {
     __shared__ int wtot[16];
     __shared__ int tile_total;
     const int nc = ctx->grid.ncell;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-    const int span = 4 * blockDim.x;
     int carry = 0;
-    for (int base = 0; base < nc; base += span) {
-        const int i0 = base + 4 * tid;
-        const int4 c = *reinterpret_cast<const int4*>(count + i0);
-        const int sum = c.x + c.y + c.z + c.w;
-        const int incl = wave_incl_scan(sum, lane);
-        if (lane == 63) wtot[wave] = incl;
-        __syncthreads();
-        if (wave == 0) {
-            const int w = lane < nw ? wtot[lane] : 0;
-            const int wi = wave_incl_scan(w, lane);
-            if (lane < nw) wtot[lane] = wi - w;
-            if (lane == nw - 1) tile_total = wi;
+    {
+        // kScanSeg consecutive cells per thread as 16-B sc1 loads (in the fused step the counts were produced by
+        // other workgroups' atomics in this launch); the next iteration's loads are issued before this one's scan
+        static_assert(kScanSeg % 4 == 0, "kScanSeg counts are loaded as int4");
+        constexpr int kQ = kScanSeg / 4;
+        const int span = kScanSeg * blockDim.x;
+        const auto rc = __builtin_amdgcn_make_buffer_rsrc((void*)count, 0, nc * 4, 0x00020000);  // past nc: 0
+        int4 cur[kQ];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) cur[q] = ld_sc1_i4(rc, (kScanSeg * tid + 4 * q) * 4);
+        for (int base = 0; base < nc; base += span) {
+            const int i0 = base + kScanSeg * tid;
+            int4 nxt[kQ];
+            if (base + span < nc) {
+#pragma unroll
+                for (int q = 0; q < kQ; ++q) nxt[q] = ld_sc1_i4(rc, (i0 + span + 4 * q) * 4);
+            }
+            int sum = 0;
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) sum += cur[q].x + cur[q].y + cur[q].z + cur[q].w;
+            const int incl = wave_incl_scan(sum, lane);
+            if (lane == 63) wtot[wave] = incl;
+            __syncthreads();
+            if (wave == 0) {
+                const int w = lane < nw ? wtot[lane] : 0;
+                const int wi = wave_incl_scan(w, lane);
+                if (lane < nw) wtot[lane] = wi - w;
+                if (lane == nw - 1) tile_total = wi;
+            }
+            __syncthreads();
+            int run = carry + wtot[wave] + incl - sum;
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) {
+                const int4 c = cur[q];
+                *reinterpret_cast<int4*>(cstart + i0 + 4 * q) =
+                    make_int4(run, run + c.x, run + c.x + c.y, run + c.x + c.y + c.z);
+                run += c.x + c.y + c.z + c.w;
+                *reinterpret_cast<int4*>(count + i0 + 4 * q) = make_int4(0, 0, 0, 0);
+            }
+            carry += tile_total;
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) cur[q] = nxt[q];
         }
-        __syncthreads();
-        const int run = carry + wtot[wave] + incl - sum;
-        *reinterpret_cast<int4*>(cstart + i0) = make_int4(run, run + c.x, run + c.x + c.y, run + c.x + c.y + c.z);
-        *reinterpret_cast<int4*>(count + i0) = make_int4(0, 0, 0, 0);
-        carry += tile_total;
-        __syncthreads();
     }
-    if (tid == 0) cstart[nc] = n;
+    if (tid == 0) {
+        cstart[nc] = n;
+        ctx->t_last[2] = wall_clock64();
+    }
     __syncthreads();
     const int nx = ctx->grid.n[0], nrows = ctx->grid.n[1] * ctx->grid.n[2];
     carry = 0;
+    const int span = 4 * blockDim.x;
     for (int base = 0; base < nrows; base += span) {
         int c[4];
         int sum = 0;
@@ -743,14 +802,14 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
 // (k_cell_scan builds the per-row tile prefix).  The WAVES waves split the tile's candidates; wave 0 then
 // adds the particle-local terms and integrates.  Per-block partials (reactions, bbox, drift, neighbours,
 // energies) are reduced in a fixed order by k_tail / the host: no atomics, bitwise reproducible.
-__device__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance, int apply_sched,
-                          int ncell_max, const double* __restrict__ sched, bool fused);
+__device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance,
+                                          int apply_sched, int ncell_max, const double* __restrict__ sched, bool fused);
 
 // FUSED (kModeStep only): the new positions are also binned into ctx->grid_next (count atomics), and the last
 // block to finish (arrival ticket, agent-scope release/acquire: cdna_hip_programming.md G16) runs the schedule
 // tail and the cell scan for the next step, so a step is three launches: scatter, sort, force.
 template <int MODE, int WAVES, bool FUSED>
-__global__ __launch_bounds__(64 * WAVES) void k_force(DevCtx* __restrict__ ctx, ForceArgs a)
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5))) void k_force(DevCtx* __restrict__ ctx, ForceArgs a)
 {
     __shared__ float red[WAVES > 1 ? WAVES : 1][4][64];
     __shared__ int s_rowV[WAVES][17];
@@ -772,7 +831,19 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(DevCtx* __restrict__ ctx, 
         for (int k = 0; k < kEnergyKinds; ++k) s_pe[k] = 0.0;
     }
 
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const unsigned long long t_start = a.dbg_times ? wall_clock64() : 0ull;
+    // XCD-aware tile order (a.xcd_tiles): workgroups are dispatched round-robin over the 8 XCDs, so block b runs
+    // on XCD b & 7; give each XCD one contiguous run of tiles (a slab of cell rows) so its private L2 holds one
+    // slab plus halo instead of the whole system.  Otherwise plain grid-stride.  The launch is a multiple of 8.
+    const int xs = a.xcd_tiles ? 8 : 1;
+    const int per = (ntiles + xs - 1) / xs;  // tiles per XCD
+    const int lane_xcd = a.xcd_tiles ? (blockIdx.x & 7) : 0;
+    const int slots = gridDim.x / xs;        // blocks per XCD
+    int first_tile = -1;
+    for (int j = a.xcd_tiles ? (blockIdx.x >> 3) : blockIdx.x; j < per; j += slots) {
+        const int tile = lane_xcd * per + j;
+        if (tile >= ntiles) break;
+        if (first_tile < 0) first_tile = tile;
         const int2 tr = a.tile_range[tile];
         const int s_begin = uniform(tr.x), s_end = uniform(tr.y);
         const int s = s_begin + lane;
@@ -870,36 +941,51 @@ __global__ __launch_bounds__(64 * WAVES) void k_force(DevCtx* __restrict__ ctx, 
         if (WAVES > 1) __syncthreads();  // `red` is reused by the next tile
     }
     if (WAVES == 1) __syncthreads();  // (WAVES > 1 synchronised at the end of every tile)
+    if (a.dbg_times && threadIdx.x == 0) {
+        a.dbg_times[4 * blockIdx.x] = t_start;
+        a.dbg_times[4 * blockIdx.x + 1] = wall_clock64();
+        a.dbg_times[4 * blockIdx.x + 2] = first_tile >= 0 ? (unsigned long long)__smid() : ~0ull;
+        a.dbg_times[4 * blockIdx.x + 3] = first_tile >= 0 ? (unsigned long long)first_tile : ~0ull;
+    }
     if (threadIdx.x == 0) {
         if (MODE == kModeEnergy) {
             for (int k = 0; k < kEnergyKinds; ++k) a.part_energy[blockIdx.x * kEnergyKinds + k] = s_pe[k];
+        } else if (FUSED) {
+            // write-through: read by the last block of this launch (sc1 loads in tail_body)
+            for (int k = 0; k < kForcePartials; ++k) st_sc1(a.part_force + blockIdx.x * kForcePartials + k, s_pr[k]);
+            for (int k = 0; k < kBBoxPartials; ++k)
+                st_sc1(a.part_bbox + blockIdx.x * kBBoxStride + k, s_pr[kForcePartials + k]);
         } else {
             for (int k = 0; k < kForcePartials; ++k) a.part_force[blockIdx.x * kForcePartials + k] = s_pr[k];
             if (MODE == kModeStep)
                 for (int k = 0; k < kBBoxPartials; ++k)
-                    a.part_bbox[blockIdx.x * kBBoxPartials + k] = s_pr[kForcePartials + k];
+                    a.part_bbox[blockIdx.x * kBBoxStride + k] = s_pr[kForcePartials + k];
         }
     }
     if (FUSED) {
+        // Hand-off to the last block: the partials were stored sc1 by lane 0 above and the cell counts are
+        // agent-scope atomics (their returned values were consumed), so no release fence: drain, then ONE
+        // ticket add per block; the last arriver reads everything with sc1 loads (no acquire either).
         __shared__ int s_last;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains (partials, cells, slots)
-        __syncthreads();
         if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const unsigned prev = atomicAdd(&ctx->ticket, 1u);
             s_last = (prev == gridDim.x - 1) ? 1 : 0;
-            if (s_last) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
         }
         __syncthreads();
         if (s_last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const unsigned long long t0 = wall_clock64();
             const int nb = gridDim.x;
             tail_body(ctx, a, nb, nb, 1, a.apply_sched, a.ncell_max, a.sched, true);
+            const unsigned long long t1 = wall_clock64();
             scan_cells_body(ctx, a.n, a.count, a.cstart_w, a.tile_start_w, a.tile_range_w);
-            if (threadIdx.x == 0) ctx->ticket = 0u;
+            if (threadIdx.x == 0) {
+                ctx->ticket = 0u;
+                ctx->t_last[0] = t0;
+                ctx->t_last[1] = t1;
+                ctx->t_last[3] = wall_clock64();
+            }
         }
     }
 }
@@ -934,7 +1020,7 @@ __global__ __launch_bounds__(kUpdateBlock) void k_update(const DevCtx* __restric
         for (int k = 0; k < 6; ++k) red[k][wave] = v[k];
     __syncthreads();
     if (threadIdx.x == 0) {
-        float* pb = a.part_bbox + blockIdx.x * kBBoxPartials;
+        float* pb = a.part_bbox + blockIdx.x * kBBoxStride;
         for (int k = 0; k < 6; ++k) {
             float r = red[k][0];
             for (int w = 1; w < kUpdateBlock / 64; ++w) r = (k < 3) ? fminf(r, red[k][w]) : fmaxf(r, red[k][w]);
@@ -962,36 +1048,61 @@ __global__ __launch_bounds__(256) void k_adapt(DevCtx* ctx, ForceArgs a, int blo
     }
 }
 
-__device__ inline double wave_max_d(double v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-    return v;
-}
-
 // Fixed-order reduction of the per-block partials (per thread strided, wave butterflies, waves in index order:
 // bitwise reproducible) + the device-resident interphase schedule + the next cell grid.  Any block size that
 // is a multiple of 64.  fused: the step's force kernel already binned the new positions with grid_next, which
 // becomes the current grid, and the grid for the following step is prepared.
-__device__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance, int apply_sched,
-                          int ncell_max, const double* __restrict__ sched, bool fused)
+__device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance,
+                                          int apply_sched, int ncell_max, const double* __restrict__ sched, bool fused)
 {
     __shared__ double s_red[16][8];
-    __shared__ float s_bb[16][6];
+    __shared__ float s_bb[16][8];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const int B = blockDim.x;
+    // Latency-shaped: the partials are rows of 8 floats; each thread takes rows tid, tid + B, ... and issues
+    // kTailRows rows' 16-B sc1 loads at once (one memory round trip per kTailRows * B rows), combines its rows
+    // in order, then lanes meet in wave butterflies and the waves in index order: a fixed order for a given
+    // (blocks, blockDim), bitwise reproducible.  Loads past the end return 0 (buffer range check).
+    constexpr int kTailRows = 8;
+    const float big = 3.0e38f;
+    const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_force, 0, fblocks * 32, 0x00020000);
+    const auto rb = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_bbox, 0, bblocks * 32, 0x00020000);
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int b = tid; b < fblocks; b += blockDim.x)
-        for (int k = 0; k < 8; ++k) {
-            const double v = a.part_force[b * kForcePartials + k];
-            acc[k] = (k == 6) ? fmax(acc[k], v) : acc[k] + v;
+    float bb[6] = {big, big, big, -big, -big, -big};
+    const int nrow = max(fblocks, bblocks);
+    for (int b0 = tid; b0 < nrow; b0 += kTailRows * B) {
+        float4 f0[kTailRows], f1[kTailRows], g0[kTailRows], g1[kTailRows];
+#pragma unroll
+        for (int j = 0; j < kTailRows; ++j) {
+            const int off = (b0 + j * B) * 32;
+            f0[j] = ld_sc1_f4(rf, off);
+            f1[j] = ld_sc1_f4(rf, off + 16);
+            g0[j] = ld_sc1_f4(rb, off);
+            g1[j] = ld_sc1_f4(rb, off + 16);
         }
-    float bb[6] = {3.0e38f, 3.0e38f, 3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
-    for (int b = tid; b < bblocks; b += blockDim.x)
-        for (int k = 0; k < 6; ++k) {
-            const float v = a.part_bbox[b * kBBoxPartials + k];
-            bb[k] = (k < 3) ? fminf(bb[k], v) : fmaxf(bb[k], v);
+#pragma unroll
+        for (int j = 0; j < kTailRows; ++j) {
+            acc[0] += f0[j].x;
+            acc[1] += f0[j].y;
+            acc[2] += f0[j].z;
+            acc[3] += f0[j].w;
+            acc[4] += f1[j].x;
+            acc[5] += f1[j].y;
+            acc[6] = fmax(acc[6], (double)f1[j].z);
+            acc[7] += f1[j].w;
+            if (b0 + j * B < bblocks) {
+                bb[0] = fminf(bb[0], g0[j].x);
+                bb[1] = fminf(bb[1], g0[j].y);
+                bb[2] = fminf(bb[2], g0[j].z);
+                bb[3] = fmaxf(bb[3], g0[j].w);
+                bb[4] = fmaxf(bb[4], g1[j].x);
+                bb[5] = fmaxf(bb[5], g1[j].y);
+            }
         }
+    }
+#pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] = (k == 6) ? wave_max_d(acc[k]) : wave_sum_d(acc[k]);
+#pragma unroll
     for (int k = 0; k < 6; ++k) bb[k] = (k < 3) ? wave_min(bb[k]) : wave_max(bb[k]);
     if (lane == 0) {
         for (int k = 0; k < 8; ++k) s_red[wave][k] = acc[k];
@@ -999,17 +1110,21 @@ __device__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblo
     }
     __syncthreads();
     if (tid == 0) {
+        double tot[8];
+        float bb[6];
+        for (int k = 0; k < 8; ++k) tot[k] = s_red[0][k];
+        for (int k = 0; k < 6; ++k) bb[k] = s_bb[0][k];
         for (int w = 1; w < nw; ++w) {
-            for (int k = 0; k < 8; ++k) acc[k] = (k == 6) ? fmax(acc[k], s_red[w][k]) : acc[k] + s_red[w][k];
+            for (int k = 0; k < 8; ++k) tot[k] = (k == 6) ? fmax(tot[k], s_red[w][k]) : tot[k] + s_red[w][k];
             for (int k = 0; k < 6; ++k) bb[k] = (k < 3) ? fminf(bb[k], s_bb[w][k]) : fmaxf(bb[k], s_bb[w][k]);
         }
         if (fblocks > 0) {
             for (int k = 0; k < 3; ++k) {
-                ctx->react_in[k] = acc[k];
-                ctx->react_out[k] = acc[3 + k];
+                ctx->react_in[k] = tot[k];
+                ctx->react_out[k] = tot[3 + k];
             }
-            ctx->max_drift = acc[6];
-            ctx->neighbors = acc[7] / (double)a.n;
+            ctx->max_drift = tot[6];
+            ctx->neighbors = tot[7] / (double)a.n;
         }
         if (bblocks > 0)
             for (int k = 0; k < 3; ++k) {

@@ -29,6 +29,7 @@ OPT_GRAPH_STEPS = 1
 OPT_WAVES_PER_TILE = 2
 OPT_CHUNK_ORDER = 3
 OPT_FUSED_STEP = 4
+OPT_XCD_TILES = 5
 
 ENERGY_KINDS = ("pair", "softwell", "bonds", "bending", "wall_in", "wall_out", "point_source", "kinetochore_fiber")
 

@@ -118,6 +118,8 @@ def main():
     ap.add_argument("--graph-steps", type=int, default=32)
     ap.add_argument("--waves", type=int, default=4)
     ap.add_argument("--chunk-order", type=int, default=1)
+    ap.add_argument("--xcd-tiles", type=int, default=0)
+    ap.add_argument("--fused", type=int, default=0, help="1: 3 launches per step (force kernel bins + runs the tail)")
     ap.add_argument("--profile-steps", type=int, default=50)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline work (0 = skip)")
     ap.add_argument("--no-start-window", action="store_true", help="skip the secondary step-0 window")
@@ -133,6 +135,8 @@ def main():
     eng.set_option(A.OPT_GRAPH_STEPS, args.graph_steps)
     eng.set_option(A.OPT_WAVES_PER_TILE, args.waves)
     eng.set_option(A.OPT_CHUNK_ORDER, args.chunk_order)
+    eng.set_option(A.OPT_FUSED_STEP, args.fused)
+    eng.set_option(A.OPT_XCD_TILES, args.xcd_tiles)
     seed = 1000003 * (rank + 1)
 
     eng.run(args.warmup, first_step=WINDOW_START, seed=seed)
@@ -198,7 +202,7 @@ def main():
                                f"{WINDOW_START} (core_scale {ctx['core_scale']:.4f})",
                    "particles": n, "replicas": world, "parallelism": f"replicas{world}",
                    "mean_neighbors": prof["mean_neighbors"], "graph_steps": args.graph_steps,
-                   "waves_per_tile": args.waves, "chunk_order": args.chunk_order, "start_window_value": start_rate, "finite": finite},
+                   "waves_per_tile": args.waves, "chunk_order": args.chunk_order, "fused": args.fused, "xcd_tiles": args.xcd_tiles, "start_window_value": start_rate, "finite": finite},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(),
                      "kernel": "k_force<kModeStep>", "force_ms": force_ms, "cell_ms": prof["cell_ms"],

@@ -202,7 +202,8 @@ typedef struct gcs_profile {
     double total_ms;          /* wall time of the probed steps (events around the whole loop) */
     double force_ms;          /* average duration of one force/integrate launch */
     double cell_ms;           /* average duration of the cell-list build (count + scan + scatter + sort) */
-    double tail_ms;           /* average duration of the schedule tail launch */
+    double tail_ms;           /* average duration of the schedule tail launch (fused step: the last-block
+                                 tail + cell-scan section inside the force launch, last step) */
     double mean_neighbors;    /* mean number of neighbours within the cutoff per particle (last step) */
 } gcs_profile;
 
@@ -267,8 +268,9 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
 /* tuning knobs */
 #define GCS_OPT_GRAPH_STEPS 1   /* steps captured per hipGraph replay (0 = eager launches) */
 #define GCS_OPT_WAVES_PER_TILE 2 /* waves sharing one 64-particle tile of the pair loop: 1, 2, 4 or 8 */
-#define GCS_OPT_CHUNK_ORDER 3    /* pair-loop candidate chunks: 0 contiguous, 1 strided across stencil rows */
+#define GCS_OPT_CHUNK_ORDER 3    /* pair-loop candidate chunks: 0 contiguous, 1 strided across stencil rows (default) */
 #define GCS_OPT_FUSED_STEP 4     /* 1: 3 launches per step (binning, tail and cell scan fused into the force kernel) */
+#define GCS_OPT_XCD_TILES 5      /* 1: each of the 8 XCDs takes one contiguous run of force tiles (default 0) */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
 
 #ifdef __cplusplus

@@ -161,12 +161,25 @@ def test_waves_per_tile_equivalent(c1_design, interphase_cfg, waves, order):
     assert te == pytest.approx(to, rel=1e-5)
 
 
-def test_chunked_runs_equal_one_run(c1_design, interphase_cfg):
-    """The Philox counter is the absolute step: 3 chunks == 1 run, bit for bit."""
+@pytest.mark.parametrize("xcd", [0, 1])
+def test_xcd_tile_order_same_forces(c2_design, interphase_cfg, xcd):
+    """The XCD-contiguous tile order only moves tiles between workgroups: per-particle forces are bit-identical."""
+    e0, _ = interphase.build_interphase(Engine, c2_design, interphase_cfg)
+    e1, _ = interphase.build_interphase(Engine, c2_design, interphase_cfg)
+    e0.set_option(A.OPT_XCD_TILES, 0)
+    e1.set_option(A.OPT_XCD_TILES, xcd)
+    assert np.array_equal(e0.compute_forces(), e1.compute_forces())
+
+
+@pytest.mark.parametrize("fused", [0, 1])
+def test_chunked_runs_equal_one_run(c1_design, interphase_cfg, fused):
+    """The Philox counter is the absolute step: 3 chunks == 1 run, bit for bit (both step shapes; the fused
+    step carries its cell list across runs that continue at the next step)."""
     cfg = interphase_cfg
     a, _ = interphase.build_interphase(Engine, c1_design, cfg)
     b, _ = interphase.build_interphase(Engine, c1_design, cfg)
     for s in (a, b):
+        s.set_option(A.OPT_FUSED_STEP, fused)
         s.set_schedule(**interphase.interphase_schedule(cfg))
         s.apply_schedule(0)
     a.run(60, seed=3)

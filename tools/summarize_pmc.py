@@ -1,5 +1,12 @@
 #!/usr/bin/env python3
-"""Average per-dispatch counters / durations per kernel from a tools/profile.sh output directory."""
+"""Average per-dispatch counters / durations per kernel from a tools/profile.sh output directory.
+
+    python tools/summarize_pmc.py gpurun_out/prof_r01 [--traffic-out profiles/pmc_force_traffic.json]
+
+HBM traffic per force launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950 FETCH_SIZE reports half the bytes
+of wide coalesced reads (MI355X_MICROARCH.md "HBM"); both counters are fabric-side (L2 misses, Infinity Cache hits
+included).
+"""
 import csv
 import glob
 import json
@@ -26,7 +33,27 @@ def main(d):
                 out["kernels"].setdefault(k, {})[c] = sum(v) / len(v)
     json.dump(out, sys.stdout, indent=1)
     print()
+    return out
+
+
+def force_traffic(out, kernel_prefix="k_force<0"):
+    for k, v in out["kernels"].items():
+        if k.startswith(kernel_prefix) and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+            fetch = 2.0 * v["FETCH_SIZE"] * 1024.0
+            write = v["WRITE_SIZE"] * 1024.0
+            return {"kernel": k, "bytes_per_launch": fetch + write, "fetch_bytes_corrected": fetch,
+                    "write_bytes": write, "FETCH_SIZE_KiB": v["FETCH_SIZE"], "WRITE_SIZE_KiB": v["WRITE_SIZE"],
+                    "avg_us": v.get("avg_us"), "correction": "2 x FETCH_SIZE (gfx950) + WRITE_SIZE"}
+    return None
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    res = main(sys.argv[1])
+    if "--traffic-out" in sys.argv:
+        t = force_traffic(res)
+        if t is None:
+            sys.exit("no k_force FETCH_SIZE/WRITE_SIZE in the profile")
+        t["source"] = sys.argv[1]
+        with open(sys.argv[sys.argv.index("--traffic-out") + 1], "w") as f:
+            json.dump(t, f, indent=1)
+            f.write("\n")
