@@ -66,6 +66,20 @@ def max_over_ranks(dist, v):
     return float(t.item())
 
 
+def replica_master_seed(rank: int) -> int:
+    """Each rank is an independent trajectory with its own master seed (like `scripts/simulate -s <seed>`)."""
+    return 1 + rank
+
+
+def replica_noise_seed(rank: int) -> int:
+    return 1000003 * (rank + 1)
+
+
+def whole_job_value(n: int, steps: int, world: int, el_max: float) -> float:
+    """bead-updates/s of the whole job: every rank advanced n particles by `steps`; the slowest rank sets the time."""
+    return n * steps * world / el_max
+
+
 def make_engine(design, cfg, device, start_step):
     e, _ = interphase.build_interphase(Engine, design, cfg, device=device)
     e.set_schedule(**interphase.interphase_schedule(cfg))
@@ -128,7 +142,7 @@ def main():
     world, rank, local, dist = dist_setup()
     cfg = InterphaseConfig()
     maker = {"c1": synthetic.make_c1, "c2": synthetic.make_c2, "c5": synthetic.make_c5}[args.config]
-    design = maker(master_seed=1 + rank)
+    design = maker(master_seed=replica_master_seed(rank))
     n = design.n
 
     eng = make_engine(design, cfg, local, WINDOW_START)
@@ -137,7 +151,7 @@ def main():
     eng.set_option(A.OPT_CHUNK_ORDER, args.chunk_order)
     eng.set_option(A.OPT_FUSED_STEP, args.fused)
     eng.set_option(A.OPT_XCD_TILES, args.xcd_tiles)
-    seed = 1000003 * (rank + 1)
+    seed = replica_noise_seed(rank)
 
     eng.run(args.warmup, first_step=WINDOW_START, seed=seed)
     eng.synchronize()
@@ -184,7 +198,7 @@ def main():
     if world == 1 and args.cpu_budget > 0:
         cpu = cpu_baseline(design, cfg, WINDOW_START, args.cpu_budget)
 
-    value = n * args.steps * world / el_max
+    value = whole_job_value(n, args.steps, world, el_max)
     line = {
         "metric": "bead-updates/sec (whole node), 60k-bead diploid interphase",
         "value": value,
