@@ -131,7 +131,7 @@ struct gcs_engine {
     // options / graph cache
     int graph_steps = 32;
     int waves = 4;
-    bool fused = false;  // GCS_OPT_FUSED_STEP (3-launch step); off: the 6-launch step measured faster
+    bool fused = true;  // GCS_OPT_FUSED_STEP: the 4-launch step
     hipGraphExec_t gexec = nullptr;
     hipGraph_t graph = nullptr;
     int g_steps = 0, g_waves = 0, g_version = -1, g_spacestep = -1;
@@ -406,13 +406,18 @@ void enqueue_bin(gcs_engine* e)
     launch_cell_scan(e->stream, e->ctx, n, e->count, e->cstart, e->tile_start, e->tile_range);
 }
 
-// scatter into the cells and order each cell by particle index: the cell-sorted copies the pair loop reads
+// order each (scattered) cell by particle index: the cell-sorted copies the pair loop reads
+void enqueue_cell_order(gcs_engine* e)
+{
+    launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, e->n, e->tmp, e->cell_of, e->cstart, e->sidx,
+                     e->scell, e->spos, e->sb, e->fa.has_pair ? e->fa.pair_mix : 1);
+}
+
+// scatter into the cells and order each cell by particle index
 void enqueue_sort(gcs_engine* e)
 {
-    const int n = e->n;
-    launch_cell_scatter(e->stream, n, e->cell_of, e->slot, e->cstart, e->tmp);
-    launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, n, e->tmp, e->cell_of, e->cstart, e->sidx,
-                     e->scell, e->spos, e->sb, e->fa.has_pair ? e->fa.pair_mix : 1);
+    launch_cell_scatter(e->stream, e->n, e->cell_of, e->slot, e->cstart, e->tmp, e->count);
+    enqueue_cell_order(e);
 }
 
 void enqueue_cells(gcs_engine* e)
@@ -423,15 +428,19 @@ void enqueue_cells(gcs_engine* e)
 
 bool fused_path(const gcs_engine* e, bool spacestep) { return e->fused && !spacestep; }
 
-// One BD step.  Fused (fixed timestep): scatter, sort, force (which bins the new positions and whose last block
-// runs the tail + the cell scan); begin_run binned the first positions.  Otherwise (spacestep, or fusion off):
-// count, scan, scatter, sort, force, [adapt, update], tail.
+// One BD step.  Fused (fixed timestep, 4 launches): sort the cells the previous step scattered; force + update,
+// which also bins the new positions into the predicted next grid; scan those counts; scatter them, with the
+// step's tail (reduction, schedule, wall, grid rotation) in one extra block.  begin_run binned, scanned and
+// scattered the first positions.  Otherwise (spacestep, or fusion off): count, scan, scatter, sort, force,
+// [adapt, update], tail.
 void enqueue_step(gcs_engine* e, bool spacestep, float spacestep_v, float timestep)
 {
     const int fb = force_grid(e->n);
     if (fused_path(e, spacestep)) {
-        enqueue_sort(e);
+        enqueue_cell_order(e);
         launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, true);
+        launch_cell_scan(e->stream, e->ctx, e->n, e->count, e->cstart, e->tile_start, e->tile_range, true);
+        launch_scatter_tail(e->stream, e->ctx, e->fa, e->tmp, fb, e->sched_flags != 0, e->ncell_max);
         return;
     }
     enqueue_cells(e);
@@ -498,7 +507,10 @@ int begin_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
     e->chain_valid = false;
     if (!cont) {
         launch_prime(e->stream, e->ctx, a, 0.f, e->ncell_max, e->dsched);
-        if (fused) enqueue_bin(e);
+        if (fused) {
+            enqueue_bin(e);
+            launch_cell_scatter(e->stream, e->n, e->cell_of, e->slot, e->cstart, e->tmp, e->count);
+        }
     }
     HIPCHK(hipGetLastError());
     return GCS_OK;
@@ -1074,7 +1086,7 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
     launch_prime(e->stream, e->s_ctx, sa, (float)distance, e->s_ncell_max, nullptr);
     launch_cell_count(e->stream, e->s_ctx, src, src, ni, e->s_cell_of, e->s_slot, e->s_count);
     launch_cell_scan(e->stream, e->s_ctx, ni, e->s_count, e->s_cstart, e->s_tile, e->s_tile_range);
-    launch_cell_scatter(e->stream, ni, e->s_cell_of, e->s_slot, e->s_cstart, e->s_tmp);
+    launch_cell_scatter(e->stream, ni, e->s_cell_of, e->s_slot, e->s_cstart, e->s_tmp, e->s_count);
     launch_cell_sort(e->stream, e->s_ctx, src, src, nullptr, ni, e->s_tmp, e->s_cell_of, e->s_cstart, e->s_sidx,
                      e->s_scell, e->s_spos, e->s_sb, 1);
     launch_search_count(e->stream, e->s_ctx, ni, e->s_spos, e->s_sidx, e->s_scell, e->s_cstart, e->s_counts);
@@ -1125,29 +1137,35 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
         return fail(GCS_ESTATE, "not enough injected noise for the requested steps");
     int rc = begin_run(e, cfg, first_step);
     if (rc) return rc;
-    std::vector<hipEvent_t> ev((size_t)steps * 4 + 2, nullptr);
-    // GCS_DEBUG_TIMES=<file>: per-block {start, end, smid, tile size} of the last profiled force launch
+    std::vector<hipEvent_t> ev((size_t)steps * 5 + 2, nullptr);
+    // GCS_DEBUG_TIMES=<file>: per-block timings of the last profiled force launch (see k_force)
     const char* dbg_path = std::getenv("GCS_DEBUG_TIMES");
     unsigned long long* dbg = nullptr;
-    const size_t dbg_n = (size_t)force_grid(e->n) * 4;
+    const size_t dbg_n = (size_t)force_grid(e->n) * 8;
     if (dbg_path) HIPCHK(hipMalloc(&dbg, dbg_n * sizeof(unsigned long long)));
     for (auto& x : ev) HIPCHK(hipEventCreate(&x));
     const int fb = force_grid(e->n);
     HIPCHK(hipEventRecord(ev[0], e->stream));
     const bool fused = fused_path(e, false);
+    // per step: [1] cells [2] force [3] fused: next-step scan / unfused: tail [4] fused: scatter + tail [5]
     for (int64_t k = 0; k < steps; ++k) {
-        HIPCHK(hipEventRecord(ev[1 + 4 * k], e->stream));
+        HIPCHK(hipEventRecord(ev[1 + 5 * k], e->stream));
         if (fused)
-            enqueue_sort(e);
+            enqueue_cell_order(e);
         else
             enqueue_cells(e);
-        HIPCHK(hipEventRecord(ev[2 + 4 * k], e->stream));
+        HIPCHK(hipEventRecord(ev[2 + 5 * k], e->stream));
         if (dbg && k == steps - 1) e->fa.dbg_times = dbg;
         launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, fused);
         e->fa.dbg_times = nullptr;
-        HIPCHK(hipEventRecord(ev[3 + 4 * k], e->stream));
-        if (!fused) launch_tail(e->stream, e->ctx, e->fa, fb, fb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
-        HIPCHK(hipEventRecord(ev[4 + 4 * k], e->stream));
+        HIPCHK(hipEventRecord(ev[3 + 5 * k], e->stream));
+        if (fused)
+            launch_cell_scan(e->stream, e->ctx, e->n, e->count, e->cstart, e->tile_start, e->tile_range, true);
+        else
+            launch_tail(e->stream, e->ctx, e->fa, fb, fb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
+        HIPCHK(hipEventRecord(ev[4 + 5 * k], e->stream));
+        if (fused) launch_scatter_tail(e->stream, e->ctx, e->fa, e->tmp, fb, e->sched_flags != 0, e->ncell_max);
+        HIPCHK(hipEventRecord(ev[5 + 5 * k], e->stream));
     }
     HIPCHK(hipEventRecord(ev[ev.size() - 1], e->stream));
     HIPCHK(hipGetLastError());
@@ -1155,13 +1173,16 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     HIPCHK(hipStreamSynchronize(e->stream));
     double cell = 0, force = 0, tail = 0;
     for (int64_t k = 0; k < steps; ++k) {
-        float a = 0, b = 0, c = 0;
-        HIPCHK(hipEventElapsedTime(&a, ev[1 + 4 * k], ev[2 + 4 * k]));
-        HIPCHK(hipEventElapsedTime(&b, ev[2 + 4 * k], ev[3 + 4 * k]));
-        HIPCHK(hipEventElapsedTime(&c, ev[3 + 4 * k], ev[4 + 4 * k]));
-        cell += a;
-        force += b;
-        tail += c;
+        float t[4] = {0, 0, 0, 0};
+        for (int q = 0; q < 4; ++q) HIPCHK(hipEventElapsedTime(&t[q], ev[1 + q + 5 * k], ev[2 + q + 5 * k]));
+        force += t[1];
+        if (fused) {
+            cell += t[0] + t[2];  // sort + scan
+            tail += t[3];         // scatter + tail
+        } else {
+            cell += t[0];
+            tail += t[2] + t[3];
+        }
     }
     float tot = 0;
     HIPCHK(hipEventElapsedTime(&tot, ev[0], ev[ev.size() - 1]));
@@ -1184,15 +1205,19 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     out->force_ms = force / (double)steps;
     out->cell_ms = cell / (double)steps;
     out->tail_ms = tail / (double)steps;
-    if (fused) {  // the tail runs inside the force launch: report its last-block section (last step)
+    if (std::getenv("GCS_DEBUG")) {
         int khz = 0;
         HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, e->device));
-        out->tail_ms = khz > 0 ? (double)(d.t_last[3] - d.t_last[0]) / (double)khz : 0.0;
-        if (std::getenv("GCS_DEBUG") && khz > 0)
-            std::fprintf(stderr, "gcs: grid %d x %d x %d (%d cells), ntiles %d; last block: tail %.2f us, scan %.2f us, "
-                         "rows %.2f us\n", d.grid.n[0], d.grid.n[1], d.grid.n[2], d.grid.ncell, d.ntiles,
-                         1e3 * (d.t_last[1] - d.t_last[0]) / khz, 1e3 * (d.t_last[2] - d.t_last[1]) / khz,
-                         1e3 * (d.t_last[3] - d.t_last[2]) / khz);
+        if (khz > 0)
+            std::fprintf(stderr, "gcs: grid %d x %d x %d (%d cells), ntiles %d; k_cell_scan body: cells %.2f us, "
+                         "rows %.2f us; k_tail body %.2f us\n", d.grid.n[0], d.grid.n[1], d.grid.n[2], d.grid.ncell,
+                         d.ntiles, 1e3 * (d.t_last[2] - d.t_last[1]) / khz, 1e3 * (d.t_last[3] - d.t_last[2]) / khz,
+                         1e3 * (d.t_tail[1] - d.t_tail[0]) / khz);
+        if (khz > 0)
+            std::fprintf(stderr, "gcs: rows probes: cellpass->rows %.2f, rows scan %.2f, barrier %.2f, stores %.2f, "
+                         "->end %.2f us\n", 1e3 * (d.t_rows[0] - d.t_last[2]) / khz,
+                         1e3 * (d.t_rows[1] - d.t_rows[0]) / khz, 1e3 * (d.t_rows[2] - d.t_rows[1]) / khz,
+                         1e3 * (d.t_rows[3] - d.t_rows[2]) / khz, 1e3 * (d.t_last[3] - d.t_rows[3]) / khz);
     }
     out->mean_neighbors = d.neighbors;
     return GCS_OK;

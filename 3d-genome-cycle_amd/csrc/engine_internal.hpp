@@ -52,6 +52,8 @@ struct DevCtx {
     Grid grid_next;        // bins the positions the next step produces (fused path)
     unsigned ticket;       // arrival counter of the fused force kernel's blocks (0 between launches)
     int pad1;
+    unsigned long long t_tail[2];  // wall clock at the start / end of k_tail
+    unsigned long long t_rows[4];  // wall clock probes inside the cell scan's row pass (GCS_DEBUG)
     unsigned long long t_last[4];  // wall clock: fused last-block section start, after tail, after scan, end
 };
 
@@ -134,7 +136,7 @@ struct ForceArgs {
     int ncell_max;
     int apply_sched;
     int xcd_tiles;  // 1: each XCD takes one contiguous run of tiles (GCS_OPT_XCD_TILES)
-    unsigned long long* dbg_times;  // optional (GCS_DEBUG_TIMES): per block {start, end, tiles, candidates} wall clock
+    unsigned long long* dbg_times;  // optional (GCS_DEBUG_TIMES): per block {start, end, smid/candidates, tile} then 4 phase stamps
 };
 
 // ---- Philox4x32-10 + Box-Muller: the production noise stream (identical on host for the oracle) ----
@@ -163,8 +165,12 @@ __host__ __device__ inline void philox4x32_10(unsigned c[4], unsigned k0, unsign
 void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed, int ncell_max, const double* sched);
 void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n,
                        int* cell_of, int* slot, int* count);
-void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start, int2* tile_range);
-void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* slot, const int* cstart, int* tmp);
+void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start, int2* tile_range,
+                      bool use_next = false);
+void launch_scatter_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int* tmp, int fblocks, int apply_sched,
+                         int ncell_max);
+void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* slot, const int* cstart, int* tmp,
+                         int* count);
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, const float4* kmu,
                       int n, const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell,
                       float4* spos, float* sb, int pair_mix);

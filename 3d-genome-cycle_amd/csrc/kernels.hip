@@ -23,14 +23,8 @@ namespace gcs {
 
 namespace {
 
-// Write-through (sc1) stores and L1-bypassing (sc1) loads: the cross-workgroup hand-off of the fused step
-// (per-block partials and cell counts -> the last block) without a release fence (MI355X_MICROARCH.md
-// "Valid forms", first row: sc1 stores drained by s_waitcnt, one agent-scope ticket add per block, sc1 loads).
-__device__ __forceinline__ void st_sc1(float* p, float v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// 16-B sc1 load through a buffer descriptor (out-of-range offsets read 0)
+// 16-B L1-bypassing (sc1) load through a buffer descriptor (out-of-range offsets read 0): the single-block
+// reductions read data written by other CUs once, so there is nothing to gain from L1
 __device__ __forceinline__ float4 ld_sc1_f4(__amdgpu_buffer_rsrc_t r, int byte_off)
 {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
@@ -45,11 +39,72 @@ __device__ __forceinline__ int4 ld_sc1_i4(__amdgpu_buffer_rsrc_t r, int byte_off
     __builtin_memcpy(&f, &v, 16);
     return f;
 }
-__device__ inline double wave_max_d(double v)
+// DPP wave primitives (GFX9 row_shr / row_bcast): an inclusive scan in 6 DPP steps without LDS.  Lanes whose
+// DPP source is out of range take `ident` (bound_ctrl off, old = ident).  After the sequence lane l holds
+// op(x_0 .. x_l); lane 63 holds the wave total.  Fixed combination order: bitwise reproducible.
+template <int CTRL, int RM>
+__device__ __forceinline__ int dpp_i(int ident, int x)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return __builtin_amdgcn_update_dpp(ident, x, CTRL, RM, 0xf, false);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ float dpp_f(float ident, float x)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(ident), __float_as_int(x), CTRL, RM, 0xf, false));
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp_d(double ident, double x)
+{
+    const long long o = __double_as_longlong(ident), v = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_update_dpp((int)o, (int)v, CTRL, RM, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(v >> 32), CTRL, RM, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+#define GCS_DPP_SCAN(DPP, OP, IDENT, X)              \
+    X = OP(X, DPP<0x111, 0xf>(IDENT, X)); /* shr 1 */ \
+    X = OP(X, DPP<0x112, 0xf>(IDENT, X)); /* shr 2 */ \
+    X = OP(X, DPP<0x114, 0xf>(IDENT, X)); /* shr 4 */ \
+    X = OP(X, DPP<0x118, 0xf>(IDENT, X)); /* shr 8 */ \
+    X = OP(X, DPP<0x142, 0xa>(IDENT, X)); /* bcast 15 -> rows 1, 3 */ \
+    X = OP(X, DPP<0x143, 0xc>(IDENT, X)); /* bcast 31 -> rows 2, 3 */
+
+__device__ __forceinline__ int add_i(int a, int b) { return a + b; }
+__device__ __forceinline__ double add_d(double a, double b) { return a + b; }
+__device__ __forceinline__ float min_f(float a, float b) { return fminf(a, b); }
+__device__ __forceinline__ float max_f(float a, float b) { return fmaxf(a, b); }
+__device__ __forceinline__ double max_d(double a, double b) { return fmax(a, b); }
+
+__device__ __forceinline__ int wave_incl_scan_dpp(int v)
+{
+    GCS_DPP_SCAN(dpp_i, add_i, 0, v)
     return v;
+}
+__device__ __forceinline__ double lane63_d(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+__device__ __forceinline__ float lane63_f(float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63)); }
+__device__ __forceinline__ double wave_total_sum_d(double v)
+{
+    GCS_DPP_SCAN(dpp_d, add_d, 0.0, v)
+    return lane63_d(v);
+}
+__device__ __forceinline__ double wave_total_max_d(double v)
+{
+    GCS_DPP_SCAN(dpp_d, max_d, -1.0e300, v)
+    return lane63_d(v);
+}
+__device__ __forceinline__ float wave_total_min_f(float v)
+{
+    GCS_DPP_SCAN(dpp_f, min_f, 3.0e38f, v)
+    return lane63_f(v);
+}
+__device__ __forceinline__ float wave_total_max_f(float v)
+{
+    GCS_DPP_SCAN(dpp_f, max_f, -3.0e38f, v)
+    return lane63_f(v);
 }
 
 __device__ inline float wave_sum(float v)
@@ -78,9 +133,8 @@ __device__ inline float wave_min(float v)
 }
 
 __device__ inline int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ inline float uniform_f(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 
-// keeps a value "used" so a float4 LDS read stays one ds_read_b128
-__device__ inline void keep_live(float v) { asm volatile("" ::"v"(v)); }
 
 __device__ inline int wave_max_int(int v)
 {
@@ -243,22 +297,108 @@ __device__ inline int wave_incl_scan(int v, int lane)
     return v;
 }
 
-// Exclusive scan count -> cstart over the grid's cells in coalesced tiles of 4 cells per thread (int4) with a
-// running carry, re-zeroing count for the next step; then the per-row tile table of k_force (a tile is <= 64
-// consecutive sorted particles of ONE row of cells).  count/cstart are padded by kScanPad so whole tiles may be
-// touched; entries past ncell are zero by invariant.  Any block size that is a multiple of 64 (<= 1024).
-__device__ __forceinline__ void scan_cells_body(DevCtx* __restrict__ ctx, int n, int* __restrict__ count,
-                                                int* __restrict__ cstart, int* __restrict__ tile_start,
-                                                int2* __restrict__ tile_range)
+// Exclusive scan count -> cstart over the grid's cells, kScanSeg consecutive cells per thread (16-B loads, the
+// next iteration's issued before this one's scan) with a running carry, re-zeroing count for the next step; then
+// the per-row tile table of k_force (a tile is <= 64 consecutive sorted particles of ONE row of cells).  Wave
+// scans are DPP (no LDS round trips); the wave totals are double-buffered in LDS, so each iteration has one
+// barrier.  Row starts are captured in LDS during the cell pass (rows <= kRowsLds), so the row pass does not
+// re-read cstart.  count/cstart are padded by kScanPad so whole iterations may be touched; entries past ncell
+// are zero by invariant.  Any block size that is a multiple of 64 (<= 1024).
+constexpr int kRowsLds = 4096;
+
+// Row pass of the cell scan: tiles per row, their prefix (tile_start) and the tile table.  Row starts come from
+// LDS (LDS = true) or from cstart; two instantiations so the LDS path carries no global-load wait (on gfx9
+// vmcnt also counts the cell pass's stores).
+template <bool LDS>
+__device__ __forceinline__ void scan_rows(DevCtx* __restrict__ ctx, const int* s_rowbeg, const int* __restrict__ cstart,
+                                          int nx, int nrows, int* __restrict__ tile_start,
+                                          int2* __restrict__ tile_range, int (*wtot)[16], int it, int* s_tstart)
 {
-    __shared__ int wtot[16];
-    __shared__ int tile_total;
-    const int nc = ctx->grid.ncell;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     int carry = 0;
+    const int span = 4 * blockDim.x;
+    if (tid == 0) ctx->t_rows[0] = wall_clock64();
+    for (int base = 0; base < nrows; base += span, ++it) {
+        int beg[5];  // starts of rows base + 4 tid + q, q = 0..4
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const int r = base + 4 * tid + q;
+            beg[q] = (r <= nrows) ? (LDS ? s_rowbeg[r] : cstart[r * nx]) : 0;
+        }
+        int c[4];
+        int sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = base + 4 * tid + q;
+            c[q] = (r < nrows) ? (beg[q + 1] - beg[q] + kTile - 1) / kTile : 0;
+            sum += c[q];
+        }
+        const int incl = wave_incl_scan_dpp(sum);
+        if (tid == 0) ctx->t_rows[1] = wall_clock64();
+        if (lane == 63) wtot[it & 1][wave] = incl;
+        __syncthreads();
+        if (tid == 0) ctx->t_rows[2] = wall_clock64();
+        int woff = 0, ttot = 0;
+        for (int w = 0; w < nw; ++w) {
+            const int t = wtot[it & 1][w];
+            woff += (w < wave) ? t : 0;
+            ttot += t;
+        }
+        int run = carry + woff + incl - sum;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = base + 4 * tid + q;
+            if (r < nrows) {
+                if (LDS) {
+                    s_tstart[r] = run;
+                } else {
+                    tile_start[r] = run;
+                    const int rb = beg[q], re = beg[q + 1];
+                    for (int k = 0; k < c[q]; ++k)
+                        tile_range[run + k] = make_int2(rb + k * kTile, min(re, rb + (k + 1) * kTile));
+                }
+            }
+            run += c[q];
+        }
+        carry += ttot;
+    }
+    if (LDS) {
+        // tile-parallel table: thread t writes tiles t, t + blockDim, ... (coalesced); its row by binary search
+        if (tid == 0) s_tstart[nrows] = carry;
+        __syncthreads();
+        for (int k = tid; k < carry; k += blockDim.x) {
+            int lo = 0, hi = nrows;  // last row r with s_tstart[r] <= k (that row is non-empty)
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (s_tstart[mid] <= k)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            const int j = k - s_tstart[lo], rb = s_rowbeg[lo], re = s_rowbeg[lo + 1];
+            tile_range[k] = make_int2(rb + j * kTile, min(re, rb + (j + 1) * kTile));
+        }
+    }
+    if (tid == 0) {
+        tile_start[nrows] = carry;
+        ctx->ntiles = carry;
+        ctx->t_rows[3] = wall_clock64();
+    }
+}
+
+__device__ __forceinline__ void scan_cells_body(DevCtx* __restrict__ ctx, int n, int* __restrict__ count,
+                                                int* __restrict__ cstart, int* __restrict__ tile_start,
+                                                int2* __restrict__ tile_range, bool use_next)
+{
+    const Grid& g = use_next ? ctx->grid_next : ctx->grid;
+    __shared__ int wtot[2][16];
+    __shared__ int s_rowbeg[kRowsLds + 1];
+    __shared__ int s_tstart[kRowsLds + 1];
+    const int nc = g.ncell, nx = g.n[0], nrows = g.n[1] * g.n[2];
+    const bool rows_lds = nrows <= kRowsLds;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    int carry = 0, it = 0;
     {
-        // kScanSeg consecutive cells per thread as 16-B sc1 loads (in the fused step the counts were produced by
-        // other workgroups' atomics in this launch); the next iteration's loads are issued before this one's scan
         static_assert(kScanSeg % 4 == 0, "kScanSeg counts are loaded as int4");
         constexpr int kQ = kScanSeg / 4;
         const int span = kScanSeg * blockDim.x;
@@ -266,102 +406,110 @@ __device__ __forceinline__ void scan_cells_body(DevCtx* __restrict__ ctx, int n,
         int4 cur[kQ];
 #pragma unroll
         for (int q = 0; q < kQ; ++q) cur[q] = ld_sc1_i4(rc, (kScanSeg * tid + 4 * q) * 4);
-        for (int base = 0; base < nc; base += span) {
+        for (int base = 0; base < nc; base += span, ++it) {
             const int i0 = base + kScanSeg * tid;
             int4 nxt[kQ];
             if (base + span < nc) {
 #pragma unroll
                 for (int q = 0; q < kQ; ++q) nxt[q] = ld_sc1_i4(rc, (i0 + span + 4 * q) * 4);
             }
+            int pre[kScanSeg];  // exclusive prefix inside the thread's segment
             int sum = 0;
 #pragma unroll
-            for (int q = 0; q < kQ; ++q) sum += cur[q].x + cur[q].y + cur[q].z + cur[q].w;
-            const int incl = wave_incl_scan(sum, lane);
-            if (lane == 63) wtot[wave] = incl;
-            __syncthreads();
-            if (wave == 0) {
-                const int w = lane < nw ? wtot[lane] : 0;
-                const int wi = wave_incl_scan(w, lane);
-                if (lane < nw) wtot[lane] = wi - w;
-                if (lane == nw - 1) tile_total = wi;
-            }
-            __syncthreads();
-            int run = carry + wtot[wave] + incl - sum;
-#pragma unroll
             for (int q = 0; q < kQ; ++q) {
-                const int4 c = cur[q];
-                *reinterpret_cast<int4*>(cstart + i0 + 4 * q) =
-                    make_int4(run, run + c.x, run + c.x + c.y, run + c.x + c.y + c.z);
-                run += c.x + c.y + c.z + c.w;
-                *reinterpret_cast<int4*>(count + i0 + 4 * q) = make_int4(0, 0, 0, 0);
+                pre[4 * q] = sum;
+                pre[4 * q + 1] = sum + cur[q].x;
+                pre[4 * q + 2] = sum + cur[q].x + cur[q].y;
+                pre[4 * q + 3] = sum + cur[q].x + cur[q].y + cur[q].z;
+                sum += cur[q].x + cur[q].y + cur[q].z + cur[q].w;
             }
-            carry += tile_total;
+            const int incl = wave_incl_scan_dpp(sum);
+            if (lane == 63) wtot[it & 1][wave] = incl;
             __syncthreads();
+            int woff = 0, ttot = 0;
+            for (int w = 0; w < nw; ++w) {
+                const int t = wtot[it & 1][w];
+                woff += (w < wave) ? t : 0;
+                ttot += t;
+            }
+            const int run = carry + woff + incl - sum;
+#pragma unroll
+            for (int q = 0; q < kQ; ++q)  // (count is re-zeroed by the scatter, which knows the occupied cells)
+                if (i0 + 4 * q < nc)
+                    *reinterpret_cast<int4*>(cstart + i0 + 4 * q) =
+                        make_int4(run + pre[4 * q], run + pre[4 * q + 1], run + pre[4 * q + 2], run + pre[4 * q + 3]);
+            if (rows_lds && i0 < nc) {  // row boundaries r * nx inside [i0, i0 + kScanSeg)
+                int r = (i0 + nx - 1) / nx;
+                for (int b = r * nx; b < i0 + kScanSeg && b < nc; b += nx, ++r) {
+                    int v = 0;
+#pragma unroll
+                    for (int q = 0; q < kScanSeg; ++q) v = (b - i0 == q) ? pre[q] : v;
+                    s_rowbeg[r] = run + v;
+                }
+            }
+            carry += ttot;
 #pragma unroll
             for (int q = 0; q < kQ; ++q) cur[q] = nxt[q];
         }
     }
     if (tid == 0) {
         cstart[nc] = n;
+        if (rows_lds) s_rowbeg[nrows] = n;
         ctx->t_last[2] = wall_clock64();
     }
     __syncthreads();
-    const int nx = ctx->grid.n[0], nrows = ctx->grid.n[1] * ctx->grid.n[2];
-    carry = 0;
-    const int span = 4 * blockDim.x;
-    for (int base = 0; base < nrows; base += span) {
-        int c[4];
-        int sum = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int r = base + 4 * tid + q;
-            c[q] = (r < nrows) ? (cstart[(r + 1) * nx] - cstart[r * nx] + kTile - 1) / kTile : 0;
-            sum += c[q];
-        }
-        const int incl = wave_incl_scan(sum, lane);
-        if (lane == 63) wtot[wave] = incl;
-        __syncthreads();
-        if (wave == 0) {
-            const int w = lane < nw ? wtot[lane] : 0;
-            const int wi = wave_incl_scan(w, lane);
-            if (lane < nw) wtot[lane] = wi - w;
-            if (lane == nw - 1) tile_total = wi;
-        }
-        __syncthreads();
-        int run = carry + wtot[wave] + incl - sum;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int r = base + 4 * tid + q;
-            if (r < nrows) {
-                tile_start[r] = run;
-                const int rb = cstart[r * nx], re = cstart[(r + 1) * nx];
-                for (int k = 0; k < c[q]; ++k)
-                    tile_range[run + k] = make_int2(rb + k * kTile, min(re, rb + (k + 1) * kTile));
-            }
-            run += c[q];
-        }
-        carry += tile_total;
-        __syncthreads();
-    }
-    if (tid == 0) {
-        tile_start[nrows] = carry;
-        ctx->ntiles = carry;
-    }
+    if (rows_lds)
+        scan_rows<true>(ctx, s_rowbeg, cstart, nx, nrows, tile_start, tile_range, wtot, it, s_tstart);
+    else
+        scan_rows<false>(ctx, s_rowbeg, cstart, nx, nrows, tile_start, tile_range, wtot, it, s_tstart);
 }
 
 __global__ __launch_bounds__(1024) void k_cell_scan(DevCtx* __restrict__ ctx, int n, int* __restrict__ count,
                                                     int* __restrict__ cstart, int* __restrict__ tile_start,
-                                                    int2* __restrict__ tile_range)
+                                                    int2* __restrict__ tile_range, int use_next)
 {
-    scan_cells_body(ctx, n, count, cstart, tile_start, tile_range);
+    const unsigned long long t0 = wall_clock64();
+    scan_cells_body(ctx, n, count, cstart, tile_start, tile_range, use_next != 0);
+    if (threadIdx.x == 0) {
+        ctx->t_last[0] = ctx->t_last[1] = t0;
+        ctx->t_last[3] = wall_clock64();
+    }
+}
+
+__device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance,
+                                          int apply_sched, int ncell_max, const double* __restrict__ sched, bool fused);
+
+// fused step: the scatter of the next step's cells, and in one extra block the tail of the step just computed
+// (partials -> reactions, schedule, wall; grid <- grid_next and the grid after it).  The scatter blocks touch
+// no DevCtx field, so the tail block owns the context.
+__global__ __launch_bounds__(256) void k_scatter_tail(DevCtx* ctx, ForceArgs a, int n, int* __restrict__ tmp,
+                                                      int fblocks, int apply_sched, int ncell_max)
+{
+    if (blockIdx.x == gridDim.x - 1) {
+        const unsigned long long t0 = wall_clock64();
+        tail_body(ctx, a, fblocks, fblocks, 1, apply_sched, ncell_max, a.sched, true);
+        if (threadIdx.x == 0) {
+            ctx->t_tail[0] = t0;
+            ctx->t_tail[1] = wall_clock64();
+        }
+        return;
+    }
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int c = a.cell_of[i];
+    tmp[a.cstart_w[c] + a.slot[i]] = i;
+    a.count[c] = 0;  // every occupied cell has a particle here: count is all-zero again for the next binning
 }
 
 __global__ __launch_bounds__(256) void k_cell_scatter(int n, const int* __restrict__ cell_of, const int* __restrict__ slot,
-                                                      const int* __restrict__ cstart, int* __restrict__ tmp)
+                                                      const int* __restrict__ cstart, int* __restrict__ tmp,
+                                                      int* __restrict__ count)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    tmp[cstart[cell_of[i]] + slot[i]] = i;
+    const int c = cell_of[i];
+    tmp[cstart[c] + slot[i]] = i;
+    count[c] = 0;  // every occupied cell has a particle here: count is all-zero again for the next binning
 }
 
 __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ctx, const float4* __restrict__ p0,
@@ -629,10 +777,17 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
 // [x_first - fx, x_last + fx] (x cells are rc / fx wide).  Candidates are staged 64 at a time in LDS
 // (software-pipelined), filtered in fp32 into a per-lane 64-bit hit mask, and the soft-core potential is
 // evaluated for the hits only.
+//
+// Tile frame: coordinates are taken relative to the tile's first particle and each staged candidate record is
+// {-2x', -2y', -2z', |x'|^2, kA a_j, kB b_j}, so the phase-1 test  |x_j'|^2 - 2 x_i'.x_j' < rc^2 - |x_i'|^2  is
+// three fma + compare (|x'| stays within the stencil, so the form is well conditioned: an error ~1e-7 rc^2
+// only moves pairs at the cutoff, where the potential and its force vanish), and phase 2 recovers
+// x_i - x_j = x_i' + (-2x_j')/2 exactly from the record.  Slot kTile holds a far-away sentinel record: an
+// exhausted hit mask points there and contributes exactly zero (no per-hit activity mask).
 template <int MODE, int WAVES>
 __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceArgs& a, int wave, int lane, int s,
                                    int s_begin, int s_end, float4 pi, float bi, float& fx, float& fy, float& fz,
-                                   float& acc, int* s_rowV, int* s_rowJ, float4* s_cand, float* s_candb, int* s_candj)
+                                   float& acc, int* s_rowV, int* s_rowJ, float4* s_cand, int* s_candj, int& ntot)
 {
     const Grid g = ctx->grid;
     const float cs = (float)ctx->cs;
@@ -640,10 +795,9 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
     const float sa = a.pa_sig * scale, sbb = a.pb_sig * scale;
     const float k2a = 1.f / (sa * sa), k2b = 1.f / (sbb * sbb);
     // F = coef * (x_i - x_j):  A * 6 eps_a k2a ga^2  +  B * 24 eps_b k2b gb^2 t^3   (A, B = pair means)
-    const float ca = 0.5f * 6.f * a.pa_eps * k2a;
-    const float cb = 0.5f * 24.f * a.pb_eps * k2b;
-    const float ea = 0.25f * a.pa_eps;  // energy: 1/2 (mean) x 1/2 (each pair seen from both ends)
-    const float eb = 0.25f * a.pb_eps;
+    // energy: 1/2 (mean) x 1/2 (each pair seen from both ends) x eps (A ga^3 + B gb^3)
+    const float kA = (MODE == kModeEnergy) ? 0.25f * a.pa_eps : 0.5f * 6.f * a.pa_eps * k2a;
+    const float kB = (MODE == kModeEnergy) ? 0.25f * a.pb_eps : 0.5f * 24.f * a.pb_eps * k2b;
     const float rc2 = g.rc2;
     const int nx = g.n[0], ny = g.n[1], nz = g.n[2], gfx = g.fx;
     const int c0 = uniform(a.scell[s_begin]), c1 = uniform(a.scell[s_end - 1]);
@@ -669,9 +823,20 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
         }
         if (lane == 15) s_rowV[16] = incl;
     }
+    // tile frame and the sentinel record
+    const float ox = uniform_f(pi.x), oy = uniform_f(pi.y), oz = uniform_f(pi.z);
+    const float xi = pi.x - ox, yi = pi.y - oy, zi = pi.z - oz;
+    const float thr = rc2 - fmaf(zi, zi, fmaf(yi, yi, xi * xi));
+    const float far = 1.0e3f * fmaxf(g.rc, 1.f);
+    const float4 sent0 = make_float4(-2.f * far, -2.f * far, -2.f * far, 3.f * far * far);
+    if (lane == 0) {
+        s_cand[2 * kTile] = sent0;
+        s_cand[2 * kTile + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     __builtin_amdgcn_wave_barrier();
     const int total = uniform(s_rowV[16]);
-    const float ahi = pi.w, bhi = bi;
+    ntot = total;
+    const float ahi = kA * pi.w, bhi = kB * bi;
     // Chunk c of this wave holds candidates v = first(c) + stride * lane, lane < count(c).
     //   contiguous (chunk_mode 0): the wave's share [wlo, whi) in runs of 64
     //   strided    (chunk_mode 1): chunk g of G = ceil(total / 64) takes v = g + G * lane; wave w owns the
@@ -689,10 +854,9 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
         return strided ? min(kTile, (total - f + G - 1) / G) : min(kTile, whi - f);
     };
 
+    // raw loads only (consumed one chunk later: the loads stay in flight over the current chunk)
     auto fetch = [&](int c, float4& p, float& b, int& jj) {
         const int v = first(c) + stride * lane;
-        p = make_float4(1e18f, 1e18f, 1e18f, 0.f);  // far-away sentinel: never a hit
-        b = 0.f;
         jj = -1;
         if (lane < count(c)) {
             int lo = 0;  // last stencil row starting at or before v (rows 9..15 start at `total`)
@@ -704,40 +868,47 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
             b = a.sb[jj];
         }
     };
-    float4 npj;
-    float nbj;
-    int njj;
+    // two chunks in flight: the load latency (an L2 miss under load is microseconds) outlasts one chunk's work
+    float4 npj, npj2;
+    float nbj, nbj2;
+    int njj, njj2 = -1;
     if (nchunk > 0) fetch(0, npj, nbj, njj);
+    if (nchunk > 1) fetch(1, npj2, nbj2, njj2);
     for (int c = 0; c < nchunk; ++c) {
         const int cnt = uniform(count(c));
         const int cnt8 = (cnt + 7) & ~7;  // sentinel-padded to a multiple of 8
-        s_cand[lane] = npj;
-        s_candb[lane] = nbj;
-        if (MODE == kModeEnergy) s_candj[lane] = njj;
+        {
+            const bool real = njj >= 0;
+            const float px = real ? npj.x - ox : far, py = real ? npj.y - oy : far, pz = real ? npj.z - oz : far;
+            s_cand[2 * lane] = make_float4(-2.f * px, -2.f * py, -2.f * pz, fmaf(pz, pz, fmaf(py, py, px * px)));
+            s_cand[2 * lane + 1] = make_float4(real ? kA * npj.w : 0.f, real ? kB * nbj : 0.f, 0.f, 0.f);
+            if (MODE == kModeEnergy) s_candj[lane] = njj;
+        }
         __builtin_amdgcn_wave_barrier();
-        if (c + 1 < nchunk) fetch(c + 1, npj, nbj, njj);  // next chunk in flight
+        npj = npj2;
+        nbj = nbj2;
+        njj = njj2;
+        if (c + 2 < nchunk) fetch(c + 2, npj2, nbj2, njj2);  // two chunks ahead
 
-        // phase 1: distance filter over the chunk; each lane keeps a 64-bit mask of its hits.  Within a group
-        // of 8 candidates the mask byte is built as byte = 2 byte + hit (v_cmp + v_addc: 2 VALU per test), so
-        // candidate k0 + u lands on bit k0 + 7 - u (decoded by k = bit ^ 7).
+        // phase 1: one fma chain + compare per candidate; each lane keeps a 64-bit mask of its hits.  Within a
+        // group of 8 candidates the mask byte is built as byte = 2 byte + hit (v_cmp + v_addc), so candidate
+        // k0 + u lands on bit k0 + 7 - u (decoded by k = bit ^ 7).
         unsigned mlo = 0u, mhi = 0u;
         for (int k0 = 0; k0 < cnt8; k0 += 8) {
             unsigned byte = 0u;
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const float4 pj = s_cand[k0 + u];
-                keep_live(pj.w);  // one ds_read_b128 (4 LDS cycles) instead of a ds_read_b96 (8)
-                const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
-                const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                const float4 q = s_cand[2 * (k0 + u)];
+                const float t = fmaf(q.x, xi, fmaf(q.y, yi, fmaf(q.z, zi, q.w)));
                 if (MODE == kModeEnergy) {
-                    const bool in = (r2 < rc2) && (s_candj[k0 + u] != s);
+                    const bool in = (t < thr) && (s_candj[k0 + u] != s);
                     byte = 2u * byte + (in ? 1u : 0u);
                 } else {
                     // the self pair contributes exactly zero force (F is proportional to x_i - x_j), so the force
                     // path keeps it (one wasted slot) instead of paying a second compare per candidate
                     asm("v_cmp_gt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
                         : "+v"(byte)
-                        : "v"(rc2), "v"(r2)
+                        : "v"(thr), "v"(t)
                         : "vcc");
                 }
             }
@@ -746,50 +917,44 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
             else
                 mhi |= byte << (k0 - 32);
         }
-        const int nh = __popc(mlo) + __popc(mhi);
-        if (MODE != kModeEnergy) acc += (float)nh;
-        // phase 2: the potential on the hits only (iterations = the wave's largest hit count), four
-        // independent hits per iteration so their LDS gathers overlap
-        const int mh = uniform(wave_max_int(nh));
-        for (int t = 0; t < mh; t += 4) {
-            int kk[4];
-            bool av[4];
+        if (MODE != kModeEnergy) acc += (float)(__popc(mlo) + __popc(mhi));
+        // phase 2: the potential on the hits only, one 32-bit half of the mask after the other (iterations =
+        // the wave's largest hit count in that half), four independent hits per iteration so their LDS reads
+        // overlap.  Pop = ffbl, xor, min (exhausted -> the sentinel slot), clear lowest bit.
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {  // pop the lowest set bits
-                av[u] = (mlo | mhi) != 0u;
-                const int klo = __ffs(mlo) - 1, khi = __ffs(mhi) + 31;
-                kk[u] = av[u] ? ((mlo ? klo : khi) ^ 7) : 0;  // bit -> candidate; inactive: a valid slot, no NaN
-                if (mlo)
-                    mlo &= mlo - 1u;
-                else
-                    mhi &= mhi - 1u;
-            }
+        for (int h = 0; h < 2; ++h) {
+            unsigned m = h ? mhi : mlo;
+            const float4* base = s_cand + 2 * (h ? 32 : 0);
+            const unsigned lim = h ? 32u : 64u;
+            const int mh = uniform(wave_max_int(__popc(m)));
+            for (int t = 0; t < mh; t += 4) {
+                unsigned kk[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const bool act = av[u];
-                const float4 pj = s_cand[kk[u]];
-                const float bj = s_candb[kk[u]];
-                const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
-                const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                const float A = ahi + pj.w, B = bhi + bj;
-                const float ua = r2 * k2a;
-                const float ga = 1.f - ua;
-                const float tt = r2 * k2b;
-                const float t2 = tt * tt;
-                const float gb = 1.f - t2 * t2;
-                const float gb2 = gb * gb;
-                const bool ina = act && (ua < 1.f);
-                const bool inb = act && (tt < 1.f);
-                if (MODE == kModeEnergy) {
-                    const float ua3 = ga * ga * ga, ub3 = gb2 * gb;
-                    acc += (ina ? A * ea * ua3 : 0.f) + (inb ? B * eb * ub3 : 0.f);
-                } else {
-                    const float fa = ina ? ga * ga : 0.f;
-                    const float fb = inb ? gb2 * t2 * tt : 0.f;
-                    const float coef = fmaf(A * ca, fa, B * cb * fb);
-                    fx = fmaf(coef, dx, fx);
-                    fy = fmaf(coef, dy, fy);
-                    fz = fmaf(coef, dz, fz);
+                for (int u = 0; u < 4; ++u) {
+                    unsigned b;
+                    asm("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(m));  // 0xffffffff when m == 0
+                    kk[u] = min(b ^ 7u, lim);
+                    m &= m - 1u;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float4 q = base[2 * kk[u]];
+                    const float4 w = base[2 * kk[u] + 1];
+                    const float dx = fmaf(0.5f, q.x, xi), dy = fmaf(0.5f, q.y, yi), dz = fmaf(0.5f, q.z, zi);
+                    const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                    const float ga = fmaxf(fmaf(-k2a, r2, 1.f), 0.f);
+                    const float tt = r2 * k2b;
+                    const float t2 = tt * tt;
+                    const float gb = fmaxf(fmaf(-t2, t2, 1.f), 0.f);
+                    const float A = ahi + w.x, B = bhi + w.y;
+                    if (MODE == kModeEnergy) {
+                        acc += fmaf(A, ga * ga * ga, B * (gb * gb * gb));
+                    } else {
+                        const float coef = fmaf(A, ga * ga, B * (gb * gb * t2 * tt));
+                        fx = fmaf(coef, dx, fx);
+                        fy = fmaf(coef, dy, fy);
+                        fz = fmaf(coef, dz, fz);
+                    }
                 }
             }
         }
@@ -805,17 +970,16 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
 __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance,
                                           int apply_sched, int ncell_max, const double* __restrict__ sched, bool fused);
 
-// FUSED (kModeStep only): the new positions are also binned into ctx->grid_next (count atomics), and the last
-// block to finish (arrival ticket, agent-scope release/acquire: cdna_hip_programming.md G16) runs the schedule
-// tail and the cell scan for the next step, so a step is three launches: scatter, sort, force.
+// FUSED (kModeStep only): the new positions are also binned into ctx->grid_next (one wave-aggregated count
+// atomic per run of equal cells), so the next step's cell list needs only scan + scatter + sort (engine.hip
+// enqueue_step).
 template <int MODE, int WAVES, bool FUSED>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5))) void k_force(DevCtx* __restrict__ ctx, ForceArgs a)
 {
     __shared__ float red[WAVES > 1 ? WAVES : 1][4][64];
     __shared__ int s_rowV[WAVES][17];
     __shared__ int s_rowJ[WAVES][16];
-    __shared__ float4 s_cand[WAVES][kTile];
-    __shared__ float s_candb[WAVES][kTile];
+    __shared__ float4 s_cand[WAVES][2 * (kTile + 1)];  // candidate records (2 x float4) + sentinel
     __shared__ int s_candj[MODE == kModeEnergy ? WAVES : 1][kTile];
     __shared__ float s_pr[kForcePartials + kBBoxPartials];  // per-block accumulators (lane 0 of wave 0)
     __shared__ double s_pe[kEnergyKinds];
@@ -832,6 +996,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     }
 
     const unsigned long long t_start = a.dbg_times ? wall_clock64() : 0ull;
+    __shared__ unsigned long long s_dbg[4];  // GCS_DEBUG_TIMES: pair start, pair end (wave 0), local start, end
     // XCD-aware tile order (a.xcd_tiles): workgroups are dispatched round-robin over the 8 XCDs, so block b runs
     // on XCD b & 7; give each XCD one contiguous run of tiles (a slab of cell rows) so its private L2 holds one
     // slab plus halo instead of the whole system.  Otherwise plain grid-stride.  The launch is a multiple of 8.
@@ -839,7 +1004,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     const int per = (ntiles + xs - 1) / xs;  // tiles per XCD
     const int lane_xcd = a.xcd_tiles ? (blockIdx.x & 7) : 0;
     const int slots = gridDim.x / xs;        // blocks per XCD
-    int first_tile = -1;
+    int first_tile = -1, ntot = 0;
     for (int j = a.xcd_tiles ? (blockIdx.x >> 3) : blockIdx.x; j < per; j += slots) {
         const int tile = lane_xcd * per + j;
         if (tile >= ntiles) break;
@@ -853,9 +1018,11 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         const float bi = a.sb[sl];
 
         float fx = 0.f, fy = 0.f, fz = 0.f, acc = 0.f;  // acc: pair energy (ENERGY) or neighbour count
+        if (a.dbg_times && threadIdx.x == 0 && first_tile == tile) s_dbg[0] = wall_clock64();
         if (a.has_pair)
             pair_forces<MODE, WAVES>(ctx, a, wave, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
-                                     s_rowJ[wave], s_cand[wave], s_candb[wave], s_candj[MODE == kModeEnergy ? wave : 0]);
+                                     s_rowJ[wave], s_cand[wave], s_candj[MODE == kModeEnergy ? wave : 0], ntot);
+        if (a.dbg_times && threadIdx.x == 0 && first_tile == tile) s_dbg[1] = wall_clock64();
         if (WAVES > 1) {
             red[wave][0][lane] = fx;
             red[wave][1][lane] = fy;
@@ -881,7 +1048,9 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
             const float4 km = a.kmu[i];
             float en[kEnergyKinds];
             float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
+            if (a.dbg_times && threadIdx.x == 0 && first_tile == tile) s_dbg[2] = wall_clock64();
             local_terms<MODE>(ctx, a, i, pi.x, pi.y, pi.z, km, fx, fy, fz, en, rin, rout);
+            if (a.dbg_times && threadIdx.x == 0 && first_tile == tile) s_dbg[3] = wall_clock64();
             en[0] = acc;
             if (MODE == kModeEnergy) {
                 for (int k = 0; k < kEnergyKinds; ++k) {
@@ -916,10 +1085,25 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                     const float nyp = pi.y + mdt * fy + amp * n1;
                     const float nzp = pi.z + mdt * fz + amp * n2;
                     if (valid) posn[i] = make_float4(nxp, nyp, nzp, 0.f);
-                    if (FUSED && valid) {
-                        const int c = cell_index(ctx->grid_next, nxp, nyp, nzp);
-                        a.cell_of[i] = c;
-                        a.slot[i] = atomicAdd(&a.count[c], 1);
+                    if (FUSED) {
+                        // bin the new position into the next step's grid.  Wave-aggregated: lanes are cell-sorted,
+                        // so runs of equal cells are common; one atomic per run returns the run's base slot.
+                        const int c = valid ? cell_index(ctx->grid_next, nxp, nyp, nzp) : -1;
+                        const int cprev = __shfl_up(c, 1);
+                        const bool head = valid && (lane == 0 || c != cprev);
+                        const unsigned long long hm = __ballot(head);
+                        const unsigned long long upto = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+                        const int h = 63 - __clzll(hm & upto);  // my run's head (lane 0 is always a head)
+                        const unsigned long long after = hm & ~upto;
+                        const int nvalid = s_end - s_begin;
+                        const int run = (after ? (__ffsll((long long)after) - 1) : nvalid) - lane;
+                        int base = 0;
+                        if (head) base = atomicAdd(&a.count[c], run);
+                        base = __shfl(base, h);
+                        if (valid) {
+                            a.cell_of[i] = c;
+                            a.slot[i] = base + (lane - h);
+                        }
                     }
                     const float big = 3.0e38f;
                     const float l0 = wave_min(valid ? nxp : big), l1 = wave_min(valid ? nyp : big),
@@ -944,48 +1128,19 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     if (a.dbg_times && threadIdx.x == 0) {
         a.dbg_times[4 * blockIdx.x] = t_start;
         a.dbg_times[4 * blockIdx.x + 1] = wall_clock64();
-        a.dbg_times[4 * blockIdx.x + 2] = first_tile >= 0 ? (unsigned long long)__smid() : ~0ull;
+        a.dbg_times[4 * blockIdx.x + 2] =
+            first_tile >= 0 ? ((unsigned long long)__smid() << 32) | (unsigned)ntot : ~0ull;
         a.dbg_times[4 * blockIdx.x + 3] = first_tile >= 0 ? (unsigned long long)first_tile : ~0ull;
+        for (int k = 0; k < 4; ++k) a.dbg_times[4 * gridDim.x + 4 * blockIdx.x + k] = first_tile >= 0 ? s_dbg[k] : 0ull;
     }
     if (threadIdx.x == 0) {
         if (MODE == kModeEnergy) {
             for (int k = 0; k < kEnergyKinds; ++k) a.part_energy[blockIdx.x * kEnergyKinds + k] = s_pe[k];
-        } else if (FUSED) {
-            // write-through: read by the last block of this launch (sc1 loads in tail_body)
-            for (int k = 0; k < kForcePartials; ++k) st_sc1(a.part_force + blockIdx.x * kForcePartials + k, s_pr[k]);
-            for (int k = 0; k < kBBoxPartials; ++k)
-                st_sc1(a.part_bbox + blockIdx.x * kBBoxStride + k, s_pr[kForcePartials + k]);
         } else {
             for (int k = 0; k < kForcePartials; ++k) a.part_force[blockIdx.x * kForcePartials + k] = s_pr[k];
             if (MODE == kModeStep)
                 for (int k = 0; k < kBBoxPartials; ++k)
                     a.part_bbox[blockIdx.x * kBBoxStride + k] = s_pr[kForcePartials + k];
-        }
-    }
-    if (FUSED) {
-        // Hand-off to the last block: the partials were stored sc1 by lane 0 above and the cell counts are
-        // agent-scope atomics (their returned values were consumed), so no release fence: drain, then ONE
-        // ticket add per block; the last arriver reads everything with sc1 loads (no acquire either).
-        __shared__ int s_last;
-        if (threadIdx.x == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const unsigned prev = atomicAdd(&ctx->ticket, 1u);
-            s_last = (prev == gridDim.x - 1) ? 1 : 0;
-        }
-        __syncthreads();
-        if (s_last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const unsigned long long t0 = wall_clock64();
-            const int nb = gridDim.x;
-            tail_body(ctx, a, nb, nb, 1, a.apply_sched, a.ncell_max, a.sched, true);
-            const unsigned long long t1 = wall_clock64();
-            scan_cells_body(ctx, a.n, a.count, a.cstart_w, a.tile_start_w, a.tile_range_w);
-            if (threadIdx.x == 0) {
-                ctx->ticket = 0u;
-                ctx->t_last[0] = t0;
-                ctx->t_last[1] = t1;
-                ctx->t_last[3] = wall_clock64();
-            }
         }
     }
 }
@@ -1059,6 +1214,21 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
     __shared__ float s_bb[16][8];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     const int B = blockDim.x;
+    // the schedule and the context fields the tail updates are loaded up front (uniform addresses: scalar
+    // loads), so their latency overlaps the partial loads instead of forming a chain of dependent round trips
+    const double s_flags = sched[kSchedFlags], s_dt = sched[kSchedDt], s_cs0 = sched[kSchedCs0],
+                 s_csTau = sched[kSchedCsTau], s_bs0 = sched[kSchedBs0], s_bsTau = sched[kSchedBsTau],
+                 s_k0 = sched[kSchedK0], s_k1 = sched[kSchedK0 + 1], s_k2 = sched[kSchedK0 + 2],
+                 s_muW = sched[kSchedMuW];
+    const long long c_step = ctx->step, c_cursor = ctx->noise_cursor;
+    const int c_parity = ctx->parity;
+    const double c_time = ctx->time, c_cs = ctx->cs, c_bs = ctx->bs;
+    const double c_w0 = ctx->wall[0], c_w1 = ctx->wall[1], c_w2 = ctx->wall[2];
+    static_assert(sizeof(Grid) % 4 == 0, "Grid is copied as 32-bit words");
+    constexpr int kGridWords = (int)(sizeof(Grid) / 4);
+    int c_gn[kGridWords];  // ctx->grid_next as words (constant indices only: stays in registers)
+#pragma unroll
+    for (int k = 0; k < kGridWords; ++k) c_gn[k] = reinterpret_cast<const int*>(&ctx->grid_next)[k];
     // Latency-shaped: the partials are rows of 8 floats; each thread takes rows tid, tid + B, ... and issues
     // kTailRows rows' 16-B sc1 loads at once (one memory round trip per kTailRows * B rows), combines its rows
     // in order, then lanes meet in wave butterflies and the waves in index order: a fixed order for a given
@@ -1101,9 +1271,9 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
         }
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = (k == 6) ? wave_max_d(acc[k]) : wave_sum_d(acc[k]);
+    for (int k = 0; k < 8; ++k) acc[k] = (k == 6) ? wave_total_max_d(acc[k]) : wave_total_sum_d(acc[k]);
 #pragma unroll
-    for (int k = 0; k < 6; ++k) bb[k] = (k < 3) ? wave_min(bb[k]) : wave_max(bb[k]);
+    for (int k = 0; k < 6; ++k) bb[k] = (k < 3) ? wave_total_min_f(bb[k]) : wave_total_max_f(bb[k]);
     if (lane == 0) {
         for (int k = 0; k < 8; ++k) s_red[wave][k] = acc[k];
         for (int k = 0; k < 6; ++k) s_bb[wave][k] = bb[k];
@@ -1118,6 +1288,7 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
             for (int k = 0; k < 8; ++k) tot[k] = (k == 6) ? fmax(tot[k], s_red[w][k]) : tot[k] + s_red[w][k];
             for (int k = 0; k < 6; ++k) bb[k] = (k < 3) ? fminf(bb[k], s_bb[w][k]) : fmaxf(bb[k], s_bb[w][k]);
         }
+        // everything below works on the values thread 0 loaded at entry (sc[], c_*): no dependent global reads
         if (fblocks > 0) {
             for (int k = 0; k < 3; ++k) {
                 ctx->react_in[k] = tot[k];
@@ -1131,33 +1302,55 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
                 ctx->bbox_lo[k] = bb[k];
                 ctx->bbox_hi[k] = bb[3 + k];
             }
+        long long step = c_step;
         if (advance) {
-            ctx->step += 1;
-            ctx->parity ^= 1;
-            if (a.noise_mode == GCS_NOISE_INJECTED) ctx->noise_cursor += 1;
+            step += 1;
+            ctx->step = step;
+            ctx->parity = c_parity ^ 1;
+            if (a.noise_mode == GCS_NOISE_INJECTED) ctx->noise_cursor = c_cursor + 1;
         }
+        double time = c_time, cs = c_cs, bs = c_bs;
+        const int flags = (int)s_flags;
         if (apply_sched) {
             // stage_interphase/simulation_driver_interphase.cpp:17 (time), :67-76 (scales), :79-90 (wall)
-            const int flags = (int)sched[kSchedFlags];
-            const double dt = sched[kSchedDt];
-            if (flags & 1) ctx->time = (double)ctx->step * dt;
+            const double dt = s_dt;
+            if (flags & 1) ctx->time = time = (double)step * dt;
             if (flags & 2) {
-                ctx->cs = 1.0 - (1.0 - sched[kSchedCs0]) * exp(-(ctx->time / sched[kSchedCsTau]));
-                ctx->bs = 1.0 - (1.0 - sched[kSchedBs0]) * exp(-(ctx->time / sched[kSchedBsTau]));
+                ctx->cs = cs = 1.0 - (1.0 - s_cs0) * exp(-(time / s_csTau));
+                ctx->bs = bs = 1.0 - (1.0 - s_bs0) * exp(-(time / s_bsTau));
             }
-            if (flags & 4)
+            if (flags & 4) {
+                const double w[3] = {c_w0, c_w1, c_w2}, kw[3] = {s_k0, s_k1, s_k2};
+#pragma unroll
                 for (int k = 0; k < 3; ++k) {
                     double net = 0.0;
-                    net += ctx->react_in[k] + ctx->react_out[k];
-                    net -= sched[kSchedK0 + k] * ctx->wall[k];
-                    ctx->wall[k] += dt * sched[kSchedMuW] * net;
+                    net += tot[k] + tot[3 + k];
+                    net -= kw[k] * w[k];
+                    ctx->wall[k] = w[k] + dt * s_muW * net;
                 }
+            }
         }
         if (fused) {
-            ctx->grid = ctx->grid_next;
-            ctx->grid_next = next_grid(ctx, a, sched, ctx->step + 1, ncell_max);
+            // the grid that bins the NEXT step's positions: this bbox padded by 2 % + 0.01 (particles move far
+            // less per step; any that leave are clamped, which is still exact) and the pair cutoff of that step
+            // (closed form of update_core_scale at step + 1)
+            float lo[3], hi[3];
+            for (int k = 0; k < 3; ++k) {
+                const float pad = 0.02f * fmaxf(bb[3 + k] - bb[k], 0.f) + 0.01f;
+                lo[k] = bb[k] - pad;
+                hi[k] = bb[3 + k] + pad;
+            }
+            double csn = cs;
+            if (apply_sched && (flags & 2)) {
+                const double t = (flags & 1) ? (double)(step + 1) * s_dt : time;
+                csn = 1.0 - (1.0 - s_cs0) * exp(-(t / s_csTau));
+            }
+            const float rc = a.has_pair ? a.pair_dist * (a.pair_scaled ? (float)fmax(csn, cs) : 1.f) : 1.f;
+#pragma unroll
+            for (int k = 0; k < kGridWords; ++k) reinterpret_cast<int*>(&ctx->grid)[k] = c_gn[k];
+            ctx->grid_next = make_grid(lo, hi, rc, ncell_max, kPairFx);
         } else {
-            compute_grid(ctx, pair_cutoff(a, ctx->cs), ncell_max, kPairFx);
+            ctx->grid = make_grid(bb, bb + 3, pair_cutoff(a, cs), ncell_max, kPairFx);
         }
     }
     __syncthreads();
@@ -1166,7 +1359,12 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
 __global__ __launch_bounds__(256) void k_tail(DevCtx* ctx, ForceArgs a, int fblocks, int bblocks, int advance,
                                               int apply_sched, int ncell_max, const double* __restrict__ sched)
 {
+    const unsigned long long t0 = wall_clock64();
     tail_body(ctx, a, fblocks, bblocks, advance, apply_sched, ncell_max, sched, false);
+    if (threadIdx.x == 0) {
+        ctx->t_tail[0] = t0;
+        ctx->t_tail[1] = wall_clock64();
+    }
 }
 
 // ----------------------------------------------------------------------------------------------------
@@ -1254,14 +1452,24 @@ void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, con
     hipLaunchKernelGGL(k_cell_count, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, n, cell_of, slot, count);
 }
 
-void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start, int2* tile_range)
+void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start, int2* tile_range,
+                      bool use_next)
 {
-    hipLaunchKernelGGL(k_cell_scan, dim3(1), dim3(1024), 0, s, ctx, n, count, cstart, tile_start, tile_range);
+    hipLaunchKernelGGL(k_cell_scan, dim3(1), dim3(1024), 0, s, ctx, n, count, cstart, tile_start, tile_range,
+                       use_next ? 1 : 0);
 }
 
-void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* slot, const int* cstart, int* tmp)
+void launch_scatter_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int* tmp, int fblocks, int apply_sched,
+                         int ncell_max)
 {
-    hipLaunchKernelGGL(k_cell_scatter, dim3((n + 255) / 256), dim3(256), 0, s, n, cell_of, slot, cstart, tmp);
+    hipLaunchKernelGGL(k_scatter_tail, dim3((a.n + 255) / 256 + 1), dim3(256), 0, s, ctx, a, a.n, tmp, fblocks,
+                       apply_sched, ncell_max);
+}
+
+void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* slot, const int* cstart, int* tmp,
+                         int* count)
+{
+    hipLaunchKernelGGL(k_cell_scatter, dim3((n + 255) / 256), dim3(256), 0, s, n, cell_of, slot, cstart, tmp, count);
 }
 
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, const float4* kmu, int n,

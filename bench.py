@@ -133,7 +133,7 @@ def main():
     ap.add_argument("--waves", type=int, default=4)
     ap.add_argument("--chunk-order", type=int, default=1)
     ap.add_argument("--xcd-tiles", type=int, default=0)
-    ap.add_argument("--fused", type=int, default=0, help="1: 3 launches per step (force kernel bins + runs the tail)")
+    ap.add_argument("--fused", type=int, default=1, help="1: 4-launch step (force kernel bins the new positions)")
     ap.add_argument("--profile-steps", type=int, default=50)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline work (0 = skip)")
     ap.add_argument("--no-start-window", action="store_true", help="skip the secondary step-0 window")
