@@ -97,6 +97,8 @@ struct gcs_engine {
     float* part_bbox = nullptr;
     double* part_energy = nullptr;
     float4* force_out = nullptr;
+    float4* pbuf = nullptr;  // split-tile partial forces
+    int* tcnt = nullptr;     // split-tile arrival counters
     // topology tables
     int* boff = nullptr;
     int2* bent = nullptr;
@@ -396,6 +398,9 @@ void fill_state_args(gcs_engine* e)
     a.sched = e->dsched;
     a.ncell_max = e->ncell_max;
     a.apply_sched = e->sched_flags != 0;
+    a.pbuf = e->pbuf;
+    a.tcnt = e->tcnt;
+    a.split_cap = force_grid(e->n);
 }
 
 // bin the current positions into ctx->grid: per-cell counts + slots, scan, tile table
@@ -427,6 +432,7 @@ void enqueue_cells(gcs_engine* e)
 }
 
 bool fused_path(const gcs_engine* e, bool spacestep) { return e->fused && !spacestep; }
+int step_grid(const gcs_engine* e) { return e->fa.split ? force_grid_split(e->n) : force_grid(e->n); }
 
 // One BD step.  Fused (fixed timestep, 4 launches): sort the cells the previous step scattered; force + update,
 // which also bins the new positions into the predicted next grid; scan those counts; scatter them, with the
@@ -436,17 +442,18 @@ bool fused_path(const gcs_engine* e, bool spacestep) { return e->fused && !space
 void enqueue_step(gcs_engine* e, bool spacestep, float spacestep_v, float timestep)
 {
     const int fb = force_grid(e->n);
+    const int sb = step_grid(e);  // kModeStep launch size (split tiles: two units per tile)
     if (fused_path(e, spacestep)) {
         enqueue_cell_order(e);
         launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, true);
         launch_cell_scan(e->stream, e->ctx, e->n, e->count, e->cstart, e->tile_start, e->tile_range, true);
-        launch_scatter_tail(e->stream, e->ctx, e->fa, e->tmp, fb, e->sched_flags != 0, e->ncell_max);
+        launch_scatter_tail(e->stream, e->ctx, e->fa, e->tmp, sb, e->sched_flags != 0, e->ncell_max);
         return;
     }
     enqueue_cells(e);
     if (!spacestep) {
         launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, false);
-        launch_tail(e->stream, e->ctx, e->fa, fb, fb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
+        launch_tail(e->stream, e->ctx, e->fa, sb, sb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
     } else {
         launch_force(e->stream, kModeForce, e->waves, e->ctx, e->fa, false);
         launch_adapt(e->stream, e->ctx, e->fa, fb, spacestep_v, timestep);
@@ -553,7 +560,8 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
     e->device = d->device;
     e->n = (int)d->particle_count;
     e->fa.chunk_mode = 1;  // strided candidate chunks (GCS_OPT_CHUNK_ORDER)
-    e->fa.xcd_tiles = 0;   // XCD-contiguous tile runs (GCS_OPT_XCD_TILES): slower, the slabs are unevenly dense
+    e->fa.split = 0;       // split tiles (GCS_OPT_SPLIT_TILES): measured slower
+    e->fa.prio_step = 700; // tile-cost wave priority (GCS_OPT_TILE_PRIORITY): +2 % on C2
     const int n = e->n;
     e->mu.assign(n, 1.0);
     e->ab.assign(2 * (size_t)n, 0.0);
@@ -574,7 +582,7 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
     if (he != hipSuccess) return bail(fail(GCS_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(he)));
     e->ncell_max = std::min(1 << 21, std::max(4096, 4 * n));
     int rc = 0;
-    const int fb = force_grid(n), ub = update_blocks(n);
+    const int fb = force_grid_split(n), ub = update_blocks(n);  // partial rows for the largest launch
     if ((rc = dalloc(&e->pos[0], n)) || (rc = dalloc(&e->pos[1], n)) || (rc = dalloc(&e->kmu, n)) ||
         (rc = dalloc(&e->spos, n)) || (rc = dalloc(&e->sb, n)) || (rc = dalloc(&e->sidx, n)) ||
         (rc = dalloc(&e->scell, n)) || (rc = dalloc(&e->cell_of, n)) || (rc = dalloc(&e->slot, n)) ||
@@ -584,9 +592,11 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
         (rc = dalloc(&e->ctx, 1)) || (rc = dalloc(&e->dsched, kSchedCount)) ||
         (rc = dalloc(&e->part_force, (size_t)std::max(fb, ub) * kForcePartials)) ||
         (rc = dalloc(&e->part_bbox, (size_t)std::max(fb, ub) * kBBoxStride)) ||
-        (rc = dalloc(&e->part_energy, (size_t)fb * kEnergyKinds)) || (rc = dalloc(&e->force_out, n)))
+        (rc = dalloc(&e->part_energy, (size_t)fb * kEnergyKinds)) || (rc = dalloc(&e->force_out, n)) ||
+        (rc = dalloc(&e->pbuf, (size_t)2 * force_grid(n) * kTile)) || (rc = dalloc(&e->tcnt, force_grid(n))))
         return bail(rc);
     he = hipMemsetAsync(e->count, 0, (e->ncell_max + kScanPad) * sizeof(int), e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->tcnt, 0, force_grid(n) * sizeof(int), e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->pos[0], 0, n * sizeof(float4), e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->pos[1], 0, n * sizeof(float4), e->stream);
     DevCtx c{};
@@ -623,6 +633,8 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->ctx);
     dfree(e->dsched);
     dfree(e->part_force);
+    dfree(e->pbuf);
+    dfree(e->tcnt);
     dfree(e->part_bbox);
     dfree(e->part_energy);
     dfree(e->force_out);
@@ -1141,10 +1153,10 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     // GCS_DEBUG_TIMES=<file>: per-block timings of the last profiled force launch (see k_force)
     const char* dbg_path = std::getenv("GCS_DEBUG_TIMES");
     unsigned long long* dbg = nullptr;
-    const size_t dbg_n = (size_t)force_grid(e->n) * 8;
+    const size_t dbg_n = (size_t)force_grid_split(e->n) * 8;
     if (dbg_path) HIPCHK(hipMalloc(&dbg, dbg_n * sizeof(unsigned long long)));
     for (auto& x : ev) HIPCHK(hipEventCreate(&x));
-    const int fb = force_grid(e->n);
+    const int fb = step_grid(e);
     HIPCHK(hipEventRecord(ev[0], e->stream));
     const bool fused = fused_path(e, false);
     // per step: [1] cells [2] force [3] fused: next-step scan / unfused: tail [4] fused: scatter + tail [5]
@@ -1244,9 +1256,15 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         drop_graph(e);
         return GCS_OK;
     }
-    if (option == GCS_OPT_XCD_TILES) {
-        if (value != 0 && value != 1) return fail(GCS_EINVAL, "xcd tiles must be 0 or 1");
-        e->fa.xcd_tiles = (int)value;
+    if (option == GCS_OPT_TILE_PRIORITY) {
+        if (value < 0 || value > (1 << 20)) return fail(GCS_EINVAL, "tile priority step must be in [0, 2^20]");
+        e->fa.prio_step = (int)value;
+        drop_graph(e);
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_SPLIT_TILES) {
+        if (value != 0 && value != 1) return fail(GCS_EINVAL, "split tiles must be 0 or 1");
+        e->fa.split = (int)value;
         drop_graph(e);
         return GCS_OK;
     }

@@ -135,7 +135,11 @@ struct ForceArgs {
     const double* sched;
     int ncell_max;
     int apply_sched;
-    int xcd_tiles;  // 1: each XCD takes one contiguous run of tiles (GCS_OPT_XCD_TILES)
+    int prio_step;  // > 0: wave priority = min(3, candidates / prio_step) (GCS_OPT_TILE_PRIORITY)
+    int split;      // 1: step launches split tiles into two units (GCS_OPT_SPLIT_TILES)
+    int split_cap;  // tiles that may be split (pbuf / tcnt capacity)
+    float4* pbuf;   // [2 * split_cap][kTile] partial forces of split units
+    int* tcnt;      // [split_cap] arrival counters of split tiles (0 between launches)
     unsigned long long* dbg_times;  // optional (GCS_DEBUG_TIMES): per block {start, end, smid/candidates, tile} then 4 phase stamps
 };
 
@@ -191,6 +195,8 @@ inline int force_blocks(int n) { return (n + kTile - 1) / kTile; }
 // k_force launch size: tiles never cross a cell row, so there are up to (rows) more tiles than force_blocks;
 // blocks walk the tiles grid-stride, any launch size is correct
 inline int force_grid(int n) { return ((force_blocks(n) + force_blocks(n) / 4 + 64) + 7) & ~7; }  // multiple of 8 (XCDs)
+// step launches with split tiles: up to two units per tile
+inline int force_grid_split(int n) { return 2 * force_grid(n); }
 constexpr int kUpdateBlock = 256;
 inline int update_blocks(int n) { return (n + kUpdateBlock - 1) / kUpdateBlock; }
 

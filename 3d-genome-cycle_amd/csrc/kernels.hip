@@ -32,6 +32,11 @@ __device__ __forceinline__ float4 ld_sc1_f4(__amdgpu_buffer_rsrc_t r, int byte_o
     __builtin_memcpy(&f, &v, 16);
     return f;
 }
+__device__ __forceinline__ void st_sc1_f4(__amdgpu_buffer_rsrc_t r, int byte_off, float4 v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const __attribute__((ext_vector_type(4))) unsigned*>(&v),
+                                           r, byte_off, 0, 16);
+}
 __device__ __forceinline__ int4 ld_sc1_i4(__amdgpu_buffer_rsrc_t r, int byte_off)
 {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
@@ -787,7 +792,8 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
 template <int MODE, int WAVES>
 __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceArgs& a, int wave, int lane, int s,
                                    int s_begin, int s_end, float4 pi, float bi, float& fx, float& fy, float& fz,
-                                   float& acc, int* s_rowV, int* s_rowJ, float4* s_cand, int* s_candj, int& ntot)
+                                   float& acc, int* s_rowV, int* s_rowJ, float4* s_cand, int* s_candj, int& ntot,
+                                   int wv, int nwv)
 {
     const Grid g = ctx->grid;
     const float cs = (float)ctx->cs;
@@ -836,19 +842,34 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
     __builtin_amdgcn_wave_barrier();
     const int total = uniform(s_rowV[16]);
     ntot = total;
+    // Wave priority by tile cost: the kernel ends with its densest tiles (block time ~ 17 us + 17.5 ns per
+    // candidate on C2), while light tiles have slack.  The SIMD arbiter issues higher-priority waves first, so
+    // the critical tiles progress at the light ones' expense.  (s_setprio takes an immediate.)
+    if (a.prio_step > 0) {
+        const int pr = total / a.prio_step;
+        if (pr >= 3)
+            __builtin_amdgcn_s_setprio(3);
+        else if (pr == 2)
+            __builtin_amdgcn_s_setprio(2);
+        else if (pr == 1)
+            __builtin_amdgcn_s_setprio(1);
+        else
+            __builtin_amdgcn_s_setprio(0);
+    }
     const float ahi = kA * pi.w, bhi = kB * bi;
     // Chunk c of this wave holds candidates v = first(c) + stride * lane, lane < count(c).
     //   contiguous (chunk_mode 0): the wave's share [wlo, whi) in runs of 64
     //   strided    (chunk_mode 1): chunk g of G = ceil(total / 64) takes v = g + G * lane; wave w owns the
-    //   chunks g = w (mod WAVES).  Every chunk then samples all stencil rows, which evens the hit counts
+    //   chunks g = w (mod nwv).  Every chunk then samples all stencil rows, which evens the hit counts
     //   across lanes (phase 2 runs as long as the lane with the most hits).
+    // (wv, nwv): this wave's index among all the waves sharing the tile (the split parts' waves included)
     const bool strided = a.chunk_mode != 0;
     const int G = (total + kTile - 1) / kTile;
-    const int wlo = (int)(((long long)total * wave) / WAVES);
-    const int whi = (int)(((long long)total * (wave + 1)) / WAVES);
-    const int nchunk = strided ? (G > wave ? (G - wave + WAVES - 1) / WAVES : 0) : (whi - wlo + kTile - 1) / kTile;
+    const int wlo = (int)(((long long)total * wv) / nwv);
+    const int whi = (int)(((long long)total * (wv + 1)) / nwv);
+    const int nchunk = strided ? (G > wv ? (G - wv + nwv - 1) / nwv : 0) : (whi - wlo + kTile - 1) / kTile;
     const int stride = strided ? G : 1;
-    auto first = [&](int c) { return strided ? wave + c * WAVES : wlo + c * kTile; };
+    auto first = [&](int c) { return strided ? wv + c * nwv : wlo + c * kTile; };
     auto count = [&](int c) {
         const int f = first(c);
         return strided ? min(kTile, (total - f + G - 1) / G) : min(kTile, whi - f);
@@ -997,17 +1018,19 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
 
     const unsigned long long t_start = a.dbg_times ? wall_clock64() : 0ull;
     __shared__ unsigned long long s_dbg[4];  // GCS_DEBUG_TIMES: pair start, pair end (wave 0), local start, end
-    // XCD-aware tile order (a.xcd_tiles): workgroups are dispatched round-robin over the 8 XCDs, so block b runs
-    // on XCD b & 7; give each XCD one contiguous run of tiles (a slab of cell rows) so its private L2 holds one
-    // slab plus halo instead of the whole system.  Otherwise plain grid-stride.  The launch is a multiple of 8.
-    const int xs = a.xcd_tiles ? 8 : 1;
-    const int per = (ntiles + xs - 1) / xs;  // tiles per XCD
-    const int lane_xcd = a.xcd_tiles ? (blockIdx.x & 7) : 0;
-    const int slots = gridDim.x / xs;        // blocks per XCD
+    // Work units: with a.split, tiles t < nsplit are split in two units (2t, 2t + 1) that take alternate halves of
+    // the tile's candidate chunks (8 waves on one tile, in two workgroups); the other tiles are one unit each.
+    // There are more units than resident workgroups, so the dispatcher balances the units over the CUs as they
+    // free up (a tile's cost varies ~5x with the local density; whole tiles pinned 4-5 per CU left the kernel
+    // waiting on the most loaded CU).  The two halves meet through a per-tile arrival counter: the second to
+    // finish adds the other's partial forces (write-through stores / sc1 loads) and integrates.
+    const int nsplit = (MODE == kModeStep && a.split) ? min(ntiles, a.split_cap) : 0;
+    const int nunits = ntiles + nsplit;
     int first_tile = -1, ntot = 0;
-    for (int j = a.xcd_tiles ? (blockIdx.x >> 3) : blockIdx.x; j < per; j += slots) {
-        const int tile = lane_xcd * per + j;
-        if (tile >= ntiles) break;
+    for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+        const int tile = (u < 2 * nsplit) ? (u >> 1) : u - nsplit;
+        const int part = (u < 2 * nsplit) ? (u & 1) : 0;
+        const int nparts = (u < 2 * nsplit) ? 2 : 1;
         if (first_tile < 0) first_tile = tile;
         const int2 tr = a.tile_range[tile];
         const int s_begin = uniform(tr.x), s_end = uniform(tr.y);
@@ -1021,7 +1044,8 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         if (a.dbg_times && threadIdx.x == 0 && first_tile == tile) s_dbg[0] = wall_clock64();
         if (a.has_pair)
             pair_forces<MODE, WAVES>(ctx, a, wave, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
-                                     s_rowJ[wave], s_cand[wave], s_candj[MODE == kModeEnergy ? wave : 0], ntot);
+                                     s_rowJ[wave], s_cand[wave], s_candj[MODE == kModeEnergy ? wave : 0], ntot,
+                                     part * WAVES + wave, nparts * WAVES);
         if (a.dbg_times && threadIdx.x == 0 && first_tile == tile) s_dbg[1] = wall_clock64();
         if (WAVES > 1) {
             red[wave][0][lane] = fx;
@@ -1043,7 +1067,25 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                 }
             }
         }
-        if (wave == 0) {
+        bool owner = true;  // the unit that integrates the tile (the later of two split halves)
+        if (MODE == kModeStep && nparts > 1 && wave == 0) {
+            const auto rp = __builtin_amdgcn_make_buffer_rsrc((void*)a.pbuf, 0, 0x7fffffff, 0x00020000);
+            st_sc1_f4(rp, (u * kTile + lane) * 16, make_float4(fx, fy, fz, acc));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial is out before the arrival add
+            int old = 0;
+            if (lane == 0) old = atomicAdd(&a.tcnt[tile], 1);
+            owner = __shfl(old, 0) == 1;
+            if (owner) {
+                // a + b == b + a in IEEE arithmetic: the sum does not depend on which half arrived last
+                const float4 o = ld_sc1_f4(rp, ((u ^ 1) * kTile + lane) * 16);
+                fx += o.x;
+                fy += o.y;
+                fz += o.z;
+                acc += o.w;
+                if (lane == 0) a.tcnt[tile] = 0;  // ready for the next launch
+            }
+        }
+        if (wave == 0 && owner) {
             const int i = a.sidx[sl];
             const float4 km = a.kmu[i];
             float en[kEnergyKinds];
@@ -1483,7 +1525,7 @@ void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, cons
 template <int MODE, bool FUSED>
 static void launch_force_mode(hipStream_t s, int waves, DevCtx* ctx, const ForceArgs& a)
 {
-    const dim3 grid(force_grid(a.n));
+    const dim3 grid((MODE == kModeStep && a.split) ? force_grid_split(a.n) : force_grid(a.n));
     switch (waves) {
     case 1: hipLaunchKernelGGL((k_force<MODE, 1, FUSED>), grid, dim3(64), 0, s, ctx, a); break;
     case 2: hipLaunchKernelGGL((k_force<MODE, 2, FUSED>), grid, dim3(128), 0, s, ctx, a); break;

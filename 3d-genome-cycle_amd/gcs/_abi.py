@@ -29,7 +29,8 @@ OPT_GRAPH_STEPS = 1
 OPT_WAVES_PER_TILE = 2
 OPT_CHUNK_ORDER = 3
 OPT_FUSED_STEP = 4
-OPT_XCD_TILES = 5
+OPT_SPLIT_TILES = 5
+OPT_TILE_PRIORITY = 6
 
 ENERGY_KINDS = ("pair", "softwell", "bonds", "bending", "wall_in", "wall_out", "point_source", "kinetochore_fiber")
 

@@ -132,7 +132,8 @@ def main():
     ap.add_argument("--graph-steps", type=int, default=32)
     ap.add_argument("--waves", type=int, default=4)
     ap.add_argument("--chunk-order", type=int, default=1)
-    ap.add_argument("--xcd-tiles", type=int, default=0)
+    ap.add_argument("--split", type=int, default=0, help="1: split each tile's candidates over two workgroups")
+    ap.add_argument("--prio", type=int, default=700, help="n > 0: wave priority min(3, tile candidates / n)")
     ap.add_argument("--fused", type=int, default=1, help="1: 4-launch step (force kernel bins the new positions)")
     ap.add_argument("--profile-steps", type=int, default=50)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline work (0 = skip)")
@@ -150,7 +151,8 @@ def main():
     eng.set_option(A.OPT_WAVES_PER_TILE, args.waves)
     eng.set_option(A.OPT_CHUNK_ORDER, args.chunk_order)
     eng.set_option(A.OPT_FUSED_STEP, args.fused)
-    eng.set_option(A.OPT_XCD_TILES, args.xcd_tiles)
+    eng.set_option(A.OPT_SPLIT_TILES, args.split)
+    eng.set_option(A.OPT_TILE_PRIORITY, args.prio)
     seed = replica_noise_seed(rank)
 
     eng.run(args.warmup, first_step=WINDOW_START, seed=seed)
@@ -216,7 +218,7 @@ def main():
                                f"{WINDOW_START} (core_scale {ctx['core_scale']:.4f})",
                    "particles": n, "replicas": world, "parallelism": f"replicas{world}",
                    "mean_neighbors": prof["mean_neighbors"], "graph_steps": args.graph_steps,
-                   "waves_per_tile": args.waves, "chunk_order": args.chunk_order, "fused": args.fused, "xcd_tiles": args.xcd_tiles, "start_window_value": start_rate, "finite": finite},
+                   "waves_per_tile": args.waves, "chunk_order": args.chunk_order, "fused": args.fused, "split_tiles": args.split, "tile_priority": args.prio, "start_window_value": start_rate, "finite": finite},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(),
                      "kernel": "k_force<kModeStep>", "force_ms": force_ms, "cell_ms": prof["cell_ms"],

@@ -161,14 +161,22 @@ def test_waves_per_tile_equivalent(c1_design, interphase_cfg, waves, order):
     assert te == pytest.approx(to, rel=1e-5)
 
 
-@pytest.mark.parametrize("xcd", [0, 1])
-def test_xcd_tile_order_same_forces(c2_design, interphase_cfg, xcd):
-    """The XCD-contiguous tile order only moves tiles between workgroups: per-particle forces are bit-identical."""
-    e0, _ = interphase.build_interphase(Engine, c2_design, interphase_cfg)
-    e1, _ = interphase.build_interphase(Engine, c2_design, interphase_cfg)
-    e0.set_option(A.OPT_XCD_TILES, 0)
-    e1.set_option(A.OPT_XCD_TILES, xcd)
-    assert np.array_equal(e0.compute_forces(), e1.compute_forces())
+@pytest.mark.parametrize("fused", [0, 1])
+def test_split_tiles_agree(c2_design, interphase_cfg, fused):
+    """Splitting each tile's candidates over two workgroups only regroups the fp32 pair sums: the C2 trajectory
+    stays within fp32 tolerance of the unsplit one, and the split run is bitwise reproducible."""
+    out = []
+    for split in (0, 1, 1):
+        e, _ = interphase.build_interphase(Engine, c2_design, interphase_cfg)
+        e.set_option(A.OPT_FUSED_STEP, fused)
+        e.set_option(A.OPT_SPLIT_TILES, split)
+        e.set_schedule(**interphase.interphase_schedule(interphase_cfg))
+        e.apply_schedule(0)
+        e.run(20, seed=11)
+        out.append(e.get_positions())
+        e.close()
+    assert np.abs(out[0] - out[1]).max() <= 2e-5
+    assert np.array_equal(out[1], out[2])
 
 
 @pytest.mark.parametrize("fused", [0, 1])
