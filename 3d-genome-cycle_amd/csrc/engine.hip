@@ -1153,7 +1153,7 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     // GCS_DEBUG_TIMES=<file>: per-block timings of the last profiled force launch (see k_force)
     const char* dbg_path = std::getenv("GCS_DEBUG_TIMES");
     unsigned long long* dbg = nullptr;
-    const size_t dbg_n = (size_t)force_grid_split(e->n) * 8;
+    const size_t dbg_n = (size_t)step_grid(e) * 8;
     if (dbg_path) HIPCHK(hipMalloc(&dbg, dbg_n * sizeof(unsigned long long)));
     for (auto& x : ev) HIPCHK(hipEventCreate(&x));
     const int fb = step_grid(e);

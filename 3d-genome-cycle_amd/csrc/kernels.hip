@@ -698,7 +698,10 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
 #pragma unroll
     for (int q = 0; q < kMaxPointSources; ++q) {
         if (q >= a.n_point) break;
-        const PointSrc& p = a.point[q];
+        PointSrc p = a.point[q];
+        // opaque to the optimizer: keeps the (rarely used, mitotic-only) point-source constants from being hoisted
+        // to the kernel entry, where they would be spilled to scratch by every wave
+        asm volatile("" : "+v"(p.b), "+v"(p.f), "+v"(p.k), "+v"(p.l));
         const float rx = xi - p.px, ry = yi - p.py, rz = zi - p.pz;
         const float r2 = rx * rx + ry * ry + rz * rz;
         float c, U;
