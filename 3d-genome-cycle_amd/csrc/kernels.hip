@@ -1004,6 +1004,9 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     __shared__ int s_rowV[WAVES][17];
     __shared__ int s_rowJ[WAVES][16];
     __shared__ float4 s_cand[WAVES][2 * (kTile + 1)];  // candidate records (2 x float4) + sentinel
+    __shared__ float4 s_locf[MODE == kModeStep ? kTile : 1];  // early local terms: force, mu
+    __shared__ float4 s_locr[MODE == kModeStep ? kTile : 1];  // inward reaction, particle index
+    __shared__ float4 s_loco[MODE == kModeStep ? kTile : 1];  // outward reaction
     __shared__ int s_candj[MODE == kModeEnergy ? WAVES : 1][kTile];
     __shared__ float s_pr[kForcePartials + kBBoxPartials];  // per-block accumulators (lane 0 of wave 0)
     __shared__ double s_pe[kEnergyKinds];
@@ -1044,6 +1047,21 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
         const float bi = a.sb[sl];
 
         float fx = 0.f, fy = 0.f, fz = 0.f, acc = 0.f;  // acc: pair energy (ENERGY) or neighbour count
+        // Step launches: the particle-local terms (bonds, bending, tethers, walls, point sources; a chain of
+        // dependent gathers) do not depend on the pair forces, so the last wave computes them FIRST, while the
+        // other waves start the pair loop (it owns the fewest strided chunks), and parks them in LDS.  Wave 0
+        // then only adds them after the block reduction instead of running that latency chain at the end.
+        const bool early = (MODE == kModeStep) && (WAVES > 1) && (nparts == 1);
+        if (early && wave == WAVES - 1) {
+            const int i = a.sidx[sl];
+            const float4 km = a.kmu[i];
+            float lfx = 0.f, lfy = 0.f, lfz = 0.f, en[kEnergyKinds];
+            float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
+            local_terms<MODE>(ctx, a, i, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout);
+            s_locf[lane] = make_float4(lfx, lfy, lfz, km.x);
+            s_locr[lane] = make_float4(rin[0], rin[1], rin[2], __int_as_float(i));
+            s_loco[lane] = make_float4(rout[0], rout[1], rout[2], 0.f);
+        }
         if (a.dbg_times && threadIdx.x == 0 && first_tile == tile) s_dbg[0] = wall_clock64();
         if (a.has_pair)
             pair_forces<MODE, WAVES>(ctx, a, wave, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
@@ -1089,12 +1107,29 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
             }
         }
         if (wave == 0 && owner) {
-            const int i = a.sidx[sl];
-            const float4 km = a.kmu[i];
+            int i;
+            float4 km;
             float en[kEnergyKinds];
             float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
             if (a.dbg_times && threadIdx.x == 0 && first_tile == tile) s_dbg[2] = wall_clock64();
-            local_terms<MODE>(ctx, a, i, pi.x, pi.y, pi.z, km, fx, fy, fz, en, rin, rout);
+            if (early) {
+                const float4 lf = s_locf[lane], lr = s_locr[lane], lo = s_loco[lane];
+                fx += lf.x;
+                fy += lf.y;
+                fz += lf.z;
+                km = make_float4(lf.w, 0.f, 0.f, 0.f);  // only mu is used below
+                i = __float_as_int(lr.w);
+                rin[0] = lr.x;
+                rin[1] = lr.y;
+                rin[2] = lr.z;
+                rout[0] = lo.x;
+                rout[1] = lo.y;
+                rout[2] = lo.z;
+            } else {
+                i = a.sidx[sl];
+                km = a.kmu[i];
+                local_terms<MODE>(ctx, a, i, pi.x, pi.y, pi.z, km, fx, fy, fz, en, rin, rout);
+            }
             if (a.dbg_times && threadIdx.x == 0 && first_tile == tile) s_dbg[3] = wall_clock64();
             en[0] = acc;
             if (MODE == kModeEnergy) {
