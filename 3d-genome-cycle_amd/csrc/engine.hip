@@ -98,6 +98,8 @@ struct gcs_engine {
     double* part_energy = nullptr;
     float4* force_out = nullptr;
     float4* pbuf = nullptr;  // split-tile partial forces
+    int4* units = nullptr;    // heavy-tile unit table (cell scan -> force kernel)
+    int resident = 0;         // force-step workgroups resident at once (split budget)
     int* tcnt = nullptr;     // split-tile arrival counters
     // topology tables
     int* boff = nullptr;
@@ -399,8 +401,9 @@ void fill_state_args(gcs_engine* e)
     a.ncell_max = e->ncell_max;
     a.apply_sched = e->sched_flags != 0;
     a.pbuf = e->pbuf;
+    a.units = e->units;
     a.tcnt = e->tcnt;
-    a.split_cap = force_grid(e->n);
+    a.split_cap = std::max(force_grid(e->n), kMaxUnits);
 }
 
 // bin the current positions into ctx->grid: per-cell counts + slots, scan, tile table
@@ -408,7 +411,8 @@ void enqueue_bin(gcs_engine* e)
 {
     const int n = e->n;
     launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count);
-    launch_cell_scan(e->stream, e->ctx, n, e->count, e->cstart, e->tile_start, e->tile_range);
+    launch_cell_scan(e->stream, e->ctx, n, e->count, e->cstart, e->tile_start, e->tile_range, false, e->units,
+                     e->fa.split == 2 ? e->resident : 0);
 }
 
 // order each (scattered) cell by particle index: the cell-sorted copies the pair loop reads
@@ -446,7 +450,8 @@ void enqueue_step(gcs_engine* e, bool spacestep, float spacestep_v, float timest
     if (fused_path(e, spacestep)) {
         enqueue_cell_order(e);
         launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, true);
-        launch_cell_scan(e->stream, e->ctx, e->n, e->count, e->cstart, e->tile_start, e->tile_range, true);
+        launch_cell_scan(e->stream, e->ctx, e->n, e->count, e->cstart, e->tile_start, e->tile_range, true,
+                         e->units, e->fa.split == 2 ? e->resident : 0);
         launch_scatter_tail(e->stream, e->ctx, e->fa, e->tmp, sb, e->sched_flags != 0, e->ncell_max);
         return;
     }
@@ -560,7 +565,7 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
     e->device = d->device;
     e->n = (int)d->particle_count;
     e->fa.chunk_mode = 1;  // strided candidate chunks (GCS_OPT_CHUNK_ORDER)
-    e->fa.split = 0;       // split tiles (GCS_OPT_SPLIT_TILES): measured slower
+    e->fa.split = 0;       // split tiles (GCS_OPT_SPLIT_TILES): 1 and 2 measured slower on C2
     e->fa.prio_step = 700; // tile-cost wave priority (GCS_OPT_TILE_PRIORITY): +2 % on C2
     const int n = e->n;
     e->mu.assign(n, 1.0);
@@ -593,10 +598,12 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
         (rc = dalloc(&e->part_force, (size_t)std::max(fb, ub) * kForcePartials)) ||
         (rc = dalloc(&e->part_bbox, (size_t)std::max(fb, ub) * kBBoxStride)) ||
         (rc = dalloc(&e->part_energy, (size_t)fb * kEnergyKinds)) || (rc = dalloc(&e->force_out, n)) ||
-        (rc = dalloc(&e->pbuf, (size_t)2 * force_grid(n) * kTile)) || (rc = dalloc(&e->tcnt, force_grid(n))))
+        (rc = dalloc(&e->pbuf, (size_t)2 * std::max(force_grid(n), kMaxUnits) * kTile)) ||
+        (rc = dalloc(&e->tcnt, std::max(force_grid(n), kMaxUnits))) || (rc = dalloc(&e->units, 2 * kMaxUnits)))
         return bail(rc);
     he = hipMemsetAsync(e->count, 0, (e->ncell_max + kScanPad) * sizeof(int), e->stream);
-    if (he == hipSuccess) he = hipMemsetAsync(e->tcnt, 0, force_grid(n) * sizeof(int), e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->tcnt, 0, std::max(force_grid(n), kMaxUnits) * sizeof(int), e->stream);
+    e->resident = std::min(force_step_resident(e->waves), kMaxUnits);
     if (he == hipSuccess) he = hipMemsetAsync(e->pos[0], 0, n * sizeof(float4), e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->pos[1], 0, n * sizeof(float4), e->stream);
     DevCtx c{};
@@ -634,6 +641,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->dsched);
     dfree(e->part_force);
     dfree(e->pbuf);
+    dfree(e->units);
     dfree(e->tcnt);
     dfree(e->part_bbox);
     dfree(e->part_energy);
@@ -1172,7 +1180,8 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
         e->fa.dbg_times = nullptr;
         HIPCHK(hipEventRecord(ev[3 + 5 * k], e->stream));
         if (fused)
-            launch_cell_scan(e->stream, e->ctx, e->n, e->count, e->cstart, e->tile_start, e->tile_range, true);
+            launch_cell_scan(e->stream, e->ctx, e->n, e->count, e->cstart, e->tile_start, e->tile_range, true,
+                         e->units, e->fa.split == 2 ? e->resident : 0);
         else
             launch_tail(e->stream, e->ctx, e->fa, fb, fb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
         HIPCHK(hipEventRecord(ev[4 + 5 * k], e->stream));
@@ -1263,7 +1272,7 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         return GCS_OK;
     }
     if (option == GCS_OPT_SPLIT_TILES) {
-        if (value != 0 && value != 1) return fail(GCS_EINVAL, "split tiles must be 0 or 1");
+        if (value < 0 || value > 2) return fail(GCS_EINVAL, "split tiles must be 0, 1 or 2");
         e->fa.split = (int)value;
         drop_graph(e);
         return GCS_OK;
@@ -1271,6 +1280,7 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
     if (option == GCS_OPT_WAVES_PER_TILE) {
         if (value != 1 && value != 2 && value != 4 && value != 8) return fail(GCS_EINVAL, "waves per tile must be 1, 2, 4 or 8");
         e->waves = (int)value;
+        e->resident = std::min(force_step_resident(e->waves), kMaxUnits);
         drop_graph(e);
         return GCS_OK;
     }

@@ -18,6 +18,7 @@ namespace gcs {
 constexpr int kTile = 64;          // particles per tile of the pair loop = one wave's lanes
 constexpr int kMaxRows = 64;       // stencil rows per batch of the pair loop's row table
 constexpr int kPairFx = 2;         // x subdivision of the pair cell grid
+constexpr int kMaxUnits = 8192;  // heavy-tile unit table / split budget capacity
 constexpr int kScanSeg = 16;        // cells per thread per iteration of the cell scan
 constexpr int kScanPad = kScanSeg * 1024 + 8;  // count/cstart padding: the scan touches whole iterations (<= 1024 threads)
 constexpr int kMaxPointSources = 4;
@@ -52,6 +53,10 @@ struct DevCtx {
     Grid grid_next;        // bins the positions the next step produces (fused path)
     unsigned ticket;       // arrival counter of the fused force kernel's blocks (0 between launches)
     int pad1;
+    int units_ok;          // the last cell scan wrote the heavy-tile unit table (ForceArgs::units)
+    int nunits;            // its length
+    int nactive;           // workgroups of the last force launch that had work (its partial rows)
+    int pad3;
     unsigned long long t_tail[2];  // wall clock at the start / end of k_tail
     unsigned long long t_rows[4];  // wall clock probes inside the cell scan's row pass (GCS_DEBUG)
     unsigned long long t_last[4];  // wall clock: fused last-block section start, after tail, after scan, end
@@ -136,7 +141,8 @@ struct ForceArgs {
     int ncell_max;
     int apply_sched;
     int prio_step;  // > 0: wave priority = min(3, candidates / prio_step) (GCS_OPT_TILE_PRIORITY)
-    int split;      // 1: step launches split tiles into two units (GCS_OPT_SPLIT_TILES)
+    int split;      // step launches: 1 split every tile in two units, 2 the heavy ones the scan picks (GCS_OPT_SPLIT_TILES)
+    const int4* units;  // [units] {s_begin, s_end, tile, part | nparts << 8} (split == 2)
     int split_cap;  // tiles that may be split (pbuf / tcnt capacity)
     float4* pbuf;   // [2 * split_cap][kTile] partial forces of split units
     int* tcnt;      // [split_cap] arrival counters of split tiles (0 between launches)
@@ -170,7 +176,8 @@ void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed
 void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n,
                        int* cell_of, int* slot, int* count);
 void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start, int2* tile_range,
-                      bool use_next = false);
+                      bool use_next = false, int4* units = nullptr, int resident = 0);
+int force_step_resident(int waves);
 void launch_scatter_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int* tmp, int fblocks, int apply_sched,
                          int ncell_max);
 void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* slot, const int* cstart, int* tmp,

@@ -74,6 +74,8 @@ __device__ __forceinline__ double dpp_d(double ident, double x)
     X = OP(X, DPP<0x143, 0xc>(IDENT, X)); /* bcast 31 -> rows 2, 3 */
 
 __device__ __forceinline__ int add_i(int a, int b) { return a + b; }
+__device__ __forceinline__ int max_i(int a, int b) { return max(a, b); }
+__device__ __forceinline__ int min_i(int a, int b) { return min(a, b); }
 __device__ __forceinline__ double add_d(double a, double b) { return a + b; }
 __device__ __forceinline__ float min_f(float a, float b) { return fminf(a, b); }
 __device__ __forceinline__ float max_f(float a, float b) { return fmaxf(a, b); }
@@ -310,6 +312,7 @@ __device__ inline int wave_incl_scan(int v, int lane)
 // re-read cstart.  count/cstart are padded by kScanPad so whole iterations may be touched; entries past ncell
 // are zero by invariant.  Any block size that is a multiple of 64 (<= 1024).
 constexpr int kRowsLds = 4096;
+constexpr int kCellsLds = 16384;
 
 // Row pass of the cell scan: tiles per row, their prefix (tile_start) and the tile table.  Row starts come from
 // LDS (LDS = true) or from cstart; two instantiations so the LDS path carries no global-load wait (on gfx9
@@ -317,7 +320,9 @@ constexpr int kRowsLds = 4096;
 template <bool LDS>
 __device__ __forceinline__ void scan_rows(DevCtx* __restrict__ ctx, const int* s_rowbeg, const int* __restrict__ cstart,
                                           int nx, int nrows, int* __restrict__ tile_start,
-                                          int2* __restrict__ tile_range, int (*wtot)[16], int it, int* s_tstart)
+                                          int2* __restrict__ tile_range, int (*wtot)[16], int it, int* s_tstart,
+                                          const int* s_cst, int4* __restrict__ units, int budget, int ny, int nz,
+                                          int gfx)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     int carry = 0;
@@ -367,11 +372,13 @@ __device__ __forceinline__ void scan_rows(DevCtx* __restrict__ ctx, const int* s
         }
         carry += ttot;
     }
+    bool units_ok = false;
+    int nunits = carry;
     if (LDS) {
         // tile-parallel table: thread t writes tiles t, t + blockDim, ... (coalesced); its row by binary search
         if (tid == 0) s_tstart[nrows] = carry;
         __syncthreads();
-        for (int k = tid; k < carry; k += blockDim.x) {
+        auto tile_of = [&](int k, int& row, int& sb, int& se) {
             int lo = 0, hi = nrows;  // last row r with s_tstart[r] <= k (that row is non-empty)
             while (hi - lo > 1) {
                 const int mid = (lo + hi) >> 1;
@@ -381,26 +388,150 @@ __device__ __forceinline__ void scan_rows(DevCtx* __restrict__ ctx, const int* s
                     hi = mid;
             }
             const int j = k - s_tstart[lo], rb = s_rowbeg[lo], re = s_rowbeg[lo + 1];
-            tile_range[k] = make_int2(rb + j * kTile, min(re, rb + (j + 1) * kTile));
+            row = lo;
+            sb = rb + j * kTile;
+            se = min(re, rb + (j + 1) * kTile);
+        };
+        const int ntl = carry;
+        const int room = budget - ntl;  // budget = resident workgroups of the force launch
+        if (s_cst && units && room > 0 && ntl <= 4 * (int)blockDim.x) {
+            // Heavy-tile selection for the next force launch.  A tile's pair work is its stencil's candidate count
+            // (the force kernel's `total`): from the cell starts in LDS, the cells of its first and last
+            // particle, x-range +-fx, 9 row segments.  Up to `budget` tiles (the workgroups that stay resident
+            // beside one per tile) whose count is at least 1.25x the mean and in the top `budget` are split in
+            // two units (split units first, adjacent pairs; then the others), so the densest tiles get 8 waves.
+            // budget - ntiles = the workgroups that stay resident beside one per tile.
+            __shared__ int s_hist[128];
+            __shared__ int s_red[2][16];
+            __shared__ int s_thr;
+            int cost[4], srow[4], ssb[4], sse[4];
+            int lmax = 0, lsum = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = 4 * tid + q;
+                cost[q] = 0;
+                srow[q] = ssb[q] = sse[q] = 0;
+                if (k < ntl) {
+                    tile_of(k, srow[q], ssb[q], sse[q]);
+                    tile_range[k] = make_int2(ssb[q], sse[q]);
+                    const int cb = srow[q] * nx;
+                    int x0 = 0, x1 = 0;
+                    for (int step = 1 << (31 - __clz(nx)); step > 0; step >>= 1) {
+                        if (x0 + step < nx && s_cst[cb + x0 + step] <= ssb[q]) x0 += step;
+                        if (x1 + step < nx && s_cst[cb + x1 + step] <= sse[q] - 1) x1 += step;
+                    }
+                    const int xlo = max(x0 - gfx, 0), xhi = min(x1 + gfx, nx - 1);
+                    const int y0 = srow[q] % ny, z0 = srow[q] / ny;
+                    int v = 0;
+#pragma unroll
+                    for (int d = 0; d < 9; ++d) {
+                        const int y = y0 + d % 3 - 1, z = z0 + d / 3 - 1;
+                        if (y >= 0 && y < ny && z >= 0 && z < nz) {
+                            const int base = (z * ny + y) * nx;
+                            v += s_cst[base + xhi + 1] - s_cst[base + xlo];
+                        }
+                    }
+                    cost[q] = v;
+                    lmax = max(lmax, v);
+                    lsum += v;
+                }
+            }
+            if (tid < 128) s_hist[tid] = 0;
+            // block max and sum
+            int wm = lmax, ws = lsum;
+            GCS_DPP_SCAN(dpp_i, max_i, 0, wm)
+            GCS_DPP_SCAN(dpp_i, add_i, 0, ws)
+            if (lane == 63) {
+                s_red[0][wave] = wm;
+                s_red[1][wave] = ws;
+            }
+            __syncthreads();
+            int cmax = 0;
+            long long csum = 0;
+            for (int w = 0; w < nw; ++w) {
+                cmax = max(cmax, s_red[0][w]);
+                csum += s_red[1][w];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (4 * tid + q < ntl) atomicAdd(&s_hist[(int)(((long long)cost[q] * 128) / (cmax + 1))], 1);
+            __syncthreads();
+            if (wave == 0) {
+                // lowest bin b whose tiles at or above it fit the room: P(b) >= ntiles - room with P the exclusive
+                // prefix of the histogram (lane l holds bins 2l, 2l + 1; one DPP scan, one wave minimum)
+                const int h0 = s_hist[2 * lane], h1 = s_hist[2 * lane + 1];
+                int pre = h0 + h1;
+                GCS_DPP_SCAN(dpp_i, add_i, 0, pre)
+                const int p_lo = pre - h0 - h1, p_mid = p_lo + h0, need = ntl - room;
+                int bmin = (p_lo >= need) ? 2 * lane : ((p_mid >= need) ? 2 * lane + 1 : 128);
+                GCS_DPP_SCAN(dpp_i, min_i, 128, bmin)
+                if (lane == 63) {
+                    // cost >= thr_bin <=> bin >= bmin; never below 1.25x the mean cost
+                    const int thr_bin = (int)(((long long)bmin * (cmax + 1) + 127) / 128);
+                    const int floor_cost = (int)((csum * 5) / (4LL * max(ntl, 1)));
+                    s_thr = max(max(thr_bin, floor_cost), 1);
+                }
+            }
+            __syncthreads();
+            const int thr = s_thr;
+            int nsp = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) nsp += (4 * tid + q < ntl && cost[q] >= thr) ? 1 : 0;
+            int incl = nsp;
+            GCS_DPP_SCAN(dpp_i, add_i, 0, incl)
+            if (lane == 63) wtot[(it + 1) & 1][wave] = incl;
+            __syncthreads();
+            int woff = 0, total_split = 0;
+            for (int w = 0; w < nw; ++w) {
+                const int t = wtot[(it + 1) & 1][w];
+                woff += (w < wave) ? t : 0;
+                total_split += t;
+            }
+            int rs = woff + incl - nsp;  // split tiles before mine
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = 4 * tid + q;
+                if (k >= ntl) continue;
+                if (cost[q] >= thr) {
+                    units[2 * rs] = make_int4(ssb[q], sse[q], k, 0 | (2 << 8));
+                    units[2 * rs + 1] = make_int4(ssb[q], sse[q], k, 1 | (2 << 8));
+                    ++rs;
+                } else {
+                    units[2 * total_split + (k - rs)] = make_int4(ssb[q], sse[q], k, 0 | (1 << 8));
+                }
+            }
+            units_ok = true;
+            nunits = ntl + total_split;
+        } else {
+            for (int k = tid; k < carry; k += blockDim.x) {
+                int row, sb, se;
+                tile_of(k, row, sb, se);
+                tile_range[k] = make_int2(sb, se);
+            }
         }
     }
     if (tid == 0) {
         tile_start[nrows] = carry;
         ctx->ntiles = carry;
+        ctx->units_ok = units_ok ? 1 : 0;
+        ctx->nunits = nunits;
         ctx->t_rows[3] = wall_clock64();
     }
 }
 
 __device__ __forceinline__ void scan_cells_body(DevCtx* __restrict__ ctx, int n, int* __restrict__ count,
                                                 int* __restrict__ cstart, int* __restrict__ tile_start,
-                                                int2* __restrict__ tile_range, bool use_next)
+                                                int2* __restrict__ tile_range, bool use_next,
+                                                int4* __restrict__ units, int resident)
 {
     const Grid& g = use_next ? ctx->grid_next : ctx->grid;
     __shared__ int wtot[2][16];
     __shared__ int s_rowbeg[kRowsLds + 1];
     __shared__ int s_tstart[kRowsLds + 1];
+    __shared__ int s_cst[kCellsLds + 1];  // cell starts (heavy-tile selection)
     const int nc = g.ncell, nx = g.n[0], nrows = g.n[1] * g.n[2];
     const bool rows_lds = nrows <= kRowsLds;
+    const bool cells_lds = rows_lds && nc <= kCellsLds && units != nullptr && resident > 0;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     int carry = 0, it = 0;
     {
@@ -443,6 +574,11 @@ __device__ __forceinline__ void scan_cells_body(DevCtx* __restrict__ ctx, int n,
                 if (i0 + 4 * q < nc)
                     *reinterpret_cast<int4*>(cstart + i0 + 4 * q) =
                         make_int4(run + pre[4 * q], run + pre[4 * q + 1], run + pre[4 * q + 2], run + pre[4 * q + 3]);
+            if (cells_lds) {
+#pragma unroll
+                for (int q = 0; q < kScanSeg; ++q)
+                    if (i0 + q < nc) s_cst[i0 + q] = run + pre[q];
+            }
             if (rows_lds && i0 < nc) {  // row boundaries r * nx inside [i0, i0 + kScanSeg)
                 int r = (i0 + nx - 1) / nx;
                 for (int b = r * nx; b < i0 + kScanSeg && b < nc; b += nx, ++r) {
@@ -460,21 +596,25 @@ __device__ __forceinline__ void scan_cells_body(DevCtx* __restrict__ ctx, int n,
     if (tid == 0) {
         cstart[nc] = n;
         if (rows_lds) s_rowbeg[nrows] = n;
+        if (cells_lds) s_cst[nc] = n;
         ctx->t_last[2] = wall_clock64();
     }
     __syncthreads();
     if (rows_lds)
-        scan_rows<true>(ctx, s_rowbeg, cstart, nx, nrows, tile_start, tile_range, wtot, it, s_tstart);
+        scan_rows<true>(ctx, s_rowbeg, cstart, nx, nrows, tile_start, tile_range, wtot, it, s_tstart,
+                        cells_lds ? s_cst : nullptr, cells_lds ? units : nullptr, resident, g.n[1], g.n[2], g.fx);
     else
-        scan_rows<false>(ctx, s_rowbeg, cstart, nx, nrows, tile_start, tile_range, wtot, it, s_tstart);
+        scan_rows<false>(ctx, s_rowbeg, cstart, nx, nrows, tile_start, tile_range, wtot, it, s_tstart, nullptr,
+                         nullptr, 0, g.n[1], g.n[2], g.fx);
 }
 
 __global__ __launch_bounds__(1024) void k_cell_scan(DevCtx* __restrict__ ctx, int n, int* __restrict__ count,
                                                     int* __restrict__ cstart, int* __restrict__ tile_start,
-                                                    int2* __restrict__ tile_range, int use_next)
+                                                    int2* __restrict__ tile_range, int use_next,
+                                                    int4* __restrict__ units, int resident)
 {
     const unsigned long long t0 = wall_clock64();
-    scan_cells_body(ctx, n, count, cstart, tile_start, tile_range, use_next != 0);
+    scan_cells_body(ctx, n, count, cstart, tile_start, tile_range, use_next != 0, units, resident);
     if (threadIdx.x == 0) {
         ctx->t_last[0] = ctx->t_last[1] = t0;
         ctx->t_last[3] = wall_clock64();
@@ -1030,15 +1170,29 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     // free up (a tile's cost varies ~5x with the local density; whole tiles pinned 4-5 per CU left the kernel
     // waiting on the most loaded CU).  The two halves meet through a per-tile arrival counter: the second to
     // finish adds the other's partial forces (write-through stores / sc1 loads) and integrates.
-    const int nsplit = (MODE == kModeStep && a.split) ? min(ntiles, a.split_cap) : 0;
-    const int nunits = ntiles + nsplit;
+    // a.split == 2: the cell scan chose the heavy tiles and wrote the unit table (ctx->units_ok)
+    const bool heavy = MODE == kModeStep && a.split == 2 && a.units != nullptr && ctx->units_ok != 0;
+    const int nsplit = (MODE == kModeStep && a.split == 1) ? min(ntiles, a.split_cap) : 0;
+    const int nunits = heavy ? ctx->nunits : ntiles + nsplit;
+    // workgroups with work: the others leave identity partials, which the tail need not read
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctx->nactive = min((int)gridDim.x, max(nunits, 1));
     int first_tile = -1, ntot = 0;
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
-        const int tile = (u < 2 * nsplit) ? (u >> 1) : u - nsplit;
-        const int part = (u < 2 * nsplit) ? (u & 1) : 0;
-        const int nparts = (u < 2 * nsplit) ? 2 : 1;
+        int tile, part, nparts;
+        int2 tr;
+        if (heavy) {
+            const int4 ud = a.units[u];
+            tr = make_int2(ud.x, ud.y);
+            tile = uniform(ud.z);
+            part = uniform(ud.w & 0xff);
+            nparts = uniform(ud.w >> 8);
+        } else {
+            tile = (u < 2 * nsplit) ? (u >> 1) : u - nsplit;
+            part = (u < 2 * nsplit) ? (u & 1) : 0;
+            nparts = (u < 2 * nsplit) ? 2 : 1;
+            tr = a.tile_range[tile];
+        }
         if (first_tile < 0) first_tile = tile;
-        const int2 tr = a.tile_range[tile];
         const int s_begin = uniform(tr.x), s_end = uniform(tr.y);
         const int s = s_begin + lane;
         const bool valid = s < s_end;
@@ -1319,6 +1473,10 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
     const auto rb = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_bbox, 0, bblocks * 32, 0x00020000);
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     float bb[6] = {big, big, big, -big, -big, -big};
+    if (fblocks == bblocks && ctx->nactive > 0) {  // step launches: only the working blocks' rows
+        fblocks = min(fblocks, ctx->nactive);
+        bblocks = fblocks;
+    }
     const int nrow = max(fblocks, bblocks);
     for (int b0 = tid; b0 < nrow; b0 += kTailRows * B) {
         float4 f0[kTailRows], f1[kTailRows], g0[kTailRows], g1[kTailRows];
@@ -1533,10 +1691,26 @@ void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, con
 }
 
 void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start, int2* tile_range,
-                      bool use_next)
+                      bool use_next, int4* units, int resident)
 {
     hipLaunchKernelGGL(k_cell_scan, dim3(1), dim3(1024), 0, s, ctx, n, count, cstart, tile_start, tile_range,
-                       use_next ? 1 : 0);
+                       use_next ? 1 : 0, units, resident);
+}
+
+int force_step_resident(int waves)
+{
+    // workgroups of the fused step kernel resident at once on the whole device
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    hipError_t e = hipErrorInvalidValue;
+    switch (waves) {
+    case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_force<kModeStep, 1, true>, 64, 0); break;
+    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_force<kModeStep, 2, true>, 128, 0); break;
+    case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_force<kModeStep, 8, true>, 512, 0); break;
+    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_force<kModeStep, 4, true>, 256, 0); break;
+    }
+    return e == hipSuccess ? per * cus : 0;
 }
 
 void launch_scatter_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int* tmp, int fblocks, int apply_sched,
@@ -1563,7 +1737,7 @@ void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, cons
 template <int MODE, bool FUSED>
 static void launch_force_mode(hipStream_t s, int waves, DevCtx* ctx, const ForceArgs& a)
 {
-    const dim3 grid((MODE == kModeStep && a.split) ? force_grid_split(a.n) : force_grid(a.n));
+    const dim3 grid((MODE == kModeStep && a.split) ? force_grid_split(a.n) : force_grid(a.n));  // >= units
     switch (waves) {
     case 1: hipLaunchKernelGGL((k_force<MODE, 1, FUSED>), grid, dim3(64), 0, s, ctx, a); break;
     case 2: hipLaunchKernelGGL((k_force<MODE, 2, FUSED>), grid, dim3(128), 0, s, ctx, a); break;

@@ -8,8 +8,11 @@ and the schedule tail), i.e. one iteration of md::simulate_brownian_dynamics.  T
 300,000 (t = 3, core_scale = 0.9988): the regime of >90 % of the reference's 700,000 production steps.
 Inputs are resident in HBM before the timed region.
 
-Multi-GPU (torchrun): one independent replica per rank (own master seed, like `scripts/simulate -s`), no data-path
-collective; value = all particle updates / max-over-ranks time ("scaling": "weak").
+Replicas: each GPU runs --replicas-per-gpu independent trajectories (default 4; own master seed and noise seed,
+like separate `scripts/simulate -s` runs), each with its own engine and HIP stream, so the GPU overlaps one
+trajectory's latency-bound launches with another's force kernel.  The single-trajectory rate is reported beside
+it (config.single_trajectory_value).  Multi-GPU (torchrun): every rank does the same with its own replicas, no
+data-path collective; value = all particle updates / max-over-ranks time ("scaling": "weak").
 
 Rank 0 prints ONE JSON line.  See DESIGN.md "Measurement" for the roofline accounting.
 """
@@ -80,9 +83,26 @@ def whole_job_value(n: int, steps: int, world: int, el_max: float) -> float:
     return n * steps * world / el_max
 
 
-def make_engine(design, cfg, device, start_step):
+STATE_FILE = ROOT / "benchdata" / "c2_interphase_step300000.npz"
+
+
+def load_state():
+    """The timed window's starting state: C2 run through the interphase schedule from step 0 to 300,000
+    (tools/make_bench_state.py): wall expanded by the wall ODE, ~25 neighbours per bead in the cutoff."""
+    z = np.load(STATE_FILE, allow_pickle=False)
+    ctx = {"step": int(z["step"]), "time": float(z["time"]), "core_scale": float(z["core_scale"]),
+           "bond_scale": float(z["bond_scale"]), "wall_semiaxes": [float(v) for v in z["wall_semiaxes"]]}
+    return z["positions"].astype(np.float64), ctx
+
+
+def make_engine(design, cfg, device, start_step, state=None):
     e, _ = interphase.build_interphase(Engine, design, cfg, device=device)
     e.set_schedule(**interphase.interphase_schedule(cfg))
+    if state is not None:
+        x, ctx = state
+        e.set_positions(x)
+        e.set_context(ctx)
+        return e
     t = start_step * cfg.timestep
     cs = 1 - (1 - cfg.core_scale_init) * np.exp(-t / cfg.core_scale_tau)
     bs = 1 - (1 - cfg.bond_scale_init) * np.exp(-t / cfg.bond_scale_tau)
@@ -91,15 +111,14 @@ def make_engine(design, cfg, device, start_step):
     return e
 
 
-def cpu_baseline(design, cfg, start_step, budget_s):
-    """The oracle (fp64, 1 thread, reference flags) on a bounded sample of the same workload."""
+def cpu_baseline(design, cfg, start_step, budget_s, state):
+    """The oracle (fp64, 1 thread, reference flags) on a bounded sample of the same workload (same state)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg only
     o, _ = interphase.build_interphase(oracle.OracleSystem, design, cfg)
     o.set_schedule(**interphase.interphase_schedule(cfg))
-    t = start_step * cfg.timestep
-    o.set_context({"step": start_step, "time": t, "core_scale": 1 - 0.5 * np.exp(-t / 0.5),
-                   "bond_scale": 1 - 0.5 * np.exp(-t / 0.5), "wall_semiaxes": list(cfg.wall_semiaxes_init)})
+    o.set_positions(state[0])
+    o.set_context(state[1])
     t0 = time.perf_counter()
     o.run(1, first_step=start_step, seed=1)
     one = time.perf_counter() - t0
@@ -108,7 +127,7 @@ def cpu_baseline(design, cfg, start_step, budget_s):
     o.run(steps, first_step=start_step + 1, seed=1)
     el = time.perf_counter() - t0
     return {"value": design.n * steps / el, "unit": "bead-updates/s", "cores": 1, "kind": "port",
-            "sample": f"C2 {design.n} particles, {steps} steps from step {start_step + 1} "
+            "sample": f"C2 {design.n} particles from the bench state, {steps} steps from step {start_step + 1} "
                       f"({el:.1f} s, oracle/libgcs_oracle.so fp64 single thread, -O2 -funsafe-math-optimizations)"}
 
 
@@ -132,10 +151,12 @@ def main():
     ap.add_argument("--graph-steps", type=int, default=32)
     ap.add_argument("--waves", type=int, default=4)
     ap.add_argument("--chunk-order", type=int, default=1)
-    ap.add_argument("--split", type=int, default=0, help="1: split each tile's candidates over two workgroups")
+    ap.add_argument("--split", type=int, default=0, help="0 off, 1 split every tile over two workgroups, 2 the heavy tiles")
     ap.add_argument("--prio", type=int, default=700, help="n > 0: wave priority min(3, tile candidates / n)")
     ap.add_argument("--fused", type=int, default=1, help="1: 4-launch step (force kernel bins the new positions)")
     ap.add_argument("--profile-steps", type=int, default=50)
+    ap.add_argument("--replicas-per-gpu", type=int, default=4,
+                    help="independent trajectories per GPU, each its own engine + stream (1 = single trajectory)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline work (0 = skip)")
     ap.add_argument("--no-start-window", action="store_true", help="skip the secondary step-0 window")
     args = ap.parse_args()
@@ -143,40 +164,76 @@ def main():
     world, rank, local, dist = dist_setup()
     cfg = InterphaseConfig()
     maker = {"c1": synthetic.make_c1, "c2": synthetic.make_c2, "c5": synthetic.make_c5}[args.config]
-    design = maker(master_seed=replica_master_seed(rank))
+    R = max(1, args.replicas_per_gpu)
+
+    # R independent trajectories per GPU (own master seed, own engine and HIP stream each): the GPU overlaps one
+    # replica's latency-bound launches (cell scan, tail) with another's force kernel.  Rank r owns replicas
+    # r*R .. r*R + R - 1, so every trajectory of the job has its own seeds.
+    # C2: every replica continues the committed step-300,000 state of the master-seed-1 system with its own noise
+    # seed (tools/make_bench_state.py); other configs start from their synthetic state at the window's context
+    state = load_state() if args.config == "c2" else None
+    designs, engines, seeds = [], [], []
+    for k in range(R):
+        rid = rank * R + k
+        d = maker(master_seed=1 if state is not None else replica_master_seed(rid))
+        e = make_engine(d, cfg, local, WINDOW_START, state)
+        e.set_option(A.OPT_GRAPH_STEPS, args.graph_steps)
+        e.set_option(A.OPT_WAVES_PER_TILE, args.waves)
+        e.set_option(A.OPT_CHUNK_ORDER, args.chunk_order)
+        e.set_option(A.OPT_FUSED_STEP, args.fused)
+        e.set_option(A.OPT_SPLIT_TILES, args.split)
+        e.set_option(A.OPT_TILE_PRIORITY, args.prio)
+        designs.append(d)
+        engines.append(e)
+        seeds.append(replica_noise_seed(rid))
+    design, eng, seed = designs[0], engines[0], seeds[0]
     n = design.n
 
-    eng = make_engine(design, cfg, local, WINDOW_START)
-    eng.set_option(A.OPT_GRAPH_STEPS, args.graph_steps)
-    eng.set_option(A.OPT_WAVES_PER_TILE, args.waves)
-    eng.set_option(A.OPT_CHUNK_ORDER, args.chunk_order)
-    eng.set_option(A.OPT_FUSED_STEP, args.fused)
-    eng.set_option(A.OPT_SPLIT_TILES, args.split)
-    eng.set_option(A.OPT_TILE_PRIORITY, args.prio)
-    seed = replica_noise_seed(rank)
-
-    eng.run(args.warmup, first_step=WINDOW_START, seed=seed)
-    eng.synchronize()
+    for e, sd in zip(engines, seeds):
+        e.run(args.warmup, first_step=WINDOW_START, seed=sd)
+    for e in engines:
+        e.synchronize()
     first = WINDOW_START + args.warmup
 
+    nxt = [first] * R  # next step of every replica (host-side: no device round trip in the timed loop)
+    # one trajectory alone on the GPU first (replica 0; the others are independent, their window starts later)
+    single_rate = None
+    if R > 1 and rank == 0:
+        k1 = max(256, args.steps // 2)
+        t1 = time.perf_counter()
+        eng.run(k1, first_step=first, seed=seed)
+        eng.synchronize()
+        single_rate = n * k1 / (time.perf_counter() - t1)
+        nxt[0] += k1
+
+    def run_all(steps):
+        chunk = 2 * args.graph_steps if args.graph_steps > 0 else 64
+        for s0 in range(0, steps, chunk):  # interleaved enqueue: the replicas' graphs run side by side
+            c = min(chunk, steps - s0)
+            for k, (e, sd) in enumerate(zip(engines, seeds)):
+                e.run(c, first_step=nxt[k], seed=sd)
+                nxt[k] += c
+        for e in engines:
+            e.synchronize()
+
     barrier(dist)
-    eng.synchronize()
+    for e in engines:
+        e.synchronize()
     t0 = time.perf_counter()
-    eng.run(args.steps, first_step=first, seed=seed)
-    eng.synchronize()
+    run_all(args.steps)
     el = time.perf_counter() - t0
     barrier(dist)
     el_max = max_over_ranks(dist, el)
+    after = nxt[0]
 
-    # per-kernel durations with HIP events on the engine's stream (after the timed region)
-    prof = eng.profile(args.profile_steps, first_step=first + args.steps, seed=seed)
+    # per-kernel durations with HIP events on the engine's stream (replica 0 alone, after the timed region)
+    prof = eng.profile(args.profile_steps, first_step=after, seed=seed)
     force_ms = prof["force_ms"]
     achieved = n * BYTES_PER_UPDATE / (force_ms * 1e-3) / 1e9
     ctx = eng.get_context()
-    x = eng.get_positions()
-    finite = bool(np.isfinite(x).all())
+    finite = all(bool(np.isfinite(e.get_positions()).all()) for e in engines)
 
-    # secondary: the production start window (step 0, core_scale 0.5, ~7x fewer neighbours)
+    # secondary: the production start window (step 0, core_scale 0.5, ~7x fewer neighbours), one replica
     start_rate = None
     if rank == 0 and not args.no_start_window:
         e0 = make_engine(design, cfg, local, 0)
@@ -191,16 +248,17 @@ def main():
         e0.close()
 
     if rank != 0:
-        eng.close()
+        for e in engines:
+            e.close()
         if dist is not None:
             dist.destroy_process_group()
         return
 
     cpu = None
-    if world == 1 and args.cpu_budget > 0:
-        cpu = cpu_baseline(design, cfg, WINDOW_START, args.cpu_budget)
+    if world == 1 and args.cpu_budget > 0 and state is not None:
+        cpu = cpu_baseline(design, cfg, WINDOW_START, args.cpu_budget, state)
 
-    value = whole_job_value(n, args.steps, world, el_max)
+    value = whole_job_value(n * R, args.steps, world, el_max)
     line = {
         "metric": "bead-updates/sec (whole node), 60k-bead diploid interphase",
         "value": value,
@@ -208,15 +266,18 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": el_max * 1e3 / args.steps,
+        "ms_per_step": el_max * 1e3 / args.steps,  # one step of every replica
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
-        "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, window from step "
-                               f"{WINDOW_START} (core_scale {ctx['core_scale']:.4f})",
-                   "particles": n, "replicas": world, "parallelism": f"replicas{world}",
+        "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, {R} independent "
+                               f"trajectories per GPU, window from step {WINDOW_START} "
+                               f"(core_scale {ctx['core_scale']:.4f})",
+                   "particles": n, "replicas": world * R, "replicas_per_gpu": R,
+                   "parallelism": f"replicas{world}x{R}",
+                   "single_trajectory_value": single_rate if R > 1 else value,
                    "mean_neighbors": prof["mean_neighbors"], "graph_steps": args.graph_steps,
                    "waves_per_tile": args.waves, "chunk_order": args.chunk_order, "fused": args.fused, "split_tiles": args.split, "tile_priority": args.prio, "start_window_value": start_rate, "finite": finite},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -226,7 +287,8 @@ def main():
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
-    eng.close()
+    for e in engines:
+        e.close()
     if dist is not None:
         dist.destroy_process_group()
 

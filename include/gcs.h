@@ -270,7 +270,8 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
 #define GCS_OPT_WAVES_PER_TILE 2 /* waves sharing one 64-particle tile of the pair loop: 1, 2, 4 or 8 */
 #define GCS_OPT_CHUNK_ORDER 3    /* pair-loop candidate chunks: 0 contiguous, 1 strided across stencil rows (default) */
 #define GCS_OPT_FUSED_STEP 4     /* 1: 4 launches per step: the force kernel bins the new positions (default) */
-#define GCS_OPT_SPLIT_TILES 5    /* 1: step launches split each tile's candidates over two workgroups (default 0) */
+#define GCS_OPT_SPLIT_TILES 5    /* step launches: 0 (default) off, 1 split every tile over two workgroups, 2 only the
+                                    densest tiles, picked by the cell scan within the resident-workgroup budget */
 #define GCS_OPT_TILE_PRIORITY 6  /* n > 0: pair-loop wave priority min(3, tile candidates / n); 0 = off (default 700) */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
 

@@ -162,11 +162,13 @@ def test_waves_per_tile_equivalent(c1_design, interphase_cfg, waves, order):
 
 
 @pytest.mark.parametrize("fused", [0, 1])
-def test_split_tiles_agree(c2_design, interphase_cfg, fused):
-    """Splitting each tile's candidates over two workgroups only regroups the fp32 pair sums: the C2 trajectory
-    stays within fp32 tolerance of the unsplit one, and the split run is bitwise reproducible."""
+@pytest.mark.parametrize("mode", [1, 2])
+def test_split_tiles_agree(c2_design, interphase_cfg, fused, mode):
+    """Splitting tiles' candidates over two workgroups (mode 1: every tile; mode 2: the heavy tiles the cell scan
+    picks) only regroups the fp32 pair sums: the C2 trajectory stays within fp32 tolerance of the unsplit one,
+    and the split run is bitwise reproducible."""
     out = []
-    for split in (0, 1, 1):
+    for split in (0, mode, mode):
         e, _ = interphase.build_interphase(Engine, c2_design, interphase_cfg)
         e.set_option(A.OPT_FUSED_STEP, fused)
         e.set_option(A.OPT_SPLIT_TILES, split)
