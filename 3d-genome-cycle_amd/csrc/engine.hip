@@ -1235,6 +1235,11 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
                          d.ntiles, 1e3 * (d.t_last[2] - d.t_last[1]) / khz, 1e3 * (d.t_last[3] - d.t_last[2]) / khz,
                          1e3 * (d.t_tail[1] - d.t_tail[0]) / khz);
         if (khz > 0)
+            std::fprintf(stderr, "gcs: cell probes: start->loaded %.2f, sum %.2f, scan+barrier %.2f, stores %.2f, "
+                         "->pass end %.2f us\n", 1e3 * (d.t_cells[0] - d.t_last[0]) / khz,
+                         1e3 * (d.t_cells[1] - d.t_cells[0]) / khz, 1e3 * (d.t_cells[2] - d.t_cells[1]) / khz,
+                         1e3 * (d.t_cells[3] - d.t_cells[2]) / khz, 1e3 * (d.t_last[2] - d.t_cells[3]) / khz);
+        if (khz > 0)
             std::fprintf(stderr, "gcs: rows probes: cellpass->rows %.2f, rows scan %.2f, barrier %.2f, stores %.2f, "
                          "->end %.2f us\n", 1e3 * (d.t_rows[0] - d.t_last[2]) / khz,
                          1e3 * (d.t_rows[1] - d.t_rows[0]) / khz, 1e3 * (d.t_rows[2] - d.t_rows[1]) / khz,

@@ -59,6 +59,7 @@ struct DevCtx {
     int pad3;
     unsigned long long t_tail[2];  // wall clock at the start / end of k_tail
     unsigned long long t_rows[4];  // wall clock probes inside the cell scan's row pass (GCS_DEBUG)
+    unsigned long long t_cells[4];  // wall clock probes inside the cell scan's cell pass (GCS_DEBUG)
     unsigned long long t_last[4];  // wall clock: fused last-block section start, after tail, after scan, end
 };
 

@@ -519,6 +519,78 @@ __device__ __forceinline__ void scan_rows(DevCtx* __restrict__ ctx, const int* s
     }
 }
 
+// Cell pass of the cell scan: SEG consecutive cells per thread (16-B loads), DPP wave scan, one barrier per pass
+// (double-buffered wave totals), cstart stores, row starts (and, for the heavy-tile selection, every cell start)
+// captured in LDS.  PREFETCH issues the next pass's loads before this pass's scan.
+template <int SEG, bool PREFETCH>
+__device__ __forceinline__ void scan_cell_pass(const int* __restrict__ count, int* __restrict__ cstart, int nc, int nx,
+                                               bool rows_lds, int* s_rowbeg, bool cells_lds, int* s_cst,
+                                               int (*wtot)[16], int& carry, int& it, DevCtx* ctx)
+{
+    static_assert(SEG % 4 == 0, "counts are loaded as int4");
+    constexpr int kQ = SEG / 4;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const int span = SEG * blockDim.x;
+    const auto rc = __builtin_amdgcn_make_buffer_rsrc((void*)count, 0, nc * 4, 0x00020000);  // past nc: 0
+    int4 cur[kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) cur[q] = ld_sc1_i4(rc, (SEG * tid + 4 * q) * 4);
+    for (int base = 0; base < nc; base += span, ++it) {
+        const int i0 = base + SEG * tid;
+        int4 nxt[PREFETCH ? kQ : 1];
+        if (PREFETCH && base + span < nc) {
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) nxt[q] = ld_sc1_i4(rc, (i0 + span + 4 * q) * 4);
+        }
+        if (tid == 0 && it == 0) ctx->t_cells[0] = wall_clock64();
+        int sum = 0;
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) sum += cur[q].x + cur[q].y + cur[q].z + cur[q].w;
+        if (tid == 0 && it == 0) ctx->t_cells[1] = wall_clock64();
+        const int incl = wave_incl_scan_dpp(sum);
+        if (lane == 63) wtot[it & 1][wave] = incl;
+        __syncthreads();
+        if (tid == 0 && it == 0) ctx->t_cells[2] = wall_clock64();
+        int woff = 0, ttot = 0;
+        for (int w = 0; w < nw; ++w) {
+            const int t = wtot[it & 1][w];
+            woff += (w < wave) ? t : 0;
+            ttot += t;
+        }
+        const int run = carry + woff + incl - sum;
+        // row boundaries (cells r * nx) are recognised as the running cell index reaches the next one
+        int r = (i0 + nx - 1) / nx;
+        int nb = (rows_lds && i0 < nc) ? r * nx : 0x7fffffff;
+        int acc = run;
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {  // (count is re-zeroed by the scatter, which knows the occupied cells)
+            const int4 st = make_int4(acc, acc + cur[q].x, acc + cur[q].x + cur[q].y,
+                                      acc + cur[q].x + cur[q].y + cur[q].z);
+            const int c = i0 + 4 * q;
+            if (c < nc) *reinterpret_cast<int4*>(cstart + c) = st;
+            if (cells_lds) {
+                if (c < nc) s_cst[c] = st.x;
+                if (c + 1 < nc) s_cst[c + 1] = st.y;
+                if (c + 2 < nc) s_cst[c + 2] = st.z;
+                if (c + 3 < nc) s_cst[c + 3] = st.w;
+            }
+            while (nb < c + 4 && nb < nc) {  // at most a few per thread
+                const int j = nb - c;
+                s_rowbeg[r] = j == 0 ? st.x : (j == 1 ? st.y : (j == 2 ? st.z : st.w));
+                nb += nx;
+                ++r;
+            }
+            acc = st.w + cur[q].w;
+        }
+        if (tid == 0 && it == 0) ctx->t_cells[3] = wall_clock64();
+        carry += ttot;
+        if (PREFETCH) {
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) cur[q] = nxt[q];
+        }
+    }
+}
+
 __device__ __forceinline__ void scan_cells_body(DevCtx* __restrict__ ctx, int n, int* __restrict__ count,
                                                 int* __restrict__ cstart, int* __restrict__ tile_start,
                                                 int2* __restrict__ tile_range, bool use_next,
@@ -532,67 +604,13 @@ __device__ __forceinline__ void scan_cells_body(DevCtx* __restrict__ ctx, int n,
     const int nc = g.ncell, nx = g.n[0], nrows = g.n[1] * g.n[2];
     const bool rows_lds = nrows <= kRowsLds;
     const bool cells_lds = rows_lds && nc <= kCellsLds && units != nullptr && resident > 0;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const int tid = threadIdx.x;
     int carry = 0, it = 0;
-    {
-        static_assert(kScanSeg % 4 == 0, "kScanSeg counts are loaded as int4");
-        constexpr int kQ = kScanSeg / 4;
-        const int span = kScanSeg * blockDim.x;
-        const auto rc = __builtin_amdgcn_make_buffer_rsrc((void*)count, 0, nc * 4, 0x00020000);  // past nc: 0
-        int4 cur[kQ];
-#pragma unroll
-        for (int q = 0; q < kQ; ++q) cur[q] = ld_sc1_i4(rc, (kScanSeg * tid + 4 * q) * 4);
-        for (int base = 0; base < nc; base += span, ++it) {
-            const int i0 = base + kScanSeg * tid;
-            int4 nxt[kQ];
-            if (base + span < nc) {
-#pragma unroll
-                for (int q = 0; q < kQ; ++q) nxt[q] = ld_sc1_i4(rc, (i0 + span + 4 * q) * 4);
-            }
-            int pre[kScanSeg];  // exclusive prefix inside the thread's segment
-            int sum = 0;
-#pragma unroll
-            for (int q = 0; q < kQ; ++q) {
-                pre[4 * q] = sum;
-                pre[4 * q + 1] = sum + cur[q].x;
-                pre[4 * q + 2] = sum + cur[q].x + cur[q].y;
-                pre[4 * q + 3] = sum + cur[q].x + cur[q].y + cur[q].z;
-                sum += cur[q].x + cur[q].y + cur[q].z + cur[q].w;
-            }
-            const int incl = wave_incl_scan_dpp(sum);
-            if (lane == 63) wtot[it & 1][wave] = incl;
-            __syncthreads();
-            int woff = 0, ttot = 0;
-            for (int w = 0; w < nw; ++w) {
-                const int t = wtot[it & 1][w];
-                woff += (w < wave) ? t : 0;
-                ttot += t;
-            }
-            const int run = carry + woff + incl - sum;
-#pragma unroll
-            for (int q = 0; q < kQ; ++q)  // (count is re-zeroed by the scatter, which knows the occupied cells)
-                if (i0 + 4 * q < nc)
-                    *reinterpret_cast<int4*>(cstart + i0 + 4 * q) =
-                        make_int4(run + pre[4 * q], run + pre[4 * q + 1], run + pre[4 * q + 2], run + pre[4 * q + 3]);
-            if (cells_lds) {
-#pragma unroll
-                for (int q = 0; q < kScanSeg; ++q)
-                    if (i0 + q < nc) s_cst[i0 + q] = run + pre[q];
-            }
-            if (rows_lds && i0 < nc) {  // row boundaries r * nx inside [i0, i0 + kScanSeg)
-                int r = (i0 + nx - 1) / nx;
-                for (int b = r * nx; b < i0 + kScanSeg && b < nc; b += nx, ++r) {
-                    int v = 0;
-#pragma unroll
-                    for (int q = 0; q < kScanSeg; ++q) v = (b - i0 == q) ? pre[q] : v;
-                    s_rowbeg[r] = run + v;
-                }
-            }
-            carry += ttot;
-#pragma unroll
-            for (int q = 0; q < kQ; ++q) cur[q] = nxt[q];
-        }
-    }
+    // up to 48 Ki cells: one pass of 48 cells per thread; beyond, 16-cell passes with the next pass prefetched
+    if (nc <= 48 * (int)blockDim.x)
+        scan_cell_pass<48, false>(count, cstart, nc, nx, rows_lds, s_rowbeg, cells_lds, s_cst, wtot, carry, it, ctx);
+    else
+        scan_cell_pass<16, true>(count, cstart, nc, nx, rows_lds, s_rowbeg, cells_lds, s_cst, wtot, carry, it, ctx);
     if (tid == 0) {
         cstart[nc] = n;
         if (rows_lds) s_rowbeg[nrows] = n;
