@@ -567,6 +567,7 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
     e->fa.chunk_mode = 1;  // strided candidate chunks (GCS_OPT_CHUNK_ORDER)
     e->fa.split = 0;       // split tiles (GCS_OPT_SPLIT_TILES): 1 and 2 measured slower on C2
     e->fa.prio_step = 700; // tile-cost wave priority (GCS_OPT_TILE_PRIORITY): +2 % on C2
+    e->fa.subtiles = 2;    // per-group stencils (GCS_OPT_SUBTILES)
     const int n = e->n;
     e->mu.assign(n, 1.0);
     e->ab.assign(2 * (size_t)n, 0.0);
@@ -1267,6 +1268,12 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
     if (option == GCS_OPT_CHUNK_ORDER) {
         if (value != 0 && value != 1) return fail(GCS_EINVAL, "chunk order must be 0 (contiguous) or 1 (strided)");
         e->fa.chunk_mode = (int)value;
+        drop_graph(e);
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_SUBTILES) {
+        if (value != 1 && value != 2 && value != 4) return fail(GCS_EINVAL, "sub-tiles must be 1, 2 or 4");
+        e->fa.subtiles = (int)value;
         drop_graph(e);
         return GCS_OK;
     }

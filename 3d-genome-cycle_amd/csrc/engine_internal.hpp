@@ -141,6 +141,7 @@ struct ForceArgs {
     const double* sched;
     int ncell_max;
     int apply_sched;
+    int subtiles;   // pair-loop stencil groups per tile: 1, 2 or 4 (GCS_OPT_SUBTILES)
     int prio_step;  // > 0: wave priority = min(3, candidates / prio_step) (GCS_OPT_TILE_PRIORITY)
     int split;      // step launches: 1 split every tile in two units, 2 the heavy ones the scan picks (GCS_OPT_SPLIT_TILES)
     const int4* units;  // [units] {s_begin, s_end, tile, part | nparts << 8} (split == 2)

@@ -1144,6 +1144,180 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
     }
 }
 
+// Sub-tile pair forces (a.subtiles = NG > 1): the tile's 64 lanes form NG groups of GL = 64 / NG consecutive
+// particles, each with its OWN stencil x-range (the cells of its first and last particle +-fx) and its own
+// candidate stream.  At the realistic interphase density a 64-particle tile spans ~10 rc of its cell row, so a
+// lane's share of the tile-wide union stencil is mostly candidates far beyond its cutoff (hit rate ~5 %); per
+// group of 16 the union shrinks ~2.5x.  Chunks are 32 candidates per group (one 32-bit hit mask per lane), staged
+// with FPL = 32 / GL loads per lane; phase-1 LDS reads then carry NG addresses (one broadcast per group, the groups
+// on disjoint banks).  Same phase-1 test, frame (per-group origin) and phase 2 as pair_forces.
+template <int MODE, int NG>
+__device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const ForceArgs& a, int lane, int s,
+                                       int s_begin, int s_end, float4 pi, float bi, float& fx, float& fy, float& fz,
+                                       float& acc, int* s_rowV, int* s_rowJ, float4* s_cand, int* s_candj, int& ntot,
+                                       int wv, int nwv)
+{
+    constexpr int GL = kTile / NG;  // lanes (particles) per group
+    constexpr int kSub = 32;        // candidates per group chunk
+    constexpr int FPL = kSub / GL;  // candidate fetches per lane per chunk
+    constexpr int kRec = 2 * (kSub + 1);  // float4 per group staging area (records + sentinel)
+    static_assert(NG >= 2 && NG <= 8 && FPL >= 1, "2, 4 or 8 groups");
+    const Grid g = ctx->grid;
+    const float cs = (float)ctx->cs;
+    const float scale = a.pair_scaled ? cs : 1.f;
+    const float sa = a.pa_sig * scale, sbb = a.pb_sig * scale;
+    const float k2a = 1.f / (sa * sa), k2b = 1.f / (sbb * sbb);
+    const float kA = (MODE == kModeEnergy) ? 0.25f * a.pa_eps : 0.5f * 6.f * a.pa_eps * k2a;
+    const float kB = (MODE == kModeEnergy) ? 0.25f * a.pb_eps : 0.5f * 24.f * a.pb_eps * k2b;
+    const float rc2 = g.rc2;
+    const int nx = g.n[0], ny = g.n[1], nz = g.n[2], gfx = g.fx;
+    const int grp = lane / GL, gl = lane % GL;
+
+    // row tables: lane (h, q) = (lane / 9, lane % 9) < 9 NG builds group h's stencil row q; groups are segments of
+    // one wave scan (offset = scan - group base)
+    {
+        const int h = lane / 9, q = lane % 9;
+        int len = 0, jb = 0;
+        const int r0 = uniform(a.scell[s_begin]) / nx;  // the tile's cell row (all groups share it)
+        const int y0 = r0 % ny, z0 = r0 / ny;
+        if (h < NG) {
+            const int hb = s_begin + h * GL, he = min(s_end, hb + GL);
+            if (hb < he) {
+                const int x0 = a.scell[hb] % nx, x1 = a.scell[he - 1] % nx;
+                const int xlo = max(x0 - gfx, 0), xhi = min(x1 + gfx, nx - 1);
+                const int y = y0 + q % 3 - 1, z = z0 + q / 3 - 1;
+                if (y >= 0 && y < ny && z >= 0 && z < nz) {
+                    const int base = (z * ny + y) * nx;
+                    jb = a.cstart[base + xlo];
+                    len = a.cstart[base + xhi + 1] - jb;
+                }
+            }
+        }
+        int incl = len;
+        GCS_DPP_SCAN(dpp_i, add_i, 0, incl)
+        const int gbase = __shfl(incl, max(9 * h - 1, 0));
+        const int off = incl - len - (h > 0 ? gbase : 0);
+        if (h < NG) {
+            s_rowV[h * 17 + q] = off;
+            s_rowJ[h * 16 + q] = jb;
+            if (q == 8)
+                for (int t = 9; t < 17; ++t) s_rowV[h * 17 + t] = off + len;  // rows 9.. start at the group total
+        }
+    }
+    // per-group frame origin: the group's first particle (the tile's first for empty trailing groups)
+    const int olane = (s_begin + grp * GL < s_end) ? grp * GL : 0;
+    const float ox = __shfl(pi.x, olane), oy = __shfl(pi.y, olane), oz = __shfl(pi.z, olane);
+    const float xi = pi.x - ox, yi = pi.y - oy, zi = pi.z - oz;
+    const float thr = rc2 - fmaf(zi, zi, fmaf(yi, yi, xi * xi));
+    const float far = 1.0e3f * fmaxf(g.rc, 1.f);
+    float4* const my_cand = s_cand + grp * kRec;
+    if (gl == 0) {
+        my_cand[2 * kSub] = make_float4(-2.f * far, -2.f * far, -2.f * far, 3.f * far * far);
+        my_cand[2 * kSub + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int* const rowV = s_rowV + grp * 17;
+    const int* const rowJ = s_rowJ + grp * 16;
+    const int total = rowV[16];  // my group's candidates
+    ntot = uniform(wave_max_int(total));
+    const float ahi = kA * pi.w, bhi = kB * bi;
+    const int G = (total + kSub - 1) / kSub;   // my group's chunks; chunk c takes v = c + G * i
+    const int Gmax = uniform(wave_max_int(G));
+    const int nchunk = Gmax > wv ? (Gmax - wv + nwv - 1) / nwv : 0;
+
+    float4 np[FPL];
+    float nb[FPL];
+    int nj[FPL];
+    auto fetch = [&](int c) {
+        const int cg = wv + c * nwv;  // chunk index within every group
+#pragma unroll
+        for (int f = 0; f < FPL; ++f) {
+            const int i = gl + GL * f;  // slot
+            const int v = cg + G * i;
+            nj[f] = -1;
+            if (cg < G && v < total) {
+                int lo = 0;
+#pragma unroll
+                for (int step = 8; step > 0; step >>= 1)
+                    if (rowV[lo + step] <= v) lo += step;
+                nj[f] = rowJ[lo] + (v - rowV[lo]);
+                np[f] = a.spos[nj[f]];
+                nb[f] = a.sb[nj[f]];
+            }
+        }
+    };
+    if (nchunk > 0) fetch(0);
+    for (int c = 0; c < nchunk; ++c) {
+#pragma unroll
+        for (int f = 0; f < FPL; ++f) {
+            const int i = gl + GL * f;
+            const bool real = nj[f] >= 0;
+            const float px = real ? np[f].x - ox : far, py = real ? np[f].y - oy : far, pz = real ? np[f].z - oz : far;
+            my_cand[2 * i] = make_float4(-2.f * px, -2.f * py, -2.f * pz, fmaf(pz, pz, fmaf(py, py, px * px)));
+            my_cand[2 * i + 1] = make_float4(real ? kA * np[f].w : 0.f, real ? kB * nb[f] : 0.f, 0.f, 0.f);
+            if (MODE == kModeEnergy) s_candj[grp * kSub + i] = nj[f];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (c + 1 < nchunk) fetch(c + 1);  // next chunk in flight
+
+        // phase 1: 32 candidates of my group -> one 32-bit hit mask (byte trick: candidate k on bit k ^ 7)
+        unsigned m = 0u;
+#pragma unroll
+        for (int k0 = 0; k0 < kSub; k0 += 8) {
+            unsigned byte = 0u;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const float4 q = my_cand[2 * (k0 + u)];
+                const float t = fmaf(q.x, xi, fmaf(q.y, yi, fmaf(q.z, zi, q.w)));
+                if (MODE == kModeEnergy) {
+                    const bool in = (t < thr) && (s_candj[grp * kSub + k0 + u] != s);
+                    byte = 2u * byte + (in ? 1u : 0u);
+                } else {
+                    asm("v_cmp_gt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+                        : "+v"(byte)
+                        : "v"(thr), "v"(t)
+                        : "vcc");
+                }
+            }
+            m |= byte << k0;
+        }
+        if (MODE != kModeEnergy) acc += (float)__popc(m);
+        // phase 2: pop ffbl, xor, min (exhausted -> the group's sentinel slot), clear
+        const int mh = uniform(wave_max_int(__popc(m)));
+        for (int t = 0; t < mh; t += 4) {
+            unsigned kk[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                unsigned b;
+                asm("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(m));
+                kk[u] = min(b ^ 7u, (unsigned)kSub);
+                m &= m - 1u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float4 q = my_cand[2 * kk[u]];
+                const float4 w = my_cand[2 * kk[u] + 1];
+                const float dx = fmaf(0.5f, q.x, xi), dy = fmaf(0.5f, q.y, yi), dz = fmaf(0.5f, q.z, zi);
+                const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                const float ga = fmaxf(fmaf(-k2a, r2, 1.f), 0.f);
+                const float tt = r2 * k2b;
+                const float t2 = tt * tt;
+                const float gb = fmaxf(fmaf(-t2, t2, 1.f), 0.f);
+                const float A = ahi + w.x, B = bhi + w.y;
+                if (MODE == kModeEnergy) {
+                    acc += fmaf(A, ga * ga * ga, B * (gb * gb * gb));
+                } else {
+                    const float coef = fmaf(A, ga * ga, B * (gb * gb * t2 * tt));
+                    fx = fmaf(coef, dx, fx);
+                    fy = fmaf(coef, dy, fy);
+                    fz = fmaf(coef, dz, fz);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // One launch = one force evaluation (+ the Euler-Maruyama update in kModeStep).  Blocks walk the tiles of the
 // current cell list (grid-stride); a tile is <= 64 consecutive sorted particles of ONE row of cells
 // (k_cell_scan builds the per-row tile prefix).  The WAVES waves split the tile's candidates; wave 0 then
@@ -1155,17 +1329,19 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
 // FUSED (kModeStep only): the new positions are also binned into ctx->grid_next (one wave-aggregated count
 // atomic per run of equal cells), so the next step's cell list needs only scan + scatter + sort (engine.hip
 // enqueue_step).
-template <int MODE, int WAVES, bool FUSED>
+template <int MODE, int WAVES, bool FUSED, int NG>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5))) void k_force(DevCtx* __restrict__ ctx, ForceArgs a)
 {
     __shared__ float red[WAVES > 1 ? WAVES : 1][4][64];
-    __shared__ int s_rowV[WAVES][17];
-    __shared__ int s_rowJ[WAVES][16];
-    __shared__ float4 s_cand[WAVES][2 * (kTile + 1)];  // candidate records (2 x float4) + sentinel
+    // per-wave pair-loop staging, sized for the larger of the two layouts: one 64-candidate stream (pair_forces) or
+    // up to 4 sub-tile streams of 32 (pair_forces_sub)
+    __shared__ int s_rowV[WAVES][4 * 17];
+    __shared__ int s_rowJ[WAVES][4 * 16];
+    __shared__ float4 s_cand[WAVES][4 * 2 * (32 + 1)];  // candidate records (2 x float4) + sentinel(s)
     __shared__ float4 s_locf[MODE == kModeStep ? kTile : 1];  // early local terms: force, mu
     __shared__ float4 s_locr[MODE == kModeStep ? kTile : 1];  // inward reaction, particle index
     __shared__ float4 s_loco[MODE == kModeStep ? kTile : 1];  // outward reaction
-    __shared__ int s_candj[MODE == kModeEnergy ? WAVES : 1][kTile];
+    __shared__ int s_candj[MODE == kModeEnergy ? WAVES : 1][4 * 32];
     __shared__ float s_pr[kForcePartials + kBBoxPartials];  // per-block accumulators (lane 0 of wave 0)
     __shared__ double s_pe[kEnergyKinds];
     const int lane = threadIdx.x & 63;
@@ -1235,10 +1411,16 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
             s_loco[lane] = make_float4(rout[0], rout[1], rout[2], 0.f);
         }
         if (a.dbg_times && threadIdx.x == 0 && first_tile == tile) s_dbg[0] = wall_clock64();
-        if (a.has_pair)
-            pair_forces<MODE, WAVES>(ctx, a, wave, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
-                                     s_rowJ[wave], s_cand[wave], s_candj[MODE == kModeEnergy ? wave : 0], ntot,
-                                     part * WAVES + wave, nparts * WAVES);
+        if (a.has_pair) {
+            int* const cj = s_candj[MODE == kModeEnergy ? wave : 0];
+            if (NG > 1)
+                pair_forces_sub<MODE, (NG > 1 ? NG : 2)>(ctx, a, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc,
+                                                         s_rowV[wave], s_rowJ[wave], s_cand[wave], cj, ntot,
+                                                         part * WAVES + wave, nparts * WAVES);
+            else
+                pair_forces<MODE, WAVES>(ctx, a, wave, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
+                                         s_rowJ[wave], s_cand[wave], cj, ntot, part * WAVES + wave, nparts * WAVES);
+        }
         if (a.dbg_times && threadIdx.x == 0 && first_tile == tile) s_dbg[1] = wall_clock64();
         if (WAVES > 1) {
             red[wave][0][lane] = fx;
@@ -1723,10 +1905,10 @@ int force_step_resident(int waves)
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
     hipError_t e = hipErrorInvalidValue;
     switch (waves) {
-    case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_force<kModeStep, 1, true>, 64, 0); break;
-    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_force<kModeStep, 2, true>, 128, 0); break;
-    case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_force<kModeStep, 8, true>, 512, 0); break;
-    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_force<kModeStep, 4, true>, 256, 0); break;
+    case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_force<kModeStep, 1, true, 1>, 64, 0); break;
+    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_force<kModeStep, 2, true, 1>, 128, 0); break;
+    case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_force<kModeStep, 8, true, 1>, 512, 0); break;
+    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_force<kModeStep, 4, true, 4>, 256, 0); break;
     }
     return e == hipSuccess ? per * cus : 0;
 }
@@ -1757,10 +1939,17 @@ static void launch_force_mode(hipStream_t s, int waves, DevCtx* ctx, const Force
 {
     const dim3 grid((MODE == kModeStep && a.split) ? force_grid_split(a.n) : force_grid(a.n));  // >= units
     switch (waves) {
-    case 1: hipLaunchKernelGGL((k_force<MODE, 1, FUSED>), grid, dim3(64), 0, s, ctx, a); break;
-    case 2: hipLaunchKernelGGL((k_force<MODE, 2, FUSED>), grid, dim3(128), 0, s, ctx, a); break;
-    case 8: hipLaunchKernelGGL((k_force<MODE, 8, FUSED>), grid, dim3(512), 0, s, ctx, a); break;
-    default: hipLaunchKernelGGL((k_force<MODE, 4, FUSED>), grid, dim3(256), 0, s, ctx, a); break;
+    case 1: hipLaunchKernelGGL((k_force<MODE, 1, FUSED, 1>), grid, dim3(64), 0, s, ctx, a); break;
+    case 2: hipLaunchKernelGGL((k_force<MODE, 2, FUSED, 1>), grid, dim3(128), 0, s, ctx, a); break;
+    case 8: hipLaunchKernelGGL((k_force<MODE, 8, FUSED, 1>), grid, dim3(512), 0, s, ctx, a); break;
+    default:
+        if (a.subtiles == 4)
+            hipLaunchKernelGGL((k_force<MODE, 4, FUSED, 4>), grid, dim3(256), 0, s, ctx, a);
+        else if (a.subtiles == 2)
+            hipLaunchKernelGGL((k_force<MODE, 4, FUSED, 2>), grid, dim3(256), 0, s, ctx, a);
+        else
+            hipLaunchKernelGGL((k_force<MODE, 4, FUSED, 1>), grid, dim3(256), 0, s, ctx, a);
+        break;
     }
 }
 
