@@ -99,6 +99,7 @@ struct gcs_engine {
     float4* force_out = nullptr;
     float4* pbuf = nullptr;  // split-tile partial forces
     int4* units = nullptr;    // heavy-tile unit table (cell scan -> force kernel)
+    unsigned long long* scan_sync = nullptr;  // multi-block cell scan: epoch word + look-back granules
     int resident = 0;         // force-step workgroups resident at once (split budget)
     int* tcnt = nullptr;     // split-tile arrival counters
     // topology tables
@@ -122,6 +123,7 @@ struct gcs_engine {
     int2* s_tile_range = nullptr;
     int s_ncell_max = 0;
     DevCtx* s_ctx = nullptr;
+    unsigned long long* s_scan_sync = nullptr;
     unsigned long long *s_keys = nullptr, *s_keys2 = nullptr;
     void* s_sort_temp = nullptr;
     size_t s_sort_bytes = 0;
@@ -136,6 +138,7 @@ struct gcs_engine {
     int graph_steps = 32;
     int waves = 4;
     bool fused = true;  // GCS_OPT_FUSED_STEP: the 4-launch step
+    bool scan_mb = true;  // GCS_OPT_SCAN_BLOCKS: multi-block cell scan (the heavy-tile split keeps one block)
     hipGraphExec_t gexec = nullptr;
     hipGraph_t graph = nullptr;
     int g_steps = 0, g_waves = 0, g_version = -1, g_spacestep = -1;
@@ -406,13 +409,20 @@ void fill_state_args(gcs_engine* e)
     a.split_cap = std::max(force_grid(e->n), kMaxUnits);
 }
 
+// scan the binned counts of ctx->grid (or ctx->grid_next): cstart, tile_start, tile table
+void enqueue_scan(gcs_engine* e, bool use_next)
+{
+    const bool heavy = e->fa.split == 2;
+    launch_cell_scan(e->stream, e->ctx, e->n, e->count, e->cstart, e->tile_start, e->tile_range, use_next, e->units,
+                     heavy ? e->resident : 0, e->scan_mb ? e->scan_sync : nullptr, e->ncell_max);
+}
+
 // bin the current positions into ctx->grid: per-cell counts + slots, scan, tile table
 void enqueue_bin(gcs_engine* e)
 {
     const int n = e->n;
     launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count);
-    launch_cell_scan(e->stream, e->ctx, n, e->count, e->cstart, e->tile_start, e->tile_range, false, e->units,
-                     e->fa.split == 2 ? e->resident : 0);
+    enqueue_scan(e, false);
 }
 
 // order each (scattered) cell by particle index: the cell-sorted copies the pair loop reads
@@ -450,8 +460,7 @@ void enqueue_step(gcs_engine* e, bool spacestep, float spacestep_v, float timest
     if (fused_path(e, spacestep)) {
         enqueue_cell_order(e);
         launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, true);
-        launch_cell_scan(e->stream, e->ctx, e->n, e->count, e->cstart, e->tile_start, e->tile_range, true,
-                         e->units, e->fa.split == 2 ? e->resident : 0);
+        enqueue_scan(e, true);
         launch_scatter_tail(e->stream, e->ctx, e->fa, e->tmp, sb, e->sched_flags != 0, e->ncell_max);
         return;
     }
@@ -600,9 +609,12 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
         (rc = dalloc(&e->part_bbox, (size_t)std::max(fb, ub) * kBBoxStride)) ||
         (rc = dalloc(&e->part_energy, (size_t)fb * kEnergyKinds)) || (rc = dalloc(&e->force_out, n)) ||
         (rc = dalloc(&e->pbuf, (size_t)2 * std::max(force_grid(n), kMaxUnits) * kTile)) ||
-        (rc = dalloc(&e->tcnt, std::max(force_grid(n), kMaxUnits))) || (rc = dalloc(&e->units, 2 * kMaxUnits)))
+        (rc = dalloc(&e->tcnt, std::max(force_grid(n), kMaxUnits))) || (rc = dalloc(&e->units, 2 * kMaxUnits)) ||
+        (rc = dalloc(&e->scan_sync, scan_sync_words(e->ncell_max))))
         return bail(rc);
     he = hipMemsetAsync(e->count, 0, (e->ncell_max + kScanPad) * sizeof(int), e->stream);
+    if (he == hipSuccess)
+        he = hipMemsetAsync(e->scan_sync, 0, scan_sync_words(e->ncell_max) * sizeof(unsigned long long), e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->tcnt, 0, std::max(force_grid(n), kMaxUnits) * sizeof(int), e->stream);
     e->resident = std::min(force_step_resident(e->waves), kMaxUnits);
     if (he == hipSuccess) he = hipMemsetAsync(e->pos[0], 0, n * sizeof(float4), e->stream);
@@ -643,6 +655,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->part_force);
     dfree(e->pbuf);
     dfree(e->units);
+    dfree(e->scan_sync);
     dfree(e->tcnt);
     dfree(e->part_bbox);
     dfree(e->part_energy);
@@ -670,6 +683,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->s_offsets);
     dfree(e->s_total);
     dfree(e->s_ctx);
+    dfree(e->s_scan_sync);
     dfree(e->s_keys);
     dfree(e->s_keys2);
     if (e->s_sort_temp) (void)hipFree(e->s_sort_temp);
@@ -1071,6 +1085,7 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
         dfree(e->s_offsets);
         dfree(e->s_total);
         dfree(e->s_ctx);
+        dfree(e->s_scan_sync);
         e->search_cap = 0;
         const int cap = (int)n;
         const int ncm = std::min(1 << 21, std::max(4096, 4 * cap));
@@ -1079,9 +1094,11 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
             (rc = dalloc(&e->s_slot, cap)) || (rc = dalloc(&e->s_tmp, cap)) || (rc = dalloc(&e->s_count, ncm + kScanPad)) ||
             (rc = dalloc(&e->s_cstart, ncm + kScanPad)) || (rc = dalloc(&e->s_counts, cap)) ||
             (rc = dalloc(&e->s_tile, ncm + 2)) || (rc = dalloc(&e->s_tile_range, (size_t)force_blocks(cap) + ncm + 2)) ||
-            (rc = dalloc(&e->s_offsets, cap)) || (rc = dalloc(&e->s_total, 1)) || (rc = dalloc(&e->s_ctx, 1)))
+            (rc = dalloc(&e->s_offsets, cap)) || (rc = dalloc(&e->s_total, 1)) || (rc = dalloc(&e->s_ctx, 1)) ||
+            (rc = dalloc(&e->s_scan_sync, scan_sync_words(ncm))))
             return rc;
         HIPCHK(hipMemsetAsync(e->s_count, 0, (ncm + kScanPad) * sizeof(int), e->stream));
+        HIPCHK(hipMemsetAsync(e->s_scan_sync, 0, scan_sync_words(ncm) * sizeof(unsigned long long), e->stream));
         e->search_cap = cap;
         e->s_ncell_max = ncm;
     }
@@ -1106,7 +1123,8 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
     sa.pos1 = const_cast<float4*>(src);
     launch_prime(e->stream, e->s_ctx, sa, (float)distance, e->s_ncell_max, nullptr);
     launch_cell_count(e->stream, e->s_ctx, src, src, ni, e->s_cell_of, e->s_slot, e->s_count);
-    launch_cell_scan(e->stream, e->s_ctx, ni, e->s_count, e->s_cstart, e->s_tile, e->s_tile_range);
+    launch_cell_scan(e->stream, e->s_ctx, ni, e->s_count, e->s_cstart, e->s_tile, e->s_tile_range, false, nullptr, 0,
+                     e->scan_mb ? e->s_scan_sync : nullptr, e->s_ncell_max);
     launch_cell_scatter(e->stream, ni, e->s_cell_of, e->s_slot, e->s_cstart, e->s_tmp, e->s_count);
     launch_cell_sort(e->stream, e->s_ctx, src, src, nullptr, ni, e->s_tmp, e->s_cell_of, e->s_cstart, e->s_sidx,
                      e->s_scell, e->s_spos, e->s_sb, 1);
@@ -1181,8 +1199,7 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
         e->fa.dbg_times = nullptr;
         HIPCHK(hipEventRecord(ev[3 + 5 * k], e->stream));
         if (fused)
-            launch_cell_scan(e->stream, e->ctx, e->n, e->count, e->cstart, e->tile_start, e->tile_range, true,
-                         e->units, e->fa.split == 2 ? e->resident : 0);
+            enqueue_scan(e, true);
         else
             launch_tail(e->stream, e->ctx, e->fa, fb, fb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
         HIPCHK(hipEventRecord(ev[4 + 5 * k], e->stream));
@@ -1268,6 +1285,12 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
     if (option == GCS_OPT_CHUNK_ORDER) {
         if (value != 0 && value != 1) return fail(GCS_EINVAL, "chunk order must be 0 (contiguous) or 1 (strided)");
         e->fa.chunk_mode = (int)value;
+        drop_graph(e);
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_SCAN_BLOCKS) {
+        if (value != 0 && value != 1) return fail(GCS_EINVAL, "scan blocks must be 0 (one block) or 1 (multi-block)");
+        e->scan_mb = value != 0;
         drop_graph(e);
         return GCS_OK;
     }

@@ -52,7 +52,7 @@ struct DevCtx {
     Grid grid;             // bins the current positions (the next force evaluation's stencil)
     Grid grid_next;        // bins the positions the next step produces (fused path)
     unsigned ticket;       // arrival counter of the fused force kernel's blocks (0 between launches)
-    int pad1;
+    int scan_stall;        // multi-block cell scans whose look-back gave up waiting (must stay 0)
     int units_ok;          // the last cell scan wrote the heavy-tile unit table (ForceArgs::units)
     int nunits;            // its length
     int nactive;           // workgroups of the last force launch that had work (its partial rows)
@@ -178,7 +178,9 @@ void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed
 void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n,
                        int* cell_of, int* slot, int* count);
 void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start, int2* tile_range,
-                      bool use_next = false, int4* units = nullptr, int resident = 0);
+                      bool use_next = false, int4* units = nullptr, int resident = 0,
+                      unsigned long long* scan_sync = nullptr, int ncell_max = 0);
+int scan_sync_words(int ncell_max);  // u64 words of the multi-block scan's look-back buffer
 int force_step_resident(int waves);
 void launch_scatter_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int* tmp, int fblocks, int apply_sched,
                          int ncell_max);

@@ -642,6 +642,182 @@ __global__ __launch_bounds__(1024) void k_cell_scan(DevCtx* __restrict__ ctx, in
 __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance,
                                           int apply_sched, int ncell_max, const double* __restrict__ sched, bool fused);
 
+// Multi-block cell scan (same outputs as k_cell_scan without the heavy-tile unit table).  Block b owns rows
+// [b*R, b*R + R) of the grid, R = max(1, kMbCells / nx): it scans their cells (8 consecutive cells per thread,
+// DPP wave scans), captures the row starts and the per-row tile counts in LDS, publishes its particle and tile
+// totals as two 8-byte {tag, value} granules, then sums its predecessors' granules (one wave; every earlier
+// block was dispatched first and waits only on blocks before it) and writes cstart, tile_start and the tile
+// table with those offsets.  The block owning the last row writes the totals and advances the epoch word
+// sync[0] (tag = epoch + 1, so granules of earlier launches never match).  Rows wider than kMbCells are scanned
+// in chunks, twice (the second pass writes).  Bitwise the same tables as the single-block scan.
+constexpr int kMbThreads = 256;
+constexpr int kMbSeg = 8;
+constexpr int kMbCells = kMbThreads * kMbSeg;
+constexpr unsigned kMbSpinCap = 1u << 22;  // look-back polls before giving up (counted in ctx->scan_stall)
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+__device__ __forceinline__ int mb_rows_per_block(int nx) { return max(1, kMbCells / nx); }
+
+// block-wide exclusive scan of one int per thread; returns the exclusive prefix, `total` the block sum
+__device__ __forceinline__ int mb_block_scan(int v, int (*wtot)[kMbThreads / 64], int it, int& total)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int incl = wave_incl_scan_dpp(v);
+    if (lane == 63) wtot[it & 1][wave] = incl;
+    __syncthreads();
+    int woff = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < kMbThreads / 64; ++w) {
+        const int t = wtot[it & 1][w];
+        woff += (w < wave) ? t : 0;
+        total += t;
+    }
+    return woff + incl - v;
+}
+
+__global__ __launch_bounds__(kMbThreads) void k_cell_scan_mb(DevCtx* __restrict__ ctx, int n,
+                                                              const int* __restrict__ count, int* __restrict__ cstart,
+                                                              int* __restrict__ tile_start,
+                                                              int2* __restrict__ tile_range, int use_next,
+                                                              unsigned long long* __restrict__ sync)
+{
+    const Grid& g = use_next ? ctx->grid_next : ctx->grid;
+    const int nx = g.n[0], nrows = g.n[1] * g.n[2], nc = g.ncell;
+    const int rpb = mb_rows_per_block(nx);
+    const int nb = (nrows + rpb - 1) / rpb;
+    const int b = blockIdx.x;
+    if (b >= nb) return;
+    __shared__ int wtot[2][kMbThreads / 64];
+    __shared__ int s_rowbeg[kMbCells + 1];  // block-local row starts (rows per block <= kMbCells)
+    __shared__ long long s_off[2];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const unsigned tag = (unsigned)sync[0] + 1u;
+    const int r0 = b * rpb, r1 = min(nrows, r0 + rpb), nr = r1 - r0;
+    const int c0 = r0 * nx, c1 = r1 * nx;
+    const bool one_chunk = c1 - c0 <= kMbCells;
+    int it = 0;
+
+    // pass 1: cell sums, the block-local cell prefix (kept in registers for a single chunk), row starts
+    int loc[kMbSeg];
+    int carry = 0;
+    for (int base = c0; base < c1; base += kMbCells, ++it) {
+        const int i0 = base + kMbSeg * tid;
+        int v[kMbSeg];
+        int sum = 0;
+#pragma unroll
+        for (int k = 0; k < kMbSeg; ++k) {
+            v[k] = (i0 + k < c1) ? count[i0 + k] : 0;
+            sum += v[k];
+        }
+        int ttot;
+        int acc = carry + mb_block_scan(sum, wtot, it, ttot);
+        int nbnd = ((i0 - c0 + nx - 1) / nx) * nx + c0;  // first row boundary at or after i0
+#pragma unroll
+        for (int k = 0; k < kMbSeg; ++k) {
+            loc[k] = acc;
+            if (i0 + k == nbnd && nbnd < c1) {
+                s_rowbeg[(nbnd - c0) / nx] = acc;
+                nbnd += nx;
+            }
+            acc += v[k];
+        }
+        carry += ttot;
+    }
+    if (tid == 0) {
+        s_rowbeg[nr] = carry;
+        __hip_atomic_store((gu64*)(sync + 2 + 2 * b), ((unsigned long long)tag << 32) | (unsigned)carry,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+
+    // tiles per row (<= kTile consecutive sorted particles of one row each) and their block-local prefix
+    const int rpt = (nr + kMbThreads - 1) / kMbThreads;  // rows per thread, contiguous
+    const int q0 = min(nr, tid * rpt), q1 = min(nr, q0 + rpt);
+    int tsum = 0;
+    for (int q = q0; q < q1; ++q) tsum += (s_rowbeg[q + 1] - s_rowbeg[q] + kTile - 1) / kTile;
+    int ttiles;
+    const int texcl = mb_block_scan(tsum, wtot, it, ttiles);
+    ++it;
+    if (tid == 0)
+        __hip_atomic_store((gu64*)(sync + 3 + 2 * b), ((unsigned long long)tag << 32) | (unsigned)ttiles,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+    // look-back: one wave sums the granules of blocks 0 .. b-1 (even words particles, odd words tiles)
+    if (wave == 0) {
+        long long p = 0, t = 0;
+        bool stalled = false;
+        for (int j = lane; j < 2 * b; j += 64) {
+            unsigned long long x;
+            unsigned spins = 0;
+            do {
+                x = __hip_atomic_load((gu64*)(sync + 2 + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } while ((unsigned)(x >> 32) != tag && ++spins < kMbSpinCap);
+            stalled |= (unsigned)(x >> 32) != tag;
+            if (j & 1)
+                t += (unsigned)x;
+            else
+                p += (unsigned)x;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            p += __shfl_xor(p, o);
+            t += __shfl_xor(t, o);
+        }
+        if (__any(stalled) && lane == 0) atomicAdd(&ctx->scan_stall, 1);
+        if (lane == 0) {
+            s_off[0] = p;
+            s_off[1] = t;
+        }
+    }
+    __syncthreads();
+    const int poff = (int)s_off[0], toff = (int)s_off[1];
+
+    // pass 2: cstart (from registers, or a second chunked scan), tile_start and the tile table
+    if (one_chunk) {
+        const int i0 = c0 + kMbSeg * tid;
+#pragma unroll
+        for (int k = 0; k < kMbSeg; ++k)
+            if (i0 + k < c1) cstart[i0 + k] = poff + loc[k];
+    } else {
+        carry = poff;
+        for (int base = c0; base < c1; base += kMbCells, ++it) {
+            const int i0 = base + kMbSeg * tid;
+            int v[kMbSeg];
+            int sum = 0;
+#pragma unroll
+            for (int k = 0; k < kMbSeg; ++k) {
+                v[k] = (i0 + k < c1) ? count[i0 + k] : 0;
+                sum += v[k];
+            }
+            int ttot;
+            int acc = carry + mb_block_scan(sum, wtot, it, ttot);
+#pragma unroll
+            for (int k = 0; k < kMbSeg; ++k) {
+                if (i0 + k < c1) cstart[i0 + k] = acc;
+                acc += v[k];
+            }
+            carry += ttot;
+        }
+    }
+    int tile = toff + texcl;  // this thread's rows' first tile
+    for (int q = q0; q < q1; ++q) {
+        const int rb = poff + s_rowbeg[q], re = poff + s_rowbeg[q + 1];
+        tile_start[r0 + q] = tile;
+        for (int s = rb; s < re; s += kTile) tile_range[tile++] = make_int2(s, min(re, s + kTile));
+    }
+    if (b == nb - 1 && tid == 0) {
+        const int ntl = toff + ttiles;
+        cstart[nc] = n;
+        tile_start[nrows] = ntl;
+        ctx->ntiles = ntl;
+        ctx->units_ok = 0;
+        ctx->nunits = ntl;
+        __hip_atomic_store((gu64*)sync, (unsigned long long)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // fused step: the scatter of the next step's cells, and in one extra block the tail of the step just computed
 // (partials -> reactions, schedule, wall; grid <- grid_next and the grid after it).  The scatter blocks touch
 // no DevCtx field, so the tail block owns the context.
@@ -1890,9 +2066,18 @@ void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, con
     hipLaunchKernelGGL(k_cell_count, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, n, cell_of, slot, count);
 }
 
+int scan_sync_words(int ncell_max) { return 2 + 2 * (ncell_max / (kMbCells / 2) + 2); }
+
 void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start, int2* tile_range,
-                      bool use_next, int4* units, int resident)
+                      bool use_next, int4* units, int resident, unsigned long long* scan_sync, int ncell_max)
 {
+    if (scan_sync && !(units && resident > 0)) {
+        // blocks for any grid of <= ncell_max cells: R*nx > kMbCells/2 cells per block (or one row of nx >= kMbCells)
+        const int blocks = ncell_max / (kMbCells / 2) + 2;
+        hipLaunchKernelGGL(k_cell_scan_mb, dim3(blocks), dim3(kMbThreads), 0, s, ctx, n, count, cstart, tile_start,
+                           tile_range, use_next ? 1 : 0, scan_sync);
+        return;
+    }
     hipLaunchKernelGGL(k_cell_scan, dim3(1), dim3(1024), 0, s, ctx, n, count, cstart, tile_start, tile_range,
                        use_next ? 1 : 0, units, resident);
 }

@@ -32,6 +32,7 @@ OPT_FUSED_STEP = 4
 OPT_SPLIT_TILES = 5
 OPT_TILE_PRIORITY = 6
 OPT_SUBTILES = 7
+OPT_SCAN_BLOCKS = 8
 
 ENERGY_KINDS = ("pair", "softwell", "bonds", "bending", "wall_in", "wall_out", "point_source", "kinetochore_fiber")
 

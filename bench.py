@@ -154,6 +154,7 @@ def main():
     ap.add_argument("--split", type=int, default=0, help="0 off, 1 split every tile over two workgroups, 2 the heavy tiles")
     ap.add_argument("--prio", type=int, default=700, help="n > 0: wave priority min(3, tile candidates / n)")
     ap.add_argument("--subtiles", type=int, default=2, help="pair-loop stencils per 64-particle tile: 1, 2, 4")
+    ap.add_argument("--scan-mb", type=int, default=1, help="1: multi-block look-back cell scan, 0: one workgroup")
     ap.add_argument("--fused", type=int, default=1, help="1: 4-launch step (force kernel bins the new positions)")
     ap.add_argument("--profile-steps", type=int, default=50)
     ap.add_argument("--replicas-per-gpu", type=int, default=4,
@@ -185,6 +186,7 @@ def main():
         e.set_option(A.OPT_SPLIT_TILES, args.split)
         e.set_option(A.OPT_TILE_PRIORITY, args.prio)
         e.set_option(A.OPT_SUBTILES, args.subtiles)
+        e.set_option(A.OPT_SCAN_BLOCKS, args.scan_mb)
         designs.append(d)
         engines.append(e)
         seeds.append(replica_noise_seed(rid))
@@ -281,7 +283,7 @@ def main():
                    "parallelism": f"replicas{world}x{R}",
                    "single_trajectory_value": single_rate if R > 1 else value,
                    "mean_neighbors": prof["mean_neighbors"], "graph_steps": args.graph_steps,
-                   "waves_per_tile": args.waves, "chunk_order": args.chunk_order, "fused": args.fused, "split_tiles": args.split, "tile_priority": args.prio, "subtiles": args.subtiles, "start_window_value": start_rate, "finite": finite},
+                   "waves_per_tile": args.waves, "chunk_order": args.chunk_order, "fused": args.fused, "split_tiles": args.split, "tile_priority": args.prio, "subtiles": args.subtiles, "scan_mb": args.scan_mb, "start_window_value": start_rate, "finite": finite},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(),
                      "kernel": "k_force<kModeStep>", "force_ms": force_ms, "cell_ms": prof["cell_ms"],

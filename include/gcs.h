@@ -273,6 +273,7 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
 #define GCS_OPT_SPLIT_TILES 5    /* step launches: 0 (default) off, 1 split every tile over two workgroups, 2 only the
                                     densest tiles, picked by the cell scan within the resident-workgroup budget */
 #define GCS_OPT_SUBTILES 7       /* pair-loop stencils per 64-particle tile: 1, 2 or 4 (default 2) */
+#define GCS_OPT_SCAN_BLOCKS 8    /* cell scan: 1 = multi-block look-back scan (default), 0 = one workgroup */
 #define GCS_OPT_TILE_PRIORITY 6  /* n > 0: pair-loop wave priority min(3, tile candidates / n); 0 = off (default 700) */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
 

@@ -182,6 +182,43 @@ def test_split_tiles_agree(c2_design, interphase_cfg, fused, mode):
 
 
 @pytest.mark.parametrize("fused", [0, 1])
+def test_scan_blocks_agree(c2_design, interphase_cfg, fused):
+    """The multi-block look-back cell scan builds the same cstart / tile tables as the one-workgroup scan, so
+    the C2 trajectories are bitwise equal."""
+    out = []
+    for mb in (0, 1):
+        e, _ = interphase.build_interphase(Engine, c2_design, interphase_cfg)
+        e.set_option(A.OPT_FUSED_STEP, fused)
+        e.set_option(A.OPT_SCAN_BLOCKS, mb)
+        e.set_schedule(**interphase.interphase_schedule(interphase_cfg))
+        e.apply_schedule(0)
+        e.run(30, seed=5)
+        out.append(e.get_positions())
+        e.close()
+    assert np.array_equal(out[0], out[1])
+
+
+@pytest.mark.parametrize("mb", [0, 1])
+@pytest.mark.parametrize("shape", ["x_line", "z_line", "slab"])
+def test_neighbor_search_grid_shapes(mb, shape):
+    """Degenerate grids for the cell scan: rows wider than one scan block (nx > 2048, chunked), one-cell rows
+    (nx = 1, 2048 rows per block) and a thin slab; pair sets bit-exact vs the oracle for both scan kinds."""
+    rng = np.random.default_rng(7)
+    d = 0.25
+    if shape == "x_line":
+        pts = np.stack([rng.uniform(0, 3000 * d, 3000), rng.uniform(0, 0.1, 3000), rng.uniform(0, 0.1, 3000)], 1)
+    elif shape == "z_line":
+        pts = np.stack([rng.uniform(0, 0.1, 3000), rng.uniform(0, 0.1, 3000), rng.uniform(0, 2500 * d, 3000)], 1)
+    else:
+        pts = np.stack([rng.uniform(0, 60, 5000), rng.uniform(0, 60, 5000), rng.uniform(0, 0.3, 5000)], 1)
+    e = Engine(4)
+    e.set_option(A.OPT_SCAN_BLOCKS, mb)
+    got = e.search_neighbors(d, points=pts)
+    exp = oracle.search_neighbors(pts, d)
+    assert got.shape == exp.shape and np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("fused", [0, 1])
 def test_chunked_runs_equal_one_run(c1_design, interphase_cfg, fused):
     """The Philox counter is the absolute step: 3 chunks == 1 run, bit for bit (both step shapes; the fused
     step carries its cell list across runs that continue at the next step)."""

@@ -10,7 +10,7 @@ root=$(pwd)
 out=$root/gpurun_out/prof_$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
-bench=(python3 "$root/bench.py" --steps "$steps" --warmup 50 --cpu-budget 0 --profile-steps 10 --no-start-window)
+bench=(python3 "$root/bench.py" --steps "$steps" --warmup 50 --cpu-budget 0 --profile-steps 10 --no-start-window --replicas-per-gpu "${REPLICAS:-1}")
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- "${bench[@]}" > "$out/trace.log" 2>&1 || exit $?
 i=0
 for ctrs in \
