@@ -102,6 +102,10 @@ struct gcs_engine {
     unsigned long long* scan_sync = nullptr;  // multi-block cell scan: epoch word + look-back granules
     int resident = 0;         // force-step workgroups resident at once (split budget)
     int* tcnt = nullptr;     // split-tile arrival counters
+    int* bucket = nullptr;   // rebuild step: [ncell_max][kBucketCap] particles filed per cell by the force kernel
+    int* ovf = nullptr;      // rebuild step: bucket overflow list [n]
+    int* ovf_n = nullptr;    // rebuild step: its two counters (step parity)
+    unsigned long long* rb_sync = nullptr;  // rebuild step: epoch word + look-back granules
     // topology tables
     int* boff = nullptr;
     int2* bent = nullptr;
@@ -137,7 +141,7 @@ struct gcs_engine {
     // options / graph cache
     int graph_steps = 32;
     int waves = 4;
-    bool fused = true;  // GCS_OPT_FUSED_STEP: the 4-launch step
+    int fused = 2;  // GCS_OPT_FUSED_STEP: 2 = the 2-launch rebuild step, 1 = the 4-launch step, 0 = unfused
     bool scan_mb = true;  // GCS_OPT_SCAN_BLOCKS: multi-block cell scan (the heavy-tile split keeps one block)
     hipGraphExec_t gexec = nullptr;
     hipGraph_t graph = nullptr;
@@ -406,6 +410,9 @@ void fill_state_args(gcs_engine* e)
     a.pbuf = e->pbuf;
     a.units = e->units;
     a.tcnt = e->tcnt;
+    a.bucket = e->fused == 2 ? e->bucket : nullptr;
+    a.ovf = e->ovf;
+    a.ovf_n = e->ovf_n;
     a.split_cap = std::max(force_grid(e->n), kMaxUnits);
 }
 
@@ -445,10 +452,14 @@ void enqueue_cells(gcs_engine* e)
     enqueue_sort(e);
 }
 
-bool fused_path(const gcs_engine* e, bool spacestep) { return e->fused && !spacestep; }
+bool fused_path(const gcs_engine* e, bool spacestep) { return e->fused != 0 && !spacestep; }
+bool rebuild_path(const gcs_engine* e, bool spacestep) { return e->fused == 2 && !spacestep; }
 int step_grid(const gcs_engine* e) { return e->fa.split ? force_grid_split(e->n) : force_grid(e->n); }
 
-// One BD step.  Fused (fixed timestep, 4 launches): sort the cells the previous step scattered; force + update,
+// One BD step.  Rebuild (fixed timestep, 2 launches, default): force + update, which also files the new positions
+// under the predicted next grid's cells; k_rebuild scans, builds the tile table and the cell-sorted copies from
+// those buckets, and runs the step's tail in its block 0.  begin_run built the first cell list.
+// Fused (fixed timestep, 4 launches): sort the cells the previous step scattered; force + update,
 // which also bins the new positions into the predicted next grid; scan those counts; scatter them, with the
 // step's tail (reduction, schedule, wall, grid rotation) in one extra block.  begin_run binned, scanned and
 // scattered the first positions.  Otherwise (spacestep, or fusion off): count, scan, scatter, sort, force,
@@ -457,6 +468,11 @@ void enqueue_step(gcs_engine* e, bool spacestep, float spacestep_v, float timest
 {
     const int fb = force_grid(e->n);
     const int sb = step_grid(e);  // kModeStep launch size (split tiles: two units per tile)
+    if (rebuild_path(e, spacestep)) {
+        launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, true);
+        launch_rebuild(e->stream, e->ctx, e->fa, e->tmp, e->rb_sync, sb, e->sched_flags != 0);
+        return;
+    }
     if (fused_path(e, spacestep)) {
         enqueue_cell_order(e);
         launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, true);
@@ -528,7 +544,10 @@ int begin_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
     e->chain_valid = false;
     if (!cont) {
         launch_prime(e->stream, e->ctx, a, 0.f, e->ncell_max, e->dsched);
-        if (fused) {
+        if (rebuild_path(e, cfg->spacestep > 0)) {
+            enqueue_cells(e);  // the first cell list; the steps rebuild it from the force kernel's buckets
+            HIPCHK(hipMemsetAsync(e->ovf_n, 0, 2 * sizeof(int), e->stream));
+        } else if (fused) {
             enqueue_bin(e);
             launch_cell_scatter(e->stream, e->n, e->cell_of, e->slot, e->cstart, e->tmp, e->count);
         }
@@ -610,11 +629,16 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
         (rc = dalloc(&e->part_energy, (size_t)fb * kEnergyKinds)) || (rc = dalloc(&e->force_out, n)) ||
         (rc = dalloc(&e->pbuf, (size_t)2 * std::max(force_grid(n), kMaxUnits) * kTile)) ||
         (rc = dalloc(&e->tcnt, std::max(force_grid(n), kMaxUnits))) || (rc = dalloc(&e->units, 2 * kMaxUnits)) ||
-        (rc = dalloc(&e->scan_sync, scan_sync_words(e->ncell_max))))
+        (rc = dalloc(&e->scan_sync, scan_sync_words(e->ncell_max))) ||
+        (rc = dalloc(&e->bucket, (size_t)e->ncell_max * kBucketCap)) || (rc = dalloc(&e->ovf, n)) ||
+        (rc = dalloc(&e->ovf_n, 2)) || (rc = dalloc(&e->rb_sync, rebuild_sync_words(e->ncell_max))))
         return bail(rc);
     he = hipMemsetAsync(e->count, 0, (e->ncell_max + kScanPad) * sizeof(int), e->stream);
     if (he == hipSuccess)
         he = hipMemsetAsync(e->scan_sync, 0, scan_sync_words(e->ncell_max) * sizeof(unsigned long long), e->stream);
+    if (he == hipSuccess)
+        he = hipMemsetAsync(e->rb_sync, 0, rebuild_sync_words(e->ncell_max) * sizeof(unsigned long long), e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->ovf_n, 0, 2 * sizeof(int), e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->tcnt, 0, std::max(force_grid(n), kMaxUnits) * sizeof(int), e->stream);
     e->resident = std::min(force_step_resident(e->waves), kMaxUnits);
     if (he == hipSuccess) he = hipMemsetAsync(e->pos[0], 0, n * sizeof(float4), e->stream);
@@ -656,6 +680,10 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->pbuf);
     dfree(e->units);
     dfree(e->scan_sync);
+    dfree(e->bucket);
+    dfree(e->ovf);
+    dfree(e->ovf_n);
+    dfree(e->rb_sync);
     dfree(e->tcnt);
     dfree(e->part_bbox);
     dfree(e->part_energy);
@@ -1185,11 +1213,14 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     for (auto& x : ev) HIPCHK(hipEventCreate(&x));
     const int fb = step_grid(e);
     HIPCHK(hipEventRecord(ev[0], e->stream));
-    const bool fused = fused_path(e, false);
+    const bool fused = fused_path(e, false), rebuild = rebuild_path(e, false);
     // per step: [1] cells [2] force [3] fused: next-step scan / unfused: tail [4] fused: scatter + tail [5]
+    // (rebuild: [1] - [2] force [3] rebuild + tail [4] - [5])
     for (int64_t k = 0; k < steps; ++k) {
         HIPCHK(hipEventRecord(ev[1 + 5 * k], e->stream));
-        if (fused)
+        if (rebuild)
+            ;
+        else if (fused)
             enqueue_cell_order(e);
         else
             enqueue_cells(e);
@@ -1198,12 +1229,14 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
         launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, fused);
         e->fa.dbg_times = nullptr;
         HIPCHK(hipEventRecord(ev[3 + 5 * k], e->stream));
-        if (fused)
+        if (rebuild)
+            launch_rebuild(e->stream, e->ctx, e->fa, e->tmp, e->rb_sync, fb, e->sched_flags != 0);
+        else if (fused)
             enqueue_scan(e, true);
         else
             launch_tail(e->stream, e->ctx, e->fa, fb, fb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
         HIPCHK(hipEventRecord(ev[4 + 5 * k], e->stream));
-        if (fused) launch_scatter_tail(e->stream, e->ctx, e->fa, e->tmp, fb, e->sched_flags != 0, e->ncell_max);
+        if (fused && !rebuild) launch_scatter_tail(e->stream, e->ctx, e->fa, e->tmp, fb, e->sched_flags != 0, e->ncell_max);
         HIPCHK(hipEventRecord(ev[5 + 5 * k], e->stream));
     }
     HIPCHK(hipEventRecord(ev[ev.size() - 1], e->stream));
@@ -1215,7 +1248,9 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
         float t[4] = {0, 0, 0, 0};
         for (int q = 0; q < 4; ++q) HIPCHK(hipEventElapsedTime(&t[q], ev[1 + q + 5 * k], ev[2 + q + 5 * k]));
         force += t[1];
-        if (fused) {
+        if (rebuild) {
+            cell += t[2];  // rebuild kernel (its tail block runs beside the cell-list blocks)
+        } else if (fused) {
             cell += t[0] + t[2];  // sort + scan
             tail += t[3];         // scatter + tail
         } else {
@@ -1278,7 +1313,8 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         return GCS_OK;
     }
     if (option == GCS_OPT_FUSED_STEP) {
-        e->fused = value != 0;
+        if (value < 0 || value > 2) return fail(GCS_EINVAL, "fused step must be 0, 1 or 2");
+        e->fused = (int)value;
         drop_graph(e);
         return GCS_OK;
     }

@@ -19,6 +19,7 @@ constexpr int kTile = 64;          // particles per tile of the pair loop = one 
 constexpr int kMaxRows = 64;       // stencil rows per batch of the pair loop's row table
 constexpr int kPairFx = 2;         // x subdivision of the pair cell grid
 constexpr int kMaxUnits = 8192;  // heavy-tile unit table / split budget capacity
+constexpr int kBucketCap = 16;   // particles filed per cell by the rebuild step's binning (more: overflow list)
 constexpr int kScanSeg = 16;        // cells per thread per iteration of the cell scan
 constexpr int kScanPad = kScanSeg * 1024 + 8;  // count/cstart padding: the scan touches whole iterations (<= 1024 threads)
 constexpr int kMaxPointSources = 4;
@@ -61,6 +62,12 @@ struct DevCtx {
     unsigned long long t_rows[4];  // wall clock probes inside the cell scan's row pass (GCS_DEBUG)
     unsigned long long t_cells[4];  // wall clock probes inside the cell scan's cell pass (GCS_DEBUG)
     unsigned long long t_last[4];  // wall clock: fused last-block section start, after tail, after scan, end
+    // rebuild step (GCS_OPT_FUSED_STEP 2): what the step's force kernel binned with, stashed by its block 0 so the
+    // rebuild kernel reads them while that kernel's tail block advances grid / parity / step
+    Grid rb_grid;
+    long long rb_step;
+    int rb_parity;
+    int pad4;
 };
 
 enum BondType : int { kSemispring = 0, kHarmonic = 1, kSpring = 2, kSoftwell = 3 };
@@ -149,6 +156,11 @@ struct ForceArgs {
     float4* pbuf;   // [2 * split_cap][kTile] partial forces of split units
     int* tcnt;      // [split_cap] arrival counters of split tiles (0 between launches)
     unsigned long long* dbg_times;  // optional (GCS_DEBUG_TIMES): per block {start, end, smid/candidates, tile} then 4 phase stamps
+    // rebuild step: the force kernel files each new position's particle under its cell (bucket[c][slot],
+    // slot < kBucketCap; the rest on the overflow list ovf, counted in ovf_n[step & 1]); nullptr = slot binning
+    int* bucket;
+    int* ovf;
+    int* ovf_n;
 };
 
 // ---- Philox4x32-10 + Box-Muller: the production noise stream (identical on host for the oracle) ----
@@ -181,6 +193,10 @@ void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart
                       bool use_next = false, int4* units = nullptr, int resident = 0,
                       unsigned long long* scan_sync = nullptr, int ncell_max = 0);
 int scan_sync_words(int ncell_max);  // u64 words of the multi-block scan's look-back buffer
+// rebuild step: cell scan + tile table + cell-sorted copies from the force kernel's buckets, and the step's tail
+void launch_rebuild(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int* tmp, unsigned long long* scan_sync,
+                    int fblocks, int apply_sched);
+int rebuild_sync_words(int ncell_max);
 int force_step_resident(int waves);
 void launch_scatter_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int* tmp, int fblocks, int apply_sched,
                          int ncell_max);

@@ -840,6 +840,273 @@ __global__ __launch_bounds__(256) void k_scatter_tail(DevCtx* ctx, ForceArgs a, 
     a.count[c] = 0;  // every occupied cell has a particle here: count is all-zero again for the next binning
 }
 
+// Rebuild step (GCS_OPT_FUSED_STEP 2): everything between two force kernels in ONE launch.  Block 0 runs the
+// step's tail (tail_body: reductions, schedule, wall, grid <- grid_next).  Blocks 1.. rebuild the cell list the
+// force kernel binned into its buckets, each owning rows of the grid (R = max(1, kRbCells / nx) rows): the
+// count scan, row starts and tiles of k_cell_scan_mb with the same look-back, and the cell-sorted copies
+// (spos / sb / sidx / scell) of its cells, members ordered by particle index inside each cell (as k_cell_sort).
+// Up to kRbPcap particles per block the members are staged and ranked in LDS (the gathers and the look-back
+// overlap); denser blocks, or rows wider than kRbCells, stage them in `tmp` (same result).  The grid, parity and
+// step come from the rb_* copies the force kernel stashed, so block 0 may advance the live ones concurrently.
+constexpr int kRbThreads = 256;
+constexpr int kRbSeg = 2;
+constexpr int kRbCells = kRbThreads * kRbSeg;
+constexpr int kRbPcap = 2048;
+constexpr int kRbUnroll = 4;  // sorted slots per thread in flight in the copy pass
+
+__device__ __forceinline__ void rb_write_sorted(const ForceArgs& a, int d, int i, int c, float4 p, float4 k)
+{
+    const_cast<float4*>(a.spos)[d] = make_float4(p.x, p.y, p.z, a.pair_mix ? k.y : 1.f);
+    const_cast<float*>(a.sb)[d] = a.pair_mix ? k.z : 0.f;
+    const_cast<int*>(a.sidx)[d] = i;
+    const_cast<int*>(a.scell)[d] = c;
+}
+
+// members of cell c beyond the bucket: the overflow list entries filed under c (rare; any order: ranked later)
+template <typename Put>
+__device__ __forceinline__ void rb_overflow(const ForceArgs& a, int novf, int c, Put put)
+{
+    int q = kBucketCap;
+    for (int t = 0; t < novf; ++t) {
+        const int i = a.ovf[t];
+        if (a.cell_of[i] == c) put(q++, i);
+    }
+}
+
+__global__ __launch_bounds__(kRbThreads) void k_rebuild(DevCtx* __restrict__ ctx, ForceArgs a, int* __restrict__ tmp,
+                                                        unsigned long long* __restrict__ sync, int fblocks,
+                                                        int apply_sched)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (blockIdx.x == 0) {
+        const long long st = ctx->rb_step;
+        const unsigned long long t0 = wall_clock64();
+        tail_body(ctx, a, fblocks, fblocks, 1, apply_sched, a.ncell_max, a.sched, true);
+        if (tid == 0) {
+            a.ovf_n[(st + 1) & 1] = 0;  // the next force kernel's overflow counter (last read one step ago)
+            ctx->t_tail[0] = t0;
+            ctx->t_tail[1] = wall_clock64();
+        }
+        return;
+    }
+    const Grid& g = ctx->rb_grid;
+    const int nx = g.n[0], nrows = g.n[1] * g.n[2], nc = g.ncell;
+    const int rpb = max(1, kRbCells / nx);
+    const int nb = (nrows + rpb - 1) / rpb;
+    const int b = blockIdx.x - 1;
+    if (b >= nb) return;
+    const float4* __restrict__ posn = ctx->rb_parity ? a.pos0 : a.pos1;  // the force kernel's new positions
+    const int novf = a.ovf_n[ctx->rb_step & 1];
+    __shared__ int wtot[2][kRbThreads / 64];
+    __shared__ int s_rowbeg[kRbCells + 1];  // block-local row starts
+    __shared__ int s_cst[kRbCells + 1];     // block-local cell starts (single chunk)
+    __shared__ int s_mem[kRbPcap];          // members, cell by cell, unsorted within a cell
+    __shared__ int s_mcell[kRbPcap];        // their block-local cell
+    __shared__ long long s_off[2];
+    const unsigned tag = (unsigned)sync[0] + 1u;
+    const int r0 = b * rpb, r1 = min(nrows, r0 + rpb), nr = r1 - r0;
+    const int c0 = r0 * nx, c1 = r1 * nx;
+    const bool one_chunk = c1 - c0 <= kRbCells;
+    int it = 0;
+
+    // pass 1: cell counts -> block-local cell starts (registers + LDS), row starts
+    int v[kRbSeg], loc[kRbSeg];
+    int carry = 0;
+    for (int base = c0; base < c1; base += kRbCells, ++it) {
+        const int i0 = base + kRbSeg * tid;
+        int sum = 0;
+#pragma unroll
+        for (int k = 0; k < kRbSeg; ++k) {
+            v[k] = (i0 + k < c1) ? a.count[i0 + k] : 0;
+            sum += v[k];
+        }
+        int ttot;
+        int acc = carry + mb_block_scan(sum, wtot, it, ttot);
+        int nbnd = ((i0 - c0 + nx - 1) / nx) * nx + c0;  // first row boundary at or after i0
+#pragma unroll
+        for (int k = 0; k < kRbSeg; ++k) {
+            loc[k] = acc;
+            if (one_chunk && i0 + k < c1) s_cst[i0 + k - c0] = acc;
+            if (i0 + k == nbnd && nbnd < c1) {
+                s_rowbeg[(nbnd - c0) / nx] = acc;
+                nbnd += nx;
+            }
+            acc += v[k];
+        }
+        carry += ttot;
+    }
+    const int P = carry;  // particles of this block's cells
+    if (tid == 0) {
+        s_rowbeg[nr] = P;
+        if (one_chunk) s_cst[c1 - c0] = P;
+        __hip_atomic_store((gu64*)(sync + 2 + 2 * b), ((unsigned long long)tag << 32) | (unsigned)P,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+
+    // tiles per row and their block-local prefix
+    const int rpt = (nr + kRbThreads - 1) / kRbThreads;
+    const int q0 = min(nr, tid * rpt), q1 = min(nr, q0 + rpt);
+    int tsum = 0;
+    for (int q = q0; q < q1; ++q) tsum += (s_rowbeg[q + 1] - s_rowbeg[q] + kTile - 1) / kTile;
+    int ttiles;
+    const int texcl = mb_block_scan(tsum, wtot, it, ttiles);
+    ++it;
+    if (tid == 0)
+        __hip_atomic_store((gu64*)(sync + 3 + 2 * b), ((unsigned long long)tag << 32) | (unsigned)ttiles,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+    // LDS path: stage the members (bucket loads overlap the look-back); counts re-zeroed for the next binning
+    const bool lds = one_chunk && P <= kRbPcap;
+    if (lds) {
+        const int i0 = c0 + kRbSeg * tid;
+#pragma unroll
+        for (int k = 0; k < kRbSeg; ++k) {
+            const int c = i0 + k;
+            if (c < c1 && v[k] > 0) {
+                a.count[c] = 0;
+                const int ls = loc[k], m = min(v[k], kBucketCap);
+                for (int j = 0; j < m; ++j) {
+                    s_mem[ls + j] = a.bucket[c * kBucketCap + j];
+                    s_mcell[ls + j] = c - c0;
+                }
+                if (v[k] > kBucketCap)
+                    rb_overflow(a, novf, c, [&](int q, int i) {
+                        s_mem[ls + q] = i;
+                        s_mcell[ls + q] = c - c0;
+                    });
+            }
+        }
+    }
+
+    // look-back: one wave sums the granules of blocks 0 .. b-1 (even words particles, odd words tiles)
+    if (wave == 0) {
+        long long p = 0, t = 0;
+        bool stalled = false;
+        for (int j = lane; j < 2 * b; j += 64) {
+            unsigned long long x;
+            unsigned spins = 0;
+            do {
+                x = __hip_atomic_load((gu64*)(sync + 2 + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } while ((unsigned)(x >> 32) != tag && ++spins < kMbSpinCap);
+            stalled |= (unsigned)(x >> 32) != tag;
+            if (j & 1)
+                t += (unsigned)x;
+            else
+                p += (unsigned)x;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            p += __shfl_xor(p, o);
+            t += __shfl_xor(t, o);
+        }
+        if (__any(stalled) && lane == 0) atomicAdd(&ctx->scan_stall, 1);
+        if (lane == 0) {
+            s_off[0] = p;
+            s_off[1] = t;
+        }
+    }
+    __syncthreads();
+    const int poff = (int)s_off[0], toff = (int)s_off[1];
+
+    // cstart, tile_start, tile table
+    if (one_chunk) {
+        const int i0 = c0 + kRbSeg * tid;
+#pragma unroll
+        for (int k = 0; k < kRbSeg; ++k)
+            if (i0 + k < c1) a.cstart_w[i0 + k] = poff + loc[k];
+    } else {
+        carry = poff;
+        for (int base = c0; base < c1; base += kRbCells, ++it) {
+            const int i0 = base + kRbSeg * tid;
+            int w[kRbSeg];
+            int sum = 0;
+#pragma unroll
+            for (int k = 0; k < kRbSeg; ++k) {
+                w[k] = (i0 + k < c1) ? a.count[i0 + k] : 0;
+                sum += w[k];
+            }
+            int ttot;
+            int acc = carry + mb_block_scan(sum, wtot, it, ttot);
+#pragma unroll
+            for (int k = 0; k < kRbSeg; ++k) {
+                if (i0 + k < c1) a.cstart_w[i0 + k] = acc;
+                acc += w[k];
+            }
+            carry += ttot;
+        }
+    }
+    int tile = toff + texcl;
+    for (int q = q0; q < q1; ++q) {
+        const int rb = poff + s_rowbeg[q], re = poff + s_rowbeg[q + 1];
+        a.tile_start_w[r0 + q] = tile;
+        for (int s = rb; s < re; s += kTile) a.tile_range_w[tile++] = make_int2(s, min(re, s + kTile));
+    }
+    if (b == nb - 1 && tid == 0) {
+        const int ntl = toff + ttiles;
+        a.cstart_w[nc] = a.n;
+        a.tile_start_w[nrows] = ntl;
+        ctx->ntiles = ntl;
+        ctx->units_ok = 0;
+        ctx->nunits = ntl;
+        __hip_atomic_store((gu64*)sync, (unsigned long long)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+
+    // cell-sorted copies: sorted slot poff + s holds the member of rank r in its cell (by particle index)
+    if (lds) {
+        for (int s0 = 0; s0 < P; s0 += kRbUnroll * kRbThreads) {
+            int d[kRbUnroll], ii[kRbUnroll], cc[kRbUnroll];
+            float4 p[kRbUnroll], k4[kRbUnroll];
+#pragma unroll
+            for (int u = 0; u < kRbUnroll; ++u) {
+                const int s = s0 + u * kRbThreads + tid;
+                d[u] = -1;
+                if (s < P) {
+                    const int m = s_mem[s], lc = s_mcell[s];
+                    const int ls = s_cst[lc], le = s_cst[lc + 1];
+                    int r = 0;
+                    for (int t = ls; t < le; ++t) r += (s_mem[t] < m) ? 1 : 0;
+                    d[u] = poff + ls + r;
+                    ii[u] = m;
+                    cc[u] = c0 + lc;
+                    p[u] = posn[m];
+                    k4[u] = a.kmu ? a.kmu[m] : make_float4(1.f, 1.f, 0.f, 0.f);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kRbUnroll; ++u)
+                if (d[u] >= 0) rb_write_sorted(a, d[u], ii[u], cc[u], p[u], k4[u]);
+        }
+    } else {
+        __syncthreads();  // this block's cstart entries are visible to all its threads
+        const int pend = poff + P;
+        for (int c = c0 + tid; c < c1; c += kRbThreads) {
+            const int cs = a.cstart_w[c], ce = (c + 1 < c1) ? a.cstart_w[c + 1] : pend;
+            const int m = min(ce - cs, kBucketCap);
+            for (int j = 0; j < m; ++j) tmp[cs + j] = a.bucket[c * kBucketCap + j];
+            if (ce - cs > kBucketCap) rb_overflow(a, novf, c, [&](int q, int i) { tmp[cs + q] = i; });
+        }
+        __syncthreads();
+        for (int s = poff + tid; s < pend; s += kRbThreads) {
+            int lo = c0, hi = c1;  // last cell c with cstart[c] <= s (it is non-empty)
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (a.cstart_w[mid] <= s)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            const int cs = a.cstart_w[lo], ce = (lo + 1 < c1) ? a.cstart_w[lo + 1] : pend;
+            const int m = tmp[s];
+            int r = 0;
+            for (int t = cs; t < ce; ++t) r += (tmp[t] < m) ? 1 : 0;
+            rb_write_sorted(a, cs + r, m, lo, posn[m], a.kmu ? a.kmu[m] : make_float4(1.f, 1.f, 0.f, 0.f));
+        }
+        __syncthreads();  // every count read above
+        for (int c = c0 + tid; c < c1; c += kRbThreads) a.count[c] = 0;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_cell_scatter(int n, const int* __restrict__ cell_of, const int* __restrict__ slot,
                                                       const int* __restrict__ cstart, int* __restrict__ tmp,
                                                       int* __restrict__ count)
@@ -1545,7 +1812,14 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     const int nsplit = (MODE == kModeStep && a.split == 1) ? min(ntiles, a.split_cap) : 0;
     const int nunits = heavy ? ctx->nunits : ntiles + nsplit;
     // workgroups with work: the others leave identity partials, which the tail need not read
-    if (blockIdx.x == 0 && threadIdx.x == 0) ctx->nactive = min((int)gridDim.x, max(nunits, 1));
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctx->nactive = min((int)gridDim.x, max(nunits, 1));
+        if (FUSED && a.bucket) {  // for the rebuild kernel (its tail block advances these)
+            ctx->rb_grid = ctx->grid_next;
+            ctx->rb_step = ctx->step;
+            ctx->rb_parity = ctx->parity;
+        }
+    }
     int first_tile = -1, ntot = 0;
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
         int tile, part, nparts;
@@ -1710,9 +1984,16 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                         int base = 0;
                         if (head) base = atomicAdd(&a.count[c], run);
                         base = __shfl(base, h);
-                        if (valid) {
+                        const int sl = base + (lane - h);
+                        if (a.bucket) {  // rebuild step: file the particle under its cell
+                            if (valid && sl < kBucketCap) a.bucket[c * kBucketCap + sl] = i;
+                            if (valid && sl >= kBucketCap) {
+                                a.cell_of[i] = c;
+                                a.ovf[atomicAdd(&a.ovf_n[ctx->step & 1], 1)] = i;
+                            }
+                        } else if (valid) {
                             a.cell_of[i] = c;
-                            a.slot[i] = base + (lane - h);
+                            a.slot[i] = sl;
                         }
                     }
                     const float big = 3.0e38f;
@@ -2064,6 +2345,17 @@ void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, con
                        int* slot, int* count)
 {
     hipLaunchKernelGGL(k_cell_count, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, n, cell_of, slot, count);
+}
+
+int rebuild_sync_words(int ncell_max) { return 2 + 2 * (ncell_max / (kRbCells / 2) + 2); }
+
+void launch_rebuild(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int* tmp, unsigned long long* scan_sync,
+                    int fblocks, int apply_sched)
+{
+    // block 0: the tail; then enough rebuild blocks for any grid of <= ncell_max cells
+    const int blocks = 1 + a.ncell_max / (kRbCells / 2) + 2;
+    hipLaunchKernelGGL(k_rebuild, dim3(blocks), dim3(kRbThreads), 0, s, ctx, a, tmp, scan_sync, fblocks,
+                       apply_sched);
 }
 
 int scan_sync_words(int ncell_max) { return 2 + 2 * (ncell_max / (kMbCells / 2) + 2); }

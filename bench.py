@@ -155,7 +155,7 @@ def main():
     ap.add_argument("--prio", type=int, default=700, help="n > 0: wave priority min(3, tile candidates / n)")
     ap.add_argument("--subtiles", type=int, default=2, help="pair-loop stencils per 64-particle tile: 1, 2, 4")
     ap.add_argument("--scan-mb", type=int, default=1, help="1: multi-block look-back cell scan, 0: one workgroup")
-    ap.add_argument("--fused", type=int, default=1, help="1: 4-launch step (force kernel bins the new positions)")
+    ap.add_argument("--fused", type=int, default=2, help="2: 2-launch rebuild step, 1: 4-launch step, 0: unfused")
     ap.add_argument("--profile-steps", type=int, default=50)
     ap.add_argument("--replicas-per-gpu", type=int, default=4,
                     help="independent trajectories per GPU, each its own engine + stream (1 = single trajectory)")

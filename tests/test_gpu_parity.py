@@ -161,7 +161,7 @@ def test_waves_per_tile_equivalent(c1_design, interphase_cfg, waves, order):
     assert te == pytest.approx(to, rel=1e-5)
 
 
-@pytest.mark.parametrize("fused", [0, 1])
+@pytest.mark.parametrize("fused", [0, 1, 2])
 @pytest.mark.parametrize("mode", [1, 2])
 def test_split_tiles_agree(c2_design, interphase_cfg, fused, mode):
     """Splitting tiles' candidates over two workgroups (mode 1: every tile; mode 2: the heavy tiles the cell scan
@@ -198,6 +198,32 @@ def test_scan_blocks_agree(c2_design, interphase_cfg, fused):
     assert np.array_equal(out[0], out[1])
 
 
+@pytest.mark.parametrize("squeeze", [1.0, 0.08])
+def test_step_shapes_bitwise_equal(c2_design, interphase_cfg, squeeze):
+    """The 4-launch fused step and the 2-launch rebuild step (cell list rebuilt from the force kernel's per-cell
+    buckets) build identical cell lists (cells ordered by particle index), so C2 trajectories are bitwise
+    equal; the unfused step bins with its own grid (fp32 sums in another order): within tolerance.  squeeze < 1
+    packs the beads into a small ball: cells far over the bucket capacity (overflow list) and blocks over the
+    LDS staging capacity (global staging path)."""
+    x0 = c2_design.positions
+    x0 = x0.mean(0) + squeeze * (x0 - x0.mean(0))
+    out = []
+    for fused in (0, 1, 2):
+        e, _ = interphase.build_interphase(Engine, c2_design, interphase_cfg)
+        e.set_positions(x0)
+        e.set_option(A.OPT_FUSED_STEP, fused)
+        e.set_schedule(**interphase.interphase_schedule(interphase_cfg))
+        e.apply_schedule(0)
+        e.run(12, seed=9)
+        e.run(8, first_step=12, seed=9)
+        out.append(e.get_positions())
+        e.close()
+    assert np.all(np.isfinite(out[2]))
+    assert np.array_equal(out[1], out[2])
+    if squeeze == 1.0:
+        assert np.abs(out[0] - out[1]).max() <= 2e-5
+
+
 @pytest.mark.parametrize("mb", [0, 1])
 @pytest.mark.parametrize("shape", ["x_line", "z_line", "slab"])
 def test_neighbor_search_grid_shapes(mb, shape):
@@ -218,7 +244,7 @@ def test_neighbor_search_grid_shapes(mb, shape):
     assert got.shape == exp.shape and np.array_equal(got, exp)
 
 
-@pytest.mark.parametrize("fused", [0, 1])
+@pytest.mark.parametrize("fused", [0, 1, 2])
 def test_chunked_runs_equal_one_run(c1_design, interphase_cfg, fused):
     """The Philox counter is the absolute step: 3 chunks == 1 run, bit for bit (both step shapes; the fused
     step carries its cell list across runs that continue at the next step)."""
