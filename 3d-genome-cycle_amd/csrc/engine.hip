@@ -102,8 +102,10 @@ struct gcs_engine {
     unsigned long long* scan_sync = nullptr;  // multi-block cell scan: epoch word + look-back granules
     int resident = 0;         // force-step workgroups resident at once (split budget)
     int* tcnt = nullptr;     // split-tile arrival counters
-    int* bucket = nullptr;   // rebuild step: [ncell_max][kBucketCap] particles filed per cell by the force kernel
-    int* ovf = nullptr;      // rebuild step: bucket overflow list [n]
+    float4* bucket_p = nullptr;  // rebuild step: [ncell_max][kBucketCap] sorted records filed by the force kernel
+    int2* bucket_q = nullptr;
+    float4* ovf_p = nullptr;     // rebuild step: bucket overflow list [n]
+    int4* ovf_q = nullptr;
     int* ovf_n = nullptr;    // rebuild step: its two counters (step parity)
     unsigned long long* rb_sync = nullptr;  // rebuild step: epoch word + look-back granules
     // topology tables
@@ -410,8 +412,10 @@ void fill_state_args(gcs_engine* e)
     a.pbuf = e->pbuf;
     a.units = e->units;
     a.tcnt = e->tcnt;
-    a.bucket = e->fused == 2 ? e->bucket : nullptr;
-    a.ovf = e->ovf;
+    a.bucket_p = e->fused == 2 ? e->bucket_p : nullptr;
+    a.bucket_q = e->bucket_q;
+    a.ovf_p = e->ovf_p;
+    a.ovf_q = e->ovf_q;
     a.ovf_n = e->ovf_n;
     a.split_cap = std::max(force_grid(e->n), kMaxUnits);
 }
@@ -630,7 +634,9 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
         (rc = dalloc(&e->pbuf, (size_t)2 * std::max(force_grid(n), kMaxUnits) * kTile)) ||
         (rc = dalloc(&e->tcnt, std::max(force_grid(n), kMaxUnits))) || (rc = dalloc(&e->units, 2 * kMaxUnits)) ||
         (rc = dalloc(&e->scan_sync, scan_sync_words(e->ncell_max))) ||
-        (rc = dalloc(&e->bucket, (size_t)e->ncell_max * kBucketCap)) || (rc = dalloc(&e->ovf, n)) ||
+        (rc = dalloc(&e->bucket_p, (size_t)e->ncell_max * kBucketCap)) ||
+        (rc = dalloc(&e->bucket_q, (size_t)e->ncell_max * kBucketCap)) || (rc = dalloc(&e->ovf_p, n)) ||
+        (rc = dalloc(&e->ovf_q, n)) ||
         (rc = dalloc(&e->ovf_n, 2)) || (rc = dalloc(&e->rb_sync, rebuild_sync_words(e->ncell_max))))
         return bail(rc);
     he = hipMemsetAsync(e->count, 0, (e->ncell_max + kScanPad) * sizeof(int), e->stream);
@@ -680,8 +686,10 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->pbuf);
     dfree(e->units);
     dfree(e->scan_sync);
-    dfree(e->bucket);
-    dfree(e->ovf);
+    dfree(e->bucket_p);
+    dfree(e->bucket_q);
+    dfree(e->ovf_p);
+    dfree(e->ovf_q);
     dfree(e->ovf_n);
     dfree(e->rb_sync);
     dfree(e->tcnt);
@@ -1208,7 +1216,7 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     // GCS_DEBUG_TIMES=<file>: per-block timings of the last profiled force launch (see k_force)
     const char* dbg_path = std::getenv("GCS_DEBUG_TIMES");
     unsigned long long* dbg = nullptr;
-    const size_t dbg_n = (size_t)step_grid(e) * 8;
+    const size_t dbg_n = (size_t)step_grid(e) * 8 + 2 * (size_t)rebuild_blocks(e->ncell_max);
     if (dbg_path) HIPCHK(hipMalloc(&dbg, dbg_n * sizeof(unsigned long long)));
     for (auto& x : ev) HIPCHK(hipEventCreate(&x));
     const int fb = step_grid(e);
@@ -1226,8 +1234,8 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
             enqueue_cells(e);
         HIPCHK(hipEventRecord(ev[2 + 5 * k], e->stream));
         if (dbg && k == steps - 1) e->fa.dbg_times = dbg;
+
         launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, fused);
-        e->fa.dbg_times = nullptr;
         HIPCHK(hipEventRecord(ev[3 + 5 * k], e->stream));
         if (rebuild)
             launch_rebuild(e->stream, e->ctx, e->fa, e->tmp, e->rb_sync, fb, e->sched_flags != 0);
@@ -1235,6 +1243,7 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
             enqueue_scan(e, true);
         else
             launch_tail(e->stream, e->ctx, e->fa, fb, fb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
+        e->fa.dbg_times = nullptr;
         HIPCHK(hipEventRecord(ev[4 + 5 * k], e->stream));
         if (fused && !rebuild) launch_scatter_tail(e->stream, e->ctx, e->fa, e->tmp, fb, e->sched_flags != 0, e->ncell_max);
         HIPCHK(hipEventRecord(ev[5 + 5 * k], e->stream));
@@ -1287,6 +1296,17 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
                          "rows %.2f us; k_tail body %.2f us\n", d.grid.n[0], d.grid.n[1], d.grid.n[2], d.grid.ncell,
                          d.ntiles, 1e3 * (d.t_last[2] - d.t_last[1]) / khz, 1e3 * (d.t_last[3] - d.t_last[2]) / khz,
                          1e3 * (d.t_tail[1] - d.t_tail[0]) / khz);
+        if (khz > 0 && rebuild) {
+            auto us = [&](unsigned long long x, unsigned long long y) { return 1e3 * ((double)y - (double)x) / khz; };
+            std::fprintf(stderr, "gcs: rebuild: tail block %.2f us\n", us(d.t_tail[0], d.t_tail[1]));
+            for (int w = 0; w < 2; ++w) {
+                const unsigned long long* pr = w ? d.t_cells : d.t_rows;
+                std::fprintf(stderr, "gcs: rebuild %s block: start %+.2f; published %.2f, staged %.2f, "
+                             "ranked %.2f, looked back %.2f, barrier %.2f, tables %.2f, copies %.2f us\n",
+                             w ? "last" : "middle", us(d.t_tail[0], pr[0]), us(pr[0], pr[1]), us(pr[0], pr[2]),
+                             us(pr[0], pr[4]), us(pr[0], pr[3]), us(pr[0], pr[5]), us(pr[0], pr[6]), us(pr[0], pr[7]));
+            }
+        }
         if (khz > 0)
             std::fprintf(stderr, "gcs: cell probes: start->loaded %.2f, sum %.2f, scan+barrier %.2f, stores %.2f, "
                          "->pass end %.2f us\n", 1e3 * (d.t_cells[0] - d.t_last[0]) / khz,

@@ -59,8 +59,8 @@ struct DevCtx {
     int nactive;           // workgroups of the last force launch that had work (its partial rows)
     int pad3;
     unsigned long long t_tail[2];  // wall clock at the start / end of k_tail
-    unsigned long long t_rows[4];  // wall clock probes inside the cell scan's row pass (GCS_DEBUG)
-    unsigned long long t_cells[4];  // wall clock probes inside the cell scan's cell pass (GCS_DEBUG)
+    unsigned long long t_rows[8];  // wall clock probes inside the cell scan's row pass (GCS_DEBUG)
+    unsigned long long t_cells[8];  // wall clock probes inside the cell scan's cell pass (GCS_DEBUG)
     unsigned long long t_last[4];  // wall clock: fused last-block section start, after tail, after scan, end
     // rebuild step (GCS_OPT_FUSED_STEP 2): what the step's force kernel binned with, stashed by its block 0 so the
     // rebuild kernel reads them while that kernel's tail block advances grid / parity / step
@@ -156,10 +156,13 @@ struct ForceArgs {
     float4* pbuf;   // [2 * split_cap][kTile] partial forces of split units
     int* tcnt;      // [split_cap] arrival counters of split tiles (0 between launches)
     unsigned long long* dbg_times;  // optional (GCS_DEBUG_TIMES): per block {start, end, smid/candidates, tile} then 4 phase stamps
-    // rebuild step: the force kernel files each new position's particle under its cell (bucket[c][slot],
-    // slot < kBucketCap; the rest on the overflow list ovf, counted in ovf_n[step & 1]); nullptr = slot binning
-    int* bucket;
-    int* ovf;
+    // rebuild step: the force kernel files each new position's sorted record under its cell: bucket_p / bucket_q
+    // [c][slot] = {x, y, z, a factor} / {particle, b factor bits} for slot < kBucketCap, the rest on the overflow
+    // list ovf_p / ovf_q ({particle, b bits, cell, 0}) counted in ovf_n[step & 1]; bucket_p == nullptr: slot binning
+    float4* bucket_p;
+    int2* bucket_q;
+    float4* ovf_p;
+    int4* ovf_q;
     int* ovf_n;
 };
 
@@ -197,6 +200,7 @@ int scan_sync_words(int ncell_max);  // u64 words of the multi-block scan's look
 void launch_rebuild(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int* tmp, unsigned long long* scan_sync,
                     int fblocks, int apply_sched);
 int rebuild_sync_words(int ncell_max);
+int rebuild_blocks(int ncell_max);
 int force_step_resident(int waves);
 void launch_scatter_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int* tmp, int fblocks, int apply_sched,
                          int ncell_max);

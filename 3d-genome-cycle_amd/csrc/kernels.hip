@@ -677,6 +677,48 @@ __device__ __forceinline__ int mb_block_scan(int v, int (*wtot)[kMbThreads / 64]
     return woff + incl - v;
 }
 
+// Look-back of the multi-block scans, by one wave: the sums of the {tag, value} granules 2 + 2j (particles) and
+// 3 + 2j (tiles) of blocks j < b into s_off[0..1].  Each lane issues its granules kLbBatch at a time (one memory
+// round trip per batch instead of one per granule) and re-polls only those not yet tagged.
+constexpr int kLbBatch = 8;
+__device__ __forceinline__ void lookback_sum(DevCtx* ctx, const unsigned long long* sync, int b, unsigned tag, int lane,
+                                             long long* s_off)
+{
+    long long p = 0, t = 0;
+    bool stalled = false;
+    for (int base = 0; base < 2 * b; base += 64 * kLbBatch) {
+        unsigned long long x[kLbBatch];
+#pragma unroll
+        for (int k = 0; k < kLbBatch; ++k) {
+            const int j = base + 64 * k + lane;
+            x[k] = (j < 2 * b) ? __hip_atomic_load((gu64*)(sync + 2 + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : ((unsigned long long)tag << 32);
+        }
+#pragma unroll
+        for (int k = 0; k < kLbBatch; ++k) {
+            const int j = base + 64 * k + lane;
+            unsigned spins = 0;
+            while ((unsigned)(x[k] >> 32) != tag && ++spins < kMbSpinCap)
+                x[k] = __hip_atomic_load((gu64*)(sync + 2 + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            stalled |= (unsigned)(x[k] >> 32) != tag;
+            if (j & 1)
+                t += (unsigned)x[k];
+            else
+                p += (unsigned)x[k];
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        p += __shfl_xor(p, o);
+        t += __shfl_xor(t, o);
+    }
+    if (__any(stalled) && lane == 0) atomicAdd(&ctx->scan_stall, 1);
+    if (lane == 0) {
+        s_off[0] = p;
+        s_off[1] = t;
+    }
+}
+
 __global__ __launch_bounds__(kMbThreads) void k_cell_scan_mb(DevCtx* __restrict__ ctx, int n,
                                                               const int* __restrict__ count, int* __restrict__ cstart,
                                                               int* __restrict__ tile_start,
@@ -745,32 +787,7 @@ __global__ __launch_bounds__(kMbThreads) void k_cell_scan_mb(DevCtx* __restrict_
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
     // look-back: one wave sums the granules of blocks 0 .. b-1 (even words particles, odd words tiles)
-    if (wave == 0) {
-        long long p = 0, t = 0;
-        bool stalled = false;
-        for (int j = lane; j < 2 * b; j += 64) {
-            unsigned long long x;
-            unsigned spins = 0;
-            do {
-                x = __hip_atomic_load((gu64*)(sync + 2 + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } while ((unsigned)(x >> 32) != tag && ++spins < kMbSpinCap);
-            stalled |= (unsigned)(x >> 32) != tag;
-            if (j & 1)
-                t += (unsigned)x;
-            else
-                p += (unsigned)x;
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            p += __shfl_xor(p, o);
-            t += __shfl_xor(t, o);
-        }
-        if (__any(stalled) && lane == 0) atomicAdd(&ctx->scan_stall, 1);
-        if (lane == 0) {
-            s_off[0] = p;
-            s_off[1] = t;
-        }
-    }
+    if (wave == 0) lookback_sum(ctx, sync, b, tag, lane, s_off);
     __syncthreads();
     const int poff = (int)s_off[0], toff = (int)s_off[1];
 
@@ -842,35 +859,50 @@ __global__ __launch_bounds__(256) void k_scatter_tail(DevCtx* ctx, ForceArgs a, 
 
 // Rebuild step (GCS_OPT_FUSED_STEP 2): everything between two force kernels in ONE launch.  Block 0 runs the
 // step's tail (tail_body: reductions, schedule, wall, grid <- grid_next).  Blocks 1.. rebuild the cell list the
-// force kernel binned into its buckets, each owning rows of the grid (R = max(1, kRbCells / nx) rows): the
-// count scan, row starts and tiles of k_cell_scan_mb with the same look-back, and the cell-sorted copies
+// force kernel filed into its per-cell buckets, each owning rows of the grid (R = max(1, kRbCells / nx) rows):
+// the count scan, row starts and tiles of k_cell_scan_mb with the same look-back, and the cell-sorted copies
 // (spos / sb / sidx / scell) of its cells, members ordered by particle index inside each cell (as k_cell_sort).
-// Up to kRbPcap particles per block the members are staged and ranked in LDS (the gathers and the look-back
-// overlap); denser blocks, or rows wider than kRbCells, stage them in `tmp` (same result).  The grid, parity and
-// step come from the rb_* copies the force kernel stashed, so block 0 may advance the live ones concurrently.
+// A bucket entry carries the whole sorted record (new position, pair factors, particle), so the copies need no
+// gathers.  Up to kRbPcap particles per block the records are staged and ranked through registers + LDS;
+// denser blocks, or rows wider than kRbCells, stage the entry ids in `tmp` (same result).  The grid, parity
+// and step come from the rb_* copies the force kernel stashed, so block 0 may advance the live ones meanwhile.
 constexpr int kRbThreads = 256;
-constexpr int kRbSeg = 2;
+constexpr int kRbSeg = 1;
 constexpr int kRbCells = kRbThreads * kRbSeg;
 constexpr int kRbPcap = 2048;
-constexpr int kRbUnroll = 4;  // sorted slots per thread in flight in the copy pass
 
-__device__ __forceinline__ void rb_write_sorted(const ForceArgs& a, int d, int i, int c, float4 p, float4 k)
+// a member's record: bucket slot j < kBucketCap of cell c, or overflow entry k (src = -(k + 1))
+__device__ __forceinline__ void rb_load(const ForceArgs& a, int c, int j, int src, float4& p, int& i, float& b)
 {
-    const_cast<float4*>(a.spos)[d] = make_float4(p.x, p.y, p.z, a.pair_mix ? k.y : 1.f);
-    const_cast<float*>(a.sb)[d] = a.pair_mix ? k.z : 0.f;
+    if (src >= 0) {
+        const size_t e = (size_t)c * kBucketCap + j;
+        p = a.bucket_p[e];
+        const int2 q = a.bucket_q[e];
+        i = q.x;
+        b = __int_as_float(q.y);
+    } else {
+        p = a.ovf_p[-src - 1];
+        const int4 q = a.ovf_q[-src - 1];
+        i = q.x;
+        b = __int_as_float(q.y);
+    }
+}
+
+__device__ __forceinline__ void rb_store(const ForceArgs& a, int d, int i, int c, float4 p, float b)
+{
+    const_cast<float4*>(a.spos)[d] = p;
+    const_cast<float*>(a.sb)[d] = b;
     const_cast<int*>(a.sidx)[d] = i;
     const_cast<int*>(a.scell)[d] = c;
 }
 
-// members of cell c beyond the bucket: the overflow list entries filed under c (rare; any order: ranked later)
+// overflow entries filed under cell c, in list order: put(q, -(k + 1)) for the q-th one (q from kBucketCap)
 template <typename Put>
 __device__ __forceinline__ void rb_overflow(const ForceArgs& a, int novf, int c, Put put)
 {
     int q = kBucketCap;
-    for (int t = 0; t < novf; ++t) {
-        const int i = a.ovf[t];
-        if (a.cell_of[i] == c) put(q++, i);
-    }
+    for (int k = 0; k < novf; ++k)
+        if (a.ovf_q[k].z == c) put(q++, -(k + 1));
 }
 
 __global__ __launch_bounds__(kRbThreads) void k_rebuild(DevCtx* __restrict__ ctx, ForceArgs a, int* __restrict__ tmp,
@@ -878,6 +910,9 @@ __global__ __launch_bounds__(kRbThreads) void k_rebuild(DevCtx* __restrict__ ctx
                                                         int apply_sched)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // GCS_DEBUG_TIMES: per-block {start, end} after the force kernel's 8 words per force block
+    unsigned long long* const dbg = (a.dbg_times && tid == 0) ? a.dbg_times + 8 * fblocks + 2 * blockIdx.x : nullptr;
+    if (dbg) dbg[0] = wall_clock64();
     if (blockIdx.x == 0) {
         const long long st = ctx->rb_step;
         const unsigned long long t0 = wall_clock64();
@@ -886,6 +921,7 @@ __global__ __launch_bounds__(kRbThreads) void k_rebuild(DevCtx* __restrict__ ctx
             a.ovf_n[(st + 1) & 1] = 0;  // the next force kernel's overflow counter (last read one step ago)
             ctx->t_tail[0] = t0;
             ctx->t_tail[1] = wall_clock64();
+            if (dbg) dbg[1] = ctx->t_tail[1];
         }
         return;
     }
@@ -894,14 +930,23 @@ __global__ __launch_bounds__(kRbThreads) void k_rebuild(DevCtx* __restrict__ ctx
     const int rpb = max(1, kRbCells / nx);
     const int nb = (nrows + rpb - 1) / rpb;
     const int b = blockIdx.x - 1;
-    if (b >= nb) return;
-    const float4* __restrict__ posn = ctx->rb_parity ? a.pos0 : a.pos1;  // the force kernel's new positions
+    if (b >= nb) {
+        if (dbg) dbg[1] = wall_clock64();
+        return;
+    }
+    // GCS_DEBUG probes: the middle block in t_rows, the last in t_cells (start, published, looked back, end)
+    unsigned long long* const probe =
+        (tid == 0 && (b == nb / 2 || b == nb - 1)) ? (b == nb / 2 ? ctx->t_rows : ctx->t_cells) : nullptr;
+    if (probe) probe[0] = wall_clock64();
     const int novf = a.ovf_n[ctx->rb_step & 1];
     __shared__ int wtot[2][kRbThreads / 64];
     __shared__ int s_rowbeg[kRbCells + 1];  // block-local row starts
     __shared__ int s_cst[kRbCells + 1];     // block-local cell starts (single chunk)
-    __shared__ int s_mem[kRbPcap];          // members, cell by cell, unsorted within a cell
-    __shared__ int s_mcell[kRbPcap];        // their block-local cell
+    __shared__ int s_mcell[kRbPcap];        // LDS path: block-local cell of each staged slot
+    __shared__ int s_src[kRbPcap];          // LDS path: overflow source of slots past kBucketCap; then slot order
+    __shared__ float4 s_rp[kRbPcap];        // LDS path: staged records (LDS-DMA): position + a factor
+    __shared__ int s_ri[kRbPcap];           //   particle
+    __shared__ int s_rb[kRbPcap];           //   b factor bits
     __shared__ long long s_off[2];
     const unsigned tag = (unsigned)sync[0] + 1u;
     const int r0 = b * rpb, r1 = min(nrows, r0 + rpb), nr = r1 - r0;
@@ -942,6 +987,27 @@ __global__ __launch_bounds__(kRbThreads) void k_rebuild(DevCtx* __restrict__ ctx
         __hip_atomic_store((gu64*)(sync + 2 + 2 * b), ((unsigned long long)tag << 32) | (unsigned)P,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    const bool lds = one_chunk && P <= kRbPcap;
+    if (lds) {
+        // slot -> cell map (and the overflow sources) by each cell's owner; counts re-zeroed for the next binning
+        const int i0 = c0 + kRbSeg * tid;
+#pragma unroll
+        for (int k = 0; k < kRbSeg; ++k) {
+            const int c = i0 + k;
+            if (c < c1 && v[k] > 0) {
+                a.count[c] = 0;
+                const int ls = loc[k];
+#pragma unroll
+                for (int j = 0; j < kBucketCap; ++j)
+                    if (j < v[k]) s_mcell[ls + j] = c - c0;
+                if (v[k] > kBucketCap)
+                    rb_overflow(a, novf, c, [&](int q, int src) {
+                        s_mcell[ls + q] = c - c0;
+                        s_src[ls + q] = src;
+                    });
+            }
+        }
+    }
     __syncthreads();
 
     // tiles per row and their block-local prefix
@@ -955,59 +1021,57 @@ __global__ __launch_bounds__(kRbThreads) void k_rebuild(DevCtx* __restrict__ ctx
     if (tid == 0)
         __hip_atomic_store((gu64*)(sync + 3 + 2 * b), ((unsigned long long)tag << 32) | (unsigned)ttiles,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (probe) probe[1] = wall_clock64();
 
-    // LDS path: stage the members (bucket loads overlap the look-back); counts re-zeroed for the next binning
-    const bool lds = one_chunk && P <= kRbPcap;
+    // LDS path: every record straight into LDS (LDS-DMA, no VGPR round trip), then each member's rank in its
+    // cell (by particle index) -> the slot order s_src[cell start + rank] = staged slot; all in rolled loops (this
+    // code runs once per step per CU: its instruction fetch is part of the critical path)
     if (lds) {
-        const int i0 = c0 + kRbSeg * tid;
-#pragma unroll
-        for (int k = 0; k < kRbSeg; ++k) {
-            const int c = i0 + k;
-            if (c < c1 && v[k] > 0) {
-                a.count[c] = 0;
-                const int ls = loc[k], m = min(v[k], kBucketCap);
-                for (int j = 0; j < m; ++j) {
-                    s_mem[ls + j] = a.bucket[c * kBucketCap + j];
-                    s_mcell[ls + j] = c - c0;
+        typedef __attribute__((address_space(1))) void gvoid;
+        typedef __attribute__((address_space(3))) void lvoid;
+        for (int s0 = wave * 64; s0 < P; s0 += kRbThreads) {
+            const int s = s0 + lane;
+            if (s < P) {
+                const int lc = s_mcell[s], j = s - s_cst[lc];
+                const float4* gp;
+                const int* gq;
+                if (j < kBucketCap) {
+                    const size_t e = (size_t)(c0 + lc) * kBucketCap + j;
+                    gp = a.bucket_p + e;
+                    gq = reinterpret_cast<const int*>(a.bucket_q + e);
+                } else {
+                    const int k = -s_src[s] - 1;
+                    gp = a.ovf_p + k;
+                    gq = reinterpret_cast<const int*>(a.ovf_q + k);
                 }
-                if (v[k] > kBucketCap)
-                    rb_overflow(a, novf, c, [&](int q, int i) {
-                        s_mem[ls + q] = i;
-                        s_mcell[ls + q] = c - c0;
-                    });
+                __builtin_amdgcn_global_load_lds((gvoid*)gp, (lvoid*)(s_rp + s0), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((gvoid*)gq, (lvoid*)(s_ri + s0), 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((gvoid*)(gq + 1), (lvoid*)(s_rb + s0), 4, 0, 0);
             }
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (probe) probe[2] = wall_clock64();
+        for (int s = tid; s < P; s += kRbThreads) {
+            const int i = s_ri[s], lc = s_mcell[s];
+            const int ls = s_cst[lc], le = s_cst[lc + 1];
+            int r = 0;
+            for (int t = ls; t < le; t += 4) {  // 4 independent LDS reads per round (clamped, masked)
+                const int x0 = s_ri[t], x1 = s_ri[min(t + 1, le - 1)], x2 = s_ri[min(t + 2, le - 1)],
+                          x3 = s_ri[min(t + 3, le - 1)];
+                r += (x0 < i) + ((t + 1 < le) & (x1 < i)) + ((t + 2 < le) & (x2 < i)) + ((t + 3 < le) & (x3 < i));
+            }
+            s_src[ls + r] = s;
+        }
+        if (probe) probe[4] = wall_clock64();
     }
 
     // look-back: one wave sums the granules of blocks 0 .. b-1 (even words particles, odd words tiles)
-    if (wave == 0) {
-        long long p = 0, t = 0;
-        bool stalled = false;
-        for (int j = lane; j < 2 * b; j += 64) {
-            unsigned long long x;
-            unsigned spins = 0;
-            do {
-                x = __hip_atomic_load((gu64*)(sync + 2 + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } while ((unsigned)(x >> 32) != tag && ++spins < kMbSpinCap);
-            stalled |= (unsigned)(x >> 32) != tag;
-            if (j & 1)
-                t += (unsigned)x;
-            else
-                p += (unsigned)x;
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            p += __shfl_xor(p, o);
-            t += __shfl_xor(t, o);
-        }
-        if (__any(stalled) && lane == 0) atomicAdd(&ctx->scan_stall, 1);
-        if (lane == 0) {
-            s_off[0] = p;
-            s_off[1] = t;
-        }
-    }
+    if (wave == 0) lookback_sum(ctx, sync, b, tag, lane, s_off);
+    if (probe) probe[3] = wall_clock64();
     __syncthreads();
     const int poff = (int)s_off[0], toff = (int)s_off[1];
+    if (probe) probe[5] = wall_clock64();
 
     // cstart, tile_start, tile table
     if (one_chunk) {
@@ -1052,39 +1116,23 @@ __global__ __launch_bounds__(kRbThreads) void k_rebuild(DevCtx* __restrict__ ctx
         __hip_atomic_store((gu64*)sync, (unsigned long long)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
-    // cell-sorted copies: sorted slot poff + s holds the member of rank r in its cell (by particle index)
+    if (probe) probe[6] = wall_clock64();
+    // cell-sorted copies: the member of rank r (by particle index) in its cell goes to slot cell start + r
     if (lds) {
-        for (int s0 = 0; s0 < P; s0 += kRbUnroll * kRbThreads) {
-            int d[kRbUnroll], ii[kRbUnroll], cc[kRbUnroll];
-            float4 p[kRbUnroll], k4[kRbUnroll];
-#pragma unroll
-            for (int u = 0; u < kRbUnroll; ++u) {
-                const int s = s0 + u * kRbThreads + tid;
-                d[u] = -1;
-                if (s < P) {
-                    const int m = s_mem[s], lc = s_mcell[s];
-                    const int ls = s_cst[lc], le = s_cst[lc + 1];
-                    int r = 0;
-                    for (int t = ls; t < le; ++t) r += (s_mem[t] < m) ? 1 : 0;
-                    d[u] = poff + ls + r;
-                    ii[u] = m;
-                    cc[u] = c0 + lc;
-                    p[u] = posn[m];
-                    k4[u] = a.kmu ? a.kmu[m] : make_float4(1.f, 1.f, 0.f, 0.f);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kRbUnroll; ++u)
-                if (d[u] >= 0) rb_write_sorted(a, d[u], ii[u], cc[u], p[u], k4[u]);
+        // coalesced: sorted slot poff + t takes the staged record s_src[t]
+        for (int t = tid; t < P; t += kRbThreads) {
+            const int src = s_src[t];
+            rb_store(a, poff + t, s_ri[src], c0 + s_mcell[src], s_rp[src], __int_as_float(s_rb[src]));
         }
     } else {
+        // global staging: tmp[slot] = the record's source (bucket entry j of its cell, or -(overflow index + 1))
         __syncthreads();  // this block's cstart entries are visible to all its threads
         const int pend = poff + P;
         for (int c = c0 + tid; c < c1; c += kRbThreads) {
             const int cs = a.cstart_w[c], ce = (c + 1 < c1) ? a.cstart_w[c + 1] : pend;
             const int m = min(ce - cs, kBucketCap);
-            for (int j = 0; j < m; ++j) tmp[cs + j] = a.bucket[c * kBucketCap + j];
-            if (ce - cs > kBucketCap) rb_overflow(a, novf, c, [&](int q, int i) { tmp[cs + q] = i; });
+            for (int j = 0; j < m; ++j) tmp[cs + j] = j;
+            if (ce - cs > kBucketCap) rb_overflow(a, novf, c, [&](int q, int src) { tmp[cs + q] = src; });
         }
         __syncthreads();
         for (int s = poff + tid; s < pend; s += kRbThreads) {
@@ -1097,14 +1145,25 @@ __global__ __launch_bounds__(kRbThreads) void k_rebuild(DevCtx* __restrict__ ctx
                     hi = mid;
             }
             const int cs = a.cstart_w[lo], ce = (lo + 1 < c1) ? a.cstart_w[lo + 1] : pend;
-            const int m = tmp[s];
+            float4 p;
+            float bf;
+            int i;
+            rb_load(a, lo, s - cs, tmp[s], p, i, bf);
             int r = 0;
-            for (int t = cs; t < ce; ++t) r += (tmp[t] < m) ? 1 : 0;
-            rb_write_sorted(a, cs + r, m, lo, posn[m], a.kmu ? a.kmu[m] : make_float4(1.f, 1.f, 0.f, 0.f));
+            for (int t = cs; t < ce; ++t) {
+                float4 pt;
+                float bt;
+                int it2;
+                rb_load(a, lo, t - cs, tmp[t], pt, it2, bt);
+                r += (it2 < i) ? 1 : 0;
+            }
+            rb_store(a, cs + r, i, lo, p, bf);
         }
         __syncthreads();  // every count read above
         for (int c = c0 + tid; c < c1; c += kRbThreads) a.count[c] = 0;
     }
+    if (probe) probe[7] = wall_clock64();
+    if (dbg) dbg[1] = wall_clock64();
 }
 
 __global__ __launch_bounds__(256) void k_cell_scatter(int n, const int* __restrict__ cell_of, const int* __restrict__ slot,
@@ -1814,7 +1873,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
     // workgroups with work: the others leave identity partials, which the tail need not read
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         ctx->nactive = min((int)gridDim.x, max(nunits, 1));
-        if (FUSED && a.bucket) {  // for the rebuild kernel (its tail block advances these)
+        if (FUSED && a.bucket_p) {  // for the rebuild kernel (its tail block advances these)
             ctx->rb_grid = ctx->grid_next;
             ctx->rb_step = ctx->step;
             ctx->rb_parity = ctx->parity;
@@ -1985,11 +2044,17 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5)))
                         if (head) base = atomicAdd(&a.count[c], run);
                         base = __shfl(base, h);
                         const int sl = base + (lane - h);
-                        if (a.bucket) {  // rebuild step: file the particle under its cell
-                            if (valid && sl < kBucketCap) a.bucket[c * kBucketCap + sl] = i;
+                        if (a.bucket_p) {  // rebuild step: file the particle's sorted record under its cell
+                            const float4 rec = make_float4(nxp, nyp, nzp, pi.w);
+                            if (valid && sl < kBucketCap) {
+                                const size_t e = (size_t)c * kBucketCap + sl;
+                                a.bucket_p[e] = rec;
+                                a.bucket_q[e] = make_int2(i, __float_as_int(bi));
+                            }
                             if (valid && sl >= kBucketCap) {
-                                a.cell_of[i] = c;
-                                a.ovf[atomicAdd(&a.ovf_n[ctx->step & 1], 1)] = i;
+                                const int k = atomicAdd(&a.ovf_n[ctx->step & 1], 1);
+                                a.ovf_p[k] = rec;
+                                a.ovf_q[k] = make_int4(i, __float_as_int(bi), c, 0);
                             }
                         } else if (valid) {
                             a.cell_of[i] = c;
@@ -2347,13 +2412,15 @@ void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, con
     hipLaunchKernelGGL(k_cell_count, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, n, cell_of, slot, count);
 }
 
+int rebuild_blocks(int ncell_max) { return 1 + ncell_max / (kRbCells / 2) + 2; }
+
 int rebuild_sync_words(int ncell_max) { return 2 + 2 * (ncell_max / (kRbCells / 2) + 2); }
 
 void launch_rebuild(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int* tmp, unsigned long long* scan_sync,
                     int fblocks, int apply_sched)
 {
     // block 0: the tail; then enough rebuild blocks for any grid of <= ncell_max cells
-    const int blocks = 1 + a.ncell_max / (kRbCells / 2) + 2;
+    const int blocks = rebuild_blocks(a.ncell_max);
     hipLaunchKernelGGL(k_rebuild, dim3(blocks), dim3(kRbThreads), 0, s, ctx, a, tmp, scan_sync, fblocks,
                        apply_sched);
 }
