@@ -32,7 +32,9 @@ import numpy as np  # noqa: E402
 
 from gcs import _abi as A  # noqa: E402
 
-A.load()  # bind the engine's HIP runtime before torch loads its own copy
+CPU_WORKER = "--cpu-worker" in sys.argv  # a CPU-baseline child process (no device use)
+if not CPU_WORKER:
+    A.load()  # bind the engine's HIP runtime before torch loads its own copy
 
 from gcs import interphase, synthetic  # noqa: E402
 from gcs.config import InterphaseConfig  # noqa: E402
@@ -111,8 +113,9 @@ def make_engine(design, cfg, device, start_step, state=None):
     return e
 
 
-def cpu_baseline(design, cfg, start_step, budget_s, state):
-    """The oracle (fp64, 1 thread, reference flags) on a bounded sample of the same workload (same state)."""
+def cpu_rate(design, cfg, start_step, budget_s, state):
+    """The oracle (fp64, 1 thread, reference flags) on a bounded sample of the same workload (same state):
+    one step to size the sample, then as many steps as fit `budget_s`.  Returns (bead-updates/s, steps, s)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg only
     o, _ = interphase.build_interphase(oracle.OracleSystem, design, cfg)
@@ -122,13 +125,62 @@ def cpu_baseline(design, cfg, start_step, budget_s, state):
     t0 = time.perf_counter()
     o.run(1, first_step=start_step, seed=1)
     one = time.perf_counter() - t0
-    steps = max(1, min(200, int(budget_s / max(one, 1e-6))))
+    steps = max(1, min(20000, int(budget_s / max(one, 1e-6))))
     t0 = time.perf_counter()
     o.run(steps, first_step=start_step + 1, seed=1)
     el = time.perf_counter() - t0
-    return {"value": design.n * steps / el, "unit": "bead-updates/s", "cores": 1, "kind": "port",
-            "sample": f"C2 {design.n} particles from the bench state, {steps} steps from step {start_step + 1} "
-                      f"({el:.1f} s, oracle/libgcs_oracle.so fp64 single thread, -O2 -funsafe-math-optimizations)"}
+    return design.n * steps / el, steps, el
+
+
+def cpu_worker(budget_s):
+    """Child-process entry (`bench.py --cpu-worker S`): one single-threaded oracle trajectory; prints its rate."""
+    r, steps, el = cpu_rate(synthetic.make_c2(master_seed=1), InterphaseConfig(), WINDOW_START, budget_s, load_state())
+    print(json.dumps({"value": r, "steps": steps, "seconds": el}), flush=True)
+
+
+def cpu_baseline(budget_s, procs):
+    """cpu_baseline of the bench line.  value: ONE oracle process on one core (the reference is single-threaded);
+    `replicas_value`: `procs` independent single-threaded trajectories side by side, aggregate.
+    Both legs run as child processes that never touch the device."""
+    import subprocess
+
+    def launch(k):
+        env = dict(os.environ, OMP_NUM_THREADS="1")
+        return [subprocess.Popen([sys.executable, str(ROOT / "bench.py"), "--cpu-worker", str(budget_s)],
+                                 stdout=subprocess.PIPE, text=True, env=env) for _ in range(k)]
+
+    def collect(ps):
+        out = []
+        for p in ps:
+            so, _ = p.communicate()
+            if p.returncode != 0:
+                raise RuntimeError(f"cpu baseline worker failed (rc {p.returncode})")
+            out.append(json.loads(so.strip().splitlines()[-1]))
+        return out
+
+    one = collect(launch(1))[0]
+    res = {"value": one["value"], "unit": "bead-updates/s", "cores": 1, "kind": "port",
+           "sample": f"C2 60662 particles from the bench state, {one['steps']} steps from step {WINDOW_START + 1} "
+                     f"({one['seconds']:.1f} s, oracle/libgcs_oracle.so fp64 single thread, "
+                     f"-O2 -funsafe-math-optimizations)",
+           "cpu_model": _cpu_model()}
+    if procs > 1:
+        many = collect(launch(procs))
+        res["replicas_value"] = sum(m["value"] for m in many)
+        res["replicas_cores"] = procs
+        res["replicas_sample"] = (f"{procs} independent single-threaded oracle trajectories run side by side, "
+                                  f"{min(m['steps'] for m in many)}-{max(m['steps'] for m in many)} steps each")
+    return res
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def read_traffic():
@@ -159,9 +211,15 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=50)
     ap.add_argument("--replicas-per-gpu", type=int, default=4,
                     help="independent trajectories per GPU, each its own engine + stream (1 = single trajectory)")
-    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline work (0 = skip)")
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work (0 = skip)")
+    ap.add_argument("--cpu-procs", type=int, default=16,
+                    help="independent single-threaded CPU trajectories for the multi-core leg (the box's CPU share)")
+    ap.add_argument("--cpu-worker", type=float, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--no-start-window", action="store_true", help="skip the secondary step-0 window")
     args = ap.parse_args()
+    if args.cpu_worker is not None:
+        cpu_worker(args.cpu_worker)
+        return
 
     world, rank, local, dist = dist_setup()
     cfg = InterphaseConfig()
@@ -260,7 +318,7 @@ def main():
 
     cpu = None
     if world == 1 and args.cpu_budget > 0 and state is not None:
-        cpu = cpu_baseline(design, cfg, WINDOW_START, args.cpu_budget, state)
+        cpu = cpu_baseline(args.cpu_budget, args.cpu_procs)
 
     value = whole_job_value(n * R, args.steps, world, el_max)
     line = {
