@@ -1,0 +1,158 @@
+// contacts.hip -- off-step-loop device work of the interphase driver surface (gfx950):
+//   * the contact map (stage_interphase/contact_map.cpp:33-85): every contactmap_update_interval steps every pair
+//     i < j closer than the contact distance is counted into an open-addressing hash table in HBM (64-bit key
+//     i << 32 | j, 32-bit count); at the output window the occupied slots are compacted and radix-sorted by (i, j)
+//     on the device (contact_map.cpp:66-85 sorts the same keys on the host)
+//   * the sampled-position quantisation of simulation_store.cpp:22-33 / 192-216 (16 fraction bits, stored as f32)
+// The pair predicate is the strict fp32 one of the neighbour search (kernels.hip k_search): bit-exact against the
+// oracle's gcso_search_neighbors.
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include "engine_internal.hpp"
+
+namespace gcs {
+namespace {
+
+__device__ __forceinline__ bool contact_pair(float4 p, float4 q, float d2)
+{
+    const float dx = __fsub_rn(p.x, q.x), dy = __fsub_rn(p.y, q.y), dz = __fsub_rn(p.z, q.z);
+    const float r2 = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
+    return r2 < d2;
+}
+
+// Fibonacci hashing of the pair key onto 2^bits slots
+__device__ __forceinline__ unsigned long long contact_slot(unsigned long long key, int bits)
+{
+    return (key * 0x9E3779B97F4A7C15ull) >> (64 - bits);
+}
+
+// One thread per cell-sorted particle (the search cell list of the current positions, grid edge >= distance):
+// walk the 3x3 neighbouring rows' x-range, count every pair i < j inside the distance into the table.  A failed
+// insert (probe sequence exhausted: table too full) raises table->overflow; counts stay exact for inserted keys.
+__global__ __launch_bounds__(256) void k_contact_insert(const DevCtx* __restrict__ ctx, int n,
+                                                        const float4* __restrict__ spos, const int* __restrict__ sidx,
+                                                        const int* __restrict__ scell, const int* __restrict__ cstart,
+                                                        unsigned long long* __restrict__ keys,
+                                                        unsigned* __restrict__ counts, int bits,
+                                                        int* __restrict__ overflow)
+{
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const Grid g = ctx->grid;
+    const float d2 = __fmul_rn(g.rc, g.rc);
+    const int i = sidx[s];
+    const float4 p = spos[s];
+    const int c = scell[s];
+    const int nx = g.n[0], ny = g.n[1], nz = g.n[2];
+    const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
+    const unsigned long long mask = (1ull << bits) - 1ull;
+    for (int z = max(cz - 1, 0); z <= min(cz + 1, nz - 1); ++z)
+        for (int y = max(cy - 1, 0); y <= min(cy + 1, ny - 1); ++y) {
+            const int base = (z * ny + y) * nx;
+            const int jb = cstart[base + max(cx - g.fx, 0)], je = cstart[base + min(cx + g.fx, nx - 1) + 1];
+            for (int t = jb; t < je; ++t) {
+                const int j = sidx[t];
+                if (j <= i || !contact_pair(p, spos[t], d2)) continue;
+                const unsigned long long key = ((unsigned long long)(unsigned)i << 32) | (unsigned)j;
+                unsigned long long h = contact_slot(key, bits);
+                bool done = false;
+                for (int probe = 0; probe < kContactMaxProbe; ++probe) {
+                    const unsigned long long prev = atomicCAS(&keys[h], kContactEmpty, key);
+                    if (prev == kContactEmpty || prev == key) {
+                        atomicAdd(&counts[h], 1u);
+                        done = true;
+                        break;
+                    }
+                    h = (h + 1) & mask;
+                }
+                if (!done) atomicOr(overflow, 1);
+            }
+        }
+}
+
+// occupied slots -> (key, count) lists; output order is arbitrary (the sort that follows fixes it)
+__global__ __launch_bounds__(256) void k_contact_compact(const unsigned long long* __restrict__ keys,
+                                                         const unsigned* __restrict__ counts, long long slots,
+                                                         unsigned long long* __restrict__ out_k,
+                                                         unsigned* __restrict__ out_c, int* __restrict__ total)
+{
+    const int lane = threadIdx.x & 63;
+    for (long long h = (long long)blockIdx.x * blockDim.x + threadIdx.x; h < slots;
+         h += (long long)gridDim.x * blockDim.x) {
+        const unsigned long long k = keys[h];
+        const bool occ = k != kContactEmpty;
+        // wave-aggregated append: one atomic per wave
+        const unsigned long long m = __ballot(occ);
+        int base = 0;
+        if (lane == 0 && m) base = atomicAdd(total, __popcll(m));
+        base = __shfl(base, 0);
+        if (occ) {
+            const int o = base + __popcll(m & ((1ull << lane) - 1ull));
+            out_k[o] = k;
+            out_c[o] = counts[h];
+        }
+    }
+}
+
+// simulation_store.cpp:22-33 on an fp32 value: frexp, round the mantissa to `bits` fraction bits (nearbyint,
+// round-half-even), ldexp back.  Every step is exact in fp32, so the result equals the fp64 reference applied to
+// the same (fp32) coordinate.
+__device__ __forceinline__ float quantize_f32(float v, int bits)
+{
+    int ex = 0;
+    const float m = frexpf(v, &ex);
+    const float sm = rintf(ldexpf(m, bits));
+    return ldexpf(sm, ex - bits);
+}
+
+__global__ __launch_bounds__(256) void k_quantize(const float4* __restrict__ pos, float* __restrict__ out, int n,
+                                                  int bits)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 p = pos[i];
+    out[3 * i] = quantize_f32(p.x, bits);
+    out[3 * i + 1] = quantize_f32(p.y, bits);
+    out[3 * i + 2] = quantize_f32(p.z, bits);
+}
+
+}  // namespace
+
+void launch_contact_insert(hipStream_t s, const DevCtx* ctx, int n, const float4* spos, const int* sidx,
+                           const int* scell, const int* cstart, unsigned long long* keys, unsigned* counts, int bits,
+                           int* overflow)
+{
+    hipLaunchKernelGGL(k_contact_insert, dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, spos, sidx, scell, cstart,
+                       keys, counts, bits, overflow);
+}
+
+void launch_contact_compact(hipStream_t s, const unsigned long long* keys, const unsigned* counts, long long slots,
+                            unsigned long long* out_k, unsigned* out_c, int* total)
+{
+    const long long blocks = std::min<long long>((slots + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_contact_compact, dim3((unsigned)blocks), dim3(256), 0, s, keys, counts, slots, out_k, out_c,
+                       total);
+}
+
+size_t sort_pairs_u64_u32_temp_bytes(int n)
+{
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (unsigned long long*)nullptr,
+                                             (unsigned long long*)nullptr, (unsigned*)nullptr, (unsigned*)nullptr, n);
+    return bytes;
+}
+
+void sort_pairs_u64_u32(hipStream_t s, const unsigned long long* k_in, unsigned long long* k_out, const unsigned* v_in,
+                        unsigned* v_out, int n, void* temp, size_t temp_bytes)
+{
+    (void)hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k_in, k_out, v_in, v_out, n, 0, 64, s);
+}
+
+void launch_quantize(hipStream_t s, const float4* pos, float* out, int n, int bits)
+{
+    hipLaunchKernelGGL(k_quantize, dim3((n + 255) / 256), dim3(256), 0, s, pos, out, n, bits);
+}
+
+}  // namespace gcs

@@ -129,11 +129,21 @@ struct gcs_engine {
     int2* s_tile_range = nullptr;
     int s_ncell_max = 0;
     DevCtx* s_ctx = nullptr;
+    DevCtx s_ctx_host{};
     unsigned long long* s_scan_sync = nullptr;
     unsigned long long *s_keys = nullptr, *s_keys2 = nullptr;
     void* s_sort_temp = nullptr;
     size_t s_sort_bytes = 0;
     int64_t s_key_cap = 0;
+    // contact map (stage_interphase/contact_map.cpp): hash table of 2^c_bits slots + compaction/sort scratch
+    int c_bits = 0;
+    unsigned long long* c_keys = nullptr;
+    unsigned* c_counts = nullptr;
+    int* c_flags = nullptr;  // [0] overflow, [1] compacted entries
+    int64_t c_updates = 0;   // host mirror: updates since the last clear
+    int c_bits_opt = 0;      // GCS_OPT_CONTACT_BITS (0: sized from N at the first update)
+    // sampled positions (store quantisation)
+    float* q_out = nullptr;
 
     ForceArgs fa{};
     gcs_schedule sched{};
@@ -573,6 +583,74 @@ void end_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_
 // ------------------------------------------------------------------------------------------------------
 // C ABI
 
+namespace {
+
+// search scratch (neighbour search, contact map) for up to n points
+int ensure_search(gcs_engine* e, int64_t n)
+{
+    if (n <= e->search_cap) return GCS_OK;
+    int rc;
+    dfree(e->s_pts);
+    dfree(e->s_spos);
+    dfree(e->s_sb);
+    dfree(e->s_sidx);
+    dfree(e->s_scell);
+    dfree(e->s_cell_of);
+    dfree(e->s_slot);
+    dfree(e->s_tmp);
+    dfree(e->s_count);
+    dfree(e->s_cstart);
+    dfree(e->s_tile);
+    dfree(e->s_tile_range);
+    dfree(e->s_counts);
+    dfree(e->s_offsets);
+    dfree(e->s_total);
+    dfree(e->s_ctx);
+    dfree(e->s_scan_sync);
+    e->search_cap = 0;
+    const int cap = (int)n;
+    const int ncm = std::min(1 << 21, std::max(4096, 4 * cap));
+    if ((rc = dalloc(&e->s_pts, cap)) || (rc = dalloc(&e->s_spos, cap)) || (rc = dalloc(&e->s_sb, cap)) ||
+        (rc = dalloc(&e->s_sidx, cap)) || (rc = dalloc(&e->s_scell, cap)) || (rc = dalloc(&e->s_cell_of, cap)) ||
+        (rc = dalloc(&e->s_slot, cap)) || (rc = dalloc(&e->s_tmp, cap)) || (rc = dalloc(&e->s_count, ncm + kScanPad)) ||
+        (rc = dalloc(&e->s_cstart, ncm + kScanPad)) || (rc = dalloc(&e->s_counts, cap)) ||
+        (rc = dalloc(&e->s_tile, ncm + 2)) || (rc = dalloc(&e->s_tile_range, (size_t)force_blocks(cap) + ncm + 2)) ||
+        (rc = dalloc(&e->s_offsets, cap)) || (rc = dalloc(&e->s_total, 1)) || (rc = dalloc(&e->s_ctx, 1)) ||
+        (rc = dalloc(&e->s_scan_sync, scan_sync_words(ncm))))
+        return rc;
+    HIPCHK(hipMemsetAsync(e->s_count, 0, (ncm + kScanPad) * sizeof(int), e->stream));
+    HIPCHK(hipMemsetAsync(e->s_scan_sync, 0, scan_sync_words(ncm) * sizeof(unsigned long long), e->stream));
+    e->search_cap = cap;
+    e->s_ncell_max = ncm;
+    return GCS_OK;
+}
+
+// the search cell list (grid edge >= distance) of n points at src, on the engine stream, no host sync:
+// s_spos / s_sidx / s_scell / s_cstart and s_ctx->grid
+int enqueue_search_cells(gcs_engine* e, const float4* src, int ni, double distance)
+{
+    // the source outlives the (possibly deferred) async copy: it is a member of the engine
+    e->s_ctx_host = DevCtx{};
+    e->s_ctx_host.cs = 1.0;
+    e->s_ctx_host.bs = 1.0;
+    HIPCHK(hipMemcpyAsync(e->s_ctx, &e->s_ctx_host, sizeof(DevCtx), hipMemcpyHostToDevice, e->stream));
+    ForceArgs sa{};
+    sa.n = ni;
+    sa.pos0 = const_cast<float4*>(src);
+    sa.pos1 = const_cast<float4*>(src);
+    launch_prime(e->stream, e->s_ctx, sa, (float)distance, e->s_ncell_max, nullptr);
+    launch_cell_count(e->stream, e->s_ctx, src, src, ni, e->s_cell_of, e->s_slot, e->s_count);
+    launch_cell_scan(e->stream, e->s_ctx, ni, e->s_count, e->s_cstart, e->s_tile, e->s_tile_range, false, nullptr, 0,
+                     e->scan_mb ? e->s_scan_sync : nullptr, e->s_ncell_max);
+    launch_cell_scatter(e->stream, ni, e->s_cell_of, e->s_slot, e->s_cstart, e->s_tmp, e->s_count);
+    launch_cell_sort(e->stream, e->s_ctx, src, src, nullptr, ni, e->s_tmp, e->s_cell_of, e->s_cstart, e->s_sidx,
+                     e->s_scell, e->s_spos, e->s_sb, 1);
+    HIPCHK(hipGetLastError());
+    return GCS_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 const char* gcs_last_error(void) { return g_last_error.c_str(); }
@@ -703,6 +781,10 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->toff);
     dfree(e->tent);
     dfree(e->noise);
+    dfree(e->c_keys);
+    dfree(e->c_counts);
+    dfree(e->c_flags);
+    dfree(e->q_out);
     dfree(e->s_pts);
     dfree(e->s_spos);
     dfree(e->s_sb);
@@ -1104,40 +1186,7 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
     if (n < 2) return GCS_OK;
     HIPCHK(hipSetDevice(e->device));
     int rc;
-    if (n > e->search_cap) {
-        dfree(e->s_pts);
-        dfree(e->s_spos);
-        dfree(e->s_sb);
-        dfree(e->s_sidx);
-        dfree(e->s_scell);
-        dfree(e->s_cell_of);
-        dfree(e->s_slot);
-        dfree(e->s_tmp);
-        dfree(e->s_count);
-        dfree(e->s_cstart);
-        dfree(e->s_tile);
-        dfree(e->s_tile_range);
-        dfree(e->s_counts);
-        dfree(e->s_offsets);
-        dfree(e->s_total);
-        dfree(e->s_ctx);
-        dfree(e->s_scan_sync);
-        e->search_cap = 0;
-        const int cap = (int)n;
-        const int ncm = std::min(1 << 21, std::max(4096, 4 * cap));
-        if ((rc = dalloc(&e->s_pts, cap)) || (rc = dalloc(&e->s_spos, cap)) || (rc = dalloc(&e->s_sb, cap)) ||
-            (rc = dalloc(&e->s_sidx, cap)) || (rc = dalloc(&e->s_scell, cap)) || (rc = dalloc(&e->s_cell_of, cap)) ||
-            (rc = dalloc(&e->s_slot, cap)) || (rc = dalloc(&e->s_tmp, cap)) || (rc = dalloc(&e->s_count, ncm + kScanPad)) ||
-            (rc = dalloc(&e->s_cstart, ncm + kScanPad)) || (rc = dalloc(&e->s_counts, cap)) ||
-            (rc = dalloc(&e->s_tile, ncm + 2)) || (rc = dalloc(&e->s_tile_range, (size_t)force_blocks(cap) + ncm + 2)) ||
-            (rc = dalloc(&e->s_offsets, cap)) || (rc = dalloc(&e->s_total, 1)) || (rc = dalloc(&e->s_ctx, 1)) ||
-            (rc = dalloc(&e->s_scan_sync, scan_sync_words(ncm))))
-            return rc;
-        HIPCHK(hipMemsetAsync(e->s_count, 0, (ncm + kScanPad) * sizeof(int), e->stream));
-        HIPCHK(hipMemsetAsync(e->s_scan_sync, 0, scan_sync_words(ncm) * sizeof(unsigned long long), e->stream));
-        e->search_cap = cap;
-        e->s_ncell_max = ncm;
-    }
+    if ((rc = ensure_search(e, n))) return rc;
     const int ni = (int)n;
     const float4* src = e->s_pts;
     if (points) {
@@ -1149,21 +1198,7 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
     } else {
         src = e->pos[e->parity];
     }
-    DevCtx c{};
-    c.cs = 1.0;
-    c.bs = 1.0;
-    HIPCHK(hipMemcpyAsync(e->s_ctx, &c, sizeof(c), hipMemcpyHostToDevice, e->stream));
-    ForceArgs sa{};
-    sa.n = ni;
-    sa.pos0 = const_cast<float4*>(src);
-    sa.pos1 = const_cast<float4*>(src);
-    launch_prime(e->stream, e->s_ctx, sa, (float)distance, e->s_ncell_max, nullptr);
-    launch_cell_count(e->stream, e->s_ctx, src, src, ni, e->s_cell_of, e->s_slot, e->s_count);
-    launch_cell_scan(e->stream, e->s_ctx, ni, e->s_count, e->s_cstart, e->s_tile, e->s_tile_range, false, nullptr, 0,
-                     e->scan_mb ? e->s_scan_sync : nullptr, e->s_ncell_max);
-    launch_cell_scatter(e->stream, ni, e->s_cell_of, e->s_slot, e->s_cstart, e->s_tmp, e->s_count);
-    launch_cell_sort(e->stream, e->s_ctx, src, src, nullptr, ni, e->s_tmp, e->s_cell_of, e->s_cstart, e->s_sidx,
-                     e->s_scell, e->s_spos, e->s_sb, 1);
+    if ((rc = enqueue_search_cells(e, src, ni, distance))) return rc;
     launch_search_count(e->stream, e->s_ctx, ni, e->s_spos, e->s_sidx, e->s_scell, e->s_cstart, e->s_counts);
     launch_exclusive_scan_small(e->stream, e->s_counts, e->s_offsets, ni, e->s_total);
     HIPCHK(hipGetLastError());
@@ -1200,6 +1235,137 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
         pairs[2 * k] = (uint32_t)(h[k] >> 32);
         pairs[2 * k + 1] = (uint32_t)h[k];
     }
+    return GCS_OK;
+}
+
+int gcs_engine_contacts_update(gcs_engine* e, double distance)
+{
+    if (!e) return fail(GCS_EINVAL, "null argument");
+    if (!(distance > 0)) return fail(GCS_EINVAL, "contact distance must be positive");
+    if (e->n < 2) return GCS_OK;
+    HIPCHK(hipSetDevice(e->device));
+    int rc;
+    if (!e->c_keys) {
+        int bits = e->c_bits_opt;
+        if (bits <= 0) {  // >= 32 slots per particle (the distinct pairs of a 10-sample window stay well below)
+            bits = 12;
+            while (bits < 34 && ((int64_t)1 << bits) < 128 * (int64_t)e->n) ++bits;
+        }
+        const size_t slots = (size_t)1 << bits;
+        if ((rc = dalloc(&e->c_keys, slots)) || (rc = dalloc(&e->c_counts, slots)) || (rc = dalloc(&e->c_flags, 2)))
+            return rc;
+        e->c_bits = bits;
+        HIPCHK(hipMemsetAsync(e->c_keys, 0xff, slots * sizeof(unsigned long long), e->stream));
+        HIPCHK(hipMemsetAsync(e->c_counts, 0, slots * sizeof(unsigned), e->stream));
+        HIPCHK(hipMemsetAsync(e->c_flags, 0, 2 * sizeof(int), e->stream));
+    }
+    if ((rc = ensure_search(e, e->n))) return rc;
+    if ((rc = enqueue_search_cells(e, e->pos[e->parity], e->n, distance))) return rc;
+    launch_contact_insert(e->stream, e->s_ctx, e->n, e->s_spos, e->s_sidx, e->s_scell, e->s_cstart, e->c_keys,
+                          e->c_counts, e->c_bits, e->c_flags);
+    HIPCHK(hipGetLastError());
+    e->c_updates++;
+    return GCS_OK;
+}
+
+int gcs_engine_contacts_clear(gcs_engine* e)
+{
+    if (!e) return fail(GCS_EINVAL, "null argument");
+    e->c_updates = 0;
+    if (!e->c_keys) return GCS_OK;
+    HIPCHK(hipSetDevice(e->device));
+    const size_t slots = (size_t)1 << e->c_bits;
+    HIPCHK(hipMemsetAsync(e->c_keys, 0xff, slots * sizeof(unsigned long long), e->stream));
+    HIPCHK(hipMemsetAsync(e->c_counts, 0, slots * sizeof(unsigned), e->stream));
+    HIPCHK(hipMemsetAsync(e->c_flags, 0, 2 * sizeof(int), e->stream));
+    return GCS_OK;
+}
+
+int gcs_engine_contacts_read(gcs_engine* e, uint32_t* ijc, int64_t capacity, int64_t* count)
+{
+    if (!e || !count || (capacity > 0 && !ijc)) return fail(GCS_EINVAL, "null argument");
+    *count = 0;
+    if (!e->c_keys) return GCS_OK;
+    HIPCHK(hipSetDevice(e->device));
+    const long long slots = (long long)1 << e->c_bits;
+    int rc;
+    // compact into the search key scratch (grown to the entry count), then radix-sort (key, count) by key
+    HIPCHK(hipMemsetAsync(e->c_flags + 1, 0, sizeof(int), e->stream));
+    int flags[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(flags, e->c_flags, sizeof(flags), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (flags[0]) return fail(GCS_ECAPACITY, "contact map overflowed its hash table: raise GCS_OPT_CONTACT_BITS");
+    // upper bound of the entries: the table size (the compaction writes at most the occupied slots)
+    unsigned long long *ck = nullptr, *ck2 = nullptr;
+    unsigned *cv = nullptr, *cv2 = nullptr;
+    void* temp = nullptr;
+    auto cleanup = [&]() {
+        dfree(ck);
+        dfree(ck2);
+        dfree(cv);
+        dfree(cv2);
+        if (temp) (void)hipFree(temp);
+    };
+    // count first (cheap: a compaction into nothing would need a separate kernel; one pass with full buffers)
+    if ((rc = dalloc(&ck, (size_t)slots)) || (rc = dalloc(&cv, (size_t)slots))) {
+        cleanup();
+        return rc;
+    }
+    launch_contact_compact(e->stream, e->c_keys, e->c_counts, slots, ck, cv, e->c_flags + 1);
+    int total = 0;
+    hipError_t he = hipMemcpyAsync(&total, e->c_flags + 1, sizeof(int), hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    if (he != hipSuccess) {
+        cleanup();
+        return fail(GCS_EHIP, std::string("contacts compact: ") + hipGetErrorString(he));
+    }
+    *count = total;
+    if (total > capacity) {
+        cleanup();
+        return fail(GCS_ECAPACITY, "contact buffer too small; *count holds the required size");
+    }
+    if (total == 0) {
+        cleanup();
+        return GCS_OK;
+    }
+    const size_t bytes = std::max<size_t>(sort_pairs_u64_u32_temp_bytes(total), 16);
+    if ((rc = dalloc(&ck2, (size_t)total)) || (rc = dalloc(&cv2, (size_t)total))) {
+        cleanup();
+        return rc;
+    }
+    he = hipMalloc(&temp, bytes);
+    if (he == hipSuccess) {
+        sort_pairs_u64_u32(e->stream, ck, ck2, cv, cv2, total, temp, bytes);
+        he = hipGetLastError();
+    }
+    std::vector<unsigned long long> hk(total);
+    std::vector<unsigned> hv(total);
+    if (he == hipSuccess)
+        he = hipMemcpyAsync(hk.data(), ck2, total * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipMemcpyAsync(hv.data(), cv2, total * sizeof(unsigned), hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    cleanup();
+    if (he != hipSuccess) return fail(GCS_EHIP, std::string("contacts sort: ") + hipGetErrorString(he));
+    for (int k = 0; k < total; ++k) {
+        ijc[3 * k] = (uint32_t)(hk[k] >> 32);
+        ijc[3 * k + 1] = (uint32_t)hk[k];
+        ijc[3 * k + 2] = hv[k];
+    }
+    return GCS_OK;
+}
+
+int gcs_engine_sample_positions(gcs_engine* e, float* xyz, int64_t n, int32_t fraction_bits)
+{
+    if (!e || !xyz) return fail(GCS_EINVAL, "null argument");
+    if (n != e->n) return fail(GCS_EINVAL, "position count does not match the particle count");
+    if (fraction_bits < 1 || fraction_bits > 23) return fail(GCS_EINVAL, "fraction_bits must be in [1, 23]");
+    HIPCHK(hipSetDevice(e->device));
+    int rc;
+    if (!e->q_out && (rc = dalloc(&e->q_out, 3 * (size_t)e->n))) return rc;
+    launch_quantize(e->stream, e->pos[e->parity], e->q_out, e->n, fraction_bits);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(xyz, e->q_out, 3 * (size_t)n * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
     return GCS_OK;
 }
 
@@ -1326,6 +1492,12 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
 {
     if (!e) return fail(GCS_EINVAL, "null argument");
     e->chain_valid = false;
+    if (option == GCS_OPT_CONTACT_BITS) {
+        if (value != 0 && (value < 10 || value > 34)) return fail(GCS_EINVAL, "contact bits must be 0 or in [10, 34]");
+        if (e->c_keys) return fail(GCS_ESTATE, "the contact map is already allocated");
+        e->c_bits_opt = (int)value;
+        return GCS_OK;
+    }
     if (option == GCS_OPT_GRAPH_STEPS) {
         if (value < 0 || value > 4096) return fail(GCS_EINVAL, "graph steps must be in [0, 4096]");
         e->graph_steps = (int)value;

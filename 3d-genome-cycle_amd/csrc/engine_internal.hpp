@@ -27,6 +27,8 @@ constexpr int kForcePartials = 8;  // per force block: reaction in[3], out[3], m
 constexpr int kBBoxPartials = 6;   // per block: bbox lo[3], hi[3]
 constexpr int kBBoxStride = 8;     // row stride of the bbox partials (rows of 8: one component per lane & 7)
 constexpr int kEnergyKinds = 8;
+constexpr unsigned long long kContactEmpty = ~0ull;  // contact-map hash table: free slot
+constexpr int kContactMaxProbe = 4096;               // linear-probe bound of one insert (then: overflow flag)
 
 struct Grid {
     float lo[3];
@@ -221,6 +223,17 @@ void launch_search_emit(hipStream_t s, const DevCtx* ctx, int n, const float4* s
 void launch_exclusive_scan_small(hipStream_t s, const int* in, int* out, int n, int* total);
 void sort_u64_keys(hipStream_t s, unsigned long long* keys, unsigned long long* tmp, int n, void* temp, size_t temp_bytes);
 size_t sort_u64_temp_bytes(int n);
+
+// contacts.hip: contact map + sampled-position quantisation
+void launch_contact_insert(hipStream_t s, const DevCtx* ctx, int n, const float4* spos, const int* sidx,
+                           const int* scell, const int* cstart, unsigned long long* keys, unsigned* counts, int bits,
+                           int* overflow);
+void launch_contact_compact(hipStream_t s, const unsigned long long* keys, const unsigned* counts, long long slots,
+                            unsigned long long* out_k, unsigned* out_c, int* total);
+size_t sort_pairs_u64_u32_temp_bytes(int n);
+void sort_pairs_u64_u32(hipStream_t s, const unsigned long long* k_in, unsigned long long* k_out, const unsigned* v_in,
+                        unsigned* v_out, int n, void* temp, size_t temp_bytes);
+void launch_quantize(hipStream_t s, const float4* pos, float* out, int n, int bits);
 
 inline int force_blocks(int n) { return (n + kTile - 1) / kTile; }
 // k_force launch size: tiles never cross a cell row, so there are up to (rows) more tiles than force_blocks;

@@ -1832,7 +1832,10 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
 // atomic per run of equal cells), so the next step's cell list needs only scan + scatter + sort (engine.hip
 // enqueue_step).
 template <int MODE, int WAVES, bool FUSED, int NG>
-__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(5))) void k_force(DevCtx* __restrict__ ctx, ForceArgs a)
+#ifndef GCS_FORCE_WAVES_PER_EU
+#define GCS_FORCE_WAVES_PER_EU 5  // occupancy target of the force kernel (VGPR cap 512 / 5 -> 96)
+#endif
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(GCS_FORCE_WAVES_PER_EU))) void k_force(DevCtx* __restrict__ ctx, ForceArgs a)
 {
     __shared__ float red[WAVES > 1 ? WAVES : 1][4][64];
     // per-wave pair-loop staging, sized for the larger of the two layouts: one 64-candidate stream (pair_forces) or

@@ -241,6 +241,37 @@ class Engine:
             A.check(rc)
             return buf[: cnt.value].copy()
 
+    # ---- contact map (stage_interphase/contact_map.cpp:28-85) and sampled positions (simulation_store.cpp:192-216)
+
+    def contacts_update(self, distance):
+        """contact_map::update: count every pair i < j of the current positions closer than `distance` (device)."""
+        A.check(self._lib.gcs_engine_contacts_update(self._h, float(distance)))
+
+    def contacts_accumulate(self):
+        """contact_map::accumulate: (K, 3) uint32 rows (i, j, count) sorted by (i, j)."""
+        cnt = C.c_int64()
+        cap = 0
+        while True:
+            buf = np.empty((max(cap, 1), 3), dtype=np.uint32)
+            rc = self._lib.gcs_engine_contacts_read(self._h, buf.ctypes.data_as(C.POINTER(C.c_uint32)), cap,
+                                                    C.byref(cnt))
+            if rc == A.GCS_ECAPACITY and cnt.value > cap:
+                cap = int(cnt.value)
+                continue
+            A.check(rc)
+            return buf[: cnt.value].copy()
+
+    def contacts_clear(self):
+        """contact_map::clear"""
+        A.check(self._lib.gcs_engine_contacts_clear(self._h))
+
+    def sample_positions(self, fraction_bits=16):
+        """Positions as simulation_store::save_positions stores them: quantised, f32 (N, 3)."""
+        out = np.empty((self.n, 3), dtype=np.float32)
+        A.check(self._lib.gcs_engine_sample_positions(self._h, out.ctypes.data_as(C.POINTER(C.c_float)), self.n,
+                                                      int(fraction_bits)))
+        return out
+
     def profile(self, steps, first_step=0, temperature=1.0, timestep=1e-5, seed=0, noise=A.NOISE_PHILOX) -> dict:
         cfg = make_bd(temperature, timestep, 0.0, seed, noise)
         p = A.Profile()

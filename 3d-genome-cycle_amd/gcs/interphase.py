@@ -146,24 +146,41 @@ class InterphaseDriver:
         return {"time": c["time"], "wall_semiaxes": c["wall_semiaxes"], "core_scale": c["core_scale"],
                 "bond_scale": c["bond_scale"], "mean_energy": self.mean_energy, "wall_energy": 0.0}
 
-    def run_simulation(self, steps=None):
+    def contact_distance(self, step):
+        """The distance contact_map::update uses in callback(step): the one update_core_scale set in callback(step - 1)
+        (simulation_driver_interphase.cpp:38-39, 68-76), i.e. contactmap_distance x core_scale(time (step - 1) dt).
+        callback(0) runs before any update_core_scale: the map's initial distance 0 (contact_map.hpp:65) -> no pairs."""
+        cfg = self.cfg
+        if step <= 0:
+            return 0.0
+        t = (step - 1) * cfg.timestep
+        cs = 1 - (1 - cfg.core_scale_init) * np.exp(-t / cfg.core_scale_tau)
+        return cfg.contactmap_distance * cs
+
+    def run_simulation(self, steps=None, contacts=True):
         """simulation_driver_interphase.cpp:9-64"""
         cfg = self.cfg
         steps = cfg.steps if steps is None else steps
         self.sys.set_schedule(**interphase_schedule(cfg))
+        intervals = [cfg.logging_interval, cfg.sampling_interval]
+        if contacts:
+            intervals.append(cfg.contactmap_update_interval)
+            self.sys.contacts_clear()
+        every = int(np.gcd.reduce(intervals))
+        if hasattr(self.sys, "set_option"):  # replay whole callback intervals from one captured graph
+            self.sys.set_option(A.OPT_GRAPH_STEPS, every)
         # callback(0): time 0, energy, log/sample, then update_core_scale + update_wall_semiaxes
-        self._callback_sim(0)
+        self._callback_sim(0, contacts)
         self.sys.apply_schedule(0)
-        every = int(np.gcd.reduce([cfg.logging_interval, cfg.sampling_interval]))
         done = 0
         while done < steps:
             k = min(every - done % every, steps - done)
             self.sys.run(k, first_step=done, temperature=cfg.temperature, timestep=cfg.timestep,
                          seed=self.interphase_seed)
             done += k
-            self._callback_sim(done)
+            self._callback_sim(done, contacts)
 
-    def _callback_sim(self, step):
+    def _callback_sim(self, step, contacts=True):
         cfg = self.cfg
         log = step % cfg.logging_interval == 0
         sample = step % cfg.sampling_interval == 0
@@ -173,3 +190,13 @@ class InterphaseDriver:
             self._progress("interphase", step)
         if sample and self.store is not None:
             self.store.save_frame("interphase", step, self.sys.get_positions(), self._context_record())
+        if contacts and step % cfg.contactmap_update_interval == 0:
+            d = self.contact_distance(step)
+            if d > 0:  # distance 0 finds no pair (callback(0))
+                self.sys.contacts_update(d)
+        if contacts and sample and (step // cfg.sampling_interval) % cfg.contactmap_output_window == 0:
+            table = self.sys.contacts_accumulate()
+            if self.store is not None:
+                self.store.save_contacts(step, table)
+            self.last_contacts = table
+            self.sys.contacts_clear()

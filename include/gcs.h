@@ -265,16 +265,32 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
 int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps,
                        gcs_profile* out);
 
+/* Contact map (replaces contact_map::update / accumulate / clear, stage_interphase/contact_map.cpp:28-85, driven
+ * from simulation_driver_interphase.cpp:38-45).  update: count every pair i < j of the CURRENT positions closer
+ * than `distance` (strict fp32 predicate, as gcs_engine_search_neighbors) into the engine's device hash map;
+ * enqueued on the engine stream, no host synchronisation (call it between gcs_engine_run chunks).
+ * read: the accumulated (i, j, count) triples sorted by (i, j) into ijc[count][3] (count = distinct pairs;
+ * GCS_ECAPACITY with *count set when capacity is too small, GCS_ECAPACITY without a count when the map
+ * overflowed — raise GCS_OPT_CONTACT_BITS).  clear: empty the map. */
+int gcs_engine_contacts_update(gcs_engine* e, double distance);
+int gcs_engine_contacts_read(gcs_engine* e, uint32_t* ijc, int64_t capacity, int64_t* count);
+int gcs_engine_contacts_clear(gcs_engine* e);
+
+/* Sampled positions as simulation_store::save_positions writes them (common/simulation_store.cpp:22-33,
+ * 192-216): every coordinate quantised to `fraction_bits` mantissa bits (16 in the reference), as f32 [N][3]. */
+int gcs_engine_sample_positions(gcs_engine* e, float* xyz, int64_t n, int32_t fraction_bits);
+
 /* tuning knobs */
 #define GCS_OPT_GRAPH_STEPS 1   /* steps captured per hipGraph replay (0 = eager launches) */
 #define GCS_OPT_WAVES_PER_TILE 2 /* waves sharing one 64-particle tile of the pair loop: 1, 2, 4 or 8 */
 #define GCS_OPT_CHUNK_ORDER 3    /* pair-loop candidate chunks: 0 contiguous, 1 strided across stencil rows (default) */
-#define GCS_OPT_FUSED_STEP 4     /* 1: 4 launches per step: the force kernel bins the new positions (default) */
+#define GCS_OPT_FUSED_STEP 4     /* 2 (default): 2 launches per step (force + rebuild); 1: 4 launches; 0: unfused */
 #define GCS_OPT_SPLIT_TILES 5    /* step launches: 0 (default) off, 1 split every tile over two workgroups, 2 only the
                                     densest tiles, picked by the cell scan within the resident-workgroup budget */
 #define GCS_OPT_SUBTILES 7       /* pair-loop stencils per 64-particle tile: 1, 2 or 4 (default 2) */
 #define GCS_OPT_SCAN_BLOCKS 8    /* cell scan: 1 = multi-block look-back scan (default), 0 = one workgroup */
 #define GCS_OPT_TILE_PRIORITY 6  /* n > 0: pair-loop wave priority min(3, tile candidates / n); 0 = off (default 700) */
+#define GCS_OPT_CONTACT_BITS 9   /* contact map: 2^bits hash slots (0 = default, >= 2 N slots sized at first update) */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
 
 #ifdef __cplusplus

@@ -220,6 +220,27 @@ class OracleSystem:
         return search_neighbors(pts, distance)
 
 
+    # contact map (stage_interphase/contact_map.cpp:33-85): a dict of pair counts on the host
+    def contacts_update(self, distance):
+        if not hasattr(self, "_contacts"):
+            self._contacts = {}
+        for i, j in search_neighbors(self.get_positions(), distance):
+            key = (int(i), int(j))
+            self._contacts[key] = self._contacts.get(key, 0) + 1
+
+    def contacts_accumulate(self):
+        items = sorted(getattr(self, "_contacts", {}).items())
+        return np.array([(i, j, c) for (i, j), c in items], dtype=np.uint32).reshape(-1, 3)
+
+    def contacts_clear(self):
+        self._contacts = {}
+
+    def sample_positions(self, fraction_bits=16):
+        """simulation_store.cpp:192-216: quantise the fp64 positions, store as f32"""
+        x = self.get_positions()
+        return np.vectorize(lambda v: quantize(v, fraction_bits))(x).astype(np.float32)
+
+
 def search_neighbors(points, distance):
     lib = load()
     pts = _f64(points, (-1, 3))

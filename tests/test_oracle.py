@@ -254,3 +254,28 @@ def test_neighbor_search_edge_cases():
     assert got.tolist() == [[0, 1]]  # 0.25 apart is not "closer than 0.25"
     assert np.array_equal(got, _brute_pairs(x, 0.25))
     assert oracle.search_neighbors(x, 0.2500001).tolist() == [[0, 1], [0, 2], [1, 2], [2, 3]]
+
+
+def test_driver_contact_schedule_on_the_oracle(c1_design):
+    """InterphaseDriver's contact-map cadence (simulation_driver_interphase.cpp:38-45, 68-76) on the oracle backend:
+    updates every 20 steps with 0.24 x core_scale of the previous step, none at callback(0), output + clear at
+    the window end."""
+    from gcs import interphase
+    from gcs.config import InterphaseConfig
+    cfg = InterphaseConfig()
+    cfg.logging_interval = 40
+    cfg.sampling_interval = 40
+    cfg.contactmap_output_window = 1
+    o, _ = interphase.build_interphase(oracle.OracleSystem, c1_design, cfg)
+    drv = interphase.InterphaseDriver(o, c1_design, cfg, log=None)
+    assert drv.contact_distance(0) == 0.0
+    assert drv.contact_distance(1) == pytest.approx(0.24 * cfg.core_scale_init)
+    t21 = 20 * cfg.timestep
+    assert drv.contact_distance(21) == pytest.approx(
+        0.24 * (1 - (1 - cfg.core_scale_init) * np.exp(-t21 / cfg.core_scale_tau)))
+    drv.run_simulation(steps=40)
+    t = drv.last_contacts
+    assert t.dtype == np.uint32 and t.shape[1] == 3 and t.shape[0] > 0
+    assert (t[:, 0] < t[:, 1]).all() and 1 <= t[:, 2].max() <= 2  # updates at steps 20 and 40
+    keys = t[:, 0].astype(np.uint64) << np.uint64(32) | t[:, 1].astype(np.uint64)
+    assert (np.diff(keys.astype(np.int64)) > 0).all()
