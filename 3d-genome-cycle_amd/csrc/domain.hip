@@ -1,0 +1,100 @@
+// domain.hip -- the band exchange of the spatial domain decomposition (C5; DESIGN.md "Multi-GPU").
+//
+// Every engine of a decomposed run holds all N particles by global index.  Domain d OWNS the particles whose z
+// lies in its slab [lo_d, hi_d) at the start of a step and integrates only those; its pair/bond terms read the
+// particles within `halo` of the slab (its region E_d = [lo_d - halo, hi_d + halo)), which must therefore be
+// fresh.  After every step each domain sends to every peer p the (index, new position) of each particle it owned
+// whose old OR new position lies in E_p; the receiver writes both position buffers.  So every copy inside E_p is
+// refreshed each step, and a copy that goes stale was last sent from outside E_p (the "old or new" rule sends the
+// exit position), i.e. it is never mistaken for a particle within the cutoff of p's slab.  Bonded partners need
+// the same guarantee: every bond of an owned particle must be shorter than `halo` (checked here each step,
+// flags[0]; LAMMPS's "bond atom missing" condition).  Ownership hand-over needs no message: a particle that
+// crosses from slab d to slab p lands in E_p, is sent, and both sides then compute the same owner from the same
+// bits.
+#include <hip/hip_runtime.h>
+
+#include "engine_internal.hpp"
+
+namespace gcs {
+namespace {
+
+// One thread per particle.  Records are float4 {x, y, z, index bits}, appended per peer with one atomic per wave
+// (order is irrelevant: the unpack is a scatter by index).  flags[0] |= 1: a bond (not the cut-off softwell) of an owned
+// particle reaches beyond the halo; flags[0] |= 2: a peer's band exceeded `cap`.
+__global__ __launch_bounds__(256) void k_domain_pack(const DevCtx* __restrict__ ctx, ForceArgs a,
+                                                     const float2* __restrict__ regions, int npeer,
+                                                     float4* __restrict__ out, int* __restrict__ counts, int cap,
+                                                     int* __restrict__ flags)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    // after the step's tail: pos[parity] holds the new positions, pos[parity ^ 1] the step's start
+    const float4* pnew = ctx->parity ? a.pos1 : a.pos0;
+    const float4* pold = ctx->parity ? a.pos0 : a.pos1;
+    const bool in = i < a.n;
+    const float4 po = in ? pold[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool own = in && po.z >= a.dom_lo && po.z < a.dom_hi;
+    const float4 pn = own ? pnew[i] : po;
+    if (own && a.has_bonds) {
+        const float h2 = a.dom_halo * a.dom_halo;
+        bool far = false;
+        for (int q = a.boff[i]; q < a.boff[i + 1]; ++q) {
+            const int2 en = a.bent[q];
+            if (a.bpar[en.y].type == kSoftwell) continue;  // cut off below the halo (droplet): a pair term
+            const float4 pj = pold[en.x];
+            const float dx = po.x - pj.x, dy = po.y - pj.y, dz = po.z - pj.z;
+            far |= dx * dx + dy * dy + dz * dz >= h2;
+        }
+        if (far) atomicOr(&flags[0], 1);
+    }
+    for (int p = 0; p < npeer; ++p) {
+        const float2 r = regions[p];
+        const bool send = own && ((po.z >= r.x && po.z < r.y) || (pn.z >= r.x && pn.z < r.y));
+        const unsigned long long m = __ballot(send);
+        if (m == 0ull) continue;
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&counts[p], __popcll(m));
+        base = __shfl(base, 0);
+        if (send) {
+            const int o = base + __popcll(m & ((1ull << lane) - 1ull));
+            if (o < cap)
+                out[(size_t)p * cap + o] = make_float4(pn.x, pn.y, pn.z, __int_as_float(i));
+            else
+                atomicOr(&flags[0], 2);
+        }
+    }
+}
+
+// received bands: nbuf buffers of `cap` records, counts[b] valid in buffer b; both position buffers are written
+__global__ __launch_bounds__(256) void k_domain_unpack(ForceArgs a, const float4* __restrict__ in,
+                                                       const int* __restrict__ counts, int nbuf, int cap)
+{
+    for (int b = 0; b < nbuf; ++b) {
+        const int c = min(counts[b], cap);
+        for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < c; k += gridDim.x * blockDim.x) {
+            const float4 r = in[(size_t)b * cap + k];
+            const int i = __float_as_int(r.w);
+            if (i < 0 || i >= a.n) continue;
+            const float4 p = make_float4(r.x, r.y, r.z, 0.f);
+            a.pos0[i] = p;
+            a.pos1[i] = p;
+        }
+    }
+}
+
+}  // namespace
+
+void launch_domain_pack(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const float2* regions, int npeer,
+                        float4* out, int* counts, int cap, int* flags)
+{
+    hipLaunchKernelGGL(k_domain_pack, dim3((a.n + 255) / 256), dim3(256), 0, s, ctx, a, regions, npeer, out, counts,
+                       cap, flags);
+}
+
+void launch_domain_unpack(hipStream_t s, const ForceArgs& a, const float4* in, const int* counts, int nbuf, int cap)
+{
+    const int blocks = std::max(1, std::min(1024, (cap + 255) / 256));
+    hipLaunchKernelGGL(k_domain_unpack, dim3(blocks), dim3(256), 0, s, a, in, counts, nbuf, cap);
+}
+
+}  // namespace gcs

@@ -144,6 +144,13 @@ struct gcs_engine {
     int c_bits_opt = 0;      // GCS_OPT_CONTACT_BITS (0: sized from N at the first update)
     // sampled positions (store quantisation)
     float* q_out = nullptr;
+    // spatial domain decomposition (gcs_engine_set_domain): slab [dom_lo, dom_hi) in z, halo, peer regions
+    bool dom = false;
+    float dom_lo = 0.f, dom_hi = 0.f, dom_halo = 0.f;
+    float2* dom_regions = nullptr;  // device copy of the peers' regions [npeer] {lo - halo, hi + halo}
+    int dom_npeer = 0;
+    bool dom_cont = false;  // the next domain step continues the previous one (no re-priming)
+    int64_t dom_next = 0;
 
     ForceArgs fa{};
     gcs_schedule sched{};
@@ -781,6 +788,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->toff);
     dfree(e->tent);
     dfree(e->noise);
+    dfree(e->dom_regions);
     dfree(e->c_keys);
     dfree(e->c_counts);
     dfree(e->c_flags);
@@ -951,6 +959,7 @@ int gcs_remove_forcefield(gcs_engine* e, int32_t handle)
 
 int gcs_engine_set_positions(gcs_engine* e, const double* xyz, int64_t n)
 {
+    if (e) e->dom_cont = false;  // a decomposed run re-primes after any outside change
     if (!e || !xyz) return fail(GCS_EINVAL, "null argument");
     e->chain_valid = false;
     if (n != e->n) return fail(GCS_EINVAL, "position count does not match the particle count");
@@ -1001,6 +1010,7 @@ int gcs_engine_get_context(gcs_engine* e, gcs_context* c)
 
 int gcs_engine_set_context(gcs_engine* e, const gcs_context* c)
 {
+    if (e) e->dom_cont = false;  // a decomposed run re-primes after any outside change
     if (!e || !c) return fail(GCS_EINVAL, "null argument");
     e->chain_valid = false;
     HIPCHK(hipSetDevice(e->device));
@@ -1024,6 +1034,7 @@ int gcs_engine_set_context(gcs_engine* e, const gcs_context* c)
 
 int gcs_engine_set_schedule(gcs_engine* e, const gcs_schedule* s)
 {
+    if (e) e->dom_cont = false;  // a decomposed run re-primes after any outside change
     if (!e || !s) return fail(GCS_EINVAL, "null argument");
     e->chain_valid = false;
     if ((s->update_scales && (!(s->core_scale_tau > 0) || !(s->bond_scale_tau > 0))))
@@ -1075,6 +1086,7 @@ int gcs_engine_set_noise(gcs_engine* e, const double* normals, int64_t steps)
 
 int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps)
 {
+    if (e) e->dom_cont = false;  // a decomposed run re-primes after any outside change
     if (!e || !cfg) return fail(GCS_EINVAL, "null argument");
     if (steps < 0) return fail(GCS_EINVAL, "negative step count");
     if (!(cfg->timestep > 0)) return fail(GCS_EINVAL, "timestep must be positive");
@@ -1366,6 +1378,121 @@ int gcs_engine_sample_positions(gcs_engine* e, float* xyz, int64_t n, int32_t fr
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(xyz, e->q_out, 3 * (size_t)n * sizeof(float), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
+    return GCS_OK;
+}
+
+// ---- spatial domain decomposition (C5) ----
+
+int gcs_engine_set_domain(gcs_engine* e, double lo, double hi, double halo, const double* peer_regions, int32_t npeer)
+{
+    if (!e) return fail(GCS_EINVAL, "null argument");
+    if (!(halo > 0)) {  // off
+        e->dom = false;
+        e->dom_cont = false;
+        return GCS_OK;
+    }
+    if (!(lo < hi)) return fail(GCS_EINVAL, "domain slab must have lo < hi");
+    if (npeer < 0 || npeer > kMaxPeers || (npeer > 0 && !peer_regions)) return fail(GCS_EINVAL, "bad peer list");
+    HIPCHK(hipSetDevice(e->device));
+    int rc;
+    if (!e->dom_regions && (rc = dalloc(&e->dom_regions, kMaxPeers))) return rc;
+    float2 h[kMaxPeers];
+    for (int p = 0; p < npeer; ++p) h[p] = make_float2((float)peer_regions[2 * p], (float)peer_regions[2 * p + 1]);
+    HIPCHK(hipMemcpyAsync(e->dom_regions, h, sizeof(h), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->dom = true;
+    e->dom_lo = (float)std::max(lo, -3.0e38);
+    e->dom_hi = (float)std::min(hi, 3.0e38);
+    e->dom_halo = (float)halo;
+    e->dom_npeer = npeer;
+    e->dom_cont = false;
+    return GCS_OK;
+}
+
+int gcs_engine_stream(gcs_engine* e, void** stream)
+{
+    if (!e || !stream) return fail(GCS_EINVAL, "null argument");
+    *stream = (void*)e->stream;
+    return GCS_OK;
+}
+
+namespace {
+ForceArgs domain_args(const gcs_engine* e)
+{
+    ForceArgs a = e->fa;
+    a.dom_on = 1;
+    a.dom_lo = e->dom_lo;
+    a.dom_hi = e->dom_hi;
+    a.dom_halo = e->dom_halo;
+    a.bucket_p = nullptr;
+    return a;
+}
+}  // namespace
+
+int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step, double* dev_reaction)
+{
+    if (!e || !cfg || !dev_reaction) return fail(GCS_EINVAL, "null argument");
+    if (!e->dom) return fail(GCS_ESTATE, "gcs_engine_set_domain first");
+    if (cfg->spacestep > 0) return fail(GCS_EINVAL, "decomposed runs use a fixed timestep");
+    if (cfg->noise == GCS_NOISE_INJECTED) return fail(GCS_EINVAL, "decomposed runs draw Philox noise");
+    HIPCHK(hipSetDevice(e->device));
+    if (!(e->dom_cont && e->dom_next == step)) {
+        int rc = begin_run(e, cfg, step);
+        if (rc) return rc;
+        // both position buffers hold the start state: a domain writes only what it owns or receives, so the
+        // buffer the first step writes must already carry every other particle's copy
+        HIPCHK(hipMemcpyAsync(e->pos[e->parity ^ 1], e->pos[e->parity], (size_t)e->n * sizeof(float4),
+                              hipMemcpyDeviceToDevice, e->stream));
+    }
+    e->chain_valid = false;
+    e->dom_next = step + 1;
+    const ForceArgs a = domain_args(e);
+    const int n = e->n;
+    launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count,
+                      e->dom_lo - e->dom_halo, e->dom_hi + e->dom_halo);
+    enqueue_scan(e, false);
+    enqueue_sort(e);
+    launch_force(e->stream, kModeStep, e->waves, e->ctx, a, false);
+    launch_tail_reduce(e->stream, e->ctx, a, step_grid(e), dev_reaction);
+    HIPCHK(hipGetLastError());
+    return GCS_OK;
+}
+
+int gcs_engine_domain_finish(gcs_engine* e, const double* dev_reaction)
+{
+    if (!e || !dev_reaction) return fail(GCS_EINVAL, "null argument");
+    if (!e->dom) return fail(GCS_ESTATE, "gcs_engine_set_domain first");
+    HIPCHK(hipSetDevice(e->device));
+    ForceArgs a = domain_args(e);
+    a.ext_react = dev_reaction;
+    const int sb = step_grid(e);
+    launch_tail(e->stream, e->ctx, a, sb, sb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
+    HIPCHK(hipGetLastError());
+    e->parity ^= 1;
+    e->dom_cont = true;
+    return GCS_OK;
+}
+
+int gcs_engine_domain_pack(gcs_engine* e, float* dev_out, int32_t* dev_counts, int32_t cap, int32_t* dev_flags)
+{
+    if (!e || (e->dom_npeer > 0 && (!dev_out || !dev_counts)) || !dev_flags) return fail(GCS_EINVAL, "null argument");
+    if (!e->dom) return fail(GCS_ESTATE, "gcs_engine_set_domain first");
+    if (cap < 1) return fail(GCS_EINVAL, "band capacity must be positive");
+    HIPCHK(hipSetDevice(e->device));
+    if (e->dom_npeer > 0) HIPCHK(hipMemsetAsync(dev_counts, 0, e->dom_npeer * sizeof(int), e->stream));
+    launch_domain_pack(e->stream, e->ctx, domain_args(e), e->dom_regions, e->dom_npeer, (float4*)dev_out, dev_counts,
+                       cap, dev_flags);
+    HIPCHK(hipGetLastError());
+    return GCS_OK;
+}
+
+int gcs_engine_domain_unpack(gcs_engine* e, const float* dev_in, const int32_t* dev_counts, int32_t nbuf, int32_t cap)
+{
+    if (!e || (nbuf > 0 && (!dev_in || !dev_counts))) return fail(GCS_EINVAL, "null argument");
+    if (nbuf <= 0) return GCS_OK;
+    HIPCHK(hipSetDevice(e->device));
+    launch_domain_unpack(e->stream, e->fa, (const float4*)dev_in, dev_counts, nbuf, cap);
+    HIPCHK(hipGetLastError());
     return GCS_OK;
 }
 

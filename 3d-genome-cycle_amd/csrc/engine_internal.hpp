@@ -166,6 +166,12 @@ struct ForceArgs {
     float4* ovf_p;
     int4* ovf_q;
     int* ovf_n;
+    // spatial domain decomposition (C5; DESIGN.md "Multi-GPU"): every engine holds all N particles by global index;
+    // it integrates only the particles it OWNS (z in [dom_lo, dom_hi) at step start) and bins only those within
+    // dom_halo of its slab (owned + ghosts, refreshed every step by the owners' band exchange).  dom_on == 0: off.
+    int dom_on;
+    float dom_lo, dom_hi, dom_halo;
+    const double* ext_react;  // != nullptr: the step's wall reaction summed over all domains (allreduced), [6]
 };
 
 // ---- Philox4x32-10 + Box-Muller: the production noise stream (identical on host for the oracle) ----
@@ -193,7 +199,7 @@ __host__ __device__ inline void philox4x32_10(unsigned c[4], unsigned k0, unsign
 // launch wrappers (kernels.hip)
 void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed, int ncell_max, const double* sched);
 void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n,
-                       int* cell_of, int* slot, int* count);
+                       int* cell_of, int* slot, int* count, float dom_lo = 0.f, float dom_hi = 0.f);
 void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start, int2* tile_range,
                       bool use_next = false, int4* units = nullptr, int resident = 0,
                       unsigned long long* scan_sync = nullptr, int ncell_max = 0);
@@ -234,6 +240,12 @@ size_t sort_pairs_u64_u32_temp_bytes(int n);
 void sort_pairs_u64_u32(hipStream_t s, const unsigned long long* k_in, unsigned long long* k_out, const unsigned* v_in,
                         unsigned* v_out, int n, void* temp, size_t temp_bytes);
 void launch_quantize(hipStream_t s, const float4* pos, float* out, int n, int bits);
+// domain.hip: spatial decomposition (band pack / unpack) + the local partial reduction of a decomposed step
+constexpr int kMaxPeers = 16;
+void launch_domain_pack(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const float2* regions, int npeer,
+                        float4* out, int* counts, int cap, int* flags);
+void launch_domain_unpack(hipStream_t s, const ForceArgs& a, const float4* in, const int* counts, int nbuf, int cap);
+void launch_tail_reduce(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int fblocks, double* out);
 
 inline int force_blocks(int n) { return (n + kTile - 1) / kTile; }
 // k_force launch size: tiles never cross a cell row, so there are up to (rows) more tiles than force_blocks;

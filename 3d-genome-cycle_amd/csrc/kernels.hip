@@ -279,9 +279,11 @@ __global__ __launch_bounds__(1024) void k_prime(DevCtx* ctx, ForceArgs a, float 
     }
 }
 
+// dom_lo < dom_hi: bin only the particles with z in [dom_lo, dom_hi) (a domain's slab extended by its halo)
 __global__ __launch_bounds__(256) void k_cell_count(const DevCtx* __restrict__ ctx, const float4* __restrict__ p0,
                                                     const float4* __restrict__ p1, int n, int* __restrict__ cell_of,
-                                                    int* __restrict__ slot, int* __restrict__ count)
+                                                    int* __restrict__ slot, int* __restrict__ count, float dom_lo,
+                                                    float dom_hi)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -289,6 +291,10 @@ __global__ __launch_bounds__(256) void k_cell_count(const DevCtx* __restrict__ c
     const Grid g = ctx->grid;
     const float4 p = pos[i];
     const int c = cell_index(g, p.x, p.y, p.z);
+    if (dom_lo < dom_hi && !(p.z >= dom_lo && p.z < dom_hi)) {  // domain: outside slab + halo, not binned
+        cell_of[i] = -1;
+        return;
+    }
     cell_of[i] = c;
     slot[i] = atomicAdd(&count[c], 1);
 }
@@ -611,10 +617,11 @@ __device__ __forceinline__ void scan_cells_body(DevCtx* __restrict__ ctx, int n,
         scan_cell_pass<48, false>(count, cstart, nc, nx, rows_lds, s_rowbeg, cells_lds, s_cst, wtot, carry, it, ctx);
     else
         scan_cell_pass<16, true>(count, cstart, nc, nx, rows_lds, s_rowbeg, cells_lds, s_cst, wtot, carry, it, ctx);
+    // the binned total (= n unless a decomposed domain left particles outside its region unbinned)
     if (tid == 0) {
-        cstart[nc] = n;
-        if (rows_lds) s_rowbeg[nrows] = n;
-        if (cells_lds) s_cst[nc] = n;
+        cstart[nc] = carry;
+        if (rows_lds) s_rowbeg[nrows] = carry;
+        if (cells_lds) s_cst[nc] = carry;
         ctx->t_last[2] = wall_clock64();
     }
     __syncthreads();
@@ -640,7 +647,8 @@ __global__ __launch_bounds__(1024) void k_cell_scan(DevCtx* __restrict__ ctx, in
 }
 
 __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance,
-                                          int apply_sched, int ncell_max, const double* __restrict__ sched, bool fused);
+                                          int apply_sched, int ncell_max, const double* __restrict__ sched, bool fused,
+                                          double* red_out = nullptr);
 
 // Multi-block cell scan (same outputs as k_cell_scan without the heavy-tile unit table).  Block b owns rows
 // [b*R, b*R + R) of the grid, R = max(1, kMbCells / nx): it scans their cells (8 consecutive cells per thread,
@@ -826,7 +834,7 @@ __global__ __launch_bounds__(kMbThreads) void k_cell_scan_mb(DevCtx* __restrict_
     }
     if (b == nb - 1 && tid == 0) {
         const int ntl = toff + ttiles;
-        cstart[nc] = n;
+        cstart[nc] = poff + carry;  // the binned total (see scan_cells_body)
         tile_start[nrows] = ntl;
         ctx->ntiles = ntl;
         ctx->units_ok = 0;
@@ -1173,6 +1181,7 @@ __global__ __launch_bounds__(256) void k_cell_scatter(int n, const int* __restri
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int c = cell_of[i];
+    if (c < 0) return;  // not binned (domain decomposition)
     tmp[cstart[c] + slot[i]] = i;
     count[c] = 0;  // every occupied cell has a particle here: count is all-zero again for the next binning
 }
@@ -1185,7 +1194,7 @@ __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ct
                                                    float* __restrict__ sb, int pair_mix)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n) return;
+    if (s >= n || s >= cstart[ctx->grid.ncell]) return;  // binned particles only (all of them, undecomposed)
     const float4* pos = ctx->parity ? p1 : p0;
     const int i = tmp[s];
     const int c = cell_of[i];
@@ -1825,16 +1834,15 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
 // (k_cell_scan builds the per-row tile prefix).  The WAVES waves split the tile's candidates; wave 0 then
 // adds the particle-local terms and integrates.  Per-block partials (reactions, bbox, drift, neighbours,
 // energies) are reduced in a fixed order by k_tail / the host: no atomics, bitwise reproducible.
-__device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance,
-                                          int apply_sched, int ncell_max, const double* __restrict__ sched, bool fused);
+
 
 // FUSED (kModeStep only): the new positions are also binned into ctx->grid_next (one wave-aggregated count
 // atomic per run of equal cells), so the next step's cell list needs only scan + scatter + sort (engine.hip
 // enqueue_step).
-template <int MODE, int WAVES, bool FUSED, int NG>
 #ifndef GCS_FORCE_WAVES_PER_EU
 #define GCS_FORCE_WAVES_PER_EU 5  // occupancy target of the force kernel (VGPR cap 512 / 5 -> 96)
 #endif
+template <int MODE, int WAVES, bool FUSED, int NG>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(GCS_FORCE_WAVES_PER_EU))) void k_force(DevCtx* __restrict__ ctx, ForceArgs a)
 {
     __shared__ float red[WAVES > 1 ? WAVES : 1][4][64];
@@ -1905,6 +1913,11 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(GCS_
         const int sl = valid ? s : s_end - 1;
         const float4 pi = a.spos[sl];
         const float bi = a.sb[sl];
+        // domain decomposition: this engine integrates the particles of its slab only; tiles of ghosts alone
+        // (the halo's cell rows) are skipped whole (the same ballot in every wave: the waves share the lanes)
+        // (the fused step kernels are never decomposed: compiled out there)
+        const bool own = FUSED || !a.dom_on || (pi.z >= a.dom_lo && pi.z < a.dom_hi);
+        if (!FUSED && a.dom_on && __ballot(valid && own) == 0ull) continue;
 
         float fx = 0.f, fy = 0.f, fz = 0.f, acc = 0.f;  // acc: pair energy (ENERGY) or neighbour count
         // Step launches: the particle-local terms (bonds, bending, tethers, walls, point sources; a chain of
@@ -2005,15 +2018,16 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(GCS_
                 }
             } else {
                 float v[kForcePartials];
-                v[0] = wave_sum(valid ? rin[0] : 0.f);
-                v[1] = wave_sum(valid ? rin[1] : 0.f);
-                v[2] = wave_sum(valid ? rin[2] : 0.f);
-                v[3] = wave_sum(valid ? rout[0] : 0.f);
-                v[4] = wave_sum(valid ? rout[1] : 0.f);
-                v[5] = wave_sum(valid ? rout[2] : 0.f);
-                v[6] = wave_max(valid ? km.x * sqrtf(fx * fx + fy * fy + fz * fz) : 0.f);
+                const bool act = valid && own;  // the particles this engine integrates
+                v[0] = wave_sum(act ? rin[0] : 0.f);
+                v[1] = wave_sum(act ? rin[1] : 0.f);
+                v[2] = wave_sum(act ? rin[2] : 0.f);
+                v[3] = wave_sum(act ? rout[0] : 0.f);
+                v[4] = wave_sum(act ? rout[1] : 0.f);
+                v[5] = wave_sum(act ? rout[2] : 0.f);
+                v[6] = wave_max(act ? km.x * sqrtf(fx * fx + fy * fy + fz * fz) : 0.f);
                 // the pair loop counted the particle itself
-                v[7] = wave_sum(valid ? acc - (a.has_pair ? 1.f : 0.f) : 0.f);
+                v[7] = wave_sum(act ? acc - (a.has_pair ? 1.f : 0.f) : 0.f);
                 if (lane == 0)
                     for (int k = 0; k < kForcePartials; ++k) s_pr[k] = (k == 6) ? fmaxf(s_pr[k], v[k]) : s_pr[k] + v[k];
                 if (MODE == kModeForce) {
@@ -2027,10 +2041,11 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(GCS_
                     noise3(a, ctx, i, n0, n1, n2);
                     const float amp = sqrtf(2.f * a.temperature * mu * dt);
                     const float mdt = mu * dt;
-                    const float nxp = pi.x + mdt * fx + amp * n0;
-                    const float nyp = pi.y + mdt * fy + amp * n1;
-                    const float nzp = pi.z + mdt * fz + amp * n2;
-                    if (valid) posn[i] = make_float4(nxp, nyp, nzp, 0.f);
+                    // ghosts (domain decomposition) keep their position: the owner's exchange refreshes both buffers
+                    const float nxp = own ? pi.x + mdt * fx + amp * n0 : pi.x;
+                    const float nyp = own ? pi.y + mdt * fy + amp * n1 : pi.y;
+                    const float nzp = own ? pi.z + mdt * fz + amp * n2 : pi.z;
+                    if (act) posn[i] = make_float4(nxp, nyp, nzp, 0.f);
                     if (FUSED) {
                         // bin the new position into the next step's grid.  Wave-aggregated: lanes are cell-sorted,
                         // so runs of equal cells are common; one atomic per run returns the run's base slot.
@@ -2167,7 +2182,8 @@ __global__ __launch_bounds__(256) void k_adapt(DevCtx* ctx, ForceArgs a, int blo
 // is a multiple of 64.  fused: the step's force kernel already binned the new positions with grid_next, which
 // becomes the current grid, and the grid for the following step is prepared.
 __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance,
-                                          int apply_sched, int ncell_max, const double* __restrict__ sched, bool fused)
+                                          int apply_sched, int ncell_max, const double* __restrict__ sched, bool fused,
+                                          double* red_out)
 {
     __shared__ double s_red[16][8];
     __shared__ float s_bb[16][8];
@@ -2251,6 +2267,12 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
             for (int k = 0; k < 8; ++k) tot[k] = (k == 6) ? fmax(tot[k], s_red[w][k]) : tot[k] + s_red[w][k];
             for (int k = 0; k < 6; ++k) bb[k] = (k < 3) ? fminf(bb[k], s_bb[w][k]) : fmaxf(bb[k], s_bb[w][k]);
         }
+        if (red_out) {  // the decomposed step's local reduction only (k_tail_reduce): the context is untouched
+            for (int k = 0; k < 8; ++k) red_out[k] = tot[k];
+        } else {
+        // domain decomposition: the wall sees the reaction of every domain (allreduced by the host's collective)
+        if (a.ext_react)
+            for (int k = 0; k < 6; ++k) tot[k] = a.ext_react[k];
         // everything below works on the values thread 0 loaded at entry (sc[], c_*): no dependent global reads
         if (fblocks > 0) {
             for (int k = 0; k < 3; ++k) {
@@ -2315,8 +2337,16 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
         } else {
             ctx->grid = make_grid(bb, bb + 3, pair_cutoff(a, cs), ncell_max, kPairFx);
         }
+        }  // !red_out
     }
     __syncthreads();
+}
+
+// the local part of a decomposed step's tail: the fixed-order partial reduction into out[8] (reaction in/out,
+// max drift, neighbours); the host allreduces out[0..5] and k_tail then runs with ext_react
+__global__ __launch_bounds__(256) void k_tail_reduce(DevCtx* ctx, ForceArgs a, int fblocks, double* out)
+{
+    tail_body(ctx, a, fblocks, fblocks, 0, 0, 0, a.sched, false, out);
 }
 
 __global__ __launch_bounds__(256) void k_tail(DevCtx* ctx, ForceArgs a, int fblocks, int bblocks, int advance,
@@ -2410,9 +2440,15 @@ void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed
 }
 
 void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n, int* cell_of,
-                       int* slot, int* count)
+                       int* slot, int* count, float dom_lo, float dom_hi)
 {
-    hipLaunchKernelGGL(k_cell_count, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, n, cell_of, slot, count);
+    hipLaunchKernelGGL(k_cell_count, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, n, cell_of, slot, count,
+                       dom_lo, dom_hi);
+}
+
+void launch_tail_reduce(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int fblocks, double* out)
+{
+    hipLaunchKernelGGL(k_tail_reduce, dim3(1), dim3(256), 0, s, ctx, a, fblocks, out);
 }
 
 int rebuild_blocks(int ncell_max) { return 1 + ncell_max / (kRbCells / 2) + 2; }

@@ -272,6 +272,33 @@ class Engine:
                                                       int(fraction_bits)))
         return out
 
+    # ---- spatial domain decomposition (gcs.domain drives these; device pointers are plain ints) ----
+
+    def set_domain(self, lo, hi, halo, peer_regions=()):
+        reg = np.ascontiguousarray(np.asarray(peer_regions, dtype=np.float64).reshape(-1, 2))
+        A.check(self._lib.gcs_engine_set_domain(self._h, float(lo), float(hi), float(halo),
+                                                _pd(reg) if reg.size else None, reg.shape[0]))
+
+    def stream_handle(self) -> int:
+        p = C.c_void_p()
+        A.check(self._lib.gcs_engine_stream(self._h, C.byref(p)))
+        return int(p.value or 0)
+
+    def domain_step(self, step, reaction_ptr, temperature=1.0, timestep=1e-5, seed=0):
+        cfg = make_bd(temperature, timestep, 0.0, seed, A.NOISE_PHILOX)
+        A.check(self._lib.gcs_engine_domain_step(self._h, C.byref(cfg), int(step), C.c_void_p(reaction_ptr)))
+
+    def domain_finish(self, reaction_ptr):
+        A.check(self._lib.gcs_engine_domain_finish(self._h, C.c_void_p(reaction_ptr)))
+
+    def domain_pack(self, out_ptr, counts_ptr, cap, flags_ptr):
+        A.check(self._lib.gcs_engine_domain_pack(self._h, C.c_void_p(out_ptr), C.c_void_p(counts_ptr), int(cap),
+                                                 C.c_void_p(flags_ptr)))
+
+    def domain_unpack(self, in_ptr, counts_ptr, nbuf, cap):
+        A.check(self._lib.gcs_engine_domain_unpack(self._h, C.c_void_p(in_ptr), C.c_void_p(counts_ptr), int(nbuf),
+                                                   int(cap)))
+
     def profile(self, steps, first_step=0, temperature=1.0, timestep=1e-5, seed=0, noise=A.NOISE_PHILOX) -> dict:
         cfg = make_bd(temperature, timestep, 0.0, seed, noise)
         p = A.Profile()

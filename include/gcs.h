@@ -280,6 +280,28 @@ int gcs_engine_contacts_clear(gcs_engine* e);
  * 192-216): every coordinate quantised to `fraction_bits` mantissa bits (16 in the reference), as f32 [N][3]. */
 int gcs_engine_sample_positions(gcs_engine* e, float* xyz, int64_t n, int32_t fraction_bits);
 
+/* Spatial domain decomposition (C5: one trajectory over several GPUs; SURVEY.md 8e, DESIGN.md "Multi-GPU").
+ * Every engine holds all N particles by global index and integrates those whose z lies in its slab [lo, hi)
+ * at the start of a step; it bins only the particles within `halo` of the slab.  `peer_regions` [npeer][2] are
+ * the other domains' extended regions [lo_p - halo, hi_p + halo): after each step the band of owned particles
+ * whose old or new z lies in a peer's region is packed for that peer.  halo <= 0 turns decomposition off.
+ * One step = gcs_engine_domain_step (cells, force + update of the owned particles, local reaction into
+ * dev_reaction[8] on the device) -> the caller's allreduce(sum) of dev_reaction[0..5] over all domains ->
+ * gcs_engine_domain_finish(allreduced reaction: wall ODE + schedule) -> gcs_engine_domain_pack (band records
+ * {x, y, z, index bits} into dev_out[npeer][cap][4], counts per peer; dev_flags[0] |= 1 a bond longer than the
+ * halo, |= 2 a band over cap) -> exchange -> gcs_engine_domain_unpack(received buffers).  All calls only
+ * enqueue on the engine stream (gcs_engine_stream), so the caller's collectives can be ordered on it too.
+ * Replaces nothing in the reference (single-threaded); the per-step callback order is kept (wall update after
+ * the force evaluation of the step, simulation_driver_interphase.cpp:51-52, 80-90). */
+int gcs_engine_set_domain(gcs_engine* e, double lo, double hi, double halo, const double* peer_regions,
+                          int32_t npeer);
+int gcs_engine_stream(gcs_engine* e, void** stream);
+int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step, double* dev_reaction);
+int gcs_engine_domain_finish(gcs_engine* e, const double* dev_reaction);
+int gcs_engine_domain_pack(gcs_engine* e, float* dev_out, int32_t* dev_counts, int32_t cap, int32_t* dev_flags);
+int gcs_engine_domain_unpack(gcs_engine* e, const float* dev_in, const int32_t* dev_counts, int32_t nbuf,
+                             int32_t cap);
+
 /* tuning knobs */
 #define GCS_OPT_GRAPH_STEPS 1   /* steps captured per hipGraph replay (0 = eager launches) */
 #define GCS_OPT_WAVES_PER_TILE 2 /* waves sharing one 64-particle tile of the pair loop: 1, 2, 4 or 8 */

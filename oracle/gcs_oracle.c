@@ -51,6 +51,10 @@ struct gcso_system {
     int64_t *cell_start, *cell_items;
     int64_t cell_cap;
     int64_t* cell_of;
+    /* domain decomposition (C5): integrate / count reactions of the particles with z in [dom_lo, dom_hi) only */
+    int dom_on;
+    double dom_lo, dom_hi;
+    unsigned char* dom_own;
 };
 
 /* ------------------------------------------------------------------------------------------------ */
@@ -617,7 +621,7 @@ static void eval_fields(gcso_system* s, int want_force, double* per_kind)
                     for (int k = 0; k < 3; k++) {
                         double fk = c * (-d * nrm[k]); /* along the wall->particle vector (inward) */
                         F[3 * i + k] += fk;
-                        s->ctx.inward_reaction[k] += fabs(fk);
+                        if (!s->dom_own || s->dom_own[i]) s->ctx.inward_reaction[k] += fabs(fk);
                     }
                 }
             }
@@ -635,7 +639,7 @@ static void eval_fields(gcso_system* s, int want_force, double* per_kind)
                     for (int k = 0; k < 3; k++) {
                         double fk = -f->spring * d * nrm[k];
                         F[3 * i + k] += fk;
-                        s->ctx.outward_reaction[k] += fabs(fk);
+                        if (!s->dom_own || s->dom_own[i]) s->ctx.outward_reaction[k] += fabs(fk);
                     }
             }
             break;
@@ -705,6 +709,10 @@ int gcso_run(gcso_system* s, const gcs_bd_config* cfg, int64_t first_step, int64
     int64_t n = s->n;
     double* xi = (double*)malloc((size_t)(3 * n + 3) * sizeof(double));
     for (int64_t st = first_step + 1; st <= first_step + steps; st++) {
+        if (s->dom_on) {
+            if (!s->dom_own) s->dom_own = (unsigned char*)malloc((size_t)n + 1);
+            for (int64_t i = 0; i < n; i++) s->dom_own[i] = s->x[3 * i + 2] >= s->dom_lo && s->x[3 * i + 2] < s->dom_hi;
+        }
         eval_fields(s, 1, NULL);
         double dt = cfg->timestep;
         if (cfg->spacestep > 0) {
@@ -731,6 +739,7 @@ int gcso_run(gcso_system* s, const gcs_bd_config* cfg, int64_t first_step, int64
             memset(xi, 0, (size_t)(3 * n) * sizeof(double));
         }
         for (int64_t i = 0; i < n; i++) {
+            if (s->dom_on && !s->dom_own[i]) continue; /* another domain integrates it */
             double mu = s->mu[i];
             double amp = sqrt(2 * cfg->temperature * mu * dt);
             for (int k = 0; k < 3; k++) s->x[3 * i + k] += mu * dt * s->F[3 * i + k] + amp * xi[3 * i + k];
@@ -738,6 +747,20 @@ int gcso_run(gcso_system* s, const gcs_bd_config* cfg, int64_t first_step, int64
         gcso_apply_schedule(s, st);
     }
     free(xi);
+    if (s->dom_on) { /* the mask is only for the steps' own evaluations */
+        free(s->dom_own);
+        s->dom_own = NULL;
+    }
     return 0;
+}
+
+/* domain decomposition (C5, DESIGN.md "Multi-GPU"): on != 0 -> run() integrates only the particles whose z lies in
+ * [lo, hi) at the start of each step, and the wall reactions count those only (the caller sums them over domains
+ * and applies the wall update itself) */
+void gcso_set_domain(gcso_system* s, int on, double lo, double hi)
+{
+    s->dom_on = on;
+    s->dom_lo = lo;
+    s->dom_hi = hi;
 }
 

@@ -63,6 +63,7 @@ def load():
             "gcso_seed_seq_generate": (None, [C.POINTER(C.c_uint32), C.c_int64, C.POINTER(C.c_uint32), C.c_int64]),
             "gcso_reference_normals": (None, [C.c_uint64, C.c_int64, pd]),
             "gcso_quantize": (C.c_double, [C.c_double, C.c_int]),
+            "gcso_set_domain": (None, [vp, C.c_int, C.c_double, C.c_double]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -219,6 +220,13 @@ class OracleSystem:
         pts = _f64(points if points is not None else self.get_positions(), (-1, 3))
         return search_neighbors(pts, distance)
 
+
+    def set_domain(self, lo=None, hi=None):
+        """Decomposed steps: integrate (and count wall reactions of) the particles with z in [lo, hi) only."""
+        if lo is None:
+            self._lib.gcso_set_domain(self._h, 0, 0.0, 0.0)
+        else:
+            self._lib.gcso_set_domain(self._h, 1, float(lo), float(hi))
 
     # contact map (stage_interphase/contact_map.cpp:33-85): a dict of pair counts on the host
     def contacts_update(self, distance):

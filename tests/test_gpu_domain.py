@@ -1,0 +1,74 @@
+"""GPU: the spatial domain decomposition (C5, gcs/domain.py + csrc/domain.hip) with HIP engines, several domains in
+one process on one device (LocalTransport), against the undecomposed engine and the fp64 oracle.
+
+Tolerances: positions |dx| <= 2e-5 after 30 steps (fp32; the domains' cell lists order the pair sums differently
+from the single engine's), wall semiaxes relative 1e-7; the protocol flags (bond beyond the halo, band over
+capacity) must stay clear."""
+import numpy as np
+import pytest
+
+from gcs import domain, interphase, synthetic
+from gcs.config import InterphaseConfig
+from gcs.engine import Engine
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 30
+SEED = 99
+
+
+def _engine(design, cfg):
+    e, _ = interphase.build_interphase(Engine, design, cfg, device=0)
+    e.set_schedule(**interphase.interphase_schedule(cfg))
+    return e
+
+
+def _decomposed(design, cfg, ndom, steps, cap=None):
+    halo = domain.domain_halo(cfg)
+    slabs = domain.plan_slabs(design.positions[:, 2], ndom)
+    doms = [domain.EngineDomain(_engine(design, cfg), d, slabs, halo, cap=cap, device=0) for d in range(ndom)]
+    run = domain.DecomposedRun(doms, domain.LocalTransport(doms))
+    run.run(steps, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    return run, doms, slabs
+
+
+@pytest.mark.parametrize("ndom", [2, 4])
+def test_decomposed_engines_match_single_engine_c1(c1_design, ndom):
+    cfg = InterphaseConfig()
+    single = _engine(c1_design, cfg)
+    single.run(STEPS, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    x1, c1 = single.get_positions(), single.get_context()
+    run, doms, slabs = _decomposed(c1_design, cfg, ndom, STEPS)
+    run.check()
+    x = domain.gather_positions(run, c1_design.n)
+    assert np.abs(x - x1).max() <= 2e-5
+    for d in doms:
+        c = d.context()
+        assert c["step"] == c1["step"]
+        assert np.allclose(c["wall_semiaxes"], c1["wall_semiaxes"], rtol=1e-7, atol=0)
+    # and against the fp64 oracle's undecomposed run
+    o, _ = interphase.build_interphase(oracle.OracleSystem, c1_design, cfg)
+    o.set_schedule(**interphase.interphase_schedule(cfg))
+    o.run(STEPS, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    assert np.abs(x - o.get_positions()).max() <= 2e-5
+
+
+def test_decomposed_engines_c2_four_domains():
+    cfg = InterphaseConfig()
+    design = synthetic.make_c2()
+    single = _engine(design, cfg)
+    single.run(20, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    x1 = single.get_positions()
+    run, doms, _ = _decomposed(design, cfg, 4, 20)
+    run.check()
+    x = domain.gather_positions(run, design.n)
+    assert np.abs(x - x1).max() <= 2e-5
+
+
+def test_band_capacity_overflow_is_reported(c1_design):
+    cfg = InterphaseConfig()
+    run, _, _ = _decomposed(c1_design, cfg, 2, 2, cap=8)
+    with pytest.raises(domain.DomainError):
+        run.check()
