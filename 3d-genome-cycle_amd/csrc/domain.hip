@@ -24,7 +24,7 @@ namespace {
 __global__ __launch_bounds__(256) void k_domain_pack(const DevCtx* __restrict__ ctx, ForceArgs a,
                                                      const float2* __restrict__ regions, int npeer,
                                                      float4* __restrict__ out, int* __restrict__ counts, int cap,
-                                                     int* __restrict__ flags)
+                                                     int* __restrict__ flags, const int* __restrict__ shared)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
@@ -35,12 +35,13 @@ __global__ __launch_bounds__(256) void k_domain_pack(const DevCtx* __restrict__ 
     const float4 po = in ? pold[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     const bool own = in && po.z >= a.dom_lo && po.z < a.dom_hi;
     const float4 pn = own ? pnew[i] : po;
-    if (own && a.has_bonds) {
+    if (own && a.has_bonds && !(shared && shared[i])) {
         const float h2 = a.dom_halo * a.dom_halo;
         bool far = false;
         for (int q = a.boff[i]; q < a.boff[i + 1]; ++q) {
             const int2 en = a.bent[q];
             if (a.bpar[en.y].type == kSoftwell) continue;  // cut off below the halo (droplet): a pair term
+            if (shared && shared[en.x]) continue;          // shared particles are fresh everywhere
             const float4 pj = pold[en.x];
             const float dx = po.x - pj.x, dy = po.y - pj.y, dz = po.z - pj.z;
             far |= dx * dx + dy * dy + dz * dz >= h2;
@@ -82,13 +83,59 @@ __global__ __launch_bounds__(256) void k_domain_unpack(ForceArgs a, const float4
     }
 }
 
+// Shared particles (the nucleolar beads and their NOR beads: their bonds are far softer than the chain's, so no
+// practical halo covers them): every domain holds them fresh each step.  Before the step's tail the owner writes
+// its shared particles' new positions into the allreduce buffer (the others write 0; one owner per particle, so
+// the sum is exact), after it every domain copies the sums into both position buffers.
+__global__ __launch_bounds__(64) void k_domain_shared_out(const DevCtx* __restrict__ ctx, ForceArgs a,
+                                                          const int* __restrict__ idx, int nshared,
+                                                          double* __restrict__ buf)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nshared) return;
+    const float4* cur = ctx->parity ? a.pos1 : a.pos0;  // before the tail: the step's start
+    const float4* nxt = ctx->parity ? a.pos0 : a.pos1;  // the owners' new positions
+    const int i = idx[k];
+    const float z = cur[i].z;
+    const bool own = z >= a.dom_lo && z < a.dom_hi;
+    const float4 p = nxt[i];
+    buf[kDomainRed + 3 * k] = own ? (double)p.x : 0.0;
+    buf[kDomainRed + 3 * k + 1] = own ? (double)p.y : 0.0;
+    buf[kDomainRed + 3 * k + 2] = own ? (double)p.z : 0.0;
+}
+
+__global__ __launch_bounds__(64) void k_domain_shared_in(ForceArgs a, const int* __restrict__ idx, int nshared,
+                                                         const double* __restrict__ buf)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nshared) return;
+    const int i = idx[k];
+    const float4 p = make_float4((float)buf[kDomainRed + 3 * k], (float)buf[kDomainRed + 3 * k + 1],
+                                 (float)buf[kDomainRed + 3 * k + 2], 0.f);
+    a.pos0[i] = p;
+    a.pos1[i] = p;
+}
+
 }  // namespace
 
 void launch_domain_pack(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const float2* regions, int npeer,
-                        float4* out, int* counts, int cap, int* flags)
+                        float4* out, int* counts, int cap, int* flags, const int* shared)
 {
     hipLaunchKernelGGL(k_domain_pack, dim3((a.n + 255) / 256), dim3(256), 0, s, ctx, a, regions, npeer, out, counts,
-                       cap, flags);
+                       cap, flags, shared);
+}
+
+void launch_domain_shared_out(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const int* idx, int nshared,
+                              double* buf)
+{
+    if (nshared > 0)
+        hipLaunchKernelGGL(k_domain_shared_out, dim3((nshared + 63) / 64), dim3(64), 0, s, ctx, a, idx, nshared, buf);
+}
+
+void launch_domain_shared_in(hipStream_t s, const ForceArgs& a, const int* idx, int nshared, const double* buf)
+{
+    if (nshared > 0)
+        hipLaunchKernelGGL(k_domain_shared_in, dim3((nshared + 63) / 64), dim3(64), 0, s, a, idx, nshared, buf);
 }
 
 void launch_domain_unpack(hipStream_t s, const ForceArgs& a, const float4* in, const int* counts, int nbuf, int cap)

@@ -150,6 +150,9 @@ struct gcs_engine {
     float2* dom_regions = nullptr;  // device copy of the peers' regions [npeer] {lo - halo, hi + halo}
     int dom_npeer = 0;
     bool dom_cont = false;  // the next domain step continues the previous one (no re-priming)
+    int* dom_shared_idx = nullptr;   // shared particles (gcs_engine_set_domain_shared) [nshared]
+    int* dom_shared_flag = nullptr;  // [n] 1 = shared
+    int dom_nshared = 0;
     int64_t dom_next = 0;
 
     ForceArgs fa{};
@@ -789,6 +792,8 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->tent);
     dfree(e->noise);
     dfree(e->dom_regions);
+    dfree(e->dom_shared_idx);
+    dfree(e->dom_shared_flag);
     dfree(e->c_keys);
     dfree(e->c_counts);
     dfree(e->c_flags);
@@ -1409,6 +1414,30 @@ int gcs_engine_set_domain(gcs_engine* e, double lo, double hi, double halo, cons
     return GCS_OK;
 }
 
+int gcs_engine_set_domain_shared(gcs_engine* e, const int64_t* idx, int32_t count)
+{
+    if (!e || (count > 0 && !idx)) return fail(GCS_EINVAL, "null argument");
+    if (count < 0) return fail(GCS_EINVAL, "negative count");
+    HIPCHK(hipSetDevice(e->device));
+    std::vector<int> h(count), flag(e->n, 0);
+    for (int k = 0; k < count; ++k) {
+        if (!valid_index(e, idx[k])) return fail(GCS_EINVAL, "shared particle index out of range");
+        h[k] = (int)idx[k];
+        flag[h[k]] = 1;
+    }
+    dfree(e->dom_shared_idx);
+    dfree(e->dom_shared_flag);
+    e->dom_nshared = 0;
+    int rc;
+    if ((rc = dalloc(&e->dom_shared_idx, std::max(count, 1))) || (rc = dalloc(&e->dom_shared_flag, e->n))) return rc;
+    if (count > 0)
+        HIPCHK(hipMemcpyAsync(e->dom_shared_idx, h.data(), count * sizeof(int), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(e->dom_shared_flag, flag.data(), e->n * sizeof(int), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->dom_nshared = count;
+    return GCS_OK;
+}
+
 int gcs_engine_stream(gcs_engine* e, void** stream)
 {
     if (!e || !stream) return fail(GCS_EINVAL, "null argument");
@@ -1454,6 +1483,7 @@ int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step
     enqueue_sort(e);
     launch_force(e->stream, kModeStep, e->waves, e->ctx, a, false);
     launch_tail_reduce(e->stream, e->ctx, a, step_grid(e), dev_reaction);
+    launch_domain_shared_out(e->stream, e->ctx, a, e->dom_shared_idx, e->dom_nshared, dev_reaction);
     HIPCHK(hipGetLastError());
     return GCS_OK;
 }
@@ -1467,6 +1497,7 @@ int gcs_engine_domain_finish(gcs_engine* e, const double* dev_reaction)
     a.ext_react = dev_reaction;
     const int sb = step_grid(e);
     launch_tail(e->stream, e->ctx, a, sb, sb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
+    launch_domain_shared_in(e->stream, a, e->dom_shared_idx, e->dom_nshared, dev_reaction);
     HIPCHK(hipGetLastError());
     e->parity ^= 1;
     e->dom_cont = true;
@@ -1481,7 +1512,7 @@ int gcs_engine_domain_pack(gcs_engine* e, float* dev_out, int32_t* dev_counts, i
     HIPCHK(hipSetDevice(e->device));
     if (e->dom_npeer > 0) HIPCHK(hipMemsetAsync(dev_counts, 0, e->dom_npeer * sizeof(int), e->stream));
     launch_domain_pack(e->stream, e->ctx, domain_args(e), e->dom_regions, e->dom_npeer, (float4*)dev_out, dev_counts,
-                       cap, dev_flags);
+                       cap, dev_flags, e->dom_shared_flag);
     HIPCHK(hipGetLastError());
     return GCS_OK;
 }

@@ -46,13 +46,26 @@ def plan_slabs(z, ndom: int):
     return [(float(edges[d]), float(edges[d + 1])) for d in range(ndom)]
 
 
-def domain_halo(cfg: InterphaseConfig, margin: float = 0.1) -> float:
-    """Pair cutoff at core_scale 1 (simulation_driver_forcefield.cpp:25-28), droplet cutoff (:175-180), plus a
-    margin for one step's displacement and for bond lengths."""
+BOND_SIGMAS = 7.5  # a chain bond stretched beyond this many thermal widths: ~1e-11 per bond-step
+
+
+def domain_halo(cfg: InterphaseConfig, margin: float = 0.05) -> float:
+    """The reach a domain must see fresh beyond its slab: the pair cutoff at core_scale 1
+    (simulation_driver_forcefield.cpp:25-28) and the chain bonds' reach l + 7.5 sqrt(T / K) at bond_scale 1
+    (:71-83; semispring, INFERRED form), plus a margin for one step's displacement.  The nucleolar bonds and the
+    droplet act among SHARED particles only (shared_particles), which every domain holds fresh."""
     rc = max(cfg.a_core_diameter, cfg.b_core_diameter)
-    if cfg.nucleolus_droplet_energy != 0:
-        rc = max(rc, cfg.nucleolus_droplet_cutoff)
+    for k, l in ((cfg.a_core_bond_spring, cfg.a_core_bond_length), (cfg.b_core_bond_spring, cfg.b_core_bond_length)):
+        if k > 0:
+            rc = max(rc, l + BOND_SIGMAS * float(np.sqrt(cfg.temperature / k)))
     return rc + margin
+
+
+def shared_particles(design):
+    """The nucleolar beads and their NOR beads (simulation_driver_forcefield.cpp:140-186): their bonds
+    (nucleolus_bond_spring 10) and the droplet (cutoff 0.4) reach beyond any practical halo."""
+    b = np.asarray(design.nucleolar_bonds, dtype=np.int64).reshape(-1, 2)
+    return np.unique(b.reshape(-1))
 
 
 def region(slab, halo):
@@ -92,9 +105,10 @@ class _Domain:
 class EngineDomain(_Domain):
     """A gcs.engine.Engine running one domain; exchange buffers are torch tensors on the engine's device."""
 
-    def __init__(self, engine, index, slabs, halo, cap=None, device=None):
+    def __init__(self, engine, index, slabs, halo, cap=None, device=None, shared=()):
         import torch
         super().__init__(index, slabs, halo)
+        self.shared = np.asarray(shared, dtype=np.int64).reshape(-1)
         self.e = engine
         self.torch = torch
         self.device = torch.device("cuda", device if device is not None else torch.cuda.current_device())
@@ -102,8 +116,9 @@ class EngineDomain(_Domain):
         self.cap = int(cap if cap is not None else n)
         npeer = max(1, len(self.peers))
         f64, f32, i32 = torch.float64, torch.float32, torch.int32
-        self.red = torch.zeros(8, dtype=f64, device=self.device)
-        self.glob = torch.zeros(8, dtype=f64, device=self.device)
+        nred = 8 + 3 * self.shared.size  # local reduction + shared particles' positions (csrc/domain.hip)
+        self.red = torch.zeros(nred, dtype=f64, device=self.device)
+        self.glob = torch.zeros(nred, dtype=f64, device=self.device)
         self.out = torch.zeros((npeer, self.cap, 4), dtype=f32, device=self.device)
         self.counts = torch.zeros(npeer, dtype=i32, device=self.device)
         self.inb = torch.zeros_like(self.out)
@@ -111,6 +126,7 @@ class EngineDomain(_Domain):
         self.flags = torch.zeros(1, dtype=i32, device=self.device)
         lo, hi = (_finite(v) for v in self.slab)
         engine.set_domain(lo, hi, halo, self.regions)
+        engine.set_domain_shared(self.shared)
         self._stream = None
 
     def stream(self):
@@ -148,9 +164,10 @@ class EngineDomain(_Domain):
 class OracleDomain(_Domain):
     """TEST INFRASTRUCTURE: the CPU oracle running one domain (oracle.OracleSystem with set_domain), fp64."""
 
-    def __init__(self, osys, index, slabs, halo, schedule: dict):
+    def __init__(self, osys, index, slabs, halo, schedule: dict, shared=()):
         import torch
         super().__init__(index, slabs, halo)
+        self.shared = np.asarray(shared, dtype=np.int64).reshape(-1)
         self.o = osys
         self.torch = torch
         self.sched = dict(schedule)
@@ -160,8 +177,8 @@ class OracleDomain(_Domain):
         n = osys.n
         self.cap = n
         npeer = max(1, len(self.peers))
-        self.red = torch.zeros(8, dtype=torch.float64)
-        self.glob = torch.zeros(8, dtype=torch.float64)
+        self.red = torch.zeros(8 + 3 * self.shared.size, dtype=torch.float64)
+        self.glob = torch.zeros_like(self.red)
         self.out = torch.zeros((npeer, n, 4), dtype=torch.float64)
         self.counts = torch.zeros(npeer, dtype=torch.int32)
         self.inb = torch.zeros_like(self.out)
@@ -175,6 +192,10 @@ class OracleDomain(_Domain):
         c = self.o.get_context()
         self.red[:3] = self.torch.tensor(c["inward_reaction"], dtype=self.torch.float64)
         self.red[3:6] = self.torch.tensor(c["outward_reaction"], dtype=self.torch.float64)
+        if self.shared.size:
+            new = self.o.get_positions()[self.shared]
+            own = self.owned_mask(self._old[self.shared])
+            self.red[8:] = self.torch.from_numpy(np.where(own[:, None], new, 0.0).reshape(-1))
 
     def finish(self):
         # simulation_driver_interphase.cpp:80-90 with the reaction summed over domains
@@ -188,6 +209,10 @@ class OracleDomain(_Domain):
         c["inward_reaction"] = list(self.glob[:3].numpy())
         c["outward_reaction"] = list(self.glob[3:6].numpy())
         self.o.set_context(c)
+        if self.shared.size:
+            x = self.o.get_positions()
+            x[self.shared] = self.glob[8:].numpy().reshape(-1, 3)
+            self.o.set_positions(x)
 
     def pack(self):
         new = self.o.get_positions()

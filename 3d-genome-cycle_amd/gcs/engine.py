@@ -279,6 +279,11 @@ class Engine:
         A.check(self._lib.gcs_engine_set_domain(self._h, float(lo), float(hi), float(halo),
                                                 _pd(reg) if reg.size else None, reg.shape[0]))
 
+    def set_domain_shared(self, idx):
+        a = np.ascontiguousarray(np.asarray(idx, dtype=np.int64).reshape(-1))
+        A.check(self._lib.gcs_engine_set_domain_shared(self._h, a.ctypes.data_as(C.POINTER(C.c_int64)) if a.size
+                                                       else None, a.size))
+
     def stream_handle(self) -> int:
         p = C.c_void_p()
         A.check(self._lib.gcs_engine_stream(self._h, C.byref(p)))

@@ -33,8 +33,14 @@ import numpy as np  # noqa: E402
 from gcs import _abi as A  # noqa: E402
 
 CPU_WORKER = "--cpu-worker" in sys.argv  # a CPU-baseline child process (no device use)
+DECOMP = "--decomp" in sys.argv  # one trajectory split over domains: torch tensors share the engine's runtime
+if DECOMP:
+    # one HIP runtime per process: torch's is initialised first and libgcs.so binds to it (tools/runtime_probe.py)
+    import torch
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    torch.zeros(1, device="cuda")
 if not CPU_WORKER:
-    A.load()  # bind the engine's HIP runtime before torch loads its own copy
+    A.load()  # (replica runs: bind the engine's HIP runtime before torch loads its own copy)
 
 from gcs import interphase, synthetic  # noqa: E402
 from gcs.config import InterphaseConfig  # noqa: E402
@@ -45,15 +51,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md "Chip-level para
 WINDOW_START = 300_000
 
 
-def dist_setup():
+def dist_setup(backend="gloo"):
+    """gloo on CPU tensors for replica runs (barrier + max only: no data-path collective); "nccl" (RCCL) for
+    decomposed runs, whose band exchange and reaction allreduce are the data path."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     dist = None
     if world > 1:
-        import torch.distributed as dist  # gloo on CPU tensors: barrier + max only (no data-path collective)
+        import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group(backend, rank=rank, world_size=world)
     return world, rank, local, dist
 
 
@@ -194,6 +202,73 @@ def read_traffic():
     return None
 
 
+def window_start(name):
+    """C2: the committed step-300,000 trajectory state.  C1/C5: their synthetic start (step 0, core_scale 0.5) --
+    a synthetic chain packed at the generator's density has ~8x the equilibrated neighbour count at core_scale 1."""
+    return WINDOW_START if name == "c2" else 0
+
+
+def bench_config(name):
+    """The interphase defaults; C5's 10 kb beads use the force field rescaled to their size
+    (gcs.config.resolution_scaled, DESIGN.md "Measurement")."""
+    from gcs.config import resolution_scaled
+    cfg = InterphaseConfig()
+    return resolution_scaled(cfg, 10.0) if name == "c5" else cfg
+
+
+def decomp_main(args):
+    """One trajectory split into z-slab domains (gcs.domain; C5 of SURVEY 8e).  value = N x steps / max-over-ranks
+    time of the whole decomposed step loop (force, update, reaction allreduce, band exchange)."""
+    import torch
+    from gcs import domain as D
+    world, rank, local, dist = dist_setup("nccl")
+    cfg = bench_config(args.config)
+    maker = {"c1": synthetic.make_c1, "c2": synthetic.make_c2, "c5": synthetic.make_c5}[args.config]
+    state = load_state() if args.config == "c2" else None
+    design = maker(master_seed=1)
+    ndom = world if world > 1 else args.decomp
+    halo = D.domain_halo(cfg)
+    x0 = state[0] if state is not None else design.positions
+    slabs = D.plan_slabs(x0[:, 2], ndom)
+    mine = [rank] if world > 1 else list(range(ndom))
+    doms = []
+    window = window_start(args.config)
+    for d in mine:
+        e = make_engine(design, cfg, local, window, state)
+        doms.append(D.EngineDomain(e, d, slabs, halo, device=local, shared=D.shared_particles(design)))
+    tr = D.DistTransport(doms[0], dist) if world > 1 else D.LocalTransport(doms)
+    run = D.DecomposedRun(doms, tr)
+    seed = replica_noise_seed(0)
+    run.run(args.warmup, first_step=window, seed=seed)
+    for d in doms:
+        d.synchronize()
+    barrier(dist)
+    t0 = time.perf_counter()
+    run.run(args.steps, first_step=window + args.warmup, seed=seed)
+    for d in doms:
+        d.synchronize()
+    el = time.perf_counter() - t0
+    barrier(dist)
+    el_max = max_over_ranks(dist, el)
+    run.check()
+    n = design.n
+    bands = [int(c) for d in doms for c in d.counts[: len(d.peers)].tolist()]
+    if rank == 0:
+        line = {
+            "metric": "bead-updates/sec (whole node), decomposed single trajectory",
+            "value": n * args.steps / el_max, "unit": "bead-updates/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el_max * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, one trajectory in "
+                                   f"{ndom} z-slab domains ({'RCCL' if world > 1 else 'in-process, one GPU'})",
+                       "particles": n, "domains": ndom, "halo": halo, "parallelism": f"domains{ndom}",
+                       "band_sizes_rank0": bands, "peers_rank0": doms[0].peers},
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -216,13 +291,19 @@ def main():
                     help="independent single-threaded CPU trajectories for the multi-core leg (the box's CPU share)")
     ap.add_argument("--cpu-worker", type=float, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--no-start-window", action="store_true", help="skip the secondary step-0 window")
+    ap.add_argument("--decomp", type=int, default=0,
+                    help="spatial domain decomposition of ONE trajectory: K domains (torchrun: one per rank over "
+                         "RCCL; single process: K domains on this GPU, in-process exchange)")
     args = ap.parse_args()
     if args.cpu_worker is not None:
         cpu_worker(args.cpu_worker)
         return
+    if args.decomp:
+        decomp_main(args)
+        return
 
     world, rank, local, dist = dist_setup()
-    cfg = InterphaseConfig()
+    cfg = bench_config(args.config)
     maker = {"c1": synthetic.make_c1, "c2": synthetic.make_c2, "c5": synthetic.make_c5}[args.config]
     R = max(1, args.replicas_per_gpu)
 
@@ -232,11 +313,12 @@ def main():
     # C2: every replica continues the committed step-300,000 state of the master-seed-1 system with its own noise
     # seed (tools/make_bench_state.py); other configs start from their synthetic state at the window's context
     state = load_state() if args.config == "c2" else None
+    window = window_start(args.config)
     designs, engines, seeds = [], [], []
     for k in range(R):
         rid = rank * R + k
         d = maker(master_seed=1 if state is not None else replica_master_seed(rid))
-        e = make_engine(d, cfg, local, WINDOW_START, state)
+        e = make_engine(d, cfg, local, window, state)
         e.set_option(A.OPT_GRAPH_STEPS, args.graph_steps)
         e.set_option(A.OPT_WAVES_PER_TILE, args.waves)
         e.set_option(A.OPT_CHUNK_ORDER, args.chunk_order)
@@ -252,10 +334,10 @@ def main():
     n = design.n
 
     for e, sd in zip(engines, seeds):
-        e.run(args.warmup, first_step=WINDOW_START, seed=sd)
+        e.run(args.warmup, first_step=window, seed=sd)
     for e in engines:
         e.synchronize()
-    first = WINDOW_START + args.warmup
+    first = window + args.warmup
 
     nxt = [first] * R  # next step of every replica (host-side: no device round trip in the timed loop)
     # one trajectory alone on the GPU first (replica 0; the others are independent, their window starts later)
@@ -317,7 +399,7 @@ def main():
         return
 
     cpu = None
-    if world == 1 and args.cpu_budget > 0 and state is not None:
+    if world == 1 and args.cpu_budget > 0 and state is not None and args.config == "c2":
         cpu = cpu_baseline(args.cpu_budget, args.cpu_procs)
 
     value = whole_job_value(n * R, args.steps, world, el_max)
@@ -335,7 +417,7 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, {R} independent "
-                               f"trajectories per GPU, window from step {WINDOW_START} "
+                               f"trajectories per GPU, window from step {window} "
                                f"(core_scale {ctx['core_scale']:.4f})",
                    "particles": n, "replicas": world * R, "replicas_per_gpu": R,
                    "parallelism": f"replicas{world}x{R}",

@@ -286,7 +286,7 @@ int gcs_engine_sample_positions(gcs_engine* e, float* xyz, int64_t n, int32_t fr
  * the other domains' extended regions [lo_p - halo, hi_p + halo): after each step the band of owned particles
  * whose old or new z lies in a peer's region is packed for that peer.  halo <= 0 turns decomposition off.
  * One step = gcs_engine_domain_step (cells, force + update of the owned particles, local reaction into
- * dev_reaction[8] on the device) -> the caller's allreduce(sum) of dev_reaction[0..5] over all domains ->
+ * dev_reaction[8 + 3 shared] on the device) -> the caller's allreduce(sum) of dev_reaction over all domains ->
  * gcs_engine_domain_finish(allreduced reaction: wall ODE + schedule) -> gcs_engine_domain_pack (band records
  * {x, y, z, index bits} into dev_out[npeer][cap][4], counts per peer; dev_flags[0] |= 1 a bond longer than the
  * halo, |= 2 a band over cap) -> exchange -> gcs_engine_domain_unpack(received buffers).  All calls only
@@ -295,6 +295,10 @@ int gcs_engine_sample_positions(gcs_engine* e, float* xyz, int64_t n, int32_t fr
  * the force evaluation of the step, simulation_driver_interphase.cpp:51-52, 80-90). */
 int gcs_engine_set_domain(gcs_engine* e, double lo, double hi, double halo, const double* peer_regions,
                           int32_t npeer);
+/* Shared particles: fresh on every domain every step (carried in the reaction allreduce, which then holds
+ * 8 + 3 * count doubles).  For particles whose bonds are too soft for any practical halo (nucleolar beads and
+ * their NOR partners; nucleolus_bond_spring 10 vs chain 50-100). */
+int gcs_engine_set_domain_shared(gcs_engine* e, const int64_t* idx, int32_t count);
 int gcs_engine_stream(gcs_engine* e, void** stream);
 int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step, double* dev_reaction);
 int gcs_engine_domain_finish(gcs_engine* e, const double* dev_reaction);

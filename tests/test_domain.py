@@ -36,8 +36,19 @@ def _domains(design, cfg, slabs, halo, only=None):
         if only is not None and d != only:
             continue
         o, _ = interphase.build_interphase(oracle.OracleSystem, design, cfg)
-        doms.append(domain.OracleDomain(o, d, slabs, halo, interphase.interphase_schedule(cfg)))
+        doms.append(domain.OracleDomain(o, d, slabs, halo, interphase.interphase_schedule(cfg),
+                                        shared=domain.shared_particles(design)))
     return doms
+
+
+def test_halo_and_shared_particles(c1_design, interphase_cfg):
+    from gcs.config import resolution_scaled
+    h = domain.domain_halo(interphase_cfg)
+    assert h == pytest.approx(7.5 * (1 / 50) ** 0.5 + 0.05)  # the B-type chain bond's reach dominates
+    h10 = domain.domain_halo(resolution_scaled(interphase_cfg, 10.0))
+    assert h10 == pytest.approx(h * 10 ** (-1 / 3) - 0.05 * 10 ** (-1 / 3) + 0.05)
+    sh = domain.shared_particles(c1_design)
+    assert set(sh.tolist()) == {500, 1000, 1001}
 
 
 def test_plan_slabs_partition_and_peers(c1_design, interphase_cfg):
@@ -59,11 +70,13 @@ def test_plan_slabs_partition_and_peers(c1_design, interphase_cfg):
     assert max(len(domain.peers_of(d, slabs, halo)) for d in range(8)) > 2
 
 
-@pytest.mark.parametrize("ndom", [2, 3, 4])
-def test_decomposed_oracle_matches_single(c1_design, ndom):
+@pytest.mark.parametrize("ndom,halo", [(2, None), (3, None), (4, None), (4, 0.45)])
+def test_decomposed_oracle_matches_single(c1_design, ndom, halo):
+    """halo None: the default (chain-bond reach 1.11); 0.45: thin halo, so the shared nucleolar particles (bonds
+    of rms 0.55) must come through the allreduce, not the bands."""
     cfg = InterphaseConfig()
     x1, c1 = _single(c1_design, cfg)
-    halo = domain.domain_halo(cfg)
+    halo = halo or domain.domain_halo(cfg)
     slabs = domain.plan_slabs(c1_design.positions[:, 2], ndom)
     doms = _domains(c1_design, cfg, slabs, halo)
     run = domain.DecomposedRun(doms, domain.LocalTransport(doms))
@@ -102,7 +115,7 @@ def _rank_main(rank, world, port, out_dir):
     halo = D.domain_halo(cfg)
     slabs = D.plan_slabs(design.positions[:, 2], world)
     o, _ = I.build_interphase(O.OracleSystem, design, cfg)
-    d = D.OracleDomain(o, rank, slabs, halo, I.interphase_schedule(cfg))
+    d = D.OracleDomain(o, rank, slabs, halo, I.interphase_schedule(cfg), shared=D.shared_particles(design))
     run = D.DecomposedRun([d], D.DistTransport(d, dist))
     run.run(STEPS, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     run.check()

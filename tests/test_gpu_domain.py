@@ -25,22 +25,24 @@ def _engine(design, cfg):
     return e
 
 
-def _decomposed(design, cfg, ndom, steps, cap=None):
-    halo = domain.domain_halo(cfg)
+def _decomposed(design, cfg, ndom, steps, cap=None, halo=None):
+    halo = halo or domain.domain_halo(cfg)
     slabs = domain.plan_slabs(design.positions[:, 2], ndom)
-    doms = [domain.EngineDomain(_engine(design, cfg), d, slabs, halo, cap=cap, device=0) for d in range(ndom)]
+    sh = domain.shared_particles(design)
+    doms = [domain.EngineDomain(_engine(design, cfg), d, slabs, halo, cap=cap, device=0, shared=sh)
+            for d in range(ndom)]
     run = domain.DecomposedRun(doms, domain.LocalTransport(doms))
     run.run(steps, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     return run, doms, slabs
 
 
-@pytest.mark.parametrize("ndom", [2, 4])
-def test_decomposed_engines_match_single_engine_c1(c1_design, ndom):
+@pytest.mark.parametrize("ndom,halo", [(2, None), (4, None), (3, 0.45)])
+def test_decomposed_engines_match_single_engine_c1(c1_design, ndom, halo):
     cfg = InterphaseConfig()
     single = _engine(c1_design, cfg)
     single.run(STEPS, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     x1, c1 = single.get_positions(), single.get_context()
-    run, doms, slabs = _decomposed(c1_design, cfg, ndom, STEPS)
+    run, doms, slabs = _decomposed(c1_design, cfg, ndom, STEPS, halo=halo)
     run.check()
     x = domain.gather_positions(run, c1_design.n)
     assert np.abs(x - x1).max() <= 2e-5
@@ -72,3 +74,34 @@ def test_band_capacity_overflow_is_reported(c1_design):
     run, _, _ = _decomposed(c1_design, cfg, 2, 2, cap=8)
     with pytest.raises(domain.DomainError):
         run.check()
+
+
+def test_bond_beyond_halo_is_reported(c1_design):
+    """A halo below the chain bonds' length (C1 starts with every bond 0.1 long): the pack kernel flags it."""
+    cfg = InterphaseConfig()
+    run, _, _ = _decomposed(c1_design, cfg, 2, 2, halo=0.09)
+    with pytest.raises(domain.DomainError, match="bond"):
+        run.check()
+
+
+def test_decomposed_c5_scaled_two_domains():
+    """C5 (606,248 beads, the 10 kb force field of config.resolution_scaled), 2 domains vs one engine, both
+    against the fp64 oracle: from the dense synthetic start, fp32 summation-order differences grow faster than in
+    C1, so the decomposed run must be as close to the oracle as the single engine is (x 2, floor 2e-5)."""
+    from gcs.config import resolution_scaled
+    cfg = resolution_scaled(InterphaseConfig(), 10.0)
+    design = synthetic.make_c5()
+    steps = 10
+    single = _engine(design, cfg)
+    single.run(steps, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    x1 = single.get_positions()
+    run, doms, _ = _decomposed(design, cfg, 2, steps)
+    run.check()
+    x = domain.gather_positions(run, design.n)
+    o, _ = interphase.build_interphase(oracle.OracleSystem, design, cfg)
+    o.set_schedule(**interphase.interphase_schedule(cfg))
+    o.run(steps, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    xo = o.get_positions()
+    e_single = np.abs(x1 - xo).max()
+    e_dec = np.abs(x - xo).max()
+    assert np.isfinite(x).all() and e_dec <= max(2e-5, 2 * e_single), (e_dec, e_single)
