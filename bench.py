@@ -376,6 +376,17 @@ def main():
     achieved = n * BYTES_PER_UPDATE / (force_ms * 1e-3) / 1e9
     ctx = eng.get_context()
     finite = all(bool(np.isfinite(e.get_positions()).all()) for e in engines)
+    # secondary (off the step metric): one contact-map update (contact_map.cpp:33-63) on this state,
+    # every 20 steps in production
+    eng.contacts_update(cfg.contactmap_distance * ctx["core_scale"])
+    eng.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(20):
+        eng.contacts_update(cfg.contactmap_distance * ctx["core_scale"])
+    eng.synchronize()
+    contacts_ms = (time.perf_counter() - t1) * 1e3 / 20
+    contacts_distinct = int(eng.contacts_accumulate().shape[0])
+    eng.contacts_clear()
 
     # secondary: the production start window (step 0, core_scale 0.5, ~7x fewer neighbours), one replica
     start_rate = None
@@ -423,7 +434,8 @@ def main():
                    "parallelism": f"replicas{world}x{R}",
                    "single_trajectory_value": single_rate if R > 1 else value,
                    "mean_neighbors": prof["mean_neighbors"], "graph_steps": args.graph_steps,
-                   "waves_per_tile": args.waves, "chunk_order": args.chunk_order, "fused": args.fused, "split_tiles": args.split, "tile_priority": args.prio, "subtiles": args.subtiles, "scan_mb": args.scan_mb, "start_window_value": start_rate, "finite": finite},
+                   "waves_per_tile": args.waves, "chunk_order": args.chunk_order, "fused": args.fused, "split_tiles": args.split, "tile_priority": args.prio, "subtiles": args.subtiles, "scan_mb": args.scan_mb, "start_window_value": start_rate, "finite": finite,
+                   "contacts_update_ms": contacts_ms, "contacts_distinct_pairs_21_updates": contacts_distinct},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(),
                      "kernel": "k_force<kModeStep>", "force_ms": force_ms, "cell_ms": prof["cell_ms"],
