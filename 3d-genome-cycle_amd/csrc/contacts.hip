@@ -28,10 +28,12 @@ __device__ __forceinline__ unsigned long long contact_slot(unsigned long long ke
     return (key * 0x9E3779B97F4A7C15ull) >> (64 - bits);
 }
 
-// One thread per cell-sorted particle (the search cell list of the current positions, grid edge >= distance):
-// walk the 3x3 neighbouring rows' x-range, count every pair i < j inside the distance into the table.  A failed
-// insert (probe sequence exhausted: table too full) raises table->overflow; counts stay exact for inserted keys.
-__global__ __launch_bounds__(256) void k_contact_insert(const DevCtx* __restrict__ ctx, int n,
+// One thread per cell-sorted particle of any cell list (the engine's own, or a search list built for the
+// distance): the stencil reach per axis is ceil(distance / cell edge) cells (for the engine's list, whose cells
+// are >= the force cutoff >= the contact distance, that is the usual 3 x 3 rows x 5 x-cells; clamped outliers
+// only get closer in cell units).  Every pair i < j inside the distance is counted into the table.  A failed insert (probe sequence
+// exhausted: table too full) raises overflow; counts stay exact for the inserted keys.
+__global__ __launch_bounds__(256) void k_contact_insert(const DevCtx* __restrict__ ctx, int n, float dist,
                                                         const float4* __restrict__ spos, const int* __restrict__ sidx,
                                                         const int* __restrict__ scell, const int* __restrict__ cstart,
                                                         unsigned long long* __restrict__ keys,
@@ -39,19 +41,22 @@ __global__ __launch_bounds__(256) void k_contact_insert(const DevCtx* __restrict
                                                         int* __restrict__ overflow)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n) return;
     const Grid g = ctx->grid;
-    const float d2 = __fmul_rn(g.rc, g.rc);
+    if (s >= n || s >= cstart[g.ncell]) return;
+    const float d2 = __fmul_rn(dist, dist);
+    const float widen = 1.0f + 1.0e-6f;  // never round a reach down
+    const int rx = (int)ceilf(dist * g.inv[0] * widen), ry = (int)ceilf(dist * g.inv[1] * widen),
+              rz = (int)ceilf(dist * g.inv[2] * widen);
     const int i = sidx[s];
     const float4 p = spos[s];
     const int c = scell[s];
     const int nx = g.n[0], ny = g.n[1], nz = g.n[2];
     const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
     const unsigned long long mask = (1ull << bits) - 1ull;
-    for (int z = max(cz - 1, 0); z <= min(cz + 1, nz - 1); ++z)
-        for (int y = max(cy - 1, 0); y <= min(cy + 1, ny - 1); ++y) {
+    for (int z = max(cz - rz, 0); z <= min(cz + rz, nz - 1); ++z)
+        for (int y = max(cy - ry, 0); y <= min(cy + ry, ny - 1); ++y) {
             const int base = (z * ny + y) * nx;
-            const int jb = cstart[base + max(cx - g.fx, 0)], je = cstart[base + min(cx + g.fx, nx - 1) + 1];
+            const int jb = cstart[base + max(cx - rx, 0)], je = cstart[base + min(cx + rx, nx - 1) + 1];
             for (int t = jb; t < je; ++t) {
                 const int j = sidx[t];
                 if (j <= i || !contact_pair(p, spos[t], d2)) continue;
@@ -120,12 +125,12 @@ __global__ __launch_bounds__(256) void k_quantize(const float4* __restrict__ pos
 
 }  // namespace
 
-void launch_contact_insert(hipStream_t s, const DevCtx* ctx, int n, const float4* spos, const int* sidx,
+void launch_contact_insert(hipStream_t s, const DevCtx* ctx, int n, float dist, const float4* spos, const int* sidx,
                            const int* scell, const int* cstart, unsigned long long* keys, unsigned* counts, int bits,
                            int* overflow)
 {
-    hipLaunchKernelGGL(k_contact_insert, dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, spos, sidx, scell, cstart,
-                       keys, counts, bits, overflow);
+    hipLaunchKernelGGL(k_contact_insert, dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, dist, spos, sidx, scell,
+                       cstart, keys, counts, bits, overflow);
 }
 
 void launch_contact_compact(hipStream_t s, const unsigned long long* keys, const unsigned* counts, long long slots,

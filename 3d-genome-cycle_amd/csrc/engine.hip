@@ -1276,10 +1276,17 @@ int gcs_engine_contacts_update(gcs_engine* e, double distance)
         HIPCHK(hipMemsetAsync(e->c_counts, 0, slots * sizeof(unsigned), e->stream));
         HIPCHK(hipMemsetAsync(e->c_flags, 0, 2 * sizeof(int), e->stream));
     }
-    if ((rc = ensure_search(e, e->n))) return rc;
-    if ((rc = enqueue_search_cells(e, e->pos[e->parity], e->n, distance))) return rc;
-    launch_contact_insert(e->stream, e->s_ctx, e->n, e->s_spos, e->s_sidx, e->s_scell, e->s_cstart, e->c_keys,
-                          e->c_counts, e->c_bits, e->c_flags);
+    if (e->fused == 2 && e->chain_valid) {
+        // right after a rebuild-step run the engine's own cell list holds the current positions (k_rebuild built
+        // it from the records the last force kernel filed): no cell build of our own
+        launch_contact_insert(e->stream, e->ctx, e->n, (float)distance, e->spos, e->sidx, e->scell, e->cstart,
+                              e->c_keys, e->c_counts, e->c_bits, e->c_flags);
+    } else {
+        if ((rc = ensure_search(e, e->n))) return rc;
+        if ((rc = enqueue_search_cells(e, e->pos[e->parity], e->n, distance))) return rc;
+        launch_contact_insert(e->stream, e->s_ctx, e->n, (float)distance, e->s_spos, e->s_sidx, e->s_scell,
+                              e->s_cstart, e->c_keys, e->c_counts, e->c_bits, e->c_flags);
+    }
     HIPCHK(hipGetLastError());
     e->c_updates++;
     return GCS_OK;

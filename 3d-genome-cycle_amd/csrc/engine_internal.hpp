@@ -231,7 +231,7 @@ void sort_u64_keys(hipStream_t s, unsigned long long* keys, unsigned long long* 
 size_t sort_u64_temp_bytes(int n);
 
 // contacts.hip: contact map + sampled-position quantisation
-void launch_contact_insert(hipStream_t s, const DevCtx* ctx, int n, const float4* spos, const int* sidx,
+void launch_contact_insert(hipStream_t s, const DevCtx* ctx, int n, float dist, const float4* spos, const int* sidx,
                            const int* scell, const int* cstart, unsigned long long* keys, unsigned* counts, int bits,
                            int* overflow);
 void launch_contact_compact(hipStream_t s, const unsigned long long* keys, const unsigned* counts, long long slots,

@@ -114,3 +114,17 @@ def test_sample_positions_bitexact(c1_design, interphase_cfg):
         got = e.sample_positions(bits)
         exp = np.vectorize(lambda v: oracle.quantize(v, bits))(x).astype(np.float32)
         assert got.dtype == np.float32 and np.array_equal(got.view(np.uint32), exp.view(np.uint32)), bits
+
+
+def test_contact_map_engine_cell_list_equals_search_cell_list(c1_design, interphase_cfg):
+    """After a rebuild-step run the update reads the engine's own cell list; otherwise (4-launch step) it builds a
+    search list: the tables are identical."""
+    a = engine_for(c1_design, interphase_cfg)
+    b = engine_for(c1_design, interphase_cfg)
+    b.set_option(A.OPT_FUSED_STEP, 1)
+    for k in range(4):
+        for e in (a, b):
+            e.run(STEPS_PER_UPDATE, first_step=k * STEPS_PER_UPDATE, seed=13)
+            e.contacts_update(0.24 * 0.6)
+    assert np.array_equal(a.get_positions(), b.get_positions())
+    assert np.array_equal(a.contacts_accumulate(), b.contacts_accumulate())

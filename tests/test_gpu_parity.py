@@ -431,3 +431,55 @@ def test_fused_c2_matches_oracle_forces_after_run(c2_design, interphase_cfg):
     ctx = e.get_context()
     o.set_context(ctx)
     assert_forces_close(e.compute_forces(), o.compute_forces())
+
+
+# ---- C3: the mitotic stages through the drivers (gcs.mitotic), engine vs oracle, Philox noise -------------------
+
+def _c3():
+    from gcs import mitotic
+    from gcs.config import MitoticPhaseConfig
+    cfg = MitoticPhaseConfig()
+    i = synthetic.make_c2()
+    a = mitotic.anatelophase_design(i, cfg)
+    p = mitotic.prometaphase_design(a, cfg, i.master_seed)
+    return mitotic, cfg, a, p
+
+
+def test_c3_anatelophase_stages_match_oracle():
+    """586 beads: rods init (same mt19937_64 draws), 40 anaphase steps with kinetochore fibers, field swap,
+    40 telophase steps with the packing well; positions within 2e-5, energies rel 1e-5."""
+    mitotic, cfg, a, _ = _c3()
+    res = []
+    for cls in (Engine, oracle.OracleSystem):
+        s, h = mitotic.build_anatelophase(cls, a, cfg)
+        drv = mitotic.AnatelophaseDriver(s, h, a, cfg, log=None)
+        drv.run(anaphase_steps=40, telophase_steps=40)
+        res.append((s.get_positions(), s.compute_energy()[0], s.compute_forces()))
+    assert np.abs(res[0][0] - res[1][0]).max() <= 2e-5
+    assert res[0][1] == pytest.approx(res[1][1], rel=1e-5)
+    assert_forces_close(res[0][2], res[1][2])
+
+
+def test_c3_prometaphase_matches_oracle():
+    """1,172 beads: sister bonds, fibers to both poles, force-flux point sources (polar ejection switched on)."""
+    import dataclasses
+    mitotic, cfg, a, p = _c3()
+    cfg = dataclasses.replace(cfg, polar_ejection_force=0.5, polar_ejection_cross_section=0.09,
+                              kfiber_length_prometaphase=1.0)
+    # a structure like the one transition writes: each sister pair side by side around the metaphase plate
+    rng = np.random.default_rng(11)
+    x0 = np.zeros((p.n, 3))
+    for (_, ts, te, _), (_, ss, se, _) in zip(p.chains[0::2], p.chains[1::2]):
+        c = rng.normal(scale=1.0, size=3)
+        d = rng.normal(size=3)
+        d /= np.linalg.norm(d)
+        for k in range(te - ts):
+            x0[ts + k] = c + (k - (te - ts) / 2) * cfg.bond_length * d
+            x0[ss + k] = x0[ts + k] + [0.0, cfg.sister_separation, 0.0]
+    res = []
+    for cls in (Engine, oracle.OracleSystem):
+        s, _ = mitotic.build_prometaphase(cls, p, cfg)
+        mitotic.PrometaphaseDriver(s, p, cfg, log=None).run(x0, steps=50)
+        res.append((s.get_positions(), s.compute_forces()))
+    assert np.abs(res[0][0] - res[1][0]).max() <= 2e-5
+    assert_forces_close(res[0][1], res[1][1])
