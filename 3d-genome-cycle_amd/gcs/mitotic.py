@@ -77,7 +77,7 @@ def prometaphase_design(adesign: MitoticDesign, cfg: MitoticPhaseConfig, master_
         types.extend(seg.tolist())
     axis = np.asarray(cfg.spindle_axis, dtype=np.float64)
     return MitoticDesign(seed=stage_seeds(master_seed)["prometaphase"], particle_types=np.array(types, dtype=np.int32),
-                         chains=chains, sister_chromatids=sisters, pole_positions=np.stack([-axis, axis]))
+                         chains=chains, sister_chromatids=sisters, pole_positions=np.stack([np.zeros(3) - axis, np.zeros(3) + axis]))  # origin -/+ axis
 
 
 class StdNormal:
@@ -162,7 +162,7 @@ class AnatelophaseDriver:
         -spindle_axis + anaphase_start_stddev * N(0, 1)^3, direction normalize(N(0, 1)^3)."""
         cfg = self.cfg
         x = np.zeros((self.design.n, 3))
-        start_center = -np.asarray(cfg.spindle_axis, dtype=np.float64)
+        start_center = np.zeros(3) - np.asarray(cfg.spindle_axis, dtype=np.float64)  # origin - spindle_axis
         for _, start, end, _ in self.design.chains:
             centroid = start_center + cfg.anaphase_start_stddev * normal_vector(self.random)
             d = normal_vector(self.random)
