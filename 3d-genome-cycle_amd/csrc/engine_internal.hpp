@@ -254,7 +254,13 @@ void launch_tail_reduce(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int fblo
 inline int force_blocks(int n) { return (n + kTile - 1) / kTile; }
 // k_force launch size: tiles never cross a cell row, so there are up to (rows) more tiles than force_blocks;
 // blocks walk the tiles grid-stride, any launch size is correct
-inline int force_grid(int n) { return ((force_blocks(n) + force_blocks(n) / 4 + 64) + 7) & ~7; }  // multiple of 8 (XCDs)
+#ifndef GCS_FORCE_GRID_PCT
+#define GCS_FORCE_GRID_PCT 125  // force launch size in % of N / 64 (+ 64 blocks)
+#endif
+inline int force_grid(int n)
+{
+    return ((int)((long long)force_blocks(n) * GCS_FORCE_GRID_PCT / 100) + 64 + 7) & ~7;  // multiple of 8 (XCDs)
+}
 // step launches with split tiles: up to two units per tile
 inline int force_grid_split(int n) { return 2 * force_grid(n); }
 constexpr int kUpdateBlock = 256;

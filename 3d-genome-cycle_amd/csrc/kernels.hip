@@ -1662,6 +1662,9 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
 // group of 16 the union shrinks ~2.5x.  Chunks are 32 candidates per group (one 32-bit hit mask per lane), staged
 // with FPL = 32 / GL loads per lane; phase-1 LDS reads then carry NG addresses (one broadcast per group, the groups
 // on disjoint banks).  Same phase-1 test, frame (per-group origin) and phase 2 as pair_forces.
+#ifndef GCS_P2_UNROLL
+#define GCS_P2_UNROLL 4  // sub-tile phase 2: hits popped per lane per round (rounds = wave max of hits / this)
+#endif
 template <int MODE, int NG>
 __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const ForceArgs& a, int lane, int s,
                                        int s_begin, int s_end, float4 pi, float bi, float& fx, float& fy, float& fz,
@@ -1672,6 +1675,7 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
     constexpr int kSub = 32;        // candidates per group chunk
     constexpr int FPL = kSub / GL;  // candidate fetches per lane per chunk
     constexpr int kRec = 2 * (kSub + 1);  // float4 per group staging area (records + sentinel)
+    constexpr int kP2 = GCS_P2_UNROLL;
     static_assert(NG >= 2 && NG <= 8 && FPL >= 1, "2, 4 or 8 groups");
     const Grid g = ctx->grid;
     const float cs = (float)ctx->cs;
@@ -1795,17 +1799,17 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
         if (MODE != kModeEnergy) acc += (float)__popc(m);
         // phase 2: pop ffbl, xor, min (exhausted -> the group's sentinel slot), clear
         const int mh = uniform(wave_max_int(__popc(m)));
-        for (int t = 0; t < mh; t += 4) {
-            unsigned kk[4];
+        for (int t = 0; t < mh; t += kP2) {
+            unsigned kk[kP2];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < kP2; ++u) {
                 unsigned b;
                 asm("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(m));
                 kk[u] = min(b ^ 7u, (unsigned)kSub);
                 m &= m - 1u;
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < kP2; ++u) {
                 const float4 q = my_cand[2 * kk[u]];
                 const float4 w = my_cand[2 * kk[u] + 1];
                 const float dx = fmaf(0.5f, q.x, xi), dy = fmaf(0.5f, q.y, yi), dz = fmaf(0.5f, q.z, zi);

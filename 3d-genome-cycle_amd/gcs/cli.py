@@ -7,13 +7,15 @@ reference's `prepare` reads TSV inputs instead).
     python -m gcs.cli interphase out.h5 [--relaxation-steps N] [--steps N] [--device 0]
     python -m gcs.cli anatelophase out.h5 [--anaphase-steps N] [--telophase-steps N]
     python -m gcs.cli prometaphase out.h5 [--steps N]   (needs /stages/prometaphase/0/positions)
+    python -m gcs.cli transition interphase|prometaphase out.h5
+    python -m gcs.cli transition cycle prev.h5 next.h5
 """
 from __future__ import annotations
 
 import argparse
 import sys
 
-from . import interphase, mitotic, store, synthetic
+from . import interphase, mitotic, store, synthetic, transition
 from .config import SimulationConfig
 
 
@@ -72,6 +74,20 @@ def cmd_prometaphase(a):
             st.load_positions(0), a.steps)
 
 
+def cmd_transition(a):
+    """stage_transition/main.cpp:43-81"""
+    if a.mode == "cycle":
+        if len(a.paths) != 2:
+            raise SystemExit("prev and next trajectory files must be specified")
+        with store.SimulationStore(a.paths[0]) as prev, store.SimulationStore(a.paths[1]) as nxt:
+            transition.transition_cycle(prev, nxt)
+        return
+    if len(a.paths) != 1:
+        raise SystemExit("single trajectory file must be specified")
+    with store.SimulationStore(a.paths[0]) as st:
+        (transition.transition_interphase if a.mode == "interphase" else transition.transition_prometaphase)(st)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="gcs")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -95,6 +111,10 @@ def main(argv=None):
         else:
             p.add_argument("--steps", type=int, default=None)
         p.set_defaults(fn=fn)
+    p = sub.add_parser("transition")
+    p.add_argument("mode", choices=["interphase", "prometaphase", "cycle"])
+    p.add_argument("paths", nargs="+")
+    p.set_defaults(fn=cmd_transition)
     a = ap.parse_args(argv)
     a.fn(a)
 

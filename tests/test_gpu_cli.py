@@ -1,5 +1,7 @@
-"""GPU: the stage entry points (gcs/cli.py, mirroring the reference's `interphase|anatelophase|prometaphase
-<trajectory.h5>`) end to end on the HIP engine, reading and writing the HDF5 store."""
+"""GPU: the whole cell-cycle pipeline (BASELINE configs[2], C3) through the stage entry points (gcs/cli.py,
+mirroring scripts/simulate and the reference's stage executables) on the HIP engine, reading and writing the HDF5
+store: prepare -> anatelophase -> transition interphase -> interphase (relaxation + simulation, contact map) ->
+transition prometaphase -> prometaphase -> transition cycle -> the daughter's anatelophase."""
 import dataclasses
 
 import numpy as np
@@ -11,33 +13,38 @@ from gcs.config import SimulationConfig
 pytestmark = pytest.mark.gpu
 
 
-def test_stages_through_the_store(tmp_path):
+def _prepare(path, master_seed, cfg):
+    d = synthetic.make_c2(master_seed)
+    a = mitotic.anatelophase_design(d, cfg.mitotic_phase)
+    pm = mitotic.prometaphase_design(a, cfg.mitotic_phase, master_seed)
+    store.write_prepared(path, cfg, d, master_seed, anatelophase=a, prometaphase=pm)
+    return d, a, pm
+
+
+def test_cell_cycle_through_the_store(tmp_path):
     cfg = SimulationConfig()
     cfg.interphase = dataclasses.replace(cfg.interphase, relaxation_sampling_interval=100,
                                          relaxation_logging_interval=100, sampling_interval=200, logging_interval=200,
                                          contactmap_output_window=2)
     cfg.mitotic_phase = dataclasses.replace(cfg.mitotic_phase, sampling_interval=50, logging_interval=50)
-    d = synthetic.make_c2()
-    a = mitotic.anatelophase_design(d, cfg.mitotic_phase)
-    pm = mitotic.prometaphase_design(a, cfg.mitotic_phase, d.master_seed)
-    p = tmp_path / "c2.h5"
-    store.write_prepared(p, cfg, d, d.master_seed, anatelophase=a, prometaphase=pm)
+    p = tmp_path / "mother.h5"
+    d, a, pm = _prepare(p, 1, cfg)
 
-    cli.main(["interphase", str(p), "--relaxation-steps", "200", "--steps", "400", "--quiet"])
     cli.main(["anatelophase", str(p), "--anaphase-steps", "100", "--telophase-steps", "100", "--quiet"])
-    with store.SimulationStore(p) as st:
-        st.set_stage("telophase")
-        x = st.load_positions(100)
-        # transition (out of scope) would refine this; duplicate the chromatids side by side
-        init = np.zeros((pm.n, 3))
-        for (_, s, e, _), (_, ts, te, _), (_, ss, se, _) in zip(a.chains, pm.chains[0::2], pm.chains[1::2]):
-            init[ts:te] = x[s:e]
-            init[ss:se] = x[s:e] + [0.0, cfg.mitotic_phase.sister_separation, 0.0]
-        st.set_stage("prometaphase")
-        st.save_positions(0, init)
+    cli.main(["transition", "interphase", str(p)])
+    cli.main(["interphase", str(p), "--relaxation-steps", "200", "--steps", "400", "--quiet"])
+    cli.main(["transition", "prometaphase", str(p)])
     cli.main(["prometaphase", str(p), "--steps", "100", "--quiet"])
+    q = tmp_path / "daughter.h5"
+    _prepare(q, 2, cfg)
+    cli.main(["transition", "cycle", str(p), str(q)])
+    cli.main(["anatelophase", str(q), "--anaphase-steps", "50", "--telophase-steps", "50", "--quiet"])
 
     with store.SimulationStore(p) as st:
+        st.set_stage("anaphase")
+        assert st.load_steps() == [0, 50, 100]
+        st.set_stage("telophase")
+        assert st.load_steps() == [0, 50, 100]
         st.set_stage("relaxation")
         assert st.load_steps() == [0, 100, 200]
         st.set_stage("interphase")
@@ -46,8 +53,11 @@ def test_stages_through_the_store(tmp_path):
         assert ctx["time"] == pytest.approx(400 * cfg.interphase.timestep) and ctx["mean_energy"] != 0
         c = st.load_contacts(400)
         assert c.shape[0] > d.n // 2 and (c[:, 0] < c[:, 1]).all() and c[:, 2].max() <= 20
-        assert np.isfinite(st.load_positions(400)).all()
-        st.set_stage("anaphase")
-        assert st.load_steps() == [0, 50, 100]
+        x = st.load_positions(400)
+        assert np.isfinite(x).all()
         st.set_stage("prometaphase")
         assert st.load_steps() == [0, 50, 100] and np.isfinite(st.load_positions(100)).all()
+    with store.SimulationStore(q) as st:
+        st.set_stage("anaphase")
+        x0 = st.load_positions(0)  # the transition's structure was used (no rods)
+        assert x0.shape == (a.n, 3) and np.isfinite(st.load_positions(50)).all()
