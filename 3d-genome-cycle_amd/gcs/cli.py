@@ -3,6 +3,7 @@
 with the HIP engine underneath.  `prepare-synthetic` writes a prepared file from the synthetic generators (the
 reference's `prepare` reads TSV inputs instead).
 
+    python -m gcs.cli prepare [-s seed] -o out.h5 config.json chains.tsv
     python -m gcs.cli prepare-synthetic out.h5 --config c1 [--master-seed 1]
     python -m gcs.cli interphase out.h5 [--relaxation-steps N] [--steps N] [--device 0]
     python -m gcs.cli anatelophase out.h5 [--anaphase-steps N] [--telophase-steps N]
@@ -15,7 +16,7 @@ from __future__ import annotations
 import argparse
 import sys
 
-from . import interphase, mitotic, store, synthetic, transition
+from . import interphase, mitotic, prepare, store, synthetic, transition
 from .config import SimulationConfig
 
 
@@ -26,6 +27,10 @@ def cmd_prepare_synthetic(a):
     prom = mitotic.prometaphase_design(anat, cfg.mitotic_phase, a.master_seed) if anat is not None else None
     store.write_prepared(a.path, cfg, design, a.master_seed, anatelophase=anat, prometaphase=prom,
                          chains_source=f"synthetic:{a.config}")
+
+
+def cmd_prepare(a):
+    prepare.prepare(a.output, a.config, a.chains, a.seed)
 
 
 def cmd_interphase(a):
@@ -91,6 +96,12 @@ def cmd_transition(a):
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="gcs")
     sub = ap.add_subparsers(dest="cmd", required=True)
+    p = sub.add_parser("prepare")  # stage_prepare/main.cpp: prepare [-s seed] -o out.h5 config.json chains.tsv
+    p.add_argument("-s", "--seed", type=int, default=None)
+    p.add_argument("-o", "--output", required=True)
+    p.add_argument("config")
+    p.add_argument("chains")
+    p.set_defaults(fn=cmd_prepare)
     p = sub.add_parser("prepare-synthetic")
     p.add_argument("path")
     p.add_argument("--config", default="c1", choices=["c1", "c2", "c5"])

@@ -66,6 +66,8 @@ def prometaphase_design(adesign: MitoticDesign, cfg: MitoticPhaseConfig, master_
     -/+ spindle_axis."""
     chains, sisters, types = [], [], []
     for k, (name, start, end, kin) in enumerate(adesign.chains):
+        if kin is None:
+            raise ValueError(f"chain {name} has no kinetochore bead (prepare.cpp:333 dereferences it)")
         length = end - start
         koff = kin - start
         ts = 2 * start

@@ -289,7 +289,7 @@ class SimulationStore:
 
 
 def write_prepared(path, cfg: SimulationConfig, design, master_seed: int, anatelophase=None, prometaphase=None,
-                   chains_source="", create=True):
+                   chains_source="", create=True, initial_positions=True):
     """What `prepare` writes (prepare.cpp:374-562) for a given interphase design (+ optional mitotic designs):
     /metadata/{master_seed, config, config_source, chains_source}; /stages/interphase/metadata/* with soft links
     from /stages/relaxation/metadata/*; per-stage seeds; the relaxation stage's initial structure at step 0 (the
@@ -316,8 +316,8 @@ def write_prepared(path, cfg: SimulationConfig, design, master_seed: int, anatel
             f.write_strings(ap + "chain_names", [c[0] for c in anatelophase.chains])
             f.write_array(ap + "chain_ranges", np.array([[c[1], c[2]] for c in anatelophase.chains], dtype=np.int32),
                           H5_I32)
-            f.write_array(ap + "kinetochore_beads", np.array([c[3] for c in anatelophase.chains], dtype=np.int32),
-                          H5_I32)
+            f.write_array(ap + "kinetochore_beads", np.array([-1 if c[3] is None else c[3]  # value_or(-1) (:470)
+                                                              for c in anatelophase.chains], dtype=np.int32), H5_I32)
             for key in ("particle_types", "chain_names", "chain_ranges"):
                 f.soft_link(ap + key, "/stages/telophase/metadata/" + key)
         if prometaphase is not None:
@@ -332,4 +332,5 @@ def write_prepared(path, cfg: SimulationConfig, design, master_seed: int, anatel
             f.write_array(pp + "pole_positions", np.asarray(prometaphase.pole_positions, dtype=np.float32), H5_F32)
         for stage in ("anaphase", "interphase", "prometaphase"):  # prepare.cpp:559-561
             f.write_array(f"/stages/{stage}/metadata/seed", np.uint32(seeds[stage]), H5_U32)
-        f.write_array("/stages/relaxation/0/positions", quantize_positions(design.positions), H5_F32, deflate=6)
+        if initial_positions:  # (synthetic designs carry a structure; prepare itself writes none)
+            f.write_array("/stages/relaxation/0/positions", quantize_positions(design.positions), H5_F32, deflate=6)

@@ -1,6 +1,6 @@
 """GPU: the whole cell-cycle pipeline (BASELINE configs[2], C3) through the stage entry points (gcs/cli.py,
 mirroring scripts/simulate and the reference's stage executables) on the HIP engine, reading and writing the HDF5
-store: prepare -> anatelophase -> transition interphase -> interphase (relaxation + simulation, contact map) ->
+store: prepare (config JSON + chain TSV) -> anatelophase -> transition interphase -> interphase (relaxation + simulation, contact map) ->
 transition prometaphase -> prometaphase -> transition cycle -> the daughter's anatelophase."""
 import dataclasses
 
@@ -14,10 +14,21 @@ pytestmark = pytest.mark.gpu
 
 
 def _prepare(path, master_seed, cfg):
+    """`prepare -s seed -o path config.json chains.tsv` with the synthetic C2 chains written as a TSV"""
+    from gcs.config import format_simulation_config
     d = synthetic.make_c2(master_seed)
+    tags = {1: "A", 2: "B", 3: "u", 4: "cen", 5: "anor", 6: "bnor", 0: ""}
+    rows = []
+    for name, s, e in d.chains:
+        for k, i in enumerate(range(s, e)):
+            a, b = d.ab_factors[i]
+            rows.append(f"{name}\t{k * 100000}\t{(k + 1) * 100000}\t{a}\t{b}\t{tags[int(d.particle_types[i])]}")
+    cj, ct = path.with_suffix(".json"), path.with_suffix(".tsv")
+    cj.write_text(format_simulation_config(cfg))
+    ct.write_text("\n".join(rows) + "\n")
+    cli.main(["prepare", "-s", str(master_seed), "-o", str(path), str(cj), str(ct)])
     a = mitotic.anatelophase_design(d, cfg.mitotic_phase)
     pm = mitotic.prometaphase_design(a, cfg.mitotic_phase, master_seed)
-    store.write_prepared(path, cfg, d, master_seed, anatelophase=a, prometaphase=pm)
     return d, a, pm
 
 
