@@ -114,29 +114,24 @@ __device__ __forceinline__ float wave_total_max_f(float v)
     return lane63_f(v);
 }
 
+// Whole-wave reductions (all lanes active, result wave-uniform): the DPP scan above plus a readlane of lane 63 --
+// six VALU steps with no LDS round trip, where a __shfl_xor butterfly is six dependent ds_bpermute waits.
+__device__ __forceinline__ float add_f(float a, float b) { return a + b; }
 __device__ inline float wave_sum(float v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    GCS_DPP_SCAN(dpp_f, add_f, 0.f, v)
+    return lane63_f(v);
 }
-__device__ inline double wave_sum_d(double v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
+__device__ inline double wave_sum_d(double v) { return wave_total_sum_d(v); }
 __device__ inline float wave_max(float v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-    return v;
+    GCS_DPP_SCAN(dpp_f, max_f, -__builtin_huge_valf(), v)
+    return lane63_f(v);
 }
 __device__ inline float wave_min(float v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
-    return v;
+    GCS_DPP_SCAN(dpp_f, min_f, __builtin_huge_valf(), v)
+    return lane63_f(v);
 }
 
 __device__ inline int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -145,9 +140,8 @@ __device__ inline float uniform_f(float v) { return __int_as_float(__builtin_amd
 
 __device__ inline int wave_max_int(int v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
-    return v;
+    GCS_DPP_SCAN(dpp_i, max_i, (int)0x80000000, v)
+    return __builtin_amdgcn_readlane(v, 63);
 }
 
 
@@ -1662,6 +1656,12 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
 // group of 16 the union shrinks ~2.5x.  Chunks are 32 candidates per group (one 32-bit hit mask per lane), staged
 // with FPL = 32 / GL loads per lane; phase-1 LDS reads then carry NG addresses (one broadcast per group, the groups
 // on disjoint banks).  Same phase-1 test, frame (per-group origin) and phase 2 as pair_forces.
+#ifndef GCS_ROW_CURSOR
+#define GCS_ROW_CURSOR 0  // 1: incremental stencil-row cursor in the sub-tile candidate fetch
+#endif
+#ifndef GCS_P1_PLAIN
+#define GCS_P1_PLAIN 0  // 1: phase-1 hit bits from plain C (compiler-scheduled) instead of the cmp+addc asm pair
+#endif
 #ifndef GCS_P2_UNROLL
 #define GCS_P2_UNROLL 4  // sub-tile phase 2: hits popped per lane per round (rounds = wave max of hits / this)
 #endif
@@ -1743,6 +1743,18 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
     float4 np[FPL];
     float nb[FPL];
     int nj[FPL];
+#if GCS_ROW_CURSOR
+    // a lane's candidate index v = cg + G i only grows from chunk to chunk, so its stencil row is found by walking
+    // forward from the previous one (usually zero or one step) instead of a 4-level binary search of dependent LDS
+    // reads; rows 9..16 start at the group total, so the walk stops for any v < total
+    int rcur[FPL], rnext[FPL], rbase[FPL];
+#pragma unroll
+    for (int f = 0; f < FPL; ++f) {
+        rcur[f] = 0;
+        rnext[f] = rowV[1];
+        rbase[f] = rowJ[0] - rowV[0];
+    }
+#endif
     auto fetch = [&](int c) {
         const int cg = wv + c * nwv;  // chunk index within every group
 #pragma unroll
@@ -1751,11 +1763,20 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
             const int v = cg + G * i;
             nj[f] = -1;
             if (cg < G && v < total) {
+#if GCS_ROW_CURSOR
+                while (rnext[f] <= v) {
+                    ++rcur[f];
+                    rnext[f] = rowV[rcur[f] + 1];
+                    rbase[f] = rowJ[rcur[f]] - rowV[rcur[f]];
+                }
+                nj[f] = rbase[f] + v;
+#else
                 int lo = 0;
 #pragma unroll
                 for (int step = 8; step > 0; step >>= 1)
                     if (rowV[lo + step] <= v) lo += step;
                 nj[f] = rowJ[lo] + (v - rowV[lo]);
+#endif
                 np[f] = a.spos[nj[f]];
                 nb[f] = a.sb[nj[f]];
             }
@@ -1780,18 +1801,28 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
 #pragma unroll
         for (int k0 = 0; k0 < kSub; k0 += 8) {
             unsigned byte = 0u;
+            // the 8 distance tests first, the compare chain after: the inline asm below is a scheduling barrier,
+            // so interleaving it with the LDS reads would serialise every read on its own lgkmcnt(0)
+            float tv[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const float4 q = my_cand[2 * (k0 + u)];
-                const float t = fmaf(q.x, xi, fmaf(q.y, yi, fmaf(q.z, zi, q.w)));
+                tv[u] = fmaf(q.x, xi, fmaf(q.y, yi, fmaf(q.z, zi, q.w)));
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
                 if (MODE == kModeEnergy) {
-                    const bool in = (t < thr) && (s_candj[grp * kSub + k0 + u] != s);
+                    const bool in = (tv[u] < thr) && (s_candj[grp * kSub + k0 + u] != s);
                     byte = 2u * byte + (in ? 1u : 0u);
                 } else {
+#if GCS_P1_PLAIN
+                    byte = 2u * byte + (tv[u] < thr ? 1u : 0u);
+#else
                     asm("v_cmp_gt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
                         : "+v"(byte)
-                        : "v"(thr), "v"(t)
+                        : "v"(thr), "v"(tv[u])
                         : "vcc");
+#endif
                 }
             }
             m |= byte << k0;
