@@ -58,7 +58,7 @@ def cmd_anatelophase(a):
         design = st.load_anatelophase_design()
         sys_, h = mitotic.build_anatelophase(Engine, design, cfg, device=a.device)
         drv = mitotic.AnatelophaseDriver(sys_, h, design, cfg, store=st, log=None if a.quiet else sys.stderr)
-        st.set_stage("anaphase")  # run (:192-200): clear_frames before set_stage
+        st.set_stage("anaphase")  # run (stage_anatelophase/simulation_driver.cpp:193-203): clear_frames before set_stage
         st.clear_frames()
         st.set_stage("anaphase")
         init = st.load_positions(0) if st.check_positions(0) else None

@@ -120,7 +120,7 @@ def resolution_scaled(cfg: "InterphaseConfig", bin_ratio: float) -> "InterphaseC
         contactmap_distance=cfg.contactmap_distance * f)
 
 
-# fields the reference's JSON traits do not list (simulation_config.cpp:218-269)
+# fields the reference's JSON traits do not list (common/simulation_config.cpp:88-118)
 NOT_IN_JSON = {"a_core_2nd_bond_spring", "b_core_2nd_bond_spring"}
 
 

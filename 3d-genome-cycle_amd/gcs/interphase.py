@@ -2,7 +2,7 @@
 
 `build_interphase` mirrors simulation_driver::setup_particles / setup_forcefield / setup_context
 (stage_interphase/simulation_driver_particles.cpp:9-35, simulation_driver_forcefield.cpp:9-244,
-simulation_driver.cpp:35-43) on any backend with the engine's method names: the HIP `Engine` (product)
+stage_interphase/simulation_driver.cpp:35-43) on any backend with the engine's method names: the HIP `Engine` (product)
 or the CPU oracle (tests only).  `InterphaseDriver` mirrors run_relaxation / run_simulation
 (simulation_driver_relaxation.cpp:8-56, simulation_driver_interphase.cpp:9-90): the per-step callback's
 state updates live on the device; the host regains control at interval boundaries only.
@@ -75,7 +75,7 @@ def interphase_schedule(cfg: InterphaseConfig) -> dict:
 
 
 def initial_context(cfg: InterphaseConfig) -> dict:
-    """simulation_driver.cpp:35-43"""
+    """stage_interphase/simulation_driver.cpp:35-43"""
     return {"step": 0, "time": 0.0, "wall_semiaxes": list(cfg.wall_semiaxes_init), "core_scale": cfg.core_scale_init,
             "bond_scale": cfg.bond_scale_init}
 

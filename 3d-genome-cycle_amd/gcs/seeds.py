@@ -2,7 +2,7 @@
 
 stage_prepare/prepare.cpp:549-562: std::seed_seq{master_seed}.generate(3 x u32) -> per-stage seeds
 (anaphase, interphase, prometaphase).  Each stage driver then draws its BD seeds from
-std::mt19937_64(stage_seed) (stage_interphase/simulation_driver.cpp:19; relaxation.cpp:53 takes the first
+std::mt19937_64(stage_seed) (stage_interphase/simulation_driver.cpp:19; stage_interphase/simulation_driver_relaxation.cpp:53 takes the first
 draw, simulation_driver_interphase.cpp:61 the second).  Both algorithms are standard-specified
 ([rand.util.seedseq], [rand.eng.mers]); tests/test_seeds.py pins them against g++ output.
 """

@@ -8,11 +8,20 @@ and the schedule tail), i.e. one iteration of md::simulate_brownian_dynamics.  T
 300,000 (t = 3, core_scale = 0.9988): the regime of >90 % of the reference's 700,000 production steps.
 Inputs are resident in HBM before the timed region.
 
-Replicas: each GPU runs --replicas-per-gpu independent trajectories (default 4; own master seed and noise seed,
-like separate `scripts/simulate -s` runs), each with its own engine and HIP stream, so the GPU overlaps one
-trajectory's latency-bound launches with another's force kernel.  The single-trajectory rate is reported beside
-it (config.single_trajectory_value).  Multi-GPU (torchrun): every rank does the same with its own replicas, no
-data-path collective; value = all particle updates / max-over-ranks time ("scaling": "weak").
+Replicas (C4; the reference's ensemble is separate `scripts/simulate -s seed` runs, scripts/simulate:15-18): each
+GPU runs --replicas-per-gpu independent trajectories (own noise seed), each with its own engine and HIP stream, so
+the GPU overlaps one trajectory's latency-bound launches with another's force kernel.  The single-trajectory rate
+is reported beside it (config.single_trajectory_value).
+
+Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) every rank runs its own replicas; with
+`--gpus N` and no WORLD_SIZE this process is only a launcher: it makes no GPU call and starts N child ranks
+(RANK = LOCAL_RANK = r, gloo rendezvous on 127.0.0.1), then exits with their status.  No data-path collective:
+gloo carries the barrier, the max-over-ranks time and the per-rank rates only; value = all particle updates of
+all ranks / the slowest rank's time ("scaling": "weak").
+
+Timed window: warm-up runs at least two graph chunks per engine (every hipGraph is captured and instantiated before
+timing), then the timed region repeats passes of --steps steps (per replica) until it lasts >= --min-window-s;
+"steps" reports the steps actually timed, "steps_requested" the flag.
 
 Rank 0 prints ONE JSON line.  See DESIGN.md "Measurement" for the roofline accounting.
 """
@@ -20,7 +29,10 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -30,25 +42,14 @@ sys.path.insert(0, str(ROOT / "3d-genome-cycle_amd"))
 
 import numpy as np  # noqa: E402
 
-from gcs import _abi as A  # noqa: E402
-
-CPU_WORKER = "--cpu-worker" in sys.argv  # a CPU-baseline child process (no device use)
-DECOMP = "--decomp" in sys.argv  # one trajectory split over domains: torch tensors share the engine's runtime
-if DECOMP:
-    # one HIP runtime per process: torch's is initialised first and libgcs.so binds to it (tools/runtime_probe.py)
-    import torch
-    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-    torch.zeros(1, device="cuda")
-if not CPU_WORKER:
-    A.load()  # (replica runs: bind the engine's HIP runtime before torch loads its own copy)
-
-from gcs import interphase, synthetic  # noqa: E402
-from gcs.config import InterphaseConfig  # noqa: E402
-from gcs.engine import Engine  # noqa: E402
-
 BYTES_PER_UPDATE = 36  # algorithmic: 12 B position read + 12 B position write + 12 B {mu, a, b}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md "Chip-level parameters")
 WINDOW_START = 300_000
+STATE_FILE = ROOT / "benchdata" / "c2_interphase_step300000.npz"
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# process topology
 
 
 def dist_setup(backend="gloo"):
@@ -79,8 +80,44 @@ def max_over_ranks(dist, v):
     return float(t.item())
 
 
+def gather_over_ranks(dist, v):
+    """every rank's value of v (a float), in rank order"""
+    if dist is None:
+        return [v]
+    import torch
+    out = [torch.zeros(1, dtype=torch.float64) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, torch.tensor([v], dtype=torch.float64))
+    return [float(t.item()) for t in out]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` without WORLD_SIZE: start N child ranks of this same script (one per GPU) and wait.
+    This process touches no device: the children load the engine after their own environment is set."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(ROOT / "bench.py")] + list(argv), env=env))
+    rc = 0
+    for p in procs:
+        code = p.wait()
+        if code != 0 and rc == 0:
+            rc = code
+            for q in procs:  # one rank failed: the others would wait forever in the next collective
+                if q.poll() is None:
+                    q.terminate()
+    return rc
+
+
 def replica_master_seed(rank: int) -> int:
-    """Each rank is an independent trajectory with its own master seed (like `scripts/simulate -s <seed>`)."""
+    """Each trajectory is independent with its own master seed (like `scripts/simulate -s <seed>`)."""
     return 1 + rank
 
 
@@ -93,7 +130,8 @@ def whole_job_value(n: int, steps: int, world: int, el_max: float) -> float:
     return n * steps * world / el_max
 
 
-STATE_FILE = ROOT / "benchdata" / "c2_interphase_step300000.npz"
+# ---------------------------------------------------------------------------------------------------------------
+# workload
 
 
 def load_state():
@@ -106,6 +144,8 @@ def load_state():
 
 
 def make_engine(design, cfg, device, start_step, state=None):
+    from gcs import interphase
+    from gcs.engine import Engine
     e, _ = interphase.build_interphase(Engine, design, cfg, device=device)
     e.set_schedule(**interphase.interphase_schedule(cfg))
     if state is not None:
@@ -121,9 +161,68 @@ def make_engine(design, cfg, device, start_step, state=None):
     return e
 
 
+class StubEngine:
+    """Stands in for gcs.engine.Engine in `--stub-engine` runs (CPU tests of the launcher and the aggregation):
+    the same calls, a fixed sleep per step, no device."""
+
+    STEP_S = 2e-5
+
+    def __init__(self, n):
+        self.n = n
+        self.step = 0
+
+    def set_option(self, *_):
+        pass
+
+    def run(self, steps, first_step=0, **_):
+        time.sleep(self.STEP_S * steps)
+        self.step = first_step + steps
+
+    def synchronize(self):
+        pass
+
+    def profile(self, steps, first_step=0, **_):
+        self.run(steps, first_step)
+        return {"force_ms": 1e3 * self.STEP_S * 0.75, "cell_ms": 1e3 * self.STEP_S * 0.25, "tail_ms": 0.0,
+                "mean_neighbors": 25.0}
+
+    def get_context(self):
+        return {"step": self.step, "core_scale": 1.0}
+
+    def get_positions(self):
+        return np.zeros((self.n, 3))
+
+    def close(self):
+        pass
+
+
+def window_start(name):
+    """C2: the committed step-300,000 trajectory state.  C1/C5: their synthetic start (step 0, core_scale 0.5) --
+    a synthetic chain packed at the generator's density has ~8x the equilibrated neighbour count at core_scale 1."""
+    return WINDOW_START if name == "c2" else 0
+
+
+def bench_config(name):
+    """The interphase defaults; C5's 10 kb beads use the force field rescaled to their size
+    (gcs.config.resolution_scaled, DESIGN.md "Measurement")."""
+    from gcs.config import InterphaseConfig, resolution_scaled
+    cfg = InterphaseConfig()
+    return resolution_scaled(cfg, 10.0) if name == "c5" else cfg
+
+
+def design_maker(name):
+    from gcs import synthetic
+    return {"c1": synthetic.make_c1, "c2": synthetic.make_c2, "c5": synthetic.make_c5}[name]
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# CPU baseline (the oracle: test infrastructure, used here only as the reported CPU leg)
+
+
 def cpu_rate(design, cfg, start_step, budget_s, state):
     """The oracle (fp64, 1 thread, reference flags) on a bounded sample of the same workload (same state):
     one step to size the sample, then as many steps as fit `budget_s`.  Returns (bead-updates/s, steps, s)."""
+    from gcs import interphase
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg only
     o, _ = interphase.build_interphase(oracle.OracleSystem, design, cfg)
@@ -142,6 +241,8 @@ def cpu_rate(design, cfg, start_step, budget_s, state):
 
 def cpu_worker(budget_s):
     """Child-process entry (`bench.py --cpu-worker S`): one single-threaded oracle trajectory; prints its rate."""
+    from gcs import synthetic
+    from gcs.config import InterphaseConfig
     r, steps, el = cpu_rate(synthetic.make_c2(master_seed=1), InterphaseConfig(), WINDOW_START, budget_s, load_state())
     print(json.dumps({"value": r, "steps": steps, "seconds": el}), flush=True)
 
@@ -150,7 +251,6 @@ def cpu_baseline(budget_s, procs):
     """cpu_baseline of the bench line.  value: ONE oracle process on one core (the reference is single-threaded);
     `replicas_value`: `procs` independent single-threaded trajectories side by side, aggregate.
     Both legs run as child processes that never touch the device."""
-    import subprocess
 
     def launch(k):
         env = dict(os.environ, OMP_NUM_THREADS="1")
@@ -202,30 +302,21 @@ def read_traffic():
     return None
 
 
-def window_start(name):
-    """C2: the committed step-300,000 trajectory state.  C1/C5: their synthetic start (step 0, core_scale 0.5) --
-    a synthetic chain packed at the generator's density has ~8x the equilibrated neighbour count at core_scale 1."""
-    return WINDOW_START if name == "c2" else 0
-
-
-def bench_config(name):
-    """The interphase defaults; C5's 10 kb beads use the force field rescaled to their size
-    (gcs.config.resolution_scaled, DESIGN.md "Measurement")."""
-    from gcs.config import resolution_scaled
-    cfg = InterphaseConfig()
-    return resolution_scaled(cfg, 10.0) if name == "c5" else cfg
+# ---------------------------------------------------------------------------------------------------------------
+# decomposed single trajectory (C5)
 
 
 def decomp_main(args):
     """One trajectory split into z-slab domains (gcs.domain; C5 of SURVEY 8e).  value = N x steps / max-over-ranks
     time of the whole decomposed step loop (force, update, reaction allreduce, band exchange)."""
     import torch
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    torch.zeros(1, device="cuda")  # one HIP runtime per process: torch's first, libgcs.so binds to it
     from gcs import domain as D
     world, rank, local, dist = dist_setup("nccl")
     cfg = bench_config(args.config)
-    maker = {"c1": synthetic.make_c1, "c2": synthetic.make_c2, "c5": synthetic.make_c5}[args.config]
     state = load_state() if args.config == "c2" else None
-    design = maker(master_seed=1)
+    design = design_maker(args.config)(master_seed=1)
     ndom = world if world > 1 else args.decomp
     halo = D.domain_halo(cfg)
     x0 = state[0] if state is not None else design.positions
@@ -269,11 +360,212 @@ def decomp_main(args):
         dist.destroy_process_group()
 
 
-def main():
+# ---------------------------------------------------------------------------------------------------------------
+# replicas (C2 / C4): the headline
+
+
+def replica_main(args):
+    world, rank, local, dist = dist_setup()
+    if not args.stub_engine:
+        from gcs import _abi as A
+        A.load()  # this rank's engine runtime (no torch HIP runtime in replica runs)
+    cfg = bench_config(args.config)
+    maker = design_maker(args.config)
+    R = max(1, args.replicas_per_gpu)
+    K = max(1, args.steps)
+    # graph chunk: a pass of K steps per replica is replayed in G-step hipGraphs (G <= K, so short passes replay
+    # graphs too); warm-up captures and instantiates every engine's graph before the timed region
+    G = min(args.graph_steps, K) if args.graph_steps > 0 else 0
+    warm = max(args.warmup, 2 * G, 1)
+
+    # R independent trajectories per GPU (own noise seed, own engine and HIP stream each).  Rank r owns
+    # replicas r*R .. r*R + R - 1, so every trajectory of the job has its own seeds.  C2: every replica continues
+    # the committed step-300,000 state of the master-seed-1 system with its own noise seed
+    # (tools/make_bench_state.py); other configs start from their synthetic state at the window's context
+    state = load_state() if args.config == "c2" and not args.stub_engine else None
+    window = window_start(args.config)
+    designs, engines, seeds = [], [], []
+    for k in range(R):
+        rid = rank * R + k
+        d = maker(master_seed=1 if state is not None else replica_master_seed(rid))
+        if args.stub_engine:
+            e = StubEngine(d.n)
+        else:
+            from gcs import _abi as A
+            e = make_engine(d, cfg, local, window, state)
+            for opt, v in ((A.OPT_GRAPH_STEPS, G), (A.OPT_WAVES_PER_TILE, args.waves),
+                           (A.OPT_CHUNK_ORDER, args.chunk_order), (A.OPT_FUSED_STEP, args.fused),
+                           (A.OPT_SPLIT_TILES, args.split), (A.OPT_TILE_PRIORITY, args.prio),
+                           (A.OPT_SUBTILES, args.subtiles), (A.OPT_SCAN_BLOCKS, args.scan_mb)):
+                e.set_option(opt, v)
+        designs.append(d)
+        engines.append(e)
+        seeds.append(replica_noise_seed(rid))
+    design, eng, seed = designs[0], engines[0], seeds[0]
+    n = design.n
+    nxt = [window] * R  # next step of every replica (host-side: no device round trip in the timed loop)
+
+    def run_all(steps):
+        """`steps` steps of every replica, enqueued interleaved chunk by chunk so their graphs run side by side"""
+        chunk = G if G > 0 else 64
+        for s0 in range(0, steps, chunk):
+            c = min(chunk, steps - s0)
+            for k, (e, sd) in enumerate(zip(engines, seeds)):
+                e.run(c, first_step=nxt[k], seed=sd)
+                nxt[k] += c
+        for e in engines:
+            e.synchronize()
+
+    t0 = time.perf_counter()
+    run_all(warm)
+    warm_s = time.perf_counter() - t0
+
+    # one trajectory alone on the GPU (replica 0; the others are independent and idle meanwhile), its own window
+    single_rate = None
+    if R > 1 and rank == 0:
+        k1 = G if G > 0 else 64
+        eng.run(k1, first_step=nxt[0], seed=seed)  # (graph already instantiated by the warm-up)
+        eng.synchronize()
+        nxt[0] += k1
+        reps = 0
+        t1 = time.perf_counter()
+        while True:  # >= half the headline window, in blocks of 8 graph replays
+            eng.run(k1, first_step=nxt[0], seed=seed)
+            nxt[0] += k1
+            reps += 1
+            if reps % 8 == 0:
+                eng.synchronize()
+                el1 = time.perf_counter() - t1
+                if el1 >= 0.5 * args.min_window_s:
+                    break
+        single_rate = n * k1 * reps / el1
+
+    # passes of K steps so the timed window lasts >= min_window_s (estimated from the warm-up, agreed by all ranks)
+    per_pass = warm_s * K / warm
+    passes = max(1, math.ceil(args.min_window_s / max(per_pass, 1e-9)))
+    passes = int(max_over_ranks(dist, float(passes)))
+    barrier(dist)
+    for e in engines:
+        e.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(passes):
+        run_all(K)
+    el = time.perf_counter() - t0
+    barrier(dist)
+    steps = passes * K
+    el_max = max_over_ranks(dist, el)
+    rank_values = gather_over_ranks(dist, n * R * steps / el)
+    after = nxt[0]
+
+    # per-kernel durations with HIP events on the engine's stream (replica 0 alone, after the timed region)
+    prof = eng.profile(args.profile_steps, first_step=after, seed=seed)
+    force_ms = prof["force_ms"]
+    achieved = n * BYTES_PER_UPDATE / (force_ms * 1e-3) / 1e9
+    ctx = eng.get_context()
+    finite = all(bool(np.isfinite(e.get_positions()).all()) for e in engines)
+    at = after + args.profile_steps
+
+    contacts_ms, contacts_distinct = None, None
+    start_rate = None
+    if not args.stub_engine:
+        # secondary (off the step metric, SURVEY 8d): the contact-map update (contact_map.cpp:33-63) that
+        # production runs every 20 steps, measured as the extra time of 20-step chunks with an update after each
+        # (the update then reads the engine's own cell list, as in production)
+        dcon = cfg.contactmap_distance * ctx["core_scale"]
+
+        def chunks(k, with_update):
+            nonlocal at
+            eng.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(k):
+                eng.run(20, first_step=at, seed=seed)
+                at += 20
+                if with_update:
+                    eng.contacts_update(dcon)
+            eng.synchronize()
+            return time.perf_counter() - t1
+
+        chunks(2, True)
+        base = chunks(20, False)
+        withc = chunks(20, True)
+        contacts_ms = max(0.0, (withc - base) * 1e3 / 20)
+        contacts_distinct = int(eng.contacts_accumulate().shape[0])
+        eng.contacts_clear()
+
+        # secondary: the production start window (step 0, core_scale 0.5, ~7x fewer neighbours), one replica
+        if rank == 0 and not args.no_start_window:
+            e0 = make_engine(design, cfg, local, 0)
+            e0.set_option(A.OPT_GRAPH_STEPS, G)
+            e0.run(max(64, 2 * G), first_step=0, seed=seed)
+            e0.synchronize()
+            k0 = max(256, K // 4)
+            t1 = time.perf_counter()
+            e0.run(k0, first_step=max(64, 2 * G), seed=seed)
+            e0.synchronize()
+            start_rate = n * k0 / (time.perf_counter() - t1)
+            e0.close()
+
+    if rank != 0:
+        for e in engines:
+            e.close()
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    cpu = None
+    if world == 1 and args.cpu_budget > 0 and state is not None and args.config == "c2":
+        cpu = cpu_baseline(args.cpu_budget, args.cpu_procs)
+
+    value = whole_job_value(n * R, steps, world, el_max)
+    line = {
+        "metric": "bead-updates/sec (whole node), 60k-bead diploid interphase",
+        "value": value,
+        "unit": "bead-updates/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": el_max * 1e3 / steps,  # one step of every replica
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic" if not args.stub_engine else "stub",
+        "steps_requested": K,
+        "passes": passes,
+        "warmup_steps_run": warm,
+        "timed_s": el_max,
+        "per_rank_values": rank_values,
+        "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, {R} independent "
+                               f"trajectories per GPU, window from step {window} "
+                               f"(core_scale {ctx['core_scale']:.4f})",
+                   "particles": n, "replicas": world * R, "replicas_per_gpu": R,
+                   "parallelism": f"replicas{world}x{R}",
+                   "single_trajectory_value": single_rate if R > 1 else value,
+                   "mean_neighbors": prof["mean_neighbors"], "graph_steps": G,
+                   "waves_per_tile": args.waves, "chunk_order": args.chunk_order, "fused": args.fused,
+                   "split_tiles": args.split, "tile_priority": args.prio, "subtiles": args.subtiles,
+                   "scan_mb": args.scan_mb, "start_window_value": start_rate, "finite": finite,
+                   "contacts_update_ms": contacts_ms, "contacts_distinct_pairs_22_updates": contacts_distinct},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(),
+                     "kernel": "k_force<kModeStep>", "force_ms": force_ms, "cell_ms": prof["cell_ms"],
+                     "tail_ms": prof["tail_ms"], "bytes_per_launch": n * BYTES_PER_UPDATE},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    for e in engines:
+        e.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=2000, help="steps per replica per timed pass")
+    ap.add_argument("--warmup", type=int, default=200, help="untimed steps per replica (at least 2 graph chunks)")
+    ap.add_argument("--min-window-s", type=float, default=0.5,
+                    help="the timed region repeats passes of --steps until it lasts this long")
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c5"])
     ap.add_argument("--graph-steps", type=int, default=32)
     ap.add_argument("--waves", type=int, default=4)
@@ -290,177 +582,28 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=16,
                     help="independent single-threaded CPU trajectories for the multi-core leg (the box's CPU share)")
     ap.add_argument("--cpu-worker", type=float, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--stub-engine", action="store_true", help=argparse.SUPPRESS)  # CPU tests of the launcher
     ap.add_argument("--no-start-window", action="store_true", help="skip the secondary step-0 window")
     ap.add_argument("--decomp", type=int, default=0,
                     help="spatial domain decomposition of ONE trajectory: K domains (torchrun: one per rank over "
                          "RCCL; single process: K domains on this GPU, in-process exchange)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
     if args.cpu_worker is not None:
         cpu_worker(args.cpu_worker)
-        return
+        return 0
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, argv)  # launcher only: no device call in this process
     if args.decomp:
         decomp_main(args)
-        return
-
-    world, rank, local, dist = dist_setup()
-    cfg = bench_config(args.config)
-    maker = {"c1": synthetic.make_c1, "c2": synthetic.make_c2, "c5": synthetic.make_c5}[args.config]
-    R = max(1, args.replicas_per_gpu)
-
-    # R independent trajectories per GPU (own master seed, own engine and HIP stream each): the GPU overlaps one
-    # replica's latency-bound launches (cell scan, tail) with another's force kernel.  Rank r owns replicas
-    # r*R .. r*R + R - 1, so every trajectory of the job has its own seeds.
-    # C2: every replica continues the committed step-300,000 state of the master-seed-1 system with its own noise
-    # seed (tools/make_bench_state.py); other configs start from their synthetic state at the window's context
-    state = load_state() if args.config == "c2" else None
-    window = window_start(args.config)
-    designs, engines, seeds = [], [], []
-    for k in range(R):
-        rid = rank * R + k
-        d = maker(master_seed=1 if state is not None else replica_master_seed(rid))
-        e = make_engine(d, cfg, local, window, state)
-        e.set_option(A.OPT_GRAPH_STEPS, args.graph_steps)
-        e.set_option(A.OPT_WAVES_PER_TILE, args.waves)
-        e.set_option(A.OPT_CHUNK_ORDER, args.chunk_order)
-        e.set_option(A.OPT_FUSED_STEP, args.fused)
-        e.set_option(A.OPT_SPLIT_TILES, args.split)
-        e.set_option(A.OPT_TILE_PRIORITY, args.prio)
-        e.set_option(A.OPT_SUBTILES, args.subtiles)
-        e.set_option(A.OPT_SCAN_BLOCKS, args.scan_mb)
-        designs.append(d)
-        engines.append(e)
-        seeds.append(replica_noise_seed(rid))
-    design, eng, seed = designs[0], engines[0], seeds[0]
-    n = design.n
-
-    for e, sd in zip(engines, seeds):
-        e.run(args.warmup, first_step=window, seed=sd)
-    for e in engines:
-        e.synchronize()
-    first = window + args.warmup
-
-    nxt = [first] * R  # next step of every replica (host-side: no device round trip in the timed loop)
-    # one trajectory alone on the GPU first (replica 0; the others are independent, their window starts later)
-    single_rate = None
-    if R > 1 and rank == 0:
-        k1 = max(256, args.steps // 2)
-        t1 = time.perf_counter()
-        eng.run(k1, first_step=first, seed=seed)
-        eng.synchronize()
-        single_rate = n * k1 / (time.perf_counter() - t1)
-        nxt[0] += k1
-
-    def run_all(steps):
-        chunk = 2 * args.graph_steps if args.graph_steps > 0 else 64
-        for s0 in range(0, steps, chunk):  # interleaved enqueue: the replicas' graphs run side by side
-            c = min(chunk, steps - s0)
-            for k, (e, sd) in enumerate(zip(engines, seeds)):
-                e.run(c, first_step=nxt[k], seed=sd)
-                nxt[k] += c
-        for e in engines:
-            e.synchronize()
-
-    barrier(dist)
-    for e in engines:
-        e.synchronize()
-    t0 = time.perf_counter()
-    run_all(args.steps)
-    el = time.perf_counter() - t0
-    barrier(dist)
-    el_max = max_over_ranks(dist, el)
-    after = nxt[0]
-
-    # per-kernel durations with HIP events on the engine's stream (replica 0 alone, after the timed region)
-    prof = eng.profile(args.profile_steps, first_step=after, seed=seed)
-    force_ms = prof["force_ms"]
-    achieved = n * BYTES_PER_UPDATE / (force_ms * 1e-3) / 1e9
-    ctx = eng.get_context()
-    finite = all(bool(np.isfinite(e.get_positions()).all()) for e in engines)
-    # secondary (off the step metric): the contact-map update (contact_map.cpp:33-63) that production
-    # runs every 20 steps, measured as the extra time of 20-step chunks with an update after each (the update then
-    # reads the engine's own cell list, as in production)
-    dcon = cfg.contactmap_distance * ctx["core_scale"]
-    at = after + args.profile_steps
-
-    def chunks(k, with_update):
-        nonlocal at
-        eng.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(k):
-            eng.run(20, first_step=at, seed=seed)
-            at += 20
-            if with_update:
-                eng.contacts_update(dcon)
-        eng.synchronize()
-        return time.perf_counter() - t1
-
-    chunks(2, True)
-    base = chunks(20, False)
-    withc = chunks(20, True)
-    contacts_ms = max(0.0, (withc - base) * 1e3 / 20)
-    contacts_distinct = int(eng.contacts_accumulate().shape[0])
-    eng.contacts_clear()
-
-    # secondary: the production start window (step 0, core_scale 0.5, ~7x fewer neighbours), one replica
-    start_rate = None
-    if rank == 0 and not args.no_start_window:
-        e0 = make_engine(design, cfg, local, 0)
-        e0.set_option(A.OPT_GRAPH_STEPS, args.graph_steps)
-        e0.run(64, first_step=0, seed=seed)
-        e0.synchronize()
-        t1 = time.perf_counter()
-        k0 = max(256, args.steps // 4)
-        e0.run(k0, first_step=64, seed=seed)
-        e0.synchronize()
-        start_rate = n * k0 / (time.perf_counter() - t1)
-        e0.close()
-
-    if rank != 0:
-        for e in engines:
-            e.close()
-        if dist is not None:
-            dist.destroy_process_group()
-        return
-
-    cpu = None
-    if world == 1 and args.cpu_budget > 0 and state is not None and args.config == "c2":
-        cpu = cpu_baseline(args.cpu_budget, args.cpu_procs)
-
-    value = whole_job_value(n * R, args.steps, world, el_max)
-    line = {
-        "metric": "bead-updates/sec (whole node), 60k-bead diploid interphase",
-        "value": value,
-        "unit": "bead-updates/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": el_max * 1e3 / args.steps,  # one step of every replica
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic",
-        "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, {R} independent "
-                               f"trajectories per GPU, window from step {window} "
-                               f"(core_scale {ctx['core_scale']:.4f})",
-                   "particles": n, "replicas": world * R, "replicas_per_gpu": R,
-                   "parallelism": f"replicas{world}x{R}",
-                   "single_trajectory_value": single_rate if R > 1 else value,
-                   "mean_neighbors": prof["mean_neighbors"], "graph_steps": args.graph_steps,
-                   "waves_per_tile": args.waves, "chunk_order": args.chunk_order, "fused": args.fused, "split_tiles": args.split, "tile_priority": args.prio, "subtiles": args.subtiles, "scan_mb": args.scan_mb, "start_window_value": start_rate, "finite": finite,
-                   "contacts_update_ms": contacts_ms, "contacts_distinct_pairs_22_updates": contacts_distinct},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(),
-                     "kernel": "k_force<kModeStep>", "force_ms": force_ms, "cell_ms": prof["cell_ms"],
-                     "tail_ms": prof["tail_ms"], "bytes_per_launch": n * BYTES_PER_UPDATE},
-        "cpu_baseline": cpu,
-    }
-    print(json.dumps(line), flush=True)
-    for e in engines:
-        e.close()
-    if dist is not None:
-        dist.destroy_process_group()
+        return 0
+    replica_main(args)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -7,38 +7,41 @@
  * as reference file:line (paths relative to src/simulation/ of the reference).
  *
  *   md::system{add_particle, view_mobilities, add_attribute}   -> gcs_engine_create
- *       stage_interphase/simulation_driver_particles.cpp:9-35, stage_anatelophase/simulation_driver.cpp:57-64
+ *       stage_interphase/simulation_driver_particles.cpp:9-35; stage_anatelophase/simulation_driver.cpp:53-64
  *   md::make_neighbor_pairwise_forcefield(a*softcore<2,3> + b*softcore<8,3>)
  *                                                              -> gcs_add_neighbor_softcore
- *       stage_interphase/simulation_driver_forcefield.cpp:21-53; stage_anatelophase/simulation_driver.cpp:123-137;
- *       stage_prometaphase/simulation_driver.cpp:99-111
+ *       stage_interphase/simulation_driver_forcefield.cpp:21-53; stage_anatelophase/simulation_driver.cpp:77-91;
+ *       stage_prometaphase/simulation_driver.cpp:51-63
  *   md::make_neighbor_pairwise_forcefield(apply_cutoff(softwell<6>)).set_neighbor_targets
  *                                                              -> gcs_add_neighbor_softwell
- *       stage_interphase/simulation_driver_forcefield.cpp:168-185
+ *       stage_interphase/simulation_driver_forcefield.cpp:162-186
  *   md::make_bonded_pairwise_forcefield + add_bonded_range / add_bonded_pair
  *                                                              -> gcs_add_bonded_pairwise
- *       stage_interphase/simulation_driver_forcefield.cpp:56-160; stage_anatelophase/simulation_driver.cpp:145-163;
- *       stage_prometaphase/simulation_driver.cpp:114-166
+ *       stage_interphase/simulation_driver_forcefield.cpp:57-160; stage_anatelophase/simulation_driver.cpp:94-117;
+ *       stage_prometaphase/simulation_driver.cpp:66-76; stage_prometaphase/simulation_driver.cpp:100-118
  *   md::make_bonded_triplewise_forcefield(cosine_bending_potential) -> gcs_add_bonded_triplewise
- *       stage_anatelophase/simulation_driver.cpp:165-187; stage_prometaphase/simulation_driver.cpp:126-144
+ *       stage_anatelophase/simulation_driver.cpp:119-145; stage_prometaphase/simulation_driver.cpp:78-96
  *   md::make_ellipsoid_inward_forcefield / make_ellipsoid_outward_forcefield (+ stats.axial_reaction)
  *                                                              -> gcs_add_ellipsoid_inward / _outward
  *       stage_interphase/simulation_driver_forcefield.cpp:189-244
  *   md::make_point_source_forcefield(semispring | force_flux_potential) -> gcs_add_point_source
- *       stage_anatelophase/simulation_driver.cpp:221-235; stage_prometaphase/simulation_driver.cpp:210-230;
+ *       stage_anatelophase/simulation_driver.cpp:176-189; stage_prometaphase/simulation_driver.cpp:162-182;
  *       common/potentials/force_flux_potential.hpp:19-37
  *   kinetochore_fiber_forcefield (custom md::forcefield)       -> gcs_add_kinetochore_fiber
- *       common/forcefield/kinetochore_fiber_forcefield.{hpp:8-30, cpp:9-84}
+ *       common/forcefield/kinetochore_fiber_forcefield.hpp:8-30; common/forcefield/kinetochore_fiber_forcefield.cpp:9-84;
+ *       used at stage_anatelophase/simulation_driver.cpp:149-172; stage_prometaphase/simulation_driver.cpp:121-159
  *   md::system::remove_forcefield                             -> gcs_remove_forcefield
  *       stage_anatelophase/simulation_driver.cpp:277-285 (anaphase -> telophase swap)
  *   md::system::view_positions (read/write)                    -> gcs_engine_set_positions / _get_positions
- *       stage_interphase/simulation_driver_relaxation.cpp:14-23; simulation_driver_interphase.cpp:34
+ *       stage_interphase/simulation_driver_relaxation.cpp:14-23; stage_interphase/simulation_driver_interphase.cpp:34
  *   md::system::compute_energy / compute_potential_energy      -> gcs_engine_compute_energy
- *       stage_interphase/simulation_driver_interphase.cpp:24-27; stage_prometaphase/simulation_driver.cpp:299
+ *       stage_interphase/simulation_driver_interphase.cpp:24-27; stage_anatelophase/simulation_driver.cpp:325;
+ *       stage_prometaphase/simulation_driver.cpp:251
  *   md::simulate_brownian_dynamics(system, {T, dt, spacestep, steps, seed, callback})
  *                                                              -> gcs_engine_run (+ gcs_engine_set_schedule)
- *       stage_interphase/simulation_driver_interphase.cpp:57-63; simulation_driver_relaxation.cpp:48-55;
- *       stage_anatelophase/simulation_driver.cpp:308-314, 349-355; stage_prometaphase/simulation_driver.cpp:278-284
+ *       stage_interphase/simulation_driver_interphase.cpp:57-63; stage_interphase/simulation_driver_relaxation.cpp:48-55;
+ *       stage_anatelophase/simulation_driver.cpp:262-268; stage_anatelophase/simulation_driver.cpp:303-309;
+ *       stage_prometaphase/simulation_driver.cpp:230-236
  *     The per-step callback's force-field mutations (update_core_scale, update_wall_semiaxes,
  *     stage_interphase/simulation_driver_interphase.cpp:67-90) run ON DEVICE via gcs_schedule; the host
  *     regains control only at interval boundaries (logging / sampling / contact map).
@@ -95,10 +98,10 @@ typedef struct gcs_system_desc {
 
 /* Neighbor-pairwise soft-core repulsion: U_ij = a_ij*SC<2,3>(r) + b_ij*SC<8,3>(r),
  * SC<p,q>(r) = eps (1 - (r/sigma)^p)^q for r < sigma.
- * mix = 1: a_ij = (a_i + a_j)/2, b_ij = (b_i + b_j)/2 (simulation_driver_forcefield.cpp:34-35);
+ * mix = 1: a_ij = (a_i + a_j)/2, b_ij = (b_i + b_j)/2 (stage_interphase/simulation_driver_forcefield.cpp:34-35);
  * mix = 0: a_ij = 1, b_ij = 0 (plain softcore<2,3>, mitotic stages).
  * scaled = 1: both diameters and neighbor_distance are multiplied by the context core_scale
- * (simulation_driver_forcefield.cpp:39-43, 49-51). */
+ * (stage_interphase/simulation_driver_forcefield.cpp:39-43, 49-51). */
 typedef struct gcs_softcore_params {
     double a_energy, a_diameter;
     double b_energy, b_diameter;
@@ -108,7 +111,7 @@ typedef struct gcs_softcore_params {
 } gcs_softcore_params;
 
 /* Bonded pairwise potential. mix = 1: K = a*a_spring + b*b_spring, l = a*a_length + b*b_length with
- * a, b the pair means of the ab factors (simulation_driver_forcefield.cpp:65-76); mix = 0: K = a_spring,
+ * a, b the pair means of the ab factors (stage_interphase/simulation_driver_forcefield.cpp:65-76); mix = 0: K = a_spring,
  * l = a_length.  scaled = 1: K /= s^2 and l *= s with s the context bond_scale (:81-83, :147-149). */
 typedef struct gcs_bond_params {
     int32_t potential; /* GCS_POT_SEMISPRING | GCS_POT_HARMONIC | GCS_POT_SPRING */
@@ -120,7 +123,7 @@ typedef struct gcs_bond_params {
 } gcs_bond_params;
 
 /* Droplet attraction among a target subset: apply_cutoff(softwell<exponent>{energy, decay}, cutoff),
- * U = -energy / (1 + (r/decay)^exponent) for r < cutoff (simulation_driver_forcefield.cpp:173-185). */
+ * U = -energy / (1 + (r/decay)^exponent) for r < cutoff (stage_interphase/simulation_driver_forcefield.cpp:173-185). */
 typedef struct gcs_softwell_params {
     double energy;
     double decay_distance;
@@ -131,7 +134,7 @@ typedef struct gcs_softwell_params {
 
 /* Ellipsoid wall inward field: per-particle a = (a_i + wall_a)/2, b = (b_i + wall_b)/2 and
  * a*SC<2,3>(a_energy, a_diameter) + b*SC<8,3>(b_energy, b_diameter) of the distance to the wall
- * (simulation_driver_forcefield.cpp:203-225). Diameters are passed already halved (the reference
+ * (stage_interphase/simulation_driver_forcefield.cpp:203-225). Diameters are passed already halved (the reference
  * uses a_core_diameter / 2); scaled multiplies them by core_scale.  The ellipsoid is centred at
  * `center` with semiaxes taken from the context (:194-201). */
 typedef struct gcs_wall_params {
@@ -266,7 +269,7 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
                        gcs_profile* out);
 
 /* Contact map (replaces contact_map::update / accumulate / clear, stage_interphase/contact_map.cpp:28-85, driven
- * from simulation_driver_interphase.cpp:38-45).  update: count every pair i < j of the CURRENT positions closer
+ * from stage_interphase/simulation_driver_interphase.cpp:38-45).  update: count every pair i < j of the CURRENT positions closer
  * than `distance` (strict fp32 predicate, as gcs_engine_search_neighbors) into the engine's device hash map;
  * enqueued on the engine stream, no host synchronisation (call it between gcs_engine_run chunks).
  * read: the accumulated (i, j, count) triples sorted by (i, j) into ijc[count][3] (count = distinct pairs;
@@ -292,7 +295,7 @@ int gcs_engine_sample_positions(gcs_engine* e, float* xyz, int64_t n, int32_t fr
  * halo, |= 2 a band over cap) -> exchange -> gcs_engine_domain_unpack(received buffers).  All calls only
  * enqueue on the engine stream (gcs_engine_stream), so the caller's collectives can be ordered on it too.
  * Replaces nothing in the reference (single-threaded); the per-step callback order is kept (wall update after
- * the force evaluation of the step, simulation_driver_interphase.cpp:51-52, 80-90). */
+ * the force evaluation of the step, stage_interphase/simulation_driver_interphase.cpp:51-52, 80-90). */
 int gcs_engine_set_domain(gcs_engine* e, double lo, double hi, double halo, const double* peer_regions,
                           int32_t npeer);
 /* Shared particles: fresh on every domain every step (carried in the reaction allreduce, which then holds

@@ -702,7 +702,7 @@ void gcso_compute_forces(gcso_system* s, double* forces)
 
 /* ------------------------------------------------------------------------------------------------ */
 /* Brownian dynamics (md::simulate_brownian_dynamics, INFERRED Euler-Maruyama form; seed plumbing    */
-/* PINNED at simulation_driver_interphase.cpp:57-63 / relaxation.cpp:48-55)                          */
+/* PINNED at simulation_driver_interphase.cpp:57-63 / simulation_driver_relaxation.cpp:48-55)                          */
 
 int gcso_run(gcso_system* s, const gcs_bd_config* cfg, int64_t first_step, int64_t steps)
 {

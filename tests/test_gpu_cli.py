@@ -13,8 +13,8 @@ from gcs.config import SimulationConfig
 pytestmark = pytest.mark.gpu
 
 
-def _prepare(path, master_seed, cfg):
-    """`prepare -s seed -o path config.json chains.tsv` with the synthetic C2 chains written as a TSV"""
+def _inputs(path, master_seed, cfg):
+    """config.json + chains.tsv (the synthetic C2 chains) next to `path`"""
     from gcs.config import format_simulation_config
     d = synthetic.make_c2(master_seed)
     tags = {1: "A", 2: "B", 3: "u", 4: "cen", 5: "anor", 6: "bnor", 0: ""}
@@ -26,6 +26,12 @@ def _prepare(path, master_seed, cfg):
     cj, ct = path.with_suffix(".json"), path.with_suffix(".tsv")
     cj.write_text(format_simulation_config(cfg))
     ct.write_text("\n".join(rows) + "\n")
+    return d, cj, ct
+
+
+def _prepare(path, master_seed, cfg):
+    """`prepare -s seed -o path config.json chains.tsv` with the synthetic C2 chains written as a TSV"""
+    d, cj, ct = _inputs(path, master_seed, cfg)
     cli.main(["prepare", "-s", str(master_seed), "-o", str(path), str(cj), str(ct)])
     a = mitotic.anatelophase_design(d, cfg.mitotic_phase)
     pm = mitotic.prometaphase_design(a, cfg.mitotic_phase, master_seed)
@@ -72,3 +78,41 @@ def test_cell_cycle_through_the_store(tmp_path):
         st.set_stage("anaphase")
         x0 = st.load_positions(0)  # the transition's structure was used (no rods)
         assert x0.shape == (a.n, 3) and np.isfinite(st.load_positions(50)).all()
+
+
+def test_scripts_simulate_argv(tmp_path):
+    """The four stage calls of the reference's scripts/simulate:44-47, with its exact argv, at the paths it uses
+    (<project>/src/simulation/<stage>): prepare -s seed -o out.h5 config.json chains.tsv; anatelophase out.h5;
+    transition interphase out.h5; interphase out.h5.  Step counts come from the config, as in the reference."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    stage = root / "src" / "simulation"
+    cfg = SimulationConfig()
+    cfg.mitotic_phase = dataclasses.replace(cfg.mitotic_phase, anaphase_steps=60, telophase_steps=40,
+                                            sampling_interval=20, logging_interval=20)
+    cfg.interphase = dataclasses.replace(cfg.interphase, relaxation_steps=100, steps=200,
+                                         relaxation_sampling_interval=50, relaxation_logging_interval=50,
+                                         sampling_interval=100, logging_interval=100, contactmap_output_window=2)
+    out = tmp_path / "out.h5"
+    d, cj, ct = _inputs(out, 7, cfg)
+    env = dict(__import__("os").environ, GCS_PYTHON=sys.executable)
+    calls = [[str(stage / "prepare"), "-s", "7", "-o", str(out), str(cj), str(ct)],
+             [str(stage / "anatelophase"), str(out)],
+             [str(stage / "transition"), "interphase", str(out)],
+             [str(stage / "interphase"), str(out)]]
+    for argv in calls:
+        p = subprocess.run(argv, capture_output=True, text=True, env=env, timeout=300)
+        assert p.returncode == 0, (argv, p.stderr[-2000:])
+    with store.SimulationStore(out) as st:
+        st.set_stage("telophase")
+        assert st.load_steps() == [0, 20, 40]
+        st.set_stage("relaxation")
+        assert st.load_steps() == [0, 50, 100]
+        st.set_stage("interphase")
+        assert st.load_steps() == [0, 100, 200]
+        x = st.load_positions(200)
+        assert x.shape == (d.n, 3) and np.isfinite(x).all()
+        c = st.load_contacts(200)
+        assert c.shape[0] > 0 and (c[:, 0] < c[:, 1]).all()

@@ -1,5 +1,5 @@
 """Mitotic stages (C3) on the CPU: prepare's coarse-graining (prepare.cpp:279-372), the libstdc++ normal stream of
-the anaphase initialisation (simulation_driver.cpp:25-32, pinned by the g++ fixtures), and the drivers' stage
+the anaphase initialisation (stage_anatelophase/simulation_driver.cpp:25-32, pinned by the g++ fixtures), and the drivers' stage
 order / field swap on the oracle backend."""
 import json
 from pathlib import Path

@@ -56,3 +56,27 @@ def test_prepare_cli_writes_the_store(tmp_path):
         assert len(a.chains) == 1 and a.chains[0][2] == d.chains[0][2] // cfg.mitotic_phase.coarse_graining
         st.set_stage("relaxation")
         assert not st.check_positions(0)  # prepare writes no structure (the anatelophase stage starts from rods)
+
+
+def test_prepare_launcher_at_the_reference_path(tmp_path):
+    """<project>/src/simulation/prepare with scripts/simulate:44's argv (a CPU stage: no device needed)."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    d = synthetic.make_c1()
+    (tmp_path / "config.json").write_text(format_simulation_config(SimulationConfig()))
+    (tmp_path / "chains.tsv").write_text(_tsv(d))
+    out = tmp_path / "out.h5"
+    env = dict(os.environ, GCS_PYTHON=sys.executable)
+    p = subprocess.run([str(root / "src" / "simulation" / "prepare"), "-s", "5", "-o", str(out),
+                        str(tmp_path / "config.json"), str(tmp_path / "chains.tsv")],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert p.returncode == 0, p.stderr
+    with store.SimulationStore(out) as st:
+        assert int(st.f.read_array("/metadata/master_seed", store.H5_U32)) == 5
+        assert st.load_interphase_design().n == d.n
+    bad = subprocess.run([str(root / "src" / "simulation" / "transition"), "interphase"], capture_output=True,
+                         text=True, env=env, timeout=120)
+    assert bad.returncode != 0  # usage errors surface as a failing status, like the reference's main
