@@ -102,14 +102,19 @@ def resolution_scaled(cfg: "InterphaseConfig", bin_ratio: float) -> "InterphaseC
     """The interphase force field for beads `bin_ratio` times finer than the 100 kb default (C5: 10 kb, ratio 10),
     rescaled so a bead's neighbourhood looks the same: every bead-scale length (core and droplet diameters, bond
     lengths, contact distance) x f, every bead-scale spring x f^-2, f = bin_ratio^(-1/3) (the bead volume is
-    bin_ratio times smaller).  Energies, mobilities, the wall and the schedule are unchanged.  The reference has
-    no 10 kb configuration of its own (simulation_config.hpp:61-115 are the 100 kb defaults); this is the
-    benchmark's stated choice (DESIGN.md "Measurement")."""
+    bin_ratio times smaller).  The timestep x f^2: with springs x f^-2 the explicit Euler-Maruyama update keeps
+    the same k mu dt (the 10 kb soft core's stiffest pairs reach k mu dt ~ 1.6 at the 100 kb timestep, where
+    the fp64 reference itself amplifies a 1-ulp perturbation of the start to 3e-2 in 10 steps -- DESIGN.md §6);
+    the Brownian time sigma^2 / D of a bead scales the same way.  Energies, mobilities, the wall and the schedule
+    (in time units) are unchanged.  The reference has no 10 kb configuration of its own
+    (common/simulation_config.hpp:61-115 are the 100 kb defaults); this is the benchmark's stated choice
+    (DESIGN.md "Measurement")."""
     import dataclasses
     f = bin_ratio ** (-1.0 / 3.0)
     k = f ** -2
     return dataclasses.replace(
         cfg,
+        timestep=cfg.timestep * f * f,
         a_core_diameter=cfg.a_core_diameter * f, b_core_diameter=cfg.b_core_diameter * f,
         a_core_bond_length=cfg.a_core_bond_length * f, b_core_bond_length=cfg.b_core_bond_length * f,
         a_core_bond_spring=cfg.a_core_bond_spring * k, b_core_bond_spring=cfg.b_core_bond_spring * k,

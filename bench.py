@@ -330,12 +330,12 @@ def decomp_main(args):
     tr = D.DistTransport(doms[0], dist) if world > 1 else D.LocalTransport(doms)
     run = D.DecomposedRun(doms, tr)
     seed = replica_noise_seed(0)
-    run.run(args.warmup, first_step=window, seed=seed)
+    run.run(args.warmup, first_step=window, seed=seed, timestep=cfg.timestep)
     for d in doms:
         d.synchronize()
     barrier(dist)
     t0 = time.perf_counter()
-    run.run(args.steps, first_step=window + args.warmup, seed=seed)
+    run.run(args.steps, first_step=window + args.warmup, seed=seed, timestep=cfg.timestep)
     for d in doms:
         d.synchronize()
     el = time.perf_counter() - t0
@@ -370,6 +370,7 @@ def replica_main(args):
         from gcs import _abi as A
         A.load()  # this rank's engine runtime (no torch HIP runtime in replica runs)
     cfg = bench_config(args.config)
+    bd = {"temperature": cfg.temperature, "timestep": cfg.timestep}  # md::brownian_dynamics_config of the stage
     maker = design_maker(args.config)
     R = max(1, args.replicas_per_gpu)
     K = max(1, args.steps)
@@ -411,26 +412,27 @@ def replica_main(args):
         for s0 in range(0, steps, chunk):
             c = min(chunk, steps - s0)
             for k, (e, sd) in enumerate(zip(engines, seeds)):
-                e.run(c, first_step=nxt[k], seed=sd)
+                e.run(c, first_step=nxt[k], seed=sd, **bd)
                 nxt[k] += c
         for e in engines:
             e.synchronize()
 
+    run_all(max(G, 1))  # first chunk: every engine captures and instantiates its graph
     t0 = time.perf_counter()
-    run_all(warm)
+    run_all(warm)  # steady-state warm-up, timed only to size the passes below
     warm_s = time.perf_counter() - t0
 
     # one trajectory alone on the GPU (replica 0; the others are independent and idle meanwhile), its own window
     single_rate = None
     if R > 1 and rank == 0:
         k1 = G if G > 0 else 64
-        eng.run(k1, first_step=nxt[0], seed=seed)  # (graph already instantiated by the warm-up)
+        eng.run(k1, first_step=nxt[0], seed=seed, **bd)  # (graph already instantiated by the warm-up)
         eng.synchronize()
         nxt[0] += k1
         reps = 0
         t1 = time.perf_counter()
         while True:  # >= half the headline window, in blocks of 8 graph replays
-            eng.run(k1, first_step=nxt[0], seed=seed)
+            eng.run(k1, first_step=nxt[0], seed=seed, **bd)
             nxt[0] += k1
             reps += 1
             if reps % 8 == 0:
@@ -458,7 +460,7 @@ def replica_main(args):
     after = nxt[0]
 
     # per-kernel durations with HIP events on the engine's stream (replica 0 alone, after the timed region)
-    prof = eng.profile(args.profile_steps, first_step=after, seed=seed)
+    prof = eng.profile(args.profile_steps, first_step=after, seed=seed, **bd)
     force_ms = prof["force_ms"]
     achieved = n * BYTES_PER_UPDATE / (force_ms * 1e-3) / 1e9
     ctx = eng.get_context()
@@ -478,7 +480,7 @@ def replica_main(args):
             eng.synchronize()
             t1 = time.perf_counter()
             for _ in range(k):
-                eng.run(20, first_step=at, seed=seed)
+                eng.run(20, first_step=at, seed=seed, **bd)
                 at += 20
                 if with_update:
                     eng.contacts_update(dcon)
@@ -496,11 +498,11 @@ def replica_main(args):
         if rank == 0 and not args.no_start_window:
             e0 = make_engine(design, cfg, local, 0)
             e0.set_option(A.OPT_GRAPH_STEPS, G)
-            e0.run(max(64, 2 * G), first_step=0, seed=seed)
+            e0.run(max(64, 2 * G), first_step=0, seed=seed, **bd)
             e0.synchronize()
             k0 = max(256, K // 4)
             t1 = time.perf_counter()
-            e0.run(k0, first_step=max(64, 2 * G), seed=seed)
+            e0.run(k0, first_step=max(64, 2 * G), seed=seed, **bd)
             e0.synchronize()
             start_rate = n * k0 / (time.perf_counter() - t1)
             e0.close()
@@ -532,7 +534,7 @@ def replica_main(args):
         "data": "synthetic" if not args.stub_engine else "stub",
         "steps_requested": K,
         "passes": passes,
-        "warmup_steps_run": warm,
+        "warmup_steps_run": warm + max(G, 1),
         "timed_s": el_max,
         "per_rank_values": rank_values,
         "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, {R} independent "
