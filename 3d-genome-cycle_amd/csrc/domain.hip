@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void k_domain_pack(const DevCtx* __restrict__ 
         bool far = false;
         for (int q = a.boff[i]; q < a.boff[i + 1]; ++q) {
             const int2 en = a.bent[q];
-            if (a.bpar[en.y].type == kSoftwell) continue;  // cut off below the halo (droplet): a pair term
+            if ((en.y & 15) == kSoftwell) continue;  // cut off below the halo (droplet): a pair term
             if (shared && shared[en.x]) continue;          // shared particles are fresh everywhere
             const float4 pj = pold[en.x];
             const float dx = po.x - pj.x, dy = po.y - pj.y, dz = po.z - pj.z;

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -111,7 +112,8 @@ struct gcs_engine {
     // topology tables
     int* boff = nullptr;
     int2* bent = nullptr;
-    BondParam* bpar = nullptr;
+    float4* bval = nullptr;
+    int* sw_idx = nullptr;  // droplet targets (<= 64)
     float* bend_eps = nullptr;
     int* toff = nullptr;
     Tether* tent = nullptr;
@@ -163,7 +165,7 @@ struct gcs_engine {
     // options / graph cache
     int graph_steps = 32;
     int waves = 4;
-    int fused = 2;  // GCS_OPT_FUSED_STEP: 2 = the 2-launch rebuild step, 1 = the 4-launch step, 0 = unfused
+    int fused = 3;  // GCS_OPT_FUSED_STEP: 3 = the list step, 2 = the 2-launch rebuild step, 1 = the 4-launch step, 0 = unfused
     bool scan_mb = true;  // GCS_OPT_SCAN_BLOCKS: multi-block cell scan (the heavy-tile split keeps one block)
     hipGraphExec_t gexec = nullptr;
     hipGraph_t graph = nullptr;
@@ -171,6 +173,24 @@ struct gcs_engine {
     gcs_bd_config g_cfg{};
     int g_sched_flags = -1;
     int g_fused = -1, g_chunk = -1;
+
+    // list step (GCS_OPT_FUSED_STEP 3): neighbour lists, pair-factor classes, rebuild period
+    int* list = nullptr;
+    int* lcount = nullptr;
+    float4* psort[2] = {nullptr, nullptr};
+    int* ptype = nullptr;
+    unsigned* lticket = nullptr;  // list step: two-level arrival counters + group rows
+    float* lgroup = nullptr;
+    float2* type_ab = nullptr;
+    int ntypes = 0;
+    bool list_ok = false;       // the system admits the list step (a pair field, <= 256 classes, N < 2^24)
+    int list_cap = 64;          // GCS_OPT_LIST_CAP: entries per (particle, wave) segment
+    size_t list_alloc = 0;      // allocated entries
+    int list_skin_pm = 400;     // GCS_OPT_LIST_SKIN: skin in 1/1000 of the pair cutoff
+    int list_every_opt = 0;     // GCS_OPT_LIST_EVERY: rebuild period in steps (0: from the noise amplitude)
+    int list_every = 1;         // the period of the current run
+    bool l_need_build = true;   // the next list step must rebuild (run start without continuity)
+    int g_list_every = -1;
 
     // fused-step continuity: after a fused run the cells of the next positions are already binned with the
     // grid the next step expects, so a run that continues at chain_step skips re-priming (bitwise identical
@@ -221,6 +241,9 @@ int compile(gcs_engine* e)
     std::vector<float> bend(n, 0.f);
     std::vector<std::vector<Tether>> tlist(n);
     int pair_mix = 1;
+    bool sw_done = false;
+    std::vector<int> sw_idx;
+    a.sw_n = 0;
 
     for (const FieldRec& f : e->fields) {
         switch (f.kind) {
@@ -238,6 +261,15 @@ int compile(gcs_engine* e)
             a.pair_dist = (float)f.sc.neighbor_distance;
             break;
         case F_SOFTWELL: {
+            if (!sw_done && f.idx.size() <= 64) {  // the wave-cooperative droplet (local_terms)
+                sw_done = true;
+                a.sw_n = (int)f.idx.size();
+                a.sw_ka = (float)f.sw.energy;
+                a.sw_kb = (float)(1.0 / (f.sw.decay_distance * f.sw.decay_distance));
+                a.sw_la = (float)(f.sw.cutoff * f.sw.cutoff);
+                sw_idx.assign(f.idx.begin(), f.idx.end());
+                break;
+            }
             BondParam bp{};
             bp.type = kSoftwell;
             bp.ka = (float)f.sw.energy;
@@ -333,12 +365,49 @@ int compile(gcs_engine* e)
     // per-particle constants {mu, a, b, 0}
     std::vector<float4> hk(n);
     for (int i = 0; i < n; ++i) hk[i] = make_float4((float)e->mu[i], (float)e->ab[2 * i], (float)e->ab[2 * i + 1], 0.f);
+    for (int t : sw_idx) hk[t].w = 1.f;  // droplet target
+    dfree(e->sw_idx);
+    if (a.sw_n > 0) {
+        int rc;
+        if ((rc = dalloc(&e->sw_idx, 64))) return rc;
+        HIPCHK(hipMemcpyAsync(e->sw_idx, sw_idx.data(), sw_idx.size() * sizeof(int), hipMemcpyHostToDevice, e->stream));
+    }
+    a.sw_idx = e->sw_idx;
     HIPCHK(hipMemcpyAsync(e->kmu, hk.data(), n * sizeof(float4), hipMemcpyHostToDevice, e->stream));
-    (void)pair_mix;
+
+    // list step: pair-factor classes (the (a, b) the pair field mixes; k_cell_sort's spos.w / sb)
+    std::vector<int> pt(n, 0);
+    std::vector<float2> tab;
+    {
+        std::map<std::pair<float, float>, int> cls;
+        bool ok = a.has_pair && n > 0 && n < (1 << kListIndexBits);
+        for (int i = 0; ok && i < n; ++i) {
+            const std::pair<float, float> key = pair_mix ? std::make_pair(hk[i].y, hk[i].z) : std::make_pair(1.f, 0.f);
+            auto it = cls.find(key);
+            if (it == cls.end()) {
+                if ((int)cls.size() >= kMaxTypes) {
+                    ok = false;
+                    break;
+                }
+                it = cls.emplace(key, (int)cls.size()).first;
+                tab.push_back(make_float2(key.first, key.second));
+            }
+            pt[i] = it->second;
+        }
+        e->list_ok = ok;
+        e->ntypes = ok ? (int)tab.size() : 0;
+        if (ok) {
+            int rc;
+            if (!e->ptype && (rc = dalloc(&e->ptype, n))) return rc;
+            if (!e->type_ab && (rc = dalloc(&e->type_ab, kMaxTypes))) return rc;
+            HIPCHK(hipMemcpyAsync(e->ptype, pt.data(), n * sizeof(int), hipMemcpyHostToDevice, e->stream));
+            HIPCHK(hipMemcpyAsync(e->type_ab, tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice, e->stream));
+        }
+    }
 
     dfree(e->boff);
     dfree(e->bent);
-    dfree(e->bpar);
+    dfree(e->bval);
     dfree(e->bend_eps);
     dfree(e->toff);
     dfree(e->tent);
@@ -348,19 +417,39 @@ int compile(gcs_engine* e)
     if (nb > 0) {
         std::vector<int> off(n + 1, 0);
         std::vector<int2> ent;
+        std::vector<float4> val;
         ent.reserve(nb);
+        val.reserve(nb);
         for (int i = 0; i < n; ++i) {
             off[i] = (int)ent.size();
-            ent.insert(ent.end(), blist[i].begin(), blist[i].end());
+            for (const int2& b : blist[i]) {
+                const BondParam& bp = params[b.y];
+                const int j = b.x;
+                float4 v = make_float4(bp.ka, bp.kb, bp.la, 0.f);
+                if (bp.type != kSoftwell) {
+                    // simulation_driver_forcefield.cpp:71-76: K = a k_a + b k_b, l = a l_a + b l_b with the pair's
+                    // mean factors a = (a_i + a_j) / 2, b = (b_i + b_j) / 2 (mix), else k_a, l_a
+                    double K = bp.ka, l = bp.la;
+                    if (bp.mix) {
+                        const double A = 0.5 * (e->ab[2 * i] + e->ab[2 * j]), B = 0.5 * (e->ab[2 * i + 1] + e->ab[2 * j + 1]);
+                        K = A * bp.ka + B * bp.kb;
+                        l = A * bp.la + B * bp.lb;
+                    }
+                    v = make_float4((float)K, (float)l, 0.f, 0.f);
+                }
+                ent.push_back(make_int2(j, bp.type | (bp.scaled ? 16 : 0)));
+                val.push_back(v);
+            }
         }
         off[n] = (int)ent.size();
         int rc;
         if ((rc = dalloc(&e->boff, n + 1))) return rc;
         if ((rc = dalloc(&e->bent, ent.size()))) return rc;
-        if ((rc = dalloc(&e->bpar, params.size()))) return rc;
+        if ((rc = dalloc(&e->bval, val.size()))) return rc;
         HIPCHK(hipMemcpyAsync(e->boff, off.data(), (n + 1) * sizeof(int), hipMemcpyHostToDevice, e->stream));
         HIPCHK(hipMemcpyAsync(e->bent, ent.data(), ent.size() * sizeof(int2), hipMemcpyHostToDevice, e->stream));
-        HIPCHK(hipMemcpyAsync(e->bpar, params.data(), params.size() * sizeof(BondParam), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipMemcpyAsync(e->bval, val.data(), val.size() * sizeof(float4), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));  // val / ent die at the end of this block
         a.has_bonds = 1;
     }
     bool any_bend = false;
@@ -390,7 +479,7 @@ int compile(gcs_engine* e)
     }
     a.boff = e->boff;
     a.bent = e->bent;
-    a.bpar = e->bpar;
+    a.bval = e->bval;
     a.bend_eps = e->bend_eps;
     a.toff = e->toff;
     a.tent = e->tent;
@@ -476,8 +565,89 @@ void enqueue_cells(gcs_engine* e)
     enqueue_sort(e);
 }
 
+bool list_path(const gcs_engine* e, bool spacestep) { return e->fused == 3 && e->list_ok && !spacestep; }
 bool fused_path(const gcs_engine* e, bool spacestep) { return e->fused != 0 && !spacestep; }
-bool rebuild_path(const gcs_engine* e, bool spacestep) { return e->fused == 2 && !spacestep; }
+bool rebuild_path(const gcs_engine* e, bool spacestep)
+{
+    // the list step falls back to the rebuild step when the system does not admit lists
+    return (e->fused == 2 || (e->fused == 3 && !e->list_ok)) && !spacestep;
+}
+
+float list_skin(const gcs_engine* e) { return 1e-3f * (float)e->list_skin_pm * e->fa.pair_dist; }
+
+// the list step's argument block: the shared one plus the lists and the skin (> 0 also makes the prime and the
+// tail build cell grids at cutoff + skin, so only list-path launches get it)
+ForceArgs list_args(const gcs_engine* e)
+{
+    ForceArgs a = e->fa;
+    a.list = e->list;
+    a.lcount = e->lcount;
+    a.ptype = e->ptype;
+    a.psort0 = e->psort[0];
+    a.psort1 = e->psort[1];
+    a.lticket = e->lticket;
+    a.lgroup = e->lgroup;
+    a.type_ab = e->type_ab;
+    a.ntypes = e->ntypes;
+    a.list_cap = e->list_cap;
+    a.list_stride = (e->n + 63) & ~63;
+    a.list_skin = list_skin(e);
+    return a;
+}
+
+int ensure_list(gcs_engine* e)
+{
+    const size_t stride = (size_t)((e->n + 63) & ~63);
+    const size_t need = stride * kListWaves * (size_t)e->list_cap;
+    if (need <= e->list_alloc && e->lcount) return GCS_OK;
+    dfree(e->list);
+    dfree(e->lcount);
+    dfree(e->psort[0]);
+    dfree(e->psort[1]);
+    e->list_alloc = 0;
+    int rc;
+    if ((rc = dalloc(&e->list, need)) || (rc = dalloc(&e->lcount, stride * kListWaves)) ||
+        (rc = dalloc(&e->psort[0], stride)) || (rc = dalloc(&e->psort[1], stride)))
+        return rc;
+    if (!e->lticket) {
+        if ((rc = dalloc(&e->lticket, 32 * 9)) || (rc = dalloc(&e->lgroup, 8 * 24))) return rc;
+        HIPCHK(hipMemsetAsync(e->lticket, 0, 32 * 9 * sizeof(unsigned), e->stream));
+    }
+    // entries past a slot's count are read (never gathered): keep them defined
+    HIPCHK(hipMemsetAsync(e->list, 0, need * sizeof(int), e->stream));
+    e->list_alloc = need;
+    return GCS_OK;
+}
+
+// rebuild period: the skin must hold the largest displacement of ~6 sigma on each side of a pair for that many
+// steps (sigma = sqrt(2 T mu_max dt) per step); a particle that outruns it anyway is searched exactly (k_lstep)
+int auto_list_every(const gcs_engine* e, const gcs_bd_config* cfg)
+{
+    if (e->list_every_opt > 0) return e->list_every_opt;
+    double mu = 0;
+    for (double m : e->mu) mu = std::max(mu, m);
+    const double sigma = std::sqrt(2.0 * std::max(cfg->temperature, 0.0) * mu * cfg->timestep);
+    const double half = 0.5 * (double)list_skin(e);
+    if (!(sigma > 0)) return 64;
+    const double m = std::floor((half / (6.0 * sigma)) * (half / (6.0 * sigma)));
+    return (int)std::min(64.0, std::max(1.0, m));
+}
+
+// one list step: on a rebuild step the cell list at cutoff + skin (ctx->grid, set by the prime or the last
+// tail), the lists, then the step itself (forces + local terms + update + tail in the last workgroup)
+void enqueue_list_step(gcs_engine* e, bool build)
+{
+    const ForceArgs la = list_args(e);
+    if (build) {
+        launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], e->n, e->cell_of, e->slot, e->count);
+        enqueue_scan(e, false);
+        launch_cell_scatter(e->stream, e->n, e->cell_of, e->slot, e->cstart, e->tmp, e->count);
+        launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, e->n, e->tmp, e->cell_of, e->cstart,
+                         e->sidx, e->scell, e->spos, e->sb, e->fa.pair_mix, e->ptype, e->psort[0], e->psort[1]);
+        launch_list_build(e->stream, e->ctx, la);
+    }
+    launch_list_step(e->stream, e->ctx, la, e->sched_flags != 0);
+}
 int step_grid(const gcs_engine* e) { return e->fa.split ? force_grid_split(e->n) : force_grid(e->n); }
 
 // One BD step.  Rebuild (fixed timestep, 2 launches, default): force + update, which also files the new positions
@@ -566,7 +736,14 @@ int begin_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
     const bool fused = fused_path(e, cfg->spacestep > 0);
     const bool cont = fused && e->chain_valid && e->chain_step == first_step && e->chain_version == e->topo_version;
     e->chain_valid = false;
-    if (!cont) {
+    if (list_path(e, cfg->spacestep > 0)) {
+        if ((rc = ensure_list(e))) return rc;
+        e->list_every = auto_list_every(e, cfg);
+        if (!cont) {
+            launch_prime(e->stream, e->ctx, list_args(e), 0.f, e->ncell_max, e->dsched);
+            e->l_need_build = true;
+        }
+    } else if (!cont) {
         launch_prime(e->stream, e->ctx, a, 0.f, e->ncell_max, e->dsched);
         if (rebuild_path(e, cfg->spacestep > 0)) {
             enqueue_cells(e);  // the first cell list; the steps rebuild it from the force kernel's buckets
@@ -757,6 +934,15 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->pos[0]);
     dfree(e->pos[1]);
     dfree(e->kmu);
+    dfree(e->sw_idx);
+    dfree(e->list);
+    dfree(e->lcount);
+    dfree(e->psort[0]);
+    dfree(e->psort[1]);
+    dfree(e->lticket);
+    dfree(e->lgroup);
+    dfree(e->ptype);
+    dfree(e->type_ab);
     dfree(e->spos);
     dfree(e->sb);
     dfree(e->sidx);
@@ -786,7 +972,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->force_out);
     dfree(e->boff);
     dfree(e->bent);
-    dfree(e->bpar);
+    dfree(e->bval);
     dfree(e->bend_eps);
     dfree(e->toff);
     dfree(e->tent);
@@ -1105,7 +1291,44 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
 
     const int G = e->graph_steps;
     int64_t done = 0;
-    if (G > 0 && steps >= G) {
+    if (list_path(e, spacestep)) {
+        // rebuilds at the steps k with (first_step + k) % M == 0 and at a run start without continuity, so a run
+        // split into chunks rebuilds where the whole run does (bitwise identical); graphs hold GM steps from an
+        // aligned step, the rest runs eagerly
+        const int M = e->list_every;
+        const int GM = G > 0 ? M * ((G + M - 1) / M) : 0;
+        while (done < steps) {
+            const int64_t st = first_step + done;
+            const bool aligned = (st % M) == 0;
+            if (GM > 0 && !e->l_need_build && aligned && steps - done >= GM) {
+                const bool same = e->gexec && e->g_steps == GM && e->g_version == e->topo_version && e->g_fused == 3 &&
+                                  e->g_list_every == M && e->g_sched_flags == e->sched_flags &&
+                                  std::memcmp(&e->g_cfg, cfg, sizeof(*cfg)) == 0;
+                if (!same) {
+                    drop_graph(e);
+                    HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+                    for (int k = 0; k < GM; ++k) enqueue_list_step(e, k % M == 0);
+                    HIPCHK(hipStreamEndCapture(e->stream, &e->graph));
+                    HIPCHK(hipGraphInstantiate(&e->gexec, e->graph, nullptr, nullptr, 0));
+                    e->g_steps = GM;
+                    e->g_version = e->topo_version;
+                    e->g_fused = 3;
+                    e->g_list_every = M;
+                    e->g_sched_flags = e->sched_flags;
+                    e->g_cfg = *cfg;
+                    e->g_spacestep = 0;
+                    e->g_waves = e->waves;
+                    e->g_chunk = e->fa.chunk_mode;
+                }
+                for (; steps - done >= GM; done += GM) HIPCHK(hipGraphLaunch(e->gexec, e->stream));
+                continue;
+            }
+            enqueue_list_step(e, e->l_need_build || aligned);
+            e->l_need_build = false;
+            ++done;
+        }
+    }
+    if (G > 0 && steps - done >= G && !list_path(e, spacestep)) {
         const bool same = e->gexec && e->g_steps == G && e->g_waves == e->waves && e->g_version == e->topo_version &&
                           e->g_fused == (int)e->fused && e->g_chunk == e->fa.chunk_mode &&
                           e->g_spacestep == (int)spacestep && e->g_sched_flags == e->sched_flags &&
@@ -1552,11 +1775,31 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     for (auto& x : ev) HIPCHK(hipEventCreate(&x));
     const int fb = step_grid(e);
     HIPCHK(hipEventRecord(ev[0], e->stream));
-    const bool fused = fused_path(e, false), rebuild = rebuild_path(e, false);
+    const bool fused = fused_path(e, false), rebuild = rebuild_path(e, false), lst = list_path(e, false);
     // per step: [1] cells [2] force [3] fused: next-step scan / unfused: tail [4] fused: scatter + tail [5]
-    // (rebuild: [1] - [2] force [3] rebuild + tail [4] - [5])
+    // (rebuild: [1] - [2] force [3] rebuild + tail [4] - [5]; list: [1] cells + list build on rebuild steps
+    // [2] list step incl. its tail [3] - [4] - [5])
     for (int64_t k = 0; k < steps; ++k) {
         HIPCHK(hipEventRecord(ev[1 + 5 * k], e->stream));
+        if (dbg && k == steps - 1) e->fa.dbg_times = dbg;
+        if (lst) {
+            const bool build = e->l_need_build || ((first_step + k) % e->list_every) == 0;
+            e->l_need_build = false;
+            const ForceArgs la = list_args(e);
+            if (build) {
+                launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], e->n, e->cell_of, e->slot, e->count);
+                enqueue_scan(e, false);
+                launch_cell_scatter(e->stream, e->n, e->cell_of, e->slot, e->cstart, e->tmp, e->count);
+                launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, e->n, e->tmp, e->cell_of, e->cstart,
+                                 e->sidx, e->scell, e->spos, e->sb, e->fa.pair_mix, e->ptype, e->psort[0], e->psort[1]);
+                launch_list_build(e->stream, e->ctx, la);
+            }
+            HIPCHK(hipEventRecord(ev[2 + 5 * k], e->stream));
+            launch_list_step(e->stream, e->ctx, la, e->sched_flags != 0);
+            e->fa.dbg_times = nullptr;
+            for (int q = 3; q <= 5; ++q) HIPCHK(hipEventRecord(ev[q + 5 * k], e->stream));
+            continue;
+        }
         if (rebuild)
             ;
         else if (fused)
@@ -1588,7 +1831,9 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
         float t[4] = {0, 0, 0, 0};
         for (int q = 0; q < 4; ++q) HIPCHK(hipEventElapsedTime(&t[q], ev[1 + q + 5 * k], ev[2 + q + 5 * k]));
         force += t[1];
-        if (rebuild) {
+        if (lst) {
+            cell += t[0];  // cell list + list build (rebuild steps only)
+        } else if (rebuild) {
             cell += t[2];  // rebuild kernel (its tail block runs beside the cell-list blocks)
         } else if (fused) {
             cell += t[0] + t[2];  // sort + scan
@@ -1653,6 +1898,24 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     return GCS_OK;
 }
 
+int gcs_engine_get_list_stats(gcs_engine* e, gcs_list_stats* out)
+{
+    if (!e || !out) return fail(GCS_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(e->device));
+    DevCtx d;
+    HIPCHK(hipMemcpyAsync(&d, e->ctx, sizeof(d), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    out->active = (e->fused == 3 && e->list_ok) ? 1 : 0;
+    out->rebuild_every = e->list_every;
+    out->builds = d.lbuilds;
+    out->fallback_particle_steps = d.lfallback;
+    out->skin = list_skin(e);
+    out->max_displacement = d.ldisp;
+    out->pair_classes = e->ntypes;
+    out->capacity = e->list_cap;
+    return GCS_OK;
+}
+
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
 {
     if (!e) return fail(GCS_EINVAL, "null argument");
@@ -1669,8 +1932,26 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         drop_graph(e);
         return GCS_OK;
     }
+    if (option == GCS_OPT_LIST_SKIN) {
+        if (value < 1 || value > 4000) return fail(GCS_EINVAL, "list skin must be in [1, 4000] per mille of the cutoff");
+        e->list_skin_pm = (int)value;
+        drop_graph(e);
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_LIST_EVERY) {
+        if (value < 0 || value > 4096) return fail(GCS_EINVAL, "list rebuild period must be in [0, 4096] (0 = auto)");
+        e->list_every_opt = (int)value;
+        drop_graph(e);
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_LIST_CAP) {
+        if (value < 8 || value > 4096) return fail(GCS_EINVAL, "list capacity must be in [8, 4096]");
+        e->list_cap = (int)value;
+        drop_graph(e);
+        return GCS_OK;
+    }
     if (option == GCS_OPT_FUSED_STEP) {
-        if (value < 0 || value > 2) return fail(GCS_EINVAL, "fused step must be 0, 1 or 2");
+        if (value < 0 || value > 3) return fail(GCS_EINVAL, "fused step must be 0, 1, 2 or 3");
         e->fused = (int)value;
         drop_graph(e);
         return GCS_OK;

@@ -2,11 +2,11 @@
 //
 // HBM layout (fp32, 16-B aligned rows so every particle access is one dwordx4):
 //   pos[2][N]   float4 {x, y, z, 0}      double-buffered particle positions, particle order
-//   kmu[N]      float4 {mu, a, b, 0}     per-particle constants (mobility, A/B factors)
+//   kmu[N]      float4 {mu, a, b, t}     per-particle constants (mobility, A/B factors, t = 1: droplet target)
 //   spos[N]     float4 {x, y, z, a}      positions re-ordered by cell (rebuilt every step)
 //   sb[N], sidx[N], scell[N]             b factor, particle index and cell of each sorted slot
 //   cstart[ncell+1]                      first sorted slot of each cell (cell = x + nx (y + ny z))
-//   bonded CSR (boff/bent/bpar), bend_eps[N], tether CSR (toff/tent)   topology, particle order
+//   bonded CSR (boff/bent/bval), bend_eps[N], tether CSR (toff/tent)   topology, particle order
 //   DevCtx                               device-resident driver context + the current cell grid
 #pragma once
 
@@ -70,6 +70,14 @@ struct DevCtx {
     long long rb_step;
     int rb_parity;
     int pad4;
+    // list step (GCS_OPT_FUSED_STEP 3): the grid the neighbour lists were built on (its rc = build cutoff + skin),
+    // the build cutoff, the largest displacement of any particle from its build position (the last tail's
+    // reduction), cumulative list builds and fallback particle-steps (diagnostics)
+    Grid lgrid;
+    float lrc_b;
+    float ldisp;
+    long long lbuilds;
+    long long lfallback;
 };
 
 enum BondType : int { kSemispring = 0, kHarmonic = 1, kSpring = 2, kSoftwell = 3 };
@@ -93,7 +101,7 @@ struct WallIn {
     int mix, scaled;
 };
 
-enum Mode : int { kModeStep = 0, kModeForce = 1, kModeEnergy = 2 };
+enum Mode : int { kModeStep = 0, kModeForce = 1, kModeEnergy = 2, kModeList = 3 };  // kModeList: build the neighbour lists
 
 struct ForceArgs {
     int n;
@@ -114,7 +122,13 @@ struct ForceArgs {
     int has_bonds;
     const int* boff;
     const int2* bent;
-    const BondParam* bpar;
+    const float4* bval;  // per CSR entry: {K, l, 0, 0} (A/B mixed at compile), softwell {energy, 1/decay^2, cutoff^2, 0};
+                         // bent[q] = {partner, type | scaled << 4}
+    // the nucleolar droplet (a softwell among <= 64 targets): evaluated wave-cooperatively (local_terms), not
+    // through the bond CSR; targets carry kmu[i].w = 1
+    int sw_n;
+    const int* sw_idx;
+    float sw_ka, sw_kb, sw_la;  // energy, 1 / decay^2, cutoff^2
     // bending
     int has_bend;
     const float* bend_eps;
@@ -172,7 +186,30 @@ struct ForceArgs {
     int dom_on;
     float dom_lo, dom_hi, dom_halo;
     const double* ext_react;  // != nullptr: the step's wall reaction summed over all domains (allreduced), [6]
+    // list step (GCS_OPT_FUSED_STEP 3; DESIGN.md "The list step"): per sorted slot s and wave w (w < 4) the
+    // sorted slots of the pair partners found within build cutoff + list_skin are
+    // list[(w * list_cap + k) * list_stride + s], k < count, count = lcount[w * list_stride + s] & kListCountMask
+    // (bit 30: some wave of the slot overflowed list_cap).  psort[2]: the current positions in sorted-slot order
+    // (ping-pong with ctx->parity), .w = particle | class << 24 (class: the (a, b) pair factors, type_ab[class]).
+    int* list;
+    int* lcount;
+    const int* ptype;       // [N] pair-factor class of each particle
+    float4* psort0;
+    float4* psort1;
+    const float2* type_ab;  // [kMaxTypes] (a, b) pair factors of each class
+    int ntypes;
+    int list_cap;           // entries per (slot, wave)
+    int list_stride;        // >= N
+    float list_skin;        // > 0 only in the list path's own argument block
+    unsigned* lticket;      // list step arrival counters: [32 g] per group of workgroups (g < 8), [32 * 8] groups
+    float* lgroup;          // [8][24] group partial rows (8 doubles + 8 floats)
 };
+
+constexpr int kListWaves = 4;           // waves per tile of the list kernels (each owns one list segment)
+constexpr int kMaxTypes = 256;          // pair-factor classes (8 bits of a list entry)
+constexpr int kListIndexBits = 24;      // particle index bits of a list entry
+constexpr int kListCountMask = (1 << 30) - 1;
+constexpr int kListOverflow = 1 << 30;
 
 // ---- Philox4x32-10 + Box-Muller: the production noise stream (identical on host for the oracle) ----
 __host__ __device__ inline void philox4x32_10(unsigned c[4], unsigned k0, unsigned k1)
@@ -216,7 +253,13 @@ void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* sl
                          int* count);
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, const float4* kmu,
                       int n, const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell,
-                      float4* spos, float* sb, int pair_mix);
+                      float4* spos, float* sb, int pair_mix, const int* ptype = nullptr, float4* psort0 = nullptr,
+                      float4* psort1 = nullptr);
+// list step: build the neighbour lists on the current cell list (grid rc = cutoff + skin); one step from them
+void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a);
+void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int apply_sched);
+int list_step_grid(int n);
+bool list_u16(int n);  // list entries are 16-bit slot indices (N <= 65536)
 void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceArgs& a, bool fused);
 void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a);
 void launch_adapt(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force_blocks, float spacestep, float timestep);

@@ -266,7 +266,7 @@ __global__ __launch_bounds__(1024) void k_prime(DevCtx* ctx, ForceArgs a, float 
             ctx->bbox_lo[k] = l;
             ctx->bbox_hi[k] = h;
         }
-        float rc = rc_fixed > 0.f ? rc_fixed : pair_cutoff(a, ctx->cs);
+        float rc = rc_fixed > 0.f ? rc_fixed : pair_cutoff(a, ctx->cs) + a.list_skin;
         compute_grid(ctx, rc, ncell_max, rc_fixed > 0.f ? 1 : kPairFx);
         if (sched) ctx->grid_next = next_grid(ctx, a, sched, ctx->step + 1, ncell_max);
         ctx->ticket = 0u;
@@ -640,6 +640,7 @@ __global__ __launch_bounds__(1024) void k_cell_scan(DevCtx* __restrict__ ctx, in
     }
 }
 
+template <int kTailRows = 8>
 __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance,
                                           int apply_sched, int ncell_max, const double* __restrict__ sched, bool fused,
                                           double* red_out = nullptr);
@@ -1185,7 +1186,9 @@ __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ct
                                                    const int* __restrict__ tmp, const int* __restrict__ cell_of,
                                                    const int* __restrict__ cstart, int* __restrict__ sidx,
                                                    int* __restrict__ scell, float4* __restrict__ spos,
-                                                   float* __restrict__ sb, int pair_mix)
+                                                   float* __restrict__ sb, int pair_mix,
+                                                   const int* __restrict__ ptype, float4* __restrict__ psort0,
+                                                   float4* __restrict__ psort1)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n || s >= cstart[ctx->grid.ncell]) return;  // binned particles only (all of them, undecomposed)
@@ -1203,6 +1206,8 @@ __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ct
     // the pair field's factors: (a, b) when it mixes A/B (interphase), (1, 0) for plain softcore<2,3>
     spos[d] = make_float4(p.x, p.y, p.z, pair_mix ? k.y : 1.f);
     sb[d] = pair_mix ? k.z : 0.f;
+    if (psort0)  // list path: the current positions in slot order, .w = particle | class << 24
+        (ctx->parity ? psort1 : psort0)[d] = make_float4(p.x, p.y, p.z, __int_as_float(i | (ptype[i] << kListIndexBits)));
 }
 
 // ----------------------------------------------------------------------------------------------------
@@ -1267,7 +1272,9 @@ __device__ inline float spring_coef(int type, float K, float l, float r2, float&
 
 // Particle-local terms of particle i at (xi, yi, zi): bonded CSR (chain/loop/nucleolar bonds, droplet),
 // cosine bending, kinetochore fibers, point sources and the ellipsoid walls (+ their reactions).
-template <int MODE>
+// BB: bonded entries whose loads are issued together (a row of the CSR is a chain of dependent loads per entry
+// otherwise: the nucleolar particles' ~20 droplet and bond partners made it the longest path of a step)
+template <int MODE, int BB = 1>
 __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceArgs& a, int i, float xi, float yi,
                                    float zi, float4 km, float& fx, float& fy, float& fz, float* en, float* rin,
                                    float* rout)
@@ -1279,38 +1286,72 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
     float e_sw = 0.f, e_bond = 0.f, e_bend = 0.f, e_win = 0.f, e_wout = 0.f, e_pt = 0.f, e_kf = 0.f;
     if (a.has_bonds) {
         const int eb = a.boff[i], ee = a.boff[i + 1];
-        for (int q = eb; q < ee; ++q) {
-            const int2 en = a.bent[q];
-            const BondParam bp = a.bpar[en.y];
-            const float4 pj = posc[en.x];
+        for (int q0 = eb; q0 < ee; q0 += BB) {
+          int2 enb[BB];
+          float4 bvb[BB], pjb[BB];
+#pragma unroll
+          for (int u = 0; u < BB; ++u) {
+              enb[u] = (q0 + u < ee) ? a.bent[q0 + u] : make_int2(i, kSemispring);
+              bvb[u] = (q0 + u < ee) ? a.bval[q0 + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+#pragma unroll
+          for (int u = 0; u < BB; ++u) pjb[u] = posc[enb[u].x];
+#pragma unroll
+          for (int u = 0; u < BB; ++u) {
+            if (q0 + u >= ee) break;
+            const int type = enb[u].y & 15;
+            const float4 bv = bvb[u];
+            const float4 pj = pjb[u];
             const float rx = xi - pj.x, ry = yi - pj.y, rz = zi - pj.z;
             const float r2 = fmaf(rz, rz, fmaf(ry, ry, rx * rx));
             float c = 0.f, U = 0.f;
-            if (bp.type == kSoftwell) {
-                if (r2 < bp.la) {
-                    const float u = r2 * bp.kb;
-                    const float den = 1.f + u * u * u;
-                    c = -6.f * bp.ka * u * u * bp.kb / (den * den);
-                    e_sw += -0.5f * bp.ka / den;
+            if (type == kSoftwell) {
+                if (r2 < bv.z) {
+                    const float u6 = r2 * bv.y;
+                    const float den = 1.f + u6 * u6 * u6;
+                    c = -6.f * bv.x * u6 * u6 * bv.y / (den * den);
+                    e_sw += -0.5f * bv.x / den;
                 }
             } else {
-                float K = bp.ka, l = bp.la;
-                if (bp.mix) {
-                    const float4 kj = a.kmu[en.x];
-                    const float A = 0.5f * (km.y + kj.y), B = 0.5f * (km.z + kj.z);
-                    K = A * bp.ka + B * bp.kb;
-                    l = A * bp.la + B * bp.lb;
-                }
-                if (bp.scaled) {
+                float K = bv.x, l = bv.y;
+                if (enb[u].y >> 4) {  // scaled by the bond scale
                     K = K * (1.f / (bs * bs));
                     l = l * bs;
                 }
-                c = spring_coef(bp.type, K, l, r2, U);
+                c = spring_coef(type, K, l, r2, U);
                 e_bond += 0.5f * U;
             }
             fx = fmaf(c, rx, fx);
             fy = fmaf(c, ry, fy);
             fz = fmaf(c, rz, fz);
+          }
+        }
+    }
+
+    if (a.sw_n > 0) {
+        // the droplet (simulation_driver_forcefield.cpp:164-185: softwell among the nucleolar targets, cut off at
+        // apply_cutoff): every target interacts with every other; a wave holding a target loads all targets' positions
+        // once (lane t: target t) and walks them by shuffles, in target order
+        const bool tgt = km.w != 0.f;
+        if (__ballot(tgt)) {
+            const int m = a.sw_n;
+            const int jt = (__lane_id() < m) ? a.sw_idx[__lane_id()] : 0;
+            const float4 pt = posc[jt];
+            for (int t = 0; t < m; ++t) {
+                const int j = __shfl(jt, t);
+                const float px = __shfl(pt.x, t), py = __shfl(pt.y, t), pz = __shfl(pt.z, t);
+                const float rx = xi - px, ry = yi - py, rz = zi - pz;
+                const float r2 = fmaf(rz, rz, fmaf(ry, ry, rx * rx));
+                if (tgt && j != i && r2 < a.sw_la) {
+                    const float u6 = r2 * a.sw_kb;
+                    const float den = 1.f + u6 * u6 * u6;
+                    const float c = -6.f * a.sw_ka * u6 * u6 * a.sw_kb / (den * den);
+                    e_sw += -0.5f * a.sw_ka / den;
+                    fx = fmaf(c, rx, fx);
+                    fy = fmaf(c, ry, fy);
+                    fz = fmaf(c, rz, fz);
+                }
+            }
         }
     }
 
@@ -1665,12 +1706,14 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
 #ifndef GCS_P2_UNROLL
 #define GCS_P2_UNROLL 4  // sub-tile phase 2: hits popped per lane per round (rounds = wave max of hits / this)
 #endif
-template <int MODE, int NG>
+template <int MODE, int NG, typename LE = int>
 __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const ForceArgs& a, int lane, int s,
                                        int s_begin, int s_end, float4 pi, float bi, float& fx, float& fy, float& fz,
                                        float& acc, int* s_rowV, int* s_rowJ, float4* s_cand, int* s_candj, int& ntot,
-                                       int wv, int nwv)
+                                       int wv, int nwv, int self = -1, bool lvalid = false, int* lcnt = nullptr)
 {
+    // kModeList: phase 2 appends each hit (other than the particle itself) to the lane's list segment wv
+    // instead of evaluating the pair force (the lists of the list step, built at the grid's rc = cutoff + skin)
     constexpr int GL = kTile / NG;  // lanes (particles) per group
     constexpr int kSub = 32;        // candidates per group chunk
     constexpr int FPL = kSub / GL;  // candidate fetches per lane per chunk
@@ -1790,7 +1833,8 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
             const bool real = nj[f] >= 0;
             const float px = real ? np[f].x - ox : far, py = real ? np[f].y - oy : far, pz = real ? np[f].z - oz : far;
             my_cand[2 * i] = make_float4(-2.f * px, -2.f * py, -2.f * pz, fmaf(pz, pz, fmaf(py, py, px * px)));
-            my_cand[2 * i + 1] = make_float4(real ? kA * np[f].w : 0.f, real ? kB * nb[f] : 0.f, 0.f, 0.f);
+            my_cand[2 * i + 1] = make_float4(real ? kA * np[f].w : 0.f, real ? kB * nb[f] : 0.f,
+                                             MODE == kModeList ? __int_as_float(real ? nj[f] : -1) : 0.f, 0.f);
             if (MODE == kModeEnergy) s_candj[grp * kSub + i] = nj[f];
         }
         __builtin_amdgcn_wave_barrier();
@@ -1830,6 +1874,25 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
         if (MODE != kModeEnergy) acc += (float)__popc(m);
         // phase 2: pop ffbl, xor, min (exhausted -> the group's sentinel slot), clear
         const int mh = uniform(wave_max_int(__popc(m)));
+        if constexpr (MODE == kModeList) {
+            // append the hits: one column-major store per hit (lanes of a wave write consecutive slots of a row)
+            LE* const seg = reinterpret_cast<LE*>(a.list) + (size_t)wv * a.list_cap * a.list_stride + s;
+            for (int t = 0; t < mh; ++t) {
+                unsigned b;
+                asm("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(m));
+                const unsigned k = min(b ^ 7u, (unsigned)kSub);
+                m &= m - 1u;
+                if (k < (unsigned)kSub && lvalid) {
+                    const int e = __float_as_int(my_cand[2 * k + 1].z);  // the partner's sorted slot
+                    if (e != s) {
+                        if (*lcnt < a.list_cap) seg[(size_t)(*lcnt) * a.list_stride] = (LE)e;
+                        *lcnt += 1;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            continue;
+        }
         for (int t = 0; t < mh; t += kP2) {
             unsigned kk[kP2];
 #pragma unroll
@@ -2216,6 +2279,7 @@ __global__ __launch_bounds__(256) void k_adapt(DevCtx* ctx, ForceArgs a, int blo
 // bitwise reproducible) + the device-resident interphase schedule + the next cell grid.  Any block size that
 // is a multiple of 64.  fused: the step's force kernel already binned the new positions with grid_next, which
 // becomes the current grid, and the grid for the following step is prepared.
+template <int kTailRows>
 __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int fblocks, int bblocks, int advance,
                                           int apply_sched, int ncell_max, const double* __restrict__ sched, bool fused,
                                           double* red_out)
@@ -2243,12 +2307,12 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
     // kTailRows rows' 16-B sc1 loads at once (one memory round trip per kTailRows * B rows), combines its rows
     // in order, then lanes meet in wave butterflies and the waves in index order: a fixed order for a given
     // (blocks, blockDim), bitwise reproducible.  Loads past the end return 0 (buffer range check).
-    constexpr int kTailRows = 8;
     const float big = 3.0e38f;
     const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_force, 0, fblocks * 32, 0x00020000);
     const auto rb = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_bbox, 0, bblocks * 32, 0x00020000);
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     float bb[6] = {big, big, big, -big, -big, -big};
+    float ldisp = 0.f, lfb = 0.f;  // list step: bbox row words 6, 7 (max displacement from the build, fallbacks)
     if (fblocks == bblocks && ctx->nactive > 0) {  // step launches: only the working blocks' rows
         fblocks = min(fblocks, ctx->nactive);
         bblocks = fblocks;
@@ -2281,6 +2345,10 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
                 bb[3] = fmaxf(bb[3], g0[j].w);
                 bb[4] = fmaxf(bb[4], g1[j].x);
                 bb[5] = fmaxf(bb[5], g1[j].y);
+                if (a.list_skin > 0.f) {
+                    ldisp = fmaxf(ldisp, g1[j].z);
+                    lfb += g1[j].w;
+                }
             }
         }
     }
@@ -2288,9 +2356,15 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
     for (int k = 0; k < 8; ++k) acc[k] = (k == 6) ? wave_total_max_d(acc[k]) : wave_total_sum_d(acc[k]);
 #pragma unroll
     for (int k = 0; k < 6; ++k) bb[k] = (k < 3) ? wave_total_min_f(bb[k]) : wave_total_max_f(bb[k]);
+    if (a.list_skin > 0.f) {
+        ldisp = wave_total_max_f(ldisp);
+        lfb = (float)wave_total_sum_d((double)lfb);
+    }
     if (lane == 0) {
         for (int k = 0; k < 8; ++k) s_red[wave][k] = acc[k];
         for (int k = 0; k < 6; ++k) s_bb[wave][k] = bb[k];
+        s_bb[wave][6] = ldisp;
+        s_bb[wave][7] = lfb;
     }
     __syncthreads();
     if (tid == 0) {
@@ -2298,9 +2372,16 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
         float bb[6];
         for (int k = 0; k < 8; ++k) tot[k] = s_red[0][k];
         for (int k = 0; k < 6; ++k) bb[k] = s_bb[0][k];
+        float ld = s_bb[0][6], lf = s_bb[0][7];
         for (int w = 1; w < nw; ++w) {
             for (int k = 0; k < 8; ++k) tot[k] = (k == 6) ? fmax(tot[k], s_red[w][k]) : tot[k] + s_red[w][k];
             for (int k = 0; k < 6; ++k) bb[k] = (k < 3) ? fminf(bb[k], s_bb[w][k]) : fmaxf(bb[k], s_bb[w][k]);
+            ld = fmaxf(ld, s_bb[w][6]);
+            lf += s_bb[w][7];
+        }
+        if (a.list_skin > 0.f && !red_out) {
+            ctx->ldisp = ld;
+            ctx->lfallback += (long long)lf;
         }
         if (red_out) {  // the decomposed step's local reduction only (k_tail_reduce): the context is untouched
             for (int k = 0; k < 8; ++k) red_out[k] = tot[k];
@@ -2370,7 +2451,8 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
             for (int k = 0; k < kGridWords; ++k) reinterpret_cast<int*>(&ctx->grid)[k] = c_gn[k];
             ctx->grid_next = make_grid(lo, hi, rc, ncell_max, kPairFx);
         } else {
-            ctx->grid = make_grid(bb, bb + 3, pair_cutoff(a, cs), ncell_max, kPairFx);
+            // the list step's cell grid (used only when the lists are rebuilt) bins at cutoff + skin
+            ctx->grid = make_grid(bb, bb + 3, pair_cutoff(a, cs) + a.list_skin, ncell_max, kPairFx);
         }
         }  // !red_out
     }
@@ -2392,6 +2474,515 @@ __global__ __launch_bounds__(256) void k_tail(DevCtx* ctx, ForceArgs a, int fblo
     if (threadIdx.x == 0) {
         ctx->t_tail[0] = t0;
         ctx->t_tail[1] = wall_clock64();
+    }
+}
+
+
+// ----------------------------------------------------------------------------------------------------
+// list step (GCS_OPT_FUSED_STEP 3; DESIGN.md "The list step")
+//
+// Neighbour lists with a skin, the md::neighbor_searcher scheme the reference's integrator relies on (SURVEY.md
+// §8a row a2): every few steps the cell list is built at cutoff + skin and k_lbuild files, per particle, every
+// partner within that radius; in between, one launch per step (k_lstep) evaluates the pair forces from the lists,
+// the particle-local terms, the Euler-Maruyama update and, in its last workgroup, the step's tail.  A list is
+// complete for the step when the particle's own displacement since the build plus the largest displacement of
+// any particle plus the cutoff's growth stays inside the skin; a particle for which that is not guaranteed (or
+// whose list overflowed) is evaluated exactly by a search of the build's cell list around its current position
+// with radius cutoff + largest displacement.  So the pair set is exact at every step, whatever the rebuild period.
+
+// The list step's context update, by thread 0 of the step's final workgroup once every partial is reduced: the
+// tail_body arithmetic of one undecomposed, unfused step (reactions, bbox, step/parity/noise cursor, the schedule of
+// stage_interphase/simulation_driver_interphase.cpp:17, :67-90 and the cell grid at cutoff + skin for a rebuild)
+__device__ void list_tail_apply(DevCtx* ctx, const ForceArgs& a, const double* tot, const float* bb, float ld, float lf,
+                                int apply_sched)
+{
+    const double* sched = a.sched;
+    // every input first (independent loads: one round trip)
+    const double s_flags = sched[kSchedFlags], s_dt = sched[kSchedDt], s_cs0 = sched[kSchedCs0],
+                 s_csTau = sched[kSchedCsTau], s_bs0 = sched[kSchedBs0], s_bsTau = sched[kSchedBsTau],
+                 s_muW = sched[kSchedMuW];
+    const double s_k[3] = {sched[kSchedK0], sched[kSchedK0 + 1], sched[kSchedK0 + 2]};
+    const long long c_step = ctx->step, c_cursor = ctx->noise_cursor, c_fb = ctx->lfallback;
+    const int c_parity = ctx->parity;
+    const double c_time = ctx->time, c_cs = ctx->cs, c_bs = ctx->bs;
+    const double c_w[3] = {ctx->wall[0], ctx->wall[1], ctx->wall[2]};
+    for (int k = 0; k < 3; ++k) {
+        ctx->react_in[k] = tot[k];
+        ctx->react_out[k] = tot[3 + k];
+        ctx->bbox_lo[k] = bb[k];
+        ctx->bbox_hi[k] = bb[3 + k];
+    }
+    ctx->max_drift = tot[6];
+    ctx->neighbors = tot[7] / (double)a.n;
+    ctx->ldisp = ld;
+    ctx->lfallback = c_fb + (long long)lf;
+    const long long step = c_step + 1;
+    ctx->step = step;
+    ctx->parity = c_parity ^ 1;
+    if (a.noise_mode == GCS_NOISE_INJECTED) ctx->noise_cursor = c_cursor + 1;
+    double time = c_time, cs = c_cs, bs = c_bs;
+    if (apply_sched) {
+        const int flags = (int)s_flags;
+        const double dt = s_dt;
+        if (flags & 1) ctx->time = time = (double)step * dt;
+        if (flags & 2) {
+            ctx->cs = cs = 1.0 - (1.0 - s_cs0) * exp(-(time / s_csTau));
+            ctx->bs = bs = 1.0 - (1.0 - s_bs0) * exp(-(time / s_bsTau));
+        }
+        if (flags & 4) {
+            for (int k = 0; k < 3; ++k) {
+                double net = 0.0;
+                net += tot[k] + tot[3 + k];
+                net -= s_k[k] * c_w[k];
+                ctx->wall[k] = c_w[k] + dt * s_muW * net;
+            }
+        }
+    }
+    (void)bs;
+    ctx->grid = make_grid(bb, bb + 3, pair_cutoff(a, cs) + a.list_skin, a.ncell_max, kPairFx);
+}
+
+// One workgroup's reduction of partial rows (force row: 8 floats, bbox row: 8 floats) in a fixed order: thread t takes
+// rows first + stride * (t + k * blockDim), lanes meet in wave butterflies, waves in index order (thread 0 returns).
+// The rows were stored write-through by other workgroups of this launch: sc1 loads.
+__device__ void list_reduce_rows(const ForceArgs& a, int first, int stride, int count, double* tot, float* bb,
+                                 float& ld, float& lf)
+{
+    __shared__ double s_red[kListWaves][8];
+    __shared__ float s_bb[kListWaves][8];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_force, 0, 0x7fffffff, 0x00020000);
+    const auto rb = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_bbox, 0, 0x7fffffff, 0x00020000);
+    const float big = 3.0e38f;
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float b[8] = {big, big, big, -big, -big, -big, 0.f, 0.f};
+    // kR rows per thread per round trip (all loads issued before any is used); rows past count read as the
+    // identity (the buffer range check returns 0 past the end: zero sums, and the bbox uses the guarded rows)
+    constexpr int kR = 4;
+    for (int k0 = tid; k0 < count; k0 += kR * blockDim.x) {
+      float4 F0[kR], F1[kR], G0[kR], G1[kR];
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+          const int k = k0 + r * blockDim.x;
+          const int off = (first + stride * min(k, count - 1)) * 32;
+          F0[r] = ld_sc1_f4(rf, off);
+          F1[r] = ld_sc1_f4(rf, off + 16);
+          G0[r] = ld_sc1_f4(rb, off);
+          G1[r] = ld_sc1_f4(rb, off + 16);
+      }
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const bool ok = k0 + r * (int)blockDim.x < count;
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f), lo4 = make_float4(big, big, big, -big),
+                     hi4 = make_float4(-big, -big, 0.f, 0.f);
+        const float4 f0 = ok ? F0[r] : z4, f1 = ok ? F1[r] : z4, g0 = ok ? G0[r] : lo4, g1 = ok ? G1[r] : hi4;
+        acc[0] += f0.x;
+        acc[1] += f0.y;
+        acc[2] += f0.z;
+        acc[3] += f0.w;
+        acc[4] += f1.x;
+        acc[5] += f1.y;
+        acc[6] = fmax(acc[6], (double)f1.z);
+        acc[7] += f1.w;
+        b[0] = fminf(b[0], g0.x);
+        b[1] = fminf(b[1], g0.y);
+        b[2] = fminf(b[2], g0.z);
+        b[3] = fmaxf(b[3], g0.w);
+        b[4] = fmaxf(b[4], g1.x);
+        b[5] = fmaxf(b[5], g1.y);
+        b[6] = fmaxf(b[6], g1.z);
+        b[7] += g1.w;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = (k == 6) ? wave_total_max_d(acc[k]) : wave_total_sum_d(acc[k]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        b[k] = (k < 3) ? wave_total_min_f(b[k]) : (k < 7 ? wave_total_max_f(b[k]) : (float)wave_total_sum_d((double)b[k]));
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k) {
+            s_red[wave][k] = acc[k];
+            s_bb[wave][k] = b[k];
+        }
+    __syncthreads();
+    if (tid == 0) {
+        for (int k = 0; k < 8; ++k) {
+            tot[k] = s_red[0][k];
+            if (k < 6) bb[k] = s_bb[0][k];
+        }
+        ld = s_bb[0][6];
+        lf = s_bb[0][7];
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            for (int k = 0; k < 8; ++k) tot[k] = (k == 6) ? fmax(tot[k], s_red[w][k]) : tot[k] + s_red[w][k];
+            for (int k = 0; k < 6; ++k) bb[k] = (k < 3) ? fminf(bb[k], s_bb[w][k]) : fmaxf(bb[k], s_bb[w][k]);
+            ld = fmaxf(ld, s_bb[w][6]);
+            lf += s_bb[w][7];
+        }
+    }
+}
+
+// LE: list entry type (unsigned short when every slot index fits 16 bits: half the list traffic)
+template <typename LE>
+__global__ __launch_bounds__(64 * kListWaves) void k_lbuild(DevCtx* __restrict__ ctx, ForceArgs a)
+{
+    __shared__ int s_rowV[kListWaves][4 * 17];
+    __shared__ int s_rowJ[kListWaves][4 * 16];
+    __shared__ float4 s_cand[kListWaves][4 * 2 * (32 + 1)];
+    __shared__ int s_ovf[kListWaves][kTile];
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    const int ntiles = ctx->ntiles;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // read by the list steps that follow (next launches); every block here reads ctx->grid only
+        ctx->lgrid = ctx->grid;
+        ctx->lrc_b = pair_cutoff(a, ctx->cs);
+        ctx->ldisp = 0.f;
+        ctx->lbuilds += 1;
+        ctx->nactive = 0;  // the list step's tail reads every workgroup's partial row
+    }
+    int ntot = 0;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int2 tr = a.tile_range[tile];
+        const int s_begin = uniform(tr.x), s_end = uniform(tr.y);
+        const int s = s_begin + lane;
+        const bool valid = s < s_end;
+        const int sl = valid ? s : s_end - 1;
+        const float4 pi = a.spos[sl];
+        const float bi = a.sb[sl];
+        const int self = a.sidx[sl];
+        float fx = 0.f, fy = 0.f, fz = 0.f, acc = 0.f;
+        int cnt = 0;
+        pair_forces_sub<kModeList, 2, LE>(ctx, a, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
+                                      s_rowJ[wave], s_cand[wave], nullptr, ntot, wave, kListWaves, self, valid, &cnt);
+        s_ovf[wave][lane] = cnt > a.list_cap ? 1 : 0;
+        __syncthreads();
+        int ovf = 0;
+#pragma unroll
+        for (int w = 0; w < kListWaves; ++w) ovf |= s_ovf[w][lane];
+        if (valid) a.lcount[(size_t)wave * a.list_stride + s] = min(cnt, a.list_cap) | (ovf ? kListOverflow : 0);
+        __syncthreads();
+    }
+}
+
+// the mixed soft-core pair force of one partner (the tile kernel's phase-2 arithmetic, in the global frame)
+__device__ __forceinline__ void list_pair(float xi, float yi, float zi, float4 q, float2 t, float ahi, float bhi,
+                                          float kA, float kB, float k2a, float k2b, float rc2, bool real, float& fx,
+                                          float& fy, float& fz, float& nbr)
+{
+    const float dx = xi - q.x, dy = yi - q.y, dz = zi - q.z;
+    const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+    const float ga = fmaxf(fmaf(-k2a, r2, 1.f), 0.f);
+    const float tt = r2 * k2b;
+    const float t2 = tt * tt;
+    const float gb = fmaxf(fmaf(-t2, t2, 1.f), 0.f);
+    const float A = fmaf(kA, t.x, ahi), B = fmaf(kB, t.y, bhi);
+    const bool in = real && r2 < rc2;
+    const float coef = in ? fmaf(A, ga * ga, B * (gb * gb * t2 * tt)) : 0.f;
+    fx = fmaf(coef, dx, fx);
+    fy = fmaf(coef, dy, fy);
+    fz = fmaf(coef, dz, fz);
+    nbr += in ? 1.f : 0.f;
+}
+
+__device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
+{
+    const float q = (v - g.lo[k]) * g.inv[k];
+    const int c = (q > 0.f) ? (int)fminf(q, 1.0e9f) : 0;
+    return min(c, g.n[k] - 1);
+}
+
+#ifndef GCS_LIST_UNROLL
+#define GCS_LIST_UNROLL 8  // list entries per batch of the pair loop
+#endif
+#ifndef GCS_LIST_PIPE
+#define GCS_LIST_PIPE 0  // 1: two batches in flight (the next batch's gathers overlap this batch's arithmetic)
+#endif
+#ifndef GCS_LIST_TAIL_ROWS
+#define GCS_LIST_TAIL_ROWS 4  // partial rows per thread per round trip of the last workgroup's tail
+#endif
+
+template <typename LE>
+__global__ __launch_bounds__(64 * kListWaves) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int apply_sched)
+{
+    __shared__ float red[kListWaves][4][kTile];
+    __shared__ float4 s_locf[kTile], s_locr[kTile], s_loco[kTile], s_noise[kTile];
+    __shared__ float2 s_tab[kMaxTypes];
+    __shared__ float s_pr[kForcePartials + kBBoxStride];  // force partials, then bbox lo/hi, max displacement, fallbacks
+    __shared__ int s_last;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = uniform(tid >> 6);
+    // GCS_DEBUG_TIMES: per workgroup 8 wall-clock stamps (start, wave 0: pair loop start / end, reduced,
+    // integrated (first tile), workgroup end, ticket taken, tail end)
+    unsigned long long* const dbg = a.dbg_times ? a.dbg_times + 8 * blockIdx.x : nullptr;
+    if (dbg && tid == 0) dbg[0] = wall_clock64();
+    for (int t = tid; t < a.ntypes; t += blockDim.x) s_tab[t] = a.type_ab[t];
+    if (tid == 0) {
+        for (int k = 0; k < kForcePartials; ++k) s_pr[k] = 0.f;
+        for (int k = 0; k < 3; ++k) {
+            s_pr[kForcePartials + k] = 3.0e38f;
+            s_pr[kForcePartials + 3 + k] = -3.0e38f;
+        }
+        s_pr[kForcePartials + 6] = 0.f;
+        s_pr[kForcePartials + 7] = 0.f;
+    }
+    const int n = a.n;
+    const float cs = (float)ctx->cs;
+    const float scale = a.pair_scaled ? cs : 1.f;
+    const float sa = a.pa_sig * scale, sbb = a.pb_sig * scale;
+    const float k2a = 1.f / (sa * sa), k2b = 1.f / (sbb * sbb);
+    const float kA = 0.5f * 6.f * a.pa_eps * k2a, kB = 0.5f * 24.f * a.pb_eps * k2b;
+    const float rc = pair_cutoff(a, ctx->cs), rc2 = rc * rc;
+    const float D = ctx->ldisp;
+    // a particle whose own displacement exceeds this may miss a partner in its list (0.999: fp32 margin)
+    const float slack = 0.999f * a.list_skin - D - fmaxf(rc - ctx->lrc_b, 0.f);
+    const int par = ctx->parity;
+    const float4* __restrict__ pc = par ? a.pos1 : a.pos0;  // particle order (bonded partners, output)
+    float4* __restrict__ pn = par ? a.pos0 : a.pos1;
+    const float4* __restrict__ qc = par ? a.psort1 : a.psort0;  // slot order (pair partners)
+    float4* __restrict__ qn = par ? a.psort0 : a.psort1;
+    const int cap = a.list_cap;
+    const size_t stride = (size_t)a.list_stride;
+    constexpr int kU = GCS_LIST_UNROLL;
+    constexpr int kIdx = (1 << kListIndexBits) - 1;
+    // software-pipelined by one tile: a tile's slot loads (one round trip, nothing depends on anything but the slot)
+    // are issued before the previous tile's work and, for the first tile, before the type-table barrier
+    // tiles: 64 consecutive slots (the lists are per slot; no cell-row structure is needed here)
+    int tile = blockIdx.x;
+    float4 n_pi = make_float4(0.f, 0.f, 0.f, 0.f), n_pb = n_pi;
+    int n_cw = 0, n_e[kU];
+    auto load_tile = [&](int t) {
+        const int sl = min(t * kTile + lane, n - 1);
+        n_pi = qc[sl];    // current position, .w = particle | class << 24
+        n_pb = a.spos[sl];  // build position
+        n_cw = a.lcount[(size_t)wave * stride + sl];
+        const LE* __restrict__ seg = reinterpret_cast<const LE*>(a.list) + (size_t)wave * cap * stride + sl;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) n_e[u] = seg[(size_t)u * stride];  // list_cap >= kU: in bounds
+    };
+    if (tile * kTile < n) load_tile(tile);
+    __syncthreads();
+    for (; tile * kTile < n; tile += gridDim.x) {
+        const int s = tile * kTile + lane;
+        const bool valid = s < n;
+        const int sl = valid ? s : n - 1;
+        const float4 pi = n_pi, pb = n_pb;
+        const int cw = n_cw;
+        int e[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) e[u] = n_e[u];
+        if ((tile + (int)gridDim.x) * kTile < n) load_tile(tile + gridDim.x);
+        const LE* __restrict__ seg = reinterpret_cast<const LE*>(a.list) + (size_t)wave * cap * stride + sl;
+        const int pk = __float_as_int(pi.w);
+        const int i = pk & kIdx;
+        const float2 own = s_tab[(unsigned)pk >> kListIndexBits];
+        const float ex = pi.x - pb.x, ey = pi.y - pb.y, ez = pi.z - pb.z;
+        const float di = sqrtf(fmaf(ez, ez, fmaf(ey, ey, ex * ex)));
+        const bool fb = valid && (di > slack || (cw & kListOverflow) != 0);
+
+        if (wave == kListWaves - 1) {  // the particle-local terms first (a dependent-gather chain), parked in LDS
+            const float4 km = a.kmu[i];
+            float lfx = 0.f, lfy = 0.f, lfz = 0.f, en[kEnergyKinds];
+            float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
+            local_terms<kModeStep, 4>(ctx, a, i, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout);
+            s_locf[lane] = make_float4(lfx, lfy, lfz, km.x);
+            s_locr[lane] = make_float4(rin[0], rin[1], rin[2], 0.f);
+            s_loco[lane] = make_float4(rout[0], rout[1], rout[2], 0.f);
+        }
+
+        float fx = 0.f, fy = 0.f, fz = 0.f, nbr = 0.f;
+        const float ahi = kA * own.x, bhi = kB * own.y;
+        const bool stamp = dbg && tid == 0 && tile == (int)blockIdx.x;
+        if (stamp) dbg[1] = wall_clock64();
+        if (a.has_pair) {
+            const int cnt = (valid && !fb) ? min(cw & kListCountMask, cap) : 0;
+            const int kmax = uniform(wave_max_int(cnt));
+#if GCS_LIST_PIPE
+            // two batches in flight: the next batch's gathers are issued before this batch's arithmetic, the
+            // entries of the batch after that before those gathers
+            float4 q[kU], qn[kU];
+            int en_[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) q[u] = qc[(u < cnt) ? e[u] : sl];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) en_[u] = (kU + u < kmax) ? seg[(size_t)(kU + u) * stride] : 0;
+            for (int k0 = 0; k0 < kmax; k0 += kU) {
+#pragma unroll
+                for (int u = 0; u < kU; ++u) qn[u] = qc[(k0 + kU + u < cnt) ? en_[u] : sl];
+#pragma unroll
+                for (int u = 0; u < kU; ++u)
+                    en_[u] = (k0 + 2 * kU + u < kmax) ? seg[(size_t)(k0 + 2 * kU + u) * stride] : 0;
+#pragma unroll
+                for (int u = 0; u < kU; ++u)
+                    list_pair(pi.x, pi.y, pi.z, q[u], s_tab[(unsigned)__float_as_int(q[u].w) >> kListIndexBits], ahi,
+                              bhi, kA, kB, k2a, k2b, rc2, k0 + u < cnt, fx, fy, fz, nbr);
+#pragma unroll
+                for (int u = 0; u < kU; ++u) q[u] = qn[u];
+            }
+#else
+            for (int k0 = 0; k0 < kmax; k0 += kU) {
+                int en_[kU];  // the next batch's entries, in flight during this batch
+#pragma unroll
+                for (int u = 0; u < kU; ++u)
+                    en_[u] = (k0 + kU + u < kmax) ? seg[(size_t)(k0 + kU + u) * stride] : 0;
+                float4 q[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) q[u] = qc[(k0 + u < cnt) ? e[u] : sl];
+#pragma unroll
+                for (int u = 0; u < kU; ++u)
+                    list_pair(pi.x, pi.y, pi.z, q[u], s_tab[(unsigned)__float_as_int(q[u].w) >> kListIndexBits], ahi,
+                              bhi, kA, kB, k2a, k2b, rc2, k0 + u < cnt, fx, fy, fz, nbr);
+#pragma unroll
+                for (int u = 0; u < kU; ++u) e[u] = en_[u];
+            }
+#endif
+            if (__ballot(fb)) {
+                // exact search of the build's cell list around the current position: a partner within rc now was
+                // within rc + D of it at the build; the waves take alternate cell rows
+                if (fb) {
+                    const Grid lg = ctx->lgrid;
+                    const float R = rc + D + 1.0e-5f * (rc + D);
+                    const int x0 = lgrid_cell(lg, 0, pi.x - R), x1 = lgrid_cell(lg, 0, pi.x + R);
+                    const int y0 = lgrid_cell(lg, 1, pi.y - R), y1 = lgrid_cell(lg, 1, pi.y + R);
+                    const int z0 = lgrid_cell(lg, 2, pi.z - R), z1 = lgrid_cell(lg, 2, pi.z + R);
+                    int row = 0;
+                    for (int z = z0; z <= z1; ++z)
+                        for (int y = y0; y <= y1; ++y, ++row) {
+                            if ((row % kListWaves) != wave) continue;
+                            const int base = (z * lg.n[1] + y) * lg.n[0];
+                            const int t0 = a.cstart[base + x0], t1 = a.cstart[base + x1 + 1];
+                            for (int t = t0; t < t1; ++t) {
+                                if (t == s) continue;
+                                const float4 q = qc[t];
+                                list_pair(pi.x, pi.y, pi.z, q, s_tab[(unsigned)__float_as_int(q.w) >> kListIndexBits],
+                                          ahi, bhi, kA, kB, k2a, k2b, rc2, true, fx, fy, fz, nbr);
+                            }
+                        }
+                }
+            }
+        }
+        if (stamp) dbg[2] = wall_clock64();
+        red[wave][0][lane] = fx;
+        red[wave][1][lane] = fy;
+        red[wave][2][lane] = fz;
+        red[wave][3][lane] = nbr;
+        if (wave == 1) {  // the noise (depends on the particle and the step only) off wave 0's path
+            float n0, n1, n2;
+            noise3(a, ctx, i, n0, n1, n2);
+            s_noise[lane] = make_float4(n0, n1, n2, 0.f);
+        }
+        __syncthreads();
+        if (stamp) dbg[3] = wall_clock64();
+        if (wave == 0) {
+            fx = red[0][0][lane];
+            fy = red[0][1][lane];
+            fz = red[0][2][lane];
+            nbr = red[0][3][lane];
+#pragma unroll
+            for (int w = 1; w < kListWaves; ++w) {
+                fx += red[w][0][lane];
+                fy += red[w][1][lane];
+                fz += red[w][2][lane];
+                nbr += red[w][3][lane];
+            }
+            const float4 lf = s_locf[lane], lr = s_locr[lane], lo = s_loco[lane];
+            fx += lf.x;
+            fy += lf.y;
+            fz += lf.z;
+            const float mu = lf.w;
+            float v[kForcePartials];
+            v[0] = wave_sum(valid ? lr.x : 0.f);
+            v[1] = wave_sum(valid ? lr.y : 0.f);
+            v[2] = wave_sum(valid ? lr.z : 0.f);
+            v[3] = wave_sum(valid ? lo.x : 0.f);
+            v[4] = wave_sum(valid ? lo.y : 0.f);
+            v[5] = wave_sum(valid ? lo.z : 0.f);
+            v[6] = wave_max(valid ? mu * sqrtf(fx * fx + fy * fy + fz * fz) : 0.f);
+            v[7] = wave_sum(valid ? nbr : 0.f);
+            // Euler-Maruyama: x += mu dt F + sqrt(2 T mu dt) xi
+            const float4 xi = s_noise[lane];
+            const float dt = a.timestep;
+            const float amp = sqrtf(2.f * a.temperature * mu * dt);
+            const float mdt = mu * dt;
+            const float nxp = pi.x + mdt * fx + amp * xi.x;
+            const float nyp = pi.y + mdt * fy + amp * xi.y;
+            const float nzp = pi.z + mdt * fz + amp * xi.z;
+            if (valid) {
+                pn[i] = make_float4(nxp, nyp, nzp, 0.f);
+                qn[s] = make_float4(nxp, nyp, nzp, pi.w);
+            }
+            const float gx = nxp - pb.x, gy = nyp - pb.y, gz = nzp - pb.z;
+            const float dmax = wave_max(valid ? sqrtf(fmaf(gz, gz, fmaf(gy, gy, gx * gx))) : 0.f);
+            const float nfb = wave_sum(fb ? 1.f : 0.f);
+            const float big = 3.0e38f;
+            const float l0 = wave_min(valid ? nxp : big), l1 = wave_min(valid ? nyp : big),
+                        l2 = wave_min(valid ? nzp : big);
+            const float h0 = wave_max(valid ? nxp : -big), h1 = wave_max(valid ? nyp : -big),
+                        h2 = wave_max(valid ? nzp : -big);
+            if (lane == 0) {
+                for (int k = 0; k < kForcePartials; ++k) s_pr[k] = (k == 6) ? fmaxf(s_pr[k], v[k]) : s_pr[k] + v[k];
+                float* b = s_pr + kForcePartials;
+                b[0] = fminf(b[0], l0);
+                b[1] = fminf(b[1], l1);
+                b[2] = fminf(b[2], l2);
+                b[3] = fmaxf(b[3], h0);
+                b[4] = fmaxf(b[4], h1);
+                b[5] = fmaxf(b[5], h2);
+                b[6] = fmaxf(b[6], dmax);
+                b[7] += nfb;
+            }
+            if (stamp) dbg[4] = wall_clock64();
+        }
+        __syncthreads();  // red / s_loc* are reused by the next tile
+    }
+    if (dbg && tid == 0) dbg[5] = wall_clock64();
+    // publish this workgroup's partial rows write-through, then a two-level ticket (one counter per group of
+    // workgroups b % 8, then one over the groups; a single counter serialises ~1000 returning atomics): the last
+    // workgroup of a group reduces the group's rows, the last group-reducer reduces the group rows in group order
+    // and advances the context (sc1 stores, vmcnt(0), one agent atomic per workgroup; rows read with sc1 loads)
+    const int ngroups = min((int)gridDim.x, 8);
+    const int g = blockIdx.x % ngroups;
+    const int gsize = ((int)gridDim.x - g + ngroups - 1) / ngroups;
+    if (tid == 0) {
+        const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_force, 0, 0x7fffffff, 0x00020000);
+        const auto rb = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_bbox, 0, 0x7fffffff, 0x00020000);
+        const int off = blockIdx.x * 32;
+        st_sc1_f4(rf, off, make_float4(s_pr[0], s_pr[1], s_pr[2], s_pr[3]));
+        st_sc1_f4(rf, off + 16, make_float4(s_pr[4], s_pr[5], s_pr[6], s_pr[7]));
+        const float* b = s_pr + kForcePartials;
+        st_sc1_f4(rb, off, make_float4(b[0], b[1], b[2], b[3]));
+        st_sc1_f4(rb, off + 16, make_float4(b[4], b[5], b[6], b[7]));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = atomicAdd(&a.lticket[32 * g], 1u);
+        s_last = (old == (unsigned)gsize - 1) ? 1 : 0;
+        if (dbg) {
+            dbg[6] = wall_clock64();
+            dbg[7] = 0ull;
+        }
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // the last workgroup of a group: count the group in; the last group's last workgroup is the final one
+    __shared__ int s_final;
+    if (tid == 0) {
+        a.lticket[32 * g] = 0u;  // ready for the next launch
+        const unsigned old = atomicAdd(&a.lticket[32 * 8], 1u);
+        s_final = (old == (unsigned)ngroups - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!s_final) return;
+    // the final workgroup: every partial row in workgroup order, then the context update
+    unsigned long long* const dbt = a.dbg_times ? a.dbg_times + 8 * gridDim.x : nullptr;
+    if (dbt && tid == 0) dbt[0] = wall_clock64();
+    {
+        double tot[8];
+        float bb[6], ld = 0.f, lf = 0.f;
+        list_reduce_rows(a, 0, 1, gridDim.x, tot, bb, ld, lf);
+        if (tid == 0) {
+            if (dbt) dbt[1] = wall_clock64();
+            a.lticket[32 * 8] = 0u;
+            list_tail_apply(ctx, a, tot, bb, ld, lf, apply_sched);
+            if (dbg) dbg[7] = wall_clock64();
+        }
     }
 }
 
@@ -2546,10 +3137,10 @@ void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* sl
 
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, const float4* kmu, int n,
                       const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell, float4* spos,
-                      float* sb, int pair_mix)
+                      float* sb, int pair_mix, const int* ptype, float4* psort0, float4* psort1)
 {
     hipLaunchKernelGGL(k_cell_sort, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, kmu, n, tmp, cell_of,
-                       cstart, sidx, scell, spos, sb, pair_mix);
+                       cstart, sidx, scell, spos, sb, pair_mix, ptype, psort0, psort1);
 }
 
 template <int MODE, bool FUSED>
@@ -2583,6 +3174,27 @@ void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceAr
     } else {
         launch_force_mode<kModeEnergy, false>(s, waves, ctx, a);
     }
+}
+
+int list_step_grid(int n) { return force_blocks(n); }
+
+bool list_u16(int n) { return n <= 65536; }
+
+void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a)
+{
+    if (list_u16(a.n))
+        hipLaunchKernelGGL(k_lbuild<unsigned short>, dim3(force_grid(a.n)), dim3(64 * kListWaves), 0, s, ctx, a);
+    else
+        hipLaunchKernelGGL(k_lbuild<int>, dim3(force_grid(a.n)), dim3(64 * kListWaves), 0, s, ctx, a);
+}
+
+void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int apply_sched)
+{
+    if (list_u16(a.n))
+        hipLaunchKernelGGL(k_lstep<unsigned short>, dim3(list_step_grid(a.n)), dim3(64 * kListWaves), 0, s, ctx, a,
+                           apply_sched);
+    else
+        hipLaunchKernelGGL(k_lstep<int>, dim3(list_step_grid(a.n)), dim3(64 * kListWaves), 0, s, ctx, a, apply_sched);
 }
 
 void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a)

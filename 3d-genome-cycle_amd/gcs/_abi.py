@@ -34,6 +34,9 @@ OPT_TILE_PRIORITY = 6
 OPT_SUBTILES = 7
 OPT_SCAN_BLOCKS = 8
 OPT_CONTACT_BITS = 9
+OPT_LIST_SKIN = 10
+OPT_LIST_EVERY = 11
+OPT_LIST_CAP = 12
 
 ENERGY_KINDS = ("pair", "softwell", "bonds", "bending", "wall_in", "wall_out", "point_source", "kinetochore_fiber")
 
@@ -99,6 +102,11 @@ class Profile(C.Structure):
                 ("mean_neighbors", _d)]
 
 
+class ListStats(C.Structure):
+    _fields_ = [("active", _i32), ("rebuild_every", _i32), ("builds", _i64), ("fallback_particle_steps", _i64),
+                ("skin", _d), ("max_displacement", _d), ("pair_classes", _i32), ("capacity", _i32)]
+
+
 # name -> (restype, argtypes); the exported surface of include/gcs.h
 PROTOTYPES = {
     "gcs_last_error": (C.c_char_p, []),
@@ -132,6 +140,7 @@ PROTOTYPES = {
                                               C.POINTER(_i64)]),
     "gcs_engine_profile": (C.c_int, [C.c_void_p, C.POINTER(BDConfig), _i64, _i64, C.POINTER(Profile)]),
     "gcs_engine_set_option": (C.c_int, [C.c_void_p, _i32, _i64]),
+    "gcs_engine_get_list_stats": (C.c_int, [C.c_void_p, C.POINTER(ListStats)]),
     "gcs_engine_contacts_update": (C.c_int, [C.c_void_p, _d]),
     "gcs_engine_contacts_read": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), _i64, C.POINTER(_i64)]),
     "gcs_engine_contacts_clear": (C.c_int, [C.c_void_p]),

@@ -314,6 +314,11 @@ class Engine:
     def set_option(self, option, value):
         A.check(self._lib.gcs_engine_set_option(self._h, int(option), int(value)))
 
+    def list_stats(self) -> dict:
+        s = A.ListStats()
+        A.check(self._lib.gcs_engine_get_list_stats(self._h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in A.ListStats._fields_}
+
 
 def device_count() -> int:
     lib = A.load()

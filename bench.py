@@ -291,9 +291,16 @@ def _cpu_model():
     return None
 
 
-def read_traffic():
-    """HBM bytes per force launch from the committed rocprofv3 PMC pass (profiles/), if present."""
-    p = ROOT / "profiles" / "pmc_force_traffic.json"
+STEP_KERNEL = {3: ("k_lstep", "pmc_lstep_traffic.json"), 2: ("k_force<kModeStep, FUSED>", "pmc_force_traffic.json"),
+               1: ("k_force<kModeStep, FUSED>", None), 0: ("k_force<kModeStep>", None)}
+
+
+def read_traffic(fused=3):
+    """HBM bytes per launch of the step's dominant kernel from the committed rocprofv3 PMC pass (profiles/)."""
+    name = STEP_KERNEL.get(fused, (None, None))[1]
+    if name is None:
+        return None
+    p = ROOT / "profiles" / name
     if p.exists():
         try:
             return json.loads(p.read_text()).get("bytes_per_launch")
@@ -464,6 +471,10 @@ def replica_main(args):
     force_ms = prof["force_ms"]
     achieved = n * BYTES_PER_UPDATE / (force_ms * 1e-3) / 1e9
     ctx = eng.get_context()
+    lst = eng.list_stats() if hasattr(eng, "list_stats") else None
+    if lst is not None:  # the list step's rebuild cadence and exact-search fallbacks (DESIGN.md "The list step")
+        lst = {k: lst[k] for k in ("active", "rebuild_every", "skin", "builds", "fallback_particle_steps",
+                                   "pair_classes", "capacity")}
     finite = all(bool(np.isfinite(e.get_positions()).all()) for e in engines)
     at = after + args.profile_steps
 
@@ -547,10 +558,11 @@ def replica_main(args):
                    "waves_per_tile": args.waves, "chunk_order": args.chunk_order, "fused": args.fused,
                    "split_tiles": args.split, "tile_priority": args.prio, "subtiles": args.subtiles,
                    "scan_mb": args.scan_mb, "start_window_value": start_rate, "finite": finite,
-                   "contacts_update_ms": contacts_ms, "contacts_distinct_pairs_22_updates": contacts_distinct},
+                   "contacts_update_ms": contacts_ms, "contacts_distinct_pairs_22_updates": contacts_distinct,
+                   "list_step": lst},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(),
-                     "kernel": "k_force<kModeStep>", "force_ms": force_ms, "cell_ms": prof["cell_ms"],
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(args.fused),
+                     "kernel": STEP_KERNEL.get(args.fused, ("?",))[0], "force_ms": force_ms, "cell_ms": prof["cell_ms"],
                      "tail_ms": prof["tail_ms"], "bytes_per_launch": n * BYTES_PER_UPDATE},
         "cpu_baseline": cpu,
     }
@@ -576,7 +588,8 @@ def parse_args(argv=None):
     ap.add_argument("--prio", type=int, default=700, help="n > 0: wave priority min(3, tile candidates / n)")
     ap.add_argument("--subtiles", type=int, default=2, help="pair-loop stencils per 64-particle tile: 1, 2, 4")
     ap.add_argument("--scan-mb", type=int, default=1, help="1: multi-block look-back cell scan, 0: one workgroup")
-    ap.add_argument("--fused", type=int, default=2, help="2: 2-launch rebuild step, 1: 4-launch step, 0: unfused")
+    ap.add_argument("--fused", type=int, default=3,
+                    help="3: list step (default), 2: 2-launch rebuild step, 1: 4-launch step, 0: unfused")
     ap.add_argument("--profile-steps", type=int, default=50)
     ap.add_argument("--replicas-per-gpu", type=int, default=4,
                     help="independent trajectories per GPU, each its own engine + stream (1 = single trajectory)")

@@ -313,14 +313,33 @@ int gcs_engine_domain_unpack(gcs_engine* e, const float* dev_in, const int32_t* 
 #define GCS_OPT_GRAPH_STEPS 1   /* steps captured per hipGraph replay (0 = eager launches) */
 #define GCS_OPT_WAVES_PER_TILE 2 /* waves sharing one 64-particle tile of the pair loop: 1, 2, 4 or 8 */
 #define GCS_OPT_CHUNK_ORDER 3    /* pair-loop candidate chunks: 0 contiguous, 1 strided across stencil rows (default) */
-#define GCS_OPT_FUSED_STEP 4     /* 2 (default): 2 launches per step (force + rebuild); 1: 4 launches; 0: unfused */
+#define GCS_OPT_FUSED_STEP 4     /* 3 (default): neighbour-list step (1 launch per step + a list rebuild every few
+                                    steps; systems with > 256 pair classes or >= 2^24 particles run step 2);
+                                    2: 2 launches per step (force + cell-list rebuild); 1: 4 launches; 0: unfused */
 #define GCS_OPT_SPLIT_TILES 5    /* step launches: 0 (default) off, 1 split every tile over two workgroups, 2 only the
                                     densest tiles, picked by the cell scan within the resident-workgroup budget */
 #define GCS_OPT_SUBTILES 7       /* pair-loop stencils per 64-particle tile: 1, 2 or 4 (default 2) */
 #define GCS_OPT_SCAN_BLOCKS 8    /* cell scan: 1 = multi-block look-back scan (default), 0 = one workgroup */
 #define GCS_OPT_TILE_PRIORITY 6  /* n > 0: pair-loop wave priority min(3, tile candidates / n); 0 = off (default 700) */
 #define GCS_OPT_CONTACT_BITS 9   /* contact map: 2^bits hash slots (0 = default, >= 2 N slots sized at first update) */
+#define GCS_OPT_LIST_SKIN 10      /* list step: skin in 1/1000 of the pair cutoff (default 400) */
+#define GCS_OPT_LIST_EVERY 11     /* list step: rebuild period in steps (0 = default: from the noise amplitude) */
+#define GCS_OPT_LIST_CAP 12       /* list step: list entries per particle and wave (default 64; more: exact search) */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
+
+/* List-step diagnostics (the neighbour lists md::neighbor_searcher keeps between rebuilds; micromd, called at
+ * stage_interphase/simulation_driver_interphase.cpp:57-63). */
+typedef struct gcs_list_stats {
+    int32_t active;                   /* 1: the engine runs the list step (GCS_OPT_FUSED_STEP 3, system admits it) */
+    int32_t rebuild_every;            /* steps between list rebuilds of the last run */
+    int64_t builds;                   /* list builds so far */
+    int64_t fallback_particle_steps;  /* particle-steps evaluated by the exact cell search instead of the list */
+    double skin;                      /* list radius - pair cutoff */
+    double max_displacement;          /* largest displacement of a particle since the last build */
+    int32_t pair_classes;             /* distinct (a, b) pair-factor classes */
+    int32_t capacity;                 /* list entries per particle and wave */
+} gcs_list_stats;
+int gcs_engine_get_list_stats(gcs_engine* e, gcs_list_stats* out);
 
 #ifdef __cplusplus
 }

@@ -120,6 +120,7 @@ def test_contact_map_engine_cell_list_equals_search_cell_list(c1_design, interph
     """After a rebuild-step run the update reads the engine's own cell list; otherwise (4-launch step) it builds a
     search list: the tables are identical."""
     a = engine_for(c1_design, interphase_cfg)
+    a.set_option(A.OPT_FUSED_STEP, 2)
     b = engine_for(c1_design, interphase_cfg)
     b.set_option(A.OPT_FUSED_STEP, 1)
     for k in range(4):

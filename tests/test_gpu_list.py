@@ -1,0 +1,196 @@
+"""GPU parity of the list step (GCS_OPT_FUSED_STEP 3: neighbour lists with a skin, one launch per step, exact
+cell search for any particle the skin no longer covers) against the fp64 oracle, through the C ABI.
+
+Bounds are the ones DESIGN.md §6 states for every step shape: positions within 2e-5 absolute after k steps,
+forces/energies through the same engine calls.  The list step changes only the order in which a particle's pair
+forces are summed, never the pair set (k_lstep: a particle whose list may be incomplete is searched exactly), so
+the same bounds hold with the rebuild period forced far beyond what the skin covers, and with lists that overflow.
+"""
+import numpy as np
+import pytest
+
+from gcs import _abi as A
+from gcs import interphase, synthetic
+from gcs.config import InterphaseConfig, resolution_scaled
+from gcs.engine import Engine
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+TOL_X = 2e-5
+LATE = {"step": 200000, "time": 2.0, "core_scale": 0.99, "bond_scale": 0.99, "wall_semiaxes": [1.5, 1.55, 1.6]}
+
+
+def _f32(x):
+    return np.asarray(x, dtype=np.float32).astype(np.float64)
+
+
+def _list_engine(design, cfg, **opts):
+    e, _ = interphase.build_interphase(Engine, design, cfg)
+    e.set_option(A.OPT_FUSED_STEP, 3)
+    for k, v in opts.items():
+        e.set_option(getattr(A, "OPT_" + k.upper()), v)
+    return e
+
+
+def _pair(design, cfg, x=None, ctx=None, **opts):
+    e = _list_engine(design, cfg, **opts)
+    o, _ = interphase.build_interphase(oracle.OracleSystem, design, cfg)
+    for s in (e, o):
+        s.set_schedule(**interphase.interphase_schedule(cfg))
+        if x is not None:
+            s.set_positions(x)
+        if ctx is not None:
+            s.set_context(ctx)
+        else:
+            s.apply_schedule(0)
+    return e, o
+
+
+def _run_both(e, o, steps, first, cfg, seed, **kw):
+    for s in (e, o):
+        s.run(steps, first_step=first, temperature=cfg.temperature, timestep=cfg.timestep, seed=seed, **kw)
+
+
+def test_list_trajectory_c1_from_step0(c1_design):
+    """production start (core scale 0.5, growing cutoff), 60 steps, Philox noise"""
+    cfg = InterphaseConfig()
+    e, o = _pair(c1_design, cfg)
+    _run_both(e, o, 60, 0, cfg, 987654321)
+    err = np.abs(e.get_positions() - o.get_positions()).max()
+    st = e.list_stats()
+    assert st["active"] == 1 and st["builds"] >= 60 // st["rebuild_every"], st
+    assert err <= TOL_X, (err, st)
+
+
+def test_list_trajectory_c1_wall_contact(c1_design):
+    cfg = InterphaseConfig()
+    e, o = _pair(c1_design, cfg, ctx=LATE)
+    _run_both(e, o, 40, LATE["step"], cfg, 5)
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X
+    ce, co = e.get_context(), o.get_context()
+    assert ce["step"] == co["step"] == LATE["step"] + 40
+    assert np.allclose(ce["wall_semiaxes"], co["wall_semiaxes"], rtol=1e-7)
+    assert np.allclose(ce["inward_reaction"], co["inward_reaction"], rtol=1e-3, atol=1e-2)
+
+
+def test_list_injected_reference_noise(c1_design):
+    cfg = InterphaseConfig()
+    steps = 12
+    xi = oracle.reference_normals(c1_design.seed, steps * c1_design.n * 3).reshape(steps, c1_design.n, 3)
+    e, o = _pair(c1_design, cfg)
+    for s in (e, o):
+        s.set_noise(xi)
+    _run_both(e, o, steps, 0, cfg, 0, noise=A.NOISE_INJECTED)
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X
+
+
+@pytest.mark.parametrize("skin,every", [(30, 200), (400, 64)])
+def test_list_exact_when_the_skin_is_outrun(c1_design, skin, every):
+    """rebuild period far beyond the skin: particles outrun it and take the exact cell search; same bound"""
+    cfg = InterphaseConfig()
+    e, o = _pair(c1_design, cfg, ctx=LATE, list_skin=skin, list_every=every)
+    _run_both(e, o, 60, LATE["step"], cfg, 17)
+    st = e.list_stats()
+    assert st["fallback_particle_steps"] > 0, st
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X
+
+
+def test_list_exact_when_lists_overflow(c1_design):
+    cfg = InterphaseConfig()
+    e, o = _pair(c1_design, cfg, ctx=LATE, list_cap=8)
+    _run_both(e, o, 30, LATE["step"], cfg, 23)
+    st = e.list_stats()
+    assert st["fallback_particle_steps"] > 0, st
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X
+
+
+@pytest.mark.parametrize("every", [0, 1, 5])
+def test_list_graph_eager_and_chunks_bitwise_identical(c1_design, every):
+    """graph vs eager launches and one run vs chunks rebuild at the same steps: identical bits"""
+    cfg = InterphaseConfig()
+    runs = []
+    for g, chunks in ((0, [70]), (8, [70]), (32, [70]), (32, [13, 40, 17])):
+        e = _list_engine(c1_design, cfg, list_every=every, graph_steps=g)
+        e.set_schedule(**interphase.interphase_schedule(cfg))
+        e.set_context(LATE)
+        first = LATE["step"]
+        for c in chunks:
+            e.run(c, first_step=first, seed=11)
+            first += c
+        runs.append((e.get_positions(), e.get_context()))
+        e.close()
+    for x, c in runs[1:]:
+        assert np.array_equal(x, runs[0][0])
+        assert c == runs[0][1]
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 65, 200])
+def test_list_small_and_ragged_sizes(n):
+    """random ab factors and mobilities (several pair classes, mixed), 20 steps at dt 1e-4"""
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-0.5, 0.5, size=(n, 3))
+    ab = rng.choice([0.0, 0.5, 1.0], size=(n, 2))
+    mu = rng.uniform(0.5, 1.5, size=n)
+    sysd = {}
+    for name, cls in (("e", Engine), ("o", oracle.OracleSystem)):
+        s = cls(n, mobilities=mu, ab_factors=ab)
+        s.add_neighbor_softcore(2.5, 0.3, 2.5, 0.24, 0.3, mix=True, scaled=True)
+        if n > 1:
+            s.add_bonded_pairwise(A.POT_SEMISPRING, a_spring=100.0, b_spring=50.0, mix=True, scaled=True,
+                                  ranges=[(0, n)])
+        s.set_context({"core_scale": 0.8, "bond_scale": 0.7, "wall_semiaxes": [1, 1, 1]})
+        s.set_positions(x)
+        if name == "e":
+            s.set_option(A.OPT_FUSED_STEP, 3)
+        sysd[name] = s
+    for s in sysd.values():
+        s.run(20, seed=1, timestep=1e-4)
+    assert sysd["e"].list_stats()["active"] == 1
+    assert np.abs(sysd["e"].get_positions() - sysd["o"].get_positions()).max() <= TOL_X
+
+
+def test_list_c2_trajectory_from_bench_state():
+    """C2 (60,662 beads) from benchdata (step 300,000): 1, 10, 50 steps vs the oracle"""
+    from pathlib import Path
+    z = np.load(Path(__file__).resolve().parents[1] / "benchdata" / "c2_interphase_step300000.npz")
+    ctx = {"step": int(z["step"]), "time": float(z["time"]), "core_scale": float(z["core_scale"]),
+           "bond_scale": float(z["bond_scale"]), "wall_semiaxes": [float(v) for v in z["wall_semiaxes"]]}
+    design, cfg = synthetic.make_c2(), InterphaseConfig()
+    e, o = _pair(design, cfg, x=_f32(z["positions"]), ctx=ctx)
+    first, done, errs = ctx["step"], 0, {}
+    for k in (1, 10, 50):
+        _run_both(e, o, k - done, first + done, cfg, 99)
+        done = k
+        errs[k] = float(np.abs(e.get_positions() - o.get_positions()).max())
+    print({"list_c2_errors": errs, "stats": e.list_stats()})
+    assert all(v <= TOL_X for v in errs.values()), errs
+    ce, co = e.get_context(), o.get_context()
+    assert np.allclose(ce["wall_semiaxes"], co["wall_semiaxes"], rtol=1e-7)
+
+
+def test_list_c5_trajectory():
+    """C5 (606,248 beads, 10 kb, resolution-scaled timestep): 10 steps from the dense synthetic start"""
+    design, cfg = synthetic.make_c5(), resolution_scaled(InterphaseConfig(), 10.0)
+    e, o = _pair(design, cfg, x=_f32(design.positions))
+    _run_both(e, o, 10, 0, cfg, 99)
+    err = float(np.abs(e.get_positions() - o.get_positions()).max())
+    print({"list_c5_err": err, "stats": e.list_stats()})
+    assert err <= TOL_X
+
+
+def test_list_and_rebuild_step_agree_on_neighbour_count():
+    """the pair set is the same: the mean neighbour count the list step reports equals the tile kernel's"""
+    cfg = InterphaseConfig()
+    c2_design = synthetic.make_c2()
+    vals = []
+    for fused in (2, 3):
+        e, _ = interphase.build_interphase(Engine, c2_design, cfg)
+        e.set_option(A.OPT_FUSED_STEP, fused)
+        e.set_schedule(**interphase.interphase_schedule(cfg))
+        e.set_context(LATE)
+        p = e.profile(1, first_step=LATE["step"], seed=3)
+        vals.append(p["mean_neighbors"])
+        e.close()
+    assert vals[0] > 0 and vals[1] == pytest.approx(vals[0], rel=1e-4), vals

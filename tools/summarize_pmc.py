@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Average per-dispatch counters / durations per kernel from a tools/profile.sh output directory.
 
-    python tools/summarize_pmc.py gpurun_out/prof_r01 [--traffic-out profiles/pmc_force_traffic.json]
+    python tools/summarize_pmc.py gpurun_out/prof_r01 [--traffic-out profiles/pmc_force_traffic.json] [--kernel k_lstep]
 
 HBM traffic per force launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950 FETCH_SIZE reports half the bytes
 of wide coalesced reads (MI355X_MICROARCH.md "HBM"); both counters are fabric-side (L2 misses, Infinity Cache hits
@@ -50,9 +50,10 @@ def force_traffic(out, kernel_prefix="k_force<0"):
 if __name__ == "__main__":
     res = main(sys.argv[1])
     if "--traffic-out" in sys.argv:
-        t = force_traffic(res)
+        prefix = sys.argv[sys.argv.index("--kernel") + 1] if "--kernel" in sys.argv else "k_force<0"
+        t = force_traffic(res, prefix)
         if t is None:
-            sys.exit("no k_force FETCH_SIZE/WRITE_SIZE in the profile")
+            sys.exit(f"no {prefix} FETCH_SIZE/WRITE_SIZE in the profile")
         t["source"] = sys.argv[1]
         with open(sys.argv[sys.argv.index("--traffic-out") + 1], "w") as f:
             json.dump(t, f, indent=1)
