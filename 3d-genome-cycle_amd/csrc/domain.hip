@@ -21,10 +21,13 @@ namespace {
 // One thread per particle.  Records are float4 {x, y, z, index bits}, appended per peer with one atomic per wave
 // (order is irrelevant: the unpack is a scatter by index).  flags[0] |= 1: a bond (not the cut-off softwell) of an owned
 // particle reaches beyond the halo; flags[0] |= 2: a peer's band exceeded `cap`.
+// Band b's records are out[b * ostride + k], its count counts[b * cstride] (the engine-owned bands keep the count in
+// the band's header row: one message per peer carries both).
 __global__ __launch_bounds__(256) void k_domain_pack(const DevCtx* __restrict__ ctx, ForceArgs a,
                                                      const float2* __restrict__ regions, int npeer,
                                                      float4* __restrict__ out, int* __restrict__ counts, int cap,
-                                                     int* __restrict__ flags, const int* __restrict__ shared)
+                                                     int* __restrict__ flags, const int* __restrict__ shared,
+                                                     int ostride, int cstride)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
@@ -54,12 +57,12 @@ __global__ __launch_bounds__(256) void k_domain_pack(const DevCtx* __restrict__ 
         const unsigned long long m = __ballot(send);
         if (m == 0ull) continue;
         int base = 0;
-        if (lane == 0) base = atomicAdd(&counts[p], __popcll(m));
+        if (lane == 0) base = atomicAdd(&counts[(size_t)p * cstride], __popcll(m));
         base = __shfl(base, 0);
         if (send) {
             const int o = base + __popcll(m & ((1ull << lane) - 1ull));
             if (o < cap)
-                out[(size_t)p * cap + o] = make_float4(pn.x, pn.y, pn.z, __int_as_float(i));
+                out[(size_t)p * ostride + o] = make_float4(pn.x, pn.y, pn.z, __int_as_float(i));
             else
                 atomicOr(&flags[0], 2);
         }
@@ -68,12 +71,13 @@ __global__ __launch_bounds__(256) void k_domain_pack(const DevCtx* __restrict__ 
 
 // received bands: nbuf buffers of `cap` records, counts[b] valid in buffer b; both position buffers are written
 __global__ __launch_bounds__(256) void k_domain_unpack(ForceArgs a, const float4* __restrict__ in,
-                                                       const int* __restrict__ counts, int nbuf, int cap)
+                                                       const int* __restrict__ counts, int nbuf, int cap, int istride,
+                                                       int cstride)
 {
     for (int b = 0; b < nbuf; ++b) {
-        const int c = min(counts[b], cap);
+        const int c = min(counts[(size_t)b * cstride], cap);
         for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < c; k += gridDim.x * blockDim.x) {
-            const float4 r = in[(size_t)b * cap + k];
+            const float4 r = in[(size_t)b * istride + k];
             const int i = __float_as_int(r.w);
             if (i < 0 || i >= a.n) continue;
             const float4 p = make_float4(r.x, r.y, r.z, 0.f);
@@ -119,10 +123,10 @@ __global__ __launch_bounds__(64) void k_domain_shared_in(ForceArgs a, const int*
 }  // namespace
 
 void launch_domain_pack(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const float2* regions, int npeer,
-                        float4* out, int* counts, int cap, int* flags, const int* shared)
+                        float4* out, int* counts, int cap, int* flags, const int* shared, int ostride, int cstride)
 {
     hipLaunchKernelGGL(k_domain_pack, dim3((a.n + 255) / 256), dim3(256), 0, s, ctx, a, regions, npeer, out, counts,
-                       cap, flags, shared);
+                       cap, flags, shared, ostride > 0 ? ostride : cap, cstride);
 }
 
 void launch_domain_shared_out(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const int* idx, int nshared,
@@ -138,10 +142,24 @@ void launch_domain_shared_in(hipStream_t s, const ForceArgs& a, const int* idx, 
         hipLaunchKernelGGL(k_domain_shared_in, dim3((nshared + 63) / 64), dim3(64), 0, s, a, idx, nshared, buf);
 }
 
-void launch_domain_unpack(hipStream_t s, const ForceArgs& a, const float4* in, const int* counts, int nbuf, int cap)
+void launch_domain_unpack(hipStream_t s, const ForceArgs& a, const float4* in, const int* counts, int nbuf, int cap,
+                          int istride, int cstride)
 {
     const int blocks = std::max(1, std::min(1024, (cap + 255) / 256));
-    hipLaunchKernelGGL(k_domain_unpack, dim3(blocks), dim3(256), 0, s, a, in, counts, nbuf, cap);
+    hipLaunchKernelGGL(k_domain_unpack, dim3(blocks), dim3(256), 0, s, a, in, counts, nbuf, cap,
+                       istride > 0 ? istride : cap, cstride);
+}
+
+// zero the header rows (counts) of npeer bands of `stride` rows
+__global__ void k_band_headers_zero(float4* bands, int npeer, int stride)
+{
+    const int p = threadIdx.x;
+    if (p < npeer) bands[(size_t)p * stride] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+void launch_band_headers_zero(hipStream_t s, float4* bands, int npeer, int stride)
+{
+    if (npeer > 0) hipLaunchKernelGGL(k_band_headers_zero, dim3(1), dim3(64), 0, s, bands, npeer, stride);
 }
 
 }  // namespace gcs

@@ -6,6 +6,9 @@
 // before the next launch.  gcs_engine_run replaces md::simulate_brownian_dynamics: the per-step callback's
 // state updates run on the device (k_tail), and chunks of steps are replayed from a captured hipGraph.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: librccl.so.1 is opened at first use (dlopen)
+
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <cmath>
@@ -156,6 +159,21 @@ struct gcs_engine {
     int* dom_shared_flag = nullptr;  // [n] 1 = shared
     int dom_nshared = 0;
     int64_t dom_next = 0;
+    // engine-owned decomposed-run exchange (gcs_engine_domain_buffers) and its RCCL transport
+    float4* dom_send = nullptr;  // [npeer][cap + 1] rows: row 0 of a band = {count bits, 0, 0, 0}, then records
+    float4* dom_recv = nullptr;
+    int dom_cap = 0;
+    double* dom_red = nullptr;   // [nred]: local reduction + shared positions; dom_glob: the sum over domains
+    double* dom_glob = nullptr;
+    int dom_nred = 0;
+    int* dom_flags = nullptr;
+    int dom_peer_rank[kMaxPeers] = {};
+    ncclComm_t nccl = nullptr;
+    int nccl_ranks = 0;
+    hipGraphExec_t dgexec = nullptr;
+    hipGraph_t dgraph = nullptr;
+    int dg_steps = 0;
+    gcs_bd_config dg_cfg{};
 
     ForceArgs fa{};
     gcs_schedule sched{};
@@ -619,8 +637,9 @@ int ensure_list(gcs_engine* e)
     return GCS_OK;
 }
 
-// rebuild period: the skin must hold the largest displacement of ~6 sigma on each side of a pair for that many
-// steps (sigma = sqrt(2 T mu_max dt) per step); a particle that outruns it anyway is searched exactly (k_lstep)
+// rebuild period: the skin must hold the largest displacement of ~4.5 sigma on each side of a pair for that many
+// steps (sigma = sqrt(2 T mu_max dt) per step; C2: 8 steps at skin 0.4 rc); the rare particle that outruns it is
+// searched exactly (k_lstep), so the period trades rebuild cost against fallbacks, never correctness
 int auto_list_every(const gcs_engine* e, const gcs_bd_config* cfg)
 {
     if (e->list_every_opt > 0) return e->list_every_opt;
@@ -629,7 +648,7 @@ int auto_list_every(const gcs_engine* e, const gcs_bd_config* cfg)
     const double sigma = std::sqrt(2.0 * std::max(cfg->temperature, 0.0) * mu * cfg->timestep);
     const double half = 0.5 * (double)list_skin(e);
     if (!(sigma > 0)) return 64;
-    const double m = std::floor((half / (6.0 * sigma)) * (half / (6.0 * sigma)));
+    const double m = std::floor((half / (4.5 * sigma)) * (half / (4.5 * sigma)));
     return (int)std::min(64.0, std::max(1.0, m));
 }
 
@@ -764,6 +783,64 @@ void end_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_
     e->chain_step = first_step + steps;
     e->chain_version = e->topo_version;
 }
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------------
+// RCCL, opened at first use (no link-time dependency: only decomposed multi-GPU runs need it; a process that has
+// already loaded a librccl.so.1, e.g. torch's, shares that one through the soname)
+
+namespace {
+
+struct RcclApi {
+    bool tried = false;
+    void* h = nullptr;
+    decltype(&ncclGetUniqueId) getUniqueId = nullptr;
+    decltype(&ncclCommInitRank) commInitRank = nullptr;
+    decltype(&ncclCommDestroy) commDestroy = nullptr;
+    decltype(&ncclAllReduce) allReduce = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) groupStart = nullptr;
+    decltype(&ncclGroupEnd) groupEnd = nullptr;
+    decltype(&ncclGetErrorString) errorString = nullptr;
+};
+RcclApi g_rccl;
+
+const RcclApi* rccl()
+{
+    if (!g_rccl.tried) {
+        g_rccl.tried = true;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (h) {
+            g_rccl.getUniqueId = (decltype(g_rccl.getUniqueId))dlsym(h, "ncclGetUniqueId");
+            g_rccl.commInitRank = (decltype(g_rccl.commInitRank))dlsym(h, "ncclCommInitRank");
+            g_rccl.commDestroy = (decltype(g_rccl.commDestroy))dlsym(h, "ncclCommDestroy");
+            g_rccl.allReduce = (decltype(g_rccl.allReduce))dlsym(h, "ncclAllReduce");
+            g_rccl.send = (decltype(g_rccl.send))dlsym(h, "ncclSend");
+            g_rccl.recv = (decltype(g_rccl.recv))dlsym(h, "ncclRecv");
+            g_rccl.groupStart = (decltype(g_rccl.groupStart))dlsym(h, "ncclGroupStart");
+            g_rccl.groupEnd = (decltype(g_rccl.groupEnd))dlsym(h, "ncclGroupEnd");
+            g_rccl.errorString = (decltype(g_rccl.errorString))dlsym(h, "ncclGetErrorString");
+            if (g_rccl.getUniqueId && g_rccl.commInitRank && g_rccl.commDestroy && g_rccl.allReduce && g_rccl.send &&
+                g_rccl.recv && g_rccl.groupStart && g_rccl.groupEnd && g_rccl.errorString)
+                g_rccl.h = h;
+        }
+    }
+    return g_rccl.h ? &g_rccl : nullptr;
+}
+
+void rccl_comm_destroy(ncclComm_t c)
+{
+    if (const RcclApi* r = rccl()) (void)r->commDestroy(c);
+}
+
+#define NCCLCHK(expr)                                                                                         \
+    do {                                                                                                      \
+        ncclResult_t _r = (expr);                                                                             \
+        if (_r != ncclSuccess) return fail(GCS_EHIP, std::string(#expr) + ": " + rccl()->errorString(_r));   \
+    } while (0)
 
 }  // namespace
 
@@ -978,6 +1055,14 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->tent);
     dfree(e->noise);
     dfree(e->dom_regions);
+    dfree(e->dom_send);
+    dfree(e->dom_recv);
+    dfree(e->dom_red);
+    dfree(e->dom_glob);
+    dfree(e->dom_flags);
+    if (e->dgexec) (void)hipGraphExecDestroy(e->dgexec);
+    if (e->dgraph) (void)hipGraphDestroy(e->dgraph);
+    if (e->nccl) rccl_comm_destroy(e->nccl);
     dfree(e->dom_shared_idx);
     dfree(e->dom_shared_flag);
     dfree(e->c_keys);
@@ -1754,6 +1839,294 @@ int gcs_engine_domain_unpack(gcs_engine* e, const float* dev_in, const int32_t* 
     HIPCHK(hipSetDevice(e->device));
     launch_domain_unpack(e->stream, e->fa, (const float4*)dev_in, dev_counts, nbuf, cap);
     HIPCHK(hipGetLastError());
+    return GCS_OK;
+}
+
+// ---- engine-owned exchange: bands with the count in their header row, the reaction buffer, the flags --------------
+
+int gcs_engine_domain_buffers(gcs_engine* e, int32_t cap, int32_t* nred)
+{
+    if (!e) return fail(GCS_EINVAL, "null argument");
+    if (!e->dom) return fail(GCS_ESTATE, "gcs_engine_set_domain first");
+    if (cap < 1) return fail(GCS_EINVAL, "band capacity must be positive");
+    HIPCHK(hipSetDevice(e->device));
+    dfree(e->dom_send);
+    dfree(e->dom_recv);
+    dfree(e->dom_red);
+    dfree(e->dom_glob);
+    const size_t rows = (size_t)std::max(e->dom_npeer, 1) * (cap + 1);
+    const int nr = kDomainRed + 3 * e->dom_nshared;
+    int rc;
+    if ((rc = dalloc(&e->dom_send, rows)) || (rc = dalloc(&e->dom_recv, rows)) || (rc = dalloc(&e->dom_red, nr)) ||
+        (rc = dalloc(&e->dom_glob, nr)))
+        return rc;
+    if (!e->dom_flags && (rc = dalloc(&e->dom_flags, 1))) return rc;
+    HIPCHK(hipMemsetAsync(e->dom_send, 0, rows * sizeof(float4), e->stream));
+    HIPCHK(hipMemsetAsync(e->dom_recv, 0, rows * sizeof(float4), e->stream));
+    HIPCHK(hipMemsetAsync(e->dom_red, 0, nr * sizeof(double), e->stream));
+    HIPCHK(hipMemsetAsync(e->dom_glob, 0, nr * sizeof(double), e->stream));
+    HIPCHK(hipMemsetAsync(e->dom_flags, 0, sizeof(int), e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->dom_cap = cap;
+    e->dom_nred = nr;
+    if (nred) *nred = nr;
+    if (e->dgexec) (void)hipGraphExecDestroy(e->dgexec);
+    if (e->dgraph) (void)hipGraphDestroy(e->dgraph);
+    e->dgexec = nullptr;
+    e->dgraph = nullptr;
+    return GCS_OK;
+}
+
+namespace {
+
+// pack this step's bands into the send buffer (header rows zeroed first, counts land in them)
+void enqueue_band_pack(gcs_engine* e)
+{
+    const int stride = e->dom_cap + 1;
+    launch_band_headers_zero(e->stream, e->dom_send, e->dom_npeer, stride);
+    launch_domain_pack(e->stream, e->ctx, domain_args(e), e->dom_regions, e->dom_npeer, e->dom_send + 1,
+                       reinterpret_cast<int*>(e->dom_send), e->dom_cap, e->dom_flags, e->dom_shared_flag, stride,
+                       4 * stride);
+}
+
+void enqueue_band_unpack(gcs_engine* e)
+{
+    const int stride = e->dom_cap + 1;
+    if (e->dom_npeer > 0)
+        launch_domain_unpack(e->stream, e->fa, e->dom_recv + 1, reinterpret_cast<const int*>(e->dom_recv), e->dom_npeer,
+                             e->dom_cap, stride, 4 * stride);
+}
+
+// one decomposed step after its start (gcs_engine_domain_step primed the run): the domain kernels, the reaction
+// allreduce, the tail, the bands to and from every peer (one grouped send/recv per peer, the count in the band)
+int enqueue_rccl_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step)
+{
+    const RcclApi* r = rccl();
+    const ForceArgs a = domain_args(e);
+    const int n = e->n;
+    launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count,
+                      e->dom_lo - e->dom_halo, e->dom_hi + e->dom_halo);
+    enqueue_scan(e, false);
+    enqueue_sort(e);
+    launch_force(e->stream, kModeStep, e->waves, e->ctx, a, false);
+    launch_tail_reduce(e->stream, e->ctx, a, step_grid(e), e->dom_red);
+    launch_domain_shared_out(e->stream, e->ctx, a, e->dom_shared_idx, e->dom_nshared, e->dom_red);
+    NCCLCHK(r->allReduce(e->dom_red, e->dom_glob, e->dom_nred, ncclDouble, ncclSum, e->nccl, e->stream));
+    ForceArgs f = a;
+    f.ext_react = e->dom_glob;
+    const int sb = step_grid(e);
+    launch_tail(e->stream, e->ctx, f, sb, sb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
+    launch_domain_shared_in(e->stream, f, e->dom_shared_idx, e->dom_nshared, e->dom_glob);
+    enqueue_band_pack(e);
+    if (e->dom_npeer > 0) {
+        const size_t cnt = (size_t)4 * (e->dom_cap + 1);
+        NCCLCHK(r->groupStart());
+        for (int p = 0; p < e->dom_npeer; ++p) {
+            NCCLCHK(r->send(e->dom_send + (size_t)p * (e->dom_cap + 1), cnt, ncclFloat, e->dom_peer_rank[p], e->nccl,
+                            e->stream));
+            NCCLCHK(r->recv(e->dom_recv + (size_t)p * (e->dom_cap + 1), cnt, ncclFloat, e->dom_peer_rank[p], e->nccl,
+                            e->stream));
+        }
+        NCCLCHK(r->groupEnd());
+    }
+    enqueue_band_unpack(e);
+    HIPCHK(hipGetLastError());
+    (void)cfg;
+    (void)step;
+    return GCS_OK;
+}
+
+}  // namespace
+
+int gcs_rccl_unique_id(uint8_t* id)
+{
+    if (!id) return fail(GCS_EINVAL, "null argument");
+    const RcclApi* r = rccl();
+    if (!r) return fail(GCS_EHIP, "librccl.so.1 could not be opened");
+    ncclUniqueId u;
+    NCCLCHK(r->getUniqueId(&u));
+    std::memcpy(id, &u, sizeof(u));
+    return GCS_OK;
+}
+
+int gcs_engine_domain_rccl(gcs_engine* e, const uint8_t* id, int32_t nranks, int32_t rank, const int32_t* peer_ranks)
+{
+    if (!e || !id || (e->dom_npeer > 0 && !peer_ranks)) return fail(GCS_EINVAL, "null argument");
+    if (!e->dom_send) return fail(GCS_ESTATE, "gcs_engine_domain_buffers first");
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(GCS_EINVAL, "bad rank");
+    const RcclApi* r = rccl();
+    if (!r) return fail(GCS_EHIP, "librccl.so.1 could not be opened");
+    for (int p = 0; p < e->dom_npeer; ++p) {
+        if (peer_ranks[p] < 0 || peer_ranks[p] >= nranks || peer_ranks[p] == rank) return fail(GCS_EINVAL, "bad peer rank");
+        e->dom_peer_rank[p] = peer_ranks[p];
+    }
+    HIPCHK(hipSetDevice(e->device));
+    if (e->nccl) {
+        (void)r->commDestroy(e->nccl);
+        e->nccl = nullptr;
+    }
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    NCCLCHK(r->commInitRank(&e->nccl, nranks, u, rank));
+    e->nccl_ranks = nranks;
+    return GCS_OK;
+}
+
+int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps)
+{
+    if (!e || !cfg) return fail(GCS_EINVAL, "null argument");
+    if (!e->nccl) return fail(GCS_ESTATE, "gcs_engine_domain_rccl first");
+    if (steps < 0) return fail(GCS_EINVAL, "negative step count");
+    int64_t k = 0, k0 = 0;
+    int rc;
+    if (steps > 0 && !(e->dom_cont && e->dom_next == first_step)) {
+        // the run's first step primes through the step entry point (begin_run, both position buffers)
+        if ((rc = gcs_engine_domain_step(e, cfg, first_step, e->dom_red))) return rc;
+        const RcclApi* r = rccl();
+        NCCLCHK(r->allReduce(e->dom_red, e->dom_glob, e->dom_nred, ncclDouble, ncclSum, e->nccl, e->stream));
+        if ((rc = gcs_engine_domain_finish(e, e->dom_glob))) return rc;
+        enqueue_band_pack(e);
+        if (e->dom_npeer > 0) {
+            const size_t cnt = (size_t)4 * (e->dom_cap + 1);
+            NCCLCHK(r->groupStart());
+            for (int p = 0; p < e->dom_npeer; ++p) {
+                NCCLCHK(r->send(e->dom_send + (size_t)p * (e->dom_cap + 1), cnt, ncclFloat, e->dom_peer_rank[p],
+                                e->nccl, e->stream));
+                NCCLCHK(r->recv(e->dom_recv + (size_t)p * (e->dom_cap + 1), cnt, ncclFloat, e->dom_peer_rank[p],
+                                e->nccl, e->stream));
+            }
+            NCCLCHK(r->groupEnd());
+        }
+        enqueue_band_unpack(e);
+        k = k0 = 1;  // gcs_engine_domain_finish flipped the host parity of this step
+    }
+    // the rest: G-step chunks captured once into a graph (kernels and collectives), the remainder eagerly
+    const int G = e->graph_steps;
+    if (G > 0 && steps - k >= G) {
+        const bool same = e->dgexec && e->dg_steps == G && std::memcmp(&e->dg_cfg, cfg, sizeof(*cfg)) == 0;
+        if (!same) {
+            if (e->dgexec) (void)hipGraphExecDestroy(e->dgexec);
+            if (e->dgraph) (void)hipGraphDestroy(e->dgraph);
+            e->dgexec = nullptr;
+            e->dgraph = nullptr;
+            HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+            for (int q = 0; q < G; ++q) {
+                if ((rc = enqueue_rccl_step(e, cfg, first_step + k + q))) {
+                    hipGraph_t g = nullptr;
+                    (void)hipStreamEndCapture(e->stream, &g);
+                    if (g) (void)hipGraphDestroy(g);
+                    return rc;
+                }
+            }
+            HIPCHK(hipStreamEndCapture(e->stream, &e->dgraph));
+            HIPCHK(hipGraphInstantiate(&e->dgexec, e->dgraph, nullptr, nullptr, 0));
+            e->dg_steps = G;
+            e->dg_cfg = *cfg;
+        }
+        for (; steps - k >= G; k += G) HIPCHK(hipGraphLaunch(e->dgexec, e->stream));
+    }
+    for (; k < steps; ++k)
+        if ((rc = enqueue_rccl_step(e, cfg, first_step + k))) return rc;
+    if ((steps - k0) & 1) e->parity ^= 1;
+    if (steps > 0) {
+        e->dom_cont = true;
+        e->dom_next = first_step + steps;
+    }
+    e->chain_valid = false;
+    return GCS_OK;
+}
+
+// ---- host-staged transport (any process layout, e.g. several processes on one device): one step's halves ------
+
+int gcs_engine_domain_step_host(gcs_engine* e, const gcs_bd_config* cfg, int64_t step, double* red, int32_t nred)
+{
+    if (!e || !red) return fail(GCS_EINVAL, "null argument");
+    if (!e->dom_red) return fail(GCS_ESTATE, "gcs_engine_domain_buffers first");
+    if (nred != e->dom_nred) return fail(GCS_EINVAL, "reaction buffer size does not match");
+    int rc = gcs_engine_domain_step(e, cfg, step, e->dom_red);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(red, e->dom_red, nred * sizeof(double), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return GCS_OK;
+}
+
+int gcs_engine_domain_finish_host(gcs_engine* e, const double* glob, int32_t nred)
+{
+    if (!e || !glob) return fail(GCS_EINVAL, "null argument");
+    if (!e->dom_glob) return fail(GCS_ESTATE, "gcs_engine_domain_buffers first");
+    if (nred != e->dom_nred) return fail(GCS_EINVAL, "reaction buffer size does not match");
+    HIPCHK(hipMemcpyAsync(e->dom_glob, glob, nred * sizeof(double), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));  // glob is the caller's
+    return gcs_engine_domain_finish(e, e->dom_glob);
+}
+
+int gcs_engine_domain_pack_host(gcs_engine* e, float* bands)
+{
+    if (!e) return fail(GCS_EINVAL, "null argument");
+    if (!e->dom_send) return fail(GCS_ESTATE, "gcs_engine_domain_buffers first");
+    HIPCHK(hipSetDevice(e->device));
+    enqueue_band_pack(e);
+    HIPCHK(hipGetLastError());
+    if (!bands) return GCS_OK;  // packed on the device only (in-process transport: gcs_engine_domain_receive)
+    if (e->dom_npeer > 0)
+        HIPCHK(hipMemcpyAsync(bands, e->dom_send, (size_t)e->dom_npeer * (e->dom_cap + 1) * sizeof(float4),
+                              hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return GCS_OK;
+}
+
+int gcs_engine_domain_unpack_host(gcs_engine* e, const float* bands)
+{
+    if (!e || (e->dom_npeer > 0 && !bands)) return fail(GCS_EINVAL, "null argument");
+    if (!e->dom_recv) return fail(GCS_ESTATE, "gcs_engine_domain_buffers first");
+    if (e->dom_npeer == 0) return GCS_OK;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipMemcpyAsync(e->dom_recv, bands, (size_t)e->dom_npeer * (e->dom_cap + 1) * sizeof(float4),
+                          hipMemcpyHostToDevice, e->stream));
+    enqueue_band_unpack(e);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));  // bands is the caller's
+    return GCS_OK;
+}
+
+int gcs_engine_domain_receive(gcs_engine* dst, int32_t dst_slot, gcs_engine* src, int32_t src_slot)
+{
+    if (!dst || !src) return fail(GCS_EINVAL, "null argument");
+    if (!dst->dom_recv || !src->dom_send) return fail(GCS_ESTATE, "gcs_engine_domain_buffers first");
+    if (dst->dom_cap != src->dom_cap) return fail(GCS_EINVAL, "band capacities differ");
+    if (dst_slot < 0 || dst_slot >= dst->dom_npeer || src_slot < 0 || src_slot >= src->dom_npeer)
+        return fail(GCS_EINVAL, "bad band slot");
+    if (dst->device != src->device) return fail(GCS_EINVAL, "in-process bands move within one device");
+    HIPCHK(hipSetDevice(dst->device));
+    hipEvent_t ev;
+    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ev, src->stream));
+    HIPCHK(hipStreamWaitEvent(dst->stream, ev, 0));
+    const size_t rows = (size_t)dst->dom_cap + 1;
+    HIPCHK(hipMemcpyAsync(dst->dom_recv + (size_t)dst_slot * rows, src->dom_send + (size_t)src_slot * rows,
+                          rows * sizeof(float4), hipMemcpyDeviceToDevice, dst->stream));
+    HIPCHK(hipEventDestroy(ev));
+    return GCS_OK;
+}
+
+int gcs_engine_domain_unpack_received(gcs_engine* e)
+{
+    if (!e) return fail(GCS_EINVAL, "null argument");
+    if (!e->dom_recv) return fail(GCS_ESTATE, "gcs_engine_domain_buffers first");
+    HIPCHK(hipSetDevice(e->device));
+    enqueue_band_unpack(e);
+    HIPCHK(hipGetLastError());
+    return GCS_OK;
+}
+
+int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags)
+{
+    if (!e || !flags) return fail(GCS_EINVAL, "null argument");
+    *flags = 0;
+    if (!e->dom_flags) return GCS_OK;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipMemcpyAsync(flags, e->dom_flags, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
     return GCS_OK;
 }
 

@@ -287,11 +287,14 @@ void launch_quantize(hipStream_t s, const float4* pos, float* out, int n, int bi
 constexpr int kMaxPeers = 16;
 constexpr int kDomainRed = 8;  // allreduce buffer: [0, 8) the local reduction, then 3 doubles per shared particle
 void launch_domain_pack(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const float2* regions, int npeer,
-                        float4* out, int* counts, int cap, int* flags, const int* shared);
+                        float4* out, int* counts, int cap, int* flags, const int* shared, int ostride = 0,
+                        int cstride = 1);
+void launch_band_headers_zero(hipStream_t s, float4* bands, int npeer, int stride);
 void launch_domain_shared_out(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const int* idx, int nshared,
                               double* buf);
 void launch_domain_shared_in(hipStream_t s, const ForceArgs& a, const int* idx, int nshared, const double* buf);
-void launch_domain_unpack(hipStream_t s, const ForceArgs& a, const float4* in, const int* counts, int nbuf, int cap);
+void launch_domain_unpack(hipStream_t s, const ForceArgs& a, const float4* in, const int* counts, int nbuf, int cap,
+                          int istride = 0, int cstride = 1);
 void launch_tail_reduce(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int fblocks, double* out);
 
 inline int force_blocks(int n) { return (n + kTile - 1) / kTile; }

@@ -2736,8 +2736,7 @@ __global__ __launch_bounds__(64 * kListWaves) void k_lstep(DevCtx* __restrict__ 
     // a particle whose own displacement exceeds this may miss a partner in its list (0.999: fp32 margin)
     const float slack = 0.999f * a.list_skin - D - fmaxf(rc - ctx->lrc_b, 0.f);
     const int par = ctx->parity;
-    const float4* __restrict__ pc = par ? a.pos1 : a.pos0;  // particle order (bonded partners, output)
-    float4* __restrict__ pn = par ? a.pos0 : a.pos1;
+    float4* __restrict__ pn = par ? a.pos0 : a.pos1;  // particle order (bonded partners read ctx->parity's)
     const float4* __restrict__ qc = par ? a.psort1 : a.psort0;  // slot order (pair partners)
     float4* __restrict__ qn = par ? a.psort0 : a.psort1;
     const int cap = a.list_cap;

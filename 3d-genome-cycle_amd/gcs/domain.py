@@ -16,11 +16,18 @@ Protocol (kernels in csrc/domain.hip, which proves the invariants):
     both of its position buffers.  Peers are the domains whose regions overlap (possibly more than the two
     neighbours when slabs are thinner than the halo).
 
-Backends: `EngineDomain` (the HIP engine; buffers are torch device tensors whose pointers go through the C ABI;
-torch's device runtime must be initialised before libgcs.so is loaded, so both share one HIP runtime)
-and `OracleDomain` (tests only: the CPU oracle, one step per call).  Transports: `LocalTransport` (all domains in
-one process, e.g. several engines on one GPU for parity tests) and `DistTransport` (one domain per rank over
-torch.distributed: RCCL for engines, ordered on the engine's HIP stream; gloo for the CPU oracle tests).
+Every exchange buffer is the engine's own (gcs_engine_domain_buffers): a band per peer whose first row holds its
+count, so one message per peer carries both, and the reaction/shared-position buffer of the allreduce.
+
+Transports:
+  * `RcclRun` -- production, one domain per GPU: the engine itself issues ncclAllReduce and one grouped
+    ncclSend/ncclRecv per peer on its HIP stream (gcs_engine_domain_run), chunks of steps captured in a hipGraph; the
+    host only hands the communicator id to the ranks (torch.distributed object broadcast, CPU).
+  * `LocalTransport` -- several domains in one process on one device: the reaction summed on the host in domain
+    order, the bands copied device-to-device between the engines (gcs_engine_domain_receive).
+  * `DistTransport` -- host-staged over torch.distributed (gloo, CPU tensors): any process layout, including several
+    processes sharing one device (RCCL refuses two ranks on one GPU); also the transport of the CPU oracle domains
+    the tests use (tests/oracle_domain.py).
 """
 from __future__ import annotations
 
@@ -85,6 +92,19 @@ def peers_of(d: int, slabs, halo: float):
     return out
 
 
+def band_capacity(x, slabs, halo, d, margin: float = 1.5, floor: int = 1024) -> int:
+    """Records per band for domain d: its particles inside the largest peer region at the start, times `margin`
+    (the bands drift slowly; an overflow is flagged on the device and raised by check()), at least `floor`."""
+    z = np.asarray(x)[:, 2]
+    lo, hi = slabs[d]
+    mine = (z >= lo) & (z < hi)
+    most = 0
+    for p in peers_of(d, slabs, halo):
+        rlo, rhi = region(slabs[p], halo)
+        most = max(most, int((mine & (z >= rlo) & (z < rhi)).sum()))
+    return int(min(z.size, max(floor, np.ceil(margin * most))))
+
+
 def _finite(v):
     return float(np.clip(v, -3.0e38, 3.0e38))
 
@@ -103,56 +123,45 @@ class _Domain:
 
 
 class EngineDomain(_Domain):
-    """A gcs.engine.Engine running one domain; exchange buffers are torch tensors on the engine's device."""
+    """A gcs.engine.Engine running one domain with its own exchange buffers (no torch tensors: host staging in numpy
+    for the host-staged transports, device-to-device or RCCL otherwise)."""
 
-    def __init__(self, engine, index, slabs, halo, cap=None, device=None, shared=()):
-        import torch
+    def __init__(self, engine, index, slabs, halo, cap=None, shared=()):
         super().__init__(index, slabs, halo)
         self.shared = np.asarray(shared, dtype=np.int64).reshape(-1)
         self.e = engine
-        self.torch = torch
-        self.device = torch.device("cuda", device if device is not None else torch.cuda.current_device())
         n = engine.n
         self.cap = int(cap if cap is not None else n)
-        npeer = max(1, len(self.peers))
-        f64, f32, i32 = torch.float64, torch.float32, torch.int32
-        nred = 8 + 3 * self.shared.size  # local reduction + shared particles' positions (csrc/domain.hip)
-        self.red = torch.zeros(nred, dtype=f64, device=self.device)
-        self.glob = torch.zeros(nred, dtype=f64, device=self.device)
-        self.out = torch.zeros((npeer, self.cap, 4), dtype=f32, device=self.device)
-        self.counts = torch.zeros(npeer, dtype=i32, device=self.device)
-        self.inb = torch.zeros_like(self.out)
-        self.inc = torch.zeros_like(self.counts)
-        self.flags = torch.zeros(1, dtype=i32, device=self.device)
         lo, hi = (_finite(v) for v in self.slab)
         engine.set_domain(lo, hi, halo, self.regions)
         engine.set_domain_shared(self.shared)
-        self._stream = None
-
-    def stream(self):
-        """The engine's HIP stream as a torch stream (collectives are ordered on it, no host synchronisation)."""
-        if self._stream is None:
-            self._stream = self.torch.cuda.ExternalStream(self.e.stream_handle(), device=self.device)
-        return self._stream
+        self.nred = engine.domain_buffers(self.cap)
+        npeer = max(1, len(self.peers))
+        self.red = np.zeros(self.nred)   # local reduction (8) + shared particles' positions (csrc/domain.hip)
+        self.glob = np.zeros(self.nred)  # its sum over domains
+        self.out = np.zeros((npeer, self.cap + 1, 4), dtype=np.float32)  # host staging: [peer][header + cap][4]
+        self.inb = np.zeros_like(self.out)
 
     def step(self, st, bd):
-        self.e.domain_step(st, self.red.data_ptr(), **bd)
+        self.e.domain_step_host(st, self.red, **bd)
 
     def finish(self):
-        self.e.domain_finish(self.glob.data_ptr())
+        self.e.domain_finish_host(self.glob)
 
-    def pack(self):
-        self.e.domain_pack(self.out.data_ptr(), self.counts.data_ptr(), self.cap, self.flags.data_ptr())
+    def pack(self, staged=True):
+        self.e.domain_pack_host(self.out if staged else None)
 
     def unpack(self):
-        self.e.domain_unpack(self.inb.data_ptr(), self.inc.data_ptr(), len(self.peers), self.cap)
+        self.e.domain_unpack_host(self.inb)
+
+    def band_count(self, k):
+        return int(self.out[k, 0, :1].view(np.int32)[0])
 
     def synchronize(self):
         self.e.synchronize()
 
     def flag_bits(self):
-        self.e.synchronize()
-        return int(self.flags.item())
+        return self.e.domain_flags()
 
     def positions(self):
         return self.e.get_positions()
@@ -161,165 +170,112 @@ class EngineDomain(_Domain):
         return self.e.get_context()
 
 
-class OracleDomain(_Domain):
-    """TEST INFRASTRUCTURE: the CPU oracle running one domain (oracle.OracleSystem with set_domain), fp64."""
-
-    def __init__(self, osys, index, slabs, halo, schedule: dict, shared=()):
-        import torch
-        super().__init__(index, slabs, halo)
-        self.shared = np.asarray(shared, dtype=np.int64).reshape(-1)
-        self.o = osys
-        self.torch = torch
-        self.sched = dict(schedule)
-        osys.set_schedule(**dict(schedule, update_wall=0))  # the wall update sees the allreduced reaction
-        lo, hi = self.slab
-        osys.set_domain(lo, hi)
-        n = osys.n
-        self.cap = n
-        npeer = max(1, len(self.peers))
-        self.red = torch.zeros(8 + 3 * self.shared.size, dtype=torch.float64)
-        self.glob = torch.zeros_like(self.red)
-        self.out = torch.zeros((npeer, n, 4), dtype=torch.float64)
-        self.counts = torch.zeros(npeer, dtype=torch.int32)
-        self.inb = torch.zeros_like(self.out)
-        self.inc = torch.zeros_like(self.counts)
-        self._old = None
-        self._flags = 0
-
-    def step(self, st, bd):
-        self._old = self.o.get_positions()
-        self.o.run(1, first_step=st, temperature=bd["temperature"], timestep=bd["timestep"], seed=bd["seed"])
-        c = self.o.get_context()
-        self.red[:3] = self.torch.tensor(c["inward_reaction"], dtype=self.torch.float64)
-        self.red[3:6] = self.torch.tensor(c["outward_reaction"], dtype=self.torch.float64)
-        if self.shared.size:
-            new = self.o.get_positions()[self.shared]
-            own = self.owned_mask(self._old[self.shared])
-            self.red[8:] = self.torch.from_numpy(np.where(own[:, None], new, 0.0).reshape(-1))
-
-    def finish(self):
-        # simulation_driver_interphase.cpp:80-90 with the reaction summed over domains
-        s = self.sched
-        c = self.o.get_context()
-        if s.get("update_wall", 0):
-            w = np.array(c["wall_semiaxes"])
-            R = self.glob[:3].numpy() + self.glob[3:6].numpy()
-            w = w + s["timestep"] * s["wall_mobility"] * (R - np.asarray(s["wall_semiaxes_spring"]) * w)
-            c["wall_semiaxes"] = list(w)
-        c["inward_reaction"] = list(self.glob[:3].numpy())
-        c["outward_reaction"] = list(self.glob[3:6].numpy())
-        self.o.set_context(c)
-        if self.shared.size:
-            x = self.o.get_positions()
-            x[self.shared] = self.glob[8:].numpy().reshape(-1, 3)
-            self.o.set_positions(x)
-
-    def pack(self):
-        new = self.o.get_positions()
-        old = self._old
-        own = self.owned_mask(old)
-        self.counts.zero_()
-        for k, (lo, hi) in enumerate(self.regions):
-            sel = own & (((old[:, 2] >= lo) & (old[:, 2] < hi)) | ((new[:, 2] >= lo) & (new[:, 2] < hi)))
-            idx = np.nonzero(sel)[0]
-            self.out[k, : idx.size, :3] = self.torch.from_numpy(new[idx])
-            self.out[k, : idx.size, 3] = self.torch.from_numpy(idx.astype(np.float64))
-            self.counts[k] = int(idx.size)
-
-    def unpack(self):
-        if not self.peers:
-            return
-        x = self.o.get_positions()
-        for k in range(len(self.peers)):
-            c = int(self.inc[k])
-            idx = self.inb[k, :c, 3].numpy().astype(np.int64)
-            x[idx] = self.inb[k, :c, :3].numpy()
-        self.o.set_positions(x)
-
-    def synchronize(self):
-        pass
-
-    def flag_bits(self):
-        return self._flags
-
-    def positions(self):
-        return self.o.get_positions()
-
-    def context(self):
-        return self.o.get_context()
-
-
 class LocalTransport:
-    """All domains in this process (indexed by domain number).  Fixed-order reaction sum; host-synchronous."""
+    """All domains in this process (indexed by domain number): the reaction summed in domain order on the host;
+    engine bands move device-to-device (one device), other domains' through their host arrays."""
 
     def __init__(self, domains):
         self.domains = domains
-
-    def _sync(self):
-        for d in self.domains:
-            d.synchronize()
-        t = self.domains[0].torch
-        if t.cuda.is_available():
-            t.cuda.synchronize()
+        self.device = all(isinstance(d, EngineDomain) for d in domains)
 
     def allreduce(self):
-        self._sync()
-        tot = self.domains[0].red.clone()
+        tot = self.domains[0].red.copy()
         for d in self.domains[1:]:
-            tot += d.red.to(tot.device)
+            tot += d.red
         for d in self.domains:
-            d.glob.copy_(tot)
-        self._sync()
+            d.glob[:] = tot
+
+    def pack(self):
+        for d in self.domains:
+            d.pack(staged=False) if self.device else d.pack()
 
     def exchange(self):
-        self._sync()
         for d in self.domains:
             for k, p in enumerate(d.peers):
                 q = self.domains[p]
                 kk = q.peers.index(d.index)
-                q.inb[kk].copy_(d.out[k])
-                q.inc[kk] = d.counts[k]
-        self._sync()
+                if self.device:
+                    q.e.domain_receive(kk, d.e, k)
+                else:
+                    q.inb[kk] = d.out[k]
+
+    def unpack(self):
+        for d in self.domains:
+            d.e.domain_unpack_received() if self.device else d.unpack()
 
 
 class DistTransport:
-    """One domain per rank over torch.distributed: RCCL (backend "nccl") for engines, with the collectives
-    ordered on the engine's HIP stream (no host synchronisation); gloo for CPU (oracle) domains."""
+    """One domain per rank over torch.distributed with host staging (gloo, CPU tensors): the reaction allreduce and
+    one send/recv of the band with each peer."""
 
     def __init__(self, domain, dist):
         self.d = domain
         self.dist = dist
-        self.gpu = isinstance(domain, EngineDomain)
-        if self.gpu and dist.get_backend() != "nccl":
-            raise DomainError("engine domains exchange over RCCL (backend 'nccl')")
-
-    def _on_stream(self):
-        import contextlib
-        return self.d.torch.cuda.stream(self.d.stream()) if self.gpu else contextlib.nullcontext()
 
     def allreduce(self):
-        with self._on_stream():
-            self.d.glob.copy_(self.d.red)
-            self.dist.all_reduce(self.d.glob)
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(self.d.red, dtype=np.float64))
+        self.dist.all_reduce(t)
+        self.d.glob[:] = t.numpy()
+
+    def pack(self):
+        self.d.pack()
 
     def exchange(self):
+        import torch
         d, dist = self.d, self.dist
         if not d.peers:
             return
-        with self._on_stream():
-            ops = []
-            for k, p in enumerate(d.peers):
-                ops.append(dist.P2POp(dist.isend, d.out[k], p))
-                ops.append(dist.P2POp(dist.isend, d.counts[k:k + 1], p))
-                ops.append(dist.P2POp(dist.irecv, d.inb[k], p))
-                ops.append(dist.P2POp(dist.irecv, d.inc[k:k + 1], p))
-            for r in dist.batch_isend_irecv(ops):
-                r.wait()
+        ops, recv = [], []
+        for k, p in enumerate(d.peers):
+            ops.append(dist.P2POp(dist.isend, torch.from_numpy(np.ascontiguousarray(d.out[k])), p))
+            r = torch.empty(d.inb[k].shape, dtype=torch.from_numpy(d.inb[k]).dtype)
+            recv.append(r)
+            ops.append(dist.P2POp(dist.irecv, r, p))
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        for k, r in enumerate(recv):
+            d.inb[k] = r.numpy()
+
+    def unpack(self):
+        self.d.unpack()
+
+
+class RcclRun:
+    """Production decomposed run: one EngineDomain per rank (one GPU each), the whole step sequence -- kernels,
+    ncclAllReduce of the reaction, grouped ncclSend/ncclRecv of the bands -- issued by the engine on its stream
+    (gcs_engine_domain_run); torch.distributed (any backend) only carries the communicator id at setup."""
+
+    def __init__(self, domain: EngineDomain, dist):
+        from .engine import rccl_unique_id
+        self.d = domain
+        self.domains = [domain]
+        rank, world = dist.get_rank(), dist.get_world_size()
+        box = [rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        domain.e.domain_rccl(box[0], world, rank, domain.peers)
+
+    def run(self, steps, first_step=0, temperature=1.0, timestep=1e-5, seed=0):
+        self.d.e.domain_run(steps, first_step=first_step, temperature=temperature, timestep=timestep, seed=seed)
+
+    def check(self):
+        _raise_flags(self.d.flag_bits())
+
+    def local_positions(self, n):
+        return DecomposedRun.local_positions(self, n)
+
+
+def _raise_flags(bits):
+    if bits & FLAG_BOND:
+        raise DomainError("a bond is longer than the domain halo: raise the halo")
+    if bits & FLAG_CAPACITY:
+        raise DomainError("a band exceeded the exchange buffer capacity: raise cap")
 
 
 class DecomposedRun:
-    """Steps of one trajectory split over domains: step -> allreduce(reaction) -> finish -> pack -> exchange ->
-    unpack.  `domains`: the domains of this process; `transport`: LocalTransport or DistTransport."""
+    """Steps of one trajectory split over domains, driven from the host: step -> allreduce(reaction) -> finish ->
+    pack -> exchange -> unpack.  `domains`: the domains of this process; `transport`: LocalTransport or
+    DistTransport (RcclRun drives the same sequence from inside the engine)."""
 
     def __init__(self, domains, transport):
         self.domains = list(domains)
@@ -333,20 +289,15 @@ class DecomposedRun:
             self.tr.allreduce()
             for d in self.domains:
                 d.finish()
-            for d in self.domains:
-                d.pack()
+            self.tr.pack()
             self.tr.exchange()
-            for d in self.domains:
-                d.unpack()
+            self.tr.unpack()
 
     def check(self):
         bits = 0
         for d in self.domains:
             bits |= d.flag_bits()
-        if bits & FLAG_BOND:
-            raise DomainError("a bond is longer than the domain halo: raise the halo")
-        if bits & FLAG_CAPACITY:
-            raise DomainError("a band exceeded the exchange buffer capacity: raise cap")
+        _raise_flags(bits)
 
     def local_positions(self, n):
         """(positions, owned mask) of this process's domains, each particle taken from its owner."""
@@ -360,7 +311,7 @@ class DecomposedRun:
         return x, m
 
 
-def gather_positions(run: DecomposedRun, n: int, dist=None):
+def gather_positions(run, n: int, dist=None):
     """Whole-system positions from the owners (every particle owned exactly once)."""
     x, m = run.local_positions(n)
     if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:

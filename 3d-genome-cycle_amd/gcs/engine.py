@@ -6,7 +6,9 @@ through one force-field composition (gcs.interphase / gcs.mitotic).
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
+import weakref
 
 import numpy as np
 
@@ -86,6 +88,17 @@ def make_bd(temperature=1.0, timestep=1e-5, spacestep=0.0, seed=0, noise=A.NOISE
     return c
 
 
+_live = weakref.WeakSet()
+
+
+@atexit.register
+def _close_live_engines():
+    # engines still alive at interpreter exit are destroyed here, while the HIP runtime (and RCCL) are intact:
+    # a destructor run from the C library's own exit handlers would free device memory of a torn-down runtime
+    for e in list(_live):
+        e.close()
+
+
 class Engine:
     """One simulated system on one HIP device (md::system + md::simulate_brownian_dynamics)."""
 
@@ -102,6 +115,7 @@ class Engine:
         h = C.c_void_p()
         A.check(self._lib.gcs_engine_create(C.byref(d), C.byref(h)))
         self._h = h
+        _live.add(self)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -304,6 +318,46 @@ class Engine:
         A.check(self._lib.gcs_engine_domain_unpack(self._h, C.c_void_p(in_ptr), C.c_void_p(counts_ptr), int(nbuf),
                                                    int(cap)))
 
+    # engine-owned exchange of a decomposed run (include/gcs.h "Engine-owned exchange")
+    def domain_buffers(self, cap) -> int:
+        nred = C.c_int32()
+        A.check(self._lib.gcs_engine_domain_buffers(self._h, int(cap), C.byref(nred)))
+        return int(nred.value)
+
+    def domain_rccl(self, uid: bytes, nranks, rank, peer_ranks):
+        buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        pr = (C.c_int32 * max(1, len(peer_ranks)))(*[int(p) for p in peer_ranks])
+        A.check(self._lib.gcs_engine_domain_rccl(self._h, buf, int(nranks), int(rank), pr))
+
+    def domain_run(self, steps, first_step=0, temperature=1.0, timestep=1e-5, seed=0):
+        cfg = make_bd(temperature, timestep, 0.0, seed, A.NOISE_PHILOX)
+        A.check(self._lib.gcs_engine_domain_run(self._h, C.byref(cfg), int(first_step), int(steps)))
+
+    def domain_step_host(self, step, red, temperature=1.0, timestep=1e-5, seed=0):
+        cfg = make_bd(temperature, timestep, 0.0, seed, A.NOISE_PHILOX)
+        A.check(self._lib.gcs_engine_domain_step_host(self._h, C.byref(cfg), int(step), _pd(red), red.size))
+
+    def domain_finish_host(self, glob):
+        A.check(self._lib.gcs_engine_domain_finish_host(self._h, _pd(glob), glob.size))
+
+    def domain_pack_host(self, bands):
+        A.check(self._lib.gcs_engine_domain_pack_host(
+            self._h, bands.ctypes.data_as(C.POINTER(C.c_float)) if bands is not None else None))
+
+    def domain_unpack_host(self, bands):
+        A.check(self._lib.gcs_engine_domain_unpack_host(self._h, bands.ctypes.data_as(C.POINTER(C.c_float))))
+
+    def domain_receive(self, slot, src, src_slot):
+        A.check(self._lib.gcs_engine_domain_receive(self._h, int(slot), src._h, int(src_slot)))
+
+    def domain_unpack_received(self):
+        A.check(self._lib.gcs_engine_domain_unpack_received(self._h))
+
+    def domain_flags(self) -> int:
+        f = C.c_int32()
+        A.check(self._lib.gcs_engine_domain_flags(self._h, C.byref(f)))
+        return int(f.value)
+
     def profile(self, steps, first_step=0, temperature=1.0, timestep=1e-5, seed=0, noise=A.NOISE_PHILOX) -> dict:
         cfg = make_bd(temperature, timestep, 0.0, seed, noise)
         p = A.Profile()
@@ -318,6 +372,14 @@ class Engine:
         s = A.ListStats()
         A.check(self._lib.gcs_engine_get_list_stats(self._h, C.byref(s)))
         return {k: getattr(s, k) for k, _ in A.ListStats._fields_}
+
+
+def rccl_unique_id() -> bytes:
+    """An RCCL communicator id (rank 0 draws it; every rank passes it to Engine.domain_rccl)."""
+    lib = A.load()
+    buf = (C.c_uint8 * 128)()
+    A.check(lib.gcs_rccl_unique_id(buf))
+    return bytes(buf)
 
 
 def device_count() -> int:

@@ -53,8 +53,8 @@ STATE_FILE = ROOT / "benchdata" / "c2_interphase_step300000.npz"
 
 
 def dist_setup(backend="gloo"):
-    """gloo on CPU tensors for replica runs (barrier + max only: no data-path collective); "nccl" (RCCL) for
-    decomposed runs, whose band exchange and reaction allreduce are the data path."""
+    """gloo on CPU tensors: the barrier, the max over ranks and (decomposed runs) the RCCL id hand-out; the
+    decomposed runs' data path (reaction allreduce, band exchange) is RCCL issued by the engine itself."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -315,12 +315,13 @@ def read_traffic(fused=3):
 
 def decomp_main(args):
     """One trajectory split into z-slab domains (gcs.domain; C5 of SURVEY 8e).  value = N x steps / max-over-ranks
-    time of the whole decomposed step loop (force, update, reaction allreduce, band exchange)."""
-    import torch
-    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-    torch.zeros(1, device="cuda")  # one HIP runtime per process: torch's first, libgcs.so binds to it
+    time of the whole decomposed step loop (force, update, reaction allreduce, band exchange).  Under torchrun: one
+    domain per GPU, the engine issues the RCCL collectives itself (gcs.domain.RcclRun); one process: K domains on
+    this GPU, bands moved device-to-device (LocalTransport)."""
+    from gcs import _abi as A
     from gcs import domain as D
-    world, rank, local, dist = dist_setup("nccl")
+    world, rank, local, dist = dist_setup()
+    A.load()
     cfg = bench_config(args.config)
     state = load_state() if args.config == "c2" else None
     design = design_maker(args.config)(master_seed=1)
@@ -331,11 +332,11 @@ def decomp_main(args):
     mine = [rank] if world > 1 else list(range(ndom))
     doms = []
     window = window_start(args.config)
+    cap = max(D.band_capacity(x0, slabs, halo, d) for d in range(ndom))  # one size: bands move between domains
     for d in mine:
         e = make_engine(design, cfg, local, window, state)
-        doms.append(D.EngineDomain(e, d, slabs, halo, device=local, shared=D.shared_particles(design)))
-    tr = D.DistTransport(doms[0], dist) if world > 1 else D.LocalTransport(doms)
-    run = D.DecomposedRun(doms, tr)
+        doms.append(D.EngineDomain(e, d, slabs, halo, cap=cap, shared=D.shared_particles(design)))
+    run = D.RcclRun(doms[0], dist) if world > 1 else D.DecomposedRun(doms, D.LocalTransport(doms))
     seed = replica_noise_seed(0)
     run.run(args.warmup, first_step=window, seed=seed, timestep=cfg.timestep)
     for d in doms:
@@ -350,7 +351,6 @@ def decomp_main(args):
     el_max = max_over_ranks(dist, el)
     run.check()
     n = design.n
-    bands = [int(c) for d in doms for c in d.counts[: len(d.peers)].tolist()]
     if rank == 0:
         line = {
             "metric": "bead-updates/sec (whole node), decomposed single trajectory",
@@ -358,11 +358,14 @@ def decomp_main(args):
             "warmup": args.warmup, "ms_per_step": el_max * 1e3 / args.steps, "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, one trajectory in "
-                                   f"{ndom} z-slab domains ({'RCCL' if world > 1 else 'in-process, one GPU'})",
+                                   f"{ndom} z-slab domains ({'RCCL from the engine' if world > 1 else 'in-process, one GPU'})",
                        "particles": n, "domains": ndom, "halo": halo, "parallelism": f"domains{ndom}",
-                       "band_sizes_rank0": bands, "peers_rank0": doms[0].peers},
+                       "band_capacity_rank0": doms[0].cap, "peers_rank0": doms[0].peers,
+                       "bytes_per_peer_per_step": 16 * (doms[0].cap + 1)},
         }
         print(json.dumps(line), flush=True)
+    for d in doms:
+        d.e.close()  # RCCL communicators go with their engines
     if dist is not None:
         dist.destroy_process_group()
 

@@ -309,6 +309,31 @@ int gcs_engine_domain_pack(gcs_engine* e, float* dev_out, int32_t* dev_counts, i
 int gcs_engine_domain_unpack(gcs_engine* e, const float* dev_in, const int32_t* dev_counts, int32_t nbuf,
                              int32_t cap);
 
+/* Engine-owned exchange of a decomposed run (C5): band buffers of `cap` records per peer (the band's first row
+ * holds its count, so one message per peer carries both), the reaction/shared-position allreduce buffer of
+ * *nred doubles, the overflow flags.  After gcs_engine_set_domain / _set_domain_shared. */
+int gcs_engine_domain_buffers(gcs_engine* e, int32_t cap, int32_t* nred);
+/* RCCL transport (one domain per GPU): rank 0 draws the communicator id, the host hands it to every rank over any
+ * channel; peer_ranks[p] is the rank of the p-th peer region given to gcs_engine_set_domain.  librccl.so.1 is
+ * opened at first use. */
+int gcs_rccl_unique_id(uint8_t* id /* [128] */);
+int gcs_engine_domain_rccl(gcs_engine* e, const uint8_t* id, int32_t nranks, int32_t rank, const int32_t* peer_ranks);
+/* `steps` decomposed steps on the engine stream: per step the domain kernels, ncclAllReduce of the reaction buffer
+ * (simulation_driver_interphase.cpp:80-90 sees the sum over domains), the tail, then one grouped ncclSend/ncclRecv
+ * of the band with each peer and the unpack; chunks of GCS_OPT_GRAPH_STEPS steps are captured in a hipGraph. */
+int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps);
+/* Host-staged transport (tests; any process layout, e.g. several processes on one device): a step's halves with
+ * host buffers -- the local reduction out, the summed one in; the bands out ([npeer][cap + 1][4] floats) and in. */
+int gcs_engine_domain_step_host(gcs_engine* e, const gcs_bd_config* cfg, int64_t step, double* red, int32_t nred);
+int gcs_engine_domain_finish_host(gcs_engine* e, const double* glob, int32_t nred);
+int gcs_engine_domain_pack_host(gcs_engine* e, float* bands /* NULL: pack on the device only */);
+int gcs_engine_domain_unpack_host(gcs_engine* e, const float* bands);
+/* In-process transport (several domains on one device): copy src's band src_slot into dst's received band
+ * dst_slot (ordered after src's stream), then unpack everything received. */
+int gcs_engine_domain_receive(gcs_engine* dst, int32_t dst_slot, gcs_engine* src, int32_t src_slot);
+int gcs_engine_domain_unpack_received(gcs_engine* e);
+int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
+
 /* tuning knobs */
 #define GCS_OPT_GRAPH_STEPS 1   /* steps captured per hipGraph replay (0 = eager launches) */
 #define GCS_OPT_WAVES_PER_TILE 2 /* waves sharing one 64-particle tile of the pair loop: 1, 2, 4 or 8 */

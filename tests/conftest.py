@@ -7,21 +7,11 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "3d-genome-cycle_amd"))
 sys.path.insert(0, str(ROOT / "oracle"))
 sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
 
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libgcs.so's HIP kernels)")
-
-
-def pytest_collection_modifyitems(config, items):
-    if any(it.get_closest_marker("gpu") for it in items):
-        # One HIP runtime per process: torch's device runtime is initialised BEFORE libgcs.so is loaded (the
-        # engine loads it at its first construction), so the engine binds to that same runtime and shares device
-        # pointers with torch tensors (gcs.domain's exchange buffers).  Loading libgcs.so first would start a
-        # second runtime that torch then cannot use (tools/runtime_probe.py).
-        import torch
-        if torch.cuda.is_available():
-            torch.zeros(1, device="cuda")
 
 
 @pytest.fixture(scope="session")

@@ -17,6 +17,7 @@ from gcs import domain, interphase
 from gcs.config import InterphaseConfig
 
 import oracle
+from oracle_domain import OracleDomain
 
 ROOT = Path(__file__).resolve().parents[1]
 STEPS = 30
@@ -36,8 +37,8 @@ def _domains(design, cfg, slabs, halo, only=None):
         if only is not None and d != only:
             continue
         o, _ = interphase.build_interphase(oracle.OracleSystem, design, cfg)
-        doms.append(domain.OracleDomain(o, d, slabs, halo, interphase.interphase_schedule(cfg),
-                                        shared=domain.shared_particles(design)))
+        doms.append(OracleDomain(o, d, slabs, halo, interphase.interphase_schedule(cfg),
+                                 shared=domain.shared_particles(design)))
     return doms
 
 
@@ -105,7 +106,9 @@ def _rank_main(rank, world, port, out_dir):
                        "MASTER_PORT": str(port)})
     sys.path.insert(0, str(ROOT / "3d-genome-cycle_amd"))
     sys.path.insert(0, str(ROOT / "oracle"))
+    sys.path.insert(0, str(ROOT / "tests"))
     import torch.distributed as dist
+    from oracle_domain import OracleDomain
     from gcs import domain as D, interphase as I, synthetic
     from gcs.config import InterphaseConfig as IC
     import oracle as O
@@ -115,7 +118,7 @@ def _rank_main(rank, world, port, out_dir):
     halo = D.domain_halo(cfg)
     slabs = D.plan_slabs(design.positions[:, 2], world)
     o, _ = I.build_interphase(O.OracleSystem, design, cfg)
-    d = D.OracleDomain(o, rank, slabs, halo, I.interphase_schedule(cfg), shared=D.shared_particles(design))
+    d = OracleDomain(o, rank, slabs, halo, I.interphase_schedule(cfg), shared=D.shared_particles(design))
     run = D.DecomposedRun([d], D.DistTransport(d, dist))
     run.run(STEPS, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     run.check()

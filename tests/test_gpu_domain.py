@@ -1,9 +1,18 @@
-"""GPU: the spatial domain decomposition (C5, gcs/domain.py + csrc/domain.hip) with HIP engines, several domains in
-one process on one device (LocalTransport), against the undecomposed engine and the fp64 oracle.
+"""GPU: the spatial domain decomposition (C5, gcs/domain.py + csrc/domain.hip) with HIP engines: several domains in
+one process on one device (LocalTransport: bands device-to-device), two processes on one device (DistTransport,
+host-staged over gloo: RCCL refuses two ranks on one GPU), and the engine-issued RCCL sequence with one rank
+(gcs_engine_domain_run: allreduce + grouped send/recv on the engine stream, graph-captured), against the undecomposed
+engine, each other and the fp64 oracle.
 
 Tolerances: positions |dx| <= 2e-5 after 30 steps (fp32; the domains' cell lists order the pair sums differently
 from the single engine's), wall semiaxes relative 1e-7; the protocol flags (bond beyond the halo, band over
 capacity) must stay clear."""
+import json
+import os
+import socket
+import sys
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -29,8 +38,7 @@ def _decomposed(design, cfg, ndom, steps, cap=None, halo=None):
     halo = halo or domain.domain_halo(cfg)
     slabs = domain.plan_slabs(design.positions[:, 2], ndom)
     sh = domain.shared_particles(design)
-    doms = [domain.EngineDomain(_engine(design, cfg), d, slabs, halo, cap=cap, device=0, shared=sh)
-            for d in range(ndom)]
+    doms = [domain.EngineDomain(_engine(design, cfg), d, slabs, halo, cap=cap, shared=sh) for d in range(ndom)]
     run = domain.DecomposedRun(doms, domain.LocalTransport(doms))
     run.run(steps, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     return run, doms, slabs
@@ -107,3 +115,85 @@ def test_decomposed_c5_scaled_two_domains():
     e_dec = np.abs(x - xo).max()
     assert np.isfinite(x).all()
     assert e_single <= 2e-5 and e_dec <= 2e-5, (e_dec, e_single)
+
+
+def test_rccl_run_one_rank_equals_host_driven(c1_design):
+    """gcs_engine_domain_run with one rank (RCCL allreduce on the engine stream; 70 steps = a priming step, two
+    captured 32-step graphs and eager steps) equals the host-driven step sequence of the same domain bit for bit"""
+    from gcs.engine import rccl_unique_id
+    cfg = InterphaseConfig()
+    halo = domain.domain_halo(cfg)
+    slabs = domain.plan_slabs(c1_design.positions[:, 2], 1)
+    sh = domain.shared_particles(c1_design)
+    ref = domain.EngineDomain(_engine(c1_design, cfg), 0, slabs, halo, shared=sh)
+    run = domain.DecomposedRun([ref], domain.LocalTransport([ref]))
+    run.run(70, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    d = domain.EngineDomain(_engine(c1_design, cfg), 0, slabs, halo, shared=sh)
+    d.e.domain_rccl(rccl_unique_id(), 1, 0, [])
+    d.e.domain_run(30, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    d.e.domain_run(40, first_step=30, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    assert d.flag_bits() == 0
+    xd, cd = d.positions(), d.context()
+    d.e.close()  # the communicator goes with the engine, before interpreter teardown
+    assert np.array_equal(xd, ref.positions())
+    assert cd == ref.context()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, out_dir):
+    """one domain per process, both on device 0, host-staged over gloo"""
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": str(port)})
+    root = Path(__file__).resolve().parents[1]
+    sys.path.insert(0, str(root / "3d-genome-cycle_amd"))
+    import torch.distributed as dist
+    from gcs import domain as D, interphase as I, synthetic as S
+    from gcs.config import InterphaseConfig as IC
+    from gcs.engine import Engine as E
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    design, cfg = S.make_c1(), IC()
+    e, _ = I.build_interphase(E, design, cfg, device=0)
+    e.set_schedule(**I.interphase_schedule(cfg))
+    slabs = D.plan_slabs(design.positions[:, 2], world)
+    d = D.EngineDomain(e, rank, slabs, D.domain_halo(cfg), shared=D.shared_particles(design))
+    run = D.DecomposedRun([d], D.DistTransport(d, dist))
+    run.run(STEPS, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    run.check()
+    x = D.gather_positions(run, design.n, dist)
+    if rank == 0:
+        np.save(Path(out_dir, "x.npy"), x)
+        Path(out_dir, "ctx.json").write_text(json.dumps(d.context()))
+    dist.destroy_process_group()
+
+
+def test_engine_domains_two_processes_host_staged(tmp_path, c1_design):
+    """two processes, one engine domain each (device 0), reaction allreduce and bands over gloo: bit for bit the
+    in-process two-domain run (the same kernels; a two-term sum is order-free), and within 2e-5 of the single
+    engine"""
+    # stdlib spawn, not torch.multiprocessing: this process keeps one HIP runtime (libgcs's); torch (for gloo) is
+    # imported by the ranks only, before their engines load libgcs
+    import multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    x = np.load(tmp_path / "x.npy")
+    ctx = json.loads((tmp_path / "ctx.json").read_text())
+    cfg = InterphaseConfig()
+    run, doms, _ = _decomposed(c1_design, cfg, world, STEPS)
+    xl = domain.gather_positions(run, c1_design.n)
+    assert np.array_equal(x, xl)
+    assert ctx["wall_semiaxes"] == doms[0].context()["wall_semiaxes"]
+    single = _engine(c1_design, cfg)
+    single.run(STEPS, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    assert np.abs(x - single.get_positions()).max() <= 2e-5
