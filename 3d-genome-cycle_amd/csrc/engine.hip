@@ -202,11 +202,12 @@ struct gcs_engine {
     float2* type_ab = nullptr;
     int ntypes = 0;
     bool list_ok = false;       // the system admits the list step (a pair field, <= 256 classes, N < 2^24)
-    int list_cap = 64;          // GCS_OPT_LIST_CAP: entries per (particle, wave) segment
+    int list_cap = 512;         // GCS_OPT_LIST_CAP: list entries per particle (split over the tile's waves)
     size_t list_alloc = 0;      // allocated entries
     int list_skin_pm = 400;     // GCS_OPT_LIST_SKIN: skin in 1/1000 of the pair cutoff
     int list_every_opt = 0;     // GCS_OPT_LIST_EVERY: rebuild period in steps (0: from the noise amplitude)
     int list_every = 1;         // the period of the current run
+    int list_waves = 4;         // GCS_OPT_LIST_WAVES: waves per tile (2: more tiles resident, for replica runs)
     bool l_need_build = true;   // the next list step must rebuild (run start without continuity)
     int g_list_every = -1;
 
@@ -607,16 +608,17 @@ ForceArgs list_args(const gcs_engine* e)
     a.lgroup = e->lgroup;
     a.type_ab = e->type_ab;
     a.ntypes = e->ntypes;
-    a.list_cap = e->list_cap;
+    a.list_cap = e->list_cap / e->list_waves;  // per (particle, wave) segment
     a.list_stride = (e->n + 63) & ~63;
     a.list_skin = list_skin(e);
+    a.list_waves = e->list_waves;
     return a;
 }
 
 int ensure_list(gcs_engine* e)
 {
     const size_t stride = (size_t)((e->n + 63) & ~63);
-    const size_t need = stride * kListWaves * (size_t)e->list_cap;
+    const size_t need = stride * (size_t)e->list_cap;  // every segment layout fits: waves x (cap / waves)
     if (need <= e->list_alloc && e->lcount) return GCS_OK;
     dfree(e->list);
     dfree(e->lcount);
@@ -624,7 +626,7 @@ int ensure_list(gcs_engine* e)
     dfree(e->psort[1]);
     e->list_alloc = 0;
     int rc;
-    if ((rc = dalloc(&e->list, need)) || (rc = dalloc(&e->lcount, stride * kListWaves)) ||
+    if ((rc = dalloc(&e->list, need)) || (rc = dalloc(&e->lcount, stride * kMaxListWaves)) ||
         (rc = dalloc(&e->psort[0], stride)) || (rc = dalloc(&e->psort[1], stride)))
         return rc;
     if (!e->lticket) {
@@ -2317,8 +2319,14 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         drop_graph(e);
         return GCS_OK;
     }
+    if (option == GCS_OPT_LIST_WAVES) {
+        if (value != 2 && value != 4) return fail(GCS_EINVAL, "list waves per tile must be 2 or 4");
+        e->list_waves = (int)value;
+        drop_graph(e);
+        return GCS_OK;
+    }
     if (option == GCS_OPT_LIST_CAP) {
-        if (value < 8 || value > 4096) return fail(GCS_EINVAL, "list capacity must be in [8, 4096]");
+        if (value < 32 || value > 16384) return fail(GCS_EINVAL, "list capacity must be in [32, 16384]");
         e->list_cap = (int)value;
         drop_graph(e);
         return GCS_OK;

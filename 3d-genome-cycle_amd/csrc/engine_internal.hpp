@@ -201,11 +201,12 @@ struct ForceArgs {
     int list_cap;           // entries per (slot, wave)
     int list_stride;        // >= N
     float list_skin;        // > 0 only in the list path's own argument block
+    int list_waves;         // waves per tile (list segments): 4, or 2 (GCS_OPT_LIST_WAVES)
     unsigned* lticket;      // list step arrival counters: [32 g] per group of workgroups (g < 8), [32 * 8] groups
     float* lgroup;          // [8][24] group partial rows (8 doubles + 8 floats)
 };
 
-constexpr int kListWaves = 4;           // waves per tile of the list kernels (each owns one list segment)
+constexpr int kMaxListWaves = 4;  // waves per tile of the list kernels (each owns one list segment): 2 or 4
 constexpr int kMaxTypes = 256;          // pair-factor classes (8 bits of a list entry)
 constexpr int kListIndexBits = 24;      // particle index bits of a list entry
 constexpr int kListCountMask = (1 << 30) - 1;

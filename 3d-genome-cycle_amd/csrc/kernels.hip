@@ -2548,8 +2548,8 @@ __device__ void list_tail_apply(DevCtx* ctx, const ForceArgs& a, const double* t
 __device__ void list_reduce_rows(const ForceArgs& a, int first, int stride, int count, double* tot, float* bb,
                                  float& ld, float& lf)
 {
-    __shared__ double s_red[kListWaves][8];
-    __shared__ float s_bb[kListWaves][8];
+    __shared__ double s_red[kMaxListWaves][8];
+    __shared__ float s_bb[kMaxListWaves][8];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_force, 0, 0x7fffffff, 0x00020000);
     const auto rb = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_bbox, 0, 0x7fffffff, 0x00020000);
@@ -2622,7 +2622,7 @@ __device__ void list_reduce_rows(const ForceArgs& a, int first, int stride, int 
 }
 
 // LE: list entry type (unsigned short when every slot index fits 16 bits: half the list traffic)
-template <typename LE>
+template <typename LE, int kListWaves>
 __global__ __launch_bounds__(64 * kListWaves) void k_lbuild(DevCtx* __restrict__ ctx, ForceArgs a)
 {
     __shared__ int s_rowV[kListWaves][4 * 17];
@@ -2701,7 +2701,7 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 #define GCS_LIST_TAIL_ROWS 4  // partial rows per thread per round trip of the last workgroup's tail
 #endif
 
-template <typename LE>
+template <typename LE, int kListWaves>
 __global__ __launch_bounds__(64 * kListWaves) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int apply_sched)
 {
     __shared__ float red[kListWaves][4][kTile];
@@ -2864,7 +2864,7 @@ __global__ __launch_bounds__(64 * kListWaves) void k_lstep(DevCtx* __restrict__ 
         red[wave][1][lane] = fy;
         red[wave][2][lane] = fz;
         red[wave][3][lane] = nbr;
-        if (wave == 1) {  // the noise (depends on the particle and the step only) off wave 0's path
+        if (wave == (kListWaves > 1 ? 1 : 0)) {  // the noise (depends on the particle and the step only) off wave 0's path
             float n0, n1, n2;
             noise3(a, ctx, i, n0, n1, n2);
             s_noise[lane] = make_float4(n0, n1, n2, 0.f);
@@ -3181,19 +3181,34 @@ bool list_u16(int n) { return n <= 65536; }
 
 void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a)
 {
-    if (list_u16(a.n))
-        hipLaunchKernelGGL(k_lbuild<unsigned short>, dim3(force_grid(a.n)), dim3(64 * kListWaves), 0, s, ctx, a);
-    else
-        hipLaunchKernelGGL(k_lbuild<int>, dim3(force_grid(a.n)), dim3(64 * kListWaves), 0, s, ctx, a);
+    const dim3 g(force_grid(a.n));
+    if (list_u16(a.n)) {
+        if (a.list_waves == 2)
+            hipLaunchKernelGGL((k_lbuild<unsigned short, 2>), g, dim3(128), 0, s, ctx, a);
+        else
+            hipLaunchKernelGGL((k_lbuild<unsigned short, 4>), g, dim3(256), 0, s, ctx, a);
+    } else {
+        if (a.list_waves == 2)
+            hipLaunchKernelGGL((k_lbuild<int, 2>), g, dim3(128), 0, s, ctx, a);
+        else
+            hipLaunchKernelGGL((k_lbuild<int, 4>), g, dim3(256), 0, s, ctx, a);
+    }
 }
 
 void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int apply_sched)
 {
-    if (list_u16(a.n))
-        hipLaunchKernelGGL(k_lstep<unsigned short>, dim3(list_step_grid(a.n)), dim3(64 * kListWaves), 0, s, ctx, a,
-                           apply_sched);
-    else
-        hipLaunchKernelGGL(k_lstep<int>, dim3(list_step_grid(a.n)), dim3(64 * kListWaves), 0, s, ctx, a, apply_sched);
+    const dim3 g(list_step_grid(a.n));
+    if (list_u16(a.n)) {
+        if (a.list_waves == 2)
+            hipLaunchKernelGGL((k_lstep<unsigned short, 2>), g, dim3(128), 0, s, ctx, a, apply_sched);
+        else
+            hipLaunchKernelGGL((k_lstep<unsigned short, 4>), g, dim3(256), 0, s, ctx, a, apply_sched);
+    } else {
+        if (a.list_waves == 2)
+            hipLaunchKernelGGL((k_lstep<int, 2>), g, dim3(128), 0, s, ctx, a, apply_sched);
+        else
+            hipLaunchKernelGGL((k_lstep<int, 4>), g, dim3(256), 0, s, ctx, a, apply_sched);
+    }
 }
 
 void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a)

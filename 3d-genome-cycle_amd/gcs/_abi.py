@@ -37,6 +37,7 @@ OPT_CONTACT_BITS = 9
 OPT_LIST_SKIN = 10
 OPT_LIST_EVERY = 11
 OPT_LIST_CAP = 12
+OPT_LIST_WAVES = 13
 
 ENERGY_KINDS = ("pair", "softwell", "bonds", "bending", "wall_in", "wall_out", "point_source", "kinetochore_fiber")
 

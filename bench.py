@@ -384,6 +384,9 @@ def replica_main(args):
     maker = design_maker(args.config)
     R = max(1, args.replicas_per_gpu)
     K = max(1, args.steps)
+    # list step: 2 waves per tile when trajectories share the GPU (twice the tiles resident; the other replicas'
+    # launches fill the latency), 4 for a trajectory alone (the lowest step latency)
+    list_waves = args.list_waves or (2 if R > 1 else 4)
     # graph chunk: a pass of K steps per replica is replayed in G-step hipGraphs (G <= K, so short passes replay
     # graphs too); warm-up captures and instantiates every engine's graph before the timed region
     G = min(args.graph_steps, K) if args.graph_steps > 0 else 0
@@ -407,7 +410,8 @@ def replica_main(args):
             for opt, v in ((A.OPT_GRAPH_STEPS, G), (A.OPT_WAVES_PER_TILE, args.waves),
                            (A.OPT_CHUNK_ORDER, args.chunk_order), (A.OPT_FUSED_STEP, args.fused),
                            (A.OPT_SPLIT_TILES, args.split), (A.OPT_TILE_PRIORITY, args.prio),
-                           (A.OPT_SUBTILES, args.subtiles), (A.OPT_SCAN_BLOCKS, args.scan_mb)):
+                           (A.OPT_SUBTILES, args.subtiles), (A.OPT_SCAN_BLOCKS, args.scan_mb),
+                           (A.OPT_LIST_WAVES, list_waves)):
                 e.set_option(opt, v)
         designs.append(d)
         engines.append(e)
@@ -562,7 +566,7 @@ def replica_main(args):
                    "split_tiles": args.split, "tile_priority": args.prio, "subtiles": args.subtiles,
                    "scan_mb": args.scan_mb, "start_window_value": start_rate, "finite": finite,
                    "contacts_update_ms": contacts_ms, "contacts_distinct_pairs_22_updates": contacts_distinct,
-                   "list_step": lst},
+                   "list_step": lst, "list_waves_per_tile": list_waves},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(args.fused),
                      "kernel": STEP_KERNEL.get(args.fused, ("?",))[0], "force_ms": force_ms, "cell_ms": prof["cell_ms"],
@@ -591,6 +595,8 @@ def parse_args(argv=None):
     ap.add_argument("--prio", type=int, default=700, help="n > 0: wave priority min(3, tile candidates / n)")
     ap.add_argument("--subtiles", type=int, default=2, help="pair-loop stencils per 64-particle tile: 1, 2, 4")
     ap.add_argument("--scan-mb", type=int, default=1, help="1: multi-block look-back cell scan, 0: one workgroup")
+    ap.add_argument("--list-waves", type=int, default=0,
+                    help="list step waves per tile: 2 or 4 (0: 2 with several replicas per GPU, else 4)")
     ap.add_argument("--fused", type=int, default=3,
                     help="3: list step (default), 2: 2-launch rebuild step, 1: 4-launch step, 0: unfused")
     ap.add_argument("--profile-steps", type=int, default=50)

@@ -349,7 +349,9 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
 #define GCS_OPT_CONTACT_BITS 9   /* contact map: 2^bits hash slots (0 = default, >= 2 N slots sized at first update) */
 #define GCS_OPT_LIST_SKIN 10      /* list step: skin in 1/1000 of the pair cutoff (default 400) */
 #define GCS_OPT_LIST_EVERY 11     /* list step: rebuild period in steps (0 = default: from the noise amplitude) */
-#define GCS_OPT_LIST_CAP 12       /* list step: list entries per particle and wave (default 64; more: exact search) */
+#define GCS_OPT_LIST_CAP 12       /* list step: list entries per particle (default 512; a longer list: exact search) */
+#define GCS_OPT_LIST_WAVES 13     /* list step: waves per 64-particle tile, 4 (default: lowest step latency) or 2 (more
+                                     tiles resident: the better throughput when several trajectories share a GPU) */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
 
 /* List-step diagnostics (the neighbour lists md::neighbor_searcher keeps between rebuilds; micromd, called at
@@ -362,7 +364,7 @@ typedef struct gcs_list_stats {
     double skin;                      /* list radius - pair cutoff */
     double max_displacement;          /* largest displacement of a particle since the last build */
     int32_t pair_classes;             /* distinct (a, b) pair-factor classes */
-    int32_t capacity;                 /* list entries per particle and wave */
+    int32_t capacity;                 /* list entries per particle */
 } gcs_list_stats;
 int gcs_engine_get_list_stats(gcs_engine* e, gcs_list_stats* out);
 

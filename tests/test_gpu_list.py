@@ -99,7 +99,7 @@ def test_list_exact_when_the_skin_is_outrun(c1_design, skin, every):
 
 def test_list_exact_when_lists_overflow(c1_design):
     cfg = InterphaseConfig()
-    e, o = _pair(c1_design, cfg, ctx=LATE, list_cap=8)
+    e, o = _pair(c1_design, cfg, ctx=LATE, list_cap=32)
     _run_both(e, o, 30, LATE["step"], cfg, 23)
     st = e.list_stats()
     assert st["fallback_particle_steps"] > 0, st
@@ -194,3 +194,11 @@ def test_list_and_rebuild_step_agree_on_neighbour_count():
         vals.append(p["mean_neighbors"])
         e.close()
     assert vals[0] > 0 and vals[1] == pytest.approx(vals[0], rel=1e-4), vals
+
+
+def test_list_two_waves_per_tile(c1_design):
+    """GCS_OPT_LIST_WAVES 2 (two list segments per particle): the same bound against the oracle"""
+    cfg = InterphaseConfig()
+    e, o = _pair(c1_design, cfg, ctx=LATE, list_waves=2)
+    _run_both(e, o, 40, LATE["step"], cfg, 7)
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X

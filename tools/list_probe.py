@@ -20,13 +20,15 @@ from gcs.config import InterphaseConfig  # noqa: E402
 
 opts = dict(a.split("=") for a in sys.argv[1:])
 cfg = InterphaseConfig()
-st = bench.load_state()
-e = bench.make_engine(synthetic.make_c2(), cfg, 0, bench.WINDOW_START, st)
+start = int(opts.pop("start", 0))  # 1: the production start window (synthetic C2, step 0, core_scale 0.5)
+st = None if start else bench.load_state()
+w0 = 0 if start else bench.WINDOW_START
+e = bench.make_engine(synthetic.make_c2(), cfg, 0, w0, st)
 e.set_option(A.OPT_FUSED_STEP, int(opts.pop("fused", 3)))
 for k, v in opts.items():
     e.set_option(getattr(A, "OPT_" + k.upper()), int(v))
-e.run(200, first_step=bench.WINDOW_START, seed=5)
-p = e.profile(40, first_step=bench.WINDOW_START + 200, seed=5)
+e.run(200, first_step=w0, seed=5)
+p = e.profile(40, first_step=w0 + 200, seed=5)
 print({k: (round(v * 1e3, 2) if k.endswith("_ms") else v) for k, v in p.items()}, "(us)")
 print(e.list_stats())
 n = e.n
