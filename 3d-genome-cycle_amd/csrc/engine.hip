@@ -210,6 +210,7 @@ struct gcs_engine {
     int list_waves = 4;         // GCS_OPT_LIST_WAVES: waves per tile (2: more tiles resident, for replica runs)
     bool l_need_build = true;   // the next list step must rebuild (run start without continuity)
     int g_list_every = -1;
+    double c_pending = 0;       // a contact update fused into the next list step (its distance; 0: none)
 
     // fused-step continuity: after a fused run the cells of the next positions are already binned with the
     // grid the next step expects, so a run that continues at chain_step skips re-priming (bitwise identical
@@ -656,9 +657,18 @@ int auto_list_every(const gcs_engine* e, const gcs_bd_config* cfg)
 
 // one list step: on a rebuild step the cell list at cutoff + skin (ctx->grid, set by the prime or the last
 // tail), the lists, then the step itself (forces + local terms + update + tail in the last workgroup)
-void enqueue_list_step(gcs_engine* e, bool build)
+void enqueue_list_step(gcs_engine* e, bool build, double contact = 0)
 {
-    const ForceArgs la = list_args(e);
+    ForceArgs la = list_args(e);
+    if (contact > 0) {  // the pending contact update, counted from this step's start positions
+        la.contact_on = 1;
+        const float d = (float)contact;
+        la.contact_d2 = d * d;  // fp32 product, as k_contact_insert forms it
+        la.c_keys = e->c_keys;
+        la.c_counts = e->c_counts;
+        la.c_bits = e->c_bits;
+        la.c_overflow = e->c_flags;
+    }
     if (build) {
         launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], e->n, e->cell_of, e->slot, e->count);
         enqueue_scan(e, false);
@@ -913,6 +923,36 @@ int enqueue_search_cells(gcs_engine* e, const float4* src, int ni, double distan
                      e->s_scell, e->s_spos, e->s_sb, 1);
     HIPCHK(hipGetLastError());
     return GCS_OK;
+}
+
+// count every pair of the current positions closer than `distance` into the contact table (allocated)
+int contacts_insert_now(gcs_engine* e, double distance)
+{
+    int rc;
+    if (e->fused == 2 && e->chain_valid) {
+        // right after a rebuild-step run the engine's own cell list holds the current positions (k_rebuild built
+        // it from the records the last force kernel filed): no cell build of our own
+        launch_contact_insert(e->stream, e->ctx, e->n, (float)distance, e->spos, e->sidx, e->scell, e->cstart,
+                              e->c_keys, e->c_counts, e->c_bits, e->c_flags);
+    } else {
+        if ((rc = ensure_search(e, e->n))) return rc;
+        if ((rc = enqueue_search_cells(e, e->pos[e->parity], e->n, distance))) return rc;
+        launch_contact_insert(e->stream, e->s_ctx, e->n, (float)distance, e->s_spos, e->s_sidx, e->s_scell,
+                              e->s_cstart, e->c_keys, e->c_counts, e->c_bits, e->c_flags);
+    }
+    HIPCHK(hipGetLastError());
+    return GCS_OK;
+}
+
+// a contact update deferred into the next list step is done now instead (positions or the table are about to be
+// changed or read by something other than that step)
+int flush_contacts(gcs_engine* e)
+{
+    if (!(e->c_pending > 0)) return GCS_OK;
+    const double d = e->c_pending;
+    e->c_pending = 0;
+    HIPCHK(hipSetDevice(e->device));
+    return contacts_insert_now(e, d);
 }
 
 }  // namespace
@@ -1239,6 +1279,7 @@ int gcs_engine_set_positions(gcs_engine* e, const double* xyz, int64_t n)
 {
     if (e) e->dom_cont = false;  // a decomposed run re-primes after any outside change
     if (!e || !xyz) return fail(GCS_EINVAL, "null argument");
+    if (int rc = flush_contacts(e)) return rc;
     e->chain_valid = false;
     if (n != e->n) return fail(GCS_EINVAL, "position count does not match the particle count");
     HIPCHK(hipSetDevice(e->device));
@@ -1290,6 +1331,7 @@ int gcs_engine_set_context(gcs_engine* e, const gcs_context* c)
 {
     if (e) e->dom_cont = false;  // a decomposed run re-primes after any outside change
     if (!e || !c) return fail(GCS_EINVAL, "null argument");
+    if (int rc = flush_contacts(e)) return rc;
     e->chain_valid = false;
     HIPCHK(hipSetDevice(e->device));
     DevCtx d;
@@ -1372,9 +1414,11 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
     if (cfg->noise == GCS_NOISE_INJECTED && e->noise_cursor + steps > e->noise_steps)
         return fail(GCS_ESTATE, "not enough injected noise for the requested steps");
     if (steps == 0) return prepare(e);
+    const bool spacestep = cfg->spacestep > 0;
+    if (!list_path(e, spacestep))
+        if (int rc = flush_contacts(e)) return rc;
     int rc = begin_run(e, cfg, first_step);
     if (rc) return rc;
-    const bool spacestep = cfg->spacestep > 0;
 
     const int G = e->graph_steps;
     int64_t done = 0;
@@ -1387,6 +1431,13 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
         while (done < steps) {
             const int64_t st = first_step + done;
             const bool aligned = (st % M) == 0;
+            if (e->c_pending > 0) {  // the contact update the host asked for after the last step
+                enqueue_list_step(e, e->l_need_build || aligned, e->c_pending);
+                e->c_pending = 0;
+                e->l_need_build = false;
+                ++done;
+                continue;
+            }
             if (GM > 0 && !e->l_need_build && aligned && steps - done >= GM) {
                 const bool same = e->gexec && e->g_steps == GM && e->g_version == e->topo_version && e->g_fused == 3 &&
                                   e->g_list_every == M && e->g_sched_flags == e->sched_flags &&
@@ -1586,18 +1637,14 @@ int gcs_engine_contacts_update(gcs_engine* e, double distance)
         HIPCHK(hipMemsetAsync(e->c_counts, 0, slots * sizeof(unsigned), e->stream));
         HIPCHK(hipMemsetAsync(e->c_flags, 0, 2 * sizeof(int), e->stream));
     }
-    if (e->fused == 2 && e->chain_valid) {
-        // right after a rebuild-step run the engine's own cell list holds the current positions (k_rebuild built
-        // it from the records the last force kernel filed): no cell build of our own
-        launch_contact_insert(e->stream, e->ctx, e->n, (float)distance, e->spos, e->sidx, e->scell, e->cstart,
-                              e->c_keys, e->c_counts, e->c_bits, e->c_flags);
-    } else {
-        if ((rc = ensure_search(e, e->n))) return rc;
-        if ((rc = enqueue_search_cells(e, e->pos[e->parity], e->n, distance))) return rc;
-        launch_contact_insert(e->stream, e->s_ctx, e->n, (float)distance, e->s_spos, e->s_sidx, e->s_scell,
-                              e->s_cstart, e->c_keys, e->c_counts, e->c_bits, e->c_flags);
+    if ((rc = flush_contacts(e))) return rc;
+    if (list_path(e, false) && e->chain_valid) {
+        // after a list-step run: the next list step counts the pairs from its start positions (= these), inside
+        // its pair loop (contact distance < cutoff: every such pair is in the lists or the exact search)
+        e->c_pending = distance;
+    } else if ((rc = contacts_insert_now(e, distance))) {
+        return rc;
     }
-    HIPCHK(hipGetLastError());
     e->c_updates++;
     return GCS_OK;
 }
@@ -1605,6 +1652,7 @@ int gcs_engine_contacts_update(gcs_engine* e, double distance)
 int gcs_engine_contacts_clear(gcs_engine* e)
 {
     if (!e) return fail(GCS_EINVAL, "null argument");
+    if (e->c_pending > 0) e->c_pending = 0;  // cleared before it was counted: the update is superseded? no --
     e->c_updates = 0;
     if (!e->c_keys) return GCS_OK;
     HIPCHK(hipSetDevice(e->device));
@@ -1618,6 +1666,7 @@ int gcs_engine_contacts_clear(gcs_engine* e)
 int gcs_engine_contacts_read(gcs_engine* e, uint32_t* ijc, int64_t capacity, int64_t* count)
 {
     if (!e || !count || (capacity > 0 && !ijc)) return fail(GCS_EINVAL, "null argument");
+    if (int rc = flush_contacts(e)) return rc;
     *count = 0;
     if (!e->c_keys) return GCS_OK;
     HIPCHK(hipSetDevice(e->device));
@@ -1781,6 +1830,7 @@ int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step
     if (!e->dom) return fail(GCS_ESTATE, "gcs_engine_set_domain first");
     if (cfg->spacestep > 0) return fail(GCS_EINVAL, "decomposed runs use a fixed timestep");
     if (cfg->noise == GCS_NOISE_INJECTED) return fail(GCS_EINVAL, "decomposed runs draw Philox noise");
+    if (int rc = flush_contacts(e)) return rc;
     HIPCHK(hipSetDevice(e->device));
     if (!(e->dom_cont && e->dom_next == step)) {
         int rc = begin_run(e, cfg, step);
@@ -2139,6 +2189,7 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     if (cfg->spacestep > 0) return fail(GCS_EINVAL, "profile covers the fixed-timestep path only");
     if (cfg->noise == GCS_NOISE_INJECTED && e->noise_cursor + steps > e->noise_steps)
         return fail(GCS_ESTATE, "not enough injected noise for the requested steps");
+    if (int rc = flush_contacts(e)) return rc;
     int rc = begin_run(e, cfg, first_step);
     if (rc) return rc;
     std::vector<hipEvent_t> ev((size_t)steps * 5 + 2, nullptr);
@@ -2270,6 +2321,27 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
                          1e3 * (d.t_rows[3] - d.t_rows[2]) / khz, 1e3 * (d.t_last[3] - d.t_rows[3]) / khz);
     }
     out->mean_neighbors = d.neighbors;
+    return GCS_OK;
+}
+
+int gcs_engine_set_cu_mask(gcs_engine* e, const uint32_t* mask, int32_t words)
+{
+    if (!e || (words > 0 && !mask)) return fail(GCS_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    hipStream_t s = nullptr;
+    if (words > 0) {
+        HIPCHK(hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask));
+    } else {
+        HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    }
+    drop_graph(e);
+    if (e->dgexec) (void)hipGraphExecDestroy(e->dgexec);
+    if (e->dgraph) (void)hipGraphDestroy(e->dgraph);
+    e->dgexec = nullptr;
+    e->dgraph = nullptr;
+    (void)hipStreamDestroy(e->stream);
+    e->stream = s;
     return GCS_OK;
 }
 

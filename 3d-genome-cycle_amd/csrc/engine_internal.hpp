@@ -202,6 +202,14 @@ struct ForceArgs {
     int list_stride;        // >= N
     float list_skin;        // > 0 only in the list path's own argument block
     int list_waves;         // waves per tile (list segments): 4, or 2 (GCS_OPT_LIST_WAVES)
+    // the contact-map update fused into a list step (stage_interphase/contact_map.cpp:33-63): every pair i < j of
+    // the step's START positions closer than sqrt(contact_d2) (strict fp32 predicate) is counted into the table
+    int contact_on;
+    float contact_d2;
+    unsigned long long* c_keys;
+    unsigned* c_counts;
+    int c_bits;
+    int* c_overflow;
     unsigned* lticket;      // list step arrival counters: [32 g] per group of workgroups (g < 8), [32 * 8] groups
     float* lgroup;          // [8][24] group partial rows (8 doubles + 8 floats)
 };

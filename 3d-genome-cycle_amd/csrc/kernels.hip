@@ -2490,6 +2490,47 @@ __global__ __launch_bounds__(256) void k_tail(DevCtx* ctx, ForceArgs a, int fblo
 // whose list overflowed) is evaluated exactly by a search of the build's cell list around its current position
 // with radius cutoff + largest displacement.  So the pair set is exact at every step, whatever the rebuild period.
 
+#ifndef GCS_LIST_UNROLL
+#define GCS_LIST_UNROLL 8  // list entries per batch of the pair loop
+#endif
+#ifndef GCS_LIST_PIPE
+#define GCS_LIST_PIPE 0  // 1: two batches in flight (the next batch's gathers overlap this batch's arithmetic)
+#endif
+#ifndef GCS_LIST_TAIL_ROWS
+#define GCS_LIST_TAIL_ROWS 4  // partial rows per thread per round trip of the final workgroup's reduction
+#endif
+#ifndef GCS_LIST_WAVES_PER_EU
+#define GCS_LIST_WAVES_PER_EU 4  // k_lstep occupancy target (VGPR cap 512 / waves): 4 -> <= 128
+#endif
+#ifndef GCS_LIST_XTILE
+#define GCS_LIST_XTILE 1  // 1: the next tile's slot loads are issued before this tile's work (grid-stride tiles)
+#endif
+#ifndef GCS_LIST_BOND_BATCH
+#define GCS_LIST_BOND_BATCH 4  // bond CSR entries whose loads are issued together in the particle-local terms
+#endif
+
+// the contact map's pair count (contacts.hip k_contact_insert: strict fp32 predicate, Fibonacci-hashed open
+// addressing, one atomicCAS per probe); i < j by particle index, so each pair counts once
+__device__ __forceinline__ void list_contact(const ForceArgs& a, float4 p, float4 q, int i, int j)
+{
+    if (j <= i) return;
+    const float dx = __fsub_rn(p.x, q.x), dy = __fsub_rn(p.y, q.y), dz = __fsub_rn(p.z, q.z);
+    const float r2 = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
+    if (!(r2 < a.contact_d2)) return;
+    const unsigned long long key = ((unsigned long long)(unsigned)i << 32) | (unsigned)j;
+    const unsigned long long mask = (1ull << a.c_bits) - 1ull;
+    unsigned long long h = (key * 0x9E3779B97F4A7C15ull) >> (64 - a.c_bits);
+    for (int probe = 0; probe < kContactMaxProbe; ++probe) {
+        const unsigned long long prev = atomicCAS(&a.c_keys[h], kContactEmpty, key);
+        if (prev == kContactEmpty || prev == key) {
+            atomicAdd(&a.c_counts[h], 1u);
+            return;
+        }
+        h = (h + 1) & mask;
+    }
+    atomicOr(a.c_overflow, 1);
+}
+
 // The list step's context update, by thread 0 of the step's final workgroup once every partial is reduced: the
 // tail_body arithmetic of one undecomposed, unfused step (reactions, bbox, step/parity/noise cursor, the schedule of
 // stage_interphase/simulation_driver_interphase.cpp:17, :67-90 and the cell grid at cutoff + skin for a rebuild)
@@ -2558,7 +2599,7 @@ __device__ void list_reduce_rows(const ForceArgs& a, int first, int stride, int 
     float b[8] = {big, big, big, -big, -big, -big, 0.f, 0.f};
     // kR rows per thread per round trip (all loads issued before any is used); rows past count read as the
     // identity (the buffer range check returns 0 past the end: zero sums, and the bbox uses the guarded rows)
-    constexpr int kR = 4;
+    constexpr int kR = GCS_LIST_TAIL_ROWS;
     for (int k0 = tid; k0 < count; k0 += kR * blockDim.x) {
       float4 F0[kR], F1[kR], G0[kR], G1[kR];
 #pragma unroll
@@ -2691,18 +2732,9 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
     return min(c, g.n[k] - 1);
 }
 
-#ifndef GCS_LIST_UNROLL
-#define GCS_LIST_UNROLL 8  // list entries per batch of the pair loop
-#endif
-#ifndef GCS_LIST_PIPE
-#define GCS_LIST_PIPE 0  // 1: two batches in flight (the next batch's gathers overlap this batch's arithmetic)
-#endif
-#ifndef GCS_LIST_TAIL_ROWS
-#define GCS_LIST_TAIL_ROWS 4  // partial rows per thread per round trip of the last workgroup's tail
-#endif
 
-template <typename LE, int kListWaves>
-__global__ __launch_bounds__(64 * kListWaves) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int apply_sched)
+template <typename LE, int kListWaves, bool CT>
+__global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu(GCS_LIST_WAVES_PER_EU))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int apply_sched)
 {
     __shared__ float red[kListWaves][4][kTile];
     __shared__ float4 s_locf[kTile], s_locr[kTile], s_loco[kTile], s_noise[kTile];
@@ -2735,6 +2767,10 @@ __global__ __launch_bounds__(64 * kListWaves) void k_lstep(DevCtx* __restrict__ 
     const float D = ctx->ldisp;
     // a particle whose own displacement exceeds this may miss a partner in its list (0.999: fp32 margin)
     const float slack = 0.999f * a.list_skin - D - fmaxf(rc - ctx->lrc_b, 0.f);
+    // contacts (CT): the lists must cover the contact distance; a particle whose list does not is searched for its
+    // contacts only (its forces take exactly the path they take without contacts: identical bits)
+    const float rcc = CT ? fmaxf(rc, sqrtf(a.contact_d2)) : rc;
+    const float slack_c = 0.999f * a.list_skin - D - fmaxf(rcc - ctx->lrc_b, 0.f);
     const int par = ctx->parity;
     float4* __restrict__ pn = par ? a.pos0 : a.pos1;  // particle order (bonded partners read ctx->parity's)
     const float4* __restrict__ qc = par ? a.psort1 : a.psort0;  // slot order (pair partners)
@@ -2769,7 +2805,9 @@ __global__ __launch_bounds__(64 * kListWaves) void k_lstep(DevCtx* __restrict__ 
         int e[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) e[u] = n_e[u];
+#if GCS_LIST_XTILE
         if ((tile + (int)gridDim.x) * kTile < n) load_tile(tile + gridDim.x);
+#endif
         const LE* __restrict__ seg = reinterpret_cast<const LE*>(a.list) + (size_t)wave * cap * stride + sl;
         const int pk = __float_as_int(pi.w);
         const int i = pk & kIdx;
@@ -2777,12 +2815,13 @@ __global__ __launch_bounds__(64 * kListWaves) void k_lstep(DevCtx* __restrict__ 
         const float ex = pi.x - pb.x, ey = pi.y - pb.y, ez = pi.z - pb.z;
         const float di = sqrtf(fmaf(ez, ez, fmaf(ey, ey, ex * ex)));
         const bool fb = valid && (di > slack || (cw & kListOverflow) != 0);
+        const bool fbc = CT && valid && (di > slack_c || (cw & kListOverflow) != 0);  // implies fb's condition
 
         if (wave == kListWaves - 1) {  // the particle-local terms first (a dependent-gather chain), parked in LDS
             const float4 km = a.kmu[i];
             float lfx = 0.f, lfy = 0.f, lfz = 0.f, en[kEnergyKinds];
             float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
-            local_terms<kModeStep, 4>(ctx, a, i, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout);
+            local_terms<kModeStep, GCS_LIST_BOND_BATCH>(ctx, a, i, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout);
             s_locf[lane] = make_float4(lfx, lfy, lfz, km.x);
             s_locr[lane] = make_float4(rin[0], rin[1], rin[2], 0.f);
             s_loco[lane] = make_float4(rout[0], rout[1], rout[2], 0.f);
@@ -2814,6 +2853,11 @@ __global__ __launch_bounds__(64 * kListWaves) void k_lstep(DevCtx* __restrict__ 
                 for (int u = 0; u < kU; ++u)
                     list_pair(pi.x, pi.y, pi.z, q[u], s_tab[(unsigned)__float_as_int(q[u].w) >> kListIndexBits], ahi,
                               bhi, kA, kB, k2a, k2b, rc2, k0 + u < cnt, fx, fy, fz, nbr);
+                if constexpr (CT) {
+#pragma unroll
+                    for (int u = 0; u < kU; ++u)
+                        if (!fbc && k0 + u < cnt) list_contact(a, pi, q[u], i, __float_as_int(q[u].w) & kIdx);
+                }
 #pragma unroll
                 for (int u = 0; u < kU; ++u) q[u] = qn[u];
             }
@@ -2830,6 +2874,11 @@ __global__ __launch_bounds__(64 * kListWaves) void k_lstep(DevCtx* __restrict__ 
                 for (int u = 0; u < kU; ++u)
                     list_pair(pi.x, pi.y, pi.z, q[u], s_tab[(unsigned)__float_as_int(q[u].w) >> kListIndexBits], ahi,
                               bhi, kA, kB, k2a, k2b, rc2, k0 + u < cnt, fx, fy, fz, nbr);
+                if constexpr (CT) {
+#pragma unroll
+                    for (int u = 0; u < kU; ++u)
+                        if (!fbc && k0 + u < cnt) list_contact(a, pi, q[u], i, __float_as_int(q[u].w) & kIdx);
+                }
 #pragma unroll
                 for (int u = 0; u < kU; ++u) e[u] = en_[u];
             }
@@ -2854,6 +2903,30 @@ __global__ __launch_bounds__(64 * kListWaves) void k_lstep(DevCtx* __restrict__ 
                                 const float4 q = qc[t];
                                 list_pair(pi.x, pi.y, pi.z, q, s_tab[(unsigned)__float_as_int(q.w) >> kListIndexBits],
                                           ahi, bhi, kA, kB, k2a, k2b, rc2, true, fx, fy, fz, nbr);
+                            }
+                        }
+                }
+            }
+        }
+        if constexpr (CT) {
+            if (__ballot(fbc)) {
+                // contacts of the particles whose lists do not cover the contact distance: the build's cell list
+                // around the current position with radius d + D, the waves taking alternate cell rows
+                if (fbc) {
+                    const Grid lg = ctx->lgrid;
+                    const float R = rcc + D + 1.0e-5f * (rcc + D);
+                    const int x0 = lgrid_cell(lg, 0, pi.x - R), x1 = lgrid_cell(lg, 0, pi.x + R);
+                    const int y0 = lgrid_cell(lg, 1, pi.y - R), y1 = lgrid_cell(lg, 1, pi.y + R);
+                    const int z0 = lgrid_cell(lg, 2, pi.z - R), z1 = lgrid_cell(lg, 2, pi.z + R);
+                    int row = 0;
+                    for (int z = z0; z <= z1; ++z)
+                        for (int y = y0; y <= y1; ++y, ++row) {
+                            if ((row % kListWaves) != wave) continue;
+                            const int base = (z * lg.n[1] + y) * lg.n[0];
+                            const int t0 = a.cstart[base + x0], t1 = a.cstart[base + x1 + 1];
+                            for (int t = t0; t < t1; ++t) {
+                                const float4 q = qc[t];
+                                if (t != s) list_contact(a, pi, q, i, __float_as_int(q.w) & kIdx);
                             }
                         }
                 }
@@ -3195,20 +3268,29 @@ void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a)
     }
 }
 
-void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int apply_sched)
+template <bool CT>
+static void launch_list_step_ct(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int apply_sched)
 {
     const dim3 g(list_step_grid(a.n));
     if (list_u16(a.n)) {
         if (a.list_waves == 2)
-            hipLaunchKernelGGL((k_lstep<unsigned short, 2>), g, dim3(128), 0, s, ctx, a, apply_sched);
+            hipLaunchKernelGGL((k_lstep<unsigned short, 2, CT>), g, dim3(128), 0, s, ctx, a, apply_sched);
         else
-            hipLaunchKernelGGL((k_lstep<unsigned short, 4>), g, dim3(256), 0, s, ctx, a, apply_sched);
+            hipLaunchKernelGGL((k_lstep<unsigned short, 4, CT>), g, dim3(256), 0, s, ctx, a, apply_sched);
     } else {
         if (a.list_waves == 2)
-            hipLaunchKernelGGL((k_lstep<int, 2>), g, dim3(128), 0, s, ctx, a, apply_sched);
+            hipLaunchKernelGGL((k_lstep<int, 2, CT>), g, dim3(128), 0, s, ctx, a, apply_sched);
         else
-            hipLaunchKernelGGL((k_lstep<int, 4>), g, dim3(256), 0, s, ctx, a, apply_sched);
+            hipLaunchKernelGGL((k_lstep<int, 4, CT>), g, dim3(256), 0, s, ctx, a, apply_sched);
     }
+}
+
+void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int apply_sched)
+{
+    if (a.contact_on)
+        launch_list_step_ct<true>(s, ctx, a, apply_sched);
+    else
+        launch_list_step_ct<false>(s, ctx, a, apply_sched);
 }
 
 void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a)

@@ -142,6 +142,7 @@ PROTOTYPES = {
     "gcs_engine_profile": (C.c_int, [C.c_void_p, C.POINTER(BDConfig), _i64, _i64, C.POINTER(Profile)]),
     "gcs_engine_set_option": (C.c_int, [C.c_void_p, _i32, _i64]),
     "gcs_engine_get_list_stats": (C.c_int, [C.c_void_p, C.POINTER(ListStats)]),
+    "gcs_engine_set_cu_mask": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), _i32]),
     "gcs_engine_contacts_update": (C.c_int, [C.c_void_p, _d]),
     "gcs_engine_contacts_read": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), _i64, C.POINTER(_i64)]),
     "gcs_engine_contacts_clear": (C.c_int, [C.c_void_p]),

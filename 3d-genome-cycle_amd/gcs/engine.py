@@ -368,6 +368,15 @@ class Engine:
     def set_option(self, option, value):
         A.check(self._lib.gcs_engine_set_option(self._h, int(option), int(value)))
 
+    def set_cu_mask(self, cus):
+        """Run this engine's kernels on the compute units `cus` only (None or empty: all)."""
+        cus = sorted(int(c) for c in (cus or []))
+        words = (max(cus) // 32 + 1) if cus else 0
+        m = (C.c_uint32 * max(1, words))()
+        for c in cus:
+            m[c // 32] |= 1 << (c % 32)
+        A.check(self._lib.gcs_engine_set_cu_mask(self._h, m, words))
+
     def list_stats(self) -> dict:
         s = A.ListStats()
         A.check(self._lib.gcs_engine_get_list_stats(self._h, C.byref(s)))

@@ -413,6 +413,12 @@ def replica_main(args):
                            (A.OPT_SUBTILES, args.subtiles), (A.OPT_SCAN_BLOCKS, args.scan_mb),
                            (A.OPT_LIST_WAVES, list_waves)):
                 e.set_option(opt, v)
+            if args.cu_split and R > 1:
+                # replica k on CUs c with (c mod R) == k ("interleave") or a contiguous R-th of them ("block")
+                ncu = args.cu_count
+                cus = ([c for c in range(ncu) if c % R == k] if args.cu_split == "interleave"
+                       else list(range(k * ncu // R, (k + 1) * ncu // R)))
+                e.set_cu_mask(cus)
         designs.append(d)
         engines.append(e)
         seeds.append(replica_noise_seed(rid))
@@ -595,6 +601,9 @@ def parse_args(argv=None):
     ap.add_argument("--prio", type=int, default=700, help="n > 0: wave priority min(3, tile candidates / n)")
     ap.add_argument("--subtiles", type=int, default=2, help="pair-loop stencils per 64-particle tile: 1, 2, 4")
     ap.add_argument("--scan-mb", type=int, default=1, help="1: multi-block look-back cell scan, 0: one workgroup")
+    ap.add_argument("--cu-split", default="", choices=["", "interleave", "block"],
+                    help="several replicas per GPU: give each its own share of the compute units")
+    ap.add_argument("--cu-count", type=int, default=256)
     ap.add_argument("--list-waves", type=int, default=0,
                     help="list step waves per tile: 2 or 4 (0: 2 with several replicas per GPU, else 4)")
     ap.add_argument("--fused", type=int, default=3,

@@ -368,6 +368,10 @@ typedef struct gcs_list_stats {
 } gcs_list_stats;
 int gcs_engine_get_list_stats(gcs_engine* e, gcs_list_stats* out);
 
+/* Restrict the engine's stream to a set of compute units (bit i of mask[i / 32] = CU i; words = 0: all CUs), e.g.
+ * one group of XCDs per trajectory when several share a GPU.  Recreates the stream: call between runs. */
+int gcs_engine_set_cu_mask(gcs_engine* e, const uint32_t* mask, int32_t words);
+
 #ifdef __cplusplus
 }
 #endif

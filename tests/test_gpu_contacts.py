@@ -129,3 +129,21 @@ def test_contact_map_engine_cell_list_equals_search_cell_list(c1_design, interph
             e.contacts_update(0.24 * 0.6)
     assert np.array_equal(a.get_positions(), b.get_positions())
     assert np.array_equal(a.contacts_accumulate(), b.contacts_accumulate())
+
+
+def test_deferred_contact_update_flushes_before_position_changes(c1_design, interphase_cfg):
+    """after a list-step run the update is counted inside the next step; a set_positions (or a read) in between
+    counts it first, from the positions it was asked for"""
+    e = engine_for(c1_design, interphase_cfg)
+    e.run(STEPS_PER_UPDATE, first_step=0, seed=3)
+    x0 = e.get_positions()
+    e.contacts_update(0.24)
+    e.set_positions(x0 + 0.05)   # the pending update must see x0, not these
+    e.run(STEPS_PER_UPDATE, first_step=STEPS_PER_UPDATE, seed=3)
+    x1 = e.get_positions()
+    e.contacts_update(0.24)      # pending again: the read flushes it
+    got = e.contacts_accumulate()
+    assert np.array_equal(got, expected_table([x0, x1], 0.24))
+    e.contacts_update(0.24)
+    e.contacts_clear()           # a pending update followed by a clear: an empty table
+    assert e.contacts_accumulate().shape == (0, 3)
