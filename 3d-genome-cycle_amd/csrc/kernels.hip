@@ -2883,50 +2883,73 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
                 for (int u = 0; u < kU; ++u) e[u] = en_[u];
             }
 #endif
-            if (__ballot(fb)) {
-                // exact search of the build's cell list around the current position: a partner within rc now was
-                // within rc + D of it at the build; the waves take alternate cell rows
-                if (fb) {
-                    const Grid lg = ctx->lgrid;
-                    const float R = rc + D + 1.0e-5f * (rc + D);
-                    const int x0 = lgrid_cell(lg, 0, pi.x - R), x1 = lgrid_cell(lg, 0, pi.x + R);
-                    const int y0 = lgrid_cell(lg, 1, pi.y - R), y1 = lgrid_cell(lg, 1, pi.y + R);
-                    const int z0 = lgrid_cell(lg, 2, pi.z - R), z1 = lgrid_cell(lg, 2, pi.z + R);
+            // exact search of the build's cell list for the particles the lists may not cover: a partner within rc
+            // now was within rc + D at the build.  Wave-cooperative: the wave takes its fallback lanes one at a
+            // time, its 64 lanes sweep that particle's candidate slots (the waves of the tile alternate over cell
+            // rows), and a wave sum hands the result to the particle's lane
+            unsigned long long fbm = __ballot(fb);
+            if (fbm) {
+                const Grid lg = ctx->lgrid;
+                const float R = rc + D + 1.0e-5f * (rc + D);
+                while (fbm) {
+                    const int L = __ffsll((long long)fbm) - 1;
+                    fbm &= fbm - 1ull;
+                    const float px = __shfl(pi.x, L), py = __shfl(pi.y, L), pz = __shfl(pi.z, L);
+                    const float pah = __shfl(ahi, L), pbh = __shfl(bhi, L);
+                    const int sL = uniform(__shfl(s, L));
+                    const int x0 = uniform(lgrid_cell(lg, 0, px - R)), x1 = uniform(lgrid_cell(lg, 0, px + R));
+                    const int y0 = uniform(lgrid_cell(lg, 1, py - R)), y1 = uniform(lgrid_cell(lg, 1, py + R));
+                    const int z0 = uniform(lgrid_cell(lg, 2, pz - R)), z1 = uniform(lgrid_cell(lg, 2, pz + R));
+                    float gx = 0.f, gy = 0.f, gz = 0.f, gn = 0.f;
                     int row = 0;
                     for (int z = z0; z <= z1; ++z)
                         for (int y = y0; y <= y1; ++y, ++row) {
                             if ((row % kListWaves) != wave) continue;
                             const int base = (z * lg.n[1] + y) * lg.n[0];
                             const int t0 = a.cstart[base + x0], t1 = a.cstart[base + x1 + 1];
-                            for (int t = t0; t < t1; ++t) {
-                                if (t == s) continue;
+                            for (int t = t0 + lane; t < t1; t += kTile) {
                                 const float4 q = qc[t];
-                                list_pair(pi.x, pi.y, pi.z, q, s_tab[(unsigned)__float_as_int(q.w) >> kListIndexBits],
-                                          ahi, bhi, kA, kB, k2a, k2b, rc2, true, fx, fy, fz, nbr);
+                                list_pair(px, py, pz, q, s_tab[(unsigned)__float_as_int(q.w) >> kListIndexBits], pah,
+                                          pbh, kA, kB, k2a, k2b, rc2, t != sL, gx, gy, gz, gn);
                             }
                         }
+                    gx = wave_sum(gx);
+                    gy = wave_sum(gy);
+                    gz = wave_sum(gz);
+                    gn = wave_sum(gn);
+                    if (lane == L) {
+                        fx += gx;
+                        fy += gy;
+                        fz += gz;
+                        nbr += gn;
+                    }
                 }
             }
         }
         if constexpr (CT) {
-            if (__ballot(fbc)) {
-                // contacts of the particles whose lists do not cover the contact distance: the build's cell list
-                // around the current position with radius d + D, the waves taking alternate cell rows
-                if (fbc) {
-                    const Grid lg = ctx->lgrid;
-                    const float R = rcc + D + 1.0e-5f * (rcc + D);
-                    const int x0 = lgrid_cell(lg, 0, pi.x - R), x1 = lgrid_cell(lg, 0, pi.x + R);
-                    const int y0 = lgrid_cell(lg, 1, pi.y - R), y1 = lgrid_cell(lg, 1, pi.y + R);
-                    const int z0 = lgrid_cell(lg, 2, pi.z - R), z1 = lgrid_cell(lg, 2, pi.z + R);
+            // contacts of the particles whose lists do not cover the contact distance: the build's cell list around
+            // the current position with radius d + D, swept by the whole wave per particle as above
+            unsigned long long fcm = __ballot(fbc);
+            if (fcm) {
+                const Grid lg = ctx->lgrid;
+                const float R = rcc + D + 1.0e-5f * (rcc + D);
+                while (fcm) {
+                    const int L = __ffsll((long long)fcm) - 1;
+                    fcm &= fcm - 1ull;
+                    const float4 pL = make_float4(__shfl(pi.x, L), __shfl(pi.y, L), __shfl(pi.z, L), 0.f);
+                    const int iL = __shfl(i, L), sL = uniform(__shfl(s, L));
+                    const int x0 = uniform(lgrid_cell(lg, 0, pL.x - R)), x1 = uniform(lgrid_cell(lg, 0, pL.x + R));
+                    const int y0 = uniform(lgrid_cell(lg, 1, pL.y - R)), y1 = uniform(lgrid_cell(lg, 1, pL.y + R));
+                    const int z0 = uniform(lgrid_cell(lg, 2, pL.z - R)), z1 = uniform(lgrid_cell(lg, 2, pL.z + R));
                     int row = 0;
                     for (int z = z0; z <= z1; ++z)
                         for (int y = y0; y <= y1; ++y, ++row) {
                             if ((row % kListWaves) != wave) continue;
                             const int base = (z * lg.n[1] + y) * lg.n[0];
                             const int t0 = a.cstart[base + x0], t1 = a.cstart[base + x1 + 1];
-                            for (int t = t0; t < t1; ++t) {
+                            for (int t = t0 + lane; t < t1; t += kTile) {
                                 const float4 q = qc[t];
-                                if (t != s) list_contact(a, pi, q, i, __float_as_int(q.w) & kIdx);
+                                if (t != sL) list_contact(a, pL, q, iL, __float_as_int(q.w) & kIdx);
                             }
                         }
                 }

@@ -187,3 +187,21 @@ def test_statistics_engine_vs_oracle(c1_design):
     assert (z <= 3.0).all(), dict(zip(names, z.tolist()))
     # and the runs did move: the seed spread is not zero
     assert (se[:3] > 0).all() and (so[:3] > 0).all()
+
+
+def test_c2_relaxation_spacestep():
+    """The relaxation stage's adaptive step (simulation_driver_relaxation.cpp:48-55: spacestep 1e-3) at C2 size from
+    the synthetic start, injected reference noise, 5 steps: positions within the bound, the adapted timestep equal"""
+    design, cfg = synthetic.make_c2(), InterphaseConfig()
+    steps = 5
+    xi = oracle.reference_normals(design.seed, steps * design.n * 3).reshape(steps, design.n, 3)
+    e, o = _pair(design, cfg, x=_f32(design.positions))
+    for s in (e, o):
+        s.apply_schedule(0)
+        s.set_noise(xi)
+        s.run(steps, temperature=cfg.temperature, timestep=cfg.timestep, spacestep=cfg.relaxation_spacestep,
+              noise=1)
+    err = float(np.abs(e.get_positions() - o.get_positions()).max())
+    _log(test="c2_relaxation", error=err)
+    assert err <= TOL_X
+    assert e.get_context()["last_timestep"] == pytest.approx(o.get_context()["last_timestep"], rel=1e-4)
