@@ -187,6 +187,8 @@ struct gcs_engine {
     bool scan_mb = true;  // GCS_OPT_SCAN_BLOCKS: multi-block cell scan (the heavy-tile split keeps one block)
     hipGraphExec_t gexec = nullptr;
     hipGraph_t graph = nullptr;
+    hipGraphExec_t lgexec[2] = {nullptr, nullptr};  // list step: one graph per starting parity
+    hipGraph_t lgraph[2] = {nullptr, nullptr};
     int g_steps = 0, g_waves = 0, g_version = -1, g_spacestep = -1;
     gcs_bd_config g_cfg{};
     int g_sched_flags = -1;
@@ -228,6 +230,12 @@ void drop_graph(gcs_engine* e)
     if (e->graph) (void)hipGraphDestroy(e->graph);
     e->gexec = nullptr;
     e->graph = nullptr;
+    for (int p = 0; p < 2; ++p) {
+        if (e->lgexec[p]) (void)hipGraphExecDestroy(e->lgexec[p]);
+        if (e->lgraph[p]) (void)hipGraphDestroy(e->lgraph[p]);
+        e->lgexec[p] = nullptr;
+        e->lgraph[p] = nullptr;
+    }
 }
 
 FieldRec* new_field(gcs_engine* e, int kind)
@@ -613,6 +621,7 @@ ForceArgs list_args(const gcs_engine* e)
     a.list_stride = (e->n + 63) & ~63;
     a.list_skin = list_skin(e);
     a.list_waves = e->list_waves;
+    a.par_hint = -1;
     return a;
 }
 
@@ -657,9 +666,10 @@ int auto_list_every(const gcs_engine* e, const gcs_bd_config* cfg)
 
 // one list step: on a rebuild step the cell list at cutoff + skin (ctx->grid, set by the prime or the last
 // tail), the lists, then the step itself (forces + local terms + update + tail in the last workgroup)
-void enqueue_list_step(gcs_engine* e, bool build, double contact = 0)
+void enqueue_list_step(gcs_engine* e, bool build, double contact = 0, int parity = -1)
 {
     ForceArgs la = list_args(e);
+    la.par_hint = parity;
     if (contact > 0) {  // the pending contact update, counted from this step's start positions
         la.contact_on = 1;
         const float d = (float)contact;
@@ -1428,26 +1438,35 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
         // aligned step, the rest runs eagerly
         const int M = e->list_every;
         const int GM = G > 0 ? M * ((G + M - 1) / M) : 0;
+        // the host knows every step's position-buffer parity (the kernels' slot loads then need no context read);
+        // a captured graph bakes its steps' parities in, so there is one graph per starting parity
+        auto par = [&](int64_t k) { return e->parity ^ (int)(k & 1); };
         while (done < steps) {
             const int64_t st = first_step + done;
             const bool aligned = (st % M) == 0;
             if (e->c_pending > 0) {  // the contact update the host asked for after the last step
-                enqueue_list_step(e, e->l_need_build || aligned, e->c_pending);
+                enqueue_list_step(e, e->l_need_build || aligned, e->c_pending, par(done));
                 e->c_pending = 0;
                 e->l_need_build = false;
                 ++done;
                 continue;
             }
             if (GM > 0 && !e->l_need_build && aligned && steps - done >= GM) {
-                const bool same = e->gexec && e->g_steps == GM && e->g_version == e->topo_version && e->g_fused == 3 &&
-                                  e->g_list_every == M && e->g_sched_flags == e->sched_flags &&
+                const int p0 = par(done);
+                const bool same = e->lgexec[p0] && e->g_steps == GM && e->g_version == e->topo_version &&
+                                  e->g_fused == 3 && e->g_list_every == M && e->g_sched_flags == e->sched_flags &&
                                   std::memcmp(&e->g_cfg, cfg, sizeof(*cfg)) == 0;
                 if (!same) {
-                    drop_graph(e);
+                    if (!(e->g_steps == GM && e->g_version == e->topo_version && e->g_fused == 3 &&
+                          e->g_list_every == M && e->g_sched_flags == e->sched_flags &&
+                          std::memcmp(&e->g_cfg, cfg, sizeof(*cfg)) == 0))
+                        drop_graph(e);  // the other parity's graph is stale too
+                    hipGraph_t g = nullptr;
                     HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
-                    for (int k = 0; k < GM; ++k) enqueue_list_step(e, k % M == 0);
-                    HIPCHK(hipStreamEndCapture(e->stream, &e->graph));
-                    HIPCHK(hipGraphInstantiate(&e->gexec, e->graph, nullptr, nullptr, 0));
+                    for (int k = 0; k < GM; ++k) enqueue_list_step(e, k % M == 0, 0, p0 ^ (k & 1));
+                    HIPCHK(hipStreamEndCapture(e->stream, &g));
+                    e->lgraph[p0] = g;
+                    HIPCHK(hipGraphInstantiate(&e->lgexec[p0], g, nullptr, nullptr, 0));
                     e->g_steps = GM;
                     e->g_version = e->topo_version;
                     e->g_fused = 3;
@@ -1458,10 +1477,15 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
                     e->g_waves = e->waves;
                     e->g_chunk = e->fa.chunk_mode;
                 }
-                for (; steps - done >= GM; done += GM) HIPCHK(hipGraphLaunch(e->gexec, e->stream));
+                // GM odd: consecutive replays alternate the starting parity
+                for (; steps - done >= GM; done += GM) {
+                    const int pk = par(done);
+                    if (!e->lgexec[pk]) break;  // the other parity's graph: captured on the next pass
+                    HIPCHK(hipGraphLaunch(e->lgexec[pk], e->stream));
+                }
                 continue;
             }
-            enqueue_list_step(e, e->l_need_build || aligned);
+            enqueue_list_step(e, e->l_need_build || aligned, 0, par(done));
             e->l_need_build = false;
             ++done;
         }
@@ -2221,7 +2245,9 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
                 launch_list_build(e->stream, e->ctx, la);
             }
             HIPCHK(hipEventRecord(ev[2 + 5 * k], e->stream));
-            launch_list_step(e->stream, e->ctx, la, e->sched_flags != 0);
+            ForceArgs lk = la;
+            lk.par_hint = e->parity ^ (int)(k & 1);  // as gcs_engine_run launches it
+            launch_list_step(e->stream, e->ctx, lk, e->sched_flags != 0);
             e->fa.dbg_times = nullptr;
             for (int q = 3; q <= 5; ++q) HIPCHK(hipEventRecord(ev[q + 5 * k], e->stream));
             continue;

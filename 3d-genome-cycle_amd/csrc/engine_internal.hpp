@@ -202,6 +202,8 @@ struct ForceArgs {
     int list_stride;        // >= N
     float list_skin;        // > 0 only in the list path's own argument block
     int list_waves;         // waves per tile (list segments): 4, or 2 (GCS_OPT_LIST_WAVES)
+    int par_hint;           // >= 0: ctx->parity of this launch, known to the host at enqueue (the slot loads need not
+                            // wait for the context); -1: read it
     // the contact-map update fused into a list step (stage_interphase/contact_map.cpp:33-63): every pair i < j of
     // the step's START positions closer than sqrt(contact_d2) (strict fp32 predicate) is counted into the table
     int contact_on;

@@ -2771,7 +2771,7 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
     // contacts only (its forces take exactly the path they take without contacts: identical bits)
     const float rcc = CT ? fmaxf(rc, sqrtf(a.contact_d2)) : rc;
     const float slack_c = 0.999f * a.list_skin - D - fmaxf(rcc - ctx->lrc_b, 0.f);
-    const int par = ctx->parity;
+    const int par = a.par_hint >= 0 ? a.par_hint : ctx->parity;
     float4* __restrict__ pn = par ? a.pos0 : a.pos1;  // particle order (bonded partners read ctx->parity's)
     const float4* __restrict__ qc = par ? a.psort1 : a.psort0;  // slot order (pair partners)
     float4* __restrict__ qn = par ? a.psort0 : a.psort1;
