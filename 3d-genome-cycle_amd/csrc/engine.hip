@@ -198,6 +198,8 @@ struct gcs_engine {
     int* list = nullptr;
     int* lcount = nullptr;
     float4* psort[2] = {nullptr, nullptr};
+    float4* skmu = nullptr;  // list step: slot-ordered kmu and bond CSR rows
+    int2* sbrow = nullptr;
     int* ptype = nullptr;
     unsigned* lticket = nullptr;  // list step: two-level arrival counters + group rows
     float* lgroup = nullptr;
@@ -613,6 +615,8 @@ ForceArgs list_args(const gcs_engine* e)
     a.ptype = e->ptype;
     a.psort0 = e->psort[0];
     a.psort1 = e->psort[1];
+    a.skmu = e->skmu;
+    a.sbrow = e->sbrow;
     a.lticket = e->lticket;
     a.lgroup = e->lgroup;
     a.type_ab = e->type_ab;
@@ -634,10 +638,13 @@ int ensure_list(gcs_engine* e)
     dfree(e->lcount);
     dfree(e->psort[0]);
     dfree(e->psort[1]);
+    dfree(e->skmu);
+    dfree(e->sbrow);
     e->list_alloc = 0;
     int rc;
     if ((rc = dalloc(&e->list, need)) || (rc = dalloc(&e->lcount, stride * kMaxListWaves)) ||
-        (rc = dalloc(&e->psort[0], stride)) || (rc = dalloc(&e->psort[1], stride)))
+        (rc = dalloc(&e->psort[0], stride)) || (rc = dalloc(&e->psort[1], stride)) ||
+        (rc = dalloc(&e->skmu, stride)) || (rc = dalloc(&e->sbrow, stride)))
         return rc;
     if (!e->lticket) {
         if ((rc = dalloc(&e->lticket, 32 * 9)) || (rc = dalloc(&e->lgroup, 8 * 24))) return rc;
@@ -684,7 +691,8 @@ void enqueue_list_step(gcs_engine* e, bool build, double contact = 0, int parity
         enqueue_scan(e, false);
         launch_cell_scatter(e->stream, e->n, e->cell_of, e->slot, e->cstart, e->tmp, e->count);
         launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, e->n, e->tmp, e->cell_of, e->cstart,
-                         e->sidx, e->scell, e->spos, e->sb, e->fa.pair_mix, e->ptype, e->psort[0], e->psort[1]);
+                         e->sidx, e->scell, e->spos, e->sb, e->fa.pair_mix, e->ptype, e->psort[0], e->psort[1], e->skmu,
+                         e->sbrow, e->fa.has_bonds ? e->boff : nullptr);
         launch_list_build(e->stream, e->ctx, la);
     }
     launch_list_step(e->stream, e->ctx, la, e->sched_flags != 0);
@@ -1022,8 +1030,8 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
         (rc = dalloc(&e->cstart, e->ncell_max + kScanPad)) || (rc = dalloc(&e->tile_start, e->ncell_max + 2)) ||
         (rc = dalloc(&e->tile_range, (size_t)force_blocks(n) + e->ncell_max + 2)) ||
         (rc = dalloc(&e->ctx, 1)) || (rc = dalloc(&e->dsched, kSchedCount)) ||
-        (rc = dalloc(&e->part_force, (size_t)std::max(fb, ub) * kForcePartials)) ||
-        (rc = dalloc(&e->part_bbox, (size_t)std::max(fb, ub) * kBBoxStride)) ||
+        (rc = dalloc(&e->part_force, (size_t)(std::max(fb, ub) + 8) * kForcePartials)) ||  // + the list step's
+        (rc = dalloc(&e->part_bbox, (size_t)(std::max(fb, ub) + 8) * kBBoxStride)) ||       // 8 group rows
         (rc = dalloc(&e->part_energy, (size_t)fb * kEnergyKinds)) || (rc = dalloc(&e->force_out, n)) ||
         (rc = dalloc(&e->pbuf, (size_t)2 * std::max(force_grid(n), kMaxUnits) * kTile)) ||
         (rc = dalloc(&e->tcnt, std::max(force_grid(n), kMaxUnits))) || (rc = dalloc(&e->units, 2 * kMaxUnits)) ||
@@ -1068,6 +1076,8 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->lcount);
     dfree(e->psort[0]);
     dfree(e->psort[1]);
+    dfree(e->skmu);
+    dfree(e->sbrow);
     dfree(e->lticket);
     dfree(e->lgroup);
     dfree(e->ptype);
@@ -2241,7 +2251,8 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
                 enqueue_scan(e, false);
                 launch_cell_scatter(e->stream, e->n, e->cell_of, e->slot, e->cstart, e->tmp, e->count);
                 launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, e->n, e->tmp, e->cell_of, e->cstart,
-                                 e->sidx, e->scell, e->spos, e->sb, e->fa.pair_mix, e->ptype, e->psort[0], e->psort[1]);
+                                 e->sidx, e->scell, e->spos, e->sb, e->fa.pair_mix, e->ptype, e->psort[0], e->psort[1], e->skmu,
+                         e->sbrow, e->fa.has_bonds ? e->boff : nullptr);
                 launch_list_build(e->stream, e->ctx, la);
             }
             HIPCHK(hipEventRecord(ev[2 + 5 * k], e->stream));

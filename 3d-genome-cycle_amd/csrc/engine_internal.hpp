@@ -196,6 +196,8 @@ struct ForceArgs {
     const int* ptype;       // [N] pair-factor class of each particle
     float4* psort0;
     float4* psort1;
+    float4* skmu;           // [N] per slot: kmu of its particle (list path, k_cell_sort)
+    int2* sbrow;            // [N] per slot: its particle's bond CSR row [boff[i], boff[i + 1])
     const float2* type_ab;  // [kMaxTypes] (a, b) pair factors of each class
     int ntypes;
     int list_cap;           // entries per (slot, wave)
@@ -265,7 +267,8 @@ void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* sl
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, const float4* kmu,
                       int n, const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell,
                       float4* spos, float* sb, int pair_mix, const int* ptype = nullptr, float4* psort0 = nullptr,
-                      float4* psort1 = nullptr);
+                      float4* psort1 = nullptr, float4* skmu = nullptr, int2* sbrow = nullptr,
+                      const int* boff = nullptr);
 // list step: build the neighbour lists on the current cell list (grid rc = cutoff + skin); one step from them
 void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a);
 void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int apply_sched);

@@ -1188,7 +1188,8 @@ __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ct
                                                    int* __restrict__ scell, float4* __restrict__ spos,
                                                    float* __restrict__ sb, int pair_mix,
                                                    const int* __restrict__ ptype, float4* __restrict__ psort0,
-                                                   float4* __restrict__ psort1)
+                                                   float4* __restrict__ psort1, float4* __restrict__ skmu,
+                                                   int2* __restrict__ sbrow, const int* __restrict__ boff)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n || s >= cstart[ctx->grid.ncell]) return;  // binned particles only (all of them, undecomposed)
@@ -1206,8 +1207,12 @@ __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ct
     // the pair field's factors: (a, b) when it mixes A/B (interphase), (1, 0) for plain softcore<2,3>
     spos[d] = make_float4(p.x, p.y, p.z, pair_mix ? k.y : 1.f);
     sb[d] = pair_mix ? k.z : 0.f;
-    if (psort0)  // list path: the current positions in slot order, .w = particle | class << 24
+    if (psort0) {  // list path: the current positions in slot order, .w = particle | class << 24; the slot's
+                   // constants and bond CSR row (the list step reads them by slot, not behind the particle index)
         (ctx->parity ? psort1 : psort0)[d] = make_float4(p.x, p.y, p.z, __int_as_float(i | (ptype[i] << kListIndexBits)));
+        skmu[d] = k;
+        sbrow[d] = boff ? make_int2(boff[i], boff[i + 1]) : make_int2(0, 0);
+    }
 }
 
 // ----------------------------------------------------------------------------------------------------
@@ -1277,7 +1282,7 @@ __device__ inline float spring_coef(int type, float K, float l, float r2, float&
 template <int MODE, int BB = 1>
 __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceArgs& a, int i, float xi, float yi,
                                    float zi, float4 km, float& fx, float& fy, float& fz, float* en, float* rin,
-                                   float* rout)
+                                   float* rout, int2 erange = make_int2(-1, -1))
 {
     const int n = a.n;
     const float4* __restrict__ posc = ctx->parity ? a.pos1 : a.pos0;
@@ -1285,7 +1290,8 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
     const float bs = (float)ctx->bs;
     float e_sw = 0.f, e_bond = 0.f, e_bend = 0.f, e_win = 0.f, e_wout = 0.f, e_pt = 0.f, e_kf = 0.f;
     if (a.has_bonds) {
-        const int eb = a.boff[i], ee = a.boff[i + 1];
+        // erange: the particle's CSR row when the caller already has it (the list step's slot-ordered copy)
+        const int eb = erange.x >= 0 ? erange.x : a.boff[i], ee = erange.x >= 0 ? erange.y : a.boff[i + 1];
         for (int q0 = eb; q0 < ee; q0 += BB) {
           int2 enb[BB];
           float4 bvb[BB], pjb[BB];
@@ -2505,6 +2511,9 @@ __global__ __launch_bounds__(256) void k_tail(DevCtx* ctx, ForceArgs a, int fblo
 #ifndef GCS_LIST_XTILE
 #define GCS_LIST_XTILE 1  // 1: the next tile's slot loads are issued before this tile's work (grid-stride tiles)
 #endif
+#ifndef GCS_LIST_GROUP_REDUCE
+#define GCS_LIST_GROUP_REDUCE 0  // 1: each group's last workgroup reduces its group's rows; the final one, 8 group rows
+#endif
 #ifndef GCS_LIST_BOND_BATCH
 #define GCS_LIST_BOND_BATCH 4  // bond CSR entries whose loads are issued together in the particle-local terms
 #endif
@@ -2534,19 +2543,47 @@ __device__ __forceinline__ void list_contact(const ForceArgs& a, float4 p, float
 // The list step's context update, by thread 0 of the step's final workgroup once every partial is reduced: the
 // tail_body arithmetic of one undecomposed, unfused step (reactions, bbox, step/parity/noise cursor, the schedule of
 // stage_interphase/simulation_driver_interphase.cpp:17, :67-90 and the cell grid at cutoff + skin for a rebuild)
-__device__ void list_tail_apply(DevCtx* ctx, const ForceArgs& a, const double* tot, const float* bb, float ld, float lf,
-                                int apply_sched)
+// The tail's inputs besides the partial rows (the schedule and the context), loaded by the final workgroup before
+// it reduces the rows, so their round trip overlaps the rows'
+struct ListTailIn {
+    double s_flags, s_dt, s_cs0, s_csTau, s_bs0, s_bsTau, s_muW, s_k[3];
+    long long c_step, c_cursor, c_fb;
+    int c_parity;
+    double c_time, c_cs, c_bs, c_w[3];
+};
+__device__ __forceinline__ ListTailIn list_tail_load(const DevCtx* ctx, const ForceArgs& a)
 {
     const double* sched = a.sched;
-    // every input first (independent loads: one round trip)
-    const double s_flags = sched[kSchedFlags], s_dt = sched[kSchedDt], s_cs0 = sched[kSchedCs0],
-                 s_csTau = sched[kSchedCsTau], s_bs0 = sched[kSchedBs0], s_bsTau = sched[kSchedBsTau],
-                 s_muW = sched[kSchedMuW];
-    const double s_k[3] = {sched[kSchedK0], sched[kSchedK0 + 1], sched[kSchedK0 + 2]};
-    const long long c_step = ctx->step, c_cursor = ctx->noise_cursor, c_fb = ctx->lfallback;
-    const int c_parity = ctx->parity;
-    const double c_time = ctx->time, c_cs = ctx->cs, c_bs = ctx->bs;
-    const double c_w[3] = {ctx->wall[0], ctx->wall[1], ctx->wall[2]};
+    ListTailIn t;
+    t.s_flags = sched[kSchedFlags];
+    t.s_dt = sched[kSchedDt];
+    t.s_cs0 = sched[kSchedCs0];
+    t.s_csTau = sched[kSchedCsTau];
+    t.s_bs0 = sched[kSchedBs0];
+    t.s_bsTau = sched[kSchedBsTau];
+    t.s_muW = sched[kSchedMuW];
+    for (int k = 0; k < 3; ++k) t.s_k[k] = sched[kSchedK0 + k];
+    t.c_step = ctx->step;
+    t.c_cursor = ctx->noise_cursor;
+    t.c_fb = ctx->lfallback;
+    t.c_parity = ctx->parity;
+    t.c_time = ctx->time;
+    t.c_cs = ctx->cs;
+    t.c_bs = ctx->bs;
+    for (int k = 0; k < 3; ++k) t.c_w[k] = ctx->wall[k];
+    return t;
+}
+
+__device__ void list_tail_apply(DevCtx* ctx, const ForceArgs& a, const ListTailIn& in, const double* tot,
+                                const float* bb, float ld, float lf, int apply_sched)
+{
+    const double s_flags = in.s_flags, s_dt = in.s_dt, s_cs0 = in.s_cs0, s_csTau = in.s_csTau, s_bs0 = in.s_bs0,
+                 s_bsTau = in.s_bsTau, s_muW = in.s_muW;
+    const double* s_k = in.s_k;
+    const long long c_step = in.c_step, c_cursor = in.c_cursor, c_fb = in.c_fb;
+    const int c_parity = in.c_parity;
+    const double c_time = in.c_time, c_cs = in.c_cs, c_bs = in.c_bs;
+    const double* c_w = in.c_w;
     for (int k = 0; k < 3; ++k) {
         ctx->react_in[k] = tot[k];
         ctx->react_out[k] = tot[3 + k];
@@ -2783,30 +2820,36 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
     // are issued before the previous tile's work and, for the first tile, before the type-table barrier
     // tiles: 64 consecutive slots (the lists are per slot; no cell-row structure is needed here)
     int tile = blockIdx.x;
-    float4 n_pi = make_float4(0.f, 0.f, 0.f, 0.f), n_pb = n_pi;
+    float4 n_pi = make_float4(0.f, 0.f, 0.f, 0.f), n_pb = n_pi, n_km = n_pi;
+    int2 n_br = make_int2(0, 0);
     int n_cw = 0, n_e[kU];
-    auto load_tile = [&](int t) {
+    auto load_tile = [&](int t, bool first) {
         const int sl = min(t * kTile + lane, n - 1);
         n_pi = qc[sl];    // current position, .w = particle | class << 24
         n_pb = a.spos[sl];  // build position
+        if (first && wave == kListWaves - 1) {  // the local-terms wave: the slot's constants and bond row (the
+            n_km = a.skmu[sl];                  // first tile only: held across a pair loop they would spill)
+            n_br = a.sbrow[sl];
+        }
         n_cw = a.lcount[(size_t)wave * stride + sl];
         const LE* __restrict__ seg = reinterpret_cast<const LE*>(a.list) + (size_t)wave * cap * stride + sl;
 #pragma unroll
         for (int u = 0; u < kU; ++u) n_e[u] = seg[(size_t)u * stride];  // list_cap >= kU: in bounds
     };
-    if (tile * kTile < n) load_tile(tile);
+    if (tile * kTile < n) load_tile(tile, true);
     __syncthreads();
     for (; tile * kTile < n; tile += gridDim.x) {
         const int s = tile * kTile + lane;
         const bool valid = s < n;
         const int sl = valid ? s : n - 1;
         const float4 pi = n_pi, pb = n_pb;
+        const bool first = tile == (int)blockIdx.x;
         const int cw = n_cw;
         int e[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) e[u] = n_e[u];
 #if GCS_LIST_XTILE
-        if ((tile + (int)gridDim.x) * kTile < n) load_tile(tile + gridDim.x);
+        if ((tile + (int)gridDim.x) * kTile < n) load_tile(tile + gridDim.x, false);
 #endif
         const LE* __restrict__ seg = reinterpret_cast<const LE*>(a.list) + (size_t)wave * cap * stride + sl;
         const int pk = __float_as_int(pi.w);
@@ -2818,10 +2861,12 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
         const bool fbc = CT && valid && (di > slack_c || (cw & kListOverflow) != 0);  // implies fb's condition
 
         if (wave == kListWaves - 1) {  // the particle-local terms first (a dependent-gather chain), parked in LDS
-            const float4 km = a.kmu[i];
+            const float4 km = first ? n_km : a.skmu[sl];
+            const int2 erow = first ? n_br : a.sbrow[sl];
             float lfx = 0.f, lfy = 0.f, lfz = 0.f, en[kEnergyKinds];
             float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
-            local_terms<kModeStep, GCS_LIST_BOND_BATCH>(ctx, a, i, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout);
+            local_terms<kModeStep, GCS_LIST_BOND_BATCH>(ctx, a, i, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout,
+                                                        erow);
             s_locf[lane] = make_float4(lfx, lfy, lfz, km.x);
             s_locr[lane] = make_float4(rin[0], rin[1], rin[2], 0.f);
             s_loco[lane] = make_float4(rout[0], rout[1], rout[2], 0.f);
@@ -3058,6 +3103,23 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
     if (!s_last) return;
     // the last workgroup of a group: count the group in; the last group's last workgroup is the final one
     __shared__ int s_final;
+#if GCS_LIST_GROUP_REDUCE
+    {  // the group's rows (workgroups g, g + 8, ...) into group row gridDim.x + g
+        double tot[8];
+        float bb[6], ld = 0.f, lf = 0.f;
+        list_reduce_rows(a, g, ngroups, gsize, tot, bb, ld, lf);
+        if (tid == 0) {
+            const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_force, 0, 0x7fffffff, 0x00020000);
+            const auto rb = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_bbox, 0, 0x7fffffff, 0x00020000);
+            const int off = (gridDim.x + g) * 32;
+            st_sc1_f4(rf, off, make_float4((float)tot[0], (float)tot[1], (float)tot[2], (float)tot[3]));
+            st_sc1_f4(rf, off + 16, make_float4((float)tot[4], (float)tot[5], (float)tot[6], (float)tot[7]));
+            st_sc1_f4(rb, off, make_float4(bb[0], bb[1], bb[2], bb[3]));
+            st_sc1_f4(rb, off + 16, make_float4(bb[4], bb[5], ld, lf));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+#endif
     if (tid == 0) {
         a.lticket[32 * g] = 0u;  // ready for the next launch
         const unsigned old = atomicAdd(&a.lticket[32 * 8], 1u);
@@ -3065,17 +3127,23 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
     }
     __syncthreads();
     if (!s_final) return;
-    // the final workgroup: every partial row in workgroup order, then the context update
+    // the final workgroup: the group rows in group order (or every partial row in workgroup order), then the
+    // context update
     unsigned long long* const dbt = a.dbg_times ? a.dbg_times + 8 * gridDim.x : nullptr;
     if (dbt && tid == 0) dbt[0] = wall_clock64();
     {
+        const ListTailIn tin = list_tail_load(ctx, a);
         double tot[8];
         float bb[6], ld = 0.f, lf = 0.f;
+#if GCS_LIST_GROUP_REDUCE
+        list_reduce_rows(a, gridDim.x, 1, ngroups, tot, bb, ld, lf);
+#else
         list_reduce_rows(a, 0, 1, gridDim.x, tot, bb, ld, lf);
+#endif
         if (tid == 0) {
             if (dbt) dbt[1] = wall_clock64();
             a.lticket[32 * 8] = 0u;
-            list_tail_apply(ctx, a, tot, bb, ld, lf, apply_sched);
+            list_tail_apply(ctx, a, tin, tot, bb, ld, lf, apply_sched);
             if (dbg) dbg[7] = wall_clock64();
         }
     }
@@ -3232,10 +3300,11 @@ void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* sl
 
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, const float4* kmu, int n,
                       const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell, float4* spos,
-                      float* sb, int pair_mix, const int* ptype, float4* psort0, float4* psort1)
+                      float* sb, int pair_mix, const int* ptype, float4* psort0, float4* psort1, float4* skmu,
+                      int2* sbrow, const int* boff)
 {
     hipLaunchKernelGGL(k_cell_sort, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, kmu, n, tmp, cell_of,
-                       cstart, sidx, scell, spos, sb, pair_mix, ptype, psort0, psort1);
+                       cstart, sidx, scell, spos, sb, pair_mix, ptype, psort0, psort1, skmu, sbrow, boff);
 }
 
 template <int MODE, bool FUSED>
