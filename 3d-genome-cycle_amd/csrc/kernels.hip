@@ -2699,6 +2699,25 @@ __device__ void list_reduce_rows(const ForceArgs& a, int first, int stride, int 
     }
 }
 
+#ifndef GCS_XCD_REMAP
+#define GCS_XCD_REMAP 1  // 1: the list kernels give each XCD a contiguous range of tiles (see xcd_block)
+#endif
+// Workgroups are dispatched to the 8 XCDs round-robin (b % 8), each XCD with its own L2.  Tiles are spatially
+// ordered (slots sorted by cell), so handing XCD x the contiguous tile range x * G / 8 ... instead of every 8th
+// tile keeps the pair partners an XCD gathers within its own slab: each L2 fetches about 1/8 of the positions
+// instead of all of them.  A bijection of [0, G) (G need not be a multiple of 8); the dispatch order only affects
+// speed, never which tiles are processed.
+__device__ __forceinline__ int xcd_block(int b, int G)
+{
+#if GCS_XCD_REMAP
+    const int x = b & 7, k = b >> 3, q = G >> 3, r = G & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+#else
+    (void)G;
+    return b;
+#endif
+}
+
 // LE: list entry type (unsigned short when every slot index fits 16 bits: half the list traffic)
 template <typename LE, int kListWaves>
 __global__ __launch_bounds__(64 * kListWaves) void k_lbuild(DevCtx* __restrict__ ctx, ForceArgs a)
@@ -2719,7 +2738,10 @@ __global__ __launch_bounds__(64 * kListWaves) void k_lbuild(DevCtx* __restrict__
         ctx->nactive = 0;  // the list step's tail reads every workgroup's partial row
     }
     int ntot = 0;
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // the launch has force_grid(n) workgroups, the cell rows need ntiles (device-side): remap over the ones in use
+    const int gused = min((int)gridDim.x, ntiles);
+    for (int tile = (int)blockIdx.x < gused ? xcd_block(blockIdx.x, gused) : ntiles; tile < ntiles;
+         tile += gridDim.x) {
         const int2 tr = a.tile_range[tile];
         const int s_begin = uniform(tr.x), s_end = uniform(tr.y);
         const int s = s_begin + lane;
@@ -2819,7 +2841,8 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
     // software-pipelined by one tile: a tile's slot loads (one round trip, nothing depends on anything but the slot)
     // are issued before the previous tile's work and, for the first tile, before the type-table barrier
     // tiles: 64 consecutive slots (the lists are per slot; no cell-row structure is needed here)
-    int tile = blockIdx.x;
+    const int tile0 = xcd_block(blockIdx.x, gridDim.x);
+    int tile = tile0;
     float4 n_pi = make_float4(0.f, 0.f, 0.f, 0.f), n_pb = n_pi, n_km = n_pi;
     int2 n_br = make_int2(0, 0);
     int n_cw = 0, n_e[kU];
@@ -2843,7 +2866,7 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
         const bool valid = s < n;
         const int sl = valid ? s : n - 1;
         const float4 pi = n_pi, pb = n_pb;
-        const bool first = tile == (int)blockIdx.x;
+        const bool first = tile == tile0;
         const int cw = n_cw;
         int e[kU];
 #pragma unroll
@@ -2874,7 +2897,7 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
 
         float fx = 0.f, fy = 0.f, fz = 0.f, nbr = 0.f;
         const float ahi = kA * own.x, bhi = kB * own.y;
-        const bool stamp = dbg && tid == 0 && tile == (int)blockIdx.x;
+        const bool stamp = dbg && tid == 0 && tile == tile0;
         if (stamp) dbg[1] = wall_clock64();
         if (a.has_pair) {
             const int cnt = (valid && !fb) ? min(cw & kListCountMask, cap) : 0;

@@ -17,7 +17,8 @@ for ctrs in \
   "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS" \
   "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
   "FETCH_SIZE" \
-  "WRITE_SIZE" ; do
+  "WRITE_SIZE" \
+  "TCC_HIT_sum TCC_MISS_sum" ; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $ctrs -d "$out/pmc$i" -o run --output-format csv -- "${bench[@]}" > "$out/pmc$i.log" 2>&1 || { echo "pmc pass $i failed rc=$?"; exit 1; }
 done
