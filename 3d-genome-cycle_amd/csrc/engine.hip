@@ -201,8 +201,7 @@ struct gcs_engine {
     float4* skmu = nullptr;  // list step: slot-ordered kmu and bond CSR rows
     int2* sbrow = nullptr;
     int* ptype = nullptr;
-    unsigned* lticket = nullptr;  // list step: two-level arrival counters + group rows
-    float* lgroup = nullptr;
+    unsigned* lticket = nullptr;  // list step: two-level arrival counters (8 groups + the top), 128 B apart
     float2* type_ab = nullptr;
     int ntypes = 0;
     bool list_ok = false;       // the system admits the list step (a pair field, <= 256 classes, N < 2^24)
@@ -618,7 +617,6 @@ ForceArgs list_args(const gcs_engine* e)
     a.skmu = e->skmu;
     a.sbrow = e->sbrow;
     a.lticket = e->lticket;
-    a.lgroup = e->lgroup;
     a.type_ab = e->type_ab;
     a.ntypes = e->ntypes;
     a.list_cap = e->list_cap / e->list_waves;  // per (particle, wave) segment
@@ -647,7 +645,7 @@ int ensure_list(gcs_engine* e)
         (rc = dalloc(&e->skmu, stride)) || (rc = dalloc(&e->sbrow, stride)))
         return rc;
     if (!e->lticket) {
-        if ((rc = dalloc(&e->lticket, 32 * 9)) || (rc = dalloc(&e->lgroup, 8 * 24))) return rc;
+        if ((rc = dalloc(&e->lticket, 32 * 9))) return rc;
         HIPCHK(hipMemsetAsync(e->lticket, 0, 32 * 9 * sizeof(unsigned), e->stream));
     }
     // entries past a slot's count are read (never gathered): keep them defined
@@ -1079,7 +1077,6 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->skmu);
     dfree(e->sbrow);
     dfree(e->lticket);
-    dfree(e->lgroup);
     dfree(e->ptype);
     dfree(e->type_ab);
     dfree(e->spos);

@@ -215,7 +215,6 @@ struct ForceArgs {
     int c_bits;
     int* c_overflow;
     unsigned* lticket;      // list step arrival counters: [32 g] per group of workgroups (g < 8), [32 * 8] groups
-    float* lgroup;          // [8][24] group partial rows (8 doubles + 8 floats)
 };
 
 constexpr int kMaxListWaves = 4;  // waves per tile of the list kernels (each owns one list segment): 2 or 4

@@ -1,6 +1,7 @@
 #!/bin/bash
 # the bench line (no CPU leg, no start window) with the default library and every build/variants/*.so
 set -u
+shopt -s nullglob
 out=gpurun_out/bench_variants.log
 : > $out
 for lib in 3d-genome-cycle_amd/gcs/libgcs.so build/variants/*.so; do

@@ -1,6 +1,7 @@
 #!/bin/bash
 # time the list step of every library under build/variants (and the default build) on the bench workload
 set -u
+shopt -s nullglob
 out=gpurun_out/variants.log
 : > $out
 for lib in 3d-genome-cycle_amd/gcs/libgcs.so build/variants/*.so; do
