@@ -2699,6 +2699,9 @@ __device__ void list_reduce_rows(const ForceArgs& a, int first, int stride, int 
     }
 }
 
+#ifndef GCS_LBUILD_GROUPS
+#define GCS_LBUILD_GROUPS 2  // k_lbuild: candidate groups per tile (2: 32 lanes each, 4: 16 lanes each)
+#endif
 #ifndef GCS_XCD_REMAP
 #define GCS_XCD_REMAP 1  // 1: the list kernels give each XCD a contiguous range of tiles (see xcd_block)
 #endif
@@ -2752,7 +2755,7 @@ __global__ __launch_bounds__(64 * kListWaves) void k_lbuild(DevCtx* __restrict__
         const int self = a.sidx[sl];
         float fx = 0.f, fy = 0.f, fz = 0.f, acc = 0.f;
         int cnt = 0;
-        pair_forces_sub<kModeList, 2, LE>(ctx, a, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
+        pair_forces_sub<kModeList, GCS_LBUILD_GROUPS, LE>(ctx, a, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
                                       s_rowJ[wave], s_cand[wave], nullptr, ntot, wave, kListWaves, self, valid, &cnt);
         s_ovf[wave][lane] = cnt > a.list_cap ? 1 : 0;
         __syncthreads();

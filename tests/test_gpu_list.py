@@ -202,3 +202,56 @@ def test_list_two_waves_per_tile(c1_design):
     e, o = _pair(c1_design, cfg, ctx=LATE, list_waves=2)
     _run_both(e, o, 40, LATE["step"], cfg, 7)
     assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X
+
+
+def _c2_observables(s, design):
+    x = s.get_positions()
+    b = np.concatenate([np.linalg.norm(x[a + 1:t] - x[a:t - 1], axis=1) for _, a, t in design.chains])
+    rg = float(np.sqrt(((x - x.mean(axis=0)) ** 2).sum(axis=1).mean()))
+    en, _ = s.compute_energy()
+    return np.array([b.mean(), rg, en / design.n] + list(s.get_context()["wall_semiaxes"]))
+
+
+def test_c2_long_horizon_list_vs_rebuild_step():
+    """Long horizon at C2 from the bench state (step 300,000): 20,000 steps per trajectory, 6 seeds, through the list
+    step (lists + skin + exact fallback; ~2,500 rebuilds in all) and through the rebuild step (a fresh cell list every
+    step, no lists): the time-averaged <|r_i,i+1|>, Rg, E/N and wall semiaxes (samples every 2,000 steps after 4,000)
+    agree within 3.5 standard errors of the difference of the seed means, every state stays finite, and the list
+    step's fallbacks stay rare (< 1e-3 of particle-steps). The two paths share no neighbour machinery, so a list
+    that missed partners over long runs would show here."""
+    from pathlib import Path
+    z = np.load(Path(__file__).resolve().parents[1] / "benchdata" / "c2_interphase_step300000.npz")
+    ctx = {"step": int(z["step"]), "time": float(z["time"]), "core_scale": float(z["core_scale"]),
+           "bond_scale": float(z["bond_scale"]), "wall_semiaxes": [float(v) for v in z["wall_semiaxes"]]}
+    design, cfg = synthetic.make_c2(), InterphaseConfig()
+    nseed, steps, every, skip = 6, 20000, 2000, 4000
+    res = {3: [], 2: []}
+    for fused in res:
+        for k in range(nseed):
+            s, _ = interphase.build_interphase(Engine, design, cfg)
+            s.set_schedule(**interphase.interphase_schedule(cfg))
+            s.set_option(A.OPT_FUSED_STEP, fused)
+            s.set_positions(z["positions"])
+            s.set_context(ctx)
+            samples, done = [], 0
+            while done < steps:
+                s.run(every, first_step=ctx["step"] + done, temperature=cfg.temperature, timestep=cfg.timestep,
+                      seed=7000 + 10 * k + fused)
+                done += every
+                if done > skip:
+                    samples.append(_c2_observables(s, design))
+            assert np.isfinite(s.get_positions()).all()
+            if fused == 3:
+                st = s.list_stats()
+                assert st["active"] == 1
+                assert st["fallback_particle_steps"] < 1e-3 * design.n * steps, st
+            res[fused].append(np.mean(samples, axis=0))
+            s.close()
+    m3, m2 = np.mean(res[3], axis=0), np.mean(res[2], axis=0)
+    s3 = np.std(res[3], axis=0, ddof=1) / np.sqrt(nseed)
+    s2 = np.std(res[2], axis=0, ddof=1) / np.sqrt(nseed)
+    zs = np.abs(m3 - m2) / np.sqrt(s3 ** 2 + s2 ** 2 + 1e-30)
+    names = ["bond", "rg", "energy_per_bead", "wall_x", "wall_y", "wall_z"]
+    print({n: (float(a), float(b), float(c)) for n, a, b, c in zip(names, m3, m2, zs)})
+    assert (zs <= 3.5).all(), dict(zip(names, zs.tolist()))
+    assert (s3[:3] > 0).all() and (s2[:3] > 0).all()
