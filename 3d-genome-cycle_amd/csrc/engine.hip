@@ -2394,6 +2394,7 @@ int gcs_engine_get_list_stats(gcs_engine* e, gcs_list_stats* out)
     out->max_displacement = d.ldisp;
     out->pair_classes = e->ntypes;
     out->capacity = e->list_cap;
+    out->sync_stalls = (int64_t)d.scan_stall;
     return GCS_OK;
 }
 

@@ -105,7 +105,8 @@ class Profile(C.Structure):
 
 class ListStats(C.Structure):
     _fields_ = [("active", _i32), ("rebuild_every", _i32), ("builds", _i64), ("fallback_particle_steps", _i64),
-                ("skin", _d), ("max_displacement", _d), ("pair_classes", _i32), ("capacity", _i32)]
+                ("skin", _d), ("max_displacement", _d), ("pair_classes", _i32), ("capacity", _i32),
+                ("sync_stalls", _i64)]
 
 
 # name -> (restype, argtypes); the exported surface of include/gcs.h

@@ -365,6 +365,7 @@ typedef struct gcs_list_stats {
     double max_displacement;          /* largest displacement of a particle since the last build */
     int32_t pair_classes;             /* distinct (a, b) pair-factor classes */
     int32_t capacity;                 /* list entries per particle */
+    int64_t sync_stalls;              /* multi-block cell-scan look-backs that gave up waiting; must stay 0 */
 } gcs_list_stats;
 int gcs_engine_get_list_stats(gcs_engine* e, gcs_list_stats* out);
 

@@ -245,6 +245,7 @@ def test_c2_long_horizon_list_vs_rebuild_step():
                 st = s.list_stats()
                 assert st["active"] == 1
                 assert st["fallback_particle_steps"] < 1e-3 * design.n * steps, st
+                assert st["sync_stalls"] == 0, st
             res[fused].append(np.mean(samples, axis=0))
             s.close()
     m3, m2 = np.mean(res[3], axis=0), np.mean(res[2], axis=0)
