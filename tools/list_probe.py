@@ -19,16 +19,17 @@ from gcs import synthetic  # noqa: E402
 from gcs.config import InterphaseConfig  # noqa: E402
 
 opts = dict(a.split("=") for a in sys.argv[1:])
-cfg = InterphaseConfig()
-start = int(opts.pop("start", 0))  # 1: the production start window (synthetic C2, step 0, core_scale 0.5)
+name = opts.pop("config", "c2")  # c5: C5 from its synthetic start (the bench's C5 window)
+cfg = bench.bench_config(name)
+start = int(opts.pop("start", 0)) or name != "c2"  # 1: the production start window (step 0, core_scale 0.5)
 st = None if start else bench.load_state()
 w0 = 0 if start else bench.WINDOW_START
-e = bench.make_engine(synthetic.make_c2(), cfg, 0, w0, st)
+e = bench.make_engine(bench.design_maker(name)(), cfg, 0, w0, st)
 e.set_option(A.OPT_FUSED_STEP, int(opts.pop("fused", 3)))
 for k, v in opts.items():
     e.set_option(getattr(A, "OPT_" + k.upper()), int(v))
-e.run(200, first_step=w0, seed=5)
-p = e.profile(40, first_step=w0 + 200, seed=5)
+e.run(200, first_step=w0, seed=5, timestep=cfg.timestep)
+p = e.profile(40, first_step=w0 + 200, seed=5, timestep=cfg.timestep)
 print({k: (round(v * 1e3, 2) if k.endswith("_ms") else v) for k, v in p.items()}, "(us)")
 print(e.list_stats())
 n = e.n
