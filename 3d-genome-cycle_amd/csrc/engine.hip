@@ -205,7 +205,7 @@ struct gcs_engine {
     float2* type_ab = nullptr;
     int ntypes = 0;
     bool list_ok = false;       // the system admits the list step (a pair field, <= 256 classes, N < 2^24)
-    int list_cap = 512;         // GCS_OPT_LIST_CAP: list entries per particle (split over the tile's waves)
+    int list_cap = 1024;        // GCS_OPT_LIST_CAP: list entries per particle (split over the tile's waves)
     size_t list_alloc = 0;      // allocated entries
     int list_skin_pm = 400;     // GCS_OPT_LIST_SKIN: skin in 1/1000 of the pair cutoff
     int list_every_opt = 0;     // GCS_OPT_LIST_EVERY: rebuild period in steps (0: from the noise amplitude)

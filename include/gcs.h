@@ -349,7 +349,7 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
 #define GCS_OPT_CONTACT_BITS 9   /* contact map: 2^bits hash slots (0 = default, >= 2 N slots sized at first update) */
 #define GCS_OPT_LIST_SKIN 10      /* list step: skin in 1/1000 of the pair cutoff (default 400) */
 #define GCS_OPT_LIST_EVERY 11     /* list step: rebuild period in steps (0 = default: from the noise amplitude) */
-#define GCS_OPT_LIST_CAP 12       /* list step: list entries per particle (default 512; a longer list: exact search) */
+#define GCS_OPT_LIST_CAP 12       /* list step: list entries per particle (default 1024; a longer list: exact search) */
 #define GCS_OPT_LIST_WAVES 13     /* list step: waves per 64-particle tile, 4 (default: lowest step latency) or 2 (more
                                      tiles resident: the better throughput when several trajectories share a GPU) */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
