@@ -2229,6 +2229,14 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     unsigned long long* dbg = nullptr;
     const size_t dbg_n = (size_t)step_grid(e) * 8 + 2 * (size_t)rebuild_blocks(e->ncell_max);
     if (dbg_path) HIPCHK(hipMalloc(&dbg, dbg_n * sizeof(unsigned long long)));
+    // GCS_DEBUG_BUILD=<file>: k_lbuild's per-workgroup stamps of the last list build in the profiled steps
+    const char* dbgb_path = std::getenv("GCS_DEBUG_BUILD");
+    unsigned long long* dbgb = nullptr;
+    const size_t dbgb_n = (size_t)force_grid(e->n) * 8;
+    if (dbgb_path) {
+        HIPCHK(hipMalloc(&dbgb, dbgb_n * sizeof(unsigned long long)));
+        HIPCHK(hipMemsetAsync(dbgb, 0, dbgb_n * sizeof(unsigned long long), e->stream));
+    }
     for (auto& x : ev) HIPCHK(hipEventCreate(&x));
     const int fb = step_grid(e);
     HIPCHK(hipEventRecord(ev[0], e->stream));
@@ -2242,8 +2250,9 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
         if (lst) {
             const bool build = e->l_need_build || ((first_step + k) % e->list_every) == 0;
             e->l_need_build = false;
-            const ForceArgs la = list_args(e);
+            ForceArgs la = list_args(e);
             if (build) {
+                la.dbg_build = dbgb;
                 launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], e->n, e->cell_of, e->slot, e->count);
                 enqueue_scan(e, false);
                 launch_cell_scatter(e->stream, e->n, e->cell_of, e->slot, e->cstart, e->tmp, e->count);
@@ -2251,6 +2260,7 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
                                  e->sidx, e->scell, e->spos, e->sb, e->fa.pair_mix, e->ptype, e->psort[0], e->psort[1], e->skmu,
                          e->sbrow, e->fa.has_bonds ? e->boff : nullptr);
                 launch_list_build(e->stream, e->ctx, la);
+                la.dbg_build = nullptr;
             }
             HIPCHK(hipEventRecord(ev[2 + 5 * k], e->stream));
             ForceArgs lk = la;
@@ -2310,6 +2320,15 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
         HIPCHK(hipMemcpy(h.data(), dbg, dbg_n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         (void)hipFree(dbg);
         if (FILE* f = std::fopen(dbg_path, "wb")) {
+            std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+            std::fclose(f);
+        }
+    }
+    if (dbgb) {
+        std::vector<unsigned long long> h(dbgb_n);
+        HIPCHK(hipMemcpy(h.data(), dbgb, dbgb_n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        (void)hipFree(dbgb);
+        if (FILE* f = std::fopen(dbgb_path, "wb")) {
             std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
             std::fclose(f);
         }

@@ -171,6 +171,8 @@ struct ForceArgs {
     int split_cap;  // tiles that may be split (pbuf / tcnt capacity)
     float4* pbuf;   // [2 * split_cap][kTile] partial forces of split units
     int* tcnt;      // [split_cap] arrival counters of split tiles (0 between launches)
+    unsigned long long* dbg_build;  // optional (GCS_DEBUG_BUILD): k_lbuild per workgroup {start, tile end, wave 0..3
+                                    // sweep end, candidates, tile} of the first tile
     unsigned long long* dbg_times;  // optional (GCS_DEBUG_TIMES): per block {start, end, smid/candidates, tile} then 4 phase stamps
     // rebuild step: the force kernel files each new position's sorted record under its cell: bucket_p / bucket_q
     // [c][slot] = {x, y, z, a factor} / {particle, b factor bits} for slot < kBucketCap, the rest on the overflow

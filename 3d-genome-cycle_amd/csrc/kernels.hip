@@ -2741,6 +2741,9 @@ __global__ __launch_bounds__(64 * kListWaves) void k_lbuild(DevCtx* __restrict__
         ctx->nactive = 0;  // the list step's tail reads every workgroup's partial row
     }
     int ntot = 0;
+    unsigned long long* const dbg = a.dbg_build ? a.dbg_build + 8 * blockIdx.x : nullptr;
+    if (dbg && threadIdx.x == 0) dbg[0] = wall_clock64();
+    bool first = true;
     // the launch has force_grid(n) workgroups, the cell rows need ntiles (device-side): remap over the ones in use
     const int gused = min((int)gridDim.x, ntiles);
     for (int tile = (int)blockIdx.x < gused ? xcd_block(blockIdx.x, gused) : ntiles; tile < ntiles;
@@ -2757,6 +2760,7 @@ __global__ __launch_bounds__(64 * kListWaves) void k_lbuild(DevCtx* __restrict__
         int cnt = 0;
         pair_forces_sub<kModeList, GCS_LBUILD_GROUPS, LE>(ctx, a, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
                                       s_rowJ[wave], s_cand[wave], nullptr, ntot, wave, kListWaves, self, valid, &cnt);
+        if (dbg && first && lane == 0) dbg[2 + wave] = wall_clock64();
         s_ovf[wave][lane] = cnt > a.list_cap ? 1 : 0;
         __syncthreads();
         int ovf = 0;
@@ -2764,6 +2768,12 @@ __global__ __launch_bounds__(64 * kListWaves) void k_lbuild(DevCtx* __restrict__
         for (int w = 0; w < kListWaves; ++w) ovf |= s_ovf[w][lane];
         if (valid) a.lcount[(size_t)wave * a.list_stride + s] = min(cnt, a.list_cap) | (ovf ? kListOverflow : 0);
         __syncthreads();
+        if (dbg && first && threadIdx.x == 0) {
+            dbg[1] = wall_clock64();
+            dbg[6] = (unsigned long long)ntot;
+            dbg[7] = (unsigned long long)tile;
+        }
+        first = false;
     }
 }
 
