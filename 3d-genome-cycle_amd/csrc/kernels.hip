@@ -2721,9 +2721,12 @@ __device__ __forceinline__ int xcd_block(int b, int G)
 #endif
 }
 
+#ifndef GCS_LBUILD_WAVES_PER_EU
+#define GCS_LBUILD_WAVES_PER_EU 8  // k_lbuild occupancy target: 8 -> <= 64 VGPRs (65 without it: 7 waves/SIMD)
+#endif
 // LE: list entry type (unsigned short when every slot index fits 16 bits: half the list traffic)
 template <typename LE, int kListWaves>
-__global__ __launch_bounds__(64 * kListWaves) void k_lbuild(DevCtx* __restrict__ ctx, ForceArgs a)
+__global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu(GCS_LBUILD_WAVES_PER_EU))) void k_lbuild(DevCtx* __restrict__ ctx, ForceArgs a)
 {
     __shared__ int s_rowV[kListWaves][4 * 17];
     __shared__ int s_rowJ[kListWaves][4 * 16];
