@@ -1709,6 +1709,9 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
 #ifndef GCS_P1_PLAIN
 #define GCS_P1_PLAIN 0  // 1: phase-1 hit bits from plain C (compiler-scheduled) instead of the cmp+addc asm pair
 #endif
+#ifndef GCS_LBUILD_PK
+#define GCS_LBUILD_PK 1  // kModeList (k_lbuild): phase 1 on candidate pairs with packed fp32 math (see below)
+#endif
 #ifndef GCS_P2_UNROLL
 #define GCS_P2_UNROLL 4  // sub-tile phase 2: hits popped per lane per round (rounds = wave max of hits / this)
 #endif
@@ -1838,6 +1841,18 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
             const int i = gl + GL * f;
             const bool real = nj[f] >= 0;
             const float px = real ? np[f].x - ox : far, py = real ? np[f].y - oy : far, pz = real ? np[f].z - oz : far;
+            if constexpr (MODE == kModeList && GCS_LBUILD_PK) {
+                // pair layout: candidates 2h, 2h+1 in float4s 2h {x, x', y, y'} and 2h+1 {z, z', w, w'}; slots at
+                // float 8 * kSub / 2 (the list build's phase 2 needs only the partner's slot)
+                float* const P = reinterpret_cast<float*>(my_cand);
+                const int h8 = 8 * (i >> 1) + (i & 1);
+                P[h8] = -2.f * px;
+                P[h8 + 2] = -2.f * py;
+                P[h8 + 4] = -2.f * pz;
+                P[h8 + 6] = fmaf(pz, pz, fmaf(py, py, px * px));
+                reinterpret_cast<int*>(my_cand)[4 * kSub + i] = real ? nj[f] : -1;
+                continue;
+            }
             my_cand[2 * i] = make_float4(-2.f * px, -2.f * py, -2.f * pz, fmaf(pz, pz, fmaf(py, py, px * px)));
             my_cand[2 * i + 1] = make_float4(real ? kA * np[f].w : 0.f, real ? kB * nb[f] : 0.f,
                                              MODE == kModeList ? __int_as_float(real ? nj[f] : -1) : 0.f, 0.f);
@@ -1848,6 +1863,32 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
 
         // phase 1: 32 candidates of my group -> one 32-bit hit mask (byte trick: candidate k on bit k ^ 7)
         unsigned m = 0u;
+        if constexpr (MODE == kModeList && GCS_LBUILD_PK) {
+            // the same fma chain per candidate, two candidates per packed instruction (v_pk_fma_f32); hit = sign of
+            // tv - thr (tv < thr exactly: a difference of unequal finite floats is never +0), shifted in by
+            // v_alignbit: 3 VALU per candidate instead of 5, the same bits in the same places
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            const f2 X = {xi, xi}, Y = {yi, yi}, Z = {zi, zi}, T = {thr, thr};
+#pragma unroll
+            for (int k0 = 0; k0 < kSub; k0 += 8) {
+                f2 tv[4];
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    const float4 A = my_cand[k0 + 2 * h], B = my_cand[k0 + 2 * h + 1];
+                    const f2 qx = {A.x, A.y}, qy = {A.z, A.w}, qz = {B.x, B.y}, qw = {B.z, B.w};
+                    tv[h] = __builtin_elementwise_fma(qx, X, __builtin_elementwise_fma(qy, Y,
+                                                      __builtin_elementwise_fma(qz, Z, qw)));
+                }
+                unsigned byte = 0u;
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    const f2 d = tv[h] - T;
+                    byte = __builtin_amdgcn_alignbit(byte, __float_as_uint(d.x), 31u);
+                    byte = __builtin_amdgcn_alignbit(byte, __float_as_uint(d.y), 31u);
+                }
+                m |= byte << k0;
+            }
+        } else
 #pragma unroll
         for (int k0 = 0; k0 < kSub; k0 += 8) {
             unsigned byte = 0u;
@@ -1889,7 +1930,8 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 const unsigned k = min(b ^ 7u, (unsigned)kSub);
                 m &= m - 1u;
                 if (k < (unsigned)kSub && lvalid) {
-                    const int e = __float_as_int(my_cand[2 * k + 1].z);  // the partner's sorted slot
+                    const int e = GCS_LBUILD_PK ? reinterpret_cast<const int*>(my_cand)[4 * kSub + k]
+                                                : __float_as_int(my_cand[2 * k + 1].z);  // the partner's sorted slot
                     if (e != s) {
                         if (*lcnt < a.list_cap) seg[(size_t)(*lcnt) * a.list_stride] = (LE)e;
                         *lcnt += 1;
