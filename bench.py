@@ -413,6 +413,9 @@ def replica_main(args):
                            (A.OPT_SUBTILES, args.subtiles), (A.OPT_SCAN_BLOCKS, args.scan_mb),
                            (A.OPT_LIST_WAVES, list_waves)):
                 e.set_option(opt, v)
+            for kv in args.engine_opt:  # experiments: --engine-opt list_skin=300 (gcs._abi OPT_<NAME>)
+                name, v = kv.split("=")
+                e.set_option(getattr(A, "OPT_" + name.upper()), int(v))
             if args.cu_split and R > 1:
                 # replica k on CUs c with (c mod R) == k ("interleave") or a contiguous R-th of them ("block")
                 ncu = args.cu_count
@@ -604,6 +607,8 @@ def parse_args(argv=None):
     ap.add_argument("--cu-split", default="", choices=["", "interleave", "block"],
                     help="several replicas per GPU: give each its own share of the compute units")
     ap.add_argument("--cu-count", type=int, default=256)
+    ap.add_argument("--engine-opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="extra engine option (gcs._abi OPT_<NAME>), repeatable; for experiments")
     ap.add_argument("--list-waves", type=int, default=0,
                     help="list step waves per tile: 2 or 4 (0: 2 with several replicas per GPU, else 4)")
     ap.add_argument("--fused", type=int, default=3,
