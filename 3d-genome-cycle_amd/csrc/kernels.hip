@@ -1876,13 +1876,24 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 for (int h = 0; h < 4; ++h) {
                     const float4 A = my_cand[k0 + 2 * h], B = my_cand[k0 + 2 * h + 1];
                     const f2 qx = {A.x, A.y}, qy = {A.z, A.w}, qz = {B.x, B.y}, qw = {B.z, B.w};
+#if GCS_LBUILD_PK == 2  // scalar chains (same bits)
+                    tv[h].x = fmaf(qx.x, xi, fmaf(qy.x, yi, fmaf(qz.x, zi, qw.x)));
+                    tv[h].y = fmaf(qx.y, xi, fmaf(qy.y, yi, fmaf(qz.y, zi, qw.y)));
+#else
                     tv[h] = __builtin_elementwise_fma(qx, X, __builtin_elementwise_fma(qy, Y,
                                                       __builtin_elementwise_fma(qz, Z, qw)));
+#endif
                 }
                 unsigned byte = 0u;
 #pragma unroll
                 for (int h = 0; h < 4; ++h) {
+#if GCS_LBUILD_PK == 2
+                    f2 d;
+                    d.x = tv[h].x - thr;
+                    d.y = tv[h].y - thr;
+#else
                     const f2 d = tv[h] - T;
+#endif
                     byte = __builtin_amdgcn_alignbit(byte, __float_as_uint(d.x), 31u);
                     byte = __builtin_amdgcn_alignbit(byte, __float_as_uint(d.y), 31u);
                 }

@@ -1,0 +1,12 @@
+#!/bin/bash
+# tools/profile.sh for R = 1 and R = 4, summarised on the box (raw rocprofv3 output exceeds what gpurun copies back)
+set -u
+tag=${1:?tag}
+for R in 1 4; do
+  t=$tag; [ $R -gt 1 ] && t=${tag}_r$R
+  REPLICAS=$R bash tools/profile.sh $t || exit 1
+  d=gpurun_out/prof_$t
+  python tools/summarize_pmc.py $d --traffic-out gpurun_out/${t}_lstep_traffic.json --kernel k_lstep > gpurun_out/${t}_pmc_summary.json || exit 1
+  cp "$(find $d/trace -name '*kernel_stats.csv' | head -n 1)" gpurun_out/${t}_kernel_stats.csv || exit 1
+  rm -rf $d
+done
