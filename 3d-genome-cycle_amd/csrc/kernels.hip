@@ -1707,7 +1707,8 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
 #define GCS_ROW_CURSOR 0  // 1: incremental stencil-row cursor in the sub-tile candidate fetch
 #endif
 #ifndef GCS_P1_PLAIN
-#define GCS_P1_PLAIN 0  // 1: phase-1 hit bits from plain C (compiler-scheduled) instead of the cmp+addc asm pair
+#define GCS_P1_PLAIN 0  // 1: phase-1 hit bits from plain C (compiler-scheduled) instead of the cmp+addc asm pair,
+                        // 2: sub + v_alignbit (the list build's form)
 #endif
 #ifndef GCS_LBUILD_PK
 #define GCS_LBUILD_PK 1  // kModeList (k_lbuild): phase 1 on candidate pairs with packed fp32 math (see below)
@@ -1917,7 +1918,10 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                     const bool in = (tv[u] < thr) && (s_candj[grp * kSub + k0 + u] != s);
                     byte = 2u * byte + (in ? 1u : 0u);
                 } else {
-#if GCS_P1_PLAIN
+#if GCS_P1_PLAIN == 2
+                    // the sign of tv - thr shifted in (tv < thr exactly; see the list build's phase 1)
+                    byte = __builtin_amdgcn_alignbit(byte, __float_as_uint(tv[u] - thr), 31u);
+#elif GCS_P1_PLAIN
                     byte = 2u * byte + (tv[u] < thr ? 1u : 0u);
 #else
                     asm("v_cmp_gt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
@@ -1997,10 +2001,15 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
 // atomic per run of equal cells), so the next step's cell list needs only scan + scatter + sort (engine.hip
 // enqueue_step).
 #ifndef GCS_FORCE_WAVES_PER_EU
-#define GCS_FORCE_WAVES_PER_EU 5  // occupancy target of the force kernel (VGPR cap 512 / 5 -> 96)
+#define GCS_FORCE_WAVES_PER_EU 5  // occupancy target of the fused force kernel (VGPR cap 512 / 5 -> 96)
+#endif
+#ifndef GCS_FORCE_WAVES_PER_EU_UNFUSED
+// the unfused instantiations (the decomposed path's step, force/energy evaluations) at 4 -> 128 VGPRs, no spills:
+// C5 decomposed (1 domain) 1.85e9 -> 1.98e9, while the fused rebuild step loses 12 % at 4 (same box, tools/force_variants.sh)
+#define GCS_FORCE_WAVES_PER_EU_UNFUSED 4
 #endif
 template <int MODE, int WAVES, bool FUSED, int NG>
-__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(GCS_FORCE_WAVES_PER_EU))) void k_force(DevCtx* __restrict__ ctx, ForceArgs a)
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(FUSED ? GCS_FORCE_WAVES_PER_EU : GCS_FORCE_WAVES_PER_EU_UNFUSED))) void k_force(DevCtx* __restrict__ ctx, ForceArgs a)
 {
     __shared__ float red[WAVES > 1 ? WAVES : 1][4][64];
     // per-wave pair-loop staging, sized for the larger of the two layouts: one 64-candidate stream (pair_forces) or
