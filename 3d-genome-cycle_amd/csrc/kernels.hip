@@ -2862,6 +2862,38 @@ __device__ __forceinline__ void list_pair(float xi, float yi, float zi, float4 q
     nbr += in ? 1.f : 0.f;
 }
 
+#ifndef GCS_LIST_PK
+#define GCS_LIST_PK 0  // 1: the pair loop evaluates entries two at a time in packed fp32 (list_pair2; same bits)
+#endif
+// list_pair for two entries: each component follows list_pair's operations in its order (v_pk_* per pair of
+// entries), and the forces are accumulated entry 0 then entry 1 as two list_pair calls would
+__device__ __forceinline__ void list_pair2(float xi, float yi, float zi, float4 q0, float4 q1, float2 t0, float2 t1,
+                                           float ahi, float bhi, float kA, float kB, float k2a, float k2b, float rc2,
+                                           bool real0, bool real1, float& fx, float& fy, float& fz, float& nbr)
+{
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 dx = f2{xi, xi} - f2{q0.x, q1.x}, dy = f2{yi, yi} - f2{q0.y, q1.y}, dz = f2{zi, zi} - f2{q0.z, q1.z};
+    const f2 r2 = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+    const f2 one = {1.f, 1.f}, zero = {0.f, 0.f};
+    const f2 ga = __builtin_elementwise_max(__builtin_elementwise_fma(f2{-k2a, -k2a}, r2, one), zero);
+    const f2 tt = r2 * f2{k2b, k2b};
+    const f2 t2 = tt * tt;
+    const f2 gb = __builtin_elementwise_max(__builtin_elementwise_fma(-t2, t2, one), zero);
+    const f2 A = __builtin_elementwise_fma(f2{kA, kA}, f2{t0.x, t1.x}, f2{ahi, ahi});
+    const f2 B = __builtin_elementwise_fma(f2{kB, kB}, f2{t0.y, t1.y}, f2{bhi, bhi});
+    const f2 c = __builtin_elementwise_fma(A, ga * ga, B * (gb * gb * t2 * tt));
+    const bool in0 = real0 && r2.x < rc2, in1 = real1 && r2.y < rc2;
+    const float c0 = in0 ? c.x : 0.f, c1 = in1 ? c.y : 0.f;
+    fx = fmaf(c0, dx.x, fx);
+    fy = fmaf(c0, dy.x, fy);
+    fz = fmaf(c0, dz.x, fz);
+    nbr += in0 ? 1.f : 0.f;
+    fx = fmaf(c1, dx.y, fx);
+    fy = fmaf(c1, dy.y, fy);
+    fz = fmaf(c1, dz.y, fz);
+    nbr += in1 ? 1.f : 0.f;
+}
+
 __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 {
     const float q = (v - g.lo[k]) * g.inv[k];
@@ -3016,10 +3048,20 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
                 float4 q[kU];
 #pragma unroll
                 for (int u = 0; u < kU; ++u) q[u] = qc[(k0 + u < cnt) ? e[u] : sl];
+#if GCS_LIST_PK
+                static_assert(kU % 2 == 0, "pairs of entries");
+#pragma unroll
+                for (int u = 0; u < kU; u += 2)
+                    list_pair2(pi.x, pi.y, pi.z, q[u], q[u + 1],
+                               s_tab[(unsigned)__float_as_int(q[u].w) >> kListIndexBits],
+                               s_tab[(unsigned)__float_as_int(q[u + 1].w) >> kListIndexBits], ahi, bhi, kA, kB, k2a,
+                               k2b, rc2, k0 + u < cnt, k0 + u + 1 < cnt, fx, fy, fz, nbr);
+#else
 #pragma unroll
                 for (int u = 0; u < kU; ++u)
                     list_pair(pi.x, pi.y, pi.z, q[u], s_tab[(unsigned)__float_as_int(q[u].w) >> kListIndexBits], ahi,
                               bhi, kA, kB, k2a, k2b, rc2, k0 + u < cnt, fx, fy, fz, nbr);
+#endif
                 if constexpr (CT) {
 #pragma unroll
                     for (int u = 0; u < kU; ++u)
