@@ -1713,6 +1713,9 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
 #ifndef GCS_LBUILD_PK
 #define GCS_LBUILD_PK 1  // kModeList (k_lbuild): phase 1 on candidate pairs with packed fp32 math (see below)
 #endif
+#ifndef GCS_LBUILD_P2U
+#define GCS_LBUILD_P2U 1  // list build phase 2: hits per round (> 1: the rounds' slot reads issued together)
+#endif
 #ifndef GCS_P2_UNROLL
 #define GCS_P2_UNROLL 4  // sub-tile phase 2: hits popped per lane per round (rounds = wave max of hits / this)
 #endif
@@ -1939,6 +1942,29 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
         if constexpr (MODE == kModeList) {
             // append the hits: one column-major store per hit (lanes of a wave write consecutive slots of a row)
             LE* const seg = reinterpret_cast<LE*>(a.list) + (size_t)wv * a.list_cap * a.list_stride + s;
+#if GCS_LBUILD_PK && GCS_LBUILD_P2U > 1
+            // GCS_LBUILD_P2U hits per round: their slot reads are issued together, the appends follow in hit order
+            for (int t = 0; t < mh; t += GCS_LBUILD_P2U) {
+                unsigned kk[GCS_LBUILD_P2U];
+                int ee[GCS_LBUILD_P2U];
+#pragma unroll
+                for (int u = 0; u < GCS_LBUILD_P2U; ++u) {
+                    unsigned b;
+                    asm("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(m));
+                    kk[u] = min(b ^ 7u, (unsigned)kSub);
+                    m &= m - 1u;
+                    ee[u] = reinterpret_cast<const int*>(my_cand)[4 * kSub + min(kk[u], (unsigned)kSub - 1u)];
+                }
+#pragma unroll
+                for (int u = 0; u < GCS_LBUILD_P2U; ++u) {
+                    if (kk[u] < (unsigned)kSub && lvalid && ee[u] != s) {
+                        if (*lcnt < a.list_cap) seg[(size_t)(*lcnt) * a.list_stride] = (LE)ee[u];
+                        *lcnt += 1;
+                    }
+                }
+            }
+            if (false)
+#endif
             for (int t = 0; t < mh; ++t) {
                 unsigned b;
                 asm("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(m));
