@@ -2891,6 +2891,7 @@ __device__ __forceinline__ void list_pair(float xi, float yi, float zi, float4 q
 #ifndef GCS_LIST_PK
 #define GCS_LIST_PK 0  // 1: the pair loop evaluates entries two at a time in packed fp32 (list_pair2; same bits)
 #endif
+#if GCS_LIST_PK
 // list_pair for two entries: each component follows list_pair's operations in its order (v_pk_* per pair of
 // entries), and the forces are accumulated entry 0 then entry 1 as two list_pair calls would
 __device__ __forceinline__ void list_pair2(float xi, float yi, float zi, float4 q0, float4 q1, float2 t0, float2 t1,
@@ -2919,6 +2920,7 @@ __device__ __forceinline__ void list_pair2(float xi, float yi, float zi, float4 
     fz = fmaf(c1, dz.y, fz);
     nbr += in1 ? 1.f : 0.f;
 }
+#endif
 
 __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 {
