@@ -2931,7 +2931,10 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 
 
 template <typename LE, int kListWaves, bool CT>
-__global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu(GCS_LIST_WAVES_PER_EU))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int apply_sched)
+#ifndef GCS_LIST_WAVES_PER_EU_CT
+#define GCS_LIST_WAVES_PER_EU_CT GCS_LIST_WAVES_PER_EU  // the contact-step instantiation (CT)
+#endif
+__global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu(CT ? GCS_LIST_WAVES_PER_EU_CT : GCS_LIST_WAVES_PER_EU))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int apply_sched)
 {
     __shared__ float red[kListWaves][4][kTile];
     __shared__ float4 s_locf[kTile], s_locr[kTile], s_loco[kTile], s_noise[kTile];
