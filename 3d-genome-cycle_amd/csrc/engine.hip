@@ -57,6 +57,28 @@ struct FieldRec {
     std::vector<gcs_kinetochore_spec> specs;
 };
 
+// What a captured step sequence depends on beyond its (phase, parity, length) key: anything else that changes
+// drops every cached graph before the next capture.
+struct GraphKey {
+    int topo_version, fused, list_every, sched_flags, waves, chunk, spacestep, list_waves;
+    gcs_bd_config cfg;
+};
+bool same_key(const GraphKey& x, const GraphKey& y)
+{
+    return x.topo_version == y.topo_version && x.fused == y.fused && x.list_every == y.list_every &&
+           x.sched_flags == y.sched_flags && x.waves == y.waves && x.chunk == y.chunk && x.spacestep == y.spacestep &&
+           x.list_waves == y.list_waves && x.cfg.temperature == y.cfg.temperature &&
+           x.cfg.timestep == y.cfg.timestep && x.cfg.spacestep == y.cfg.spacestep && x.cfg.seed == y.cfg.seed &&
+           x.cfg.noise == y.cfg.noise;
+}
+struct GraphEntry {
+    int phase, parity, len;
+    hipGraph_t graph;
+    hipGraphExec_t exec;
+    unsigned long long used;
+};
+constexpr size_t kMaxGraphs = 32;  // cached step sequences per engine (least recently used evicted)
+
 template <class T>
 int dalloc(T** p, size_t count)
 {
@@ -174,6 +196,7 @@ struct gcs_engine {
     hipGraph_t dgraph = nullptr;
     int dg_steps = 0;
     gcs_bd_config dg_cfg{};
+    int dg_version = -1, dg_sched_flags = -1;
 
     ForceArgs fa{};
     gcs_schedule sched{};
@@ -185,14 +208,13 @@ struct gcs_engine {
     int waves = 4;
     int fused = 3;  // GCS_OPT_FUSED_STEP: 3 = the list step, 2 = the 2-launch rebuild step, 1 = the 4-launch step, 0 = unfused
     bool scan_mb = true;  // GCS_OPT_SCAN_BLOCKS: multi-block cell scan (the heavy-tile split keeps one block)
-    hipGraphExec_t gexec = nullptr;
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t lgexec[2] = {nullptr, nullptr};  // list step: one graph per starting parity
-    hipGraph_t lgraph[2] = {nullptr, nullptr};
-    int g_steps = 0, g_waves = 0, g_version = -1, g_spacestep = -1;
-    gcs_bd_config g_cfg{};
-    int g_sched_flags = -1;
-    int g_fused = -1, g_chunk = -1;
+    // captured step sequences, keyed by what a replay bakes in besides the launch arguments below: the list
+    // step's rebuild phase (first step mod M) and starting position-buffer parity, and the sequence length
+    std::vector<GraphEntry> graphs;
+    unsigned long long graph_clock = 0;  // LRU stamp
+    GraphKey g_key{};                     // what every cached graph was captured under (else the cache is dropped)
+    bool g_key_set = false;
+    gcs_run_stats rstats{};
 
     // list step (GCS_OPT_FUSED_STEP 3): neighbour lists, pair-factor classes, rebuild period
     int* list = nullptr;
@@ -212,8 +234,7 @@ struct gcs_engine {
     int list_every = 1;         // the period of the current run
     int list_waves = 4;         // GCS_OPT_LIST_WAVES: waves per tile (2: more tiles resident, for replica runs)
     bool l_need_build = true;   // the next list step must rebuild (run start without continuity)
-    int g_list_every = -1;
-    double c_pending = 0;       // a contact update fused into the next list step (its distance; 0: none)
+    double c_pending = 0;      // a contact update fused into the next list step (its distance; 0: none)
 
     // fused-step continuity: after a fused run the cells of the next positions are already binned with the
     // grid the next step expects, so a run that continues at chain_step skips re-priming (bitwise identical
@@ -225,18 +246,25 @@ struct gcs_engine {
 
 namespace {
 
+// the decomposed run's captured chunk (kernels + RCCL collectives): it bakes in the domain geometry, the
+// exchange buffers and the communicator, so every change of those drops it
+void drop_domain_graph(gcs_engine* e)
+{
+    if (e->dgexec) (void)hipGraphExecDestroy(e->dgexec);
+    if (e->dgraph) (void)hipGraphDestroy(e->dgraph);
+    e->dgexec = nullptr;
+    e->dgraph = nullptr;
+}
+
 void drop_graph(gcs_engine* e)
 {
-    if (e->gexec) (void)hipGraphExecDestroy(e->gexec);
-    if (e->graph) (void)hipGraphDestroy(e->graph);
-    e->gexec = nullptr;
-    e->graph = nullptr;
-    for (int p = 0; p < 2; ++p) {
-        if (e->lgexec[p]) (void)hipGraphExecDestroy(e->lgexec[p]);
-        if (e->lgraph[p]) (void)hipGraphDestroy(e->lgraph[p]);
-        e->lgexec[p] = nullptr;
-        e->lgraph[p] = nullptr;
+    for (GraphEntry& g : e->graphs) {
+        (void)hipGraphExecDestroy(g.exec);
+        (void)hipGraphDestroy(g.graph);
     }
+    e->graphs.clear();
+    e->g_key_set = false;
+    drop_domain_graph(e);
 }
 
 FieldRec* new_field(gcs_engine* e, int kind)
@@ -804,6 +832,61 @@ int begin_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
     return GCS_OK;
 }
 
+// The cached graph of `len` steps from rebuild phase `phase` and parity `parity`, captured by `body` on a miss
+// (the least recently used entry makes room).  `key` is what the run would capture under: a different key than
+// the cache's drops the whole cache first.
+template <class Body>
+int cached_graph(gcs_engine* e, const GraphKey& key, int phase, int parity, int len, Body body, hipGraphExec_t* out)
+{
+    if (!e->g_key_set || !same_key(e->g_key, key)) {
+        drop_graph(e);
+        e->g_key = key;
+        e->g_key_set = true;
+    }
+    for (GraphEntry& g : e->graphs)
+        if (g.phase == phase && g.parity == parity && g.len == len) {
+            g.used = ++e->graph_clock;
+            *out = g.exec;
+            return GCS_OK;
+        }
+    if (e->graphs.size() >= kMaxGraphs) {
+        auto lru = std::min_element(e->graphs.begin(), e->graphs.end(),
+                                    [](const GraphEntry& x, const GraphEntry& y) { return x.used < y.used; });
+        (void)hipGraphExecDestroy(lru->exec);
+        (void)hipGraphDestroy(lru->graph);
+        e->graphs.erase(lru);
+    }
+    GraphEntry g{phase, parity, len, nullptr, nullptr, ++e->graph_clock};
+    HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+    body();
+    HIPCHK(hipStreamEndCapture(e->stream, &g.graph));
+    const hipError_t he = hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0);
+    if (he != hipSuccess) {
+        (void)hipGraphDestroy(g.graph);
+        return fail(GCS_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(he));
+    }
+    e->graphs.push_back(g);
+    e->rstats.graphs_captured++;
+    *out = g.exec;
+    return GCS_OK;
+}
+
+GraphKey run_key(const gcs_engine* e, const gcs_bd_config* cfg, bool spacestep)
+{
+    GraphKey k;
+    std::memset(&k, 0, sizeof(k));
+    k.topo_version = e->topo_version;
+    k.fused = e->fused;
+    k.list_every = e->list_every;
+    k.sched_flags = e->sched_flags;
+    k.waves = e->waves;
+    k.chunk = e->fa.chunk_mode;
+    k.spacestep = spacestep ? 1 : 0;
+    k.list_waves = e->list_waves;
+    k.cfg = *cfg;
+    return k;
+}
+
 // after a run's steps were enqueued
 void end_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps)
 {
@@ -1119,8 +1202,6 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->dom_red);
     dfree(e->dom_glob);
     dfree(e->dom_flags);
-    if (e->dgexec) (void)hipGraphExecDestroy(e->dgexec);
-    if (e->dgraph) (void)hipGraphDestroy(e->dgraph);
     if (e->nccl) rccl_comm_destroy(e->nccl);
     dfree(e->dom_shared_idx);
     dfree(e->dom_shared_flag);
@@ -1438,88 +1519,60 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
     if (rc) return rc;
 
     const int G = e->graph_steps;
+    const GraphKey key = run_key(e, cfg, spacestep);
     int64_t done = 0;
     if (list_path(e, spacestep)) {
         // rebuilds at the steps k with (first_step + k) % M == 0 and at a run start without continuity, so a run
-        // split into chunks rebuilds where the whole run does (bitwise identical); graphs hold GM steps from an
-        // aligned step, the rest runs eagerly
+        // split into chunks rebuilds where the whole run does (bitwise identical).  Every stretch of up to G steps
+        // is replayed from a graph captured once per (first step mod M, starting parity, length): a run of any
+        // length, from any step, replays graphs (only the forced rebuild of a run start and a pending contact
+        // update run eagerly)
         const int M = e->list_every;
-        const int GM = G > 0 ? M * ((G + M - 1) / M) : 0;
         // the host knows every step's position-buffer parity (the kernels' slot loads then need no context read);
-        // a captured graph bakes its steps' parities in, so there is one graph per starting parity
+        // a captured graph bakes its steps' parities in
         auto par = [&](int64_t k) { return e->parity ^ (int)(k & 1); };
         while (done < steps) {
             const int64_t st = first_step + done;
-            const bool aligned = (st % M) == 0;
-            if (e->c_pending > 0) {  // the contact update the host asked for after the last step
-                enqueue_list_step(e, e->l_need_build || aligned, e->c_pending, par(done));
+            const int phase = (int)(((st % M) + M) % M);
+            if (e->c_pending > 0 || e->l_need_build || G == 0) {
+                // the contact update the host asked for after the last step, a run start's rebuild, or no graphs
+                enqueue_list_step(e, e->l_need_build || phase == 0, e->c_pending, par(done));
                 e->c_pending = 0;
                 e->l_need_build = false;
                 ++done;
+                e->rstats.eager_steps++;
                 continue;
             }
-            if (GM > 0 && !e->l_need_build && aligned && steps - done >= GM) {
-                const int p0 = par(done);
-                const bool same = e->lgexec[p0] && e->g_steps == GM && e->g_version == e->topo_version &&
-                                  e->g_fused == 3 && e->g_list_every == M && e->g_sched_flags == e->sched_flags &&
-                                  std::memcmp(&e->g_cfg, cfg, sizeof(*cfg)) == 0;
-                if (!same) {
-                    if (!(e->g_steps == GM && e->g_version == e->topo_version && e->g_fused == 3 &&
-                          e->g_list_every == M && e->g_sched_flags == e->sched_flags &&
-                          std::memcmp(&e->g_cfg, cfg, sizeof(*cfg)) == 0))
-                        drop_graph(e);  // the other parity's graph is stale too
-                    hipGraph_t g = nullptr;
-                    HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
-                    for (int k = 0; k < GM; ++k) enqueue_list_step(e, k % M == 0, 0, p0 ^ (k & 1));
-                    HIPCHK(hipStreamEndCapture(e->stream, &g));
-                    e->lgraph[p0] = g;
-                    HIPCHK(hipGraphInstantiate(&e->lgexec[p0], g, nullptr, nullptr, 0));
-                    e->g_steps = GM;
-                    e->g_version = e->topo_version;
-                    e->g_fused = 3;
-                    e->g_list_every = M;
-                    e->g_sched_flags = e->sched_flags;
-                    e->g_cfg = *cfg;
-                    e->g_spacestep = 0;
-                    e->g_waves = e->waves;
-                    e->g_chunk = e->fa.chunk_mode;
-                }
-                // GM odd: consecutive replays alternate the starting parity
-                for (; steps - done >= GM; done += GM) {
-                    const int pk = par(done);
-                    if (!e->lgexec[pk]) break;  // the other parity's graph: captured on the next pass
-                    HIPCHK(hipGraphLaunch(e->lgexec[pk], e->stream));
-                }
-                continue;
-            }
-            enqueue_list_step(e, e->l_need_build || aligned, 0, par(done));
-            e->l_need_build = false;
-            ++done;
+            const int len = (int)std::min<int64_t>(G, steps - done);
+            const int p0 = par(done);
+            hipGraphExec_t x = nullptr;
+            rc = cached_graph(e, key, phase, p0, len, [&]() {
+                for (int k = 0; k < len; ++k) enqueue_list_step(e, (phase + k) % M == 0, 0, p0 ^ (k & 1));
+            }, &x);
+            if (rc) return rc;
+            HIPCHK(hipGraphLaunch(x, e->stream));
+            e->rstats.graph_launches++;
+            e->rstats.graph_steps += len;
+            done += len;
         }
     }
-    if (G > 0 && steps - done >= G && !list_path(e, spacestep)) {
-        const bool same = e->gexec && e->g_steps == G && e->g_waves == e->waves && e->g_version == e->topo_version &&
-                          e->g_fused == (int)e->fused && e->g_chunk == e->fa.chunk_mode &&
-                          e->g_spacestep == (int)spacestep && e->g_sched_flags == e->sched_flags &&
-                          std::memcmp(&e->g_cfg, cfg, sizeof(*cfg)) == 0;
-        if (!same) {
-            drop_graph(e);
-            HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
-            for (int k = 0; k < G; ++k) enqueue_step(e, spacestep, (float)cfg->spacestep, (float)cfg->timestep);
-            HIPCHK(hipStreamEndCapture(e->stream, &e->graph));
-            HIPCHK(hipGraphInstantiate(&e->gexec, e->graph, nullptr, nullptr, 0));
-            e->g_steps = G;
-            e->g_waves = e->waves;
-            e->g_version = e->topo_version;
-            e->g_spacestep = (int)spacestep;
-            e->g_sched_flags = e->sched_flags;
-            e->g_fused = (int)e->fused;
-            e->g_chunk = e->fa.chunk_mode;
-            e->g_cfg = *cfg;
-        }
-        for (; done + G <= steps; done += G) HIPCHK(hipGraphLaunch(e->gexec, e->stream));
+    // other step shapes: every step is the same launch sequence (the context carries the parity)
+    while (G > 0 && done < steps) {
+        const int len = (int)std::min<int64_t>(G, steps - done);
+        hipGraphExec_t x = nullptr;
+        rc = cached_graph(e, key, 0, 0, len, [&]() {
+            for (int k = 0; k < len; ++k) enqueue_step(e, spacestep, (float)cfg->spacestep, (float)cfg->timestep);
+        }, &x);
+        if (rc) return rc;
+        HIPCHK(hipGraphLaunch(x, e->stream));
+        e->rstats.graph_launches++;
+        e->rstats.graph_steps += len;
+        done += len;
     }
-    for (; done < steps; ++done) enqueue_step(e, spacestep, (float)cfg->spacestep, (float)cfg->timestep);
+    for (; done < steps; ++done) {
+        enqueue_step(e, spacestep, (float)cfg->spacestep, (float)cfg->timestep);
+        e->rstats.eager_steps++;
+    }
     HIPCHK(hipGetLastError());
     end_run(e, cfg, first_step, steps);
     if (steps & 1) e->parity ^= 1;
@@ -1683,7 +1736,8 @@ int gcs_engine_contacts_update(gcs_engine* e, double distance)
 int gcs_engine_contacts_clear(gcs_engine* e)
 {
     if (!e) return fail(GCS_EINVAL, "null argument");
-    if (e->c_pending > 0) e->c_pending = 0;  // cleared before it was counted: the update is superseded? no --
+    // a pending (deferred) update followed by a clear leaves an empty table: dropping it equals counting it first
+    e->c_pending = 0;
     e->c_updates = 0;
     if (!e->c_keys) return GCS_OK;
     HIPCHK(hipSetDevice(e->device));
@@ -1802,6 +1856,7 @@ int gcs_engine_set_domain(gcs_engine* e, double lo, double hi, double halo, cons
     for (int p = 0; p < npeer; ++p) h[p] = make_float2((float)peer_regions[2 * p], (float)peer_regions[2 * p + 1]);
     HIPCHK(hipMemcpyAsync(e->dom_regions, h, sizeof(h), hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
+    drop_domain_graph(e);  // the captured chunk holds the slab bounds and the peer count by value
     e->dom = true;
     e->dom_lo = (float)std::max(lo, -3.0e38);
     e->dom_hi = (float)std::min(hi, 3.0e38);
@@ -1821,6 +1876,17 @@ int gcs_engine_set_domain_shared(gcs_engine* e, const int64_t* idx, int32_t coun
         if (!valid_index(e, idx[k])) return fail(GCS_EINVAL, "shared particle index out of range");
         h[k] = (int)idx[k];
         flag[h[k]] = 1;
+    }
+    drop_domain_graph(e);
+    if (e->dom_red && kDomainRed + 3 * count != e->dom_nred) {
+        // the allreduce buffer holds the shared positions: its size changes, so the exchange buffers must be
+        // set up again (gcs_engine_domain_buffers) before the next decomposed run
+        dfree(e->dom_send);
+        dfree(e->dom_recv);
+        dfree(e->dom_red);
+        dfree(e->dom_glob);
+        e->dom_nred = 0;
+        e->dom_cap = 0;
     }
     dfree(e->dom_shared_idx);
     dfree(e->dom_shared_flag);
@@ -1953,10 +2019,7 @@ int gcs_engine_domain_buffers(gcs_engine* e, int32_t cap, int32_t* nred)
     e->dom_cap = cap;
     e->dom_nred = nr;
     if (nred) *nred = nr;
-    if (e->dgexec) (void)hipGraphExecDestroy(e->dgexec);
-    if (e->dgraph) (void)hipGraphDestroy(e->dgraph);
-    e->dgexec = nullptr;
-    e->dgraph = nullptr;
+    drop_domain_graph(e);
     return GCS_OK;
 }
 
@@ -2044,6 +2107,7 @@ int gcs_engine_domain_rccl(gcs_engine* e, const uint8_t* id, int32_t nranks, int
         e->dom_peer_rank[p] = peer_ranks[p];
     }
     HIPCHK(hipSetDevice(e->device));
+    drop_domain_graph(e);  // its collectives name the old communicator
     if (e->nccl) {
         (void)r->commDestroy(e->nccl);
         e->nccl = nullptr;
@@ -2059,6 +2123,7 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
 {
     if (!e || !cfg) return fail(GCS_EINVAL, "null argument");
     if (!e->nccl) return fail(GCS_ESTATE, "gcs_engine_domain_rccl first");
+    if (!e->dom_red || !e->dom_send) return fail(GCS_ESTATE, "gcs_engine_domain_buffers first");
     if (steps < 0) return fail(GCS_EINVAL, "negative step count");
     int64_t k = 0, k0 = 0;
     int rc;
@@ -2086,12 +2151,11 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
     // the rest: G-step chunks captured once into a graph (kernels and collectives), the remainder eagerly
     const int G = e->graph_steps;
     if (G > 0 && steps - k >= G) {
-        const bool same = e->dgexec && e->dg_steps == G && std::memcmp(&e->dg_cfg, cfg, sizeof(*cfg)) == 0;
+        // (geometry, buffers, communicator and options drop the graph when they change: drop_domain_graph)
+        const bool same = e->dgexec && e->dg_steps == G && std::memcmp(&e->dg_cfg, cfg, sizeof(*cfg)) == 0 &&
+                          e->dg_version == e->topo_version && e->dg_sched_flags == e->sched_flags;
         if (!same) {
-            if (e->dgexec) (void)hipGraphExecDestroy(e->dgexec);
-            if (e->dgraph) (void)hipGraphDestroy(e->dgraph);
-            e->dgexec = nullptr;
-            e->dgraph = nullptr;
+            drop_domain_graph(e);
             HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
             for (int q = 0; q < G; ++q) {
                 if ((rc = enqueue_rccl_step(e, cfg, first_step + k + q))) {
@@ -2105,11 +2169,20 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
             HIPCHK(hipGraphInstantiate(&e->dgexec, e->dgraph, nullptr, nullptr, 0));
             e->dg_steps = G;
             e->dg_cfg = *cfg;
+            e->dg_version = e->topo_version;
+            e->dg_sched_flags = e->sched_flags;
+            e->rstats.graphs_captured++;
         }
-        for (; steps - k >= G; k += G) HIPCHK(hipGraphLaunch(e->dgexec, e->stream));
+        for (; steps - k >= G; k += G) {
+            HIPCHK(hipGraphLaunch(e->dgexec, e->stream));
+            e->rstats.graph_launches++;
+            e->rstats.graph_steps += G;
+        }
     }
-    for (; k < steps; ++k)
+    for (; k < steps; ++k) {
         if ((rc = enqueue_rccl_step(e, cfg, first_step + k))) return rc;
+        e->rstats.eager_steps++;
+    }
     if ((steps - k0) & 1) e->parity ^= 1;
     if (steps > 0) {
         e->dom_cont = true;
@@ -2317,7 +2390,8 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     HIPCHK(hipEventElapsedTime(&tot, ev[0], ev[ev.size() - 1]));
     if (dbg) {
         std::vector<unsigned long long> h(dbg_n);
-        HIPCHK(hipMemcpy(h.data(), dbg, dbg_n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(h.data(), dbg, dbg_n * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
         (void)hipFree(dbg);
         if (FILE* f = std::fopen(dbg_path, "wb")) {
             std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
@@ -2326,7 +2400,8 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     }
     if (dbgb) {
         std::vector<unsigned long long> h(dbgb_n);
-        HIPCHK(hipMemcpy(h.data(), dbgb, dbgb_n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(h.data(), dbgb, dbgb_n * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
         (void)hipFree(dbgb);
         if (FILE* f = std::fopen(dbgb_path, "wb")) {
             std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
@@ -2337,7 +2412,8 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     if (steps & 1) e->parity ^= 1;
     if (cfg->noise == GCS_NOISE_INJECTED) e->noise_cursor += steps;
     DevCtx d;
-    HIPCHK(hipMemcpy(&d, e->ctx, sizeof(d), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(&d, e->ctx, sizeof(d), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
     out->steps = steps;
     out->total_ms = tot;
     out->force_ms = force / (double)steps;
@@ -2384,15 +2460,13 @@ int gcs_engine_set_cu_mask(gcs_engine* e, const uint32_t* mask, int32_t words)
     HIPCHK(hipStreamSynchronize(e->stream));
     hipStream_t s = nullptr;
     if (words > 0) {
+        // a CU-masked stream has the default (blocking) flags: it orders against legacy null-stream work, so the
+        // engine issues no null-stream copies (every copy is async on e->stream)
         HIPCHK(hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask));
     } else {
         HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     }
     drop_graph(e);
-    if (e->dgexec) (void)hipGraphExecDestroy(e->dgexec);
-    if (e->dgraph) (void)hipGraphDestroy(e->dgraph);
-    e->dgexec = nullptr;
-    e->dgraph = nullptr;
     (void)hipStreamDestroy(e->stream);
     e->stream = s;
     return GCS_OK;
@@ -2414,6 +2488,14 @@ int gcs_engine_get_list_stats(gcs_engine* e, gcs_list_stats* out)
     out->pair_classes = e->ntypes;
     out->capacity = e->list_cap;
     out->sync_stalls = (int64_t)d.scan_stall;
+    return GCS_OK;
+}
+
+int gcs_engine_get_run_stats(gcs_engine* e, gcs_run_stats* out)
+{
+    if (!e || !out) return fail(GCS_EINVAL, "null argument");
+    *out = e->rstats;
+    out->graphs_cached = (int64_t)e->graphs.size() + (e->dgexec ? 1 : 0);
     return GCS_OK;
 }
 
@@ -2452,7 +2534,8 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         return GCS_OK;
     }
     if (option == GCS_OPT_LIST_CAP) {
-        if (value < 32 || value > 16384) return fail(GCS_EINVAL, "list capacity must be in [32, 16384]");
+        if (value < 32 || value > 16384 || (value % kMaxListWaves) != 0)
+            return fail(GCS_EINVAL, "list capacity must be a multiple of 4 in [32, 16384]");
         e->list_cap = (int)value;
         drop_graph(e);
         return GCS_OK;

@@ -109,6 +109,11 @@ class ListStats(C.Structure):
                 ("sync_stalls", _i64)]
 
 
+class RunStats(C.Structure):
+    _fields_ = [("graph_launches", _i64), ("graph_steps", _i64), ("eager_steps", _i64), ("graphs_captured", _i64),
+                ("graphs_cached", _i64)]
+
+
 # name -> (restype, argtypes); the exported surface of include/gcs.h
 PROTOTYPES = {
     "gcs_last_error": (C.c_char_p, []),
@@ -143,6 +148,7 @@ PROTOTYPES = {
     "gcs_engine_profile": (C.c_int, [C.c_void_p, C.POINTER(BDConfig), _i64, _i64, C.POINTER(Profile)]),
     "gcs_engine_set_option": (C.c_int, [C.c_void_p, _i32, _i64]),
     "gcs_engine_get_list_stats": (C.c_int, [C.c_void_p, C.POINTER(ListStats)]),
+    "gcs_engine_get_run_stats": (C.c_int, [C.c_void_p, C.POINTER(RunStats)]),
     "gcs_engine_set_cu_mask": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), _i32]),
     "gcs_engine_contacts_update": (C.c_int, [C.c_void_p, _d]),
     "gcs_engine_contacts_read": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), _i64, C.POINTER(_i64)]),

@@ -382,6 +382,12 @@ class Engine:
         A.check(self._lib.gcs_engine_get_list_stats(self._h, C.byref(s)))
         return {k: getattr(s, k) for k, _ in A.ListStats._fields_}
 
+    def run_stats(self) -> dict:
+        """graph replays vs eager steps of every run so far (gcs_engine_get_run_stats)"""
+        s = A.RunStats()
+        A.check(self._lib.gcs_engine_get_run_stats(self._h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in A.RunStats._fields_}
+
 
 def rccl_unique_id() -> bytes:
     """An RCCL communicator id (rank 0 draws it; every rank passes it to Engine.domain_rccl)."""

@@ -19,9 +19,10 @@ Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) every rank runs
 gloo carries the barrier, the max-over-ranks time and the per-rank rates only; value = all particle updates of
 all ranks / the slowest rank's time ("scaling": "weak").
 
-Timed window: warm-up runs at least two graph chunks per engine (every hipGraph is captured and instantiated before
-timing), then the timed region repeats passes of --steps steps (per replica) until it lasts >= --min-window-s;
-"steps" reports the steps actually timed, "steps_requested" the flag.
+Timed window: warm-up runs passes of the timed region's own shape (>= 2 passes, >= --warmup steps), so every hipGraph
+the timed passes replay is captured and instantiated before timing; then the timed region repeats passes of --steps
+steps (per replica) with no host synchronisation until the end, sized to last >= --min-window-s; "steps" reports the
+steps actually timed, "steps_requested" the flag, "graph_replays" / "timed_runs" how the engines issued them.
 
 Rank 0 prints ONE JSON line.  See DESIGN.md "Measurement" for the roofline accounting.
 """
@@ -31,6 +32,7 @@ import argparse
 import json
 import math
 import os
+import shutil
 import socket
 import subprocess
 import sys
@@ -252,10 +254,18 @@ def cpu_baseline(budget_s, procs):
     `replicas_value`: `procs` independent single-threaded trajectories side by side, aggregate.
     Both legs run as child processes that never touch the device."""
 
+    cpus = cpu_share(procs)
+
     def launch(k):
         env = dict(os.environ, OMP_NUM_THREADS="1")
-        return [subprocess.Popen([sys.executable, str(ROOT / "bench.py"), "--cpu-worker", str(budget_s)],
-                                 stdout=subprocess.PIPE, text=True, env=env) for _ in range(k)]
+        out = []
+        for q in range(k):
+            # pinned one per core (taskset -c <cpu>): the legs never share a core, so the aggregate is k cores' worth
+            cmd = [sys.executable, str(ROOT / "bench.py"), "--cpu-worker", str(budget_s)]
+            if shutil.which("taskset"):
+                cmd = ["taskset", "-c", str(cpus[q % len(cpus)])] + cmd
+            out.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env))
+        return out
 
     def collect(ps):
         out = []
@@ -272,13 +282,25 @@ def cpu_baseline(budget_s, procs):
                      f"({one['seconds']:.1f} s, oracle/libgcs_oracle.so fp64 single thread, "
                      f"-O2 -funsafe-math-optimizations)",
            "cpu_model": _cpu_model()}
-    if procs > 1:
-        many = collect(launch(procs))
+    if len(cpus) > 1:
+        many = collect(launch(len(cpus)))
         res["replicas_value"] = sum(m["value"] for m in many)
-        res["replicas_cores"] = procs
-        res["replicas_sample"] = (f"{procs} independent single-threaded oracle trajectories run side by side, "
+        res["replicas_cores"] = len(cpus)
+        res["replicas_cpus"] = cpus
+        res["replicas_sample"] = (f"{len(cpus)} independent single-threaded oracle trajectories run side by side, "
+                                  f"each pinned to its own core (taskset -c), "
                                   f"{min(m['steps'] for m in many)}-{max(m['steps'] for m in many)} steps each")
     return res
+
+
+def cpu_share(limit):
+    """The cores this process may use (its affinity set; SURVEY 8d (ii) `nproc`), at most `limit` (the GPU box's CPU
+    share is 16 cores per GPU, while its affinity set may show the whole machine)."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = list(range(os.cpu_count() or 1))
+    return cpus[:max(1, limit)]
 
 
 def _cpu_model():
@@ -307,6 +329,90 @@ def read_traffic(fused=3):
         except Exception:
             return None
     return None
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# secondary legs of the default line: C5 on one GPU, the C3 cell cycle
+
+
+def c5_leg(local, seed, steps, log=sys.stderr):
+    """C5 (606,248 particles, BASELINE configs[4]'s system) as ONE trajectory on this GPU, from its synthetic start
+    (step 0, core_scale 0.5 and growing; gcs.config.resolution_scaled force field): the engine's default step and
+    the explicit step shapes (list step, 2-launch rebuild step, 6-launch unfused tile step), each warmed by 64 steps
+    (graphs captured)."""
+    from gcs import _abi as A
+    from gcs import synthetic
+    cfg = bench_config("c5")
+    d = synthetic.make_c5(master_seed=1)
+    bd = {"temperature": cfg.temperature, "timestep": cfg.timestep, "seed": seed}
+    out = {"particles": d.n, "window": f"steps 64..{64 + steps} from the synthetic start", "steps": steps}
+    for name, fused in (("default", None), ("list_step", 3), ("rebuild_step", 2), ("unfused_tile_step", 0)):
+        e = make_engine(d, cfg, local, 0)
+        if fused is not None:
+            e.set_option(A.OPT_FUSED_STEP, fused)
+        e.run(64, first_step=0, **bd)
+        e.synchronize()
+        t0 = time.perf_counter()
+        e.run(steps, first_step=64, **bd)
+        e.synchronize()
+        out[name] = d.n * steps / (time.perf_counter() - t0)
+        if name == "default":
+            out["default_step"] = "list" if e.list_stats()["active"] else "rebuild"
+        e.close()
+        print(f"bench: C5 {name} {out[name]:.3e} bead-updates/s", file=log, flush=True)
+    return out
+
+
+def cycle_leg(local, scale, log=sys.stderr):
+    """C3 (BASELINE configs[2]): one interphase -> mitosis -> interphase cell cycle of the synthetic C2 genome
+    through the stage entry points and the HDF5 store (gcs.cli, as scripts/simulate:44-47 runs the reference's
+    executables): prepare -> anatelophase (anaphase + telophase, 586 particles) -> transition interphase ->
+    interphase (relaxation + simulation with the contact map, 60,662) -> transition prometaphase -> prometaphase
+    (1,172) -> transition cycle into the daughter's file.  Step counts are the reference defaults
+    (common/simulation_config.hpp:15-115) divided by `scale`; the sampling/logging/contact cadence is the
+    reference's.  Each stage's wall time includes its engine setup and host work (HDF5 frames, energies, contacts)."""
+    import tempfile
+    from gcs import cli, mitotic, synthetic
+    from gcs.config import SimulationConfig
+    cfg = SimulationConfig()
+    m, ip = cfg.mitotic_phase, cfg.interphase
+    steps = {"anaphase": m.anaphase_steps // scale, "telophase": m.telophase_steps // scale,
+             "relaxation": ip.relaxation_steps // scale, "interphase": ip.steps // scale,
+             "prometaphase": m.prometaphase_steps // scale}
+    d = synthetic.make_c2(master_seed=1)
+    a = mitotic.anatelophase_design(d, m)
+    pm = mitotic.prometaphase_design(a, m, 1)
+    dev = ["--device", str(local), "--quiet"]
+    out = {"scale": f"reference step counts / {scale}", "steps": steps,
+           "particles": {"anatelophase": a.n, "interphase": d.n, "prometaphase": pm.n}, "stages": {}}
+    with tempfile.TemporaryDirectory() as td:
+        p, q = str(Path(td) / "mother.h5"), str(Path(td) / "daughter.h5")
+        calls = [
+            ("prepare", ["prepare-synthetic", p, "--config", "c2", "--master-seed", "1"], 0, 0),
+            ("anatelophase", ["anatelophase", p, "--anaphase-steps", str(steps["anaphase"]), "--telophase-steps",
+                              str(steps["telophase"])] + dev, steps["anaphase"] + steps["telophase"], a.n),
+            ("transition_interphase", ["transition", "interphase", p], 0, 0),
+            ("interphase", ["interphase", p, "--relaxation-steps", str(steps["relaxation"]), "--steps",
+                            str(steps["interphase"])] + dev, steps["relaxation"] + steps["interphase"], d.n),
+            ("transition_prometaphase", ["transition", "prometaphase", p], 0, 0),
+            ("prometaphase", ["prometaphase", p, "--steps", str(steps["prometaphase"])] + dev,
+             steps["prometaphase"], pm.n),
+            ("prepare_daughter", ["prepare-synthetic", q, "--config", "c2", "--master-seed", "2"], 0, 0),
+            ("transition_cycle", ["transition", "cycle", p, q], 0, 0),
+        ]
+        total = 0.0
+        for name, argv, nsteps, n in calls:
+            t0 = time.perf_counter()
+            cli.main(argv)
+            el = time.perf_counter() - t0
+            total += el
+            rec = {"wall_s": el}
+            if nsteps:
+                rec.update(steps=nsteps, particles=n, steps_per_s=nsteps / el, bead_updates_per_s=n * nsteps / el)
+            out["stages"][name] = rec
+            print(f"bench: cycle {name} {el:.2f} s", file=log, flush=True)
+    out["cycle_wall_s"] = total
+    return out
 
 
 # ---------------------------------------------------------------------------------------------------------------
@@ -429,21 +535,41 @@ def replica_main(args):
     n = design.n
     nxt = [window] * R  # next step of every replica (host-side: no device round trip in the timed loop)
 
-    def run_all(steps):
-        """`steps` steps of every replica, enqueued interleaved chunk by chunk so their graphs run side by side"""
+    def enqueue_all(steps):
+        """`steps` steps of every replica, enqueued interleaved chunk by chunk so their graphs run side by side
+        (no host synchronisation: the engines' run calls only enqueue)"""
         chunk = G if G > 0 else 64
         for s0 in range(0, steps, chunk):
             c = min(chunk, steps - s0)
             for k, (e, sd) in enumerate(zip(engines, seeds)):
                 e.run(c, first_step=nxt[k], seed=sd, **bd)
                 nxt[k] += c
+
+    def sync_all():
         for e in engines:
             e.synchronize()
 
-    run_all(max(G, 1))  # first chunk: every engine captures and instantiates its graph
+    def run_stats():
+        if not hasattr(eng, "run_stats"):
+            return {}
+        tot = {}
+        for e in engines:
+            for k, v in e.run_stats().items():
+                tot[k] = tot.get(k, 0) + v
+        return tot
+
+    # warm-up: passes of exactly the timed region's shape, so every graph the timed passes replay (one per rebuild
+    # phase, starting parity and length, gcs_engine_get_run_stats) is captured and instantiated before timing
+    # (3 passes at least: the first pass of a run starts with an eager forced rebuild, which shifts its graphs by a
+    # step, so the timed passes' first shape appears in the warm-up's second pass at the earliest)
+    warm_passes = max(3, math.ceil(warm / K))
+    enqueue_all(K)
+    sync_all()
     t0 = time.perf_counter()
-    run_all(warm)  # steady-state warm-up, timed only to size the passes below
-    warm_s = time.perf_counter() - t0
+    for _ in range(warm_passes - 1):
+        enqueue_all(K)
+    sync_all()
+    per_pass = (time.perf_counter() - t0) / (warm_passes - 1)
 
     # one trajectory alone on the GPU (replica 0; the others are independent and idle meanwhile), its own window
     single_rate = None
@@ -466,16 +592,18 @@ def replica_main(args):
         single_rate = n * k1 * reps / el1
 
     # passes of K steps so the timed window lasts >= min_window_s (estimated from the warm-up, agreed by all ranks)
-    per_pass = warm_s * K / warm
     passes = max(1, math.ceil(args.min_window_s / max(per_pass, 1e-9)))
     passes = int(max_over_ranks(dist, float(passes)))
     barrier(dist)
-    for e in engines:
-        e.synchronize()
+    sync_all()
+    rs0 = run_stats()
     t0 = time.perf_counter()
     for _ in range(passes):
-        run_all(K)
+        enqueue_all(K)
+    sync_all()
     el = time.perf_counter() - t0
+    rs1 = run_stats()
+    timed_runs = {k: rs1[k] - rs0.get(k, 0) for k in rs1 if k != "graphs_cached"}
     barrier(dist)
     steps = passes * K
     el_max = max_over_ranks(dist, el)
@@ -540,6 +668,15 @@ def replica_main(args):
         if dist is not None:
             dist.destroy_process_group()
         return
+    for e in engines[1:]:
+        e.close()  # (replica 0 stays for the line's context)
+
+    c5 = cycle = None
+    if world == 1 and not args.stub_engine:
+        if args.c5_steps > 0:
+            c5 = c5_leg(local, seed, args.c5_steps)
+        if args.cycle_scale > 0:
+            cycle = cycle_leg(local, args.cycle_scale)
 
     cpu = None
     if world == 1 and args.cpu_budget > 0 and state is not None and args.config == "c2":
@@ -561,7 +698,9 @@ def replica_main(args):
         "data": "synthetic" if not args.stub_engine else "stub",
         "steps_requested": K,
         "passes": passes,
-        "warmup_steps_run": warm + max(G, 1),
+        "warmup_steps_run": warm_passes * K,
+        "graph_replays": timed_runs.get("graph_launches"),
+        "timed_runs": timed_runs,
         "timed_s": el_max,
         "per_rank_values": rank_values,
         "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, {R} independent "
@@ -575,7 +714,9 @@ def replica_main(args):
                    "split_tiles": args.split, "tile_priority": args.prio, "subtiles": args.subtiles,
                    "scan_mb": args.scan_mb, "start_window_value": start_rate, "finite": finite,
                    "contacts_update_ms": contacts_ms, "contacts_distinct_pairs_22_updates": contacts_distinct,
-                   "list_step": lst, "list_waves_per_tile": list_waves},
+                   "list_step": lst, "list_waves_per_tile": list_waves,
+                   "c5_value": c5["default"] if c5 else None, "c5": c5,
+                   "c3_cycle_wall_s": cycle["cycle_wall_s"] if cycle else None, "c3_cycle": cycle},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(args.fused),
                      "kernel": STEP_KERNEL.get(args.fused, ("?",))[0], "force_ms": force_ms, "cell_ms": prof["cell_ms"],
@@ -583,8 +724,7 @@ def replica_main(args):
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
-    for e in engines:
-        e.close()
+    eng.close()
     if dist is not None:
         dist.destroy_process_group()
 
@@ -622,6 +762,9 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-worker", type=float, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--stub-engine", action="store_true", help=argparse.SUPPRESS)  # CPU tests of the launcher
     ap.add_argument("--no-start-window", action="store_true", help="skip the secondary step-0 window")
+    ap.add_argument("--c5-steps", type=int, default=256, help="secondary C5 window per step shape (0 = skip)")
+    ap.add_argument("--cycle-scale", type=int, default=10,
+                    help="secondary C3 cell cycle at the reference step counts / this (0 = skip)")
     ap.add_argument("--decomp", type=int, default=0,
                     help="spatial domain decomposition of ONE trajectory: K domains (torchrun: one per rank over "
                          "RCCL; single process: K domains on this GPU, in-process exchange)")

@@ -369,6 +369,20 @@ typedef struct gcs_list_stats {
 } gcs_list_stats;
 int gcs_engine_get_list_stats(gcs_engine* e, gcs_list_stats* out);
 
+/* How gcs_engine_run / gcs_engine_domain_run issued their steps (cumulative over the engine's life): steps
+ * replayed from captured hipGraphs (any stretch of up to GCS_OPT_GRAPH_STEPS steps, captured once per rebuild
+ * phase, starting buffer parity and length) and steps launched eagerly (a run start's forced list rebuild, a
+ * step carrying a deferred contact update, GCS_OPT_GRAPH_STEPS 0).  Replaces nothing in the reference (the
+ * integrator loop of micromd, stage_interphase/simulation_driver_interphase.cpp:57-63, has no launches). */
+typedef struct gcs_run_stats {
+    int64_t graph_launches;   /* hipGraphLaunch calls */
+    int64_t graph_steps;      /* steps inside those replays */
+    int64_t eager_steps;      /* steps launched one by one */
+    int64_t graphs_captured;  /* captures (a cache miss: new phase / parity / length, or changed settings) */
+    int64_t graphs_cached;    /* captured sequences held now */
+} gcs_run_stats;
+int gcs_engine_get_run_stats(gcs_engine* e, gcs_run_stats* out);
+
 /* Restrict the engine's stream to a set of compute units (bit i of mask[i / 32] = CU i; words = 0: all CUs), e.g.
  * one group of XCDs per trajectory when several share a GPU.  Recreates the stream: call between runs. */
 int gcs_engine_set_cu_mask(gcs_engine* e, const uint32_t* mask, int32_t words);

@@ -42,7 +42,7 @@ STRUCTS = {
     "gcs_system_desc": A.SystemDesc, "gcs_softcore_params": A.SoftcoreParams, "gcs_bond_params": A.BondParams,
     "gcs_softwell_params": A.SoftwellParams, "gcs_wall_params": A.WallParams,
     "gcs_point_source_params": A.PointSourceParams, "gcs_kinetochore_spec": A.KinetochoreSpec,
-    "gcs_context": A.Context, "gcs_schedule": A.Schedule, "gcs_bd_config": A.BDConfig, "gcs_profile": A.Profile, "gcs_list_stats": A.ListStats,
+    "gcs_context": A.Context, "gcs_schedule": A.Schedule, "gcs_bd_config": A.BDConfig, "gcs_profile": A.Profile, "gcs_list_stats": A.ListStats, "gcs_run_stats": A.RunStats,
 }
 
 

@@ -147,3 +147,107 @@ def test_deferred_contact_update_flushes_before_position_changes(c1_design, inte
     e.contacts_update(0.24)
     e.contacts_clear()           # a pending update followed by a clear: an empty table
     assert e.contacts_accumulate().shape == (0, 3)
+
+
+# ---- the production path: the update counted INSIDE the next list step (k_lstep<..., CT>) ------------------------
+#
+# After a list-step run, contacts_update only records the distance; the next run's first step counts the pairs of
+# its start positions from its neighbour lists (partners within the contact distance), or, for particles whose
+# lists do not cover that distance (skin outrun, overflowed list, distance beyond cutoff + skin), by a contact-only
+# cell search.  InterphaseDriver and the bench take exactly this path (update, then run, no read in between).
+# Each snapshot is read BEFORE its update, when nothing is pending, so no read flushes the update through the
+# standalone k_contact_insert: every count below comes from the fused step.  Reference: contact_map.cpp:33-85,
+# simulation_driver_interphase.cpp:38-45.
+
+def _bench_state():
+    from pathlib import Path
+    z = np.load(Path(__file__).resolve().parents[1] / "benchdata" / "c2_interphase_step300000.npz")
+    ctx = {"step": int(z["step"]), "time": float(z["time"]), "core_scale": float(z["core_scale"]),
+           "bond_scale": float(z["bond_scale"]), "wall_semiaxes": [float(v) for v in z["wall_semiaxes"]]}
+    return np.asarray(z["positions"], dtype=np.float32).astype(np.float64), ctx
+
+
+LATE = {"step": 200000, "time": 2.0, "core_scale": 0.99, "bond_scale": 0.99, "wall_semiaxes": [1.5, 1.55, 1.6]}
+
+
+def _fused_contacts(design, cfg, ctx, distance, updates, seed, x=None, **opts):
+    e = engine_for(design, cfg)
+    e.set_option(A.OPT_FUSED_STEP, 3)
+    for k, v in opts.items():
+        e.set_option(getattr(A, "OPT_" + k.upper()), v)
+    if x is not None:
+        e.set_positions(x)
+    e.set_context(ctx)
+    step = ctx["step"]
+    e.run(STEPS_PER_UPDATE, first_step=step, seed=seed)
+    step += STEPS_PER_UPDATE
+    before = e.run_stats()
+    snaps = []
+    for _ in range(updates):
+        snaps.append(e.get_positions())  # nothing pending: a plain read
+        e.contacts_update(distance)      # deferred
+        e.run(STEPS_PER_UPDATE, first_step=step, seed=seed)  # counted by this run's first step
+        step += STEPS_PER_UPDATE
+    after = e.run_stats()
+    st = e.list_stats()
+    got = e.contacts_accumulate()
+    return e, got, snaps, st, {k: after[k] - before[k] for k in before}
+
+
+def _check_fused(got, snaps, distance, runs, updates):
+    exp = expected_table(snaps, distance)
+    # the update steps ran eagerly (the contact-counting instantiation), everything else from graphs
+    assert runs["eager_steps"] == updates, runs
+    assert got.shape == exp.shape and np.array_equal(got, exp)
+    assert (got[:, 0] < got[:, 1]).all() and got[:, 2].max() <= updates
+
+
+@pytest.mark.parametrize("frac", [0.24, 0.5])
+def test_fused_contacts_c1_match_oracle(c1_design, frac):
+    """C1, late schedule: 0.24 cs (inside the lists) and 0.5 cs (beyond cutoff + skin: the contact-only search)"""
+    cfg = InterphaseConfig()
+    d = frac * LATE["core_scale"]
+    e, got, snaps, st, runs = _fused_contacts(c1_design, cfg, LATE, d, 5, 31)
+    assert st["active"] == 1
+    _check_fused(got, snaps, d, runs, 5)
+
+
+@pytest.mark.parametrize("frac", [0.24, 0.5])
+def test_fused_contacts_c2_match_oracle(frac):
+    """C2 (60,662 particles) from the bench state (step 300,000)"""
+    design, cfg = synthetic.make_c2(), InterphaseConfig()
+    x, ctx = _bench_state()
+    d = frac * ctx["core_scale"]
+    e, got, snaps, st, runs = _fused_contacts(design, cfg, ctx, d, 2, 41, x=x, contact_bits=25)
+    assert st["active"] == 1
+    _check_fused(got, snaps, d, runs, 2)
+
+
+def test_fused_contacts_forced_fallbacks_match_oracle(c1_design):
+    """skin 30 per mille with a 200-step rebuild period: particles outrun the skin and are searched exactly, for
+    their forces and for their contacts"""
+    cfg = InterphaseConfig()
+    d = 0.24 * LATE["core_scale"]
+    e, got, snaps, st, runs = _fused_contacts(c1_design, cfg, LATE, d, 5, 43, list_skin=30, list_every=200)
+    assert st["fallback_particle_steps"] > 0, st
+    _check_fused(got, snaps, d, runs, 5)
+
+
+def test_fused_contacts_overflowed_lists_match_oracle(c1_design):
+    """32-entry lists: the overflowed particles' contacts come from the contact-only search"""
+    cfg = InterphaseConfig()
+    d = 0.24 * LATE["core_scale"]
+    e, got, snaps, st, runs = _fused_contacts(c1_design, cfg, LATE, d, 4, 47, list_cap=32)
+    assert st["fallback_particle_steps"] > 0, st
+    _check_fused(got, snaps, d, runs, 4)
+
+
+def test_fused_contacts_leave_the_trajectory_unchanged(c1_design):
+    """the contact-counting step computes the same forces bit for bit: a run with fused updates equals one without"""
+    cfg = InterphaseConfig()
+    a, _, _, _, _ = _fused_contacts(c1_design, cfg, LATE, 0.5, 3, 53)
+    b = engine_for(c1_design, cfg)
+    b.set_option(A.OPT_FUSED_STEP, 3)
+    b.set_context(LATE)
+    b.run(4 * STEPS_PER_UPDATE, first_step=LATE["step"], seed=53)
+    assert np.array_equal(a.get_positions(), b.get_positions())
