@@ -78,6 +78,7 @@ struct GraphEntry {
     unsigned long long used;
 };
 constexpr size_t kMaxGraphs = 32;  // cached step sequences per engine (least recently used evicted)
+constexpr int kInflight = 32;      // graph launches an engine lets run ahead of the device
 
 template <class T>
 int dalloc(T** p, size_t count)
@@ -214,6 +215,11 @@ struct gcs_engine {
     unsigned long long graph_clock = 0;  // LRU stamp
     GraphKey g_key{};                     // what every cached graph was captured under (else the cache is dropped)
     bool g_key_set = false;
+    // bounded run-ahead: an event after every graph launch; the host waits for the one kInflight launches back
+    // before enqueueing another (a host that enqueues thousands of replays ahead of the device gains nothing and
+    // exhausted a tracing profiler's per-dispatch records)
+    hipEvent_t inflight[kInflight] = {};
+    unsigned long long inflight_n = 0;
     gcs_run_stats rstats{};
 
     // list step (GCS_OPT_FUSED_STEP 3): neighbour lists, pair-factor classes, rebuild period
@@ -250,6 +256,7 @@ namespace {
 // exchange buffers and the communicator, so every change of those drops it
 void drop_domain_graph(gcs_engine* e)
 {
+    if (e->dgexec) (void)hipStreamSynchronize(e->stream);  // it may still be executing
     if (e->dgexec) (void)hipGraphExecDestroy(e->dgexec);
     if (e->dgraph) (void)hipGraphDestroy(e->dgraph);
     e->dgexec = nullptr;
@@ -258,6 +265,7 @@ void drop_domain_graph(gcs_engine* e)
 
 void drop_graph(gcs_engine* e)
 {
+    if (!e->graphs.empty() || e->dgexec) (void)hipStreamSynchronize(e->stream);  // none may still be executing
     for (GraphEntry& g : e->graphs) {
         (void)hipGraphExecDestroy(g.exec);
         (void)hipGraphDestroy(g.graph);
@@ -673,8 +681,15 @@ int ensure_list(gcs_engine* e)
         (rc = dalloc(&e->skmu, stride)) || (rc = dalloc(&e->sbrow, stride)))
         return rc;
     if (!e->lticket) {
-        if ((rc = dalloc(&e->lticket, 32 * 9))) return rc;
-        HIPCHK(hipMemsetAsync(e->lticket, 0, 32 * 9 * sizeof(unsigned), e->stream));
+        // arrival counters 0, the launch accumulators at their identities (k_lstep resets them after every launch)
+        if ((rc = dalloc(&e->lticket, kListTicketWords))) return rc;
+        std::vector<unsigned> h(kListTicketWords, 0u);
+        for (int k = 0; k < 8 * (kListAccSlots + 1); ++k) {
+            const unsigned long long v = list_acc_identity(k % (kListAccSlots + 1));
+            std::memcpy(&h[kListAccBase + 32 * k], &v, sizeof(v));
+        }
+        HIPCHK(hipMemcpyAsync(e->lticket, h.data(), h.size() * sizeof(unsigned), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
     }
     // entries past a slot's count are read (never gathered): keep them defined
     HIPCHK(hipMemsetAsync(e->list, 0, need * sizeof(int), e->stream));
@@ -697,9 +712,18 @@ int auto_list_every(const gcs_engine* e, const gcs_bd_config* cfg)
     return (int)std::min(64.0, std::max(1.0, m));
 }
 
+// k_lstep launch flags of the step that starts at step index st: the schedule; the bounding box when the next step
+// rebuilds (its grid); neighbour-count statistics on those steps too (ctx->neighbors)
+int list_flags(const gcs_engine* e, int64_t st)
+{
+    const bool next_build = ((st + 1) % e->list_every) == 0;
+    return (e->sched_flags != 0 ? 1 : 0) | (next_build ? 2 | 4 : 0);
+}
+
 // one list step: on a rebuild step the cell list at cutoff + skin (ctx->grid, set by the prime or the last
-// tail), the lists, then the step itself (forces + local terms + update + tail in the last workgroup)
-void enqueue_list_step(gcs_engine* e, bool build, double contact = 0, int parity = -1)
+// bounding-box step's tail), the lists, then the step itself (forces + local terms + update + tail in the final
+// workgroup)
+void enqueue_list_step(gcs_engine* e, bool build, int lflags, double contact = 0, int parity = -1)
 {
     ForceArgs la = list_args(e);
     la.par_hint = parity;
@@ -721,7 +745,7 @@ void enqueue_list_step(gcs_engine* e, bool build, double contact = 0, int parity
                          e->sbrow, e->fa.has_bonds ? e->boff : nullptr);
         launch_list_build(e->stream, e->ctx, la);
     }
-    launch_list_step(e->stream, e->ctx, la, e->sched_flags != 0);
+    launch_list_step(e->stream, e->ctx, la, lflags);
 }
 int step_grid(const gcs_engine* e) { return e->fa.split ? force_grid_split(e->n) : force_grid(e->n); }
 
@@ -852,6 +876,7 @@ int cached_graph(gcs_engine* e, const GraphKey& key, int phase, int parity, int 
     if (e->graphs.size() >= kMaxGraphs) {
         auto lru = std::min_element(e->graphs.begin(), e->graphs.end(),
                                     [](const GraphEntry& x, const GraphEntry& y) { return x.used < y.used; });
+        HIPCHK(hipStreamSynchronize(e->stream));  // it may still be executing
         (void)hipGraphExecDestroy(lru->exec);
         (void)hipGraphDestroy(lru->graph);
         e->graphs.erase(lru);
@@ -868,6 +893,22 @@ int cached_graph(gcs_engine* e, const GraphKey& key, int phase, int parity, int 
     e->graphs.push_back(g);
     e->rstats.graphs_captured++;
     *out = g.exec;
+    return GCS_OK;
+}
+
+// hipGraphLaunch with the engine's run-ahead bound (see gcs_engine::inflight)
+int launch_graph(gcs_engine* e, hipGraphExec_t x)
+{
+    hipEvent_t& ev = e->inflight[e->inflight_n % kInflight];
+    if (!ev) {
+        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    } else if (e->inflight_n >= (unsigned long long)kInflight) {
+        HIPCHK(hipEventSynchronize(ev));
+    }
+    HIPCHK(hipGraphLaunch(x, e->stream));
+    HIPCHK(hipEventRecord(ev, e->stream));
+    e->inflight_n++;
+    e->rstats.graph_launches++;
     return GCS_OK;
 }
 
@@ -1149,6 +1190,8 @@ int gcs_engine_destroy(gcs_engine* e)
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     drop_graph(e);
+    for (hipEvent_t& ev : e->inflight)
+        if (ev) (void)hipEventDestroy(ev);
     dfree(e->pos[0]);
     dfree(e->pos[1]);
     dfree(e->kmu);
@@ -1536,7 +1579,7 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
             const int phase = (int)(((st % M) + M) % M);
             if (e->c_pending > 0 || e->l_need_build || G == 0) {
                 // the contact update the host asked for after the last step, a run start's rebuild, or no graphs
-                enqueue_list_step(e, e->l_need_build || phase == 0, e->c_pending, par(done));
+                enqueue_list_step(e, e->l_need_build || phase == 0, list_flags(e, st), e->c_pending, par(done));
                 e->c_pending = 0;
                 e->l_need_build = false;
                 ++done;
@@ -1547,11 +1590,10 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
             const int p0 = par(done);
             hipGraphExec_t x = nullptr;
             rc = cached_graph(e, key, phase, p0, len, [&]() {
-                for (int k = 0; k < len; ++k) enqueue_list_step(e, (phase + k) % M == 0, 0, p0 ^ (k & 1));
+                for (int k = 0; k < len; ++k)
+                    enqueue_list_step(e, (phase + k) % M == 0, list_flags(e, st + k), 0, p0 ^ (k & 1));
             }, &x);
-            if (rc) return rc;
-            HIPCHK(hipGraphLaunch(x, e->stream));
-            e->rstats.graph_launches++;
+            if (rc || (rc = launch_graph(e, x))) return rc;
             e->rstats.graph_steps += len;
             done += len;
         }
@@ -1563,9 +1605,7 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
         rc = cached_graph(e, key, 0, 0, len, [&]() {
             for (int k = 0; k < len; ++k) enqueue_step(e, spacestep, (float)cfg->spacestep, (float)cfg->timestep);
         }, &x);
-        if (rc) return rc;
-        HIPCHK(hipGraphLaunch(x, e->stream));
-        e->rstats.graph_launches++;
+        if (rc || (rc = launch_graph(e, x))) return rc;
         e->rstats.graph_steps += len;
         done += len;
     }
@@ -2174,8 +2214,7 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
             e->rstats.graphs_captured++;
         }
         for (; steps - k >= G; k += G) {
-            HIPCHK(hipGraphLaunch(e->dgexec, e->stream));
-            e->rstats.graph_launches++;
+            if ((rc = launch_graph(e, e->dgexec))) return rc;
             e->rstats.graph_steps += G;
         }
     }
@@ -2338,7 +2377,7 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
             HIPCHK(hipEventRecord(ev[2 + 5 * k], e->stream));
             ForceArgs lk = la;
             lk.par_hint = e->parity ^ (int)(k & 1);  // as gcs_engine_run launches it
-            launch_list_step(e->stream, e->ctx, lk, e->sched_flags != 0);
+            launch_list_step(e->stream, e->ctx, lk, list_flags(e, first_step + k) | 4);  // statistics every step
             e->fa.dbg_times = nullptr;
             for (int q = 3; q <= 5; ++q) HIPCHK(hipEventRecord(ev[q + 5 * k], e->stream));
             continue;

@@ -216,9 +216,20 @@ struct ForceArgs {
     unsigned* c_counts;
     int c_bits;
     int* c_overflow;
-    unsigned* lticket;      // list step arrival counters: [32 g] per group of workgroups (g < 8), [32 * 8] groups
+    unsigned* lticket;      // list step arrival counters: [32 g] per group of workgroups (g < 8), [32 * 8] groups;
+                            // then the launch accumulators (kListAccBase)
 };
 
+// list step launch accumulators behind the arrival counters in ForceArgs::lticket (unsigned words, 128 B per slot):
+// per group of workgroups (b % 8) kListAccSlots slots + one overflow flag (kernels.hip list_accumulate)
+constexpr int kListAccBase = 32 * 9;
+constexpr int kListAccSlots = 15;
+constexpr int kListTicketWords = kListAccBase + 8 * 32 * (kListAccSlots + 1);
+// identity of accumulator slot k (what list_accumulate starts from)
+__host__ __device__ inline unsigned long long list_acc_identity(int k)
+{
+    return (k >= 9 && k < 12) ? 0xffffffffull : 0ull;  // bbox lo: the largest ordered value; everything else 0
+}
 constexpr int kMaxListWaves = 4;  // waves per tile of the list kernels (each owns one list segment): 2 or 4
 constexpr int kMaxTypes = 256;          // pair-factor classes (8 bits of a list entry)
 constexpr int kListIndexBits = 24;      // particle index bits of a list entry
@@ -272,7 +283,8 @@ void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, cons
                       const int* boff = nullptr);
 // list step: build the neighbour lists on the current cell list (grid rc = cutoff + skin); one step from them
 void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a);
-void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int apply_sched);
+// flags: 1 apply the schedule, 2 the next step rebuilds (bounding box -> grid), 4 neighbour-count statistics
+void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags);
 int list_step_grid(int n);
 bool list_u16(int n);  // list entries are 16-bit slot indices (N <= 65536)
 void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceArgs& a, bool fused);

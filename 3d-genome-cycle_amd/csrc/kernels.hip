@@ -1703,19 +1703,6 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
 // group of 16 the union shrinks ~2.5x.  Chunks are 32 candidates per group (one 32-bit hit mask per lane), staged
 // with FPL = 32 / GL loads per lane; phase-1 LDS reads then carry NG addresses (one broadcast per group, the groups
 // on disjoint banks).  Same phase-1 test, frame (per-group origin) and phase 2 as pair_forces.
-#ifndef GCS_ROW_CURSOR
-#define GCS_ROW_CURSOR 0  // 1: incremental stencil-row cursor in the sub-tile candidate fetch
-#endif
-#ifndef GCS_P1_PLAIN
-#define GCS_P1_PLAIN 0  // 1: phase-1 hit bits from plain C (compiler-scheduled) instead of the cmp+addc asm pair,
-                        // 2: sub + v_alignbit (the list build's form)
-#endif
-#ifndef GCS_LBUILD_PK
-#define GCS_LBUILD_PK 1  // kModeList (k_lbuild): phase 1 on candidate pairs with packed fp32 math (see below)
-#endif
-#ifndef GCS_LBUILD_P2U
-#define GCS_LBUILD_P2U 1  // list build phase 2: hits per round (> 1: the rounds' slot reads issued together)
-#endif
 #ifndef GCS_P2_UNROLL
 #define GCS_P2_UNROLL 4  // sub-tile phase 2: hits popped per lane per round (rounds = wave max of hits / this)
 #endif
@@ -1799,18 +1786,6 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
     float4 np[FPL];
     float nb[FPL];
     int nj[FPL];
-#if GCS_ROW_CURSOR
-    // a lane's candidate index v = cg + G i only grows from chunk to chunk, so its stencil row is found by walking
-    // forward from the previous one (usually zero or one step) instead of a 4-level binary search of dependent LDS
-    // reads; rows 9..16 start at the group total, so the walk stops for any v < total
-    int rcur[FPL], rnext[FPL], rbase[FPL];
-#pragma unroll
-    for (int f = 0; f < FPL; ++f) {
-        rcur[f] = 0;
-        rnext[f] = rowV[1];
-        rbase[f] = rowJ[0] - rowV[0];
-    }
-#endif
     auto fetch = [&](int c) {
         const int cg = wv + c * nwv;  // chunk index within every group
 #pragma unroll
@@ -1819,20 +1794,11 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
             const int v = cg + G * i;
             nj[f] = -1;
             if (cg < G && v < total) {
-#if GCS_ROW_CURSOR
-                while (rnext[f] <= v) {
-                    ++rcur[f];
-                    rnext[f] = rowV[rcur[f] + 1];
-                    rbase[f] = rowJ[rcur[f]] - rowV[rcur[f]];
-                }
-                nj[f] = rbase[f] + v;
-#else
-                int lo = 0;
+                int lo = 0;  // the stencil row of candidate v: a 4-level binary search of the row starts
 #pragma unroll
                 for (int step = 8; step > 0; step >>= 1)
                     if (rowV[lo + step] <= v) lo += step;
                 nj[f] = rowJ[lo] + (v - rowV[lo]);
-#endif
                 np[f] = a.spos[nj[f]];
                 nb[f] = a.sb[nj[f]];
             }
@@ -1845,7 +1811,7 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
             const int i = gl + GL * f;
             const bool real = nj[f] >= 0;
             const float px = real ? np[f].x - ox : far, py = real ? np[f].y - oy : far, pz = real ? np[f].z - oz : far;
-            if constexpr (MODE == kModeList && GCS_LBUILD_PK) {
+            if constexpr (MODE == kModeList) {
                 // pair layout: candidates 2h, 2h+1 in float4s 2h {x, x', y, y'} and 2h+1 {z, z', w, w'}; slots at
                 // float 8 * kSub / 2 (the list build's phase 2 needs only the partner's slot)
                 float* const P = reinterpret_cast<float*>(my_cand);
@@ -1858,8 +1824,7 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 continue;
             }
             my_cand[2 * i] = make_float4(-2.f * px, -2.f * py, -2.f * pz, fmaf(pz, pz, fmaf(py, py, px * px)));
-            my_cand[2 * i + 1] = make_float4(real ? kA * np[f].w : 0.f, real ? kB * nb[f] : 0.f,
-                                             MODE == kModeList ? __int_as_float(real ? nj[f] : -1) : 0.f, 0.f);
+            my_cand[2 * i + 1] = make_float4(real ? kA * np[f].w : 0.f, real ? kB * nb[f] : 0.f, 0.f, 0.f);
             if (MODE == kModeEnergy) s_candj[grp * kSub + i] = nj[f];
         }
         __builtin_amdgcn_wave_barrier();
@@ -1867,7 +1832,7 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
 
         // phase 1: 32 candidates of my group -> one 32-bit hit mask (byte trick: candidate k on bit k ^ 7)
         unsigned m = 0u;
-        if constexpr (MODE == kModeList && GCS_LBUILD_PK) {
+        if constexpr (MODE == kModeList) {
             // the same fma chain per candidate, two candidates per packed instruction (v_pk_fma_f32); hit = sign of
             // tv - thr (tv < thr exactly: a difference of unequal finite floats is never +0), shifted in by
             // v_alignbit: 3 VALU per candidate instead of 5, the same bits in the same places
@@ -1880,24 +1845,13 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 for (int h = 0; h < 4; ++h) {
                     const float4 A = my_cand[k0 + 2 * h], B = my_cand[k0 + 2 * h + 1];
                     const f2 qx = {A.x, A.y}, qy = {A.z, A.w}, qz = {B.x, B.y}, qw = {B.z, B.w};
-#if GCS_LBUILD_PK == 2  // scalar chains (same bits)
-                    tv[h].x = fmaf(qx.x, xi, fmaf(qy.x, yi, fmaf(qz.x, zi, qw.x)));
-                    tv[h].y = fmaf(qx.y, xi, fmaf(qy.y, yi, fmaf(qz.y, zi, qw.y)));
-#else
                     tv[h] = __builtin_elementwise_fma(qx, X, __builtin_elementwise_fma(qy, Y,
                                                       __builtin_elementwise_fma(qz, Z, qw)));
-#endif
                 }
                 unsigned byte = 0u;
 #pragma unroll
                 for (int h = 0; h < 4; ++h) {
-#if GCS_LBUILD_PK == 2
-                    f2 d;
-                    d.x = tv[h].x - thr;
-                    d.y = tv[h].y - thr;
-#else
                     const f2 d = tv[h] - T;
-#endif
                     byte = __builtin_amdgcn_alignbit(byte, __float_as_uint(d.x), 31u);
                     byte = __builtin_amdgcn_alignbit(byte, __float_as_uint(d.y), 31u);
                 }
@@ -1921,17 +1875,10 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                     const bool in = (tv[u] < thr) && (s_candj[grp * kSub + k0 + u] != s);
                     byte = 2u * byte + (in ? 1u : 0u);
                 } else {
-#if GCS_P1_PLAIN == 2
-                    // the sign of tv - thr shifted in (tv < thr exactly; see the list build's phase 1)
-                    byte = __builtin_amdgcn_alignbit(byte, __float_as_uint(tv[u] - thr), 31u);
-#elif GCS_P1_PLAIN
-                    byte = 2u * byte + (tv[u] < thr ? 1u : 0u);
-#else
                     asm("v_cmp_gt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
                         : "+v"(byte)
                         : "v"(thr), "v"(tv[u])
                         : "vcc");
-#endif
                 }
             }
             m |= byte << k0;
@@ -1942,37 +1889,13 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
         if constexpr (MODE == kModeList) {
             // append the hits: one column-major store per hit (lanes of a wave write consecutive slots of a row)
             LE* const seg = reinterpret_cast<LE*>(a.list) + (size_t)wv * a.list_cap * a.list_stride + s;
-#if GCS_LBUILD_PK && GCS_LBUILD_P2U > 1
-            // GCS_LBUILD_P2U hits per round: their slot reads are issued together, the appends follow in hit order
-            for (int t = 0; t < mh; t += GCS_LBUILD_P2U) {
-                unsigned kk[GCS_LBUILD_P2U];
-                int ee[GCS_LBUILD_P2U];
-#pragma unroll
-                for (int u = 0; u < GCS_LBUILD_P2U; ++u) {
-                    unsigned b;
-                    asm("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(m));
-                    kk[u] = min(b ^ 7u, (unsigned)kSub);
-                    m &= m - 1u;
-                    ee[u] = reinterpret_cast<const int*>(my_cand)[4 * kSub + min(kk[u], (unsigned)kSub - 1u)];
-                }
-#pragma unroll
-                for (int u = 0; u < GCS_LBUILD_P2U; ++u) {
-                    if (kk[u] < (unsigned)kSub && lvalid && ee[u] != s) {
-                        if (*lcnt < a.list_cap) seg[(size_t)(*lcnt) * a.list_stride] = (LE)ee[u];
-                        *lcnt += 1;
-                    }
-                }
-            }
-            if (false)
-#endif
             for (int t = 0; t < mh; ++t) {
                 unsigned b;
                 asm("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(m));
                 const unsigned k = min(b ^ 7u, (unsigned)kSub);
                 m &= m - 1u;
                 if (k < (unsigned)kSub && lvalid) {
-                    const int e = GCS_LBUILD_PK ? reinterpret_cast<const int*>(my_cand)[4 * kSub + k]
-                                                : __float_as_int(my_cand[2 * k + 1].z);  // the partner's sorted slot
+                    const int e = reinterpret_cast<const int*>(my_cand)[4 * kSub + k];  // the partner's sorted slot
                     if (e != s) {
                         if (*lcnt < a.list_cap) seg[(size_t)(*lcnt) * a.list_stride] = (LE)e;
                         *lcnt += 1;
@@ -2587,20 +2510,8 @@ __global__ __launch_bounds__(256) void k_tail(DevCtx* ctx, ForceArgs a, int fblo
 #ifndef GCS_LIST_UNROLL
 #define GCS_LIST_UNROLL 8  // list entries per batch of the pair loop
 #endif
-#ifndef GCS_LIST_PIPE
-#define GCS_LIST_PIPE 0  // 1: two batches in flight (the next batch's gathers overlap this batch's arithmetic)
-#endif
-#ifndef GCS_LIST_TAIL_ROWS
-#define GCS_LIST_TAIL_ROWS 4  // partial rows per thread per round trip of the final workgroup's reduction
-#endif
 #ifndef GCS_LIST_WAVES_PER_EU
-#define GCS_LIST_WAVES_PER_EU 4  // k_lstep occupancy target (VGPR cap 512 / waves): 4 -> <= 128
-#endif
-#ifndef GCS_LIST_XTILE
-#define GCS_LIST_XTILE 1  // 1: the next tile's slot loads are issued before this tile's work (grid-stride tiles)
-#endif
-#ifndef GCS_LIST_GROUP_REDUCE
-#define GCS_LIST_GROUP_REDUCE 0  // 1: each group's last workgroup reduces its group's rows; the final one, 8 group rows
+#define GCS_LIST_WAVES_PER_EU 5  // k_lstep occupancy target (VGPR cap 512 / waves): 5 -> <= 96, no spills
 #endif
 #ifndef GCS_LIST_BOND_BATCH
 #define GCS_LIST_BOND_BATCH 4  // bond CSR entries whose loads are issued together in the particle-local terms
@@ -2662,129 +2573,139 @@ __device__ __forceinline__ ListTailIn list_tail_load(const DevCtx* ctx, const Fo
     return t;
 }
 
-__device__ void list_tail_apply(DevCtx* ctx, const ForceArgs& a, const ListTailIn& in, const double* tot,
-                                const float* bb, float ld, float lf, int apply_sched)
+// the launch's totals (list_totals)
+struct ListTotals {
+    double react[6];  // wall reactions in[3], out[3]
+    double nbr;       // neighbour count (stats launches)
+    long long nfb;    // fallback particles
+    float ld;         // largest displacement from the build
+    float bb[6];      // bbox lo[3], hi[3] (bbox launches)
+};
+
+// launch flags of k_lstep
+constexpr int kLFlagSched = 1;  // apply the device schedule (gcs_schedule)
+constexpr int kLFlagBBox = 2;   // the next step rebuilds: reduce the bounding box of the new positions -> its cell grid
+constexpr int kLFlagStats = 4;  // reduce the neighbour count (diagnostics: ctx->neighbors)
+
+__device__ void list_tail_apply(DevCtx* ctx, const ForceArgs& a, const ListTailIn& in, const ListTotals& t, int flags)
 {
-    const double s_flags = in.s_flags, s_dt = in.s_dt, s_cs0 = in.s_cs0, s_csTau = in.s_csTau, s_bs0 = in.s_bs0,
-                 s_bsTau = in.s_bsTau, s_muW = in.s_muW;
-    const double* s_k = in.s_k;
-    const long long c_step = in.c_step, c_cursor = in.c_cursor, c_fb = in.c_fb;
-    const int c_parity = in.c_parity;
-    const double c_time = in.c_time, c_cs = in.c_cs, c_bs = in.c_bs;
-    const double* c_w = in.c_w;
+    const long long step = in.c_step + 1;
     for (int k = 0; k < 3; ++k) {
-        ctx->react_in[k] = tot[k];
-        ctx->react_out[k] = tot[3 + k];
-        ctx->bbox_lo[k] = bb[k];
-        ctx->bbox_hi[k] = bb[3 + k];
+        ctx->react_in[k] = t.react[k];
+        ctx->react_out[k] = t.react[3 + k];
     }
-    ctx->max_drift = tot[6];
-    ctx->neighbors = tot[7] / (double)a.n;
-    ctx->ldisp = ld;
-    ctx->lfallback = c_fb + (long long)lf;
-    const long long step = c_step + 1;
+    if (flags & kLFlagStats) ctx->neighbors = t.nbr / (double)a.n;
+    ctx->ldisp = t.ld;
+    ctx->lfallback = in.c_fb + t.nfb;
     ctx->step = step;
-    ctx->parity = c_parity ^ 1;
-    if (a.noise_mode == GCS_NOISE_INJECTED) ctx->noise_cursor = c_cursor + 1;
-    double time = c_time, cs = c_cs, bs = c_bs;
-    if (apply_sched) {
-        const int flags = (int)s_flags;
-        const double dt = s_dt;
-        if (flags & 1) ctx->time = time = (double)step * dt;
-        if (flags & 2) {
-            ctx->cs = cs = 1.0 - (1.0 - s_cs0) * exp(-(time / s_csTau));
-            ctx->bs = bs = 1.0 - (1.0 - s_bs0) * exp(-(time / s_bsTau));
+    ctx->parity = in.c_parity ^ 1;
+    if (a.noise_mode == GCS_NOISE_INJECTED) ctx->noise_cursor = in.c_cursor + 1;
+    double time = in.c_time, cs = in.c_cs;
+    if (flags & kLFlagSched) {
+        const int sf = (int)in.s_flags;
+        const double dt = in.s_dt;
+        if (sf & 1) ctx->time = time = (double)step * dt;
+        if (sf & 2) {
+            ctx->cs = cs = 1.0 - (1.0 - in.s_cs0) * exp(-(time / in.s_csTau));
+            ctx->bs = 1.0 - (1.0 - in.s_bs0) * exp(-(time / in.s_bsTau));
         }
-        if (flags & 4) {
+        if (sf & 4) {
             for (int k = 0; k < 3; ++k) {
                 double net = 0.0;
-                net += tot[k] + tot[3 + k];
-                net -= s_k[k] * c_w[k];
-                ctx->wall[k] = c_w[k] + dt * s_muW * net;
+                net += t.react[k] + t.react[3 + k];
+                net -= in.s_k[k] * in.c_w[k];
+                ctx->wall[k] = in.c_w[k] + dt * in.s_muW * net;
             }
         }
     }
-    (void)bs;
-    ctx->grid = make_grid(bb, bb + 3, pair_cutoff(a, cs) + a.list_skin, a.ncell_max, kPairFx);
+    if (flags & kLFlagBBox) {  // the grid the next step's rebuild bins with (cutoff at the new core scale + skin)
+        for (int k = 0; k < 3; ++k) {
+            ctx->bbox_lo[k] = t.bb[k];
+            ctx->bbox_hi[k] = t.bb[3 + k];
+        }
+        ctx->grid = make_grid(t.bb, t.bb + 3, pair_cutoff(a, cs) + a.list_skin, a.ncell_max, kPairFx);
+    }
 }
 
-// One workgroup's reduction of partial rows (force row: 8 floats, bbox row: 8 floats) in a fixed order: thread t takes
-// rows first + stride * (t + k * blockDim), lanes meet in wave butterflies, waves in index order (thread 0 returns).
-// The rows were stored write-through by other workgroups of this launch: sc1 loads.
-__device__ void list_reduce_rows(const ForceArgs& a, int first, int stride, int count, double* tot, float* bb,
-                                 float& ld, float& lf)
+// The list step's launch accumulators (a.lticket + kListAccBase, one 128-B line per slot; identities between
+// launches), one set per group of workgroups g = b % 8 (a device-scope atomic word takes ~11 ns per arrival: a
+// single set would queue all ~1000 workgroups of a C2 launch on each word).  Integer atomics only: the totals do
+// not depend on the arrival order, so runs stay bitwise reproducible.
+//   0-5   wall reactions in[3], out[3]   int64 fixed point (2^-24), added
+//   6     neighbour count                integer, added (stats launches)
+//   7     max displacement from the build (>= 0): float bits, atomic max
+//   8     fallback particles             integer, added
+//   9-11  bbox lo, 12-14 bbox hi         order-preserving integer image of the float, atomic min / max (bbox launches)
+//   15    a reaction whose fixed-point image would not fit (non-finite or > 2^38): the totals carry a NaN reaction, as
+//         a float sum would
+constexpr double kAccScale = 16777216.0;  // 2^24
+constexpr int kAccWords = kListAccSlots + 1;  // slots + the overflow flag, per group
+__device__ __forceinline__ unsigned ordered_bits(float v)
 {
-    __shared__ double s_red[kMaxListWaves][8];
-    __shared__ float s_bb[kMaxListWaves][8];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_force, 0, 0x7fffffff, 0x00020000);
-    const auto rb = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_bbox, 0, 0x7fffffff, 0x00020000);
-    const float big = 3.0e38f;
-    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    float b[8] = {big, big, big, -big, -big, -big, 0.f, 0.f};
-    // kR rows per thread per round trip (all loads issued before any is used); rows past count read as the
-    // identity (the buffer range check returns 0 past the end: zero sums, and the bbox uses the guarded rows)
-    constexpr int kR = GCS_LIST_TAIL_ROWS;
-    for (int k0 = tid; k0 < count; k0 += kR * blockDim.x) {
-      float4 F0[kR], F1[kR], G0[kR], G1[kR];
-#pragma unroll
-      for (int r = 0; r < kR; ++r) {
-          const int k = k0 + r * blockDim.x;
-          const int off = (first + stride * min(k, count - 1)) * 32;
-          F0[r] = ld_sc1_f4(rf, off);
-          F1[r] = ld_sc1_f4(rf, off + 16);
-          G0[r] = ld_sc1_f4(rb, off);
-          G1[r] = ld_sc1_f4(rb, off + 16);
-      }
-#pragma unroll
-      for (int r = 0; r < kR; ++r) {
-        const bool ok = k0 + r * (int)blockDim.x < count;
-        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f), lo4 = make_float4(big, big, big, -big),
-                     hi4 = make_float4(-big, -big, 0.f, 0.f);
-        const float4 f0 = ok ? F0[r] : z4, f1 = ok ? F1[r] : z4, g0 = ok ? G0[r] : lo4, g1 = ok ? G1[r] : hi4;
-        acc[0] += f0.x;
-        acc[1] += f0.y;
-        acc[2] += f0.z;
-        acc[3] += f0.w;
-        acc[4] += f1.x;
-        acc[5] += f1.y;
-        acc[6] = fmax(acc[6], (double)f1.z);
-        acc[7] += f1.w;
-        b[0] = fminf(b[0], g0.x);
-        b[1] = fminf(b[1], g0.y);
-        b[2] = fminf(b[2], g0.z);
-        b[3] = fmaxf(b[3], g0.w);
-        b[4] = fmaxf(b[4], g1.x);
-        b[5] = fmaxf(b[5], g1.y);
-        b[6] = fmaxf(b[6], g1.z);
-        b[7] += g1.w;
-      }
+    const unsigned b = __float_as_uint(v);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float from_ordered(unsigned o)
+{
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+__device__ __forceinline__ unsigned long long* acc_slot(unsigned* base, int k)
+{
+    return reinterpret_cast<unsigned long long*>(base + 32 * k);
+}
+// fold one value into slot k of a group's accumulators (one lane per slot)
+__device__ __forceinline__ void acc_fold(unsigned* base, int k, float v)
+{
+    unsigned long long* w = acc_slot(base, k);
+    unsigned* w32 = reinterpret_cast<unsigned*>(w);
+    if (k < 6) {
+        const double d = (double)v * kAccScale;
+        if (fabs(d) < 0x1p62)
+            __hip_atomic_fetch_add(w, (unsigned long long)__double2ll_rn(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            __hip_atomic_fetch_or(reinterpret_cast<unsigned*>(acc_slot(base, kListAccSlots)), 1u, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+    } else if (k == 6 || k == 8) {
+        __hip_atomic_fetch_add(w, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (k == 7) {
+        __hip_atomic_fetch_max(w32, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (k < 12) {
+        __hip_atomic_fetch_min(w32, ordered_bits(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        __hip_atomic_fetch_max(w32, ordered_bits(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = (k == 6) ? wave_total_max_d(acc[k]) : wave_total_sum_d(acc[k]);
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        b[k] = (k < 3) ? wave_total_min_f(b[k]) : (k < 7 ? wave_total_max_f(b[k]) : (float)wave_total_sum_d((double)b[k]));
-    if (lane == 0)
-        for (int k = 0; k < 8; ++k) {
-            s_red[wave][k] = acc[k];
-            s_bb[wave][k] = b[k];
-        }
+}
+// the final workgroup (all threads): read every group's accumulators (device-coherent loads), combine them (integer
+// sums, min, max: independent of the order) and reset them for the next launch; thread 0 gets the totals
+__device__ void list_totals(unsigned* base, int ngroups, ListTotals& t)
+{
+    __shared__ unsigned long long s_acc[8 * kAccWords];
+    const int tid = threadIdx.x;
+    for (int q = tid; q < ngroups * kAccWords; q += blockDim.x) {
+        unsigned long long* w = acc_slot(base, q);
+        s_acc[q] = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(w, list_acc_identity(q % kAccWords), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     __syncthreads();
-    if (tid == 0) {
-        for (int k = 0; k < 8; ++k) {
-            tot[k] = s_red[0][k];
-            if (k < 6) bb[k] = s_bb[0][k];
-        }
-        ld = s_bb[0][6];
-        lf = s_bb[0][7];
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
-            for (int k = 0; k < 8; ++k) tot[k] = (k == 6) ? fmax(tot[k], s_red[w][k]) : tot[k] + s_red[w][k];
-            for (int k = 0; k < 6; ++k) bb[k] = (k < 3) ? fminf(bb[k], s_bb[w][k]) : fmaxf(bb[k], s_bb[w][k]);
-            ld = fmaxf(ld, s_bb[w][6]);
-            lf += s_bb[w][7];
+    if (tid != 0) return;
+    unsigned long long v[kAccWords];
+    for (int k = 0; k < kAccWords; ++k) v[k] = s_acc[k];
+    for (int g = 1; g < ngroups; ++g) {
+        const unsigned long long* x = s_acc + g * kAccWords;
+        for (int k = 0; k < kAccWords; ++k) {
+            if (k <= 6 || k == 8) v[k] += x[k];
+            else if (k >= 9 && k < 12) v[k] = min((unsigned)v[k], (unsigned)x[k]);
+            else if (k == kListAccSlots) v[k] |= x[k];
+            else v[k] = max((unsigned)v[k], (unsigned)x[k]);
         }
     }
+    const bool bad = (v[kListAccSlots] & 1ull) != 0;
+    for (int k = 0; k < 6; ++k) t.react[k] = bad ? __longlong_as_double(0x7ff8000000000000ll)
+                                                  : (double)(long long)v[k] / kAccScale;
+    t.nbr = (double)v[6];
+    t.ld = __uint_as_float((unsigned)v[7]);
+    t.nfb = (long long)v[8];
+    for (int k = 0; k < 6; ++k) t.bb[k] = from_ordered((unsigned)v[9 + k]);
 }
 
 #ifndef GCS_LBUILD_GROUPS
@@ -2888,39 +2809,6 @@ __device__ __forceinline__ void list_pair(float xi, float yi, float zi, float4 q
     nbr += in ? 1.f : 0.f;
 }
 
-#ifndef GCS_LIST_PK
-#define GCS_LIST_PK 0  // 1: the pair loop evaluates entries two at a time in packed fp32 (list_pair2; same bits)
-#endif
-#if GCS_LIST_PK
-// list_pair for two entries: each component follows list_pair's operations in its order (v_pk_* per pair of
-// entries), and the forces are accumulated entry 0 then entry 1 as two list_pair calls would
-__device__ __forceinline__ void list_pair2(float xi, float yi, float zi, float4 q0, float4 q1, float2 t0, float2 t1,
-                                           float ahi, float bhi, float kA, float kB, float k2a, float k2b, float rc2,
-                                           bool real0, bool real1, float& fx, float& fy, float& fz, float& nbr)
-{
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    const f2 dx = f2{xi, xi} - f2{q0.x, q1.x}, dy = f2{yi, yi} - f2{q0.y, q1.y}, dz = f2{zi, zi} - f2{q0.z, q1.z};
-    const f2 r2 = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
-    const f2 one = {1.f, 1.f}, zero = {0.f, 0.f};
-    const f2 ga = __builtin_elementwise_max(__builtin_elementwise_fma(f2{-k2a, -k2a}, r2, one), zero);
-    const f2 tt = r2 * f2{k2b, k2b};
-    const f2 t2 = tt * tt;
-    const f2 gb = __builtin_elementwise_max(__builtin_elementwise_fma(-t2, t2, one), zero);
-    const f2 A = __builtin_elementwise_fma(f2{kA, kA}, f2{t0.x, t1.x}, f2{ahi, ahi});
-    const f2 B = __builtin_elementwise_fma(f2{kB, kB}, f2{t0.y, t1.y}, f2{bhi, bhi});
-    const f2 c = __builtin_elementwise_fma(A, ga * ga, B * (gb * gb * t2 * tt));
-    const bool in0 = real0 && r2.x < rc2, in1 = real1 && r2.y < rc2;
-    const float c0 = in0 ? c.x : 0.f, c1 = in1 ? c.y : 0.f;
-    fx = fmaf(c0, dx.x, fx);
-    fy = fmaf(c0, dy.x, fy);
-    fz = fmaf(c0, dz.x, fz);
-    nbr += in0 ? 1.f : 0.f;
-    fx = fmaf(c1, dx.y, fx);
-    fy = fmaf(c1, dy.y, fy);
-    fz = fmaf(c1, dz.y, fz);
-    nbr += in1 ? 1.f : 0.f;
-}
-#endif
 
 __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 {
@@ -2930,342 +2818,275 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 }
 
 
-template <typename LE, int kListWaves, bool CT>
 #ifndef GCS_LIST_WAVES_PER_EU_CT
-#define GCS_LIST_WAVES_PER_EU_CT GCS_LIST_WAVES_PER_EU  // the contact-step instantiation (CT)
+#define GCS_LIST_WAVES_PER_EU_CT 4  // the contact-step instantiation (CT, 1 launch in 20): 4 -> <= 128, no spills
 #endif
-__global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu(CT ? GCS_LIST_WAVES_PER_EU_CT : GCS_LIST_WAVES_PER_EU))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int apply_sched)
+// One list step: ONE tile of 64 consecutive slots per workgroup (the launch has one workgroup per tile), W waves.
+// Phases, with nothing but LDS carried from one to the next (every wave's registers are free for the next phase):
+//   1. slot loads: current position (.w = particle | class << 24), build position, list count, the first kU
+//      entries of the wave's segment; the local-terms wave (W - 1) also the slot's constants and bond row
+//   2. wave W - 1: the particle-local terms (bond CSR, droplet, bending, tethers, point sources, walls) -> LDS
+//   3. every wave: its list segment, kU entries per batch (the next batch's entries in flight), the exact search
+//      for the lanes the lists may not cover; forces + neighbour counts -> LDS.  Wave 1: the Philox noise -> LDS
+//   4. (barrier) wave 0: sum the waves' forces, integrate, store; the launch statistics it owns (largest
+//      displacement, fallbacks; bbox / neighbour count on flagged launches) into the group's accumulators.
+//      Waves 1.. (in parallel): the wall reactions into the accumulators
+//   5. (barrier) the two-level ticket; the final workgroup reads the accumulators and advances the context
+template <typename LE, int W, bool CT>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS_LIST_WAVES_PER_EU_CT : GCS_LIST_WAVES_PER_EU))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int flags)
 {
-    __shared__ float red[kListWaves][4][kTile];
+    __shared__ float red[W][4][kTile];
     __shared__ float4 s_locf[kTile], s_locr[kTile], s_loco[kTile], s_noise[kTile];
     __shared__ float2 s_tab[kMaxTypes];
-    __shared__ float s_pr[kForcePartials + kBBoxStride];  // force partials, then bbox lo/hi, max displacement, fallbacks
-    __shared__ int s_last;
+    __shared__ int s_last, s_final;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = uniform(tid >> 6);
-    // GCS_DEBUG_TIMES: per workgroup 8 wall-clock stamps (start, wave 0: pair loop start / end, reduced,
-    // integrated (first tile), workgroup end, ticket taken, tail end)
+    // GCS_DEBUG_TIMES: per workgroup 8 wall-clock stamps (start, wave 0: pair loop start / end, reduced, integrated,
+    // workgroup end, ticket taken, tail end)
     unsigned long long* const dbg = a.dbg_times ? a.dbg_times + 8 * blockIdx.x : nullptr;
     if (dbg && tid == 0) dbg[0] = wall_clock64();
-    for (int t = tid; t < a.ntypes; t += blockDim.x) s_tab[t] = a.type_ab[t];
-    if (tid == 0) {
-        for (int k = 0; k < kForcePartials; ++k) s_pr[k] = 0.f;
-        for (int k = 0; k < 3; ++k) {
-            s_pr[kForcePartials + k] = 3.0e38f;
-            s_pr[kForcePartials + 3 + k] = -3.0e38f;
-        }
-        s_pr[kForcePartials + 6] = 0.f;
-        s_pr[kForcePartials + 7] = 0.f;
-    }
     const int n = a.n;
-    const float cs = (float)ctx->cs;
-    const float scale = a.pair_scaled ? cs : 1.f;
-    const float sa = a.pa_sig * scale, sbb = a.pb_sig * scale;
-    const float k2a = 1.f / (sa * sa), k2b = 1.f / (sbb * sbb);
-    const float kA = 0.5f * 6.f * a.pa_eps * k2a, kB = 0.5f * 24.f * a.pb_eps * k2b;
-    const float rc = pair_cutoff(a, ctx->cs), rc2 = rc * rc;
-    const float D = ctx->ldisp;
-    // a particle whose own displacement exceeds this may miss a partner in its list (0.999: fp32 margin)
-    const float slack = 0.999f * a.list_skin - D - fmaxf(rc - ctx->lrc_b, 0.f);
-    // contacts (CT): the lists must cover the contact distance; a particle whose list does not is searched for its
-    // contacts only (its forces take exactly the path they take without contacts: identical bits)
-    const float rcc = CT ? fmaxf(rc, sqrtf(a.contact_d2)) : rc;
-    const float slack_c = 0.999f * a.list_skin - D - fmaxf(rcc - ctx->lrc_b, 0.f);
+    const int tile = xcd_block(blockIdx.x, gridDim.x);
+    const int s = tile * kTile + lane;
+    const bool valid = s < n;
+    const int sl = valid ? s : n - 1;
     const int par = a.par_hint >= 0 ? a.par_hint : ctx->parity;
-    float4* __restrict__ pn = par ? a.pos0 : a.pos1;  // particle order (bonded partners read ctx->parity's)
     const float4* __restrict__ qc = par ? a.psort1 : a.psort0;  // slot order (pair partners)
-    float4* __restrict__ qn = par ? a.psort0 : a.psort1;
     const int cap = a.list_cap;
     const size_t stride = (size_t)a.list_stride;
     constexpr int kU = GCS_LIST_UNROLL;
     constexpr int kIdx = (1 << kListIndexBits) - 1;
-    // software-pipelined by one tile: a tile's slot loads (one round trip, nothing depends on anything but the slot)
-    // are issued before the previous tile's work and, for the first tile, before the type-table barrier
-    // tiles: 64 consecutive slots (the lists are per slot; no cell-row structure is needed here)
-    const int tile0 = xcd_block(blockIdx.x, gridDim.x);
-    int tile = tile0;
-    float4 n_pi = make_float4(0.f, 0.f, 0.f, 0.f), n_pb = n_pi, n_km = n_pi;
-    int2 n_br = make_int2(0, 0);
-    int n_cw = 0, n_e[kU];
-    auto load_tile = [&](int t, bool first) {
-        const int sl = min(t * kTile + lane, n - 1);
-        n_pi = qc[sl];    // current position, .w = particle | class << 24
-        n_pb = a.spos[sl];  // build position
-        if (first && wave == kListWaves - 1) {  // the local-terms wave: the slot's constants and bond row (the
-            n_km = a.skmu[sl];                  // first tile only: held across a pair loop they would spill)
-            n_br = a.sbrow[sl];
-        }
-        n_cw = a.lcount[(size_t)wave * stride + sl];
-        const LE* __restrict__ seg = reinterpret_cast<const LE*>(a.list) + (size_t)wave * cap * stride + sl;
-#pragma unroll
-        for (int u = 0; u < kU; ++u) n_e[u] = seg[(size_t)u * stride];  // list_cap >= kU: in bounds
-    };
-    if (tile * kTile < n) load_tile(tile, true);
-    __syncthreads();
-    for (; tile * kTile < n; tile += gridDim.x) {
-        const int s = tile * kTile + lane;
-        const bool valid = s < n;
-        const int sl = valid ? s : n - 1;
-        const float4 pi = n_pi, pb = n_pb;
-        const bool first = tile == tile0;
-        const int cw = n_cw;
-        int e[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) e[u] = n_e[u];
-#if GCS_LIST_XTILE
-        if ((tile + (int)gridDim.x) * kTile < n) load_tile(tile + gridDim.x, false);
-#endif
-        const LE* __restrict__ seg = reinterpret_cast<const LE*>(a.list) + (size_t)wave * cap * stride + sl;
-        const int pk = __float_as_int(pi.w);
-        const int i = pk & kIdx;
-        const float2 own = s_tab[(unsigned)pk >> kListIndexBits];
-        const float ex = pi.x - pb.x, ey = pi.y - pb.y, ez = pi.z - pb.z;
-        const float di = sqrtf(fmaf(ez, ez, fmaf(ey, ey, ex * ex)));
-        const bool fb = valid && (di > slack || (cw & kListOverflow) != 0);
-        const bool fbc = CT && valid && (di > slack_c || (cw & kListOverflow) != 0);  // implies fb's condition
+    const LE* __restrict__ seg = reinterpret_cast<const LE*>(a.list) + (size_t)wave * cap * stride + sl;
 
-        if (wave == kListWaves - 1) {  // the particle-local terms first (a dependent-gather chain), parked in LDS
-            const float4 km = first ? n_km : a.skmu[sl];
-            const int2 erow = first ? n_br : a.sbrow[sl];
-            float lfx = 0.f, lfy = 0.f, lfz = 0.f, en[kEnergyKinds];
-            float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
-            local_terms<kModeStep, GCS_LIST_BOND_BATCH>(ctx, a, i, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout,
-                                                        erow);
-            s_locf[lane] = make_float4(lfx, lfy, lfz, km.x);
-            s_locr[lane] = make_float4(rin[0], rin[1], rin[2], 0.f);
-            s_loco[lane] = make_float4(rout[0], rout[1], rout[2], 0.f);
-        }
+    // 1. slot loads (one round trip; the type table's load beside them)
+    for (int t = tid; t < a.ntypes; t += blockDim.x) s_tab[t] = a.type_ab[t];
+    const float4 pi = qc[sl];
+    const float4 pb = a.spos[sl];
+    const int cw = a.lcount[(size_t)wave * stride + sl];
+    int e[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) e[u] = seg[(size_t)u * stride];  // list_cap >= kU: in bounds
+    const float cs = (float)ctx->cs;
+    const float D = ctx->ldisp;
+    const float lrc_b = ctx->lrc_b;
+    __syncthreads();  // s_tab
 
-        float fx = 0.f, fy = 0.f, fz = 0.f, nbr = 0.f;
-        const float ahi = kA * own.x, bhi = kB * own.y;
-        const bool stamp = dbg && tid == 0 && tile == tile0;
-        if (stamp) dbg[1] = wall_clock64();
-        if (a.has_pair) {
-            const int cnt = (valid && !fb) ? min(cw & kListCountMask, cap) : 0;
-            const int kmax = uniform(wave_max_int(cnt));
-#if GCS_LIST_PIPE
-            // two batches in flight: the next batch's gathers are issued before this batch's arithmetic, the
-            // entries of the batch after that before those gathers
-            float4 q[kU], qn[kU];
-            int en_[kU];
+    const int pk = __float_as_int(pi.w);
+    const int i = pk & kIdx;
+    const float scale = a.pair_scaled ? cs : 1.f;
+    const float sa = a.pa_sig * scale, sbb = a.pb_sig * scale;
+    const float k2a = 1.f / (sa * sa), k2b = 1.f / (sbb * sbb);
+    const float kA = 0.5f * 6.f * a.pa_eps * k2a, kB = 0.5f * 24.f * a.pb_eps * k2b;
+    const float rc = pair_cutoff(a, (double)cs), rc2 = rc * rc;
+    // a particle whose own displacement exceeds this may miss a partner in its list (0.999: fp32 margin)
+    const float slack = 0.999f * a.list_skin - D - fmaxf(rc - lrc_b, 0.f);
+    const float ex = pi.x - pb.x, ey = pi.y - pb.y, ez = pi.z - pb.z;
+    const float di = sqrtf(fmaf(ez, ez, fmaf(ey, ey, ex * ex)));
+    const bool fb = valid && (di > slack || (cw & kListOverflow) != 0);
+    // contacts (CT): the lists must cover the contact distance; a particle whose list does not is searched for its
+    // contacts only (its forces take exactly the path they take without contacts: identical bits)
+    const float rcc = CT ? fmaxf(rc, sqrtf(a.contact_d2)) : rc;
+    const bool fbc = CT && valid && (di > 0.999f * a.list_skin - D - fmaxf(rcc - lrc_b, 0.f) || (cw & kListOverflow) != 0);
+
+    // 2. the particle-local terms (a dependent-gather chain: first, on the last wave), parked in LDS
+    if (wave == W - 1) {
+        const float4 km = a.skmu[sl];
+        const int2 erow = a.sbrow[sl];
+        float lfx = 0.f, lfy = 0.f, lfz = 0.f, en[kEnergyKinds];
+        float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
+        local_terms<kModeStep, GCS_LIST_BOND_BATCH>(ctx, a, i, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout, erow);
+        s_locf[lane] = make_float4(lfx, lfy, lfz, km.x);
+        s_locr[lane] = make_float4(valid ? rin[0] : 0.f, valid ? rin[1] : 0.f, valid ? rin[2] : 0.f, 0.f);
+        s_loco[lane] = make_float4(valid ? rout[0] : 0.f, valid ? rout[1] : 0.f, valid ? rout[2] : 0.f, 0.f);
+    }
+
+    // 3. the wave's list segment
+    float fx = 0.f, fy = 0.f, fz = 0.f, nbr = 0.f;
+    const float2 own = s_tab[(unsigned)pk >> kListIndexBits];
+    const float ahi = kA * own.x, bhi = kB * own.y;
+    if (dbg && tid == 0) dbg[1] = wall_clock64();
+    if (a.has_pair) {
+        const int cnt = (valid && !fb) ? min(cw & kListCountMask, cap) : 0;
+        const int kmax = uniform(wave_max_int(cnt));
+        for (int k0 = 0; k0 < kmax; k0 += kU) {
+            int en_[kU];  // the next batch's entries, in flight during this batch
 #pragma unroll
-            for (int u = 0; u < kU; ++u) q[u] = qc[(u < cnt) ? e[u] : sl];
+            for (int u = 0; u < kU; ++u) en_[u] = (k0 + kU + u < kmax) ? seg[(size_t)(k0 + kU + u) * stride] : 0;
+            float4 q[kU];
 #pragma unroll
-            for (int u = 0; u < kU; ++u) en_[u] = (kU + u < kmax) ? seg[(size_t)(kU + u) * stride] : 0;
-            for (int k0 = 0; k0 < kmax; k0 += kU) {
+            for (int u = 0; u < kU; ++u) q[u] = qc[(k0 + u < cnt) ? e[u] : sl];
 #pragma unroll
-                for (int u = 0; u < kU; ++u) qn[u] = qc[(k0 + kU + u < cnt) ? en_[u] : sl];
+            for (int u = 0; u < kU; ++u)
+                list_pair(pi.x, pi.y, pi.z, q[u], s_tab[(unsigned)__float_as_int(q[u].w) >> kListIndexBits], ahi, bhi,
+                          kA, kB, k2a, k2b, rc2, k0 + u < cnt, fx, fy, fz, nbr);
+            if constexpr (CT) {
 #pragma unroll
                 for (int u = 0; u < kU; ++u)
-                    en_[u] = (k0 + 2 * kU + u < kmax) ? seg[(size_t)(k0 + 2 * kU + u) * stride] : 0;
-#pragma unroll
-                for (int u = 0; u < kU; ++u)
-                    list_pair(pi.x, pi.y, pi.z, q[u], s_tab[(unsigned)__float_as_int(q[u].w) >> kListIndexBits], ahi,
-                              bhi, kA, kB, k2a, k2b, rc2, k0 + u < cnt, fx, fy, fz, nbr);
-                if constexpr (CT) {
-#pragma unroll
-                    for (int u = 0; u < kU; ++u)
-                        if (!fbc && k0 + u < cnt) list_contact(a, pi, q[u], i, __float_as_int(q[u].w) & kIdx);
-                }
-#pragma unroll
-                for (int u = 0; u < kU; ++u) q[u] = qn[u];
+                    if (!fbc && k0 + u < cnt) list_contact(a, pi, q[u], i, __float_as_int(q[u].w) & kIdx);
             }
-#else
-            for (int k0 = 0; k0 < kmax; k0 += kU) {
-                int en_[kU];  // the next batch's entries, in flight during this batch
 #pragma unroll
-                for (int u = 0; u < kU; ++u)
-                    en_[u] = (k0 + kU + u < kmax) ? seg[(size_t)(k0 + kU + u) * stride] : 0;
-                float4 q[kU];
-#pragma unroll
-                for (int u = 0; u < kU; ++u) q[u] = qc[(k0 + u < cnt) ? e[u] : sl];
-#if GCS_LIST_PK
-                static_assert(kU % 2 == 0, "pairs of entries");
-#pragma unroll
-                for (int u = 0; u < kU; u += 2)
-                    list_pair2(pi.x, pi.y, pi.z, q[u], q[u + 1],
-                               s_tab[(unsigned)__float_as_int(q[u].w) >> kListIndexBits],
-                               s_tab[(unsigned)__float_as_int(q[u + 1].w) >> kListIndexBits], ahi, bhi, kA, kB, k2a,
-                               k2b, rc2, k0 + u < cnt, k0 + u + 1 < cnt, fx, fy, fz, nbr);
-#else
-#pragma unroll
-                for (int u = 0; u < kU; ++u)
-                    list_pair(pi.x, pi.y, pi.z, q[u], s_tab[(unsigned)__float_as_int(q[u].w) >> kListIndexBits], ahi,
-                              bhi, kA, kB, k2a, k2b, rc2, k0 + u < cnt, fx, fy, fz, nbr);
-#endif
-                if constexpr (CT) {
-#pragma unroll
-                    for (int u = 0; u < kU; ++u)
-                        if (!fbc && k0 + u < cnt) list_contact(a, pi, q[u], i, __float_as_int(q[u].w) & kIdx);
-                }
-#pragma unroll
-                for (int u = 0; u < kU; ++u) e[u] = en_[u];
-            }
-#endif
-            // exact search of the build's cell list for the particles the lists may not cover: a partner within rc
-            // now was within rc + D at the build.  Wave-cooperative: the wave takes its fallback lanes one at a
-            // time, its 64 lanes sweep that particle's candidate slots (the waves of the tile alternate over cell
-            // rows), and a wave sum hands the result to the particle's lane
-            unsigned long long fbm = __ballot(fb);
-            if (fbm) {
-                const Grid lg = ctx->lgrid;
-                const float R = rc + D + 1.0e-5f * (rc + D);
-                while (fbm) {
-                    const int L = __ffsll((long long)fbm) - 1;
-                    fbm &= fbm - 1ull;
-                    const float px = __shfl(pi.x, L), py = __shfl(pi.y, L), pz = __shfl(pi.z, L);
-                    const float pah = __shfl(ahi, L), pbh = __shfl(bhi, L);
-                    const int sL = uniform(__shfl(s, L));
-                    const int x0 = uniform(lgrid_cell(lg, 0, px - R)), x1 = uniform(lgrid_cell(lg, 0, px + R));
-                    const int y0 = uniform(lgrid_cell(lg, 1, py - R)), y1 = uniform(lgrid_cell(lg, 1, py + R));
-                    const int z0 = uniform(lgrid_cell(lg, 2, pz - R)), z1 = uniform(lgrid_cell(lg, 2, pz + R));
-                    float gx = 0.f, gy = 0.f, gz = 0.f, gn = 0.f;
-                    int row = 0;
-                    for (int z = z0; z <= z1; ++z)
-                        for (int y = y0; y <= y1; ++y, ++row) {
-                            if ((row % kListWaves) != wave) continue;
-                            const int base = (z * lg.n[1] + y) * lg.n[0];
-                            const int t0 = a.cstart[base + x0], t1 = a.cstart[base + x1 + 1];
-                            for (int t = t0 + lane; t < t1; t += kTile) {
-                                const float4 q = qc[t];
-                                list_pair(px, py, pz, q, s_tab[(unsigned)__float_as_int(q.w) >> kListIndexBits], pah,
-                                          pbh, kA, kB, k2a, k2b, rc2, t != sL, gx, gy, gz, gn);
-                            }
+            for (int u = 0; u < kU; ++u) e[u] = en_[u];
+        }
+        // exact search of the build's cell list for the particles the lists may not cover: a partner within rc
+        // now was within rc + D at the build.  Wave-cooperative: the wave takes its fallback lanes one at a time,
+        // its 64 lanes sweep that particle's candidate slots (the waves of the tile alternate over cell rows), and
+        // a wave sum hands the result to the particle's lane
+        unsigned long long fbm = __ballot(fb);
+        if (fbm) {
+            const Grid lg = ctx->lgrid;
+            const float R = rc + D + 1.0e-5f * (rc + D);
+            while (fbm) {
+                const int L = __ffsll((long long)fbm) - 1;
+                fbm &= fbm - 1ull;
+                const float px = __shfl(pi.x, L), py = __shfl(pi.y, L), pz = __shfl(pi.z, L);
+                const float pah = __shfl(ahi, L), pbh = __shfl(bhi, L);
+                const int sL = uniform(__shfl(s, L));
+                const int x0 = uniform(lgrid_cell(lg, 0, px - R)), x1 = uniform(lgrid_cell(lg, 0, px + R));
+                const int y0 = uniform(lgrid_cell(lg, 1, py - R)), y1 = uniform(lgrid_cell(lg, 1, py + R));
+                const int z0 = uniform(lgrid_cell(lg, 2, pz - R)), z1 = uniform(lgrid_cell(lg, 2, pz + R));
+                float gx = 0.f, gy = 0.f, gz = 0.f, gn = 0.f;
+                int row = 0;
+                for (int z = z0; z <= z1; ++z)
+                    for (int y = y0; y <= y1; ++y, ++row) {
+                        if ((row % W) != wave) continue;
+                        const int base = (z * lg.n[1] + y) * lg.n[0];
+                        const int t0 = a.cstart[base + x0], t1 = a.cstart[base + x1 + 1];
+                        for (int t = t0 + lane; t < t1; t += kTile) {
+                            const float4 q = qc[t];
+                            list_pair(px, py, pz, q, s_tab[(unsigned)__float_as_int(q.w) >> kListIndexBits], pah, pbh,
+                                      kA, kB, k2a, k2b, rc2, t != sL, gx, gy, gz, gn);
                         }
-                    gx = wave_sum(gx);
-                    gy = wave_sum(gy);
-                    gz = wave_sum(gz);
-                    gn = wave_sum(gn);
-                    if (lane == L) {
-                        fx += gx;
-                        fy += gy;
-                        fz += gz;
-                        nbr += gn;
                     }
+                gx = wave_sum(gx);
+                gy = wave_sum(gy);
+                gz = wave_sum(gz);
+                gn = wave_sum(gn);
+                if (lane == L) {
+                    fx += gx;
+                    fy += gy;
+                    fz += gz;
+                    nbr += gn;
                 }
             }
         }
-        if constexpr (CT) {
-            // contacts of the particles whose lists do not cover the contact distance: the build's cell list around
-            // the current position with radius d + D, swept by the whole wave per particle as above
-            unsigned long long fcm = __ballot(fbc);
-            if (fcm) {
-                const Grid lg = ctx->lgrid;
-                const float R = rcc + D + 1.0e-5f * (rcc + D);
-                while (fcm) {
-                    const int L = __ffsll((long long)fcm) - 1;
-                    fcm &= fcm - 1ull;
-                    const float4 pL = make_float4(__shfl(pi.x, L), __shfl(pi.y, L), __shfl(pi.z, L), 0.f);
-                    const int iL = __shfl(i, L), sL = uniform(__shfl(s, L));
-                    const int x0 = uniform(lgrid_cell(lg, 0, pL.x - R)), x1 = uniform(lgrid_cell(lg, 0, pL.x + R));
-                    const int y0 = uniform(lgrid_cell(lg, 1, pL.y - R)), y1 = uniform(lgrid_cell(lg, 1, pL.y + R));
-                    const int z0 = uniform(lgrid_cell(lg, 2, pL.z - R)), z1 = uniform(lgrid_cell(lg, 2, pL.z + R));
-                    int row = 0;
-                    for (int z = z0; z <= z1; ++z)
-                        for (int y = y0; y <= y1; ++y, ++row) {
-                            if ((row % kListWaves) != wave) continue;
-                            const int base = (z * lg.n[1] + y) * lg.n[0];
-                            const int t0 = a.cstart[base + x0], t1 = a.cstart[base + x1 + 1];
-                            for (int t = t0 + lane; t < t1; t += kTile) {
-                                const float4 q = qc[t];
-                                if (t != sL) list_contact(a, pL, q, iL, __float_as_int(q.w) & kIdx);
-                            }
+    }
+    if constexpr (CT) {
+        // contacts of the particles whose lists do not cover the contact distance: the build's cell list around
+        // the current position with radius d + D, swept by the whole wave per particle as above
+        unsigned long long fcm = __ballot(fbc);
+        if (fcm) {
+            const Grid lg = ctx->lgrid;
+            const float R = rcc + D + 1.0e-5f * (rcc + D);
+            while (fcm) {
+                const int L = __ffsll((long long)fcm) - 1;
+                fcm &= fcm - 1ull;
+                const float4 pL = make_float4(__shfl(pi.x, L), __shfl(pi.y, L), __shfl(pi.z, L), 0.f);
+                const int iL = __shfl(i, L), sL = uniform(__shfl(s, L));
+                const int x0 = uniform(lgrid_cell(lg, 0, pL.x - R)), x1 = uniform(lgrid_cell(lg, 0, pL.x + R));
+                const int y0 = uniform(lgrid_cell(lg, 1, pL.y - R)), y1 = uniform(lgrid_cell(lg, 1, pL.y + R));
+                const int z0 = uniform(lgrid_cell(lg, 2, pL.z - R)), z1 = uniform(lgrid_cell(lg, 2, pL.z + R));
+                int row = 0;
+                for (int z = z0; z <= z1; ++z)
+                    for (int y = y0; y <= y1; ++y, ++row) {
+                        if ((row % W) != wave) continue;
+                        const int base = (z * lg.n[1] + y) * lg.n[0];
+                        const int t0 = a.cstart[base + x0], t1 = a.cstart[base + x1 + 1];
+                        for (int t = t0 + lane; t < t1; t += kTile) {
+                            const float4 q = qc[t];
+                            if (t != sL) list_contact(a, pL, q, iL, __float_as_int(q.w) & kIdx);
                         }
-                }
+                    }
             }
         }
-        if (stamp) dbg[2] = wall_clock64();
-        red[wave][0][lane] = fx;
-        red[wave][1][lane] = fy;
-        red[wave][2][lane] = fz;
-        red[wave][3][lane] = nbr;
-        if (wave == (kListWaves > 1 ? 1 : 0)) {  // the noise (depends on the particle and the step only) off wave 0's path
-            float n0, n1, n2;
-            noise3(a, ctx, i, n0, n1, n2);
-            s_noise[lane] = make_float4(n0, n1, n2, 0.f);
-        }
-        __syncthreads();
-        if (stamp) dbg[3] = wall_clock64();
-        if (wave == 0) {
-            fx = red[0][0][lane];
-            fy = red[0][1][lane];
-            fz = red[0][2][lane];
-            nbr = red[0][3][lane];
+    }
+    if (dbg && tid == 0) dbg[2] = wall_clock64();
+    red[wave][0][lane] = fx;
+    red[wave][1][lane] = fy;
+    red[wave][2][lane] = fz;
+    red[wave][3][lane] = nbr;
+    if (wave == (W > 1 ? 1 : 0)) {  // the noise (depends on the particle and the step only) off wave 0's path
+        float n0, n1, n2;
+        noise3(a, ctx, i, n0, n1, n2);
+        s_noise[lane] = make_float4(n0, n1, n2, 0.f);
+    }
+    __syncthreads();
+    if (dbg && tid == 0) dbg[3] = wall_clock64();
+
+    // 4. integrate (wave 0) / the reactions (waves 1..)
+    const int ngroups = min((int)gridDim.x, 8);
+    const int g = blockIdx.x % ngroups;
+    unsigned* const acc = a.lticket + kListAccBase + 32 * kAccWords * g;
+    if (wave == 0) {
+        float fsx = red[0][0][lane], fsy = red[0][1][lane], fsz = red[0][2][lane], ns = red[0][3][lane];
 #pragma unroll
-            for (int w = 1; w < kListWaves; ++w) {
-                fx += red[w][0][lane];
-                fy += red[w][1][lane];
-                fz += red[w][2][lane];
-                nbr += red[w][3][lane];
-            }
-            const float4 lf = s_locf[lane], lr = s_locr[lane], lo = s_loco[lane];
-            fx += lf.x;
-            fy += lf.y;
-            fz += lf.z;
-            const float mu = lf.w;
-            float v[kForcePartials];
-            v[0] = wave_sum(valid ? lr.x : 0.f);
-            v[1] = wave_sum(valid ? lr.y : 0.f);
-            v[2] = wave_sum(valid ? lr.z : 0.f);
-            v[3] = wave_sum(valid ? lo.x : 0.f);
-            v[4] = wave_sum(valid ? lo.y : 0.f);
-            v[5] = wave_sum(valid ? lo.z : 0.f);
-            v[6] = wave_max(valid ? mu * sqrtf(fx * fx + fy * fy + fz * fz) : 0.f);
-            v[7] = wave_sum(valid ? nbr : 0.f);
-            // Euler-Maruyama: x += mu dt F + sqrt(2 T mu dt) xi
-            const float4 xi = s_noise[lane];
-            const float dt = a.timestep;
-            const float amp = sqrtf(2.f * a.temperature * mu * dt);
-            const float mdt = mu * dt;
-            const float nxp = pi.x + mdt * fx + amp * xi.x;
-            const float nyp = pi.y + mdt * fy + amp * xi.y;
-            const float nzp = pi.z + mdt * fz + amp * xi.z;
-            if (valid) {
-                pn[i] = make_float4(nxp, nyp, nzp, 0.f);
-                qn[s] = make_float4(nxp, nyp, nzp, pi.w);
-            }
-            const float gx = nxp - pb.x, gy = nyp - pb.y, gz = nzp - pb.z;
-            const float dmax = wave_max(valid ? sqrtf(fmaf(gz, gz, fmaf(gy, gy, gx * gx))) : 0.f);
-            const float nfb = wave_sum(fb ? 1.f : 0.f);
+        for (int w = 1; w < W; ++w) {
+            fsx += red[w][0][lane];
+            fsy += red[w][1][lane];
+            fsz += red[w][2][lane];
+            ns += red[w][3][lane];
+        }
+        const float4 lf = s_locf[lane];
+        fsx += lf.x;
+        fsy += lf.y;
+        fsz += lf.z;
+        const float mu = lf.w;
+        // Euler-Maruyama: x += mu dt F + sqrt(2 T mu dt) xi
+        const float4 xi = s_noise[lane];
+        const float dt = a.timestep;
+        const float amp = sqrtf(2.f * a.temperature * mu * dt);
+        const float mdt = mu * dt;
+        const float nxp = pi.x + mdt * fsx + amp * xi.x;
+        const float nyp = pi.y + mdt * fsy + amp * xi.y;
+        const float nzp = pi.z + mdt * fsz + amp * xi.z;
+        if (valid) {
+            float4* __restrict__ pn = par ? a.pos0 : a.pos1;  // particle order (bonded partners read ctx->parity's)
+            float4* __restrict__ qn = par ? a.psort0 : a.psort1;
+            pn[i] = make_float4(nxp, nyp, nzp, 0.f);
+            qn[s] = make_float4(nxp, nyp, nzp, pi.w);
+        }
+        if (dbg && tid == 0) dbg[4] = wall_clock64();
+        const float gx = nxp - pb.x, gy = nyp - pb.y, gz = nzp - pb.z;
+        const float dmax = wave_max(valid ? sqrtf(fmaf(gz, gz, fmaf(gy, gy, gx * gx))) : 0.f);
+        const float nfb = (float)__popcll(__ballot(fb));
+        float v = 0.f;  // lane k: the value of accumulator slot k this wave owns
+        if (flags & kLFlagStats) {
+            const float nt = wave_sum(valid ? ns : 0.f);
+            if (lane == 6) v = nt;
+        }
+        if (flags & kLFlagBBox) {
             const float big = 3.0e38f;
             const float l0 = wave_min(valid ? nxp : big), l1 = wave_min(valid ? nyp : big),
                         l2 = wave_min(valid ? nzp : big);
             const float h0 = wave_max(valid ? nxp : -big), h1 = wave_max(valid ? nyp : -big),
                         h2 = wave_max(valid ? nzp : -big);
-            if (lane == 0) {
-                for (int k = 0; k < kForcePartials; ++k) s_pr[k] = (k == 6) ? fmaxf(s_pr[k], v[k]) : s_pr[k] + v[k];
-                float* b = s_pr + kForcePartials;
-                b[0] = fminf(b[0], l0);
-                b[1] = fminf(b[1], l1);
-                b[2] = fminf(b[2], l2);
-                b[3] = fmaxf(b[3], h0);
-                b[4] = fmaxf(b[4], h1);
-                b[5] = fmaxf(b[5], h2);
-                b[6] = fmaxf(b[6], dmax);
-                b[7] += nfb;
-            }
-            if (stamp) dbg[4] = wall_clock64();
+            v = lane == 9 ? l0 : lane == 10 ? l1 : lane == 11 ? l2 : lane == 12 ? h0 : lane == 13 ? h1 : lane == 14 ? h2 : v;
         }
-        __syncthreads();  // red / s_loc* are reused by the next tile
+        if (lane == 7) v = dmax;
+        if (lane == 8) v = nfb;
+        const bool mine = lane == 7 || lane == 8 || ((flags & kLFlagStats) && lane == 6) ||
+                          ((flags & kLFlagBBox) && lane >= 9 && lane < 15);
+        if (mine) acc_fold(acc, lane, v);
+    } else {
+        // the wall reactions: waves 1.. take the six components in turn (W = 4: wave 1 inward, wave 2 outward)
+        const int c0 = W > 2 ? 3 * (wave - 1) : 0, c1 = W > 2 ? c0 + 3 : 6;
+        if (c0 < 6) {
+            float v = 0.f;
+            for (int c = c0; c < c1; ++c) {
+                const float4 r = c < 3 ? s_locr[lane] : s_loco[lane];
+                const float x = wave_sum((c % 3) == 0 ? r.x : (c % 3) == 1 ? r.y : r.z);
+                if (lane == c) v = x;
+            }
+            if (lane >= c0 && lane < c1) acc_fold(acc, lane, v);
+        }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's accumulator atomics are performed
+    __syncthreads();
     if (dbg && tid == 0) dbg[5] = wall_clock64();
-    // publish this workgroup's partial rows write-through, then a two-level ticket (one counter per group of
-    // workgroups b % 8, then one over the groups; a single counter serialises ~1000 returning atomics): the last
-    // workgroup of a group reduces the group's rows, the last group-reducer reduces the group rows in group order
-    // and advances the context (sc1 stores, vmcnt(0), one agent atomic per workgroup; rows read with sc1 loads)
-    const int ngroups = min((int)gridDim.x, 8);
-    const int g = blockIdx.x % ngroups;
+
+    // 5. the two-level ticket (one counter per group of workgroups b % 8, then one over the groups; a single
+    // counter serialises ~1000 returning atomics); the final workgroup reads the totals and advances the context
     const int gsize = ((int)gridDim.x - g + ngroups - 1) / ngroups;
     if (tid == 0) {
-        const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_force, 0, 0x7fffffff, 0x00020000);
-        const auto rb = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_bbox, 0, 0x7fffffff, 0x00020000);
-        const int off = blockIdx.x * 32;
-        st_sc1_f4(rf, off, make_float4(s_pr[0], s_pr[1], s_pr[2], s_pr[3]));
-        st_sc1_f4(rf, off + 16, make_float4(s_pr[4], s_pr[5], s_pr[6], s_pr[7]));
-        const float* b = s_pr + kForcePartials;
-        st_sc1_f4(rb, off, make_float4(b[0], b[1], b[2], b[3]));
-        st_sc1_f4(rb, off + 16, make_float4(b[4], b[5], b[6], b[7]));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned old = atomicAdd(&a.lticket[32 * g], 1u);
         s_last = (old == (unsigned)gsize - 1) ? 1 : 0;
         if (dbg) {
@@ -3275,25 +3096,6 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
     }
     __syncthreads();
     if (!s_last) return;
-    // the last workgroup of a group: count the group in; the last group's last workgroup is the final one
-    __shared__ int s_final;
-#if GCS_LIST_GROUP_REDUCE
-    {  // the group's rows (workgroups g, g + 8, ...) into group row gridDim.x + g
-        double tot[8];
-        float bb[6], ld = 0.f, lf = 0.f;
-        list_reduce_rows(a, g, ngroups, gsize, tot, bb, ld, lf);
-        if (tid == 0) {
-            const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_force, 0, 0x7fffffff, 0x00020000);
-            const auto rb = __builtin_amdgcn_make_buffer_rsrc((void*)a.part_bbox, 0, 0x7fffffff, 0x00020000);
-            const int off = (gridDim.x + g) * 32;
-            st_sc1_f4(rf, off, make_float4((float)tot[0], (float)tot[1], (float)tot[2], (float)tot[3]));
-            st_sc1_f4(rf, off + 16, make_float4((float)tot[4], (float)tot[5], (float)tot[6], (float)tot[7]));
-            st_sc1_f4(rb, off, make_float4(bb[0], bb[1], bb[2], bb[3]));
-            st_sc1_f4(rb, off + 16, make_float4(bb[4], bb[5], ld, lf));
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
-#endif
     if (tid == 0) {
         a.lticket[32 * g] = 0u;  // ready for the next launch
         const unsigned old = atomicAdd(&a.lticket[32 * 8], 1u);
@@ -3301,26 +3103,17 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
     }
     __syncthreads();
     if (!s_final) return;
-    // the final workgroup: the group rows in group order (or every partial row in workgroup order), then the
-    // context update
     unsigned long long* const dbt = a.dbg_times ? a.dbg_times + 8 * gridDim.x : nullptr;
     if (dbt && tid == 0) dbt[0] = wall_clock64();
-    {
-        const ListTailIn tin = list_tail_load(ctx, a);
-        double tot[8];
-        float bb[6], ld = 0.f, lf = 0.f;
-#if GCS_LIST_GROUP_REDUCE
-        list_reduce_rows(a, gridDim.x, 1, ngroups, tot, bb, ld, lf);
-#else
-        list_reduce_rows(a, 0, 1, gridDim.x, tot, bb, ld, lf);
-#endif
-        if (tid == 0) {
-            if (dbt) dbt[1] = wall_clock64();
-            a.lticket[32 * 8] = 0u;
-            list_tail_apply(ctx, a, tin, tot, bb, ld, lf, apply_sched);
-            if (dbg) dbg[7] = wall_clock64();
-        }
-    }
+    ListTailIn tin;
+    if (tid == 0) tin = list_tail_load(ctx, a);  // in flight during the accumulator reads
+    ListTotals tot;
+    list_totals(a.lticket + kListAccBase, ngroups, tot);
+    if (tid != 0) return;
+    if (dbt) dbt[1] = wall_clock64();
+    a.lticket[32 * 8] = 0u;
+    list_tail_apply(ctx, a, tin, tot, flags);
+    if (dbg) dbg[7] = wall_clock64();
 }
 
 // ----------------------------------------------------------------------------------------------------
@@ -3535,28 +3328,28 @@ void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a)
 }
 
 template <bool CT>
-static void launch_list_step_ct(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int apply_sched)
+static void launch_list_step_ct(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)
 {
     const dim3 g(list_step_grid(a.n));
     if (list_u16(a.n)) {
         if (a.list_waves == 2)
-            hipLaunchKernelGGL((k_lstep<unsigned short, 2, CT>), g, dim3(128), 0, s, ctx, a, apply_sched);
+            hipLaunchKernelGGL((k_lstep<unsigned short, 2, CT>), g, dim3(128), 0, s, ctx, a, flags);
         else
-            hipLaunchKernelGGL((k_lstep<unsigned short, 4, CT>), g, dim3(256), 0, s, ctx, a, apply_sched);
+            hipLaunchKernelGGL((k_lstep<unsigned short, 4, CT>), g, dim3(256), 0, s, ctx, a, flags);
     } else {
         if (a.list_waves == 2)
-            hipLaunchKernelGGL((k_lstep<int, 2, CT>), g, dim3(128), 0, s, ctx, a, apply_sched);
+            hipLaunchKernelGGL((k_lstep<int, 2, CT>), g, dim3(128), 0, s, ctx, a, flags);
         else
-            hipLaunchKernelGGL((k_lstep<int, 4, CT>), g, dim3(256), 0, s, ctx, a, apply_sched);
+            hipLaunchKernelGGL((k_lstep<int, 4, CT>), g, dim3(256), 0, s, ctx, a, flags);
     }
 }
 
-void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int apply_sched)
+void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)
 {
     if (a.contact_on)
-        launch_list_step_ct<true>(s, ctx, a, apply_sched);
+        launch_list_step_ct<true>(s, ctx, a, flags);
     else
-        launch_list_step_ct<false>(s, ctx, a, apply_sched);
+        launch_list_step_ct<false>(s, ctx, a, flags);
 }
 
 void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a)
