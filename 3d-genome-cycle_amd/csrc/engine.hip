@@ -78,7 +78,7 @@ struct GraphEntry {
     unsigned long long used;
 };
 constexpr size_t kMaxGraphs = 32;  // cached step sequences per engine (least recently used evicted)
-constexpr int kInflight = 32;      // graph launches an engine lets run ahead of the device
+constexpr int kInflight = 8;       // graph launches an engine lets run ahead of the device
 
 template <class T>
 int dalloc(T** p, size_t count)
@@ -169,6 +169,12 @@ struct gcs_engine {
     unsigned* c_counts = nullptr;
     int* c_flags = nullptr;  // [0] overflow, [1] compacted entries
     int64_t c_updates = 0;   // host mirror: updates since the last clear
+    // contacts_read scratch, kept between reads (compaction into the table's size, the sorted copies, sort temp)
+    unsigned long long *c_ck = nullptr, *c_ck2 = nullptr;
+    unsigned *c_cv = nullptr, *c_cv2 = nullptr;
+    void* c_temp = nullptr;
+    size_t c_temp_bytes = 0;
+    int64_t c_sorted_cap = 0;
     int c_bits_opt = 0;      // GCS_OPT_CONTACT_BITS (0: sized from N at the first update)
     // sampled positions (store quantisation)
     float* q_out = nullptr;
@@ -1251,6 +1257,11 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->c_keys);
     dfree(e->c_counts);
     dfree(e->c_flags);
+    dfree(e->c_ck);
+    dfree(e->c_cv);
+    dfree(e->c_ck2);
+    dfree(e->c_cv2);
+    if (e->c_temp) (void)hipFree(e->c_temp);
     dfree(e->q_out);
     dfree(e->s_pts);
     dfree(e->s_spos);
@@ -1797,63 +1808,45 @@ int gcs_engine_contacts_read(gcs_engine* e, uint32_t* ijc, int64_t capacity, int
     HIPCHK(hipSetDevice(e->device));
     const long long slots = (long long)1 << e->c_bits;
     int rc;
-    // compact into the search key scratch (grown to the entry count), then radix-sort (key, count) by key
     HIPCHK(hipMemsetAsync(e->c_flags + 1, 0, sizeof(int), e->stream));
     int flags[2] = {0, 0};
     HIPCHK(hipMemcpyAsync(flags, e->c_flags, sizeof(flags), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     if (flags[0]) return fail(GCS_ECAPACITY, "contact map overflowed its hash table: raise GCS_OPT_CONTACT_BITS");
-    // upper bound of the entries: the table size (the compaction writes at most the occupied slots)
-    unsigned long long *ck = nullptr, *ck2 = nullptr;
-    unsigned *cv = nullptr, *cv2 = nullptr;
-    void* temp = nullptr;
-    auto cleanup = [&]() {
-        dfree(ck);
-        dfree(ck2);
-        dfree(cv);
-        dfree(cv2);
-        if (temp) (void)hipFree(temp);
-    };
-    // count first (cheap: a compaction into nothing would need a separate kernel; one pass with full buffers)
-    if ((rc = dalloc(&ck, (size_t)slots)) || (rc = dalloc(&cv, (size_t)slots))) {
-        cleanup();
-        return rc;
+    // compact into scratch of the table's size (the compaction writes at most the occupied slots), then radix-sort
+    // (key, count) by key; the scratch stays allocated for the next read
+    if (!e->c_ck) {
+        if ((rc = dalloc(&e->c_ck, (size_t)slots)) || (rc = dalloc(&e->c_cv, (size_t)slots))) return rc;
     }
-    launch_contact_compact(e->stream, e->c_keys, e->c_counts, slots, ck, cv, e->c_flags + 1);
+    launch_contact_compact(e->stream, e->c_keys, e->c_counts, slots, e->c_ck, e->c_cv, e->c_flags + 1);
     int total = 0;
-    hipError_t he = hipMemcpyAsync(&total, e->c_flags + 1, sizeof(int), hipMemcpyDeviceToHost, e->stream);
-    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
-    if (he != hipSuccess) {
-        cleanup();
-        return fail(GCS_EHIP, std::string("contacts compact: ") + hipGetErrorString(he));
-    }
+    HIPCHK(hipMemcpyAsync(&total, e->c_flags + 1, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
     *count = total;
-    if (total > capacity) {
-        cleanup();
-        return fail(GCS_ECAPACITY, "contact buffer too small; *count holds the required size");
-    }
-    if (total == 0) {
-        cleanup();
-        return GCS_OK;
+    if (total > capacity) return fail(GCS_ECAPACITY, "contact buffer too small; *count holds the required size");
+    if (total == 0) return GCS_OK;
+    if (total > e->c_sorted_cap) {
+        dfree(e->c_ck2);
+        dfree(e->c_cv2);
+        e->c_sorted_cap = 0;
+        if ((rc = dalloc(&e->c_ck2, (size_t)total)) || (rc = dalloc(&e->c_cv2, (size_t)total))) return rc;
+        e->c_sorted_cap = total;
     }
     const size_t bytes = std::max<size_t>(sort_pairs_u64_u32_temp_bytes(total), 16);
-    if ((rc = dalloc(&ck2, (size_t)total)) || (rc = dalloc(&cv2, (size_t)total))) {
-        cleanup();
-        return rc;
+    if (bytes > e->c_temp_bytes) {
+        if (e->c_temp) (void)hipFree(e->c_temp);
+        e->c_temp = nullptr;
+        e->c_temp_bytes = 0;
+        HIPCHK(hipMalloc(&e->c_temp, bytes));
+        e->c_temp_bytes = bytes;
     }
-    he = hipMalloc(&temp, bytes);
-    if (he == hipSuccess) {
-        sort_pairs_u64_u32(e->stream, ck, ck2, cv, cv2, total, temp, bytes);
-        he = hipGetLastError();
-    }
+    sort_pairs_u64_u32(e->stream, e->c_ck, e->c_ck2, e->c_cv, e->c_cv2, total, e->c_temp, e->c_temp_bytes);
+    HIPCHK(hipGetLastError());
     std::vector<unsigned long long> hk(total);
     std::vector<unsigned> hv(total);
-    if (he == hipSuccess)
-        he = hipMemcpyAsync(hk.data(), ck2, total * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream);
-    if (he == hipSuccess) he = hipMemcpyAsync(hv.data(), cv2, total * sizeof(unsigned), hipMemcpyDeviceToHost, e->stream);
-    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
-    cleanup();
-    if (he != hipSuccess) return fail(GCS_EHIP, std::string("contacts sort: ") + hipGetErrorString(he));
+    HIPCHK(hipMemcpyAsync(hk.data(), e->c_ck2, total * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(hv.data(), e->c_cv2, total * sizeof(unsigned), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
     for (int k = 0; k < total; ++k) {
         ijc[3 * k] = (uint32_t)(hk[k] >> 32);
         ijc[3 * k + 1] = (uint32_t)hk[k];
@@ -2573,8 +2566,9 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         return GCS_OK;
     }
     if (option == GCS_OPT_LIST_CAP) {
-        if (value < 32 || value > 16384 || (value % kMaxListWaves) != 0)
-            return fail(GCS_EINVAL, "list capacity must be a multiple of 4 in [32, 16384]");
+        // whole batches of 8 entries per wave segment (2 or 4 waves)
+        if (value < 32 || value > 16384 || (value % (8 * kMaxListWaves)) != 0)
+            return fail(GCS_EINVAL, "list capacity must be a multiple of 32 in [32, 16384]");
         e->list_cap = (int)value;
         drop_graph(e);
         return GCS_OK;

@@ -1706,11 +1706,34 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
 #ifndef GCS_P2_UNROLL
 #define GCS_P2_UNROLL 4  // sub-tile phase 2: hits popped per lane per round (rounds = wave max of hits / this)
 #endif
+// Neighbour-list layout (the list step): per wave segment w of a slot s, its entries packed by 8-byte words of
+// E = 8 / sizeof(LE) consecutive entries (4 16-bit or 2 32-bit slot indices), the words column-major over the slots:
+// entry k of (w, s) is element E ((w cap / E + k / E) stride + s) + k % E.  A wave loads E entries of each of its 64
+// slots with one 8-B load per lane (512 contiguous bytes), so a batch of 8 entries is 2 (16-bit) or 4 loads.
+template <typename LE>
+__device__ __forceinline__ size_t list_at(int w, int cap, int k, int s, size_t stride)
+{
+    constexpr int E = 8 / (int)sizeof(LE);
+    return (((size_t)w * (size_t)(cap / E) + (size_t)(k / E)) * stride + (size_t)s) * E + (size_t)(k % E);
+}
+// entry u of a batch held as 8-byte words
+template <typename LE>
+__device__ __forceinline__ int list_entry(const uint2* w, int u)
+{
+    if constexpr (sizeof(LE) == 2) {
+        const unsigned x = (u & 2) ? w[u >> 2].y : w[u >> 2].x;
+        return (int)((u & 1) ? (x >> 16) : (x & 0xffffu));
+    } else {
+        return (int)((u & 1) ? w[u >> 1].y : w[u >> 1].x);
+    }
+}
+
 template <int MODE, int NG, typename LE = int>
 __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const ForceArgs& a, int lane, int s,
                                        int s_begin, int s_end, float4 pi, float bi, float& fx, float& fy, float& fz,
                                        float& acc, int* s_rowV, int* s_rowJ, float4* s_cand, int* s_candj, int& ntot,
-                                       int wv, int nwv, int self = -1, bool lvalid = false, int* lcnt = nullptr)
+                                       int wv, int nwv, int self = -1, bool lvalid = false, int* lcnt = nullptr,
+                                       uint2* lpend = nullptr)
 {
     // kModeList: phase 2 appends each hit (other than the particle itself) to the lane's list segment wv
     // instead of evaluating the pair force (the lists of the list step, built at the grid's rc = cutoff + skin)
@@ -1887,8 +1910,11 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
         // phase 2: pop ffbl, xor, min (exhausted -> the group's sentinel slot), clear
         const int mh = uniform(wave_max_int(__popc(m)));
         if constexpr (MODE == kModeList) {
-            // append the hits: one column-major store per hit (lanes of a wave write consecutive slots of a row)
-            LE* const seg = reinterpret_cast<LE*>(a.list) + (size_t)wv * a.list_cap * a.list_stride + s;
+            // append the hits: entries collect in the lane's pending 8-byte word (lpend), stored whole when full
+            // (list_at's layout: lanes of a wave write consecutive words of a row); the caller stores the last,
+            // partial word
+            constexpr int E = 8 / (int)sizeof(LE);
+            uint2* const lw = reinterpret_cast<uint2*>(a.list);
             for (int t = 0; t < mh; ++t) {
                 unsigned b;
                 asm("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(m));
@@ -1897,8 +1923,23 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 if (k < (unsigned)kSub && lvalid) {
                     const int e = reinterpret_cast<const int*>(my_cand)[4 * kSub + k];  // the partner's sorted slot
                     if (e != s) {
-                        if (*lcnt < a.list_cap) seg[(size_t)(*lcnt) * a.list_stride] = (LE)e;
-                        *lcnt += 1;
+                        const int kk = *lcnt;
+                        if (kk < a.list_cap) {
+                            const int j = kk % E;
+                            if constexpr (E == 4) {
+                                const unsigned v = (unsigned)e & 0xffffu;
+                                if (j == 0) lpend->x = v;
+                                else if (j == 1) lpend->x |= v << 16;
+                                else if (j == 2) lpend->y = v;
+                                else lpend->y |= v << 16;
+                            } else {
+                                if (j == 0) lpend->x = (unsigned)e;
+                                else lpend->y = (unsigned)e;
+                            }
+                            if (j == E - 1)
+                                lw[((size_t)wv * (a.list_cap / E) + kk / E) * a.list_stride + s] = *lpend;
+                        }
+                        *lcnt = kk + 1;
                     }
                 }
             }
@@ -2770,8 +2811,15 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
         const int self = a.sidx[sl];
         float fx = 0.f, fy = 0.f, fz = 0.f, acc = 0.f;
         int cnt = 0;
+        uint2 pend = make_uint2(0u, 0u);
         pair_forces_sub<kModeList, GCS_LBUILD_GROUPS, LE>(ctx, a, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
-                                      s_rowJ[wave], s_cand[wave], nullptr, ntot, wave, kListWaves, self, valid, &cnt);
+                                      s_rowJ[wave], s_cand[wave], nullptr, ntot, wave, kListWaves, self, valid, &cnt,
+                                      &pend);
+        {  // the last, partial word of the lane's segment
+            constexpr int E = 8 / (int)sizeof(LE);
+            if (valid && cnt < a.list_cap && (cnt % E) != 0)
+                reinterpret_cast<uint2*>(a.list)[((size_t)wave * (a.list_cap / E) + cnt / E) * a.list_stride + s] = pend;
+        }
         if (dbg && first && lane == 0) dbg[2 + wave] = wall_clock64();
         s_ovf[wave][lane] = cnt > a.list_cap ? 1 : 0;
         __syncthreads();
@@ -2855,17 +2903,20 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     const int cap = a.list_cap;
     const size_t stride = (size_t)a.list_stride;
     constexpr int kU = GCS_LIST_UNROLL;
+    constexpr int kE = 8 / (int)sizeof(LE);  // entries per 8-byte list word
+    constexpr int kW = kU / kE;              // list words per batch
+    static_assert(kU % kE == 0, "a batch is whole list words");
     constexpr int kIdx = (1 << kListIndexBits) - 1;
-    const LE* __restrict__ seg = reinterpret_cast<const LE*>(a.list) + (size_t)wave * cap * stride + sl;
+    const uint2* __restrict__ segw = reinterpret_cast<const uint2*>(a.list) + (size_t)wave * (cap / kE) * stride + sl;
 
     // 1. slot loads (one round trip; the type table's load beside them)
     for (int t = tid; t < a.ntypes; t += blockDim.x) s_tab[t] = a.type_ab[t];
     const float4 pi = qc[sl];
     const float4 pb = a.spos[sl];
     const int cw = a.lcount[(size_t)wave * stride + sl];
-    int e[kU];
+    uint2 e[kW];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) e[u] = seg[(size_t)u * stride];  // list_cap >= kU: in bounds
+    for (int j = 0; j < kW; ++j) e[j] = segw[(size_t)j * stride];  // list_cap >= kU: in bounds
     const float cs = (float)ctx->cs;
     const float D = ctx->ldisp;
     const float lrc_b = ctx->lrc_b;
@@ -2908,13 +2959,17 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     if (a.has_pair) {
         const int cnt = (valid && !fb) ? min(cw & kListCountMask, cap) : 0;
         const int kmax = uniform(wave_max_int(cnt));
+        // batches of kU entries: the partners' gathers are issued first, then the next batch's entry words (they
+        // return right behind the gathers, so each batch costs one round trip), then the pair forces (and contacts)
+        const int klast = (cap / kU - 1) * kU;  // the segment's last batch (list_cap is a multiple of kU)
         for (int k0 = 0; k0 < kmax; k0 += kU) {
-            int en_[kU];  // the next batch's entries, in flight during this batch
-#pragma unroll
-            for (int u = 0; u < kU; ++u) en_[u] = (k0 + kU + u < kmax) ? seg[(size_t)(k0 + kU + u) * stride] : 0;
             float4 q[kU];
 #pragma unroll
-            for (int u = 0; u < kU; ++u) q[u] = qc[(k0 + u < cnt) ? e[u] : sl];
+            for (int u = 0; u < kU; ++u) q[u] = qc[(k0 + u < cnt) ? list_entry<LE>(e, u) : sl];
+            const int kn = min(k0 + kU, klast);
+#pragma unroll
+            for (int j = 0; j < kW; ++j) e[j] = segw[(size_t)(kn / kE + j) * stride];
+            __builtin_amdgcn_sched_barrier(0);  // keep the entry loads here, ahead of the arithmetic
 #pragma unroll
             for (int u = 0; u < kU; ++u)
                 list_pair(pi.x, pi.y, pi.z, q[u], s_tab[(unsigned)__float_as_int(q[u].w) >> kListIndexBits], ahi, bhi,
@@ -2924,8 +2979,6 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
                 for (int u = 0; u < kU; ++u)
                     if (!fbc && k0 + u < cnt) list_contact(a, pi, q[u], i, __float_as_int(q[u].w) & kIdx);
             }
-#pragma unroll
-            for (int u = 0; u < kU; ++u) e[u] = en_[u];
         }
         // exact search of the build's cell list for the particles the lists may not cover: a partner within rc
         // now was within rc + D at the build.  Wave-cooperative: the wave takes its fallback lanes one at a time,

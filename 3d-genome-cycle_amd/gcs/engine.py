@@ -253,6 +253,7 @@ class Engine:
                 cap = int(cnt.value)
                 continue
             A.check(rc)
+            self._last_contacts = int(cnt.value)
             return buf[: cnt.value].copy()
 
     # ---- contact map (stage_interphase/contact_map.cpp:28-85) and sampled positions (simulation_store.cpp:192-216)
@@ -264,7 +265,8 @@ class Engine:
     def contacts_accumulate(self):
         """contact_map::accumulate: (K, 3) uint32 rows (i, j, count) sorted by (i, j)."""
         cnt = C.c_int64()
-        cap = 0
+        # one read in the common case: room for the last table's size (+25 %) or 16 pairs per particle
+        cap = max(int(1.25 * getattr(self, "_last_contacts", 0)), 16 * self.n)
         while True:
             buf = np.empty((max(cap, 1), 3), dtype=np.uint32)
             rc = self._lib.gcs_engine_contacts_read(self._h, buf.ctypes.data_as(C.POINTER(C.c_uint32)), cap,
@@ -273,6 +275,7 @@ class Engine:
                 cap = int(cnt.value)
                 continue
             A.check(rc)
+            self._last_contacts = int(cnt.value)
             return buf[: cnt.value].copy()
 
     def contacts_clear(self):

@@ -102,6 +102,19 @@ class InterphaseDriver:
         self.relaxation_seed, self.interphase_seed = interphase_bd_seeds(design.seed)
         self.context = initial_context(cfg)
         self.mean_energy = 0.0
+        self._writer = None
+
+    def _out(self):
+        """the store's sampling writes, on a background writer for the length of a stage (gcs.store.AsyncWriter)"""
+        if self._writer is None:
+            from .store import AsyncWriter
+            self._writer = AsyncWriter(self.store)
+        return self._writer
+
+    def _close_out(self):
+        if self._writer is not None:
+            w, self._writer = self._writer, None
+            w.close()
 
     def _progress(self, phase, step):
         if self.log is None:
@@ -121,14 +134,17 @@ class InterphaseDriver:
         steps = cfg.relaxation_steps if steps is None else steps
         self.sys.set_schedule(update_time=0, update_scales=0, update_wall=0, timestep=cfg.timestep)
         every = np.gcd(cfg.relaxation_logging_interval, cfg.relaxation_sampling_interval)
-        self._callback_relax(0)
-        done = 0
-        while done < steps:
-            k = min(every - done % every, steps - done)
-            self.sys.run(k, first_step=done, temperature=cfg.temperature, timestep=cfg.timestep,
-                         spacestep=cfg.relaxation_spacestep, seed=self.relaxation_seed)
-            done += k
-            self._callback_relax(done)
+        try:
+            self._callback_relax(0)
+            done = 0
+            while done < steps:
+                k = min(every - done % every, steps - done)
+                self.sys.run(k, first_step=done, temperature=cfg.temperature, timestep=cfg.timestep,
+                             spacestep=cfg.relaxation_spacestep, seed=self.relaxation_seed)
+                done += k
+                self._callback_relax(done)
+        finally:
+            self._close_out()
 
     def _callback_relax(self, step):
         cfg = self.cfg
@@ -139,7 +155,9 @@ class InterphaseDriver:
         if log:
             self._progress("relaxation", step)
         if sample and self.store is not None:
-            self.store.save_frame("relaxation", step, self.sys.get_positions(), self._context_record())
+            from .store import sampled_positions
+            x, q = sampled_positions(self.sys)
+            self._out().save_frame("relaxation", step, x, self._context_record(), quantized=q)
 
     def _context_record(self):
         c = self.sys.get_context()
@@ -170,15 +188,18 @@ class InterphaseDriver:
         if hasattr(self.sys, "set_option"):  # replay whole callback intervals from one captured graph
             self.sys.set_option(A.OPT_GRAPH_STEPS, every)
         # callback(0): time 0, energy, log/sample, then update_core_scale + update_wall_semiaxes
-        self._callback_sim(0, contacts)
-        self.sys.apply_schedule(0)
-        done = 0
-        while done < steps:
-            k = min(every - done % every, steps - done)
-            self.sys.run(k, first_step=done, temperature=cfg.temperature, timestep=cfg.timestep,
-                         seed=self.interphase_seed)
-            done += k
-            self._callback_sim(done, contacts)
+        try:
+            self._callback_sim(0, contacts)
+            self.sys.apply_schedule(0)
+            done = 0
+            while done < steps:
+                k = min(every - done % every, steps - done)
+                self.sys.run(k, first_step=done, temperature=cfg.temperature, timestep=cfg.timestep,
+                             seed=self.interphase_seed)
+                done += k
+                self._callback_sim(done, contacts)
+        finally:
+            self._close_out()
 
     def _callback_sim(self, step, contacts=True):
         cfg = self.cfg
@@ -189,7 +210,9 @@ class InterphaseDriver:
         if log:
             self._progress("interphase", step)
         if sample and self.store is not None:
-            self.store.save_frame("interphase", step, self.sys.get_positions(), self._context_record())
+            from .store import sampled_positions
+            x, q = sampled_positions(self.sys)
+            self._out().save_frame("interphase", step, x, self._context_record(), quantized=q)
         if contacts and step % cfg.contactmap_update_interval == 0:
             d = self.contact_distance(step)
             if d > 0:  # distance 0 finds no pair (callback(0))
@@ -197,6 +220,6 @@ class InterphaseDriver:
         if contacts and sample and (step // cfg.sampling_interval) % cfg.contactmap_output_window == 0:
             table = self.sys.contacts_accumulate()
             if self.store is not None:
-                self.store.save_contacts(step, table)
+                self._out().save_contacts(step, table)
             self.last_contacts = table
             self.sys.contacts_clear()

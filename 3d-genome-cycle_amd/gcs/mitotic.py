@@ -109,6 +109,19 @@ class StdNormal:
         return y * mult
 
 
+def _writer(store):
+    """the stage's sampling writes on a background thread (gcs.store.AsyncWriter), or None without a store"""
+    if store is None:
+        return None
+    from .store import AsyncWriter
+    return AsyncWriter(store)
+
+
+def sampled_positions(system):
+    from .store import sampled_positions as sp
+    return sp(system)
+
+
 def normal_vector(rng: MT19937_64) -> np.ndarray:
     """stage_anatelophase/simulation_driver.cpp:25-32: a FRESH normal_distribution per vector."""
     nd = StdNormal(rng)
@@ -187,18 +200,24 @@ class AnatelophaseDriver:
     def _stage(self, name, steps, seed):
         cfg = self.cfg
         every = math.gcd(cfg.sampling_interval, cfg.logging_interval)
-        self._callback(name, 0)
-        done = 0
-        while done < steps:
-            k = min(every - done % every, steps - done)
-            self.sys.run(k, first_step=done, temperature=cfg.temperature, timestep=cfg.timestep, seed=seed)
-            done += k
-            self._callback(name, done)
+        self._writer = _writer(self.store)
+        try:
+            self._callback(name, 0)
+            done = 0
+            while done < steps:
+                k = min(every - done % every, steps - done)
+                self.sys.run(k, first_step=done, temperature=cfg.temperature, timestep=cfg.timestep, seed=seed)
+                done += k
+                self._callback(name, done)
+        finally:
+            if self._writer is not None:
+                self._writer.close()
 
     def _callback(self, name, step):
         cfg = self.cfg
         if step % cfg.sampling_interval == 0 and self.store is not None:
-            self.store.save_frame(name, step, self.sys.get_positions(), None)
+            x, q = sampled_positions(self.sys)
+            self._writer.save_frame(name, step, x, None, quantized=q)
         if step % cfg.logging_interval == 0 and self.log is not None:
             e, _ = self.sys.compute_energy()
             stamp = _time.strftime("%Y-%m-%d %H:%M:%S")
@@ -280,14 +299,19 @@ class PrometaphaseDriver:
         cfg = self.cfg
         steps = cfg.prometaphase_steps if steps is None else steps
         every = math.gcd(cfg.sampling_interval, cfg.logging_interval)
-        self._callback(0)
-        seed = self.random()  # .seed = _random() (:230; callback(0) draws nothing)
-        done = 0
-        while done < steps:
-            k = min(every - done % every, steps - done)
-            self.sys.run(k, first_step=done, temperature=cfg.temperature, timestep=cfg.timestep, seed=seed)
-            done += k
-            self._callback(done)
+        self._writer = _writer(self.store)
+        try:
+            self._callback(0)
+            seed = self.random()  # .seed = _random() (:230; callback(0) draws nothing)
+            done = 0
+            while done < steps:
+                k = min(every - done % every, steps - done)
+                self.sys.run(k, first_step=done, temperature=cfg.temperature, timestep=cfg.timestep, seed=seed)
+                done += k
+                self._callback(done)
+        finally:
+            if self._writer is not None:
+                self._writer.close()
 
     def _callback(self, step):
         cfg = self.cfg
@@ -297,4 +321,5 @@ class PrometaphaseDriver:
             stamp = _time.strftime("%Y-%m-%d %H:%M:%S")
             print(f"[prometaphase] {stamp}\t{step}\tE: {e:g}", file=self.log)
         if step % cfg.sampling_interval == 0 and self.store is not None:
-            self.store.save_frame("prometaphase", step, self.sys.get_positions(), None)
+            x, q = sampled_positions(self.sys)
+            self._writer.save_frame("prometaphase", step, x, None, quantized=q)

@@ -288,6 +288,70 @@ class SimulationStore:
         self.append_frame(step)
 
 
+class AsyncWriter:
+    """The drivers' sampling writes (save_frame / save_contacts) on a background thread, so the device keeps stepping
+    while a frame is deflated and written (deflate 6 of a C2 frame takes ~0.1 s of one host core: at the reference's
+    cadence of one frame per 1,000 steps that is several times the steps' own device time).  The HDF5 library is not
+    thread-safe: while a writer is open only its thread touches the store; `flush()` waits for every queued write
+    (the drivers flush at the end of each stage, before any other store call).  Writes keep their order, so the
+    file is the one the synchronous calls would write.  ctypes releases the GIL inside the HDF5 calls."""
+
+    def __init__(self, store, depth=8):
+        import queue
+        import threading
+        self.store = store
+        self.q = queue.Queue(maxsize=depth)
+        self.err = None
+        self.t = threading.Thread(target=self._loop, name="gcs-store-writer", daemon=True)
+        self.t.start()
+
+    def _loop(self):
+        while True:
+            item = self.q.get()
+            try:
+                if item is None:
+                    return
+                if self.err is None:
+                    fn, args, kw = item
+                    fn(*args, **kw)
+            except BaseException as exc:  # re-raised on the caller's thread at the next put / flush
+                self.err = exc
+            finally:
+                self.q.task_done()
+
+    def _put(self, fn, *args, **kw):
+        if self.err is not None:
+            raise self.err
+        self.q.put((fn, args, kw))
+
+    def save_frame(self, *args, **kw):
+        self._put(self.store.save_frame, *args, **kw)
+
+    def save_contacts(self, *args, **kw):
+        self._put(self.store.save_contacts, *args, **kw)
+
+    def flush(self):
+        self.q.join()
+        if self.err is not None:
+            err, self.err = self.err, None
+            raise err
+
+    def close(self):
+        try:
+            self.flush()
+        finally:
+            self.q.put(None)
+            self.t.join()
+
+
+def sampled_positions(system):
+    """Positions as save_positions stores them, and whether they are already quantised: the engine quantises on the
+    device (gcs_engine_sample_positions, bit-exact with quantize_positions), other backends return raw positions."""
+    if hasattr(system, "sample_positions"):
+        return system.sample_positions(16), True
+    return system.get_positions(), False
+
+
 def write_prepared(path, cfg: SimulationConfig, design, master_seed: int, anatelophase=None, prometaphase=None,
                    chains_source="", create=True, initial_positions=True):
     """What `prepare` writes (prepare.cpp:374-562) for a given interphase design (+ optional mitotic designs):

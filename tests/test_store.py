@@ -149,3 +149,29 @@ def test_store_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(str(store.LIB_PATH))
     for n in names:
         assert hasattr(lib, n), n
+
+
+def test_async_writer_keeps_order_and_raises(prepared):
+    """gcs.store.AsyncWriter: the drivers' sampling writes on a background thread land exactly as the synchronous
+    calls would write them (same frames, same .steps order), and a failing write re-raises on the caller's thread"""
+    p, _ = prepared
+    rng = np.random.default_rng(3)
+    frames = [rng.normal(size=(50, 3)) for _ in range(6)]
+    with store.SimulationStore(p) as s:
+        s.set_stage("interphase")
+        s.clear_frames()
+        w = store.AsyncWriter(s, depth=2)
+        for k, x in enumerate(frames):
+            w.save_frame("interphase", 10 * (k + 1), x)
+        w.save_contacts(60, np.array([[0, 1, 2], [0, 3, 1]], dtype=np.uint32))
+        w.flush()
+        assert s.load_steps() == [10, 20, 30, 40, 50, 60]
+        for k, x in enumerate(frames):
+            got = s.load_positions(10 * (k + 1))
+            assert np.array_equal(got.astype(np.float32), store.quantize_positions(x))
+        assert np.array_equal(s.load_contacts(60), [[0, 1, 2], [0, 3, 1]])
+        def bad():
+            raise store.StoreError("write failed")
+        w._put(bad)  # a failing write: raised on this thread at close, not lost
+        with pytest.raises(store.StoreError):
+            w.close()
