@@ -246,6 +246,17 @@ struct gcs_engine {
     int list_every = 1;         // the period of the current run
     int list_waves = 4;         // GCS_OPT_LIST_WAVES: waves per tile (2: more tiles resident, for replica runs)
     bool l_need_build = true;   // the next list step must rebuild (run start without continuity)
+    // small systems (N <= kSmallMax, GCS_OPT_SMALL_PATH): one single-workgroup launch per run (k_small) and its
+    // persistent list state; small_cont: the next small run at small_step continues the last one (no rebuild)
+    int small_opt = 0;
+    unsigned short* sm_list = nullptr;
+    int* sm_lcount = nullptr;
+    float4* sm_bpos = nullptr;
+    int* sm_cstart = nullptr;
+    unsigned short* sm_cidx = nullptr;
+    bool small_cont = false;
+    int64_t small_step = 0;
+    int small_version = -1;
     double c_pending = 0;      // a contact update fused into the next list step (its distance; 0: none)
 
     // fused-step continuity: after a fused run the cells of the next positions are already binned with the
@@ -637,6 +648,11 @@ void enqueue_cells(gcs_engine* e)
 }
 
 bool list_path(const gcs_engine* e, bool spacestep) { return e->fused == 3 && e->list_ok && !spacestep; }
+// small systems: the single-workgroup step loop (k_small) instead of the list step
+bool small_path(const gcs_engine* e, bool spacestep)
+{
+    return e->small_opt != 0 && e->n <= kSmallMax && e->fused == 3 && !spacestep && !e->dom;
+}
 bool fused_path(const gcs_engine* e, bool spacestep) { return e->fused != 0 && !spacestep; }
 bool rebuild_path(const gcs_engine* e, bool spacestep)
 {
@@ -841,6 +857,7 @@ int begin_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
     const bool fused = fused_path(e, cfg->spacestep > 0);
     const bool cont = fused && e->chain_valid && e->chain_step == first_step && e->chain_version == e->topo_version;
     e->chain_valid = false;
+    e->small_cont = false;
     if (list_path(e, cfg->spacestep > 0)) {
         if ((rc = ensure_list(e))) return rc;
         e->list_every = auto_list_every(e, cfg);
@@ -932,6 +949,66 @@ GraphKey run_key(const gcs_engine* e, const gcs_bd_config* cfg, bool spacestep)
     k.list_waves = e->list_waves;
     k.cfg = *cfg;
     return k;
+}
+
+int flush_contacts(gcs_engine* e);  // (below)
+
+// a run on the small-system path: one k_small launch for all its steps
+int run_small(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps)
+{
+    if (int rc = flush_contacts(e)) return rc;
+    int rc = prepare(e);
+    if (rc) return rc;
+    const size_t n = (size_t)e->n;
+    if (!e->sm_lcount) {
+        if ((rc = dalloc(&e->sm_list, n * kSmallCap)) || (rc = dalloc(&e->sm_lcount, n)) ||
+            (rc = dalloc(&e->sm_bpos, n)) || (rc = dalloc(&e->sm_cstart, kSmallCells + 1)) ||
+            (rc = dalloc(&e->sm_cidx, n)))
+            return rc;
+        e->small_cont = false;
+    }
+    ForceArgs& a = e->fa;
+    a.temperature = (float)cfg->temperature;
+    a.timestep = (float)cfg->timestep;
+    a.seed_lo = (unsigned)cfg->seed;
+    a.seed_hi = (unsigned)(cfg->seed >> 32);
+    a.noise_mode = cfg->noise;
+    long long st = first_step;
+    if ((rc = set_ctx_field(e, offsetof(DevCtx, step), &st, sizeof(st)))) return rc;
+    double dt = cfg->timestep;
+    if ((rc = set_ctx_field(e, offsetof(DevCtx, dt_used), &dt, sizeof(dt)))) return rc;
+    const bool cont = e->small_cont && e->small_step == first_step && e->small_version == e->topo_version;
+    const int flags = (e->sched_flags != 0 ? 1 : 0) | 4;  // schedule; neighbour-count statistics every step
+    // GCS_DEBUG_SMALL: thread 0's wall-clock per phase of the last launch, printed to stderr
+    unsigned long long* dbg = nullptr;
+    if (std::getenv("GCS_DEBUG_SMALL")) HIPCHK(hipMalloc(&dbg, 8 * sizeof(unsigned long long)));
+    for (int64_t done = 0; done < steps;) {
+        // chunks of at most 2^20 steps per launch (one launch holds the device for ~ms per thousand steps)
+        const int k = (int)std::min<int64_t>(steps - done, 1 << 20);
+        launch_small(e->stream, e->ctx, a, first_step + done, k, flags, (done == 0 && !cont) ? 1 : 0, list_skin(e),
+                     e->sm_list, e->sm_lcount, e->sm_bpos, e->sm_cstart, e->sm_cidx, dbg);
+        done += k;
+        e->rstats.small_launches++;
+    }
+    HIPCHK(hipGetLastError());
+    if (dbg) {
+        unsigned long long h[5];
+        HIPCHK(hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        (void)hipFree(dbg);
+        std::fprintf(stderr, "gcs small: %lld steps, per step (us): build %.3f forces %.3f totals %.3f tail %.3f; "
+                     "builds %llu\n", (long long)steps, h[0] / 100.0 / steps, h[1] / 100.0 / steps,
+                     h[2] / 100.0 / steps, h[3] / 100.0 / steps, h[4]);
+    }
+    e->rstats.small_steps += steps;
+    e->chain_valid = false;   // the list step's own state did not follow
+    e->l_need_build = true;
+    e->small_cont = true;
+    e->small_step = first_step + steps;
+    e->small_version = e->topo_version;
+    if (steps & 1) e->parity ^= 1;
+    if (cfg->noise == GCS_NOISE_INJECTED) e->noise_cursor += steps;
+    return GCS_OK;
 }
 
 // after a run's steps were enqueued
@@ -1254,6 +1331,11 @@ int gcs_engine_destroy(gcs_engine* e)
     if (e->nccl) rccl_comm_destroy(e->nccl);
     dfree(e->dom_shared_idx);
     dfree(e->dom_shared_flag);
+    dfree(e->sm_list);
+    dfree(e->sm_lcount);
+    dfree(e->sm_bpos);
+    dfree(e->sm_cstart);
+    dfree(e->sm_cidx);
     dfree(e->c_keys);
     dfree(e->c_counts);
     dfree(e->c_flags);
@@ -1433,6 +1515,7 @@ int gcs_engine_set_positions(gcs_engine* e, const double* xyz, int64_t n)
     if (!e || !xyz) return fail(GCS_EINVAL, "null argument");
     if (int rc = flush_contacts(e)) return rc;
     e->chain_valid = false;
+    e->small_cont = false;
     if (n != e->n) return fail(GCS_EINVAL, "position count does not match the particle count");
     HIPCHK(hipSetDevice(e->device));
     std::vector<float4> h(n);
@@ -1485,6 +1568,7 @@ int gcs_engine_set_context(gcs_engine* e, const gcs_context* c)
     if (!e || !c) return fail(GCS_EINVAL, "null argument");
     if (int rc = flush_contacts(e)) return rc;
     e->chain_valid = false;
+    e->small_cont = false;
     HIPCHK(hipSetDevice(e->device));
     DevCtx d;
     HIPCHK(hipMemcpyAsync(&d, e->ctx, sizeof(d), hipMemcpyDeviceToHost, e->stream));
@@ -1509,6 +1593,7 @@ int gcs_engine_set_schedule(gcs_engine* e, const gcs_schedule* s)
     if (e) e->dom_cont = false;  // a decomposed run re-primes after any outside change
     if (!e || !s) return fail(GCS_EINVAL, "null argument");
     e->chain_valid = false;
+    e->small_cont = false;
     if ((s->update_scales && (!(s->core_scale_tau > 0) || !(s->bond_scale_tau > 0))))
         return fail(GCS_EINVAL, "scale time constants must be positive");
     HIPCHK(hipSetDevice(e->device));
@@ -1523,6 +1608,7 @@ int gcs_engine_apply_schedule(gcs_engine* e, int64_t step)
 {
     if (!e) return fail(GCS_EINVAL, "null argument");
     e->chain_valid = false;
+    e->small_cont = false;
     int rc = prepare(e);
     if (rc) return rc;
     long long st = step;
@@ -1567,6 +1653,8 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
         return fail(GCS_ESTATE, "not enough injected noise for the requested steps");
     if (steps == 0) return prepare(e);
     const bool spacestep = cfg->spacestep > 0;
+    if (small_path(e, spacestep)) return run_small(e, cfg, first_step, steps);
+    e->small_cont = false;  // another step shape moves the state on: the small path rebuilds next time
     if (!list_path(e, spacestep))
         if (int rc = flush_contacts(e)) return rc;
     int rc = begin_run(e, cfg, first_step);
@@ -1971,6 +2059,7 @@ int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step
                               hipMemcpyDeviceToDevice, e->stream));
     }
     e->chain_valid = false;
+    e->small_cont = false;
     e->dom_next = step + 1;
     const ForceArgs a = domain_args(e);
     const int n = e->n;
@@ -2221,6 +2310,7 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
         e->dom_next = first_step + steps;
     }
     e->chain_valid = false;
+    e->small_cont = false;
     return GCS_OK;
 }
 
@@ -2535,6 +2625,7 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
 {
     if (!e) return fail(GCS_EINVAL, "null argument");
     e->chain_valid = false;
+    e->small_cont = false;
     if (option == GCS_OPT_CONTACT_BITS) {
         if (value != 0 && (value < 10 || value > 34)) return fail(GCS_EINVAL, "contact bits must be 0 or in [10, 34]");
         if (e->c_keys) return fail(GCS_ESTATE, "the contact map is already allocated");
@@ -2571,6 +2662,12 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
             return fail(GCS_EINVAL, "list capacity must be a multiple of 32 in [32, 16384]");
         e->list_cap = (int)value;
         drop_graph(e);
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_SMALL_PATH) {
+        if (value != 0 && value != 1) return fail(GCS_EINVAL, "small path must be 0 (off) or 1 (auto)");
+        e->small_opt = (int)value;
+        e->small_cont = false;
         return GCS_OK;
     }
     if (option == GCS_OPT_FUSED_STEP) {

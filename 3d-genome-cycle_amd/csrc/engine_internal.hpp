@@ -286,6 +286,14 @@ void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a);
 // flags: 1 apply the schedule, 2 the next step rebuilds (bounding box -> grid), 4 neighbour-count statistics
 void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags);
 int list_step_grid(int n);
+// small systems (N <= kSmallMax): `steps` steps in one single-workgroup launch (kernels.hip k_small); its list state
+// (list [kSmallCap][N] u16, lcount [N], build positions [N], the build's cells [kSmallCells + 1] + [N]) persists
+constexpr int kSmallMax = 2048;
+constexpr int kSmallCap = 256;
+constexpr int kSmallCells = 4096;
+void launch_small(hipStream_t s, DevCtx* ctx, const ForceArgs& a, long long first_step, int steps, int flags,
+                  int force_build, float skin, unsigned short* list, int* lcount, float4* bpos, int* cstart,
+                  unsigned short* cidx, unsigned long long* dbg = nullptr);
 bool list_u16(int n);  // list entries are 16-bit slot indices (N <= 65536)
 void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceArgs& a, bool fused);
 void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a);

@@ -1733,7 +1733,7 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                                        int s_begin, int s_end, float4 pi, float bi, float& fx, float& fy, float& fz,
                                        float& acc, int* s_rowV, int* s_rowJ, float4* s_cand, int* s_candj, int& ntot,
                                        int wv, int nwv, int self = -1, bool lvalid = false, int* lcnt = nullptr,
-                                       uint2* lpend = nullptr)
+                                       unsigned long long* lpend = nullptr)
 {
     // kModeList: phase 2 appends each hit (other than the particle itself) to the lane's list segment wv
     // instead of evaluating the pair force (the lists of the list step, built at the grid's rc = cutoff + skin)
@@ -1910,11 +1910,12 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
         // phase 2: pop ffbl, xor, min (exhausted -> the group's sentinel slot), clear
         const int mh = uniform(wave_max_int(__popc(m)));
         if constexpr (MODE == kModeList) {
-            // append the hits: entries collect in the lane's pending 8-byte word (lpend), stored whole when full
-            // (list_at's layout: lanes of a wave write consecutive words of a row); the caller stores the last,
-            // partial word
+            // append the hits: entries shift into the lane's pending 8-byte word (lpend: the newest in the top
+            // bits), stored whole when full (list_at's layout: lanes of a wave write consecutive words of a row);
+            // the caller stores the last, partial word
             constexpr int E = 8 / (int)sizeof(LE);
-            uint2* const lw = reinterpret_cast<uint2*>(a.list);
+            constexpr int EB = 8 * (int)sizeof(LE);  // bits per entry
+            unsigned long long* const lw = reinterpret_cast<unsigned long long*>(a.list);
             for (int t = 0; t < mh; ++t) {
                 unsigned b;
                 asm("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(m));
@@ -1925,18 +1926,8 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                     if (e != s) {
                         const int kk = *lcnt;
                         if (kk < a.list_cap) {
-                            const int j = kk % E;
-                            if constexpr (E == 4) {
-                                const unsigned v = (unsigned)e & 0xffffu;
-                                if (j == 0) lpend->x = v;
-                                else if (j == 1) lpend->x |= v << 16;
-                                else if (j == 2) lpend->y = v;
-                                else lpend->y |= v << 16;
-                            } else {
-                                if (j == 0) lpend->x = (unsigned)e;
-                                else lpend->y = (unsigned)e;
-                            }
-                            if (j == E - 1)
+                            *lpend = (*lpend >> EB) | ((unsigned long long)(LE)e << (64 - EB));
+                            if (kk % E == E - 1)
                                 lw[((size_t)wv * (a.list_cap / E) + kk / E) * a.list_stride + s] = *lpend;
                         }
                         *lcnt = kk + 1;
@@ -2811,14 +2802,16 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
         const int self = a.sidx[sl];
         float fx = 0.f, fy = 0.f, fz = 0.f, acc = 0.f;
         int cnt = 0;
-        uint2 pend = make_uint2(0u, 0u);
+        unsigned long long pend = 0ull;
         pair_forces_sub<kModeList, GCS_LBUILD_GROUPS, LE>(ctx, a, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
                                       s_rowJ[wave], s_cand[wave], nullptr, ntot, wave, kListWaves, self, valid, &cnt,
                                       &pend);
-        {  // the last, partial word of the lane's segment
+        {  // the last, partial word of the lane's segment (its r entries sit in the top r slots: shift them down)
             constexpr int E = 8 / (int)sizeof(LE);
-            if (valid && cnt < a.list_cap && (cnt % E) != 0)
-                reinterpret_cast<uint2*>(a.list)[((size_t)wave * (a.list_cap / E) + cnt / E) * a.list_stride + s] = pend;
+            const int r = cnt % E;
+            if (valid && cnt < a.list_cap && r != 0)
+                reinterpret_cast<unsigned long long*>(a.list)[((size_t)wave * (a.list_cap / E) + cnt / E) * a.list_stride + s] =
+                    pend >> (8 * (int)sizeof(LE) * (E - r));
         }
         if (dbg && first && lane == 0) dbg[2 + wave] = wall_clock64();
         s_ovf[wave][lane] = cnt > a.list_cap ? 1 : 0;
@@ -3238,6 +3231,388 @@ __global__ __launch_bounds__(1024) void k_scan_small(const int* __restrict__ in,
     }
 }
 
+// ----------------------------------------------------------------------------------------------------
+// small systems (N <= kSmallMax: the mitotic stages' 586 / 1,172 particles of C3, the 1,002 of C1): ONE workgroup
+// runs a whole chunk of steps -- no kernel boundary, no grid-wide reduction, no atomics on the step path.  The
+// system lives in LDS (positions, per-particle constants, an LDS copy of the context); a step is: [list rebuild when
+// the skin is used up] -> forces of every particle from its neighbour list + the particle-local terms -> block
+// reductions (reactions, largest displacement) -> Euler-Maruyama update in LDS -> the schedule / wall ODE by thread
+// 0 (list_tail_apply on the LDS context).  At this size the multi-workgroup list step spends ~12 us per step on
+// launch, memory round trips and its cross-workgroup tail for ~10 workgroups of work.
+//
+// Neighbour lists (Verlet, the list step's skin): every partner within cutoff + skin of a particle at the build,
+// u16 particle indices in global memory [k][N], in the order of a cell scan of the build (cells ordered by
+// particle index: deterministic); rebuilt when 2 D + (cutoff growth) reaches 0.999 skin (D: the largest
+// displacement of any particle since the build, reduced every step), so a pair within the cutoff is always in the
+// lists -- the pair set is exact.  The build state (lists, build positions, the build's cell list, the context's
+// lgrid / lrc_b / ldisp) persists across launches: a chunked run rebuilds where one long run does (bitwise
+// identical).  A particle whose list overflowed kSmallCap is evaluated by a scan of the build's cells (exact by
+// the same bound).
+
+struct SmallArgs {
+    long long first_step;
+    int steps;
+    int flags;          // kLFlagSched | kLFlagStats
+    int force_build;    // the chunk starts without continuity: build before its first step
+    float skin;
+    unsigned short* list;   // [kSmallCap][N]
+    int* lcount;            // [N] count | kListOverflow
+    float4* bpos;           // [N] positions at the build
+    int* cstart;            // [kSmallCells + 1] the build's cell starts
+    unsigned short* cidx;   // [N] particles ordered by cell (index order inside a cell)
+    unsigned long long* dbg;  // optional (GCS_DEBUG_SMALL): thread 0's wall-clock totals per phase
+};
+
+constexpr int kSmallThreads = 1024;
+constexpr int kSmallWaves = kSmallThreads / 64;
+
+// block totals in one pass: K values per thread, value k summed, or maxed (bit k of MAXM), or minned (bit k of
+// MINM) -> thread 0, in a fixed order (DPP wave reductions, waves in index order); one barrier
+template <int K, unsigned MAXM, unsigned MINM>
+__device__ __forceinline__ void small_totals(float* v, float (*s_tmp)[kSmallWaves])
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const float w = ((MAXM >> k) & 1) ? wave_max(v[k]) : (((MINM >> k) & 1) ? wave_min(v[k]) : wave_sum(v[k]));
+        if (lane == 0) s_tmp[k][wave] = w;
+    }
+    __syncthreads();
+    if (tid == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            float r = s_tmp[k][0];
+            for (int q = 1; q < kSmallWaves; ++q)
+                r = ((MAXM >> k) & 1) ? fmaxf(r, s_tmp[k][q]) : (((MINM >> k) & 1) ? fminf(r, s_tmp[k][q]) : r + s_tmp[k][q]);
+            v[k] = r;
+        }
+    }
+}
+
+// the pair factors (a, b) particle j brings into a mixed pair (the list step's type_ab[class_j])
+__device__ __forceinline__ float2 small_ab(int pair_mix, float4 kj)
+{
+    return pair_mix ? make_float2(kj.y, kj.z) : make_float2(1.f, 0.f);
+}
+
+__global__ __launch_bounds__(kSmallThreads) void k_small(DevCtx* __restrict__ gctx, ForceArgs a, SmallArgs sa)
+{
+    __shared__ float4 s_pos[kSmallMax];
+    __shared__ float4 s_new[kSmallMax];
+    __shared__ float4 s_kmu[kSmallMax];
+    __shared__ int s_cnt[kSmallCells + 1];
+    __shared__ int s_fill[kSmallCells];
+    __shared__ unsigned short s_cidx[kSmallMax];
+    __shared__ unsigned short s_arr[kSmallMax];
+    __shared__ DevCtx s_ctx;
+    __shared__ double s_sched[kSchedCount];
+    __shared__ float s_red[10][kSmallWaves];
+    __shared__ int s_build;
+    const int tid = threadIdx.x;
+    const int n = a.n;
+    const int pair_mix = a.pair_mix;
+    const size_t N = (size_t)n;
+    const float skin = sa.skin;
+
+    // the system into LDS: the context, the schedule, the current positions, the per-particle constants
+    if (tid == 0) s_ctx = *gctx;
+    if (tid < kSchedCount) s_sched[tid] = a.sched[tid];
+    __syncthreads();
+    {
+        const float4* pcur = s_ctx.parity ? a.pos1 : a.pos0;
+        for (int i = tid; i < n; i += kSmallThreads) {
+            s_pos[i] = pcur[i];
+            s_kmu[i] = a.kmu[i];
+        }
+    }
+    // the local terms read positions through ForceArgs and the context through a pointer: both point into LDS
+    ForceArgs la = a;
+    la.pos0 = s_pos;
+    la.pos1 = s_pos;
+    la.kmu = s_kmu;
+    __syncthreads();
+
+    unsigned long long ph[5] = {0, 0, 0, 0, 0};  // GCS_DEBUG_SMALL: build, forces, totals, tail+barrier, builds
+    for (int k = 0; k < sa.steps; ++k) {
+        const unsigned long long t0 = sa.dbg ? wall_clock64() : 0;
+        // ---- rebuild the lists when the skin may be used up (or at a chunk start without continuity)
+        if (tid == 0) {
+            const float rc = pair_cutoff(a, s_ctx.cs);
+            const bool used = 2.f * s_ctx.ldisp + fmaxf(rc - s_ctx.lrc_b, 0.f) > 0.999f * skin;
+            s_build = (a.has_pair && ((k == 0 && sa.force_build) || used)) ? 1 : 0;
+        }
+        __syncthreads();
+        if (s_build) {
+            const float rcb = pair_cutoff(a, s_ctx.cs) + skin;
+            float lo[3] = {3.0e38f, 3.0e38f, 3.0e38f}, hi[3] = {-3.0e38f, -3.0e38f, -3.0e38f};
+            for (int i = tid; i < n; i += kSmallThreads) {
+                const float4 p = s_pos[i];
+                lo[0] = fminf(lo[0], p.x);
+                lo[1] = fminf(lo[1], p.y);
+                lo[2] = fminf(lo[2], p.z);
+                hi[0] = fmaxf(hi[0], p.x);
+                hi[1] = fmaxf(hi[1], p.y);
+                hi[2] = fmaxf(hi[2], p.z);
+            }
+            {
+                float bb[6] = {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]};
+                small_totals<6, 0x38u, 0x07u>(bb, s_red);
+                if (tid == 0) {
+                    for (int d = 0; d < 3; ++d) {
+                        s_ctx.bbox_lo[d] = bb[d];
+                        s_ctx.bbox_hi[d] = bb[3 + d];
+                    }
+                    s_ctx.lgrid = make_grid(s_ctx.bbox_lo, s_ctx.bbox_hi, rcb, kSmallCells, 1);
+                }
+            }
+            __syncthreads();
+            const Grid g = s_ctx.lgrid;
+            for (int c = tid; c <= g.ncell; c += kSmallThreads) {
+                s_cnt[c] = 0;
+                if (c < g.ncell) s_fill[c] = 0;
+            }
+            __syncthreads();
+            for (int i = tid; i < n; i += kSmallThreads) {
+                const float4 p = s_pos[i];
+                atomicAdd(&s_cnt[cell_index(g, p.x, p.y, p.z)], 1);
+            }
+            __syncthreads();
+            {  // exclusive scan of the counts -> cell starts: 5 consecutive cells per thread, DPP wave scans, wave totals
+                constexpr int kC = (kSmallCells + 1 + kSmallThreads - 1) / kSmallThreads;
+                const int c0 = kC * tid;
+                int v[kC], sum = 0;
+#pragma unroll
+                for (int q = 0; q < kC; ++q) {
+                    v[q] = c0 + q <= g.ncell ? s_cnt[c0 + q] : 0;
+                    sum += v[q];
+                }
+                int incl = sum;
+                GCS_DPP_SCAN(dpp_i, add_i, 0, incl)
+                const int lane = tid & 63, wave = tid >> 6;
+                __shared__ int s_wsum[kSmallWaves];
+                if (lane == 63) s_wsum[wave] = incl;
+                __syncthreads();
+                int base = 0;
+                for (int w = 0; w < wave; ++w) base += s_wsum[w];
+                int run = base + incl - sum;
+#pragma unroll
+                for (int q = 0; q < kC; ++q) {
+                    if (c0 + q <= g.ncell) s_cnt[c0 + q] = run;
+                    run += v[q];
+                }
+            }
+            __syncthreads();
+            // file every particle under its cell in arrival order, then rank it by index inside the cell
+            for (int i = tid; i < n; i += kSmallThreads) {
+                const float4 p = s_pos[i];
+                const int c = cell_index(g, p.x, p.y, p.z);
+                s_arr[s_cnt[c] + atomicAdd(&s_fill[c], 1)] = (unsigned short)i;
+            }
+            __syncthreads();
+            for (int i = tid; i < n; i += kSmallThreads) {
+                const float4 p = s_pos[i];
+                const int c = cell_index(g, p.x, p.y, p.z);
+                const int b = s_cnt[c], e = s_cnt[c + 1];
+                int r = 0;
+                for (int t = b; t < e; ++t) r += (s_arr[t] < i) ? 1 : 0;
+                s_cidx[b + r] = (unsigned short)i;
+            }
+            __syncthreads();
+            for (int c = tid; c <= g.ncell; c += kSmallThreads) sa.cstart[c] = s_cnt[c];
+            for (int i = tid; i < n; i += kSmallThreads) sa.cidx[i] = s_cidx[i];
+            // the lists: every particle within rcb of each particle at the build (27 cells, cell order)
+            const float rcb2 = rcb * rcb;
+            const int nx = g.n[0], ny = g.n[1], nz = g.n[2];
+            for (int i = tid; i < n; i += kSmallThreads) {
+                const float4 p = s_pos[i];
+                const int c = cell_index(g, p.x, p.y, p.z);
+                const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
+                int cnt = 0;
+                for (int z = max(cz - 1, 0); z <= min(cz + 1, nz - 1); ++z)
+                    for (int y = max(cy - 1, 0); y <= min(cy + 1, ny - 1); ++y) {
+                        const int base = (z * ny + y) * nx;
+                        const int jb = s_cnt[base + max(cx - 1, 0)], je = s_cnt[base + min(cx + 1, nx - 1) + 1];
+                        for (int t = jb; t < je; ++t) {
+                            const int j = s_cidx[t];
+                            if (j == i) continue;
+                            const float4 q = s_pos[j];
+                            const float dx = p.x - q.x, dy = p.y - q.y, dz = p.z - q.z;
+                            if (fmaf(dz, dz, fmaf(dy, dy, dx * dx)) < rcb2) {
+                                if (cnt < kSmallCap) sa.list[(size_t)cnt * N + i] = (unsigned short)j;
+                                ++cnt;
+                            }
+                        }
+                    }
+                sa.lcount[i] = min(cnt, kSmallCap) | (cnt > kSmallCap ? kListOverflow : 0);
+                sa.bpos[i] = p;
+            }
+            if (tid == 0) {
+                s_ctx.lrc_b = pair_cutoff(a, s_ctx.cs);
+                s_ctx.ldisp = 0.f;
+                s_ctx.lbuilds += 1;
+            }
+            __threadfence_block();  // the lists and build positions are read back by this block below
+            __syncthreads();
+        }
+
+        const unsigned long long t1 = sa.dbg ? wall_clock64() : 0;
+        if (sa.dbg && s_build) ph[4] += 1;
+        // ---- forces + update (each thread: particles tid, tid + 1024, ...; every lane active, so the local terms'
+        // wave-cooperative droplet sees whole waves; the lanes past N compute particle N - 1 and discard it)
+        const float cs = (float)s_ctx.cs;
+        const float scale = a.pair_scaled ? cs : 1.f;
+        const float sga = a.pa_sig * scale, sgb = a.pb_sig * scale;
+        const float k2a = 1.f / (sga * sga), k2b = 1.f / (sgb * sgb);
+        const float kA = 0.5f * 6.f * a.pa_eps * k2a, kB = 0.5f * 24.f * a.pb_eps * k2b;
+        const float rc = pair_cutoff(a, s_ctx.cs), rc2 = rc * rc;
+        float rin_s[3] = {0.f, 0.f, 0.f}, rout_s[3] = {0.f, 0.f, 0.f};
+        float dmax = 0.f, nbr_s = 0.f, nfb = 0.f;
+#pragma unroll 1
+        for (int q = 0; q * kSmallThreads < n; ++q) {  // uniform trip count
+            const int i0 = q * kSmallThreads + tid;
+            const bool valid = i0 < n;
+            const int i = valid ? i0 : n - 1;
+            const float4 pi = s_pos[i];
+            const float4 km = s_kmu[i];
+            float fx = 0.f, fy = 0.f, fz = 0.f, nbr = 0.f;
+            if (a.has_pair) {
+                const float2 own = small_ab(pair_mix, km);
+                const float ahi = kA * own.x, bhi = kB * own.y;
+                const int cw = sa.lcount[i];
+                const bool ovf = (cw & kListOverflow) != 0;
+                // (every lane of the wave takes part in the maximum: overflowed lanes count 0 entries)
+                const int cnt = ovf ? 0 : min(cw & kListCountMask, kSmallCap);
+                const int cmax = uniform(wave_max_int(cnt));
+                if (!ovf) {
+                    // batches of 8 entries: their loads are independent (one round trip per batch); entries past
+                    // the count read a clamped in-bounds slot and are masked
+                    for (int t0 = 0; t0 < cmax; t0 += 8) {
+                        int ej[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) ej[u] = sa.list[(size_t)min(t0 + u, kSmallCap - 1) * N + i];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) {
+                            const int j = min(ej[u], n - 1);
+                            list_pair(pi.x, pi.y, pi.z, s_pos[j], small_ab(pair_mix, s_kmu[j]), ahi, bhi, kA, kB, k2a,
+                                      k2b, rc2, t0 + u < cnt, fx, fy, fz, nbr);
+                        }
+                    }
+                } else {  // overflowed list: the build's cells around the current position, radius rc + D
+                    nfb += valid ? 1.f : 0.f;
+                    const Grid lg = s_ctx.lgrid;
+                    const float D = s_ctx.ldisp;
+                    const float R = rc + D + 1.0e-5f * (rc + D);
+                    const int x0 = lgrid_cell(lg, 0, pi.x - R), x1 = lgrid_cell(lg, 0, pi.x + R);
+                    const int y0 = lgrid_cell(lg, 1, pi.y - R), y1 = lgrid_cell(lg, 1, pi.y + R);
+                    const int z0 = lgrid_cell(lg, 2, pi.z - R), z1 = lgrid_cell(lg, 2, pi.z + R);
+                    for (int z = z0; z <= z1; ++z)
+                        for (int y = y0; y <= y1; ++y) {
+                            const int base = (z * lg.n[1] + y) * lg.n[0];
+                            const int t0 = sa.cstart[base + x0], t1 = sa.cstart[base + x1 + 1];
+                            for (int t = t0; t < t1; ++t) {
+                                const int j = sa.cidx[t];
+                                list_pair(pi.x, pi.y, pi.z, s_pos[j], small_ab(pair_mix, s_kmu[j]), ahi, bhi, kA, kB,
+                                          k2a, k2b, rc2, j != i, fx, fy, fz, nbr);
+                            }
+                        }
+                }
+            }
+            float en[kEnergyKinds];
+            float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
+            local_terms<kModeStep, GCS_LIST_BOND_BATCH>(&s_ctx, la, i, pi.x, pi.y, pi.z, km, fx, fy, fz, en, rin, rout);
+            float n0, n1, n2;
+            noise3(a, &s_ctx, i, n0, n1, n2);
+            const float mu = km.x, dt = a.timestep;
+            const float amp = sqrtf(2.f * a.temperature * mu * dt);
+            const float mdt = mu * dt;
+            const float4 np = make_float4(pi.x + mdt * fx + amp * n0, pi.y + mdt * fy + amp * n1,
+                                          pi.z + mdt * fz + amp * n2, 0.f);
+            if (valid) {
+                s_new[i] = np;
+                for (int d = 0; d < 3; ++d) {
+                    rin_s[d] += rin[d];
+                    rout_s[d] += rout[d];
+                }
+                nbr_s += nbr;
+                if (a.has_pair) {
+                    const float4 b = sa.bpos[i];
+                    const float gx = np.x - b.x, gy = np.y - b.y, gz = np.z - b.z;
+                    dmax = fmaxf(dmax, sqrtf(fmaf(gz, gz, fmaf(gy, gy, gx * gx))));
+                }
+            }
+        }
+        // ---- the step's totals (fixed order; the barrier inside also orders every force's reads of the old
+        // positions before the copy below), then the positions, then the context (thread 0)
+        const unsigned long long t2 = sa.dbg ? wall_clock64() : 0;
+        float tot[9] = {rin_s[0], rin_s[1], rin_s[2], rout_s[0], rout_s[1], rout_s[2], nbr_s, nfb, dmax};
+        small_totals<9, 0x100u, 0u>(tot, s_red);
+        const unsigned long long t3 = sa.dbg ? wall_clock64() : 0;
+        for (int i = tid; i < n; i += kSmallThreads) s_pos[i] = s_new[i];
+        if (tid == 0) {
+            ListTailIn tin;
+            tin.s_flags = s_sched[kSchedFlags];
+            tin.s_dt = s_sched[kSchedDt];
+            tin.s_cs0 = s_sched[kSchedCs0];
+            tin.s_csTau = s_sched[kSchedCsTau];
+            tin.s_bs0 = s_sched[kSchedBs0];
+            tin.s_bsTau = s_sched[kSchedBsTau];
+            tin.s_muW = s_sched[kSchedMuW];
+            for (int d = 0; d < 3; ++d) tin.s_k[d] = s_sched[kSchedK0 + d];
+            tin.c_step = s_ctx.step;
+            tin.c_cursor = s_ctx.noise_cursor;
+            tin.c_fb = s_ctx.lfallback;
+            tin.c_parity = s_ctx.parity;
+            tin.c_time = s_ctx.time;
+            tin.c_cs = s_ctx.cs;
+            tin.c_bs = s_ctx.bs;
+            for (int d = 0; d < 3; ++d) tin.c_w[d] = s_ctx.wall[d];
+            ListTotals t;
+            for (int d = 0; d < 6; ++d) t.react[d] = (double)tot[d];
+            t.nbr = (double)tot[6];
+            t.nfb = (long long)tot[7];
+            t.ld = tot[8];
+            list_tail_apply(&s_ctx, a, tin, t, sa.flags & (kLFlagSched | kLFlagStats));
+        }
+        __syncthreads();
+        if (sa.dbg) {
+            const unsigned long long t4 = wall_clock64();
+            ph[0] += t1 - t0;
+            ph[1] += t2 - t1;
+            ph[2] += t3 - t2;
+            ph[3] += t4 - t3;
+        }
+    }
+    if (sa.dbg && tid == 0)
+        for (int q = 0; q < 5; ++q) sa.dbg[q] = ph[q];
+    // ---- the state back: positions into the buffer the context now names current, the context
+    {
+        float4* pout = s_ctx.parity ? a.pos1 : a.pos0;
+        for (int i = tid; i < n; i += kSmallThreads) pout[i] = s_pos[i];
+    }
+    if (tid == 0) {
+        const DevCtx& c = s_ctx;
+        gctx->step = c.step;
+        gctx->parity = c.parity;
+        gctx->time = c.time;
+        gctx->cs = c.cs;
+        gctx->bs = c.bs;
+        for (int d = 0; d < 3; ++d) {
+            gctx->wall[d] = c.wall[d];
+            gctx->react_in[d] = c.react_in[d];
+            gctx->react_out[d] = c.react_out[d];
+            gctx->bbox_lo[d] = c.bbox_lo[d];
+            gctx->bbox_hi[d] = c.bbox_hi[d];
+        }
+        gctx->noise_cursor = c.noise_cursor;
+        gctx->neighbors = c.neighbors;
+        gctx->lgrid = c.lgrid;
+        gctx->lrc_b = c.lrc_b;
+        gctx->ldisp = c.ldisp;
+        gctx->lbuilds = c.lbuilds;
+        gctx->lfallback = c.lfallback;
+    }
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------------------------------------------
@@ -3403,6 +3778,25 @@ void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)
         launch_list_step_ct<true>(s, ctx, a, flags);
     else
         launch_list_step_ct<false>(s, ctx, a, flags);
+}
+
+void launch_small(hipStream_t s, DevCtx* ctx, const ForceArgs& a, long long first_step, int steps, int flags,
+                  int force_build, float skin, unsigned short* list, int* lcount, float4* bpos, int* cstart,
+                  unsigned short* cidx, unsigned long long* dbg)
+{
+    SmallArgs sa;
+    sa.first_step = first_step;
+    sa.steps = steps;
+    sa.flags = flags;
+    sa.force_build = force_build;
+    sa.skin = skin;
+    sa.list = list;
+    sa.lcount = lcount;
+    sa.bpos = bpos;
+    sa.cstart = cstart;
+    sa.cidx = cidx;
+    sa.dbg = dbg;
+    hipLaunchKernelGGL(k_small, dim3(1), dim3(kSmallThreads), 0, s, ctx, a, sa);
 }
 
 void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a)

@@ -38,6 +38,7 @@ OPT_LIST_SKIN = 10
 OPT_LIST_EVERY = 11
 OPT_LIST_CAP = 12
 OPT_LIST_WAVES = 13
+OPT_SMALL_PATH = 14
 
 ENERGY_KINDS = ("pair", "softwell", "bonds", "bending", "wall_in", "wall_out", "point_source", "kinetochore_fiber")
 
@@ -111,7 +112,7 @@ class ListStats(C.Structure):
 
 class RunStats(C.Structure):
     _fields_ = [("graph_launches", _i64), ("graph_steps", _i64), ("eager_steps", _i64), ("graphs_captured", _i64),
-                ("graphs_cached", _i64)]
+                ("graphs_cached", _i64), ("small_launches", _i64), ("small_steps", _i64)]
 
 
 # name -> (restype, argtypes); the exported surface of include/gcs.h

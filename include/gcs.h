@@ -352,6 +352,9 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
 #define GCS_OPT_LIST_CAP 12       /* list step: list entries per particle (default 1024; a longer list: exact search) */
 #define GCS_OPT_LIST_WAVES 13     /* list step: waves per 64-particle tile, 4 (default: lowest step latency) or 2 (more
                                      tiles resident: the better throughput when several trajectories share a GPU) */
+#define GCS_OPT_SMALL_PATH 14     /* 1: systems of <= 2,048 particles run every chunk of fixed-timestep steps in ONE
+                                     single-workgroup launch (Verlet lists rebuilt by displacement); 0 (default): the
+                                     list step's cached graphs (faster on C3's prometaphase / telophase) */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
 
 /* List-step diagnostics (the neighbour lists md::neighbor_searcher keeps between rebuilds; micromd, called at
@@ -380,6 +383,8 @@ typedef struct gcs_run_stats {
     int64_t eager_steps;      /* steps launched one by one */
     int64_t graphs_captured;  /* captures (a cache miss: new phase / parity / length, or changed settings) */
     int64_t graphs_cached;    /* captured sequences held now */
+    int64_t small_launches;   /* single-workgroup launches of the small-system path (GCS_OPT_SMALL_PATH) */
+    int64_t small_steps;      /* steps they ran */
 } gcs_run_stats;
 int gcs_engine_get_run_stats(gcs_engine* e, gcs_run_stats* out);
 

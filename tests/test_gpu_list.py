@@ -29,6 +29,7 @@ def _f32(x):
 def _list_engine(design, cfg, **opts):
     e, _ = interphase.build_interphase(Engine, design, cfg)
     e.set_option(A.OPT_FUSED_STEP, 3)
+    e.set_option(A.OPT_SMALL_PATH, 0)  # the multi-workgroup list step even at C1 size (tests/test_gpu_small.py: the other)
     for k, v in opts.items():
         e.set_option(getattr(A, "OPT_" + k.upper()), v)
     return e
@@ -126,8 +127,9 @@ def test_list_graph_eager_and_chunks_bitwise_identical(c1_design, every):
         assert c == runs[0][1]
 
 
+@pytest.mark.parametrize("small", [0, 1])
 @pytest.mark.parametrize("n", [1, 2, 63, 65, 200])
-def test_list_small_and_ragged_sizes(n):
+def test_list_small_and_ragged_sizes(n, small):
     """random ab factors and mobilities (several pair classes, mixed), 20 steps at dt 1e-4"""
     rng = np.random.default_rng(n)
     x = rng.uniform(-0.5, 0.5, size=(n, 3))
@@ -144,10 +146,12 @@ def test_list_small_and_ragged_sizes(n):
         s.set_positions(x)
         if name == "e":
             s.set_option(A.OPT_FUSED_STEP, 3)
+            s.set_option(A.OPT_SMALL_PATH, small)
         sysd[name] = s
     for s in sysd.values():
         s.run(20, seed=1, timestep=1e-4)
     assert sysd["e"].list_stats()["active"] == 1
+    assert (sysd["e"].run_stats()["small_steps"] == 20) == bool(small)
     assert np.abs(sysd["e"].get_positions() - sysd["o"].get_positions()).max() <= TOL_X
 
 
