@@ -1,16 +1,17 @@
 // domain.hip -- the band exchange of the spatial domain decomposition (C5; DESIGN.md "Multi-GPU").
 //
-// Every engine of a decomposed run holds all N particles by global index.  Domain d OWNS the particles whose z
-// lies in its slab [lo_d, hi_d) at the start of a step and integrates only those; its pair/bond terms read the
-// particles within `halo` of the slab (its region E_d = [lo_d - halo, hi_d + halo)), which must therefore be
-// fresh.  After every step each domain sends to every peer p the (index, new position) of each particle it owned
+// Every engine of a decomposed run holds all N particles by global index.  Domain d OWNS the particles that lie in
+// its box [lo_d, hi_d) (per axis; the boxes tile space) at the start of a step and integrates only those; its
+// pair/bond terms read the particles within `halo` of the box (its region E_d = [lo_d - halo, hi_d + halo)), which
+// must therefore be fresh.  After every step each domain sends to every peer p the (index, new position) of each particle it owned
 // whose old OR new position lies in E_p; the receiver writes both position buffers.  So every copy inside E_p is
 // refreshed each step, and a copy that goes stale was last sent from outside E_p (the "old or new" rule sends the
 // exit position), i.e. it is never mistaken for a particle within the cutoff of p's slab.  Bonded partners need
 // the same guarantee: every bond of an owned particle must be shorter than `halo` (checked here each step,
 // flags[0]; LAMMPS's "bond atom missing" condition).  Ownership hand-over needs no message: a particle that
-// crosses from slab d to slab p lands in E_p, is sent, and both sides then compute the same owner from the same
-// bits.
+// crosses from box d to box p lands in E_p, is sent, and both sides then compute the same owner from the same
+// bits.  The decomposed list step packs from its list slots (every owned particle has one: kDomFlagLost otherwise)
+// and the receiver refreshes the records' slots too (islot), so the pair gathers by slot see fresh ghosts.
 #include <hip/hip_runtime.h>
 
 #include "engine_internal.hpp"
@@ -18,61 +19,75 @@
 namespace gcs {
 namespace {
 
-// One thread per particle.  Records are float4 {x, y, z, index bits}, appended per peer with one atomic per wave
-// (order is irrelevant: the unpack is a scatter by index).  flags[0] |= 1: a bond (not the cut-off softwell) of an owned
-// particle reaches beyond the halo; flags[0] |= 2: a peer's band exceeded `cap`.
+// Records are float4 {x, y, z, index bits}, appended per peer with one atomic per wave (order is irrelevant: the
+// unpack is a scatter by index).  flags[0] |= 1: a bond (not the cut-off softwell) of an owned particle reaches beyond
+// the halo; flags[0] |= 2: a peer's band exceeded `cap`.
 // Band b's records are out[b * ostride + k], its count counts[b * cstride] (the engine-owned bands keep the count in
 // the band's header row: one message per peer carries both).
+// One lane per particle (slots == 0: every particle by index) or per list slot (slots != 0: the ctx->lnslots slots
+// of the decomposed list step's lists, the particle index in the record's .w), grid-stride with wave-uniform trips.
 __global__ __launch_bounds__(256) void k_domain_pack(const DevCtx* __restrict__ ctx, ForceArgs a,
-                                                     const float2* __restrict__ regions, int npeer,
+                                                     const DomBox* __restrict__ regions, int npeer,
                                                      float4* __restrict__ out, int* __restrict__ counts, int cap,
                                                      int* __restrict__ flags, const int* __restrict__ shared,
-                                                     int ostride, int cstride)
+                                                     int ostride, int cstride, int slots)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
     // after the step's tail: pos[parity] holds the new positions, pos[parity ^ 1] the step's start
     const float4* pnew = ctx->parity ? a.pos1 : a.pos0;
     const float4* pold = ctx->parity ? a.pos0 : a.pos1;
-    const bool in = i < a.n;
-    const float4 po = in ? pold[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const bool own = in && po.z >= a.dom_lo && po.z < a.dom_hi;
-    const float4 pn = own ? pnew[i] : po;
-    if (own && a.has_bonds && !(shared && shared[i])) {
-        const float h2 = a.dom_halo * a.dom_halo;
-        bool far = false;
-        for (int q = a.boff[i]; q < a.boff[i + 1]; ++q) {
-            const int2 en = a.bent[q];
-            if ((en.y & 15) == kSoftwell) continue;  // cut off below the halo (droplet): a pair term
-            if (shared && shared[en.x]) continue;          // shared particles are fresh everywhere
-            const float4 pj = pold[en.x];
-            const float dx = po.x - pj.x, dy = po.y - pj.y, dz = po.z - pj.z;
-            far |= dx * dx + dy * dy + dz * dz >= h2;
+    const float4* qnew = ctx->parity ? a.psort1 : a.psort0;
+    const float4* qold = ctx->parity ? a.psort0 : a.psort1;
+    const int total = slots ? ctx->lnslots : a.n;
+    const int stride = gridDim.x * blockDim.x;
+    for (int base = blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < total; base += stride) {
+        const int k = base + lane;
+        const bool in = k < total;
+        float4 po = make_float4(0.f, 0.f, 0.f, 0.f);
+        int i = 0;
+        if (in) {
+            po = slots ? qold[k] : pold[k];
+            i = slots ? (__float_as_int(po.w) & ((1 << kListIndexBits) - 1)) : k;
         }
-        if (far) atomicOr(&flags[0], 1);
-    }
-    for (int p = 0; p < npeer; ++p) {
-        const float2 r = regions[p];
-        const bool send = own && ((po.z >= r.x && po.z < r.y) || (pn.z >= r.x && pn.z < r.y));
-        const unsigned long long m = __ballot(send);
-        if (m == 0ull) continue;
-        int base = 0;
-        if (lane == 0) base = atomicAdd(&counts[(size_t)p * cstride], __popcll(m));
-        base = __shfl(base, 0);
-        if (send) {
-            const int o = base + __popcll(m & ((1ull << lane) - 1ull));
-            if (o < cap)
-                out[(size_t)p * ostride + o] = make_float4(pn.x, pn.y, pn.z, __int_as_float(i));
-            else
-                atomicOr(&flags[0], 2);
+        const bool own = in && box_has(a.dom, po.x, po.y, po.z);
+        const float4 pn = own ? (slots ? qnew[k] : pnew[k]) : po;
+        if (own && a.has_bonds && !(shared && shared[i])) {
+            const float h2 = a.dom_halo * a.dom_halo;
+            bool far = false;
+            for (int q = a.boff[i]; q < a.boff[i + 1]; ++q) {
+                const int2 en = a.bent[q];
+                if ((en.y & 15) == kSoftwell) continue;  // cut off below the halo (droplet): a pair term
+                if (shared && shared[en.x]) continue;    // shared particles are fresh everywhere
+                const float4 pj = pold[en.x];
+                const float dx = po.x - pj.x, dy = po.y - pj.y, dz = po.z - pj.z;
+                far |= dx * dx + dy * dy + dz * dz >= h2;
+            }
+            if (far) atomicOr(&flags[0], 1);
+        }
+        for (int p = 0; p < npeer; ++p) {
+            const DomBox r = regions[p];
+            const bool send = own && (box_has(r, po.x, po.y, po.z) || box_has(r, pn.x, pn.y, pn.z));
+            const unsigned long long m = __ballot(send);
+            if (m == 0ull) continue;
+            int at = 0;
+            if (lane == 0) at = atomicAdd(&counts[(size_t)p * cstride], __popcll(m));
+            at = __shfl(at, 0);
+            if (send) {
+                const int o = at + __popcll(m & ((1ull << lane) - 1ull));
+                if (o < cap)
+                    out[(size_t)p * ostride + o] = make_float4(pn.x, pn.y, pn.z, __int_as_float(i));
+                else
+                    atomicOr(&flags[0], 2);
+            }
         }
     }
 }
 
 // received bands: nbuf buffers of `cap` records, counts[b] valid in buffer b; both position buffers are written
+// (slots != 0: also the record's list slot in both slot-order buffers, when the current lists have one)
 __global__ __launch_bounds__(256) void k_domain_unpack(ForceArgs a, const float4* __restrict__ in,
                                                        const int* __restrict__ counts, int nbuf, int cap, int istride,
-                                                       int cstride)
+                                                       int cstride, int slots)
 {
     for (int b = 0; b < nbuf; ++b) {
         const int c = min(counts[(size_t)b * cstride], cap);
@@ -83,6 +98,12 @@ __global__ __launch_bounds__(256) void k_domain_unpack(ForceArgs a, const float4
             const float4 p = make_float4(r.x, r.y, r.z, 0.f);
             a.pos0[i] = p;
             a.pos1[i] = p;
+            const int sl = slots ? a.islot[i] : -1;
+            if (sl >= 0) {
+                const float4 q = make_float4(r.x, r.y, r.z, __int_as_float(i | (a.ptype[i] << kListIndexBits)));
+                a.psort0[sl] = q;
+                a.psort1[sl] = q;
+            }
         }
     }
 }
@@ -100,8 +121,8 @@ __global__ __launch_bounds__(64) void k_domain_shared_out(const DevCtx* __restri
     const float4* cur = ctx->parity ? a.pos1 : a.pos0;  // before the tail: the step's start
     const float4* nxt = ctx->parity ? a.pos0 : a.pos1;  // the owners' new positions
     const int i = idx[k];
-    const float z = cur[i].z;
-    const bool own = z >= a.dom_lo && z < a.dom_hi;
+    const float4 c = cur[i];
+    const bool own = box_has(a.dom, c.x, c.y, c.z);
     const float4 p = nxt[i];
     buf[kDomainRed + 3 * k] = own ? (double)p.x : 0.0;
     buf[kDomainRed + 3 * k + 1] = own ? (double)p.y : 0.0;
@@ -122,11 +143,13 @@ __global__ __launch_bounds__(64) void k_domain_shared_in(ForceArgs a, const int*
 
 }  // namespace
 
-void launch_domain_pack(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const float2* regions, int npeer,
-                        float4* out, int* counts, int cap, int* flags, const int* shared, int ostride, int cstride)
+void launch_domain_pack(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const DomBox* regions, int npeer,
+                        float4* out, int* counts, int cap, int* flags, const int* shared, int ostride, int cstride,
+                        int slots)
 {
-    hipLaunchKernelGGL(k_domain_pack, dim3((a.n + 255) / 256), dim3(256), 0, s, ctx, a, regions, npeer, out, counts,
-                       cap, flags, shared, ostride > 0 ? ostride : cap, cstride);
+    const int blocks = std::max(1, std::min(2048, (a.n + 255) / 256));
+    hipLaunchKernelGGL(k_domain_pack, dim3(blocks), dim3(256), 0, s, ctx, a, regions, npeer, out, counts, cap, flags,
+                       shared, ostride > 0 ? ostride : cap, cstride, slots);
 }
 
 void launch_domain_shared_out(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const int* idx, int nshared,
@@ -143,11 +166,11 @@ void launch_domain_shared_in(hipStream_t s, const ForceArgs& a, const int* idx, 
 }
 
 void launch_domain_unpack(hipStream_t s, const ForceArgs& a, const float4* in, const int* counts, int nbuf, int cap,
-                          int istride, int cstride)
+                          int istride, int cstride, int slots)
 {
     const int blocks = std::max(1, std::min(1024, (cap + 255) / 256));
     hipLaunchKernelGGL(k_domain_unpack, dim3(blocks), dim3(256), 0, s, a, in, counts, nbuf, cap,
-                       istride > 0 ? istride : cap, cstride);
+                       istride > 0 ? istride : cap, cstride, slots);
 }
 
 // zero the header rows (counts) of npeer bands of `stride` rows

@@ -178,11 +178,16 @@ struct gcs_engine {
     int c_bits_opt = 0;      // GCS_OPT_CONTACT_BITS (0: sized from N at the first update)
     // sampled positions (store quantisation)
     float* q_out = nullptr;
-    // spatial domain decomposition (gcs_engine_set_domain): slab [dom_lo, dom_hi) in z, halo, peer regions
+    // spatial domain decomposition (gcs_engine_set_domain): own box, halo, peer regions, domain index / count
     bool dom = false;
-    float dom_lo = 0.f, dom_hi = 0.f, dom_halo = 0.f;
-    float2* dom_regions = nullptr;  // device copy of the peers' regions [npeer] {lo - halo, hi + halo}
+    DomBox dom_box{};
+    float dom_halo = 0.f;
+    DomBox* dom_regions = nullptr;  // device copy of the peers' regions [npeer] (box - halo, box + halo)
     int dom_npeer = 0;
+    int dom_index = 0, dom_ndom = 1;
+    bool dom_list = false;  // the decomposed run takes the list step (decided when it is primed)
+    int dom_flags_step = 0;  // k_lstep flags of the last decomposed list step (its tail uses the same)
+    int* islot = nullptr;   // [n] particle -> slot of the current lists (-1: not binned), decomposed list step
     bool dom_cont = false;  // the next domain step continues the previous one (no re-priming)
     int* dom_shared_idx = nullptr;   // shared particles (gcs_engine_set_domain_shared) [nshared]
     int* dom_shared_flag = nullptr;  // [n] 1 = shared
@@ -203,7 +208,7 @@ struct gcs_engine {
     hipGraph_t dgraph = nullptr;
     int dg_steps = 0;
     gcs_bd_config dg_cfg{};
-    int dg_version = -1, dg_sched_flags = -1;
+    int dg_version = -1, dg_sched_flags = -1, dg_phase = -1;
 
     ForceArgs fa{};
     gcs_schedule sched{};
@@ -1323,6 +1328,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->tent);
     dfree(e->noise);
     dfree(e->dom_regions);
+    dfree(e->islot);
     dfree(e->dom_send);
     dfree(e->dom_recv);
     dfree(e->dom_red);
@@ -1960,7 +1966,33 @@ int gcs_engine_sample_positions(gcs_engine* e, float* xyz, int64_t n, int32_t fr
 
 // ---- spatial domain decomposition (C5) ----
 
-int gcs_engine_set_domain(gcs_engine* e, double lo, double hi, double halo, const double* peer_regions, int32_t npeer)
+namespace {
+float finite_f(double v) { return (float)std::min(std::max(v, -3.0e38), 3.0e38); }
+DomBox make_box(const double* lohi)
+{
+    DomBox b;
+    for (int k = 0; k < 3; ++k) {
+        b.lo[k] = finite_f(lohi[k]);
+        b.hi[k] = finite_f(lohi[3 + k]);
+    }
+    return b;
+}
+// a domain's region: its (fp32) box extended by the (fp32) halo.  Every engine derives its own region and its
+// peers' with this one formula, so a particle is inside a region bit-identically for the domain that bins by it
+// and for the owner that decides whether to send (a 1-ulp disagreement would leave a binned ghost stale)
+DomBox region_of(const DomBox& b, float halo)
+{
+    DomBox r;
+    for (int k = 0; k < 3; ++k) {
+        r.lo[k] = finite_f((double)b.lo[k] - (double)halo);
+        r.hi[k] = finite_f((double)b.hi[k] + (double)halo);
+    }
+    return r;
+}
+}  // namespace
+
+int gcs_engine_set_domain(gcs_engine* e, const double* box, double halo, const double* peer_boxes, int32_t npeer,
+                          int32_t index, int32_t ndomains)
 {
     if (!e) return fail(GCS_EINVAL, "null argument");
     if (!(halo > 0)) {  // off
@@ -1968,21 +2000,36 @@ int gcs_engine_set_domain(gcs_engine* e, double lo, double hi, double halo, cons
         e->dom_cont = false;
         return GCS_OK;
     }
-    if (!(lo < hi)) return fail(GCS_EINVAL, "domain slab must have lo < hi");
-    if (npeer < 0 || npeer > kMaxPeers || (npeer > 0 && !peer_regions)) return fail(GCS_EINVAL, "bad peer list");
+    if (!box) return fail(GCS_EINVAL, "null argument");
+    for (int k = 0; k < 3; ++k)
+        if (!(box[k] < box[3 + k])) return fail(GCS_EINVAL, "domain box must have lo < hi on every axis");
+    if (npeer < 0 || npeer > kMaxPeers || (npeer > 0 && !peer_boxes)) return fail(GCS_EINVAL, "bad peer list");
+    if (ndomains < 1 || ndomains > kMaxDomains || index < 0 || index >= ndomains)
+        return fail(GCS_EINVAL, "bad domain index / count");
     HIPCHK(hipSetDevice(e->device));
     int rc;
     if (!e->dom_regions && (rc = dalloc(&e->dom_regions, kMaxPeers))) return rc;
-    float2 h[kMaxPeers];
-    for (int p = 0; p < npeer; ++p) h[p] = make_float2((float)peer_regions[2 * p], (float)peer_regions[2 * p + 1]);
+    if (!e->dom_flags && (rc = dalloc(&e->dom_flags, 1))) return rc;
+    DomBox h[kMaxPeers] = {};
+    for (int p = 0; p < npeer; ++p) h[p] = region_of(make_box(peer_boxes + 6 * p), (float)halo);
     HIPCHK(hipMemcpyAsync(e->dom_regions, h, sizeof(h), hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    drop_domain_graph(e);  // the captured chunk holds the slab bounds and the peer count by value
+    drop_domain_graph(e);  // the captured chunk holds the box and the peer count by value
+    if (e->dom_red && e->dom_ndom != ndomains) {
+        // the allreduce buffer holds one slot per domain: set up again (gcs_engine_domain_buffers)
+        dfree(e->dom_send);
+        dfree(e->dom_recv);
+        dfree(e->dom_red);
+        dfree(e->dom_glob);
+        e->dom_nred = 0;
+        e->dom_cap = 0;
+    }
     e->dom = true;
-    e->dom_lo = (float)std::max(lo, -3.0e38);
-    e->dom_hi = (float)std::min(hi, 3.0e38);
+    e->dom_box = make_box(box);
     e->dom_halo = (float)halo;
     e->dom_npeer = npeer;
+    e->dom_index = index;
+    e->dom_ndom = ndomains;
     e->dom_cont = false;
     return GCS_OK;
 }
@@ -1999,7 +2046,7 @@ int gcs_engine_set_domain_shared(gcs_engine* e, const int64_t* idx, int32_t coun
         flag[h[k]] = 1;
     }
     drop_domain_graph(e);
-    if (e->dom_red && kDomainRed + 3 * count != e->dom_nred) {
+    if (e->dom_red && kDomainRed + 3 * count + e->dom_ndom != e->dom_nred) {
         // the allreduce buffer holds the shared positions: its size changes, so the exchange buffers must be
         // set up again (gcs_engine_domain_buffers) before the next decomposed run
         dfree(e->dom_send);
@@ -2030,15 +2077,62 @@ int gcs_engine_stream(gcs_engine* e, void** stream)
 }
 
 namespace {
-ForceArgs domain_args(const gcs_engine* e)
+// the decomposed step's argument block: the list step's (dom_list) or the tile step's, with the domain geometry, the
+// reduction layout (dom_red: the caller's buffer) and the flags
+ForceArgs domain_args(const gcs_engine* e, double* red = nullptr)
 {
-    ForceArgs a = e->fa;
+    ForceArgs a = e->dom_list ? list_args(e) : e->fa;
     a.dom_on = 1;
-    a.dom_lo = e->dom_lo;
-    a.dom_hi = e->dom_hi;
+    a.dom = e->dom_box;
     a.dom_halo = e->dom_halo;
     a.bucket_p = nullptr;
+    a.dom_red = red;
+    a.dom_dbase = kDomainRed + 3 * e->dom_nshared;
+    a.dom_index = e->dom_index;
+    a.dom_ndom = e->dom_ndom;
+    a.dom_flags = e->dom_flags;
+    a.islot = e->islot;
     return a;
+}
+
+DomBox dom_region(const gcs_engine* e) { return region_of(e->dom_box, e->dom_halo); }
+
+// the decomposed run takes the list step when the engine would (list step selected, lists admitted) and the halo
+// holds the list radius: a partner within the cutoff of an owned particle must have been binned at the build
+// (cutoff + skin at cs = 1; the tail checks cutoff + largest displacement every step, kDomFlagMotion)
+bool dom_list_ok(const gcs_engine* e)
+{
+    return list_path(e, false) && e->fa.has_pair && e->dom_halo >= e->fa.pair_dist + list_skin(e);
+}
+
+// the list-step half of a decomposed step before the allreduce: on a rebuild step the cells of this domain's region
+// (owned + ghosts) and the lists, then k_lstep<..., DOM> (owned slots; local reduction -> red), then the shared
+// particles' new positions into red
+void enqueue_dom_list_step(gcs_engine* e, int64_t st, double* red)
+{
+    const ForceArgs a = domain_args(e, red);
+    if (e->l_need_build || st % e->list_every == 0) {
+        const DomBox reg = dom_region(e);
+        launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], e->n, e->cell_of, e->slot, e->count, &reg,
+                          e->islot);
+        enqueue_scan(e, false);
+        launch_cell_scatter(e->stream, e->n, e->cell_of, e->slot, e->cstart, e->tmp, e->count);
+        launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, e->n, e->tmp, e->cell_of, e->cstart,
+                         e->sidx, e->scell, e->spos, e->sb, e->fa.pair_mix, e->ptype, e->psort[0], e->psort[1], e->skmu,
+                         e->sbrow, e->fa.has_bonds ? e->boff : nullptr, e->islot);
+        launch_list_build(e->stream, e->ctx, a);
+        e->l_need_build = false;
+    }
+    e->dom_flags_step = list_flags(e, st) | 8;  // 8: kLFlagDomain
+    launch_list_step(e->stream, e->ctx, a, e->dom_flags_step);
+    launch_domain_shared_out(e->stream, e->ctx, a, e->dom_shared_idx, e->dom_nshared, red);
+}
+
+// after the allreduce: the tail from the global sums, the shared particles in, the send bands' headers zeroed
+void enqueue_dom_list_finish(gcs_engine* e, const double* glob, float4* bands, int npeer)
+{
+    launch_list_domain_tail(e->stream, e->ctx, domain_args(e), glob, e->dom_flags_step & ~8, e->dom_shared_idx,
+                            e->dom_nshared, bands, npeer, e->dom_cap + 1);
 }
 }  // namespace
 
@@ -2051,8 +2145,12 @@ int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step
     if (int rc = flush_contacts(e)) return rc;
     HIPCHK(hipSetDevice(e->device));
     if (!(e->dom_cont && e->dom_next == step)) {
-        int rc = begin_run(e, cfg, step);
+        int rc = prepare(e);
         if (rc) return rc;
+        e->dom_list = dom_list_ok(e);
+        if (e->dom_list && !e->islot && (rc = dalloc(&e->islot, e->n))) return rc;
+        drop_domain_graph(e);  // captured for the other step shape, or another rebuild phase
+        if ((rc = begin_run(e, cfg, step))) return rc;
         // both position buffers hold the start state: a domain writes only what it owns or receives, so the
         // buffer the first step writes must already carry every other particle's copy
         HIPCHK(hipMemcpyAsync(e->pos[e->parity ^ 1], e->pos[e->parity], (size_t)e->n * sizeof(float4),
@@ -2061,10 +2159,15 @@ int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step
     e->chain_valid = false;
     e->small_cont = false;
     e->dom_next = step + 1;
+    if (e->dom_list) {
+        enqueue_dom_list_step(e, step, dev_reaction);
+        HIPCHK(hipGetLastError());
+        return GCS_OK;
+    }
     const ForceArgs a = domain_args(e);
     const int n = e->n;
-    launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count,
-                      e->dom_lo - e->dom_halo, e->dom_hi + e->dom_halo);
+    const DomBox reg = dom_region(e);
+    launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count, &reg);
     enqueue_scan(e, false);
     enqueue_sort(e);
     launch_force(e->stream, kModeStep, e->waves, e->ctx, a, false);
@@ -2079,11 +2182,15 @@ int gcs_engine_domain_finish(gcs_engine* e, const double* dev_reaction)
     if (!e || !dev_reaction) return fail(GCS_EINVAL, "null argument");
     if (!e->dom) return fail(GCS_ESTATE, "gcs_engine_set_domain first");
     HIPCHK(hipSetDevice(e->device));
-    ForceArgs a = domain_args(e);
-    a.ext_react = dev_reaction;
-    const int sb = step_grid(e);
-    launch_tail(e->stream, e->ctx, a, sb, sb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
-    launch_domain_shared_in(e->stream, a, e->dom_shared_idx, e->dom_nshared, dev_reaction);
+    if (e->dom_list) {
+        enqueue_dom_list_finish(e, dev_reaction, nullptr, 0);
+    } else {
+        ForceArgs a = domain_args(e);
+        a.ext_react = dev_reaction;
+        const int sb = step_grid(e);
+        launch_tail(e->stream, e->ctx, a, sb, sb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
+        launch_domain_shared_in(e->stream, a, e->dom_shared_idx, e->dom_nshared, dev_reaction);
+    }
     HIPCHK(hipGetLastError());
     e->parity ^= 1;
     e->dom_cont = true;
@@ -2098,7 +2205,7 @@ int gcs_engine_domain_pack(gcs_engine* e, float* dev_out, int32_t* dev_counts, i
     HIPCHK(hipSetDevice(e->device));
     if (e->dom_npeer > 0) HIPCHK(hipMemsetAsync(dev_counts, 0, e->dom_npeer * sizeof(int), e->stream));
     launch_domain_pack(e->stream, e->ctx, domain_args(e), e->dom_regions, e->dom_npeer, (float4*)dev_out, dev_counts,
-                       cap, dev_flags, e->dom_shared_flag);
+                       cap, dev_flags, e->dom_shared_flag, 0, 1, e->dom_list ? 1 : 0);
     HIPCHK(hipGetLastError());
     return GCS_OK;
 }
@@ -2108,7 +2215,8 @@ int gcs_engine_domain_unpack(gcs_engine* e, const float* dev_in, const int32_t* 
     if (!e || (nbuf > 0 && (!dev_in || !dev_counts))) return fail(GCS_EINVAL, "null argument");
     if (nbuf <= 0) return GCS_OK;
     HIPCHK(hipSetDevice(e->device));
-    launch_domain_unpack(e->stream, e->fa, (const float4*)dev_in, dev_counts, nbuf, cap);
+    launch_domain_unpack(e->stream, domain_args(e), (const float4*)dev_in, dev_counts, nbuf, cap, 0, 1,
+                         e->dom_list ? 1 : 0);
     HIPCHK(hipGetLastError());
     return GCS_OK;
 }
@@ -2126,7 +2234,7 @@ int gcs_engine_domain_buffers(gcs_engine* e, int32_t cap, int32_t* nred)
     dfree(e->dom_red);
     dfree(e->dom_glob);
     const size_t rows = (size_t)std::max(e->dom_npeer, 1) * (cap + 1);
-    const int nr = kDomainRed + 3 * e->dom_nshared;
+    const int nr = kDomainRed + 3 * e->dom_nshared + e->dom_ndom;
     int rc;
     if ((rc = dalloc(&e->dom_send, rows)) || (rc = dalloc(&e->dom_recv, rows)) || (rc = dalloc(&e->dom_red, nr)) ||
         (rc = dalloc(&e->dom_glob, nr)))
@@ -2147,22 +2255,39 @@ int gcs_engine_domain_buffers(gcs_engine* e, int32_t cap, int32_t* nred)
 
 namespace {
 
-// pack this step's bands into the send buffer (header rows zeroed first, counts land in them)
-void enqueue_band_pack(gcs_engine* e)
+// pack this step's bands into the send buffer (header rows zeroed first unless the tail did, counts land in them)
+void enqueue_band_pack(gcs_engine* e, bool headers_zeroed = false)
 {
     const int stride = e->dom_cap + 1;
-    launch_band_headers_zero(e->stream, e->dom_send, e->dom_npeer, stride);
+    if (!headers_zeroed) launch_band_headers_zero(e->stream, e->dom_send, e->dom_npeer, stride);
     launch_domain_pack(e->stream, e->ctx, domain_args(e), e->dom_regions, e->dom_npeer, e->dom_send + 1,
                        reinterpret_cast<int*>(e->dom_send), e->dom_cap, e->dom_flags, e->dom_shared_flag, stride,
-                       4 * stride);
+                       4 * stride, e->dom_list ? 1 : 0);
 }
 
 void enqueue_band_unpack(gcs_engine* e)
 {
     const int stride = e->dom_cap + 1;
     if (e->dom_npeer > 0)
-        launch_domain_unpack(e->stream, e->fa, e->dom_recv + 1, reinterpret_cast<const int*>(e->dom_recv), e->dom_npeer,
-                             e->dom_cap, stride, 4 * stride);
+        launch_domain_unpack(e->stream, domain_args(e), e->dom_recv + 1, reinterpret_cast<const int*>(e->dom_recv),
+                             e->dom_npeer, e->dom_cap, stride, 4 * stride, e->dom_list ? 1 : 0);
+}
+
+// one grouped send/recv of every peer's band (the count in its header row)
+int enqueue_band_exchange(gcs_engine* e)
+{
+    if (e->dom_npeer == 0) return GCS_OK;
+    const RcclApi* r = rccl();
+    const size_t cnt = (size_t)4 * (e->dom_cap + 1);
+    NCCLCHK(r->groupStart());
+    for (int p = 0; p < e->dom_npeer; ++p) {
+        NCCLCHK(r->send(e->dom_send + (size_t)p * (e->dom_cap + 1), cnt, ncclFloat, e->dom_peer_rank[p], e->nccl,
+                        e->stream));
+        NCCLCHK(r->recv(e->dom_recv + (size_t)p * (e->dom_cap + 1), cnt, ncclFloat, e->dom_peer_rank[p], e->nccl,
+                        e->stream));
+    }
+    NCCLCHK(r->groupEnd());
+    return GCS_OK;
 }
 
 // one decomposed step after its start (gcs_engine_domain_step primed the run): the domain kernels, the reaction
@@ -2170,10 +2295,23 @@ void enqueue_band_unpack(gcs_engine* e)
 int enqueue_rccl_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step)
 {
     const RcclApi* r = rccl();
+    if (e->dom_list) {
+        // list step: k_lstep<DOM> (+ rebuild) + shared out, allreduce, tail + shared in + headers, pack, exchange,
+        // unpack: 5 launches and 2 collectives per step
+        enqueue_dom_list_step(e, step, e->dom_red);
+        NCCLCHK(r->allReduce(e->dom_red, e->dom_glob, e->dom_nred, ncclDouble, ncclSum, e->nccl, e->stream));
+        enqueue_dom_list_finish(e, e->dom_glob, e->dom_send, e->dom_npeer);
+        enqueue_band_pack(e, true);
+        if (int rc = enqueue_band_exchange(e)) return rc;
+        enqueue_band_unpack(e);
+        HIPCHK(hipGetLastError());
+        (void)cfg;
+        return GCS_OK;
+    }
     const ForceArgs a = domain_args(e);
     const int n = e->n;
-    launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count,
-                      e->dom_lo - e->dom_halo, e->dom_hi + e->dom_halo);
+    const DomBox reg = dom_region(e);
+    launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count, &reg);
     enqueue_scan(e, false);
     enqueue_sort(e);
     launch_force(e->stream, kModeStep, e->waves, e->ctx, a, false);
@@ -2186,17 +2324,7 @@ int enqueue_rccl_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step)
     launch_tail(e->stream, e->ctx, f, sb, sb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
     launch_domain_shared_in(e->stream, f, e->dom_shared_idx, e->dom_nshared, e->dom_glob);
     enqueue_band_pack(e);
-    if (e->dom_npeer > 0) {
-        const size_t cnt = (size_t)4 * (e->dom_cap + 1);
-        NCCLCHK(r->groupStart());
-        for (int p = 0; p < e->dom_npeer; ++p) {
-            NCCLCHK(r->send(e->dom_send + (size_t)p * (e->dom_cap + 1), cnt, ncclFloat, e->dom_peer_rank[p], e->nccl,
-                            e->stream));
-            NCCLCHK(r->recv(e->dom_recv + (size_t)p * (e->dom_cap + 1), cnt, ncclFloat, e->dom_peer_rank[p], e->nccl,
-                            e->stream));
-        }
-        NCCLCHK(r->groupEnd());
-    }
+    if (int rc = enqueue_band_exchange(e)) return rc;
     enqueue_band_unpack(e);
     HIPCHK(hipGetLastError());
     (void)cfg;
@@ -2256,26 +2384,20 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
         NCCLCHK(r->allReduce(e->dom_red, e->dom_glob, e->dom_nred, ncclDouble, ncclSum, e->nccl, e->stream));
         if ((rc = gcs_engine_domain_finish(e, e->dom_glob))) return rc;
         enqueue_band_pack(e);
-        if (e->dom_npeer > 0) {
-            const size_t cnt = (size_t)4 * (e->dom_cap + 1);
-            NCCLCHK(r->groupStart());
-            for (int p = 0; p < e->dom_npeer; ++p) {
-                NCCLCHK(r->send(e->dom_send + (size_t)p * (e->dom_cap + 1), cnt, ncclFloat, e->dom_peer_rank[p],
-                                e->nccl, e->stream));
-                NCCLCHK(r->recv(e->dom_recv + (size_t)p * (e->dom_cap + 1), cnt, ncclFloat, e->dom_peer_rank[p],
-                                e->nccl, e->stream));
-            }
-            NCCLCHK(r->groupEnd());
-        }
+        if ((rc = enqueue_band_exchange(e))) return rc;
         enqueue_band_unpack(e);
         k = k0 = 1;  // gcs_engine_domain_finish flipped the host parity of this step
     }
-    // the rest: G-step chunks captured once into a graph (kernels and collectives), the remainder eagerly
-    const int G = e->graph_steps;
+    // the rest: G-step chunks captured once into a graph (kernels and collectives), the remainder eagerly.  The list
+    // step rebuilds at steps = 0 (mod M): its chunks are whole periods, captured for the rebuild phase they start at
+    const int M = e->dom_list ? e->list_every : 1;
+    const int G = e->graph_steps > 0 ? (e->graph_steps + M - 1) / M * M : 0;
+    const int phase = e->dom_list ? (int)((first_step + k) % M) : 0;
     if (G > 0 && steps - k >= G) {
         // (geometry, buffers, communicator and options drop the graph when they change: drop_domain_graph)
         const bool same = e->dgexec && e->dg_steps == G && std::memcmp(&e->dg_cfg, cfg, sizeof(*cfg)) == 0 &&
-                          e->dg_version == e->topo_version && e->dg_sched_flags == e->sched_flags;
+                          e->dg_version == e->topo_version && e->dg_sched_flags == e->sched_flags &&
+                          e->dg_phase == phase;
         if (!same) {
             drop_domain_graph(e);
             HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
@@ -2293,6 +2415,7 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
             e->dg_cfg = *cfg;
             e->dg_version = e->topo_version;
             e->dg_sched_flags = e->sched_flags;
+            e->dg_phase = phase;
             e->rstats.graphs_captured++;
         }
         for (; steps - k >= G; k += G) {

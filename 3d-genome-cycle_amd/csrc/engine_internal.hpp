@@ -78,7 +78,18 @@ struct DevCtx {
     float ldisp;
     long long lbuilds;
     long long lfallback;
+    int lnslots;  // slots of the current lists (binned particles: N, or a decomposed domain's owned + ghosts)
+    int pad5;
 };
+
+// an axis-aligned box [lo, hi) (a decomposed domain's own box, or a peer's region: its box extended by the halo)
+struct DomBox {
+    float lo[3], hi[3];
+};
+__host__ __device__ inline bool box_has(const DomBox& b, float x, float y, float z)
+{
+    return x >= b.lo[0] && x < b.hi[0] && y >= b.lo[1] && y < b.hi[1] && z >= b.lo[2] && z < b.hi[2];
+}
 
 enum BondType : int { kSemispring = 0, kHarmonic = 1, kSpring = 2, kSoftwell = 3 };
 
@@ -183,11 +194,19 @@ struct ForceArgs {
     int4* ovf_q;
     int* ovf_n;
     // spatial domain decomposition (C5; DESIGN.md "Multi-GPU"): every engine holds all N particles by global index;
-    // it integrates only the particles it OWNS (z in [dom_lo, dom_hi) at step start) and bins only those within
-    // dom_halo of its slab (owned + ghosts, refreshed every step by the owners' band exchange).  dom_on == 0: off.
+    // it integrates only the particles it OWNS (inside its box `dom` at step start) and bins only those within
+    // dom_halo of the box (owned + ghosts, refreshed every step by the owners' band exchange).  dom_on == 0: off.
     int dom_on;
-    float dom_lo, dom_hi, dom_halo;
+    DomBox dom;
+    float dom_halo;
     const double* ext_react;  // != nullptr: the step's wall reaction summed over all domains (allreduced), [6]
+    // decomposed list step: the local reduction goes to dom_red (layout kDomainRed), the per-domain slot of the
+    // largest displacement at dom_red[dom_dbase + dom_index] (dom_ndom slots: a sum-allreduce carries the max);
+    // islot[i]: particle i's slot in the current lists (-1: not binned), written by the rebuild
+    double* dom_red;
+    int dom_dbase, dom_index, dom_ndom;
+    int* dom_flags;
+    int* islot;
     // list step (GCS_OPT_FUSED_STEP 3; DESIGN.md "The list step"): per sorted slot s and wave w (w < 4) the
     // sorted slots of the pair partners found within build cutoff + list_skin are
     // list[(w * list_cap + k) * list_stride + s], k < count, count = lcount[w * list_stride + s] & kListCountMask
@@ -223,7 +242,7 @@ struct ForceArgs {
 // list step launch accumulators behind the arrival counters in ForceArgs::lticket (unsigned words, 128 B per slot):
 // per group of workgroups (b % 8) kListAccSlots slots + one overflow flag (kernels.hip list_accumulate)
 constexpr int kListAccBase = 32 * 9;
-constexpr int kListAccSlots = 15;
+constexpr int kListAccSlots = 16;
 constexpr int kListTicketWords = kListAccBase + 8 * 32 * (kListAccSlots + 1);
 // identity of accumulator slot k (what list_accumulate starts from)
 __host__ __device__ inline unsigned long long list_acc_identity(int k)
@@ -260,8 +279,9 @@ __host__ __device__ inline void philox4x32_10(unsigned c[4], unsigned k0, unsign
 
 // launch wrappers (kernels.hip)
 void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed, int ncell_max, const double* sched);
+// reg != nullptr: bin only the particles inside *reg (a decomposed domain's region); islot != nullptr: reset to -1
 void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n,
-                       int* cell_of, int* slot, int* count, float dom_lo = 0.f, float dom_hi = 0.f);
+                       int* cell_of, int* slot, int* count, const DomBox* reg = nullptr, int* islot = nullptr);
 void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start, int2* tile_range,
                       bool use_next = false, int4* units = nullptr, int resident = 0,
                       unsigned long long* scan_sync = nullptr, int ncell_max = 0);
@@ -280,11 +300,16 @@ void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, cons
                       int n, const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell,
                       float4* spos, float* sb, int pair_mix, const int* ptype = nullptr, float4* psort0 = nullptr,
                       float4* psort1 = nullptr, float4* skmu = nullptr, int2* sbrow = nullptr,
-                      const int* boff = nullptr);
+                      const int* boff = nullptr, int* islot = nullptr);
 // list step: build the neighbour lists on the current cell list (grid rc = cutoff + skin); one step from them
 void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a);
-// flags: 1 apply the schedule, 2 the next step rebuilds (bounding box -> grid), 4 neighbour-count statistics
+// flags: 1 apply the schedule, 2 the next step rebuilds (bounding box -> grid), 4 neighbour-count statistics,
+// 8 decomposed (a.dom_on): the owned slots only, the local reduction into a.dom_red instead of the tail
 void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags);
+// the decomposed list step's tail from the allreduced buffer glob (one workgroup), then the shared particles'
+// positions into both buffers (by index and by slot) and the send bands' header rows zeroed
+void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const double* glob, int flags,
+                             const int* shared, int nshared, float4* bands, int npeer, int band_stride);
 int list_step_grid(int n);
 // small systems (N <= kSmallMax): `steps` steps in one single-workgroup launch (kernels.hip k_small); its list state
 // (list [kSmallCap][N] u16, lcount [N], build positions [N], the build's cells [kSmallCells + 1] + [N]) persists
@@ -319,17 +344,28 @@ void sort_pairs_u64_u32(hipStream_t s, const unsigned long long* k_in, unsigned 
                         unsigned* v_out, int n, void* temp, size_t temp_bytes);
 void launch_quantize(hipStream_t s, const float4* pos, float* out, int n, int bits);
 // domain.hip: spatial decomposition (band pack / unpack) + the local partial reduction of a decomposed step
-constexpr int kMaxPeers = 16;
-constexpr int kDomainRed = 8;  // allreduce buffer: [0, 8) the local reduction, then 3 doubles per shared particle
-void launch_domain_pack(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const float2* regions, int npeer,
+constexpr int kMaxPeers = 32;
+constexpr int kMaxDomains = 256;
+// allreduce buffer: [0, kDomainRed) the local reduction (reactions in[3] out[3]; tile step: max drift, neighbours;
+// list step: neighbours, owned particles, fallback particles), then 3 doubles per shared particle, then (list step)
+// one slot per domain for the largest displacement from the build
+constexpr int kDomainRed = 10;
+// domain flags (gcs_engine_domain_flags)
+constexpr int kDomFlagBond = 1;      // a bond of an owned particle is longer than the halo
+constexpr int kDomFlagCapacity = 2;  // a band exceeded its capacity
+constexpr int kDomFlagLost = 4;      // a particle owned by no domain's lists (moved further than the halo allows)
+constexpr int kDomFlagMotion = 8;    // cutoff + largest displacement since the build exceeds the halo
+// pack: slots != 0 packs from the list slots (the decomposed list step), else by particle index
+void launch_domain_pack(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const DomBox* regions, int npeer,
                         float4* out, int* counts, int cap, int* flags, const int* shared, int ostride = 0,
-                        int cstride = 1);
+                        int cstride = 1, int slots = 0);
 void launch_band_headers_zero(hipStream_t s, float4* bands, int npeer, int stride);
 void launch_domain_shared_out(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const int* idx, int nshared,
                               double* buf);
 void launch_domain_shared_in(hipStream_t s, const ForceArgs& a, const int* idx, int nshared, const double* buf);
+// slots != 0 also refreshes the records' list slots (both psort buffers)
 void launch_domain_unpack(hipStream_t s, const ForceArgs& a, const float4* in, const int* counts, int nbuf, int cap,
-                          int istride = 0, int cstride = 1);
+                          int istride = 0, int cstride = 1, int slots = 0);
 void launch_tail_reduce(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int fblocks, double* out);
 
 inline int force_blocks(int n) { return (n + kTile - 1) / kTile; }

@@ -273,11 +273,12 @@ __global__ __launch_bounds__(1024) void k_prime(DevCtx* ctx, ForceArgs a, float 
     }
 }
 
-// dom_lo < dom_hi: bin only the particles with z in [dom_lo, dom_hi) (a domain's slab extended by its halo)
+// dom != 0: bin only the particles inside reg (a domain's box extended by its halo); islot: reset to -1 (k_cell_sort
+// writes the binned particles' slots)
 __global__ __launch_bounds__(256) void k_cell_count(const DevCtx* __restrict__ ctx, const float4* __restrict__ p0,
                                                     const float4* __restrict__ p1, int n, int* __restrict__ cell_of,
-                                                    int* __restrict__ slot, int* __restrict__ count, float dom_lo,
-                                                    float dom_hi)
+                                                    int* __restrict__ slot, int* __restrict__ count, int dom,
+                                                    DomBox reg, int* __restrict__ islot)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -285,7 +286,8 @@ __global__ __launch_bounds__(256) void k_cell_count(const DevCtx* __restrict__ c
     const Grid g = ctx->grid;
     const float4 p = pos[i];
     const int c = cell_index(g, p.x, p.y, p.z);
-    if (dom_lo < dom_hi && !(p.z >= dom_lo && p.z < dom_hi)) {  // domain: outside slab + halo, not binned
+    if (islot) islot[i] = -1;
+    if (dom && !box_has(reg, p.x, p.y, p.z)) {  // domain: outside its region, not binned
         cell_of[i] = -1;
         return;
     }
@@ -1189,7 +1191,8 @@ __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ct
                                                    float* __restrict__ sb, int pair_mix,
                                                    const int* __restrict__ ptype, float4* __restrict__ psort0,
                                                    float4* __restrict__ psort1, float4* __restrict__ skmu,
-                                                   int2* __restrict__ sbrow, const int* __restrict__ boff)
+                                                   int2* __restrict__ sbrow, const int* __restrict__ boff,
+                                                   int* __restrict__ islot)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n || s >= cstart[ctx->grid.ncell]) return;  // binned particles only (all of them, undecomposed)
@@ -1212,6 +1215,7 @@ __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ct
         (ctx->parity ? psort1 : psort0)[d] = make_float4(p.x, p.y, p.z, __int_as_float(i | (ptype[i] << kListIndexBits)));
         skmu[d] = k;
         sbrow[d] = boff ? make_int2(boff[i], boff[i + 1]) : make_int2(0, 0);
+        if (islot) islot[i] = d;
     }
 }
 
@@ -2063,7 +2067,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(FUSE
         // domain decomposition: this engine integrates the particles of its slab only; tiles of ghosts alone
         // (the halo's cell rows) are skipped whole (the same ballot in every wave: the waves share the lanes)
         // (the fused step kernels are never decomposed: compiled out there)
-        const bool own = FUSED || !a.dom_on || (pi.z >= a.dom_lo && pi.z < a.dom_hi);
+        const bool own = FUSED || !a.dom_on || box_has(a.dom, pi.x, pi.y, pi.z);
         if (!FUSED && a.dom_on && __ballot(valid && own) == 0ull) continue;
 
         float fx = 0.f, fy = 0.f, fz = 0.f, acc = 0.f;  // acc: pair energy (ENERGY) or neighbour count
@@ -2610,6 +2614,7 @@ struct ListTotals {
     double react[6];  // wall reactions in[3], out[3]
     double nbr;       // neighbour count (stats launches)
     long long nfb;    // fallback particles
+    long long nown;   // owned particles (decomposed launches)
     float ld;         // largest displacement from the build
     float bb[6];      // bbox lo[3], hi[3] (bbox launches)
 };
@@ -2618,6 +2623,7 @@ struct ListTotals {
 constexpr int kLFlagSched = 1;  // apply the device schedule (gcs_schedule)
 constexpr int kLFlagBBox = 2;   // the next step rebuilds: reduce the bounding box of the new positions -> its cell grid
 constexpr int kLFlagStats = 4;  // reduce the neighbour count (diagnostics: ctx->neighbors)
+constexpr int kLFlagDomain = 8;  // decomposed (k_lstep<..., DOM>): owned slots only, local reduction -> a.dom_red
 
 __device__ void list_tail_apply(DevCtx* ctx, const ForceArgs& a, const ListTailIn& in, const ListTotals& t, int flags)
 {
@@ -2668,7 +2674,8 @@ __device__ void list_tail_apply(DevCtx* ctx, const ForceArgs& a, const ListTailI
 //   7     max displacement from the build (>= 0): float bits, atomic max
 //   8     fallback particles             integer, added
 //   9-11  bbox lo, 12-14 bbox hi         order-preserving integer image of the float, atomic min / max (bbox launches)
-//   15    a reaction whose fixed-point image would not fit (non-finite or > 2^38): the totals carry a NaN reaction, as
+//   15    owned particles                integer, added (decomposed launches)
+//   16    a reaction whose fixed-point image would not fit (non-finite or > 2^38): the totals carry a NaN reaction, as
 //         a float sum would
 constexpr double kAccScale = 16777216.0;  // 2^24
 constexpr int kAccWords = kListAccSlots + 1;  // slots + the overflow flag, per group
@@ -2697,7 +2704,7 @@ __device__ __forceinline__ void acc_fold(unsigned* base, int k, float v)
         else
             __hip_atomic_fetch_or(reinterpret_cast<unsigned*>(acc_slot(base, kListAccSlots)), 1u, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
-    } else if (k == 6 || k == 8) {
+    } else if (k == 6 || k == 8 || k == 15) {
         __hip_atomic_fetch_add(w, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (k == 7) {
         __hip_atomic_fetch_max(w32, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2725,7 +2732,7 @@ __device__ void list_totals(unsigned* base, int ngroups, ListTotals& t)
     for (int g = 1; g < ngroups; ++g) {
         const unsigned long long* x = s_acc + g * kAccWords;
         for (int k = 0; k < kAccWords; ++k) {
-            if (k <= 6 || k == 8) v[k] += x[k];
+            if (k <= 6 || k == 8 || k == 15) v[k] += x[k];
             else if (k >= 9 && k < 12) v[k] = min((unsigned)v[k], (unsigned)x[k]);
             else if (k == kListAccSlots) v[k] |= x[k];
             else v[k] = max((unsigned)v[k], (unsigned)x[k]);
@@ -2737,6 +2744,7 @@ __device__ void list_totals(unsigned* base, int ngroups, ListTotals& t)
     t.nbr = (double)v[6];
     t.ld = __uint_as_float((unsigned)v[7]);
     t.nfb = (long long)v[8];
+    t.nown = (long long)v[15];
     for (int k = 0; k < 6; ++k) t.bb[k] = from_ordered((unsigned)v[9 + k]);
 }
 
@@ -2780,6 +2788,7 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
         // read by the list steps that follow (next launches); every block here reads ctx->grid only
         ctx->lgrid = ctx->grid;
         ctx->lrc_b = pair_cutoff(a, ctx->cs);
+        ctx->lnslots = a.cstart[ctx->grid.ncell];  // binned particles (N undecomposed)
         ctx->ldisp = 0.f;
         ctx->lbuilds += 1;
         ctx->nactive = 0;  // the list step's tail reads every workgroup's partial row
@@ -2873,7 +2882,10 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 //      displacement, fallbacks; bbox / neighbour count on flagged launches) into the group's accumulators.
 //      Waves 1.. (in parallel): the wall reactions into the accumulators
 //   5. (barrier) the two-level ticket; the final workgroup reads the accumulators and advances the context
-template <typename LE, int W, bool CT>
+// DOM (decomposed): a slot is integrated only when it belongs to this build (s < ctx->lnslots) and its
+// particle lies in the domain's box at the step start; the final workgroup writes the local reduction to a.dom_red
+// (the tail runs after the allreduce: k_ldom_tail)
+template <typename LE, int W, bool CT, bool DOM = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS_LIST_WAVES_PER_EU_CT : GCS_LIST_WAVES_PER_EU))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int flags)
 {
     __shared__ float red[W][4][kTile];
@@ -2917,6 +2929,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
 
     const int pk = __float_as_int(pi.w);
     const int i = pk & kIdx;
+    const bool act = DOM ? (valid && s < ctx->lnslots && box_has(a.dom, pi.x, pi.y, pi.z)) : valid;
     const float scale = a.pair_scaled ? cs : 1.f;
     const float sa = a.pa_sig * scale, sbb = a.pb_sig * scale;
     const float k2a = 1.f / (sa * sa), k2b = 1.f / (sbb * sbb);
@@ -2926,7 +2939,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     const float slack = 0.999f * a.list_skin - D - fmaxf(rc - lrc_b, 0.f);
     const float ex = pi.x - pb.x, ey = pi.y - pb.y, ez = pi.z - pb.z;
     const float di = sqrtf(fmaf(ez, ez, fmaf(ey, ey, ex * ex)));
-    const bool fb = valid && (di > slack || (cw & kListOverflow) != 0);
+    const bool fb = act && (di > slack || (cw & kListOverflow) != 0);
     // contacts (CT): the lists must cover the contact distance; a particle whose list does not is searched for its
     // contacts only (its forces take exactly the path they take without contacts: identical bits)
     const float rcc = CT ? fmaxf(rc, sqrtf(a.contact_d2)) : rc;
@@ -2940,8 +2953,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
         local_terms<kModeStep, GCS_LIST_BOND_BATCH>(ctx, a, i, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout, erow);
         s_locf[lane] = make_float4(lfx, lfy, lfz, km.x);
-        s_locr[lane] = make_float4(valid ? rin[0] : 0.f, valid ? rin[1] : 0.f, valid ? rin[2] : 0.f, 0.f);
-        s_loco[lane] = make_float4(valid ? rout[0] : 0.f, valid ? rout[1] : 0.f, valid ? rout[2] : 0.f, 0.f);
+        s_locr[lane] = make_float4(act ? rin[0] : 0.f, act ? rin[1] : 0.f, act ? rin[2] : 0.f, 0.f);
+        s_loco[lane] = make_float4(act ? rout[0] : 0.f, act ? rout[1] : 0.f, act ? rout[2] : 0.f, 0.f);
     }
 
     // 3. the wave's list segment
@@ -2950,7 +2963,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     const float ahi = kA * own.x, bhi = kB * own.y;
     if (dbg && tid == 0) dbg[1] = wall_clock64();
     if (a.has_pair) {
-        const int cnt = (valid && !fb) ? min(cw & kListCountMask, cap) : 0;
+        const int cnt = (act && !fb) ? min(cw & kListCountMask, cap) : 0;
         const int kmax = uniform(wave_max_int(cnt));
         // batches of kU entries: the partners' gathers are issued first, then the next batch's entry words (they
         // return right behind the gathers, so each batch costs one round trip), then the pair forces (and contacts)
@@ -3084,7 +3097,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         const float nxp = pi.x + mdt * fsx + amp * xi.x;
         const float nyp = pi.y + mdt * fsy + amp * xi.y;
         const float nzp = pi.z + mdt * fsz + amp * xi.z;
-        if (valid) {
+        if (act) {
             float4* __restrict__ pn = par ? a.pos0 : a.pos1;  // particle order (bonded partners read ctx->parity's)
             float4* __restrict__ qn = par ? a.psort0 : a.psort1;
             pn[i] = make_float4(nxp, nyp, nzp, 0.f);
@@ -3092,25 +3105,27 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         }
         if (dbg && tid == 0) dbg[4] = wall_clock64();
         const float gx = nxp - pb.x, gy = nyp - pb.y, gz = nzp - pb.z;
-        const float dmax = wave_max(valid ? sqrtf(fmaf(gz, gz, fmaf(gy, gy, gx * gx))) : 0.f);
+        const float dmax = wave_max(act ? sqrtf(fmaf(gz, gz, fmaf(gy, gy, gx * gx))) : 0.f);
         const float nfb = (float)__popcll(__ballot(fb));
+        const float nact = DOM ? (float)__popcll(__ballot(act)) : 0.f;  // (ballots outside the lane branches)
         float v = 0.f;  // lane k: the value of accumulator slot k this wave owns
         if (flags & kLFlagStats) {
-            const float nt = wave_sum(valid ? ns : 0.f);
+            const float nt = wave_sum(act ? ns : 0.f);
             if (lane == 6) v = nt;
         }
         if (flags & kLFlagBBox) {
             const float big = 3.0e38f;
-            const float l0 = wave_min(valid ? nxp : big), l1 = wave_min(valid ? nyp : big),
-                        l2 = wave_min(valid ? nzp : big);
-            const float h0 = wave_max(valid ? nxp : -big), h1 = wave_max(valid ? nyp : -big),
-                        h2 = wave_max(valid ? nzp : -big);
+            const float l0 = wave_min(act ? nxp : big), l1 = wave_min(act ? nyp : big),
+                        l2 = wave_min(act ? nzp : big);
+            const float h0 = wave_max(act ? nxp : -big), h1 = wave_max(act ? nyp : -big),
+                        h2 = wave_max(act ? nzp : -big);
             v = lane == 9 ? l0 : lane == 10 ? l1 : lane == 11 ? l2 : lane == 12 ? h0 : lane == 13 ? h1 : lane == 14 ? h2 : v;
         }
         if (lane == 7) v = dmax;
         if (lane == 8) v = nfb;
+        if (DOM && lane == 15) v = nact;
         const bool mine = lane == 7 || lane == 8 || ((flags & kLFlagStats) && lane == 6) ||
-                          ((flags & kLFlagBBox) && lane >= 9 && lane < 15);
+                          ((flags & kLFlagBBox) && lane >= 9 && lane < 15) || (DOM && lane == 15);
         if (mine) acc_fold(acc, lane, v);
     } else {
         // the wall reactions: waves 1.. take the six components in turn (W = 4: wave 1 inward, wave 2 outward)
@@ -3152,14 +3167,79 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     unsigned long long* const dbt = a.dbg_times ? a.dbg_times + 8 * gridDim.x : nullptr;
     if (dbt && tid == 0) dbt[0] = wall_clock64();
     ListTailIn tin;
-    if (tid == 0) tin = list_tail_load(ctx, a);  // in flight during the accumulator reads
+    if (!DOM && tid == 0) tin = list_tail_load(ctx, a);  // in flight during the accumulator reads
     ListTotals tot;
     list_totals(a.lticket + kListAccBase, ngroups, tot);
     if (tid != 0) return;
     if (dbt) dbt[1] = wall_clock64();
     a.lticket[32 * 8] = 0u;
+    if constexpr (DOM) {
+        // the local reduction (layout kDomainRed); this domain's largest displacement in its own slot
+        double* r = a.dom_red;
+        for (int k = 0; k < 6; ++k) r[k] = tot.react[k];
+        r[6] = tot.nbr;
+        r[7] = (double)tot.nown;
+        r[8] = (double)tot.nfb;
+        r[9] = 0.0;
+        for (int q = 0; q < a.dom_ndom; ++q) r[a.dom_dbase + q] = q == a.dom_index ? (double)tot.ld : 0.0;
+        if ((flags & kLFlagBBox) && tot.nown > 0)  // the local box of the next build (k_ldom_tail pads it)
+            for (int k = 0; k < 3; ++k) {
+                ctx->bbox_lo[k] = tot.bb[k];
+                ctx->bbox_hi[k] = tot.bb[3 + k];
+            }
+        return;
+    }
     list_tail_apply(ctx, a, tin, tot, flags);
     if (dbg) dbg[7] = wall_clock64();
+}
+
+// The decomposed list step's tail (one workgroup, after the allreduce of every domain's k_lstep<..., DOM> reduction):
+// the same context update as the undecomposed step's final workgroup from the global sums (reactions, neighbours,
+// fallbacks) and the largest of the domains' displacement slots; the next build's grid is this domain's owned bbox
+// padded by the halo (ghosts beyond it are clamped into the edge cells, which is still exact).  Checks: every
+// particle owned by some domain's lists (kDomFlagLost), cutoff + largest displacement within the halo
+// (kDomFlagMotion).  Then the shared particles' allreduced positions into both buffers, by index and by slot, and the
+// send bands' header rows zeroed for the pack.
+__global__ __launch_bounds__(64) void k_ldom_tail(DevCtx* __restrict__ ctx, ForceArgs a, const double* __restrict__ glob,
+                                                  int flags, const int* __restrict__ shared, int nshared,
+                                                  float4* __restrict__ bands, int npeer, int bstride)
+{
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        const ListTailIn tin = list_tail_load(ctx, a);
+        ListTotals t;
+        for (int k = 0; k < 6; ++k) t.react[k] = glob[k];
+        t.nbr = glob[6];
+        const long long nown = (long long)glob[7];
+        t.nfb = (long long)glob[8];
+        t.nown = nown;
+        float ld = 0.f;
+        for (int q = 0; q < a.dom_ndom; ++q) ld = fmaxf(ld, (float)glob[a.dom_dbase + q]);
+        t.ld = ld;
+        for (int k = 0; k < 3; ++k) {
+            t.bb[k] = ctx->bbox_lo[k] - a.dom_halo;
+            t.bb[3 + k] = ctx->bbox_hi[k] + a.dom_halo;
+        }
+        list_tail_apply(ctx, a, tin, t, flags);
+        int fl = nown != (long long)a.n ? kDomFlagLost : 0;
+        if (pair_cutoff(a, ctx->cs) + ld > a.dom_halo) fl |= kDomFlagMotion;
+        if (fl) atomicOr(a.dom_flags, fl);
+    }
+    constexpr int kIdx = (1 << kListIndexBits) - 1;
+    for (int k = tid; k < nshared; k += blockDim.x) {
+        const int i = shared[k];
+        const float x = (float)glob[kDomainRed + 3 * k], y = (float)glob[kDomainRed + 3 * k + 1],
+                    z = (float)glob[kDomainRed + 3 * k + 2];
+        a.pos0[i] = make_float4(x, y, z, 0.f);
+        a.pos1[i] = make_float4(x, y, z, 0.f);
+        const int sl = a.islot[i];
+        if (sl >= 0) {
+            const float4 q = make_float4(x, y, z, __int_as_float((i & kIdx) | (a.ptype[i] << kListIndexBits)));
+            a.psort0[sl] = q;
+            a.psort1[sl] = q;
+        }
+    }
+    for (int p = tid; p < npeer; p += blockDim.x) bands[(size_t)p * bstride] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 // ----------------------------------------------------------------------------------------------------
@@ -3624,10 +3704,11 @@ void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed
 }
 
 void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n, int* cell_of,
-                       int* slot, int* count, float dom_lo, float dom_hi)
+                       int* slot, int* count, const DomBox* reg, int* islot)
 {
+    const DomBox r = reg ? *reg : DomBox{};
     hipLaunchKernelGGL(k_cell_count, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, n, cell_of, slot, count,
-                       dom_lo, dom_hi);
+                       reg ? 1 : 0, r, islot);
 }
 
 void launch_tail_reduce(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int fblocks, double* out)
@@ -3696,10 +3777,10 @@ void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* sl
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, const float4* kmu, int n,
                       const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell, float4* spos,
                       float* sb, int pair_mix, const int* ptype, float4* psort0, float4* psort1, float4* skmu,
-                      int2* sbrow, const int* boff)
+                      int2* sbrow, const int* boff, int* islot)
 {
     hipLaunchKernelGGL(k_cell_sort, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, kmu, n, tmp, cell_of,
-                       cstart, sidx, scell, spos, sb, pair_mix, ptype, psort0, psort1, skmu, sbrow, boff);
+                       cstart, sidx, scell, spos, sb, pair_mix, ptype, psort0, psort1, skmu, sbrow, boff, islot);
 }
 
 template <int MODE, bool FUSED>
@@ -3774,10 +3855,32 @@ static void launch_list_step_ct(hipStream_t s, DevCtx* ctx, const ForceArgs& a, 
 
 void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)
 {
+    if (flags & kLFlagDomain) {  // decomposed (no fused contacts: the engine flushes them before a decomposed step)
+        const dim3 g(list_step_grid(a.n));
+        if (list_u16(a.n)) {
+            if (a.list_waves == 2)
+                hipLaunchKernelGGL((k_lstep<unsigned short, 2, false, true>), g, dim3(128), 0, s, ctx, a, flags);
+            else
+                hipLaunchKernelGGL((k_lstep<unsigned short, 4, false, true>), g, dim3(256), 0, s, ctx, a, flags);
+        } else {
+            if (a.list_waves == 2)
+                hipLaunchKernelGGL((k_lstep<int, 2, false, true>), g, dim3(128), 0, s, ctx, a, flags);
+            else
+                hipLaunchKernelGGL((k_lstep<int, 4, false, true>), g, dim3(256), 0, s, ctx, a, flags);
+        }
+        return;
+    }
     if (a.contact_on)
         launch_list_step_ct<true>(s, ctx, a, flags);
     else
         launch_list_step_ct<false>(s, ctx, a, flags);
+}
+
+void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const double* glob, int flags,
+                             const int* shared, int nshared, float4* bands, int npeer, int band_stride)
+{
+    hipLaunchKernelGGL(k_ldom_tail, dim3(1), dim3(64), 0, s, ctx, a, glob, flags, shared, nshared, bands, npeer,
+                       band_stride);
 }
 
 void launch_small(hipStream_t s, DevCtx* ctx, const ForceArgs& a, long long first_step, int steps, int flags,

@@ -155,7 +155,7 @@ PROTOTYPES = {
     "gcs_engine_contacts_read": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), _i64, C.POINTER(_i64)]),
     "gcs_engine_contacts_clear": (C.c_int, [C.c_void_p]),
     "gcs_engine_sample_positions": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), _i64, _i32]),
-    "gcs_engine_set_domain": (C.c_int, [C.c_void_p, _d, _d, _d, _pd, _i32]),
+    "gcs_engine_set_domain": (C.c_int, [C.c_void_p, _pd, _d, _pd, _i32, _i32, _i32]),
     "gcs_engine_stream": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
     "gcs_engine_set_domain_shared": (C.c_int, [C.c_void_p, C.POINTER(_i64), _i32]),
     "gcs_engine_domain_step": (C.c_int, [C.c_void_p, C.POINTER(BDConfig), _i64, C.c_void_p]),

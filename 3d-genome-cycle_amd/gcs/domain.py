@@ -1,20 +1,24 @@
 """Spatial domain decomposition of ONE trajectory over several devices (C5; DESIGN.md "Multi-GPU").
 
 The reference integrates one system on one thread (md::simulate_brownian_dynamics called from
-stage_interphase/simulation_driver_interphase.cpp:57-63); this module splits one such system into z-slabs, one per
+stage_interphase/simulation_driver_interphase.cpp:57-63); this module splits one such system into boxes, one per
 domain (one GPU per rank in production), and keeps the reference's per-step order: force evaluation, Euler-Maruyama
 update, then the callback's schedule with the wall update from the step's reaction (:51-52, :80-90), where the
-reaction is now the SUM over domains (one allreduce of 6 doubles per step).
+reaction is now the SUM over domains (one allreduce per step).
+
+Geometry: `plan_boxes` bisects the particles recursively (k-d style: each cut along the longest extent of the
+particles it splits, at the count quantile), so 8 domains are 2 x 2 x 2 blocks of equal bead counts whose sides stay
+several halos thick; `plan_slabs` cuts z only.  The boxes tile space (outer faces at +-inf).
 
 Protocol (kernels in csrc/domain.hip, which proves the invariants):
-  * every domain holds all N particles by global index; domain d OWNS the particles whose z lies in its slab
-    [lo_d, hi_d) at the start of a step and integrates only those (Philox noise is keyed by the global index, so a
-    particle draws the same noise whichever domain owns it);
-  * domain d bins only the particles inside its region E_d = [lo_d - halo, hi_d + halo); `halo` exceeds the pair
-    cutoff, the droplet cutoff and the longest bond (the pack kernel checks the bonds every step);
-  * after every step d sends each peer p the owned particles whose old or new z lies in E_p; p writes them into
-    both of its position buffers.  Peers are the domains whose regions overlap (possibly more than the two
-    neighbours when slabs are thinner than the halo).
+  * every domain holds all N particles by global index; domain d OWNS the particles inside its box [lo_d, hi_d) at
+    the start of a step and integrates only those (Philox noise is keyed by the global index, so a particle draws
+    the same noise whichever domain owns it);
+  * domain d bins only the particles inside its region E_d = [lo_d - halo, hi_d + halo); `halo` exceeds the list
+    radius (pair cutoff + skin), the droplet cutoff and the longest bond (the pack kernel checks the bonds every
+    step, the list step's tail the displacement since the last build);
+  * after every step d sends each peer p the owned particles whose old or new position lies in E_p; p writes them
+    into both of its position buffers (and its list slots).  Peers are the domains whose regions overlap.
 
 Every exchange buffer is the engine's own (gcs_engine_domain_buffers): a band per peer whose first row holds its
 count, so one message per peer carries both, and the reaction/shared-position buffer of the allreduce.
@@ -37,35 +41,89 @@ from .config import InterphaseConfig
 
 FLAG_BOND = 1       # a bond of an owned particle is longer than the halo (its partner may be stale)
 FLAG_CAPACITY = 2   # a band exceeded the exchange buffer capacity
+FLAG_LOST = 4       # a particle owned by no domain's lists (it moved further than the halo between list builds)
+FLAG_MOTION = 8     # pair cutoff + largest displacement since the last list build exceeds the halo
 
 
 class DomainError(RuntimeError):
     pass
 
 
+def _f32(v):
+    """a cut the device compares exactly (its boxes are fp32)"""
+    return float(np.float32(v))
+
+
+def _open_box():
+    return (np.full(3, -np.inf), np.full(3, np.inf))
+
+
 def plan_slabs(z, ndom: int):
-    """Equal-count z-slabs of the current positions: [(lo, hi)] with open outer ends."""
+    """Equal-count z-slabs of the current positions as boxes [(lo[3], hi[3])], x and y open, outer z ends open."""
     z = np.asarray(z, dtype=np.float64)
     if ndom < 1:
         raise ValueError("need at least one domain")
     cuts = np.quantile(z, np.arange(1, ndom) / ndom) if ndom > 1 else np.array([])
-    edges = np.concatenate([[-np.inf], cuts, [np.inf]])
-    return [(float(edges[d]), float(edges[d + 1])) for d in range(ndom)]
+    edges = np.concatenate([[-np.inf], [_f32(c) for c in cuts], [np.inf]])
+    out = []
+    for d in range(ndom):
+        lo, hi = _open_box()
+        lo[2], hi[2] = edges[d], edges[d + 1]
+        out.append((lo, hi))
+    return out
+
+
+def plan_boxes(x, ndom: int):
+    """Recursive bisection of the current positions into `ndom` boxes of equal particle counts (+-1): each cut runs
+    across the longest extent of the particles it splits, at the count quantile k1 / k (k1 = k // 2 of the k domains
+    go below it).  8 domains of a compact nucleus are 2 x 2 x 2 blocks.  Boxes [(lo[3], hi[3])], outer faces open."""
+    x = np.asarray(x, dtype=np.float64)[:, :3]
+    if ndom < 1:
+        raise ValueError("need at least one domain")
+    out = []
+
+    def split(idx, lo, hi, k):
+        if k == 1:
+            out.append((lo.copy(), hi.copy()))
+            return
+        if idx.size < k:
+            raise ValueError("fewer particles than domains")
+        pts = x[idx]
+        ax = int(np.argmax(pts.max(axis=0) - pts.min(axis=0)))
+        k1 = k // 2
+        v = np.sort(pts[:, ax])
+        m = min(max(int(round(v.size * k1 / k)), 1), v.size - 1)
+        cut = _f32(0.5 * (v[m - 1] + v[m]))
+        below = x[idx, ax] < cut
+        hi1 = hi.copy()
+        hi1[ax] = cut
+        lo2 = lo.copy()
+        lo2[ax] = cut
+        split(idx[below], lo, hi1, k1)
+        split(idx[~below], lo2, hi, k - k1)
+
+    split(np.arange(x.shape[0]), *_open_box(), ndom)
+    return out
 
 
 BOND_SIGMAS = 7.5  # a chain bond stretched beyond this many thermal widths: ~1e-11 per bond-step
 
 
-def domain_halo(cfg: InterphaseConfig, margin: float = 0.05) -> float:
-    """The reach a domain must see fresh beyond its slab: the pair cutoff at core_scale 1
-    (simulation_driver_forcefield.cpp:25-28) and the chain bonds' reach l + 7.5 sqrt(T / K) at bond_scale 1
-    (:71-83; semispring, INFERRED form), plus a margin for one step's displacement.  The nucleolar bonds and the
-    droplet act among SHARED particles only (shared_particles), which every domain holds fresh."""
+LIST_SKIN = 0.4  # the list step's skin / pair cutoff (GCS_OPT_LIST_SKIN default 400 per mille)
+
+
+def domain_halo(cfg: InterphaseConfig, margin: float = 0.05, list_skin: float = LIST_SKIN) -> float:
+    """The reach a domain must see fresh beyond its box: the list radius, pair cutoff at core_scale 1
+    (simulation_driver_forcefield.cpp:25-28) + the list skin (list_skin x cutoff; 0: the tile step's halo), and the
+    chain bonds' reach l + 7.5 sqrt(T / K) at bond_scale 1 (:71-83; semispring, INFERRED form), plus a margin for one
+    step's displacement.  The nucleolar bonds and the droplet act among SHARED particles only (shared_particles),
+    which every domain holds fresh."""
     rc = max(cfg.a_core_diameter, cfg.b_core_diameter)
+    reach = rc * (1.0 + list_skin)
     for k, l in ((cfg.a_core_bond_spring, cfg.a_core_bond_length), (cfg.b_core_bond_spring, cfg.b_core_bond_length)):
         if k > 0:
-            rc = max(rc, l + BOND_SIGMAS * float(np.sqrt(cfg.temperature / k)))
-    return rc + margin
+            reach = max(reach, l + BOND_SIGMAS * float(np.sqrt(cfg.temperature / k)))
+    return reach + margin
 
 
 def shared_particles(design):
@@ -75,69 +133,76 @@ def shared_particles(design):
     return np.unique(b.reshape(-1))
 
 
-def region(slab, halo):
-    return (slab[0] - halo, slab[1] + halo)
+def region(box, halo):
+    """a box extended by the halo on every face"""
+    return (np.asarray(box[0], dtype=np.float64) - halo, np.asarray(box[1], dtype=np.float64) + halo)
 
 
-def peers_of(d: int, slabs, halo: float):
-    """Domains whose regions overlap d's (symmetric)."""
-    lo, hi = region(slabs[d], halo)
+def in_box(x, box):
+    """mask of the rows of x inside box [lo, hi) (per axis)"""
+    x = np.asarray(x)[:, :3]
+    return np.all((x >= np.asarray(box[0])) & (x < np.asarray(box[1])), axis=1)
+
+
+def peers_of(d: int, boxes, halo: float):
+    """Domains whose regions overlap d's (symmetric; touching counts, so the engines' fp32 regions can never overlap
+    where these do not)."""
+    lo, hi = region(boxes[d], halo)
     out = []
-    for p, s in enumerate(slabs):
+    for p, b in enumerate(boxes):
         if p == d:
             continue
-        plo, phi = region(s, halo)
-        if plo < hi and lo < phi:
+        plo, phi = region(b, halo)
+        if np.all(plo <= hi + 1e-5) and np.all(lo <= phi + 1e-5):
             out.append(p)
     return out
 
 
-def band_capacity(x, slabs, halo, d, margin: float = 1.5, floor: int = 1024) -> int:
+def band_capacity(x, boxes, halo, d, margin: float = 1.5, floor: int = 1024) -> int:
     """Records per band for domain d: its particles inside the largest peer region at the start, times `margin`
     (the bands drift slowly; an overflow is flagged on the device and raised by check()), at least `floor`."""
-    z = np.asarray(x)[:, 2]
-    lo, hi = slabs[d]
-    mine = (z >= lo) & (z < hi)
+    x = np.asarray(x)
+    mine = in_box(x, boxes[d])
     most = 0
-    for p in peers_of(d, slabs, halo):
-        rlo, rhi = region(slabs[p], halo)
-        most = max(most, int((mine & (z >= rlo) & (z < rhi)).sum()))
-    return int(min(z.size, max(floor, np.ceil(margin * most))))
+    for p in peers_of(d, boxes, halo):
+        most = max(most, int((mine & in_box(x, region(boxes[p], halo))).sum()))
+    return int(min(x.shape[0], max(floor, np.ceil(margin * most))))
 
 
 def _finite(v):
-    return float(np.clip(v, -3.0e38, 3.0e38))
+    return np.clip(np.asarray(v, dtype=np.float64), -3.0e38, 3.0e38)
 
 
 class _Domain:
-    def __init__(self, index, slabs, halo):
+    def __init__(self, index, boxes, halo):
         self.index = index
-        self.slab = slabs[index]
+        self.ndom = len(boxes)
+        self.box = (np.asarray(boxes[index][0], dtype=np.float64), np.asarray(boxes[index][1], dtype=np.float64))
         self.halo = halo
-        self.peers = peers_of(index, slabs, halo)
-        self.regions = [tuple(_finite(v) for v in region(slabs[p], halo)) for p in self.peers]
+        self.peers = peers_of(index, boxes, halo)
+        self.peer_boxes = [boxes[p] for p in self.peers]
+        self.regions = [tuple(_finite(v) for v in region(boxes[p], halo)) for p in self.peers]
 
     def owned_mask(self, x):
-        z = np.asarray(x)[:, 2]
-        return (z >= self.slab[0]) & (z < self.slab[1])
+        return in_box(x, self.box)
 
 
 class EngineDomain(_Domain):
     """A gcs.engine.Engine running one domain with its own exchange buffers (no torch tensors: host staging in numpy
     for the host-staged transports, device-to-device or RCCL otherwise)."""
 
-    def __init__(self, engine, index, slabs, halo, cap=None, shared=()):
-        super().__init__(index, slabs, halo)
+    def __init__(self, engine, index, boxes, halo, cap=None, shared=()):
+        super().__init__(index, boxes, halo)
         self.shared = np.asarray(shared, dtype=np.int64).reshape(-1)
         self.e = engine
         n = engine.n
         self.cap = int(cap if cap is not None else n)
-        lo, hi = (_finite(v) for v in self.slab)
-        engine.set_domain(lo, hi, halo, self.regions)
+        engine.set_domain(self.box, halo, self.peer_boxes, index, self.ndom)
         engine.set_domain_shared(self.shared)
         self.nred = engine.domain_buffers(self.cap)
         npeer = max(1, len(self.peers))
-        self.red = np.zeros(self.nred)   # local reduction (8) + shared particles' positions (csrc/domain.hip)
+        # local reduction (10) + shared particles' positions + one displacement slot per domain (csrc/domain.hip)
+        self.red = np.zeros(self.nred)
         self.glob = np.zeros(self.nred)  # its sum over domains
         self.out = np.zeros((npeer, self.cap + 1, 4), dtype=np.float32)  # host staging: [peer][header + cap][4]
         self.inb = np.zeros_like(self.out)
@@ -270,6 +335,8 @@ def _raise_flags(bits):
         raise DomainError("a bond is longer than the domain halo: raise the halo")
     if bits & FLAG_CAPACITY:
         raise DomainError("a band exceeded the exchange buffer capacity: raise cap")
+    if bits & (FLAG_LOST | FLAG_MOTION):
+        raise DomainError("particles moved further than the halo allows between list builds: raise the halo")
 
 
 class DecomposedRun:

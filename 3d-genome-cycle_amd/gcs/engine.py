@@ -291,10 +291,14 @@ class Engine:
 
     # ---- spatial domain decomposition (gcs.domain drives these; device pointers are plain ints) ----
 
-    def set_domain(self, lo, hi, halo, peer_regions=()):
-        reg = np.ascontiguousarray(np.asarray(peer_regions, dtype=np.float64).reshape(-1, 2))
-        A.check(self._lib.gcs_engine_set_domain(self._h, float(lo), float(hi), float(halo),
-                                                _pd(reg) if reg.size else None, reg.shape[0]))
+    def set_domain(self, box, halo, peer_boxes=(), index=0, ndomains=1):
+        """box: (lo[3], hi[3]) of this domain (+-inf: an open face); peer_boxes: [(lo[3], hi[3])] of the domains whose
+        regions overlap this one's (the engine extends them by the halo); index / ndomains: this domain's number and
+        the domain count."""
+        b = np.ascontiguousarray(np.clip(np.asarray(box, dtype=np.float64).reshape(6), -3e38, 3e38))
+        reg = np.ascontiguousarray(np.clip(np.asarray(peer_boxes, dtype=np.float64).reshape(-1, 6), -3e38, 3e38))
+        A.check(self._lib.gcs_engine_set_domain(self._h, _pd(b), float(halo), _pd(reg) if reg.size else None,
+                                                reg.shape[0], int(index), int(ndomains)))
 
     def set_domain_shared(self, idx):
         a = np.ascontiguousarray(np.asarray(idx, dtype=np.int64).reshape(-1))

@@ -420,8 +420,9 @@ def cycle_leg(local, scale, log=sys.stderr):
 
 
 def decomp_main(args):
-    """One trajectory split into z-slab domains (gcs.domain; C5 of SURVEY 8e).  value = N x steps / max-over-ranks
-    time of the whole decomposed step loop (force, update, reaction allreduce, band exchange).  Under torchrun: one
+    """One trajectory split into recursive-bisection boxes (gcs.domain.plan_boxes, 2 x 2 x 2 at 8; --slabs: z-slabs;
+    C5 of SURVEY 8e).  value = N x steps / max-over-ranks time of the whole decomposed step loop (the decomposed list
+    step: forces, update, reaction allreduce, band exchange, list rebuilds).  Under torchrun: one
     domain per GPU, the engine issues the RCCL collectives itself (gcs.domain.RcclRun); one process: K domains on
     this GPU, bands moved device-to-device (LocalTransport)."""
     from gcs import _abi as A
@@ -434,14 +435,14 @@ def decomp_main(args):
     ndom = world if world > 1 else args.decomp
     halo = D.domain_halo(cfg)
     x0 = state[0] if state is not None else design.positions
-    slabs = D.plan_slabs(x0[:, 2], ndom)
+    boxes = D.plan_slabs(x0[:, 2], ndom) if args.slabs else D.plan_boxes(x0, ndom)
     mine = [rank] if world > 1 else list(range(ndom))
     doms = []
     window = window_start(args.config)
-    cap = max(D.band_capacity(x0, slabs, halo, d) for d in range(ndom))  # one size: bands move between domains
+    cap = max(D.band_capacity(x0, boxes, halo, d) for d in range(ndom))  # one size: bands move between domains
     for d in mine:
         e = make_engine(design, cfg, local, window, state)
-        doms.append(D.EngineDomain(e, d, slabs, halo, cap=cap, shared=D.shared_particles(design)))
+        doms.append(D.EngineDomain(e, d, boxes, halo, cap=cap, shared=D.shared_particles(design)))
     run = D.RcclRun(doms[0], dist) if world > 1 else D.DecomposedRun(doms, D.LocalTransport(doms))
     seed = replica_noise_seed(0)
     run.run(args.warmup, first_step=window, seed=seed, timestep=cfg.timestep)
@@ -464,10 +465,12 @@ def decomp_main(args):
             "warmup": args.warmup, "ms_per_step": el_max * 1e3 / args.steps, "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, one trajectory in "
-                                   f"{ndom} z-slab domains ({'RCCL from the engine' if world > 1 else 'in-process, one GPU'})",
+                                   f"{ndom} {'z-slab' if args.slabs else 'box'} domains "
+                                   f"({'RCCL from the engine' if world > 1 else 'in-process, one GPU'})",
                        "particles": n, "domains": ndom, "halo": halo, "parallelism": f"domains{ndom}",
                        "band_capacity_rank0": doms[0].cap, "peers_rank0": doms[0].peers,
-                       "bytes_per_peer_per_step": 16 * (doms[0].cap + 1)},
+                       "bytes_per_peer_per_step": 16 * (doms[0].cap + 1),
+                       "step_shape": "list" if doms[0].e.list_stats()["builds"] > 0 else "tile"},
         }
         print(json.dumps(line), flush=True)
     for d in doms:
@@ -768,6 +771,7 @@ def parse_args(argv=None):
     ap.add_argument("--decomp", type=int, default=0,
                     help="spatial domain decomposition of ONE trajectory: K domains (torchrun: one per rank over "
                          "RCCL; single process: K domains on this GPU, in-process exchange)")
+    ap.add_argument("--slabs", action="store_true", help="--decomp: z-slabs instead of recursive-bisection boxes")
     return ap.parse_args(argv)
 
 

@@ -284,23 +284,29 @@ int gcs_engine_contacts_clear(gcs_engine* e);
 int gcs_engine_sample_positions(gcs_engine* e, float* xyz, int64_t n, int32_t fraction_bits);
 
 /* Spatial domain decomposition (C5: one trajectory over several GPUs; SURVEY.md 8e, DESIGN.md "Multi-GPU").
- * Every engine holds all N particles by global index and integrates those whose z lies in its slab [lo, hi)
- * at the start of a step; it bins only the particles within `halo` of the slab.  `peer_regions` [npeer][2] are
- * the other domains' extended regions [lo_p - halo, hi_p + halo): after each step the band of owned particles
- * whose old or new z lies in a peer's region is packed for that peer.  halo <= 0 turns decomposition off.
- * One step = gcs_engine_domain_step (cells, force + update of the owned particles, local reaction into
- * dev_reaction[8 + 3 shared] on the device) -> the caller's allreduce(sum) of dev_reaction over all domains ->
- * gcs_engine_domain_finish(allreduced reaction: wall ODE + schedule) -> gcs_engine_domain_pack (band records
+ * Every engine holds all N particles by global index and integrates those that lie in its box
+ * box = {lo[3], hi[3]} ([lo, hi) per axis; the domains' boxes tile space, outer faces at +-inf) at the start of a
+ * step; it bins only the particles within `halo` of the box (its region).  `peer_boxes` [npeer][6] are the boxes of
+ * the domains whose regions overlap this one's: after each step the band of owned particles whose old or new
+ * position lies in a peer's region (its box extended by `halo`) is packed for that peer.  Every engine derives the
+ * regions with one fp32 formula, so membership is bit-identical on both sides.  `index` / `ndomains`: this domain's number and the domain
+ * count (one slot each in the allreduce buffer).  halo <= 0 turns decomposition off.
+ * The step shape follows the engine's: the list step (GCS_OPT_FUSED_STEP 3, the default) when the halo holds the
+ * list radius (cutoff + skin at core scale 1), the tile step otherwise.
+ * One step = gcs_engine_domain_step (force + update of the owned particles, local reduction into
+ * dev_reaction[nred] on the device) -> the caller's allreduce(sum) of dev_reaction over all domains ->
+ * gcs_engine_domain_finish(allreduced buffer: wall ODE + schedule) -> gcs_engine_domain_pack (band records
  * {x, y, z, index bits} into dev_out[npeer][cap][4], counts per peer; dev_flags[0] |= 1 a bond longer than the
- * halo, |= 2 a band over cap) -> exchange -> gcs_engine_domain_unpack(received buffers).  All calls only
+ * halo, |= 2 a band over cap, |= 4 a particle owned by no domain's lists, |= 8 cutoff + largest displacement since
+ * the last list build beyond the halo) -> exchange -> gcs_engine_domain_unpack(received buffers).  All calls only
  * enqueue on the engine stream (gcs_engine_stream), so the caller's collectives can be ordered on it too.
  * Replaces nothing in the reference (single-threaded); the per-step callback order is kept (wall update after
  * the force evaluation of the step, stage_interphase/simulation_driver_interphase.cpp:51-52, 80-90). */
-int gcs_engine_set_domain(gcs_engine* e, double lo, double hi, double halo, const double* peer_regions,
-                          int32_t npeer);
+int gcs_engine_set_domain(gcs_engine* e, const double* box /* [6] */, double halo,
+                          const double* peer_boxes /* [npeer][6] */, int32_t npeer, int32_t index, int32_t ndomains);
 /* Shared particles: fresh on every domain every step (carried in the reaction allreduce, which then holds
- * 8 + 3 * count doubles).  For particles whose bonds are too soft for any practical halo (nucleolar beads and
- * their NOR partners; nucleolus_bond_spring 10 vs chain 50-100). */
+ * 10 + 3 * count + ndomains doubles).  For particles whose bonds are too soft for any practical halo (nucleolar
+ * beads and their NOR partners; nucleolus_bond_spring 10 vs chain 50-100). */
 int gcs_engine_set_domain_shared(gcs_engine* e, const int64_t* idx, int32_t count);
 int gcs_engine_stream(gcs_engine* e, void** stream);
 int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step, double* dev_reaction);

@@ -51,9 +51,9 @@ struct gcso_system {
     int64_t *cell_start, *cell_items;
     int64_t cell_cap;
     int64_t* cell_of;
-    /* domain decomposition (C5): integrate / count reactions of the particles with z in [dom_lo, dom_hi) only */
+    /* domain decomposition (C5): integrate / count reactions of the particles inside the box [dom_lo, dom_hi) only */
     int dom_on;
-    double dom_lo, dom_hi;
+    double dom_lo[3], dom_hi[3];
     unsigned char* dom_own;
 };
 
@@ -711,7 +711,11 @@ int gcso_run(gcso_system* s, const gcs_bd_config* cfg, int64_t first_step, int64
     for (int64_t st = first_step + 1; st <= first_step + steps; st++) {
         if (s->dom_on) {
             if (!s->dom_own) s->dom_own = (unsigned char*)malloc((size_t)n + 1);
-            for (int64_t i = 0; i < n; i++) s->dom_own[i] = s->x[3 * i + 2] >= s->dom_lo && s->x[3 * i + 2] < s->dom_hi;
+            for (int64_t i = 0; i < n; i++) {
+                int own = 1;
+                for (int k = 0; k < 3; k++) own &= s->x[3 * i + k] >= s->dom_lo[k] && s->x[3 * i + k] < s->dom_hi[k];
+                s->dom_own[i] = (unsigned char)own;
+            }
         }
         eval_fields(s, 1, NULL);
         double dt = cfg->timestep;
@@ -754,13 +758,15 @@ int gcso_run(gcso_system* s, const gcs_bd_config* cfg, int64_t first_step, int64
     return 0;
 }
 
-/* domain decomposition (C5, DESIGN.md "Multi-GPU"): on != 0 -> run() integrates only the particles whose z lies in
- * [lo, hi) at the start of each step, and the wall reactions count those only (the caller sums them over domains
- * and applies the wall update itself) */
-void gcso_set_domain(gcso_system* s, int on, double lo, double hi)
+/* domain decomposition (C5, DESIGN.md "Multi-GPU"): on != 0 -> run() integrates only the particles inside the box
+ * [lo, hi) (per axis) at the start of each step, and the wall reactions count those only (the caller sums them over
+ * domains and applies the wall update itself) */
+void gcso_set_domain(gcso_system* s, int on, const double* lo, const double* hi)
 {
     s->dom_on = on;
-    s->dom_lo = lo;
-    s->dom_hi = hi;
+    for (int k = 0; k < 3; k++) {
+        s->dom_lo[k] = on ? lo[k] : 0.0;
+        s->dom_hi[k] = on ? hi[k] : 0.0;
+    }
 }
 

@@ -70,7 +70,7 @@ uint64_t gcso_mt19937_64_next(gcso_mt19937_64* g);
 /* `count` normals of std::normal_distribution<double> driven by std::mt19937_64(seed) (libstdc++) */
 void gcso_reference_normals(uint64_t seed, int64_t count, double* out);
 double gcso_quantize(double value, int bits);
-void gcso_set_domain(gcso_system* s, int on, double lo, double hi);
+void gcso_set_domain(gcso_system* s, int on, const double* lo /* [3] */, const double* hi /* [3] */);
 
 #ifdef __cplusplus
 }

@@ -63,7 +63,7 @@ def load():
             "gcso_seed_seq_generate": (None, [C.POINTER(C.c_uint32), C.c_int64, C.POINTER(C.c_uint32), C.c_int64]),
             "gcso_reference_normals": (None, [C.c_uint64, C.c_int64, pd]),
             "gcso_quantize": (C.c_double, [C.c_double, C.c_int]),
-            "gcso_set_domain": (None, [vp, C.c_int, C.c_double, C.c_double]),
+            "gcso_set_domain": (None, [vp, C.c_int, pd, pd]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -222,11 +222,15 @@ class OracleSystem:
 
 
     def set_domain(self, lo=None, hi=None):
-        """Decomposed steps: integrate (and count wall reactions of) the particles with z in [lo, hi) only."""
+        """Decomposed steps: integrate (and count wall reactions of) the particles inside the box [lo, hi) (3-vectors,
+        +-inf for open faces) only."""
         if lo is None:
-            self._lib.gcso_set_domain(self._h, 0, 0.0, 0.0)
+            self._lib.gcso_set_domain(self._h, 0, None, None)
         else:
-            self._lib.gcso_set_domain(self._h, 1, float(lo), float(hi))
+            lo_ = _f64(lo, (3,))
+            hi_ = _f64(hi, (3,))
+            self._lib.gcso_set_domain(self._h, 1, lo_.ctypes.data_as(C.POINTER(C.c_double)),
+                                      hi_.ctypes.data_as(C.POINTER(C.c_double)))
 
     # contact map (stage_interphase/contact_map.cpp:33-85): a dict of pair counts on the host
     def contacts_update(self, distance):

@@ -3,22 +3,23 @@ run, with the same band layout as gcs.domain.EngineDomain ([peer][header + recor
 is the band's count) so gcs.domain's transports move either."""
 import numpy as np
 
-from gcs.domain import _Domain
+from gcs.domain import _Domain, in_box
+
+RED = 10  # the engine's allreduce layout (csrc/engine_internal.hpp kDomainRed): reactions [0, 6), shared from RED
 
 
 class OracleDomain(_Domain):
-    def __init__(self, osys, index, slabs, halo, schedule: dict, shared=()):
-        super().__init__(index, slabs, halo)
+    def __init__(self, osys, index, boxes, halo, schedule: dict, shared=()):
+        super().__init__(index, boxes, halo)
         self.shared = np.asarray(shared, dtype=np.int64).reshape(-1)
         self.o = osys
         self.sched = dict(schedule)
         osys.set_schedule(**dict(schedule, update_wall=0))  # the wall update sees the allreduced reaction
-        lo, hi = self.slab
-        osys.set_domain(lo, hi)
+        osys.set_domain(*self.box)
         n = osys.n
         self.cap = n
         npeer = max(1, len(self.peers))
-        self.red = np.zeros(8 + 3 * self.shared.size)
+        self.red = np.zeros(RED + 3 * self.shared.size)
         self.glob = np.zeros_like(self.red)
         self.out = np.zeros((npeer, n + 1, 4))
         self.inb = np.zeros_like(self.out)
@@ -35,7 +36,7 @@ class OracleDomain(_Domain):
         if self.shared.size:
             new = self.o.get_positions()[self.shared]
             own = self.owned_mask(self._old[self.shared])
-            self.red[8:] = np.where(own[:, None], new, 0.0).reshape(-1)
+            self.red[RED:] = np.where(own[:, None], new, 0.0).reshape(-1)
 
     def finish(self):
         # simulation_driver_interphase.cpp:80-90 with the reaction summed over domains
@@ -51,7 +52,7 @@ class OracleDomain(_Domain):
         self.o.set_context(c)
         if self.shared.size:
             x = self.o.get_positions()
-            x[self.shared] = self.glob[8:].reshape(-1, 3)
+            x[self.shared] = self.glob[RED:].reshape(-1, 3)
             self.o.set_positions(x)
 
     def pack(self, staged=True):
@@ -59,8 +60,8 @@ class OracleDomain(_Domain):
         old = self._old
         own = self.owned_mask(old)
         self.out[:, 0, :] = 0.0
-        for k, (lo, hi) in enumerate(self.regions):
-            sel = own & (((old[:, 2] >= lo) & (old[:, 2] < hi)) | ((new[:, 2] >= lo) & (new[:, 2] < hi)))
+        for k, reg in enumerate(self.regions):
+            sel = own & (in_box(old, reg) | in_box(new, reg))
             idx = np.nonzero(sel)[0]
             self.out[k, 0, 0] = idx.size
             self.out[k, 1: idx.size + 1, :3] = new[idx]

@@ -1,12 +1,13 @@
 """GPU: the spatial domain decomposition (C5, gcs/domain.py + csrc/domain.hip) with HIP engines: several domains in
-one process on one device (LocalTransport: bands device-to-device), two processes on one device (DistTransport,
+one process on one device (LocalTransport: bands device-to-device), several processes on one device (DistTransport,
 host-staged over gloo: RCCL refuses two ranks on one GPU), and the engine-issued RCCL sequence with one rank
 (gcs_engine_domain_run: allreduce + grouped send/recv on the engine stream, graph-captured), against the undecomposed
-engine, each other and the fp64 oracle.
+engine, each other and the fp64 oracle.  Both decomposed step shapes: the list step (k_lstep<..., DOM>, the default)
+and the tile step (GCS_OPT_FUSED_STEP 0); both geometries: z-slabs and recursive-bisection boxes (2 x 2 x 2 at 8).
 
 Tolerances: positions |dx| <= 2e-5 after 30 steps (fp32; the domains' cell lists order the pair sums differently
 from the single engine's), wall semiaxes relative 1e-7; the protocol flags (bond beyond the halo, band over
-capacity) must stay clear."""
+capacity, lost particle, displacement beyond the halo) must stay clear."""
 import json
 import os
 import socket
@@ -16,6 +17,7 @@ from pathlib import Path
 import numpy as np
 import pytest
 
+from gcs import _abi as A
 from gcs import domain, interphase, synthetic
 from gcs.config import InterphaseConfig
 from gcs.engine import Engine
@@ -28,30 +30,44 @@ STEPS = 30
 SEED = 99
 
 
-def _engine(design, cfg):
+def _engine(design, cfg, fused=None):
     e, _ = interphase.build_interphase(Engine, design, cfg, device=0)
     e.set_schedule(**interphase.interphase_schedule(cfg))
+    if fused is not None:
+        e.set_option(A.OPT_FUSED_STEP, fused)
     return e
 
 
-def _decomposed(design, cfg, ndom, steps, cap=None, halo=None):
+def _plan(kind, design, ndom):
+    x = design.positions
+    return domain.plan_slabs(x[:, 2], ndom) if kind == "slabs" else domain.plan_boxes(x, ndom)
+
+
+def _decomposed(design, cfg, ndom, steps, cap=None, halo=None, kind="slabs", fused=None):
     halo = halo or domain.domain_halo(cfg)
-    slabs = domain.plan_slabs(design.positions[:, 2], ndom)
+    boxes = _plan(kind, design, ndom)
     sh = domain.shared_particles(design)
-    doms = [domain.EngineDomain(_engine(design, cfg), d, slabs, halo, cap=cap, shared=sh) for d in range(ndom)]
+    doms = [domain.EngineDomain(_engine(design, cfg, fused), d, boxes, halo, cap=cap, shared=sh)
+            for d in range(ndom)]
     run = domain.DecomposedRun(doms, domain.LocalTransport(doms))
     run.run(steps, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
-    return run, doms, slabs
+    return run, doms, boxes
 
 
-@pytest.mark.parametrize("ndom,halo", [(2, None), (4, None), (3, 0.45)])
-def test_decomposed_engines_match_single_engine_c1(c1_design, ndom, halo):
+@pytest.mark.parametrize("kind,ndom,halo,fused", [("slabs", 2, None, None), ("slabs", 4, None, None),
+                                                  ("slabs", 3, 0.45, None), ("boxes", 4, None, None),
+                                                  ("boxes", 8, None, None), ("slabs", 2, None, 0),
+                                                  ("boxes", 4, None, 0)])
+def test_decomposed_engines_match_single_engine_c1(c1_design, kind, ndom, halo, fused):
     cfg = InterphaseConfig()
     single = _engine(c1_design, cfg)
     single.run(STEPS, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     x1, c1 = single.get_positions(), single.get_context()
-    run, doms, slabs = _decomposed(c1_design, cfg, ndom, STEPS, halo=halo)
+    run, doms, boxes = _decomposed(c1_design, cfg, ndom, STEPS, halo=halo, kind=kind, fused=fused)
     run.check()
+    # the list step ran decomposed (its builds), or the tile step (no lists)
+    builds = doms[0].e.list_stats()["builds"]
+    assert (builds >= STEPS // 8) if fused is None else builds == 0, builds
     x = domain.gather_positions(run, c1_design.n)
     assert np.abs(x - x1).max() <= 2e-5
     for d in doms:
@@ -65,16 +81,33 @@ def test_decomposed_engines_match_single_engine_c1(c1_design, ndom, halo):
     assert np.abs(x - o.get_positions()).max() <= 2e-5
 
 
-def test_decomposed_engines_c2_four_domains():
+@pytest.mark.parametrize("kind,ndom", [("slabs", 4), ("boxes", 8)])
+def test_decomposed_engines_c2(kind, ndom):
     cfg = InterphaseConfig()
     design = synthetic.make_c2()
     single = _engine(design, cfg)
     single.run(20, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     x1 = single.get_positions()
-    run, doms, _ = _decomposed(design, cfg, 4, 20)
+    run, doms, _ = _decomposed(design, cfg, ndom, 20, kind=kind)
     run.check()
     x = domain.gather_positions(run, design.n)
     assert np.abs(x - x1).max() <= 2e-5
+
+
+def test_motion_beyond_halo_is_reported(c1_design):
+    """list step: a hot system (T x 400) rebuilt every 64 steps with a halo just above the list radius; the
+    largest displacement since the build soon exceeds halo - cutoff, which the domain tail flags"""
+    cfg = InterphaseConfig()
+    doms = []
+    boxes = domain.plan_boxes(c1_design.positions, 2)
+    for d in range(2):
+        e = _engine(c1_design, cfg)
+        e.set_option(A.OPT_LIST_EVERY, 64)
+        doms.append(domain.EngineDomain(e, d, boxes, 0.3 * 1.4 + 0.01, shared=domain.shared_particles(c1_design)))
+    run = domain.DecomposedRun(doms, domain.LocalTransport(doms))
+    run.run(60, first_step=0, temperature=400.0 * cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    with pytest.raises(domain.DomainError, match="halo"):
+        run.check()
 
 
 def test_band_capacity_overflow_is_reported(c1_design):
@@ -103,7 +136,7 @@ def test_decomposed_c5_scaled_two_domains():
     single = _engine(design, cfg)
     single.run(steps, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     x1 = single.get_positions()
-    run, doms, _ = _decomposed(design, cfg, 2, steps)
+    run, doms, _ = _decomposed(design, cfg, 2, steps, kind="boxes")
     run.check()
     x = domain.gather_positions(run, design.n)
     o, _ = interphase.build_interphase(oracle.OracleSystem, design, cfg)
@@ -117,18 +150,20 @@ def test_decomposed_c5_scaled_two_domains():
     assert e_single <= 2e-5 and e_dec <= 2e-5, (e_dec, e_single)
 
 
-def test_rccl_run_one_rank_equals_host_driven(c1_design):
+@pytest.mark.parametrize("fused", [None, 0])
+def test_rccl_run_one_rank_equals_host_driven(c1_design, fused):
     """gcs_engine_domain_run with one rank (RCCL allreduce on the engine stream; 70 steps = a priming step, two
-    captured 32-step graphs and eager steps) equals the host-driven step sequence of the same domain bit for bit"""
+    captured 32-step graphs (list step: whole rebuild periods, recaptured for the second call's phase) and eager
+    steps) equals the host-driven step sequence of the same domain bit for bit"""
     from gcs.engine import rccl_unique_id
     cfg = InterphaseConfig()
     halo = domain.domain_halo(cfg)
     slabs = domain.plan_slabs(c1_design.positions[:, 2], 1)
     sh = domain.shared_particles(c1_design)
-    ref = domain.EngineDomain(_engine(c1_design, cfg), 0, slabs, halo, shared=sh)
+    ref = domain.EngineDomain(_engine(c1_design, cfg, fused), 0, slabs, halo, shared=sh)
     run = domain.DecomposedRun([ref], domain.LocalTransport([ref]))
     run.run(70, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
-    d = domain.EngineDomain(_engine(c1_design, cfg), 0, slabs, halo, shared=sh)
+    d = domain.EngineDomain(_engine(c1_design, cfg, fused), 0, slabs, halo, shared=sh)
     d.e.domain_rccl(rccl_unique_id(), 1, 0, [])
     d.e.domain_run(30, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     d.e.domain_run(40, first_step=30, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
@@ -145,8 +180,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, out_dir):
-    """one domain per process, both on device 0, host-staged over gloo"""
+def _rank_main(rank, world, port, out_dir, config):
+    """one domain per process, all on device 0, host-staged over gloo (C1: z-slabs; C2: boxes)"""
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
                        "MASTER_PORT": str(port)})
     root = Path(__file__).resolve().parents[1]
@@ -156,13 +191,14 @@ def _rank_main(rank, world, port, out_dir):
     from gcs.config import InterphaseConfig as IC
     from gcs.engine import Engine as E
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    design, cfg = S.make_c1(), IC()
+    design, cfg = (S.make_c1() if config == "c1" else S.make_c2()), IC()
     e, _ = I.build_interphase(E, design, cfg, device=0)
     e.set_schedule(**I.interphase_schedule(cfg))
-    slabs = D.plan_slabs(design.positions[:, 2], world)
-    d = D.EngineDomain(e, rank, slabs, D.domain_halo(cfg), shared=D.shared_particles(design))
+    boxes = (D.plan_slabs(design.positions[:, 2], world) if config == "c1"
+             else D.plan_boxes(design.positions, world))
+    d = D.EngineDomain(e, rank, boxes, D.domain_halo(cfg), shared=D.shared_particles(design))
     run = D.DecomposedRun([d], D.DistTransport(d, dist))
-    run.run(STEPS, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    run.run(_steps(config), first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     run.check()
     x = D.gather_positions(run, design.n, dist)
     if rank == 0:
@@ -171,17 +207,21 @@ def _rank_main(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_engine_domains_two_processes_host_staged(tmp_path, c1_design):
-    """two processes, one engine domain each (device 0), reaction allreduce and bands over gloo: bit for bit the
-    in-process two-domain run (the same kernels; a two-term sum is order-free), and within 2e-5 of the single
-    engine"""
+def _steps(config):
+    return STEPS if config == "c1" else 20
+
+
+@pytest.mark.parametrize("config,world", [("c1", 2), ("c2", 4)])
+def test_engine_domains_processes_host_staged(tmp_path, config, world):
+    """`world` processes, one engine domain each (device 0), reaction allreduce and bands over gloo: within 2e-5 of
+    the single engine; with two domains also bit for bit the in-process run (the same kernels; a two-term sum is
+    order-free; gloo's 4-term sum may associate differently from the host's)"""
     # stdlib spawn, not torch.multiprocessing: this process keeps one HIP runtime (libgcs's); torch (for gloo) is
     # imported by the ranks only, before their engines load libgcs
     import multiprocessing as mp
-    world = 2
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, str(tmp_path), config)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -190,10 +230,14 @@ def test_engine_domains_two_processes_host_staged(tmp_path, c1_design):
     x = np.load(tmp_path / "x.npy")
     ctx = json.loads((tmp_path / "ctx.json").read_text())
     cfg = InterphaseConfig()
-    run, doms, _ = _decomposed(c1_design, cfg, world, STEPS)
-    xl = domain.gather_positions(run, c1_design.n)
-    assert np.array_equal(x, xl)
-    assert ctx["wall_semiaxes"] == doms[0].context()["wall_semiaxes"]
-    single = _engine(c1_design, cfg)
-    single.run(STEPS, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    design = synthetic.make_c1() if config == "c1" else synthetic.make_c2()
+    steps = _steps(config)
+    if world == 2:
+        run, doms, _ = _decomposed(design, cfg, world, steps)
+        xl = domain.gather_positions(run, design.n)
+        assert np.array_equal(x, xl)
+        assert ctx["wall_semiaxes"] == doms[0].context()["wall_semiaxes"]
+    single = _engine(design, cfg)
+    single.run(steps, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     assert np.abs(x - single.get_positions()).max() <= 2e-5
+    assert np.allclose(ctx["wall_semiaxes"], single.get_context()["wall_semiaxes"], rtol=1e-7, atol=0)
