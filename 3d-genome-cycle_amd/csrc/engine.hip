@@ -254,6 +254,11 @@ struct gcs_engine {
     // small systems (N <= kSmallMax, GCS_OPT_SMALL_PATH): one single-workgroup launch per run (k_small) and its
     // persistent list state; small_cont: the next small run at small_step continues the last one (no rebuild)
     int small_opt = 0;
+    // dense systems: mean neighbours within the cutoff above which a fresh run takes the 2-launch tile step instead
+    // of the list step (GCS_OPT_DENSE_NEIGHBORS; 0: never), and the current chain's verdict
+    int dense_opt = 48;
+    bool dense = false;
+    double dense_mean = -1.0;  // the last probe's mean neighbour count
     unsigned short* sm_list = nullptr;
     int* sm_lcount = nullptr;
     float4* sm_bpos = nullptr;
@@ -652,18 +657,24 @@ void enqueue_cells(gcs_engine* e)
     enqueue_sort(e);
 }
 
-bool list_path(const gcs_engine* e, bool spacestep) { return e->fused == 3 && e->list_ok && !spacestep; }
+// the dense-system switch applies to undecomposed runs (a decomposed run picks its shape when it is primed)
+bool dense_switch(const gcs_engine* e) { return e->dense && !e->dom; }
+// the step shape a fixed-timestep run takes (GCS_OPT_FUSED_STEP semantics): the list step (3) falls back to the
+// rebuild step (2) when the system does not admit lists, and hands a dense chain to the unfused tile step (0)
+int eff_fused(const gcs_engine* e)
+{
+    if (e->fused != 3) return e->fused;
+    if (!e->list_ok) return 2;
+    return dense_switch(e) ? 0 : 3;
+}
+bool list_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) == 3 && !spacestep; }
 // small systems: the single-workgroup step loop (k_small) instead of the list step
 bool small_path(const gcs_engine* e, bool spacestep)
 {
     return e->small_opt != 0 && e->n <= kSmallMax && e->fused == 3 && !spacestep && !e->dom;
 }
-bool fused_path(const gcs_engine* e, bool spacestep) { return e->fused != 0 && !spacestep; }
-bool rebuild_path(const gcs_engine* e, bool spacestep)
-{
-    // the list step falls back to the rebuild step when the system does not admit lists
-    return (e->fused == 2 || (e->fused == 3 && !e->list_ok)) && !spacestep;
-}
+bool fused_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) != 0 && !spacestep; }
+bool rebuild_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) == 2 && !spacestep; }
 
 float list_skin(const gcs_engine* e) { return 1e-3f * (float)e->list_skin_pm * e->fa.pair_dist; }
 
@@ -844,6 +855,57 @@ int prepare(gcs_engine* e)
     return GCS_OK;
 }
 
+int ensure_search(gcs_engine* e, int64_t n);
+int enqueue_search_cells(gcs_engine* e, const float4* src, int ni, double distance);
+
+// The step shape of a fresh chain: the list step walks ~2.5 x (neighbours within the cutoff) entries per particle
+// with one gather each, the tile step shares each staged candidate among a tile's 64 lanes, so above a density the
+// unfused tile step is faster.  Measured single-trajectory bead-updates/s (tools/shape_probe.py):
+// C2 window, 25 neighbours, 16-bit entries: list 2.32e9 / tile 1.09e9; C2 start, 32: 1.44e9 / 1.05e9; C5 start, 43,
+// 32-bit entries: 1.34e9 / 2.37e9 (the rebuild step: 0.6e9, its 16-slot cell buckets overflow there).  So the
+// verdict weighs the neighbour count by the entry size (list bytes per particle): dense when mean neighbours x
+// (entry bytes / 2) exceeds GCS_OPT_DENSE_NEIGHBORS.  The mean over the current positions within the current cutoff
+// (the neighbour search's count kernel) decides once per chain, so a chain's trajectory is reproducible.
+int probe_density(gcs_engine* e)
+{
+    double cs = 1.0;
+    HIPCHK(hipMemcpyAsync(&cs, (const char*)e->ctx + offsetof(DevCtx, cs), sizeof(cs), hipMemcpyDeviceToHost,
+                          e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    const double rc = (double)e->fa.pair_dist * (e->fa.pair_scaled ? cs : 1.0);
+    int rc_;
+    if (!(rc > 0) || e->n < 2) return GCS_OK;
+    if ((rc_ = ensure_search(e, e->n))) return rc_;
+    if ((rc_ = enqueue_search_cells(e, e->pos[e->parity], e->n, rc))) return rc_;
+    launch_search_count(e->stream, e->s_ctx, e->n, e->s_spos, e->s_sidx, e->s_scell, e->s_cstart, e->s_counts);
+    launch_exclusive_scan_small(e->stream, e->s_counts, e->s_offsets, e->n, e->s_total);
+    HIPCHK(hipGetLastError());
+    int pairs = 0;
+    HIPCHK(hipMemcpyAsync(&pairs, e->s_total, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->dense_mean = 2.0 * pairs / (double)e->n;
+    e->dense = e->dense_mean * (list_u16(e->n) ? 1.0 : 2.0) > (double)e->dense_opt;
+    return GCS_OK;
+}
+
+// before a run of the default shape: a fresh undecomposed chain probes the density (the verdict holds while the
+// chain continues)
+int choose_shape(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
+{
+    int rc = prepare(e);
+    if (rc) return rc;
+    if (e->fused != 3 || e->dense_opt <= 0 || !e->list_ok) {
+        e->dense = false;
+        return GCS_OK;
+    }
+    const bool cont = e->chain_valid && e->chain_step == first_step && e->chain_version == e->topo_version;
+    if (e->dom || cfg->spacestep > 0 || cont) return GCS_OK;
+    const bool was = e->dense;
+    if ((rc = probe_density(e))) return rc;
+    if (e->dense != was) e->chain_valid = false;
+    return GCS_OK;
+}
+
 // compile, load the BD parameters into the kernel arguments, set the step counter, build the first grid
 int begin_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
 {
@@ -945,7 +1007,7 @@ GraphKey run_key(const gcs_engine* e, const gcs_bd_config* cfg, bool spacestep)
     GraphKey k;
     std::memset(&k, 0, sizeof(k));
     k.topo_version = e->topo_version;
-    k.fused = e->fused;
+    k.fused = eff_fused(e);  // the shape the run takes
     k.list_every = e->list_every;
     k.sched_flags = e->sched_flags;
     k.waves = e->waves;
@@ -1661,10 +1723,11 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
     const bool spacestep = cfg->spacestep > 0;
     if (small_path(e, spacestep)) return run_small(e, cfg, first_step, steps);
     e->small_cont = false;  // another step shape moves the state on: the small path rebuilds next time
-    if (!list_path(e, spacestep))
-        if (int rc = flush_contacts(e)) return rc;
-    int rc = begin_run(e, cfg, first_step);
+    int rc = choose_shape(e, cfg, first_step);
     if (rc) return rc;
+    if (!list_path(e, spacestep))
+        if ((rc = flush_contacts(e))) return rc;
+    if ((rc = begin_run(e, cfg, first_step))) return rc;
 
     const int G = e->graph_steps;
     const GraphKey key = run_key(e, cfg, spacestep);
@@ -2724,7 +2787,7 @@ int gcs_engine_get_list_stats(gcs_engine* e, gcs_list_stats* out)
     DevCtx d;
     HIPCHK(hipMemcpyAsync(&d, e->ctx, sizeof(d), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    out->active = (e->fused == 3 && e->list_ok) ? 1 : 0;
+    out->active = list_path(e, false) ? 1 : 0;
     out->rebuild_every = e->list_every;
     out->builds = d.lbuilds;
     out->fallback_particle_steps = d.lfallback;
@@ -2785,6 +2848,13 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
             return fail(GCS_EINVAL, "list capacity must be a multiple of 32 in [32, 16384]");
         e->list_cap = (int)value;
         drop_graph(e);
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_DENSE_NEIGHBORS) {
+        if (value < 0) return fail(GCS_EINVAL, "dense threshold must be >= 0");
+        e->dense_opt = (int)value;
+        e->chain_valid = false;
+        e->small_cont = false;
         return GCS_OK;
     }
     if (option == GCS_OPT_SMALL_PATH) {

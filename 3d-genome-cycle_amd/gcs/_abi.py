@@ -39,6 +39,7 @@ OPT_LIST_EVERY = 11
 OPT_LIST_CAP = 12
 OPT_LIST_WAVES = 13
 OPT_SMALL_PATH = 14
+OPT_DENSE_NEIGHBORS = 15
 
 ENERGY_KINDS = ("pair", "softwell", "bonds", "bending", "wall_in", "wall_out", "point_source", "kinetochore_fiber")
 

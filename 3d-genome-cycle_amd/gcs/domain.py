@@ -311,13 +311,15 @@ class RcclRun:
     ncclAllReduce of the reaction, grouped ncclSend/ncclRecv of the bands -- issued by the engine on its stream
     (gcs_engine_domain_run); torch.distributed (any backend) only carries the communicator id at setup."""
 
-    def __init__(self, domain: EngineDomain, dist):
+    def __init__(self, domain: EngineDomain, dist=None):
+        """dist: torch.distributed (any backend) to hand the communicator id to the ranks; None: one rank."""
         from .engine import rccl_unique_id
         self.d = domain
         self.domains = [domain]
-        rank, world = dist.get_rank(), dist.get_world_size()
+        rank, world = (dist.get_rank(), dist.get_world_size()) if dist is not None else (0, 1)
         box = [rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
+        if dist is not None:
+            dist.broadcast_object_list(box, src=0)
         domain.e.domain_rccl(box[0], world, rank, domain.peers)
 
     def run(self, steps, first_step=0, temperature=1.0, timestep=1e-5, seed=0):

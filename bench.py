@@ -357,7 +357,8 @@ def c5_leg(local, seed, steps, log=sys.stderr):
         e.synchronize()
         out[name] = d.n * steps / (time.perf_counter() - t0)
         if name == "default":
-            out["default_step"] = "list" if e.list_stats()["active"] else "rebuild"
+            # the engine's density verdict (GCS_OPT_DENSE_NEIGHBORS): list step, or the unfused tile step when dense
+            out["default_step"] = "list" if e.list_stats()["active"] else "unfused tile (dense start)"
         e.close()
         print(f"bench: C5 {name} {out[name]:.3e} bead-updates/s", file=log, flush=True)
     return out
@@ -442,8 +443,11 @@ def decomp_main(args):
     cap = max(D.band_capacity(x0, boxes, halo, d) for d in range(ndom))  # one size: bands move between domains
     for d in mine:
         e = make_engine(design, cfg, local, window, state)
+        if args.fused is not None:
+            e.set_option(A.OPT_FUSED_STEP, args.fused)  # e.g. 0: the decomposed tile step
         doms.append(D.EngineDomain(e, d, boxes, halo, cap=cap, shared=D.shared_particles(design)))
-    run = D.RcclRun(doms[0], dist) if world > 1 else D.DecomposedRun(doms, D.LocalTransport(doms))
+    rccl = world > 1 or (args.rccl and ndom == 1)
+    run = D.RcclRun(doms[0], dist) if rccl else D.DecomposedRun(doms, D.LocalTransport(doms))
     seed = replica_noise_seed(0)
     run.run(args.warmup, first_step=window, seed=seed, timestep=cfg.timestep)
     for d in doms:
@@ -466,7 +470,7 @@ def decomp_main(args):
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, one trajectory in "
                                    f"{ndom} {'z-slab' if args.slabs else 'box'} domains "
-                                   f"({'RCCL from the engine' if world > 1 else 'in-process, one GPU'})",
+                                   f"({'RCCL from the engine' if rccl else 'in-process, one GPU'})",
                        "particles": n, "domains": ndom, "halo": halo, "parallelism": f"domains{ndom}",
                        "band_capacity_rank0": doms[0].cap, "peers_rank0": doms[0].peers,
                        "bytes_per_peer_per_step": 16 * (doms[0].cap + 1),
@@ -772,6 +776,8 @@ def parse_args(argv=None):
                     help="spatial domain decomposition of ONE trajectory: K domains (torchrun: one per rank over "
                          "RCCL; single process: K domains on this GPU, in-process exchange)")
     ap.add_argument("--slabs", action="store_true", help="--decomp: z-slabs instead of recursive-bisection boxes")
+    ap.add_argument("--rccl", action="store_true",
+                    help="--decomp 1 in one process: the engine-issued RCCL sequence with one rank (graph-captured)")
     return ap.parse_args(argv)
 
 

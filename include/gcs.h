@@ -361,6 +361,9 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
 #define GCS_OPT_SMALL_PATH 14     /* 1: systems of <= 2,048 particles run every chunk of fixed-timestep steps in ONE
                                      single-workgroup launch (Verlet lists rebuilt by displacement); 0 (default): the
                                      list step's cached graphs (faster on C3's prometaphase / telophase) */
+#define GCS_OPT_DENSE_NEIGHBORS 15 /* list step (GCS_OPT_FUSED_STEP 3): a fresh run whose mean neighbour count within the
+                                     cutoff, x 2 when list entries are 32-bit (N > 65,536), exceeds this takes the
+                                     unfused tile step instead (default 48; 0: never) */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
 
 /* List-step diagnostics (the neighbour lists md::neighbor_searcher keeps between rebuilds; micromd, called at

@@ -30,6 +30,7 @@ def _list_engine(design, cfg, **opts):
     e, _ = interphase.build_interphase(Engine, design, cfg)
     e.set_option(A.OPT_FUSED_STEP, 3)
     e.set_option(A.OPT_SMALL_PATH, 0)  # the multi-workgroup list step even at C1 size (tests/test_gpu_small.py: the other)
+    e.set_option(A.OPT_DENSE_NEIGHBORS, 0)  # the list step at any density (test_dense_start_takes_tile_step: the switch)
     for k, v in opts.items():
         e.set_option(getattr(A, "OPT_" + k.upper()), v)
     return e
@@ -182,6 +183,28 @@ def test_list_c5_trajectory():
     err = float(np.abs(e.get_positions() - o.get_positions()).max())
     print({"list_c5_err": err, "stats": e.list_stats()})
     assert err <= TOL_X
+
+
+def test_dense_start_takes_tile_step():
+    """the default engine (GCS_OPT_DENSE_NEIGHBORS 48) probes a fresh chain's density: C5's synthetic start (64
+    neighbours within the cutoff at core scale 0.5, 32-bit entries) runs the unfused tile step, C2's start (41, 16-bit)
+    the list step; a continuing chain keeps its verdict; the tile-step trajectory matches the fp64 oracle"""
+    cfg5 = resolution_scaled(InterphaseConfig(), 10.0)
+    d5 = synthetic.make_c5()
+    e, o = _pair(d5, cfg5, x=_f32(d5.positions), dense_neighbors=48)
+    _run_both(e, o, 4, 0, cfg5, 99)
+    st = e.list_stats()
+    assert st["active"] == 0 and st["builds"] == 0, st
+    err = float(np.abs(e.get_positions() - o.get_positions()).max())
+    assert err <= TOL_X, err
+    cfg2 = InterphaseConfig()
+    d2 = synthetic.make_c2()
+    e2, _ = interphase.build_interphase(Engine, d2, cfg2)
+    e2.set_schedule(**interphase.interphase_schedule(cfg2))
+    e2.run(8, first_step=0, temperature=cfg2.temperature, timestep=cfg2.timestep, seed=1)
+    e2.run(8, first_step=8, temperature=cfg2.temperature, timestep=cfg2.timestep, seed=1)
+    st2 = e2.list_stats()
+    assert st2["active"] == 1 and st2["builds"] >= 2, st2
 
 
 def test_list_and_rebuild_step_agree_on_neighbour_count():
