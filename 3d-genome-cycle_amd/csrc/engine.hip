@@ -868,10 +868,11 @@ int enqueue_search_cells(gcs_engine* e, const float4* src, int ni, double distan
 // (the neighbour search's count kernel) decides once per chain, so a chain's trajectory is reproducible.
 int probe_density(gcs_engine* e)
 {
+    // (rocprofv3 --kernel-trace segfaults in the first graph launch after this probe, measured with every variant of
+    // its copies and kernels; profiling runs turn the probe off: GCS_OPT_DENSE_NEIGHBORS 0, tools/profile.sh)
     double cs = 1.0;
-    HIPCHK(hipMemcpyAsync(&cs, (const char*)e->ctx + offsetof(DevCtx, cs), sizeof(cs), hipMemcpyDeviceToHost,
-                          e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpy(&cs, (const char*)e->ctx + offsetof(DevCtx, cs), sizeof(cs), hipMemcpyDeviceToHost));
     const double rc = (double)e->fa.pair_dist * (e->fa.pair_scaled ? cs : 1.0);
     int rc_;
     if (!(rc > 0) || e->n < 2) return GCS_OK;
@@ -881,8 +882,8 @@ int probe_density(gcs_engine* e)
     launch_exclusive_scan_small(e->stream, e->s_counts, e->s_offsets, e->n, e->s_total);
     HIPCHK(hipGetLastError());
     int pairs = 0;
-    HIPCHK(hipMemcpyAsync(&pairs, e->s_total, sizeof(int), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpy(&pairs, e->s_total, sizeof(int), hipMemcpyDeviceToHost));
     e->dense_mean = 2.0 * pairs / (double)e->n;
     e->dense = e->dense_mean * (list_u16(e->n) ? 1.0 : 2.0) > (double)e->dense_opt;
     return GCS_OK;

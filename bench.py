@@ -150,6 +150,9 @@ def make_engine(design, cfg, device, start_step, state=None):
     from gcs.engine import Engine
     e, _ = interphase.build_interphase(Engine, design, cfg, device=device)
     e.set_schedule(**interphase.interphase_schedule(cfg))
+    if os.environ.get("GCS_BENCH_DENSE") is not None:  # (experiments) the dense-start threshold of every engine
+        from gcs import _abi as A
+        e.set_option(A.OPT_DENSE_NEIGHBORS, int(os.environ["GCS_BENCH_DENSE"]))
     if state is not None:
         x, ctx = state
         e.set_positions(x)

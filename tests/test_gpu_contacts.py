@@ -174,6 +174,7 @@ def _fused_contacts(design, cfg, ctx, distance, updates, seed, x=None, **opts):
     e = engine_for(design, cfg)
     e.set_option(A.OPT_FUSED_STEP, 3)
     e.set_option(A.OPT_SMALL_PATH, 0)  # the list step (the small-system path counts contacts after its run)
+    e.set_option(A.OPT_DENSE_NEIGHBORS, 0)  # at any density (C1 at core scale 0.99 is dense)
     for k, v in opts.items():
         e.set_option(getattr(A, "OPT_" + k.upper()), v)
     if x is not None:
@@ -250,6 +251,7 @@ def test_fused_contacts_leave_the_trajectory_unchanged(c1_design):
     b = engine_for(c1_design, cfg)
     b.set_option(A.OPT_FUSED_STEP, 3)
     b.set_option(A.OPT_SMALL_PATH, 0)
+    b.set_option(A.OPT_DENSE_NEIGHBORS, 0)
     b.set_context(LATE)
     b.run(4 * STEPS_PER_UPDATE, first_step=LATE["step"], seed=53)
     assert np.array_equal(a.get_positions(), b.get_positions())

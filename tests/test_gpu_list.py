@@ -148,6 +148,7 @@ def test_list_small_and_ragged_sizes(n, small):
         if name == "e":
             s.set_option(A.OPT_FUSED_STEP, 3)
             s.set_option(A.OPT_SMALL_PATH, small)
+            s.set_option(A.OPT_DENSE_NEIGHBORS, 0)
         sysd[name] = s
     for s in sysd.values():
         s.run(20, seed=1, timestep=1e-4)

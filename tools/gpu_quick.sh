@@ -13,7 +13,7 @@ tail -2 $out/${tag}_tests.log
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --cpu-budget 0 --c5-steps 0 --cycle-scale 0 > $out/${tag}_bench.log 2>&1 || exit 1
 timeout -k 10 200 python bench.py --steps 200 --warmup 50 --cpu-budget 0 --c5-steps 0 --cycle-scale 0 --replicas-per-gpu 1 --no-start-window > $out/${tag}_bench_r1.log 2>&1 || exit 1
 for R in 1 4; do
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $out/prof_${tag}_r$R -o run --output-format csv -- \
+  GCS_BENCH_DENSE=0 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $out/prof_${tag}_r$R -o run --output-format csv -- \
     python3 bench.py --steps 300 --warmup 50 --cpu-budget 0 --c5-steps 0 --cycle-scale 0 --profile-steps 10 \
     --no-start-window --replicas-per-gpu $R > $out/${tag}_prof_r$R.log 2>&1 || exit 1
   cp "$(find $out/prof_${tag}_r$R -name '*kernel_stats.csv' | head -n 1)" $out/${tag}_r${R}_kernel_stats.csv

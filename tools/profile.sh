@@ -10,7 +10,10 @@ root=$(pwd)
 out=$root/gpurun_out/prof_$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
-bench=(python3 "$root/bench.py" --steps "$steps" --warmup 50 --cpu-budget 0 --profile-steps 10 --no-start-window --replicas-per-gpu "${REPLICAS:-1}")
+bench=(python3 "$root/bench.py" --steps "$steps" --warmup 50 --cpu-budget 0 --profile-steps 10 --no-start-window --replicas-per-gpu "${REPLICAS:-1}" --c5-steps 0 --cycle-scale 0)
+# the engines' density probe (GCS_OPT_DENSE_NEIGHBORS) makes rocprofv3 --kernel-trace segfault in the first graph
+# launch (engine.hip probe_density); the C2 window is list-step territory either way (25 neighbours)
+export GCS_BENCH_DENSE=0
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- "${bench[@]}" > "$out/trace.log" 2>&1 || exit $?
 i=0
 for ctrs in \
