@@ -246,7 +246,7 @@ struct gcs_engine {
     bool list_ok = false;       // the system admits the list step (a pair field, <= 256 classes, N < 2^24)
     int list_cap = 1024;        // GCS_OPT_LIST_CAP: list entries per particle (split over the tile's waves)
     size_t list_alloc = 0;      // allocated entries
-    int list_skin_pm = 400;     // GCS_OPT_LIST_SKIN: skin in 1/1000 of the pair cutoff
+    int list_skin_pm = 500;     // GCS_OPT_LIST_SKIN: skin in 1/1000 of the pair cutoff
     int list_every_opt = 0;     // GCS_OPT_LIST_EVERY: rebuild period in steps (0: from the noise amplitude)
     int list_every = 1;         // the period of the current run
     int list_waves = 4;         // GCS_OPT_LIST_WAVES: waves per tile (2: more tiles resident, for replica runs)
@@ -735,9 +735,11 @@ int ensure_list(gcs_engine* e)
     return GCS_OK;
 }
 
-// rebuild period: the skin must hold the largest displacement of ~4.5 sigma on each side of a pair for that many
-// steps (sigma = sqrt(2 T mu_max dt) per step; C2: 8 steps at skin 0.4 rc); the rare particle that outruns it is
-// searched exactly (k_lstep), so the period trades rebuild cost against fallbacks, never correctness
+// rebuild period: the skin must hold the largest displacement of ~3.95 sigma on each side of a pair for that many
+// steps (sigma = sqrt(2 T mu_max dt) per step; C2: 16 steps at skin 0.5 rc); the rare particle that outruns it is
+// searched exactly (k_lstep), so the period trades rebuild cost against fallbacks, never correctness.  Skin and
+// factor from a sweep on the bench (profiles/r03_skin_sweep.txt: 4 replicas, bead-updates/s): skin 0.4 / M 8 (4.5 sigma)
+// 6.17e9, 0.45 / 14 6.33e9, 0.5 / 13 6.27e9, 0.5 / 16 6.32e9, 0.5 / 18 6.1e9, 0.55 / 18 6.13e9, 0.6 / 20 5.97e9
 int auto_list_every(const gcs_engine* e, const gcs_bd_config* cfg)
 {
     if (e->list_every_opt > 0) return e->list_every_opt;
@@ -746,7 +748,7 @@ int auto_list_every(const gcs_engine* e, const gcs_bd_config* cfg)
     const double sigma = std::sqrt(2.0 * std::max(cfg->temperature, 0.0) * mu * cfg->timestep);
     const double half = 0.5 * (double)list_skin(e);
     if (!(sigma > 0)) return 64;
-    const double m = std::floor((half / (4.5 * sigma)) * (half / (4.5 * sigma)));
+    const double m = std::floor((half / (3.95 * sigma)) * (half / (3.95 * sigma)));
     return (int)std::min(64.0, std::max(1.0, m));
 }
 

@@ -23,7 +23,7 @@ else:
 x = design.positions
 n = x.shape[0]
 halo = domain.domain_halo(cfg)
-print(f"{config}: {n} beads, halo {halo:.3f} (list radius {max(cfg.a_core_diameter, cfg.b_core_diameter) * 1.4:.3f})")
+print(f"{config}: {n} beads, halo {halo:.3f} (list radius {max(cfg.a_core_diameter, cfg.b_core_diameter) * (1 + domain.LIST_SKIN):.3f})")
 for kind in ("boxes", "slabs"):
     for k in ranks:
         boxes = domain.plan_boxes(x, k) if kind == "boxes" else domain.plan_slabs(x[:, 2], k)
