@@ -250,6 +250,8 @@ struct gcs_engine {
     int list_every_opt = 0;     // GCS_OPT_LIST_EVERY: rebuild period in steps (0: from the noise amplitude)
     int list_every = 1;         // the period of the current run
     int list_waves = 4;         // GCS_OPT_LIST_WAVES: waves per tile (2: more tiles resident, for replica runs)
+    long long list_deal_opt = -1;  // GCS_OPT_LIST_DEAL: chunk -> wave pattern of the list build (-1: the default for
+                                   // list_waves, 0: round robin)
     bool l_need_build = true;   // the next list step must rebuild (run start without continuity)
     // small systems (N <= kSmallMax, GCS_OPT_SMALL_PATH): one single-workgroup launch per run (k_small) and its
     // persistent list state; small_cont: the next small run at small_step continues the last one (no rebuild)
@@ -678,6 +680,26 @@ bool rebuild_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) == 
 
 float list_skin(const gcs_engine* e) { return 1e-3f * (float)e->list_skin_pm * e->fa.pair_dist; }
 
+// the list build's chunk deal (kernels.hip deal_nth): the option, or the default for the waves per tile
+unsigned long long list_deal(const gcs_engine* e)
+{
+    if (e->list_deal_opt >= 0) return (unsigned long long)e->list_deal_opt;
+    return e->list_waves == 2 ? kListDeal2 : kListDeal4;
+}
+// a deal pattern is valid for W waves when its period is 1..15 and every nibble of the period names a wave < W
+bool deal_valid(long long d, int W)
+{
+    if (d == 0) return true;
+    const int T = (int)((unsigned long long)d >> 60);
+    if (T < 1 || T > 15) return false;
+    if ((unsigned long long)d & ~((1ull << 60) - 1ull) & ~(15ull << 60)) return false;
+    for (int p = 0; p < 15; ++p) {
+        const int w = (int)(((unsigned long long)d >> (4 * p)) & 15ull);
+        if (p < T ? w >= W : w != 0) return false;
+    }
+    return true;
+}
+
 // the list step's argument block: the shared one plus the lists and the skin (> 0 also makes the prime and the
 // tail build cell grids at cutoff + skin, so only list-path launches get it)
 ForceArgs list_args(const gcs_engine* e)
@@ -697,6 +719,7 @@ ForceArgs list_args(const gcs_engine* e)
     a.list_stride = (e->n + 63) & ~63;
     a.list_skin = list_skin(e);
     a.list_waves = e->list_waves;
+    a.list_deal = list_deal(e);
     a.par_hint = -1;
     return a;
 }
@@ -2842,6 +2865,14 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
     if (option == GCS_OPT_LIST_WAVES) {
         if (value != 2 && value != 4) return fail(GCS_EINVAL, "list waves per tile must be 2 or 4");
         e->list_waves = (int)value;
+        if (!deal_valid(e->list_deal_opt, e->list_waves)) e->list_deal_opt = -1;  // back to the default
+        drop_graph(e);
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_LIST_DEAL) {
+        if (value != -1 && !deal_valid(value, e->list_waves))
+            return fail(GCS_EINVAL, "list deal must be -1, 0 or (period << 60 | wave nibbles < waves per tile)");
+        e->list_deal_opt = value;
         drop_graph(e);
         return GCS_OK;
     }

@@ -225,6 +225,7 @@ struct ForceArgs {
     int list_stride;        // >= N
     float list_skin;        // > 0 only in the list path's own argument block
     int list_waves;         // waves per tile (list segments): 4, or 2 (GCS_OPT_LIST_WAVES)
+    unsigned long long list_deal;  // list build: candidate chunk -> wave segment pattern (GCS_OPT_LIST_DEAL; 0: round robin)
     int par_hint;           // >= 0: ctx->parity of this launch, known to the host at enqueue (the slot loads need not
                             // wait for the context); -1: read it
     // the contact-map update fused into a list step (stage_interphase/contact_map.cpp:33-63): every pair i < j of
@@ -249,6 +250,11 @@ __host__ __device__ inline unsigned long long list_acc_identity(int k)
 {
     return (k >= 9 && k < 12) ? 0xffffffffull : 0ull;  // bbox lo: the largest ordered value; everything else 0
 }
+// the list build's default chunk deal per waves per tile (kernels.hip deal_nth; 0: round robin): the last wave, which
+// also carries the step's particle-local terms, takes 1 chunk in 3 ("001") / 1 in 7 ("0120123").  Same-box A/B
+// (tools/deal_sweep.sh, profiles/r03c_deal_sweep.txt): 4 replicas 5.85-6.21 -> 6.24-6.26e9, single 2.52-2.53 -> 2.60-2.61e9
+constexpr unsigned long long kListDeal2 = (3ull << 60) | 0x100ull;
+constexpr unsigned long long kListDeal4 = (7ull << 60) | 0x3210210ull;
 constexpr int kMaxListWaves = 4;  // waves per tile of the list kernels (each owns one list segment): 2 or 4
 constexpr int kMaxTypes = 256;          // pair-factor classes (8 bits of a list entry)
 constexpr int kListIndexBits = 24;      // particle index bits of a list entry

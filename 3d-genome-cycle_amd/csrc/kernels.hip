@@ -1732,6 +1732,30 @@ __device__ __forceinline__ int list_entry(const uint2* w, int u)
     }
 }
 
+// The list build's deal of candidate chunks to the waves (GCS_OPT_LIST_DEAL): chunk p of every period of T = d >> 60
+// chunks goes to wave nibble p of d (0 < T <= 15; d = 0: round robin over the waves).  The wave's entries form its list
+// segment, and the list step's last wave also carries the particle-local terms: a pattern that deals that wave fewer
+// chunks evens the step's waves out.  Any pattern covers every chunk exactly once, in increasing order per wave, so
+// the union of a slot's segments (the pair set) does not depend on it.  Scalar arithmetic (every operand uniform).
+__device__ __forceinline__ int deal_wave(unsigned long long d, int p)
+{
+    return (int)((d >> (4 * p)) & 15ull);
+}
+__device__ __forceinline__ int deal_count(unsigned long long d, int T, int w, int upto)
+{
+    int k = 0;
+    for (int p = 0; p < upto && p < T; ++p) k += deal_wave(d, p) == w ? 1 : 0;
+    return k;
+}
+// the c-th chunk of wave w (kw = its chunks per period, > 0)
+__device__ __forceinline__ int deal_nth(unsigned long long d, int T, int kw, int w, int c)
+{
+    int r = c % kw, p = 0;
+    for (; p < T; ++p)
+        if (deal_wave(d, p) == w && r-- == 0) break;
+    return (c / kw) * T + p;
+}
+
 template <int MODE, int NG, typename LE = int>
 __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const ForceArgs& a, int lane, int s,
                                        int s_begin, int s_end, float4 pi, float bi, float& fx, float& fy, float& fz,
@@ -1808,13 +1832,18 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
     const float ahi = kA * pi.w, bhi = kB * bi;
     const int G = (total + kSub - 1) / kSub;   // my group's chunks; chunk c takes v = c + G * i
     const int Gmax = uniform(wave_max_int(G));
-    const int nchunk = Gmax > wv ? (Gmax - wv + nwv - 1) / nwv : 0;
+    // kModeList: the chunks of a deal pattern (deal_nth), otherwise wave wv takes chunks wv, wv + nwv, ...
+    const unsigned long long deal = MODE == kModeList ? a.list_deal : 0ull;
+    const int dT = (int)(deal >> 60);
+    const int dkw = deal ? deal_count(deal, dT, wv, dT) : 0;
+    const int nchunk = deal ? (dkw ? (Gmax / dT) * dkw + deal_count(deal, dT, wv, Gmax % dT) : 0)
+                            : (Gmax > wv ? (Gmax - wv + nwv - 1) / nwv : 0);
 
     float4 np[FPL];
     float nb[FPL];
     int nj[FPL];
     auto fetch = [&](int c) {
-        const int cg = wv + c * nwv;  // chunk index within every group
+        const int cg = deal ? deal_nth(deal, dT, dkw, wv, c) : wv + c * nwv;  // chunk index within every group
 #pragma unroll
         for (int f = 0; f < FPL; ++f) {
             const int i = gl + GL * f;  // slot

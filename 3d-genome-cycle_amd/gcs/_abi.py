@@ -40,6 +40,20 @@ OPT_LIST_CAP = 12
 OPT_LIST_WAVES = 13
 OPT_SMALL_PATH = 14
 OPT_DENSE_NEIGHBORS = 15
+OPT_LIST_DEAL = 16
+
+
+def list_deal(pattern: str) -> int:
+    """GCS_OPT_LIST_DEAL value of a chunk deal pattern: "0120123" = chunk p of every period of 7 goes to wave
+    pattern[p] (include/gcs.h); "" = round robin (0)."""
+    if not pattern:
+        return 0
+    if len(pattern) > 15:
+        raise ValueError("a deal pattern has at most 15 chunks")
+    v = len(pattern) << 60
+    for p, c in enumerate(pattern):
+        v |= int(c) << (4 * p)
+    return v - (1 << 64) if v >= 1 << 63 else v  # as the int64 the ABI takes
 
 ENERGY_KINDS = ("pair", "softwell", "bonds", "bending", "wall_in", "wall_out", "point_source", "kinetochore_fiber")
 

@@ -530,8 +530,8 @@ def replica_main(args):
                            (A.OPT_LIST_WAVES, list_waves)):
                 e.set_option(opt, v)
             for kv in args.engine_opt:  # experiments: --engine-opt list_skin=300 (gcs._abi OPT_<NAME>)
-                name, v = kv.split("=")
-                e.set_option(getattr(A, "OPT_" + name.upper()), int(v))
+                name, v = kv.split("=")  # list_deal=d:0120123 -> a deal pattern (gcs._abi.list_deal)
+                e.set_option(getattr(A, "OPT_" + name.upper()), A.list_deal(v[2:]) if v.startswith("d:") else int(v))
             if args.cu_split and R > 1:
                 # replica k on CUs c with (c mod R) == k ("interleave") or a contiguous R-th of them ("block")
                 ncu = args.cu_count
