@@ -22,11 +22,6 @@ __device__ __forceinline__ bool contact_pair(float4 p, float4 q, float d2)
     return r2 < d2;
 }
 
-// Fibonacci hashing of the pair key onto 2^bits slots
-__device__ __forceinline__ unsigned long long contact_slot(unsigned long long key, int bits)
-{
-    return (key * 0x9E3779B97F4A7C15ull) >> (64 - bits);
-}
 
 // One thread per cell-sorted particle of any cell list (the engine's own, or a search list built for the
 // distance): the stencil reach per axis is ceil(distance / cell edge) cells (for the engine's list, whose cells
@@ -52,7 +47,6 @@ __global__ __launch_bounds__(256) void k_contact_insert(const DevCtx* __restrict
     const int c = scell[s];
     const int nx = g.n[0], ny = g.n[1], nz = g.n[2];
     const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
-    const unsigned long long mask = (1ull << bits) - 1ull;
     for (int z = max(cz - rz, 0); z <= min(cz + rz, nz - 1); ++z)
         for (int y = max(cy - ry, 0); y <= min(cy + ry, ny - 1); ++y) {
             const int base = (z * ny + y) * nx;
@@ -61,18 +55,7 @@ __global__ __launch_bounds__(256) void k_contact_insert(const DevCtx* __restrict
                 const int j = sidx[t];
                 if (j <= i || !contact_pair(p, spos[t], d2)) continue;
                 const unsigned long long key = ((unsigned long long)(unsigned)i << 32) | (unsigned)j;
-                unsigned long long h = contact_slot(key, bits);
-                bool done = false;
-                for (int probe = 0; probe < kContactMaxProbe; ++probe) {
-                    const unsigned long long prev = atomicCAS(&keys[h], kContactEmpty, key);
-                    if (prev == kContactEmpty || prev == key) {
-                        atomicAdd(&counts[h], 1u);
-                        done = true;
-                        break;
-                    }
-                    h = (h + 1) & mask;
-                }
-                if (!done) atomicOr(overflow, 1);
+                if (!contact_count(keys, counts, bits, key)) atomicOr(overflow, 1);
             }
         }
 }

@@ -758,11 +758,13 @@ int ensure_list(gcs_engine* e)
     return GCS_OK;
 }
 
-// rebuild period: the skin must hold the largest displacement of ~3.95 sigma on each side of a pair for that many
+// rebuild period: the skin must hold the largest displacement of ~4.15 sigma on each side of a pair for that many
 // steps (sigma = sqrt(2 T mu_max dt) per step; C2: 16 steps at skin 0.5 rc); the rare particle that outruns it is
 // searched exactly (k_lstep), so the period trades rebuild cost against fallbacks, never correctness.  Skin and
 // factor from a sweep on the bench (profiles/r03_skin_sweep.txt: 4 replicas, bead-updates/s): skin 0.4 / M 8 (4.5 sigma)
 // 6.17e9, 0.45 / 14 6.33e9, 0.5 / 13 6.27e9, 0.5 / 16 6.32e9, 0.5 / 18 6.1e9, 0.55 / 18 6.13e9, 0.6 / 20 5.97e9
+// (C2's largest mobility 1, dt 1e-5: (0.075 / (4.15 sigma))^2 = 16.3 -> 16; 3.95 sigma gave 18, whose fallbacks
+// reach 1.7e-3 of the particle-steps over 20,000 C2 steps)
 int auto_list_every(const gcs_engine* e, const gcs_bd_config* cfg)
 {
     if (e->list_every_opt > 0) return e->list_every_opt;
@@ -771,7 +773,7 @@ int auto_list_every(const gcs_engine* e, const gcs_bd_config* cfg)
     const double sigma = std::sqrt(2.0 * std::max(cfg->temperature, 0.0) * mu * cfg->timestep);
     const double half = 0.5 * (double)list_skin(e);
     if (!(sigma > 0)) return 64;
-    const double m = std::floor((half / (3.95 * sigma)) * (half / (3.95 * sigma)));
+    const double m = std::floor((half / (4.15 * sigma)) * (half / (4.15 * sigma)));
     return (int)std::min(64.0, std::max(1.0, m));
 }
 

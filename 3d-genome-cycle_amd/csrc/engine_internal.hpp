@@ -30,6 +30,28 @@ constexpr int kEnergyKinds = 8;
 constexpr unsigned long long kContactEmpty = ~0ull;  // contact-map hash table: free slot
 constexpr int kContactMaxProbe = 4096;               // linear-probe bound of one insert (then: overflow flag)
 
+// Count one contact pair (key = i << 32 | j) into the open-addressing table (Fibonacci hash onto 2^bits slots, linear
+// probing).  Each probed key is LOADED first and claimed by CAS only when the slot is empty: a key never moves or
+// leaves its slot between clears (a memset between launches), so a load can be stale only as "empty", which the
+// CAS then settles; a pair already in the table (the common case: the same contacts recur every update of a window)
+// costs one atomic instead of two.  false: kContactMaxProbe slots probed without a place (the caller flags overflow).
+__device__ __forceinline__ bool contact_count(unsigned long long* keys, unsigned* counts, int bits,
+                                              unsigned long long key)
+{
+    const unsigned long long mask = (1ull << bits) - 1ull;
+    unsigned long long h = (key * 0x9E3779B97F4A7C15ull) >> (64 - bits);
+    for (int probe = 0; probe < kContactMaxProbe; ++probe) {
+        unsigned long long cur = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == kContactEmpty) cur = atomicCAS(&keys[h], kContactEmpty, key);
+        if (cur == kContactEmpty || cur == key) {
+            atomicAdd(&counts[h], 1u);
+            return true;
+        }
+        h = (h + 1) & mask;
+    }
+    return false;
+}
+
 struct Grid {
     float lo[3];
     float inv[3];

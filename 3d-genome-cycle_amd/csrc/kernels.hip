@@ -2583,7 +2583,7 @@ __global__ __launch_bounds__(256) void k_tail(DevCtx* ctx, ForceArgs a, int fblo
 #endif
 
 // the contact map's pair count (contacts.hip k_contact_insert: strict fp32 predicate, Fibonacci-hashed open
-// addressing, one atomicCAS per probe); i < j by particle index, so each pair counts once
+// addressing, contact_count); i < j by particle index, so each pair counts once
 __device__ __forceinline__ void list_contact(const ForceArgs& a, float4 p, float4 q, int i, int j)
 {
     if (j <= i) return;
@@ -2591,17 +2591,7 @@ __device__ __forceinline__ void list_contact(const ForceArgs& a, float4 p, float
     const float r2 = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
     if (!(r2 < a.contact_d2)) return;
     const unsigned long long key = ((unsigned long long)(unsigned)i << 32) | (unsigned)j;
-    const unsigned long long mask = (1ull << a.c_bits) - 1ull;
-    unsigned long long h = (key * 0x9E3779B97F4A7C15ull) >> (64 - a.c_bits);
-    for (int probe = 0; probe < kContactMaxProbe; ++probe) {
-        const unsigned long long prev = atomicCAS(&a.c_keys[h], kContactEmpty, key);
-        if (prev == kContactEmpty || prev == key) {
-            atomicAdd(&a.c_counts[h], 1u);
-            return;
-        }
-        h = (h + 1) & mask;
-    }
-    atomicOr(a.c_overflow, 1);
+    if (!contact_count(a.c_keys, a.c_counts, a.c_bits, key)) atomicOr(a.c_overflow, 1);
 }
 
 // The list step's context update, by thread 0 of the step's final workgroup once every partial is reduced: the

@@ -1,6 +1,6 @@
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/r03c_gpu_tests.log 2>&1 || { tail -40 gpurun_out/r03c_gpu_tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread > gpurun_out/r03c_gpu_tests.log 2>&1 || { tail -40 gpurun_out/r03c_gpu_tests.log; exit 1; }
 tail -3 gpurun_out/r03c_gpu_tests.log
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r03c_bench.log 2>&1 || { tail -30 gpurun_out/r03c_bench.log; exit 1; }
 tail -1 gpurun_out/r03c_bench.log
