@@ -304,6 +304,40 @@ int gcs_store_write_array(gcs_store* s, const char* path, int32_t dtype, int32_t
     return rc;
 }
 
+int gcs_store_write_deflated(gcs_store* s, const char* path, int32_t dtype, int32_t rank, const int64_t* dims,
+                             const void* zdata, int64_t zbytes, int32_t deflate)
+{
+    if (!s || !path || !dims || !zdata) return fail("null argument");
+    if (rank < 1 || rank > 2) return fail("rank must be 1 or 2");
+    if (deflate < 1 || deflate > 9) return fail("deflate level must be in [1, 9]");
+    if (zbytes <= 0) return fail("empty compressed chunk");
+    const hid_t ft = file_type(dtype);
+    if (ft < 0) return fail("unknown dtype");
+    Silence q;
+    if (replace(s->file, path)) return 1;
+    hsize_t hd[2] = {0, 0};
+    for (int k = 0; k < rank; ++k) {
+        hd[k] = (hsize_t)dims[k];
+        if (hd[k] == 0) return fail("empty array");
+    }
+    hid_t sp = H5Screate_simple(rank, hd, nullptr);
+    hid_t cp = H5Pcreate(H5P_DATASET_CREATE);
+    H5Pset_chunk(cp, rank, hd);  // one chunk, as gcs_store_write_array lays a filtered array out
+    H5Pset_deflate(cp, (unsigned)deflate);
+    hid_t lp = lcpl_parents();
+    hid_t d = H5Dcreate2(s->file, path, ft, sp, lp, cp, H5P_DEFAULT);
+    const hsize_t off[2] = {0, 0};
+    int rc = 0;
+    // filter mask 0: every filter of the pipeline (deflate) was applied to the chunk
+    if (d < 0 || H5Dwrite_chunk(d, H5P_DEFAULT, 0u, off, (size_t)zbytes, zdata) < 0)
+        rc = fail(std::string("cannot write ") + path);
+    if (d >= 0) H5Dclose(d);
+    H5Pclose(lp);
+    H5Pclose(cp);
+    H5Sclose(sp);
+    return rc;
+}
+
 int gcs_store_read_array(gcs_store* s, const char* path, int32_t dtype, void* buf, int64_t cap_elems, int32_t* rank,
                          int64_t* dims)
 {

@@ -48,6 +48,12 @@ int gcs_store_read_strings(gcs_store* s, const char* path, char* buf, int64_t ca
 /* rank 0 (scalar) to 2; deflate 0-9 (0 = none); scaleoffset_int != 0: integer scale-offset filter, min bits 0 */
 int gcs_store_write_array(gcs_store* s, const char* path, int32_t dtype, int32_t rank, const int64_t* dims,
                           const void* data, int32_t deflate, int32_t scaleoffset_int);
+/* rank 1 or 2, one chunk holding the whole array, deflate filter at level `deflate` (1-9), written from `zdata`: the
+ * array (in the file type's byte order) already deflated by the caller into zlib format (compress2 at that level),
+ * zbytes long.  The file is the one gcs_store_write_array(..., deflate, 0) writes; the caller can deflate frames on
+ * several host threads while one thread owns the (not thread-safe) HDF5 library. */
+int gcs_store_write_deflated(gcs_store* s, const char* path, int32_t dtype, int32_t rank, const int64_t* dims,
+                             const void* zdata, int64_t zbytes, int32_t deflate);
 /* converts to dtype; dims[0..rank) out; cap_elems = capacity of buf in elements (0 to query) */
 int gcs_store_read_array(gcs_store* s, const char* path, int32_t dtype, void* buf, int64_t cap_elems,
                          int32_t* rank, int64_t* dims);

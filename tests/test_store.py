@@ -175,3 +175,30 @@ def test_async_writer_keeps_order_and_raises(prepared):
         w._put(bad)  # a failing write: raised on this thread at close, not lost
         with pytest.raises(store.StoreError):
             w.close()
+
+
+def test_deflated_frames_equal_the_filter_path(prepared):
+    """gcs_store_write_deflated (the async writer's frames, deflated on a thread pool): the chunk stored is byte for
+    byte the one HDF5's deflate-6 filter stores for the same positions, and the dataset reads back the same"""
+    p, _ = prepared
+    x = store.quantize_positions(np.random.default_rng(5).normal(size=(3000, 3)))
+    with store.SimulationStore(p) as s:
+        s.set_stage("interphase")
+        s.save_positions(1000, x, quantized=True)
+        s.save_positions(2000, x, quantized=True, zdata=store.deflated_frame(x))
+        assert np.array_equal(s.load_positions(1000), s.load_positions(2000))
+        assert np.array_equal(s.load_positions(2000).astype(np.float32), x)
+    if PY39 is None:
+        pytest.skip("no h5py interpreter for the raw-chunk comparison")
+    code = f"""
+import h5py
+f = h5py.File({str(p)!r}, "r")
+a, b = f["stages/interphase/1000/positions"], f["stages/interphase/2000/positions"]
+assert b.compression == "gzip" and b.compression_opts == 6 and b.chunks == (3000, 3)
+ma, ca = a.id.read_direct_chunk((0, 0))
+mb, cb = b.id.read_direct_chunk((0, 0))
+assert ma == mb == 0 and ca == cb, (ma, mb, len(ca), len(cb))
+print("ok")
+"""
+    out = subprocess.run([PY39, "-c", code], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stderr
