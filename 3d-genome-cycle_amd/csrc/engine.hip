@@ -276,6 +276,7 @@ struct gcs_engine {
     // to one longer run).  Anything that touches positions, context, schedule or cells clears it.
     bool chain_valid = false;
     int64_t chain_step = 0;
+    double chain_dt = 0;  // the timestep begin_run last wrote to ctx->dt_used
     int chain_version = -1;
 };
 
@@ -792,10 +793,8 @@ void enqueue_list_step(gcs_engine* e, bool build, int lflags, double contact = 0
 {
     ForceArgs la = list_args(e);
     la.par_hint = parity;
-    if (contact > 0) {  // the pending contact update, counted from this step's start positions
+    if (contact > 0) {  // the pending contact update, counted from this step's start positions (its distance: ctx)
         la.contact_on = 1;
-        const float d = (float)contact;
-        la.contact_d2 = d * d;  // fp32 product, as k_contact_insert forms it
         la.c_keys = e->c_keys;
         la.c_counts = e->c_counts;
         la.c_bits = e->c_bits;
@@ -945,12 +944,18 @@ int begin_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
     a.seed_lo = (unsigned)cfg->seed;
     a.seed_hi = (unsigned)(cfg->seed >> 32);
     a.noise_mode = cfg->noise;
-    long long st = first_step;
-    if ((rc = set_ctx_field(e, offsetof(DevCtx, step), &st, sizeof(st)))) return rc;
-    double dt = cfg->timestep;
-    if ((rc = set_ctx_field(e, offsetof(DevCtx, dt_used), &dt, sizeof(dt)))) return rc;
     const bool fused = fused_path(e, cfg->spacestep > 0);
     const bool cont = fused && e->chain_valid && e->chain_step == first_step && e->chain_version == e->topo_version;
+    // a continuing list-step chain at the same timestep already has ctx->step == first_step (its tails counted the
+    // steps) and this dt_used (only spacestep changes it): no host copy, which from pageable memory would stall the
+    // host until the stream drained (the interphase driver runs a chunk per contact update, every 20 steps)
+    if (!(cont && list_path(e, cfg->spacestep > 0) && e->chain_dt == cfg->timestep)) {
+        long long st = first_step;
+        if ((rc = set_ctx_field(e, offsetof(DevCtx, step), &st, sizeof(st)))) return rc;
+        double dt = cfg->timestep;
+        if ((rc = set_ctx_field(e, offsetof(DevCtx, dt_used), &dt, sizeof(dt)))) return rc;
+    }
+    e->chain_dt = cfg->timestep;
     e->chain_valid = false;
     e->small_cont = false;
     if (list_path(e, cfg->spacestep > 0)) {
@@ -1773,10 +1778,18 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
         while (done < steps) {
             const int64_t st = first_step + done;
             const int phase = (int)(((st % M) + M) % M);
-            if (e->c_pending > 0 || e->l_need_build || G == 0) {
-                // the contact update the host asked for after the last step, a run start's rebuild, or no graphs
-                enqueue_list_step(e, e->l_need_build || phase == 0, list_flags(e, st), e->c_pending, par(done));
+            // the contact update the host asked for after the last step: counted by this stretch's first step, its
+            // distance set in the context (so the stretch's graph does not depend on it)
+            const bool ct = e->c_pending > 0;
+            if (ct) {
+                const float d = (float)e->c_pending;
+                launch_set_contact(e->stream, e->ctx, d * d);  // fp32 product, as k_contact_insert forms it
                 e->c_pending = 0;
+                e->rstats.fused_contact_steps++;
+            }
+            if (e->l_need_build || G == 0) {
+                // a run start's rebuild, or no graphs
+                enqueue_list_step(e, e->l_need_build || phase == 0, list_flags(e, st), ct ? 1.0 : 0.0, par(done));
                 e->l_need_build = false;
                 ++done;
                 e->rstats.eager_steps++;
@@ -1785,9 +1798,11 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
             const int len = (int)std::min<int64_t>(G, steps - done);
             const int p0 = par(done);
             hipGraphExec_t x = nullptr;
-            rc = cached_graph(e, key, phase, p0, len, [&]() {
+            // cache slot: rebuild phase, and whether the first step counts contacts
+            rc = cached_graph(e, key, phase | (ct ? 1 << 20 : 0), p0, len, [&]() {
                 for (int k = 0; k < len; ++k)
-                    enqueue_list_step(e, (phase + k) % M == 0, list_flags(e, st + k), 0, p0 ^ (k & 1));
+                    enqueue_list_step(e, (phase + k) % M == 0, list_flags(e, st + k), (ct && k == 0) ? 1.0 : 0.0,
+                                      p0 ^ (k & 1));
             }, &x);
             if (rc || (rc = launch_graph(e, x))) return rc;
             e->rstats.graph_steps += len;
@@ -1945,9 +1960,12 @@ int gcs_engine_contacts_update(gcs_engine* e, double distance)
     int rc;
     if (!e->c_keys) {
         int bits = e->c_bits_opt;
-        if (bits <= 0) {  // >= 32 slots per particle (the distinct pairs of a 10-sample window stay well below)
+        if (bits <= 0) {
+            // >= 512 slots per particle, at most 2^28 (3 GB): a C2 window of the reference's cadence (10 samples x
+            // 50 updates) holds ~4.1 million distinct pairs, 12 % of C2's 2^25 slots; at 128 per particle (2^23,
+            // 49 % full) the probe chains cost 3 % of the interphase stage (tools/interphase_probe.py, r03d)
             bits = 12;
-            while (bits < 34 && ((int64_t)1 << bits) < 128 * (int64_t)e->n) ++bits;
+            while (bits < 28 && ((int64_t)1 << bits) < 512 * (int64_t)e->n) ++bits;
         }
         const size_t slots = (size_t)1 << bits;
         if ((rc = dalloc(&e->c_keys, slots)) || (rc = dalloc(&e->c_counts, slots)) || (rc = dalloc(&e->c_flags, 2)))

@@ -101,7 +101,7 @@ struct DevCtx {
     long long lbuilds;
     long long lfallback;
     int lnslots;  // slots of the current lists (binned particles: N, or a decomposed domain's owned + ghosts)
-    int pad5;
+    float contact_d2;  // the squared distance of the contact update a list step counts (k_set_contact, fp32 product)
 };
 
 // an axis-aligned box [lo, hi) (a decomposed domain's own box, or a peer's region: its box extended by the halo)
@@ -251,9 +251,8 @@ struct ForceArgs {
     int par_hint;           // >= 0: ctx->parity of this launch, known to the host at enqueue (the slot loads need not
                             // wait for the context); -1: read it
     // the contact-map update fused into a list step (stage_interphase/contact_map.cpp:33-63): every pair i < j of
-    // the step's START positions closer than sqrt(contact_d2) (strict fp32 predicate) is counted into the table
+    // the step's START positions closer than sqrt(DevCtx::contact_d2) (strict fp32 predicate) is counted into the table
     int contact_on;
-    float contact_d2;
     unsigned long long* c_keys;
     unsigned* c_counts;
     int c_bits;
@@ -334,6 +333,7 @@ void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a);
 // flags: 1 apply the schedule, 2 the next step rebuilds (bounding box -> grid), 4 neighbour-count statistics,
 // 8 decomposed (a.dom_on): the owned slots only, the local reduction into a.dom_red instead of the tail
 void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags);
+void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2);
 // the decomposed list step's tail from the allreduced buffer glob (one workgroup), then the shared particles'
 // positions into both buffers (by index and by slot) and the send bands' header rows zeroed
 void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const double* glob, int flags,

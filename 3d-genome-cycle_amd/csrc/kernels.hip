@@ -2584,12 +2584,12 @@ __global__ __launch_bounds__(256) void k_tail(DevCtx* ctx, ForceArgs a, int fblo
 
 // the contact map's pair count (contacts.hip k_contact_insert: strict fp32 predicate, Fibonacci-hashed open
 // addressing, contact_count); i < j by particle index, so each pair counts once
-__device__ __forceinline__ void list_contact(const ForceArgs& a, float4 p, float4 q, int i, int j)
+__device__ __forceinline__ void list_contact(const ForceArgs& a, float d2, float4 p, float4 q, int i, int j)
 {
     if (j <= i) return;
     const float dx = __fsub_rn(p.x, q.x), dy = __fsub_rn(p.y, q.y), dz = __fsub_rn(p.z, q.z);
     const float r2 = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
-    if (!(r2 < a.contact_d2)) return;
+    if (!(r2 < d2)) return;
     const unsigned long long key = ((unsigned long long)(unsigned)i << 32) | (unsigned)j;
     if (!contact_count(a.c_keys, a.c_counts, a.c_bits, key)) atomicOr(a.c_overflow, 1);
 }
@@ -2944,6 +2944,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     const float cs = (float)ctx->cs;
     const float D = ctx->ldisp;
     const float lrc_b = ctx->lrc_b;
+    // the contact distance from the context (k_set_contact before the launch), so a captured graph serves any update
+    const float cd2 = CT ? ctx->contact_d2 : 0.f;
     __syncthreads();  // s_tab
 
     const int pk = __float_as_int(pi.w);
@@ -2961,7 +2963,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     const bool fb = act && (di > slack || (cw & kListOverflow) != 0);
     // contacts (CT): the lists must cover the contact distance; a particle whose list does not is searched for its
     // contacts only (its forces take exactly the path they take without contacts: identical bits)
-    const float rcc = CT ? fmaxf(rc, sqrtf(a.contact_d2)) : rc;
+    const float rcc = CT ? fmaxf(rc, sqrtf(cd2)) : rc;
     const bool fbc = CT && valid && (di > 0.999f * a.list_skin - D - fmaxf(rcc - lrc_b, 0.f) || (cw & kListOverflow) != 0);
 
     // 2. the particle-local terms (a dependent-gather chain: first, on the last wave), parked in LDS
@@ -3002,7 +3004,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
             if constexpr (CT) {
 #pragma unroll
                 for (int u = 0; u < kU; ++u)
-                    if (!fbc && k0 + u < cnt) list_contact(a, pi, q[u], i, __float_as_int(q[u].w) & kIdx);
+                    if (!fbc && k0 + u < cnt) list_contact(a, cd2, pi, q[u], i, __float_as_int(q[u].w) & kIdx);
             }
         }
         // exact search of the build's cell list for the particles the lists may not cover: a partner within rc
@@ -3071,7 +3073,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
                         const int t0 = a.cstart[base + x0], t1 = a.cstart[base + x1 + 1];
                         for (int t = t0 + lane; t < t1; t += kTile) {
                             const float4 q = qc[t];
-                            if (t != sL) list_contact(a, pL, q, iL, __float_as_int(q.w) & kIdx);
+                            if (t != sL) list_contact(a, cd2, pL, q, iL, __float_as_int(q.w) & kIdx);
                         }
                     }
             }
@@ -3870,6 +3872,15 @@ static void launch_list_step_ct(hipStream_t s, DevCtx* ctx, const ForceArgs& a, 
         else
             hipLaunchKernelGGL((k_lstep<int, 4, CT>), g, dim3(256), 0, s, ctx, a, flags);
     }
+}
+
+__global__ void k_set_contact(DevCtx* ctx, float d2)
+{
+    ctx->contact_d2 = d2;
+}
+void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2)
+{
+    hipLaunchKernelGGL(k_set_contact, dim3(1), dim3(1), 0, s, ctx, d2);
 }
 
 void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)

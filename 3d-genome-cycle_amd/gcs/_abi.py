@@ -127,7 +127,8 @@ class ListStats(C.Structure):
 
 class RunStats(C.Structure):
     _fields_ = [("graph_launches", _i64), ("graph_steps", _i64), ("eager_steps", _i64), ("graphs_captured", _i64),
-                ("graphs_cached", _i64), ("small_launches", _i64), ("small_steps", _i64)]
+                ("graphs_cached", _i64), ("small_launches", _i64), ("small_steps", _i64),
+                ("fused_contact_steps", _i64)]
 
 
 # name -> (restype, argtypes); the exported surface of include/gcs.h

@@ -388,8 +388,8 @@ int gcs_engine_get_list_stats(gcs_engine* e, gcs_list_stats* out);
 
 /* How gcs_engine_run / gcs_engine_domain_run issued their steps (cumulative over the engine's life): steps
  * replayed from captured hipGraphs (any stretch of up to GCS_OPT_GRAPH_STEPS steps, captured once per rebuild
- * phase, starting buffer parity and length) and steps launched eagerly (a run start's forced list rebuild, a
- * step carrying a deferred contact update, GCS_OPT_GRAPH_STEPS 0).  Replaces nothing in the reference (the
+ * phase, starting buffer parity, length and whether its first step counts a deferred contact update) and steps
+ * launched eagerly (a run start's forced list rebuild, GCS_OPT_GRAPH_STEPS 0).  Replaces nothing in the reference (the
  * integrator loop of micromd, stage_interphase/simulation_driver_interphase.cpp:57-63, has no launches). */
 typedef struct gcs_run_stats {
     int64_t graph_launches;   /* hipGraphLaunch calls */
@@ -399,6 +399,7 @@ typedef struct gcs_run_stats {
     int64_t graphs_cached;    /* captured sequences held now */
     int64_t small_launches;   /* single-workgroup launches of the small-system path (GCS_OPT_SMALL_PATH) */
     int64_t small_steps;      /* steps they ran */
+    int64_t fused_contact_steps; /* list steps that counted a deferred contact update (gcs_engine_contacts_update) */
 } gcs_run_stats;
 int gcs_engine_get_run_stats(gcs_engine* e, gcs_run_stats* out);
 

@@ -198,8 +198,8 @@ def _fused_contacts(design, cfg, ctx, distance, updates, seed, x=None, **opts):
 
 def _check_fused(got, snaps, distance, runs, updates):
     exp = expected_table(snaps, distance)
-    # the update steps ran eagerly (the contact-counting instantiation), everything else from graphs
-    assert runs["eager_steps"] == updates, runs
+    # every update was counted inside a list step (the contact-counting instantiation, replayed from graphs)
+    assert runs["fused_contact_steps"] == updates and runs["eager_steps"] == 0, runs
     assert got.shape == exp.shape and np.array_equal(got, exp)
     assert (got[:, 0] < got[:, 1]).all() and got[:, 2].max() <= updates
 

@@ -11,12 +11,13 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "3d-genome-cycle_amd"))
-from gcs import interphase, synthetic  # noqa: E402
+from gcs import _abi, interphase, synthetic  # noqa: E402
 from gcs.config import InterphaseConfig  # noqa: E402
 from gcs.engine import Engine  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 relax = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
+cbits = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0]  # GCS_OPT_CONTACT_BITS (0: default)
 
 
 def timed(eng, acc):
@@ -35,9 +36,10 @@ def timed(eng, acc):
 
 
 d = synthetic.make_c2(1)
-for contacts in (True, False):
+for contacts, bits in [(True, b) for b in cbits] + [(False, 0)]:
     cfg = InterphaseConfig()
     eng, _ = interphase.build_interphase(Engine, d, cfg)
+    eng.set_option(_abi.OPT_CONTACT_BITS, bits)
     acc = defaultdict(lambda: [0.0, 0])
     timed(eng, acc)
     drv = interphase.InterphaseDriver(eng, d, cfg, store=None, log=None)
@@ -49,6 +51,9 @@ for contacts in (True, False):
     drv.run_simulation(steps, contacts=contacts)
     eng.synchronize()
     t2 = time.perf_counter()
+    if contacts:
+        print(f"  contact bits {bits or 'default'}: last window's table {len(drv.last_contacts)} distinct pairs",
+              flush=True)
     print(f"contacts={contacts}: relaxation {relax} steps {t1 - t0:.2f} s; simulation {steps} steps {t2 - t1:.2f} s "
           f"= {steps / (t2 - t1):.0f} steps/s ({d.n * steps / (t2 - t1):.3e} bead-updates/s)", flush=True)
     r1 = eng.run_stats()
@@ -56,4 +61,27 @@ for contacts in (True, False):
     print("  list:", eng.list_stats(), flush=True)
     for k, (s, n) in sorted(acc.items(), key=lambda kv: -kv[1][0]):
         print(f"  {k:22s} {n:7d} calls {s:8.3f} s  {1e3 * s / max(n, 1):8.3f} ms/call", flush=True)
+    eng.close()
+
+# the step loop alone, from the same start (after a short run): graph stretches of 20 vs 1,000 steps, with and
+# without a contact update per 20 steps
+cfg = InterphaseConfig()
+for chunk, contacts in ((1000, False), (20, False)):
+    eng, _ = interphase.build_interphase(Engine, d, cfg)
+    eng.set_schedule(**interphase.interphase_schedule(cfg))
+    eng.apply_schedule(0)
+    eng.set_option(_abi.OPT_GRAPH_STEPS, chunk)
+    bd = dict(temperature=cfg.temperature, timestep=cfg.timestep, seed=5)
+    eng.run(2000, first_step=0, **bd)
+    eng.synchronize()
+    t0, done = time.perf_counter(), 2000
+    while done < 22000:
+        if contacts:
+            eng.contacts_update(0.2)
+        eng.run(chunk, first_step=done, **bd)
+        done += chunk
+    eng.synchronize()
+    el = time.perf_counter() - t0
+    print(f"loop: run({chunk}) x {20000 // chunk}, contacts={contacts}: {20000 / el:.0f} steps/s "
+          f"({el / (20000 // chunk) * 1e6:.0f} us per run call)", flush=True)
     eng.close()
