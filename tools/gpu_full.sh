@@ -1,15 +1,16 @@
+TAG=${TAG:-r03c}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread > gpurun_out/r03c_gpu_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.log 2>&1
 rc=$?
-tail -3 gpurun_out/r03c_gpu_tests.log
+tail -3 gpurun_out/${TAG}_gpu_tests.log
 # a failed assertion (rc 1) still lets the bench run; a crash, abort or time limit ends the call
 case $rc in 0|1) ;; *) echo "tests ended with rc=$rc"; exit $rc ;; esac
-timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r03c_bench.log 2>&1 || { tail -30 gpurun_out/r03c_bench.log; exit 1; }
-tail -1 gpurun_out/r03c_bench.log
-timeout -k 10 300 python tools/interphase_probe.py 20000 1000 > gpurun_out/r03c_interphase_probe.txt 2>&1 || { tail -30 gpurun_out/r03c_interphase_probe.txt; exit 1; }
-cat gpurun_out/r03c_interphase_probe.txt
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${TAG}_bench.log 2>&1 || { tail -30 gpurun_out/${TAG}_bench.log; exit 1; }
+tail -1 gpurun_out/${TAG}_bench.log
+timeout -k 10 300 python tools/interphase_probe.py 20000 1000 > gpurun_out/${TAG}_interphase_probe.txt 2>&1 || { tail -30 gpurun_out/${TAG}_interphase_probe.txt; exit 1; }
+cat gpurun_out/${TAG}_interphase_probe.txt
 if [ "${1:-}" = prof ]; then
-  bash tools/profile_round.sh r03c > gpurun_out/r03c_profile.log 2>&1 || { tail -20 gpurun_out/r03c_profile.log; exit 1; }
-  tail -3 gpurun_out/r03c_profile.log
+  bash tools/profile_round.sh $TAG > gpurun_out/${TAG}_profile.log 2>&1 || { tail -20 gpurun_out/${TAG}_profile.log; exit 1; }
+  tail -3 gpurun_out/${TAG}_profile.log
 fi
