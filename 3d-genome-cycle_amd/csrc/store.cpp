@@ -5,9 +5,12 @@
 // Python tools (dumpgsd.py, cool.py) read: vlen strings, f32 positions with deflate 6, i32 contacts with deflate 4 +
 // integer scale-offset, an i32 enum for particle_types, soft links between stage metadata groups.
 #include <hdf5.h>
+#include <zlib.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/gcs_store.h"
@@ -331,6 +334,119 @@ int gcs_store_write_deflated(gcs_store* s, const char* path, int32_t dtype, int3
     // filter mask 0: every filter of the pipeline (deflate) was applied to the chunk
     if (d < 0 || H5Dwrite_chunk(d, H5P_DEFAULT, 0u, off, (size_t)zbytes, zdata) < 0)
         rc = fail(std::string("cannot write ") + path);
+    if (d >= 0) H5Dclose(d);
+    H5Pclose(lp);
+    H5Pclose(cp);
+    H5Sclose(sp);
+    return rc;
+}
+
+namespace {
+// HDF5's integer scale-offset filter (H5Z_SO_INT, minimum bits computed by the library) on one chunk of i32 values,
+// as the library encodes it when the dataset's fill value (0, the default) is defined: the fill value is kept out of
+// the min / max and coded as the all-ones code, every other value as (v - min) in minbits = ceil(log2(range + 2))
+// bits, packed most significant bit first; a 21-byte header {minbits u32 LE, 8, min as i64 LE, 8 zero bytes}; the
+// packed buffer is n * minbits / 8 + 1 bytes.  Checked byte for byte against the library's chunks
+// (tests/test_store.py).  Empty result: a chunk the encoder does not cover (only fill values, or 32 bits needed).
+std::vector<unsigned char> scaleoffset_i32(const int32_t* v, size_t n)
+{
+    bool any = false;
+    long long mn = 0, mx = 0;
+    for (size_t k = 0; k < n; ++k)
+        if (v[k] != 0) {
+            if (!any || v[k] < mn) mn = v[k];
+            if (!any || v[k] > mx) mx = v[k];
+            any = true;
+        }
+    if (!any) return {};
+    const unsigned long long range = (unsigned long long)(mx - mn);
+    int minbits = 0;
+    while (minbits < 32 && (1ull << minbits) < range + 2) ++minbits;
+    if (minbits >= 32) return {};
+    std::vector<unsigned char> out(21 + n * (size_t)minbits / 8 + 1, 0);
+    const unsigned mb = (unsigned)minbits;
+    for (int b = 0; b < 4; ++b) out[b] = (unsigned char)(mb >> (8 * b));
+    out[4] = 8;
+    for (int b = 0; b < 8; ++b) out[5 + b] = (unsigned char)((unsigned long long)mn >> (8 * b));
+    const unsigned long long fillcode = (1ull << minbits) - 1ull;
+    unsigned char* d = out.data() + 21;
+    unsigned long long acc = 0;  // pending bits, the oldest highest (MSB-first stream)
+    int nb = 0;
+    for (size_t k = 0; k < n; ++k) {
+        const unsigned long long c = v[k] == 0 ? fillcode : (unsigned long long)((long long)v[k] - mn);
+        acc = (acc << minbits) | c;  // nb < 8 before: at most 39 bits held
+        nb += minbits;
+        while (nb >= 8) {
+            nb -= 8;
+            *d++ = (unsigned char)(acc >> nb);
+        }
+        acc &= (1ull << nb) - 1ull;
+    }
+    if (nb > 0) *d = (unsigned char)(acc << (8 - nb));
+    return out;
+}
+}  // namespace
+
+int gcs_store_write_scaleoffset_i32(gcs_store* s, const char* path, const int32_t* data, int64_t rows, int32_t cols,
+                                    int32_t deflate, int64_t chunk_rows, int32_t threads)
+{
+    if (!s || !path || !data) return fail("null argument");
+    if (rows <= 0 || cols <= 0 || chunk_rows <= 0) return fail("rows, columns and chunk rows must be positive");
+    if (deflate < 1 || deflate > 9) return fail("deflate level must be in [1, 9]");
+    const int64_t cr = std::min(rows, chunk_rows);
+    const int64_t nchunk = (rows + cr - 1) / cr;
+    // encode every chunk (edge chunks padded with the fill value, as the library stores them) on `threads` threads
+    std::vector<std::vector<unsigned char>> z((size_t)nchunk);
+    std::vector<int> bad((size_t)nchunk, 0);
+    auto work = [&](int64_t c0, int64_t step) {
+        std::vector<int32_t> buf((size_t)(cr * cols));
+        for (int64_t c = c0; c < nchunk; c += step) {
+            const int64_t r0 = c * cr, nr = std::min(cr, rows - r0);
+            std::fill(buf.begin(), buf.end(), 0);
+            std::memcpy(buf.data(), data + r0 * cols, (size_t)(nr * cols) * sizeof(int32_t));
+            const std::vector<unsigned char> so = scaleoffset_i32(buf.data(), buf.size());
+            if (so.empty()) {
+                bad[(size_t)c] = 1;
+                continue;
+            }
+            // the library's deflate filter: compress2 into so.size() * 1.001 + 12 bytes, or the filter fails
+            uLongf cap = (uLongf)((double)so.size() * 1.001 + 12);
+            std::vector<unsigned char> out(cap);
+            if (compress2(out.data(), &cap, so.data(), (uLong)so.size(), deflate) != Z_OK) {
+                bad[(size_t)c] = 1;
+                continue;
+            }
+            out.resize(cap);
+            z[(size_t)c] = std::move(out);
+        }
+    };
+    const int64_t nt = std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::max(threads, 1), nchunk, 64}));
+    std::vector<std::thread> pool;
+    for (int64_t t = 1; t < nt; ++t) pool.emplace_back(work, t, nt);
+    work(0, nt);
+    for (auto& t : pool) t.join();
+    const bool direct = std::find(bad.begin(), bad.end(), 1) == bad.end();
+
+    Silence q;
+    if (replace(s->file, path)) return 1;
+    hsize_t hd[2] = {(hsize_t)rows, (hsize_t)cols}, ch[2] = {(hsize_t)cr, (hsize_t)cols};
+    hid_t sp = H5Screate_simple(2, hd, nullptr);
+    hid_t cp = H5Pcreate(H5P_DATASET_CREATE);
+    H5Pset_chunk(cp, 2, ch);
+    H5Pset_scaleoffset(cp, H5Z_SO_INT, H5Z_SO_INT_MINBITS_DEFAULT);
+    H5Pset_deflate(cp, (unsigned)deflate);
+    hid_t lp = lcpl_parents();
+    hid_t d = H5Dcreate2(s->file, path, H5T_STD_I32LE, sp, lp, cp, H5P_DEFAULT);
+    int rc = d < 0 ? fail(std::string("cannot create ") + path) : 0;
+    if (!rc && !direct) {  // some chunk the encoder does not cover: the library filters the whole array
+        if (H5Dwrite(d, H5T_NATIVE_INT32, H5S_ALL, H5S_ALL, H5P_DEFAULT, data) < 0)
+            rc = fail(std::string("cannot write ") + path);
+    }
+    for (int64_t c = 0; !rc && direct && c < nchunk; ++c) {
+        const hsize_t off[2] = {(hsize_t)(c * cr), 0};
+        if (H5Dwrite_chunk(d, H5P_DEFAULT, 0u, off, z[(size_t)c].size(), z[(size_t)c].data()) < 0)
+            rc = fail(std::string("cannot write a chunk of ") + path);
+    }
     if (d >= 0) H5Dclose(d);
     H5Pclose(lp);
     H5Pclose(cp);

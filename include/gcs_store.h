@@ -54,6 +54,11 @@ int gcs_store_write_array(gcs_store* s, const char* path, int32_t dtype, int32_t
  * several host threads while one thread owns the (not thread-safe) HDF5 library. */
 int gcs_store_write_deflated(gcs_store* s, const char* path, int32_t dtype, int32_t rank, const int64_t* dims,
                              const void* zdata, int64_t zbytes, int32_t deflate);
+/* i32 (rows, cols) with integer scale-offset + deflate (the contact tables' filters), chunks of chunk_rows rows
+ * encoded on `threads` host threads (the library's filter encoding restated, byte-identical chunks) and written
+ * with H5Dwrite_chunk; a chunk the restated encoder does not cover makes the library filter the array instead. */
+int gcs_store_write_scaleoffset_i32(gcs_store* s, const char* path, const int32_t* data, int64_t rows, int32_t cols,
+                                    int32_t deflate, int64_t chunk_rows, int32_t threads);
 /* converts to dtype; dims[0..rank) out; cap_elems = capacity of buf in elements (0 to query) */
 int gcs_store_read_array(gcs_store* s, const char* path, int32_t dtype, void* buf, int64_t cap_elems,
                          int32_t* rank, int64_t* dims);

@@ -301,3 +301,17 @@ def test_c2_long_horizon_list_vs_rebuild_step():
     print({n: (float(a), float(b), float(c)) for n, a, b, c in zip(names, m3, m2, zs)})
     assert (zs <= 3.5).all(), dict(zip(names, zs.tolist()))
     assert (s3[:3] > 0).all() and (s2[:3] > 0).all()
+
+
+def test_second_neighbour_harmonic_nonzero_k(c1_design):
+    """setup_loop_forcefield (simulation_driver_forcefield.cpp:100-136) with K != 0: the (i, i+2) harmonic bonds are
+    compiled in (the default config's K = 0 drops them); forces and a 40-step list-step trajectory vs the oracle"""
+    import dataclasses
+    cfg = dataclasses.replace(InterphaseConfig(), a_core_2nd_bond_spring=40.0, b_core_2nd_bond_spring=15.0)
+    e, o = _pair(c1_design, cfg, ctx=LATE)
+    fe, fo = e.compute_forces(), o.compute_forces()
+    assert np.abs(fe - fo).max() <= 1e-4 * np.abs(fo).max() + 1e-3
+    base, _ = _pair(c1_design, InterphaseConfig(), ctx=LATE)
+    assert np.abs(base.compute_forces() - fo).max() > 1e-2  # the field changes the forces
+    _run_both(e, o, 40, LATE["step"], cfg, 7)
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X

@@ -202,3 +202,39 @@ print("ok")
 """
     out = subprocess.run([PY39, "-c", code], capture_output=True, text=True)
     assert out.returncode == 0 and out.stdout.strip() == "ok", out.stderr
+
+
+@pytest.mark.parametrize("rows,chunk", [(1, 8), (7, 8), (16, 8), (1000, 64), (5000, 1 << 16)])
+def test_scaleoffset_contacts_equal_the_library_chunks(tmp_path, rows, chunk):
+    """gcs_store_write_scaleoffset_i32 (contact tables encoded on host threads): every stored chunk is byte for byte
+    the one HDF5's scale-offset + deflate-4 filters store for the same chunking (h5py writes the reference), and the
+    array reads back exactly; the tables hold index 0 (the fill value, coded apart by the filter)"""
+    rng = np.random.default_rng(rows)
+    i = np.sort(rng.integers(0, 50, rows))
+    t = np.stack([i, i + rng.integers(1, 40, rows), rng.integers(1, 9, rows)], axis=1).astype(np.int32)
+    t[0, 0] = 0
+    p = tmp_path / "c.h5"
+    with store.H5File(p, create=True) as h:
+        h.write_scaleoffset_i32("/ours", t, 4, chunk_rows=chunk, threads=4)
+        assert np.array_equal(h.read_array("/ours", store.H5_I32).reshape(-1, 3), t)
+    if PY39 is None:
+        pytest.skip("no h5py interpreter for the raw-chunk comparison")
+    np.save(tmp_path / "t.npy", t)
+    code = f"""
+import h5py, numpy as np
+t = np.load({str(tmp_path / "t.npy")!r})
+cr = min({chunk}, t.shape[0])
+with h5py.File({str(p)!r}, "a") as f:
+    f.create_dataset("lib", data=t, chunks=(cr, 3), scaleoffset=0, compression="gzip", compression_opts=4)
+with h5py.File({str(p)!r}, "r") as f:
+    a, b = f["lib"], f["ours"]
+    assert b.chunks == a.chunks and b.scaleoffset == 0 and b.compression == "gzip" and b.compression_opts == 4
+    assert a.id.get_create_plist().get_filter(0)[0] == b.id.get_create_plist().get_filter(0)[0]
+    for r0 in range(0, t.shape[0], cr):
+        ma, ca = a.id.read_direct_chunk((r0, 0))
+        mb, cb = b.id.read_direct_chunk((r0, 0))
+        assert ma == mb == 0 and ca == cb, (r0, len(ca), len(cb))
+print("ok")
+"""
+    out = subprocess.run([PY39, "-c", code], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stderr
