@@ -63,7 +63,8 @@
 extern "C" {
 #endif
 
-#define GCS_ABI_VERSION 1
+/* 2: gcs_run_stats gained fused_contact_steps (an out-struct grew: callers built against 1 must rebuild) */
+#define GCS_ABI_VERSION 2
 
 /* status codes */
 #define GCS_OK 0

@@ -35,7 +35,7 @@ def test_library_exports_every_symbol():
 
 
 def test_abi_version():
-    assert A.load().gcs_abi_version() == 1
+    assert A.load().gcs_abi_version() == 2
 
 
 STRUCTS = {
