@@ -124,6 +124,24 @@ void launch_contact_compact(hipStream_t s, const unsigned long long* keys, const
                        total);
 }
 
+// sorted (key, count) -> the (i, j, count) rows the caller reads (one copy to the host, no host-side reformatting)
+__global__ __launch_bounds__(256) void k_contact_emit(const unsigned long long* __restrict__ k,
+                                                      const unsigned* __restrict__ c, int n, unsigned* __restrict__ out)
+{
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+        const unsigned long long key = k[t];
+        out[3 * (size_t)t] = (unsigned)(key >> 32);
+        out[3 * (size_t)t + 1] = (unsigned)key;
+        out[3 * (size_t)t + 2] = c[t];
+    }
+}
+
+void launch_contact_emit(hipStream_t s, const unsigned long long* k, const unsigned* c, int n, unsigned* out)
+{
+    const int blocks = std::max(1, std::min((n + 255) / 256, 4096));
+    hipLaunchKernelGGL(k_contact_emit, dim3(blocks), dim3(256), 0, s, k, c, n, out);
+}
+
 size_t sort_pairs_u64_u32_temp_bytes(int n)
 {
     size_t bytes = 0;
@@ -133,9 +151,9 @@ size_t sort_pairs_u64_u32_temp_bytes(int n)
 }
 
 void sort_pairs_u64_u32(hipStream_t s, const unsigned long long* k_in, unsigned long long* k_out, const unsigned* v_in,
-                        unsigned* v_out, int n, void* temp, size_t temp_bytes)
+                        unsigned* v_out, int n, void* temp, size_t temp_bytes, int end_bit)
 {
-    (void)hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k_in, k_out, v_in, v_out, n, 0, 64, s);
+    (void)hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k_in, k_out, v_in, v_out, n, 0, end_bit, s);
 }
 
 void launch_quantize(hipStream_t s, const float4* pos, float* out, int n, int bits)

@@ -172,6 +172,7 @@ struct gcs_engine {
     // contacts_read scratch, kept between reads (compaction into the table's size, the sorted copies, sort temp)
     unsigned long long *c_ck = nullptr, *c_ck2 = nullptr;
     unsigned *c_cv = nullptr, *c_cv2 = nullptr;
+    unsigned* c_rows = nullptr;  // the read's (i, j, count) rows, 3 x c_sorted_cap
     void* c_temp = nullptr;
     size_t c_temp_bytes = 0;
     int64_t c_sorted_cap = 0;
@@ -1444,6 +1445,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->c_cv);
     dfree(e->c_ck2);
     dfree(e->c_cv2);
+    dfree(e->c_rows);
     if (e->c_temp) (void)hipFree(e->c_temp);
     dfree(e->q_out);
     dfree(e->s_pts);
@@ -2031,8 +2033,11 @@ int gcs_engine_contacts_read(gcs_engine* e, uint32_t* ijc, int64_t capacity, int
     if (total > e->c_sorted_cap) {
         dfree(e->c_ck2);
         dfree(e->c_cv2);
+        dfree(e->c_rows);
         e->c_sorted_cap = 0;
-        if ((rc = dalloc(&e->c_ck2, (size_t)total)) || (rc = dalloc(&e->c_cv2, (size_t)total))) return rc;
+        if ((rc = dalloc(&e->c_ck2, (size_t)total)) || (rc = dalloc(&e->c_cv2, (size_t)total)) ||
+            (rc = dalloc(&e->c_rows, 3 * (size_t)total)))
+            return rc;
         e->c_sorted_cap = total;
     }
     const size_t bytes = std::max<size_t>(sort_pairs_u64_u32_temp_bytes(total), 16);
@@ -2043,18 +2048,15 @@ int gcs_engine_contacts_read(gcs_engine* e, uint32_t* ijc, int64_t capacity, int
         HIPCHK(hipMalloc(&e->c_temp, bytes));
         e->c_temp_bytes = bytes;
     }
-    sort_pairs_u64_u32(e->stream, e->c_ck, e->c_ck2, e->c_cv, e->c_cv2, total, e->c_temp, e->c_temp_bytes);
+    // keys are i << 32 | j with i, j < N: the radix passes stop at 32 + bit length of N - 1
+    int nbits = 1;
+    while (nbits < 32 && ((int64_t)1 << nbits) < e->n) ++nbits;
+    sort_pairs_u64_u32(e->stream, e->c_ck, e->c_ck2, e->c_cv, e->c_cv2, total, e->c_temp, e->c_temp_bytes,
+                       32 + nbits);
+    launch_contact_emit(e->stream, e->c_ck2, e->c_cv2, total, e->c_rows);
     HIPCHK(hipGetLastError());
-    std::vector<unsigned long long> hk(total);
-    std::vector<unsigned> hv(total);
-    HIPCHK(hipMemcpyAsync(hk.data(), e->c_ck2, total * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(hv.data(), e->c_cv2, total * sizeof(unsigned), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(ijc, e->c_rows, 3 * (size_t)total * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    for (int k = 0; k < total; ++k) {
-        ijc[3 * k] = (uint32_t)(hk[k] >> 32);
-        ijc[3 * k + 1] = (uint32_t)hk[k];
-        ijc[3 * k + 2] = hv[k];
-    }
     return GCS_OK;
 }
 

@@ -368,8 +368,10 @@ void launch_contact_insert(hipStream_t s, const DevCtx* ctx, int n, float dist, 
 void launch_contact_compact(hipStream_t s, const unsigned long long* keys, const unsigned* counts, long long slots,
                             unsigned long long* out_k, unsigned* out_c, int* total);
 size_t sort_pairs_u64_u32_temp_bytes(int n);
+// keys below 2^end_bit (end_bit <= 64: fewer radix passes)
 void sort_pairs_u64_u32(hipStream_t s, const unsigned long long* k_in, unsigned long long* k_out, const unsigned* v_in,
-                        unsigned* v_out, int n, void* temp, size_t temp_bytes);
+                        unsigned* v_out, int n, void* temp, size_t temp_bytes, int end_bit = 64);
+void launch_contact_emit(hipStream_t s, const unsigned long long* k, const unsigned* c, int n, unsigned* out);
 void launch_quantize(hipStream_t s, const float4* pos, float* out, int n, int bits);
 // domain.hip: spatial decomposition (band pack / unpack) + the local partial reduction of a decomposed step
 constexpr int kMaxPeers = 32;
