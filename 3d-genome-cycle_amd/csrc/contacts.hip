@@ -4,8 +4,8 @@
 //     i << 32 | j, 32-bit count); at the output window the occupied slots are compacted and radix-sorted by (i, j)
 //     on the device (contact_map.cpp:66-85 sorts the same keys on the host)
 //   * the sampled-position quantisation of simulation_store.cpp:22-33 / 192-216 (16 fraction bits, stored as f32)
-// The pair predicate is the strict fp32 one of the neighbour search (kernels.hip k_search): bit-exact against the
-// oracle's gcso_search_neighbors.
+// The pair predicate is the strict one of the neighbour search (kernels.hip k_search), fp32 or (the fp64 engine)
+// fp64: bit-exact against the oracle's gcso_search_neighbors / gcso_search_neighbors64.
 #include <hip/hip_runtime.h>
 
 #include <hipcub/hipcub.hpp>
@@ -21,6 +21,13 @@ __device__ __forceinline__ bool contact_pair(float4 p, float4 q, float d2)
     const float r2 = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
     return r2 < d2;
 }
+// the fp64 engine's predicate (the same strict form in fp64, kernels.hip strict_lt)
+__device__ __forceinline__ bool contact_pair(double4 p, double4 q, double d2)
+{
+    const double dx = __dsub_rn(p.x, q.x), dy = __dsub_rn(p.y, q.y), dz = __dsub_rn(p.z, q.z);
+    const double r2 = __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
+    return r2 < d2;
+}
 
 
 // One thread per cell-sorted particle of any cell list (the engine's own, or a search list built for the
@@ -28,22 +35,28 @@ __device__ __forceinline__ bool contact_pair(float4 p, float4 q, float d2)
 // are >= the force cutoff >= the contact distance, that is the usual 3 x 3 rows x 5 x-cells; clamped outliers
 // only get closer in cell units).  Every pair i < j inside the distance is counted into the table.  A failed insert (probe sequence
 // exhausted: table too full) raises overflow; counts stay exact for the inserted keys.
+// F64: the pair test in fp64 on pos64[particle] (the fp64 engine's positions) with d2 = dist64 * dist64
+template <bool F64>
 __global__ __launch_bounds__(256) void k_contact_insert(const DevCtx* __restrict__ ctx, int n, float dist,
                                                         const float4* __restrict__ spos, const int* __restrict__ sidx,
                                                         const int* __restrict__ scell, const int* __restrict__ cstart,
                                                         unsigned long long* __restrict__ keys,
                                                         unsigned* __restrict__ counts, int bits,
-                                                        int* __restrict__ overflow)
+                                                        int* __restrict__ overflow, const double4* __restrict__ pos64,
+                                                        double dist64)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     const Grid g = ctx->grid;
     if (s >= n || s >= cstart[g.ncell]) return;
     const float d2 = __fmul_rn(dist, dist);
+    const double d2_64 = __dmul_rn(dist64, dist64);
     const float widen = 1.0f + 1.0e-6f;  // never round a reach down
     const int rx = (int)ceilf(dist * g.inv[0] * widen), ry = (int)ceilf(dist * g.inv[1] * widen),
               rz = (int)ceilf(dist * g.inv[2] * widen);
     const int i = sidx[s];
     const float4 p = spos[s];
+    double4 p64 = make_double4(0.0, 0.0, 0.0, 0.0);
+    if constexpr (F64) p64 = pos64[i];
     const int c = scell[s];
     const int nx = g.n[0], ny = g.n[1], nz = g.n[2];
     const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
@@ -53,7 +66,12 @@ __global__ __launch_bounds__(256) void k_contact_insert(const DevCtx* __restrict
             const int jb = cstart[base + max(cx - rx, 0)], je = cstart[base + min(cx + rx, nx - 1) + 1];
             for (int t = jb; t < je; ++t) {
                 const int j = sidx[t];
-                if (j <= i || !contact_pair(p, spos[t], d2)) continue;
+                if (j <= i) continue;
+                if constexpr (F64) {
+                    if (!contact_pair(p64, pos64[j], d2_64)) continue;
+                } else {
+                    if (!contact_pair(p, spos[t], d2)) continue;
+                }
                 const unsigned long long key = ((unsigned long long)(unsigned)i << 32) | (unsigned)j;
                 if (!contact_count(keys, counts, bits, key)) atomicOr(overflow, 1);
             }
@@ -84,36 +102,48 @@ __global__ __launch_bounds__(256) void k_contact_compact(const unsigned long lon
     }
 }
 
-// simulation_store.cpp:22-33 on an fp32 value: frexp, round the mantissa to `bits` fraction bits (nearbyint,
-// round-half-even), ldexp back.  Every step is exact in fp32, so the result equals the fp64 reference applied to
-// the same (fp32) coordinate.
-__device__ __forceinline__ float quantize_f32(float v, int bits)
+// simulation_store.cpp:22-33: frexp, round the mantissa to `bits` fraction bits (nearbyint, round-half-even), ldexp
+// back.  On an fp32 value every step is exact in fp32, so the result equals the fp64 reference applied to the same
+// (fp32) coordinate; on an fp64 value it is the reference's arithmetic itself, and the result (<= 24 significant
+// bits for bits <= 23) converts to the stored f32 exactly.
+__device__ __forceinline__ float quantize_v(float v, int bits)
 {
     int ex = 0;
     const float m = frexpf(v, &ex);
     const float sm = rintf(ldexpf(m, bits));
     return ldexpf(sm, ex - bits);
 }
+__device__ __forceinline__ float quantize_v(double v, int bits)
+{
+    int ex = 0;
+    const double m = frexp(v, &ex);
+    const double sm = rint(ldexp(m, bits));
+    return (float)ldexp(sm, ex - bits);
+}
 
-__global__ __launch_bounds__(256) void k_quantize(const float4* __restrict__ pos, float* __restrict__ out, int n,
-                                                  int bits)
+template <typename P>
+__global__ __launch_bounds__(256) void k_quantize(const P* __restrict__ pos, float* __restrict__ out, int n, int bits)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float4 p = pos[i];
-    out[3 * i] = quantize_f32(p.x, bits);
-    out[3 * i + 1] = quantize_f32(p.y, bits);
-    out[3 * i + 2] = quantize_f32(p.z, bits);
+    const P p = pos[i];
+    out[3 * i] = quantize_v(p.x, bits);
+    out[3 * i + 1] = quantize_v(p.y, bits);
+    out[3 * i + 2] = quantize_v(p.z, bits);
 }
 
 }  // namespace
 
-void launch_contact_insert(hipStream_t s, const DevCtx* ctx, int n, float dist, const float4* spos, const int* sidx,
+void launch_contact_insert(hipStream_t s, const DevCtx* ctx, int n, double dist, const float4* spos, const int* sidx,
                            const int* scell, const int* cstart, unsigned long long* keys, unsigned* counts, int bits,
-                           int* overflow)
+                           int* overflow, const double4* pos64)
 {
-    hipLaunchKernelGGL(k_contact_insert, dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, dist, spos, sidx, scell,
-                       cstart, keys, counts, bits, overflow);
+    if (pos64)
+        hipLaunchKernelGGL(k_contact_insert<true>, dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, (float)dist, spos,
+                           sidx, scell, cstart, keys, counts, bits, overflow, pos64, dist);
+    else
+        hipLaunchKernelGGL(k_contact_insert<false>, dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, (float)dist, spos,
+                           sidx, scell, cstart, keys, counts, bits, overflow, pos64, dist);
 }
 
 void launch_contact_compact(hipStream_t s, const unsigned long long* keys, const unsigned* counts, long long slots,
@@ -158,7 +188,12 @@ void sort_pairs_u64_u32(hipStream_t s, const unsigned long long* k_in, unsigned 
 
 void launch_quantize(hipStream_t s, const float4* pos, float* out, int n, int bits)
 {
-    hipLaunchKernelGGL(k_quantize, dim3((n + 255) / 256), dim3(256), 0, s, pos, out, n, bits);
+    hipLaunchKernelGGL(k_quantize<float4>, dim3((n + 255) / 256), dim3(256), 0, s, pos, out, n, bits);
+}
+
+void launch_quantize(hipStream_t s, const double4* pos, float* out, int n, int bits)
+{
+    hipLaunchKernelGGL(k_quantize<double4>, dim3((n + 255) / 256), dim3(256), 0, s, pos, out, n, bits);
 }
 
 }  // namespace gcs

@@ -103,6 +103,7 @@ struct gcs_engine {
     int device = 0;
     hipStream_t stream = nullptr;
     int n = 0;
+    int prec = 64;  // GCS_PRECISION_F64 (the reference's double; default) or GCS_PRECISION_F32
     std::vector<double> mu, ab;
     std::vector<FieldRec> fields;
     int next_handle = 1;
@@ -143,6 +144,21 @@ struct gcs_engine {
     float* bend_eps = nullptr;
     int* toff = nullptr;
     Tether* tent = nullptr;
+    // fp64 state (prec 64; include/gcs.h GCS_PRECISION_F64): positions, constants, forces, the evaluation's partial
+    // rows and reaction buffer, the topology values, the list step's slot-ordered copies, injected normals
+    double4* dpos[2] = {nullptr, nullptr};
+    double4* dkmu = nullptr;
+    double4* dforce_out = nullptr;
+    double* dpart = nullptr;
+    double* dred = nullptr;  // [6] the reactions of a spacestep step's force pass (k_red64 -> the tail's ext_react)
+    double4* dbval = nullptr;
+    double* dbend_eps = nullptr;
+    TetherT<double>* dtent = nullptr;
+    double2* dtype_ab = nullptr;
+    double4* dpsort[2] = {nullptr, nullptr};
+    double4* dskmu = nullptr;
+    double* dnoise = nullptr;
+    double4* s_pts64 = nullptr;  // fp64 query points of gcs_engine_search_neighbors
     // injected noise
     float* noise = nullptr;
     int64_t noise_steps = 0;
@@ -254,22 +270,11 @@ struct gcs_engine {
     long long list_deal_opt = -1;  // GCS_OPT_LIST_DEAL: chunk -> wave pattern of the list build (-1: the default for
                                    // list_waves, 0: round robin)
     bool l_need_build = true;   // the next list step must rebuild (run start without continuity)
-    // small systems (N <= kSmallMax, GCS_OPT_SMALL_PATH): one single-workgroup launch per run (k_small) and its
-    // persistent list state; small_cont: the next small run at small_step continues the last one (no rebuild)
-    int small_opt = 0;
     // dense systems: mean neighbours within the cutoff above which a fresh run takes the 2-launch tile step instead
     // of the list step (GCS_OPT_DENSE_NEIGHBORS; 0: never), and the current chain's verdict
     int dense_opt = 48;
     bool dense = false;
     double dense_mean = -1.0;  // the last probe's mean neighbour count
-    unsigned short* sm_list = nullptr;
-    int* sm_lcount = nullptr;
-    float4* sm_bpos = nullptr;
-    int* sm_cstart = nullptr;
-    unsigned short* sm_cidx = nullptr;
-    bool small_cont = false;
-    int64_t small_step = 0;
-    int small_version = -1;
     double c_pending = 0;      // a contact update fused into the next list step (its distance; 0: none)
 
     // fused-step continuity: after a fused run the cells of the next positions are already binned with the
@@ -318,11 +323,14 @@ FieldRec* new_field(gcs_engine* e, int kind)
 
 bool valid_index(const gcs_engine* e, int64_t i) { return i >= 0 && i < e->n; }
 
-// Flatten the registered fields into device tables (DESIGN.md "device layout").
+// Flatten the registered fields into device tables (DESIGN.md "device layout"): the fp32 parameter block always, the
+// fp64 block and tables (dkmu, dbval, dbend_eps, dtent, dtype_ab) for an fp64 engine.  Every derived value (mixed
+// bond constants, 1 / decay^2, cutoff^2, K / mobility) is formed in double first; the fp32 engine rounds it once.
 int compile(gcs_engine* e)
 {
     if (!e->dirty) return GCS_OK;
     const int n = e->n;
+    const bool f64 = e->prec == 64;
     ForceArgs& a = e->fa;
     a.has_pair = 0;
     a.has_bonds = 0;
@@ -331,11 +339,12 @@ int compile(gcs_engine* e)
     a.n_point = 0;
     a.has_wall_in = 0;
     a.has_wall_out = 0;
+    FieldPrm<double> pd = e->fa.pd;  // keeps temperature / timestep (begin_run sets them)
 
     std::vector<std::vector<int2>> blist(n);
     std::vector<BondParam> params;
-    std::vector<float> bend(n, 0.f);
-    std::vector<std::vector<Tether>> tlist(n);
+    std::vector<double> bend(n, 0.0);
+    std::vector<std::vector<TetherT<double>>> tlist(n);
     int pair_mix = 1;
     bool sw_done = false;
     std::vector<int> sw_idx;
@@ -349,28 +358,27 @@ int compile(gcs_engine* e)
             a.pair_mix = f.sc.mix ? 1 : 0;
             pair_mix = a.pair_mix;
             a.pair_scaled = f.sc.scaled ? 1 : 0;
-            a.pa_eps = (float)f.sc.a_energy;
-            a.pa_sig = (float)f.sc.a_diameter;
-            a.pb_eps = (float)f.sc.b_energy;
-            a.pb_sig = (float)(f.sc.b_diameter > 0 ? f.sc.b_diameter : 1.0);
-            if (!f.sc.mix) a.pb_eps = 0.f;
-            a.pair_dist = (float)f.sc.neighbor_distance;
+            pd.pa_eps = f.sc.a_energy;
+            pd.pa_sig = f.sc.a_diameter;
+            pd.pb_eps = f.sc.mix ? f.sc.b_energy : 0.0;
+            pd.pb_sig = f.sc.b_diameter > 0 ? f.sc.b_diameter : 1.0;
+            pd.pair_dist = f.sc.neighbor_distance;
             break;
         case F_SOFTWELL: {
             if (!sw_done && f.idx.size() <= 64) {  // the wave-cooperative droplet (local_terms)
                 sw_done = true;
                 a.sw_n = (int)f.idx.size();
-                a.sw_ka = (float)f.sw.energy;
-                a.sw_kb = (float)(1.0 / (f.sw.decay_distance * f.sw.decay_distance));
-                a.sw_la = (float)(f.sw.cutoff * f.sw.cutoff);
+                pd.sw_ka = f.sw.energy;
+                pd.sw_kb = 1.0 / (f.sw.decay_distance * f.sw.decay_distance);
+                pd.sw_la = f.sw.cutoff * f.sw.cutoff;
                 sw_idx.assign(f.idx.begin(), f.idx.end());
                 break;
             }
             BondParam bp{};
             bp.type = kSoftwell;
-            bp.ka = (float)f.sw.energy;
-            bp.kb = (float)(1.0 / (f.sw.decay_distance * f.sw.decay_distance));
-            bp.la = (float)(f.sw.cutoff * f.sw.cutoff);
+            bp.ka = f.sw.energy;
+            bp.kb = 1.0 / (f.sw.decay_distance * f.sw.decay_distance);
+            bp.la = f.sw.cutoff * f.sw.cutoff;
             const int pid = (int)params.size();
             params.push_back(bp);
             for (size_t p = 0; p < f.idx.size(); ++p)
@@ -387,10 +395,16 @@ int compile(gcs_engine* e)
                       : (f.bond.potential == GCS_POT_SPRING ? kSpring : kSemispring);
             bp.mix = f.bond.mix ? 1 : 0;
             bp.scaled = f.bond.scaled ? 1 : 0;
-            bp.ka = (float)f.bond.a_spring;
-            bp.kb = (float)f.bond.b_spring;
-            bp.la = (float)f.bond.a_length;
-            bp.lb = (float)f.bond.b_length;
+            bp.ka = f.bond.a_spring;
+            bp.kb = f.bond.b_spring;
+            bp.la = f.bond.a_length;
+            bp.lb = f.bond.b_length;
+            if (e->prec != 64) {  // the fp32 engine took the field's constants as fp32 (its own parameter rounding)
+                bp.ka = (float)bp.ka;
+                bp.kb = (float)bp.kb;
+                bp.la = (float)bp.la;
+                bp.lb = (float)bp.lb;
+            }
             const int pid = (int)params.size();
             params.push_back(bp);
             for (size_t q = 0; q + 1 < f.idx.size(); q += 2) {
@@ -401,67 +415,96 @@ int compile(gcs_engine* e)
             break;
         }
         case F_BENDING:
-            for (int64_t k : f.idx) bend[k] += (float)f.energy;
+            for (int64_t k : f.idx) bend[k] += f64 ? f.energy : (double)(float)f.energy;
             break;
         case F_WALL_IN:
             if (a.has_wall_in) return fail(GCS_EINVAL, "only one ellipsoid inward field may be active");
             a.has_wall_in = 1;
-            a.win.a_eps = (float)f.wall.a_energy;
-            a.win.a_sig = (float)f.wall.a_diameter;
-            a.win.b_eps = (float)f.wall.b_energy;
-            a.win.b_sig = (float)(f.wall.b_diameter > 0 ? f.wall.b_diameter : 1.0);
-            a.win.wall_a = (float)f.wall.wall_a;
-            a.win.wall_b = (float)f.wall.wall_b;
-            a.win.cx = (float)f.wall.center[0];
-            a.win.cy = (float)f.wall.center[1];
-            a.win.cz = (float)f.wall.center[2];
-            a.win.mix = f.wall.mix ? 1 : 0;
-            a.win.scaled = f.wall.scaled ? 1 : 0;
-            if (!f.wall.mix) a.win.b_eps = 0.f;
+            pd.win.a_eps = f.wall.a_energy;
+            pd.win.a_sig = f.wall.a_diameter;
+            pd.win.b_eps = f.wall.mix ? f.wall.b_energy : 0.0;
+            pd.win.b_sig = f.wall.b_diameter > 0 ? f.wall.b_diameter : 1.0;
+            pd.win.wall_a = f.wall.wall_a;
+            pd.win.wall_b = f.wall.wall_b;
+            pd.win.cx = f.wall.center[0];
+            pd.win.cy = f.wall.center[1];
+            pd.win.cz = f.wall.center[2];
+            pd.win.mix = f.wall.mix ? 1 : 0;
+            pd.win.scaled = f.wall.scaled ? 1 : 0;
             break;
         case F_WALL_OUT:
             if (a.has_wall_out) return fail(GCS_EINVAL, "only one ellipsoid outward field may be active");
             a.has_wall_out = 1;
-            a.wout_k = (float)f.spring;
-            a.wout_cx = (float)f.center[0];
-            a.wout_cy = (float)f.center[1];
-            a.wout_cz = (float)f.center[2];
+            pd.wout_k = f.spring;
+            pd.wout_cx = f.center[0];
+            pd.wout_cy = f.center[1];
+            pd.wout_cz = f.center[2];
             break;
         case F_POINT: {
             if (a.n_point >= kMaxPointSources) return fail(GCS_EINVAL, "too many point-source fields (max 4)");
-            PointSrc& p = a.point[a.n_point++];
+            PointSrcT<double>& p = pd.point[a.n_point++];
             p.type = f.point.potential;
-            p.px = (float)f.point.point[0];
-            p.py = (float)f.point.point[1];
-            p.pz = (float)f.point.point[2];
-            p.k = (float)f.point.spring;
-            p.l = (float)f.point.length;
-            p.f = (float)f.point.force;
-            p.b = (float)f.point.reactive_distance;
+            p.px = f.point.point[0];
+            p.py = f.point.point[1];
+            p.pz = f.point.point[2];
+            p.k = f.point.spring;
+            p.l = f.point.length;
+            p.f = f.point.force;
+            p.b = f.point.reactive_distance;
             break;
         }
         case F_KFIBER:
             for (const gcs_kinetochore_spec& sp : f.specs) {
-                Tether t{};
-                t.px = (float)f.pole[0];
-                t.py = (float)f.pole[1];
-                t.pz = (float)f.pole[2];
-                t.k = (float)(sp.decay_rate / sp.mobility);  // kinetochore_fiber_forcefield.cpp:46-53
-                t.l = (float)sp.stationary_length;
+                TetherT<double> t{};
+                t.px = f.pole[0];
+                t.py = f.pole[1];
+                t.pz = f.pole[2];
+                t.k = sp.decay_rate / sp.mobility;  // kinetochore_fiber_forcefield.cpp:46-53
+                t.l = sp.stationary_length;
                 tlist[sp.particle_index].push_back(t);
             }
             break;
         }
     }
     if (a.has_wall_in && a.has_wall_out) {
-        if (a.win.cx != a.wout_cx || a.win.cy != a.wout_cy || a.win.cz != a.wout_cz)
+        if (pd.win.cx != pd.wout_cx || pd.win.cy != pd.wout_cy || pd.win.cz != pd.wout_cz)
             return fail(GCS_EINVAL, "inward and outward ellipsoid fields must share the centre");
     }
+    // the fp32 block: every parameter rounded once
+    FieldPrm<float>& pf = a.pf;
+    pf.pa_eps = (float)pd.pa_eps;
+    pf.pa_sig = (float)pd.pa_sig;
+    pf.pb_eps = (float)pd.pb_eps;
+    pf.pb_sig = (float)pd.pb_sig;
+    pf.pair_dist = (float)pd.pair_dist;
+    pf.sw_ka = (float)pd.sw_ka;
+    pf.sw_kb = (float)pd.sw_kb;
+    pf.sw_la = (float)pd.sw_la;
+    for (int q = 0; q < kMaxPointSources; ++q) {
+        const PointSrcT<double>& d = pd.point[q];
+        pf.point[q] = PointSrcT<float>{d.type, (float)d.px, (float)d.py, (float)d.pz, (float)d.k, (float)d.l,
+                                       (float)d.f, (float)d.b};
+    }
+    const WallInT<double>& w = pd.win;
+    pf.win = WallInT<float>{(float)w.a_eps, (float)w.a_sig, (float)w.b_eps, (float)w.b_sig, (float)w.wall_a,
+                            (float)w.wall_b, (float)w.cx, (float)w.cy, (float)w.cz, w.mix, w.scaled};
+    pf.wout_k = (float)pd.wout_k;
+    pf.wout_cx = (float)pd.wout_cx;
+    pf.wout_cy = (float)pd.wout_cy;
+    pf.wout_cz = (float)pd.wout_cz;
+    a.pd = pd;
 
-    // per-particle constants {mu, a, b, 0}
+    // per-particle constants {mu, a, b, t}
     std::vector<float4> hk(n);
-    for (int i = 0; i < n; ++i) hk[i] = make_float4((float)e->mu[i], (float)e->ab[2 * i], (float)e->ab[2 * i + 1], 0.f);
-    for (int t : sw_idx) hk[t].w = 1.f;  // droplet target
+    std::vector<double4> hkd(f64 ? n : 0);
+    for (int i = 0; i < n; ++i) {
+        hk[i] = make_float4((float)e->mu[i], (float)e->ab[2 * i], (float)e->ab[2 * i + 1], 0.f);
+        if (f64) hkd[i] = make_double4(e->mu[i], e->ab[2 * i], e->ab[2 * i + 1], 0.0);
+    }
+    for (int t : sw_idx) {  // droplet target
+        hk[t].w = 1.f;
+        if (f64) hkd[t].w = 1.0;
+    }
     dfree(e->sw_idx);
     if (a.sw_n > 0) {
         int rc;
@@ -470,15 +513,19 @@ int compile(gcs_engine* e)
     }
     a.sw_idx = e->sw_idx;
     HIPCHK(hipMemcpyAsync(e->kmu, hk.data(), n * sizeof(float4), hipMemcpyHostToDevice, e->stream));
+    if (f64) HIPCHK(hipMemcpyAsync(e->dkmu, hkd.data(), n * sizeof(double4), hipMemcpyHostToDevice, e->stream));
 
-    // list step: pair-factor classes (the (a, b) the pair field mixes; k_cell_sort's spos.w / sb)
+    // list step: pair-factor classes (the (a, b) the pair field mixes; k_cell_sort's spos.w / sb), keyed by the
+    // double factors (the fp32 engine's table holds their roundings)
     std::vector<int> pt(n, 0);
     std::vector<float2> tab;
+    std::vector<double2> tabd;
     {
-        std::map<std::pair<float, float>, int> cls;
+        std::map<std::pair<double, double>, int> cls;
         bool ok = a.has_pair && n > 0 && n < (1 << kListIndexBits);
         for (int i = 0; ok && i < n; ++i) {
-            const std::pair<float, float> key = pair_mix ? std::make_pair(hk[i].y, hk[i].z) : std::make_pair(1.f, 0.f);
+            const std::pair<double, double> key =
+                pair_mix ? std::make_pair(e->ab[2 * i], e->ab[2 * i + 1]) : std::make_pair(1.0, 0.0);
             auto it = cls.find(key);
             if (it == cls.end()) {
                 if ((int)cls.size() >= kMaxTypes) {
@@ -486,7 +533,8 @@ int compile(gcs_engine* e)
                     break;
                 }
                 it = cls.emplace(key, (int)cls.size()).first;
-                tab.push_back(make_float2(key.first, key.second));
+                tab.push_back(make_float2((float)key.first, (float)key.second));
+                tabd.push_back(make_double2(key.first, key.second));
             }
             pt[i] = it->second;
         }
@@ -496,8 +544,12 @@ int compile(gcs_engine* e)
             int rc;
             if (!e->ptype && (rc = dalloc(&e->ptype, n))) return rc;
             if (!e->type_ab && (rc = dalloc(&e->type_ab, kMaxTypes))) return rc;
+            if (f64 && !e->dtype_ab && (rc = dalloc(&e->dtype_ab, kMaxTypes))) return rc;
             HIPCHK(hipMemcpyAsync(e->ptype, pt.data(), n * sizeof(int), hipMemcpyHostToDevice, e->stream));
             HIPCHK(hipMemcpyAsync(e->type_ab, tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice, e->stream));
+            if (f64)
+                HIPCHK(hipMemcpyAsync(e->dtype_ab, tabd.data(), tabd.size() * sizeof(double2), hipMemcpyHostToDevice,
+                                      e->stream));
         }
     }
 
@@ -507,6 +559,9 @@ int compile(gcs_engine* e)
     dfree(e->bend_eps);
     dfree(e->toff);
     dfree(e->tent);
+    dfree(e->dbval);
+    dfree(e->dbend_eps);
+    dfree(e->dtent);
 
     size_t nb = 0;
     for (auto& l : blist) nb += l.size();
@@ -514,6 +569,7 @@ int compile(gcs_engine* e)
         std::vector<int> off(n + 1, 0);
         std::vector<int2> ent;
         std::vector<float4> val;
+        std::vector<double4> vald;
         ent.reserve(nb);
         val.reserve(nb);
         for (int i = 0; i < n; ++i) {
@@ -521,7 +577,7 @@ int compile(gcs_engine* e)
             for (const int2& b : blist[i]) {
                 const BondParam& bp = params[b.y];
                 const int j = b.x;
-                float4 v = make_float4(bp.ka, bp.kb, bp.la, 0.f);
+                double4 v = make_double4(bp.ka, bp.kb, bp.la, 0.0);
                 if (bp.type != kSoftwell) {
                     // simulation_driver_forcefield.cpp:71-76: K = a k_a + b k_b, l = a l_a + b l_b with the pair's
                     // mean factors a = (a_i + a_j) / 2, b = (b_i + b_j) / 2 (mix), else k_a, l_a
@@ -531,10 +587,11 @@ int compile(gcs_engine* e)
                         K = A * bp.ka + B * bp.kb;
                         l = A * bp.la + B * bp.lb;
                     }
-                    v = make_float4((float)K, (float)l, 0.f, 0.f);
+                    v = make_double4(K, l, 0.0, 0.0);
                 }
                 ent.push_back(make_int2(j, bp.type | (bp.scaled ? 16 : 0)));
-                val.push_back(v);
+                val.push_back(make_float4((float)v.x, (float)v.y, (float)v.z, 0.f));
+                if (f64) vald.push_back(v);
             }
         }
         off[n] = (int)ent.size();
@@ -542,18 +599,28 @@ int compile(gcs_engine* e)
         if ((rc = dalloc(&e->boff, n + 1))) return rc;
         if ((rc = dalloc(&e->bent, ent.size()))) return rc;
         if ((rc = dalloc(&e->bval, val.size()))) return rc;
+        if (f64 && (rc = dalloc(&e->dbval, vald.size()))) return rc;
         HIPCHK(hipMemcpyAsync(e->boff, off.data(), (n + 1) * sizeof(int), hipMemcpyHostToDevice, e->stream));
         HIPCHK(hipMemcpyAsync(e->bent, ent.data(), ent.size() * sizeof(int2), hipMemcpyHostToDevice, e->stream));
         HIPCHK(hipMemcpyAsync(e->bval, val.data(), val.size() * sizeof(float4), hipMemcpyHostToDevice, e->stream));
+        if (f64)
+            HIPCHK(hipMemcpyAsync(e->dbval, vald.data(), vald.size() * sizeof(double4), hipMemcpyHostToDevice, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));  // val / ent die at the end of this block
         a.has_bonds = 1;
     }
     bool any_bend = false;
-    for (float v : bend) any_bend |= (v != 0.f);
+    for (double v : bend) any_bend |= (v != 0.0);
     if (any_bend) {
+        std::vector<float> bf(n);
+        for (int i = 0; i < n; ++i) bf[i] = (float)bend[i];
         int rc;
         if ((rc = dalloc(&e->bend_eps, n))) return rc;
-        HIPCHK(hipMemcpyAsync(e->bend_eps, bend.data(), n * sizeof(float), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipMemcpyAsync(e->bend_eps, bf.data(), n * sizeof(float), hipMemcpyHostToDevice, e->stream));
+        if (f64) {
+            if ((rc = dalloc(&e->dbend_eps, n))) return rc;
+            HIPCHK(hipMemcpyAsync(e->dbend_eps, bend.data(), n * sizeof(double), hipMemcpyHostToDevice, e->stream));
+        }
+        HIPCHK(hipStreamSynchronize(e->stream));  // bf dies here
         a.has_bend = 1;
     }
     size_t nt = 0;
@@ -561,9 +628,13 @@ int compile(gcs_engine* e)
     if (nt > 0) {
         std::vector<int> off(n + 1, 0);
         std::vector<Tether> ent;
+        std::vector<TetherT<double>> entd;
         for (int i = 0; i < n; ++i) {
             off[i] = (int)ent.size();
-            ent.insert(ent.end(), tlist[i].begin(), tlist[i].end());
+            for (const TetherT<double>& t : tlist[i]) {
+                ent.push_back(Tether{(float)t.px, (float)t.py, (float)t.pz, (float)t.k, (float)t.l, 0.f, 0.f, 0.f});
+                entd.push_back(t);
+            }
         }
         off[n] = (int)ent.size();
         int rc;
@@ -571,6 +642,11 @@ int compile(gcs_engine* e)
         if ((rc = dalloc(&e->tent, ent.size()))) return rc;
         HIPCHK(hipMemcpyAsync(e->toff, off.data(), (n + 1) * sizeof(int), hipMemcpyHostToDevice, e->stream));
         HIPCHK(hipMemcpyAsync(e->tent, ent.data(), ent.size() * sizeof(Tether), hipMemcpyHostToDevice, e->stream));
+        if (f64) {
+            if ((rc = dalloc(&e->dtent, entd.size()))) return rc;
+            HIPCHK(hipMemcpyAsync(e->dtent, entd.data(), entd.size() * sizeof(TetherT<double>), hipMemcpyHostToDevice,
+                                  e->stream));
+        }
         a.has_tether = 1;
     }
     a.boff = e->boff;
@@ -579,6 +655,9 @@ int compile(gcs_engine* e)
     a.bend_eps = e->bend_eps;
     a.toff = e->toff;
     a.tent = e->tent;
+    a.dbval = e->dbval;
+    a.dbend_eps = e->dbend_eps;
+    a.dtent = e->dtent;
     HIPCHK(hipStreamSynchronize(e->stream));  // host vectors die here
     e->dirty = false;
     e->topo_version++;
@@ -590,9 +669,16 @@ void fill_state_args(gcs_engine* e)
 {
     ForceArgs& a = e->fa;
     a.n = e->n;
+    a.prec = e->prec;
     a.pos0 = e->pos[0];
     a.pos1 = e->pos[1];
     a.kmu = e->kmu;
+    a.dpos0 = e->dpos[0];
+    a.dpos1 = e->dpos[1];
+    a.dkmu = e->dkmu;
+    a.dforce_out = e->dforce_out;
+    a.dpart = e->dpart;
+    a.dnoise = e->dnoise;
     a.spos = e->spos;
     a.sb = e->sb;
     a.sidx = e->sidx;
@@ -634,18 +720,44 @@ void enqueue_scan(gcs_engine* e, bool use_next)
 }
 
 // bin the current positions into ctx->grid: per-cell counts + slots, scan, tile table
+// count the current positions (either precision) into ctx->grid's cells; reg / islot: a decomposed domain's region
+void enqueue_count(gcs_engine* e, const DomBox* reg = nullptr, int* islot = nullptr)
+{
+    if (e->prec == 64)
+        launch_cell_count(e->stream, e->ctx, e->dpos[0], e->dpos[1], e->n, e->cell_of, e->slot, e->count, reg, islot);
+    else
+        launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], e->n, e->cell_of, e->slot, e->count, reg, islot);
+}
+
 void enqueue_bin(gcs_engine* e)
 {
-    const int n = e->n;
-    launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count);
+    enqueue_count(e);
     enqueue_scan(e, false);
 }
 
-// order each (scattered) cell by particle index: the cell-sorted copies the pair loop reads
-void enqueue_cell_order(gcs_engine* e)
+// order each (scattered) cell by particle index: the cell-sorted copies the pair loop reads; lists: also the
+// slot-ordered positions, constants and bond rows of the list step (islot: a decomposed build's particle -> slot)
+void enqueue_cell_order(gcs_engine* e, bool lists = false, int* islot = nullptr)
 {
-    launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, e->n, e->tmp, e->cell_of, e->cstart, e->sidx,
-                     e->scell, e->spos, e->sb, e->fa.has_pair ? e->fa.pair_mix : 1);
+    const int mix = e->fa.has_pair ? e->fa.pair_mix : 1;
+    const int* boff = e->fa.has_bonds ? e->boff : nullptr;
+    if (e->prec == 64) {
+        if (lists)
+            launch_cell_sort(e->stream, e->ctx, e->dpos[0], e->dpos[1], e->dkmu, e->n, e->tmp, e->cell_of, e->cstart,
+                             e->sidx, e->scell, e->spos, e->sb, mix, e->ptype, e->dpsort[0], e->dpsort[1], e->dskmu,
+                             e->sbrow, boff, islot);
+        else
+            launch_cell_sort(e->stream, e->ctx, e->dpos[0], e->dpos[1], e->dkmu, e->n, e->tmp, e->cell_of, e->cstart,
+                             e->sidx, e->scell, e->spos, e->sb, mix);
+    } else {
+        if (lists)
+            launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, e->n, e->tmp, e->cell_of, e->cstart,
+                             e->sidx, e->scell, e->spos, e->sb, mix, e->ptype, e->psort[0], e->psort[1], e->skmu,
+                             e->sbrow, boff, islot);
+        else
+            launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, e->n, e->tmp, e->cell_of, e->cstart,
+                             e->sidx, e->scell, e->spos, e->sb, mix);
+    }
 }
 
 // scatter into the cells and order each cell by particle index
@@ -662,25 +774,21 @@ void enqueue_cells(gcs_engine* e)
 }
 
 // the dense-system switch applies to undecomposed runs (a decomposed run picks its shape when it is primed)
-bool dense_switch(const gcs_engine* e) { return e->dense && !e->dom; }
+bool dense_switch(const gcs_engine* e) { return e->dense && !e->dom && e->prec != 64; }
 // the step shape a fixed-timestep run takes (GCS_OPT_FUSED_STEP semantics): the list step (3) falls back to the
 // rebuild step (2) when the system does not admit lists, and hands a dense chain to the unfused tile step (0)
 int eff_fused(const gcs_engine* e)
 {
+    if (e->prec == 64) return 3;  // the fp64 engine has the list step only (run() checks that the system admits it)
     if (e->fused != 3) return e->fused;
     if (!e->list_ok) return 2;
     return dense_switch(e) ? 0 : 3;
 }
 bool list_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) == 3 && !spacestep; }
-// small systems: the single-workgroup step loop (k_small) instead of the list step
-bool small_path(const gcs_engine* e, bool spacestep)
-{
-    return e->small_opt != 0 && e->n <= kSmallMax && e->fused == 3 && !spacestep && !e->dom;
-}
 bool fused_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) != 0 && !spacestep; }
 bool rebuild_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) == 2 && !spacestep; }
 
-float list_skin(const gcs_engine* e) { return 1e-3f * (float)e->list_skin_pm * e->fa.pair_dist; }
+float list_skin(const gcs_engine* e) { return 1e-3f * (float)e->list_skin_pm * e->fa.pf.pair_dist; }
 
 // the list build's chunk deal (kernels.hip deal_nth): the option, or the default for the waves per tile
 unsigned long long list_deal(const gcs_engine* e)
@@ -713,6 +821,10 @@ ForceArgs list_args(const gcs_engine* e)
     a.psort0 = e->psort[0];
     a.psort1 = e->psort[1];
     a.skmu = e->skmu;
+    a.dpsort0 = e->dpsort[0];
+    a.dpsort1 = e->dpsort[1];
+    a.dskmu = e->dskmu;
+    a.dtype_ab = e->dtype_ab;
     a.sbrow = e->sbrow;
     a.lticket = e->lticket;
     a.type_ab = e->type_ab;
@@ -737,12 +849,21 @@ int ensure_list(gcs_engine* e)
     dfree(e->psort[1]);
     dfree(e->skmu);
     dfree(e->sbrow);
+    dfree(e->dpsort[0]);
+    dfree(e->dpsort[1]);
+    dfree(e->dskmu);
     e->list_alloc = 0;
     int rc;
     if ((rc = dalloc(&e->list, need)) || (rc = dalloc(&e->lcount, stride * kMaxListWaves)) ||
-        (rc = dalloc(&e->psort[0], stride)) || (rc = dalloc(&e->psort[1], stride)) ||
-        (rc = dalloc(&e->skmu, stride)) || (rc = dalloc(&e->sbrow, stride)))
+        (rc = dalloc(&e->sbrow, stride)))
         return rc;
+    if (e->prec == 64) {  // the slot-ordered copies in the engine's precision only
+        if ((rc = dalloc(&e->dpsort[0], stride)) || (rc = dalloc(&e->dpsort[1], stride)) || (rc = dalloc(&e->dskmu, stride)))
+            return rc;
+    } else {
+        if ((rc = dalloc(&e->psort[0], stride)) || (rc = dalloc(&e->psort[1], stride)) || (rc = dalloc(&e->skmu, stride)))
+            return rc;
+    }
     if (!e->lticket) {
         // arrival counters 0, the launch accumulators at their identities (k_lstep resets them after every launch)
         if ((rc = dalloc(&e->lticket, kListTicketWords))) return rc;
@@ -802,12 +923,10 @@ void enqueue_list_step(gcs_engine* e, bool build, int lflags, double contact = 0
         la.c_overflow = e->c_flags;
     }
     if (build) {
-        launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], e->n, e->cell_of, e->slot, e->count);
+        enqueue_count(e);
         enqueue_scan(e, false);
         launch_cell_scatter(e->stream, e->n, e->cell_of, e->slot, e->cstart, e->tmp, e->count);
-        launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, e->n, e->tmp, e->cell_of, e->cstart,
-                         e->sidx, e->scell, e->spos, e->sb, e->fa.pair_mix, e->ptype, e->psort[0], e->psort[1], e->skmu,
-                         e->sbrow, e->fa.has_bonds ? e->boff : nullptr);
+        enqueue_cell_order(e, true);
         launch_list_build(e->stream, e->ctx, la);
     }
     launch_list_step(e->stream, e->ctx, la, lflags);
@@ -822,20 +941,25 @@ int step_grid(const gcs_engine* e) { return e->fa.split ? force_grid_split(e->n)
 // step's tail (reduction, schedule, wall, grid rotation) in one extra block.  begin_run binned, scanned and
 // scattered the first positions.  Otherwise (spacestep, or fusion off): count, scan, scatter, sort, force,
 // [adapt, update], tail.
-void enqueue_step(gcs_engine* e, bool spacestep, float spacestep_v, float timestep)
+void enqueue_step(gcs_engine* e, bool spacestep, double spacestep_v, double timestep)
 {
+    if (e->prec == 64) {
+        // fp64 (the spacestep relaxation step; fixed-timestep runs take the list step): cells, the fp64 force pass,
+        // its reduction (reactions, max drift -> the adapted dt), the update, the tail with those reactions
+        enqueue_cells(e);
+        launch_eval64(e->stream, kModeForce, e->ctx, e->fa);
+        launch_red64(e->stream, e->ctx, e->fa, spacestep ? spacestep_v : 0.0, timestep, e->dred);
+        launch_update(e->stream, e->ctx, e->fa);
+        ForceArgs t = e->fa;
+        t.ext_react = e->dred;
+        launch_tail(e->stream, e->ctx, t, 0, update_blocks(e->n), 1, e->sched_flags != 0, e->ncell_max, e->dsched);
+        return;
+    }
     const int fb = force_grid(e->n);
     const int sb = step_grid(e);  // kModeStep launch size (split tiles: two units per tile)
     if (rebuild_path(e, spacestep)) {
         launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, true);
         launch_rebuild(e->stream, e->ctx, e->fa, e->tmp, e->rb_sync, sb, e->sched_flags != 0);
-        return;
-    }
-    if (fused_path(e, spacestep)) {
-        enqueue_cell_order(e);
-        launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, true);
-        enqueue_scan(e, true);
-        launch_scatter_tail(e->stream, e->ctx, e->fa, e->tmp, sb, e->sched_flags != 0, e->ncell_max);
         return;
     }
     enqueue_cells(e);
@@ -844,7 +968,7 @@ void enqueue_step(gcs_engine* e, bool spacestep, float spacestep_v, float timest
         launch_tail(e->stream, e->ctx, e->fa, sb, sb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
     } else {
         launch_force(e->stream, kModeForce, e->waves, e->ctx, e->fa, false);
-        launch_adapt(e->stream, e->ctx, e->fa, fb, spacestep_v, timestep);
+        launch_adapt(e->stream, e->ctx, e->fa, fb, (float)spacestep_v, (float)timestep);
         launch_update(e->stream, e->ctx, e->fa);
         launch_tail(e->stream, e->ctx, e->fa, fb, update_blocks(e->n), 1, e->sched_flags != 0, e->ncell_max, e->dsched);
     }
@@ -883,7 +1007,7 @@ int prepare(gcs_engine* e)
 }
 
 int ensure_search(gcs_engine* e, int64_t n);
-int enqueue_search_cells(gcs_engine* e, const float4* src, int ni, double distance);
+int enqueue_search_cells(gcs_engine* e, const float4* src, const double4* src64, int ni, double distance);
 
 // The step shape of a fresh chain: the list step walks ~2.5 x (neighbours within the cutoff) entries per particle
 // with one gather each, the tile step shares each staged candidate among a tile's 64 lanes, so above a density the
@@ -900,11 +1024,11 @@ int probe_density(gcs_engine* e)
     double cs = 1.0;
     HIPCHK(hipStreamSynchronize(e->stream));
     HIPCHK(hipMemcpy(&cs, (const char*)e->ctx + offsetof(DevCtx, cs), sizeof(cs), hipMemcpyDeviceToHost));
-    const double rc = (double)e->fa.pair_dist * (e->fa.pair_scaled ? cs : 1.0);
+    const double rc = (double)e->fa.pf.pair_dist * (e->fa.pair_scaled ? cs : 1.0);
     int rc_;
     if (!(rc > 0) || e->n < 2) return GCS_OK;
     if ((rc_ = ensure_search(e, e->n))) return rc_;
-    if ((rc_ = enqueue_search_cells(e, e->pos[e->parity], e->n, rc))) return rc_;
+    if ((rc_ = enqueue_search_cells(e, e->pos[e->parity], nullptr, e->n, rc))) return rc_;
     launch_search_count(e->stream, e->s_ctx, e->n, e->s_spos, e->s_sidx, e->s_scell, e->s_cstart, e->s_counts);
     launch_exclusive_scan_small(e->stream, e->s_counts, e->s_offsets, e->n, e->s_total);
     HIPCHK(hipGetLastError());
@@ -922,7 +1046,7 @@ int choose_shape(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
 {
     int rc = prepare(e);
     if (rc) return rc;
-    if (e->fused != 3 || e->dense_opt <= 0 || !e->list_ok) {
+    if (e->fused != 3 || e->dense_opt <= 0 || !e->list_ok || e->prec == 64) {
         e->dense = false;
         return GCS_OK;
     }
@@ -940,8 +1064,10 @@ int begin_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
     int rc = prepare(e);
     if (rc) return rc;
     ForceArgs& a = e->fa;
-    a.temperature = (float)cfg->temperature;
-    a.timestep = (float)cfg->timestep;
+    a.pf.temperature = (float)cfg->temperature;
+    a.pf.timestep = (float)cfg->timestep;
+    a.pd.temperature = cfg->temperature;
+    a.pd.timestep = cfg->timestep;
     a.seed_lo = (unsigned)cfg->seed;
     a.seed_hi = (unsigned)(cfg->seed >> 32);
     a.noise_mode = cfg->noise;
@@ -958,7 +1084,6 @@ int begin_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
     }
     e->chain_dt = cfg->timestep;
     e->chain_valid = false;
-    e->small_cont = false;
     if (list_path(e, cfg->spacestep > 0)) {
         if ((rc = ensure_list(e))) return rc;
         e->list_every = auto_list_every(e, cfg);
@@ -971,9 +1096,6 @@ int begin_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
         if (rebuild_path(e, cfg->spacestep > 0)) {
             enqueue_cells(e);  // the first cell list; the steps rebuild it from the force kernel's buckets
             HIPCHK(hipMemsetAsync(e->ovf_n, 0, 2 * sizeof(int), e->stream));
-        } else if (fused) {
-            enqueue_bin(e);
-            launch_cell_scatter(e->stream, e->n, e->cell_of, e->slot, e->cstart, e->tmp, e->count);
         }
     }
     HIPCHK(hipGetLastError());
@@ -1053,64 +1175,6 @@ GraphKey run_key(const gcs_engine* e, const gcs_bd_config* cfg, bool spacestep)
 }
 
 int flush_contacts(gcs_engine* e);  // (below)
-
-// a run on the small-system path: one k_small launch for all its steps
-int run_small(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps)
-{
-    if (int rc = flush_contacts(e)) return rc;
-    int rc = prepare(e);
-    if (rc) return rc;
-    const size_t n = (size_t)e->n;
-    if (!e->sm_lcount) {
-        if ((rc = dalloc(&e->sm_list, n * kSmallCap)) || (rc = dalloc(&e->sm_lcount, n)) ||
-            (rc = dalloc(&e->sm_bpos, n)) || (rc = dalloc(&e->sm_cstart, kSmallCells + 1)) ||
-            (rc = dalloc(&e->sm_cidx, n)))
-            return rc;
-        e->small_cont = false;
-    }
-    ForceArgs& a = e->fa;
-    a.temperature = (float)cfg->temperature;
-    a.timestep = (float)cfg->timestep;
-    a.seed_lo = (unsigned)cfg->seed;
-    a.seed_hi = (unsigned)(cfg->seed >> 32);
-    a.noise_mode = cfg->noise;
-    long long st = first_step;
-    if ((rc = set_ctx_field(e, offsetof(DevCtx, step), &st, sizeof(st)))) return rc;
-    double dt = cfg->timestep;
-    if ((rc = set_ctx_field(e, offsetof(DevCtx, dt_used), &dt, sizeof(dt)))) return rc;
-    const bool cont = e->small_cont && e->small_step == first_step && e->small_version == e->topo_version;
-    const int flags = (e->sched_flags != 0 ? 1 : 0) | 4;  // schedule; neighbour-count statistics every step
-    // GCS_DEBUG_SMALL: thread 0's wall-clock per phase of the last launch, printed to stderr
-    unsigned long long* dbg = nullptr;
-    if (std::getenv("GCS_DEBUG_SMALL")) HIPCHK(hipMalloc(&dbg, 8 * sizeof(unsigned long long)));
-    for (int64_t done = 0; done < steps;) {
-        // chunks of at most 2^20 steps per launch (one launch holds the device for ~ms per thousand steps)
-        const int k = (int)std::min<int64_t>(steps - done, 1 << 20);
-        launch_small(e->stream, e->ctx, a, first_step + done, k, flags, (done == 0 && !cont) ? 1 : 0, list_skin(e),
-                     e->sm_list, e->sm_lcount, e->sm_bpos, e->sm_cstart, e->sm_cidx, dbg);
-        done += k;
-        e->rstats.small_launches++;
-    }
-    HIPCHK(hipGetLastError());
-    if (dbg) {
-        unsigned long long h[5];
-        HIPCHK(hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(hipStreamSynchronize(e->stream));
-        (void)hipFree(dbg);
-        std::fprintf(stderr, "gcs small: %lld steps, per step (us): build %.3f forces %.3f totals %.3f tail %.3f; "
-                     "builds %llu\n", (long long)steps, h[0] / 100.0 / steps, h[1] / 100.0 / steps,
-                     h[2] / 100.0 / steps, h[3] / 100.0 / steps, h[4]);
-    }
-    e->rstats.small_steps += steps;
-    e->chain_valid = false;   // the list step's own state did not follow
-    e->l_need_build = true;
-    e->small_cont = true;
-    e->small_step = first_step + steps;
-    e->small_version = e->topo_version;
-    if (steps & 1) e->parity ^= 1;
-    if (cfg->noise == GCS_NOISE_INJECTED) e->noise_cursor += steps;
-    return GCS_OK;
-}
 
 // after a run's steps were enqueued
 void end_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps)
@@ -1225,9 +1289,9 @@ int ensure_search(gcs_engine* e, int64_t n)
     return GCS_OK;
 }
 
-// the search cell list (grid edge >= distance) of n points at src, on the engine stream, no host sync:
-// s_spos / s_sidx / s_scell / s_cstart and s_ctx->grid
-int enqueue_search_cells(gcs_engine* e, const float4* src, int ni, double distance)
+// the search cell list (grid edge >= distance) of n points at src (fp32) or src64 (fp64: binned by their roundings),
+// on the engine stream, no host sync: s_spos / s_sidx / s_scell / s_cstart and s_ctx->grid
+int enqueue_search_cells(gcs_engine* e, const float4* src, const double4* src64, int ni, double distance)
 {
     // the source outlives the (possibly deferred) async copy: it is a member of the engine
     e->s_ctx_host = DevCtx{};
@@ -1236,15 +1300,25 @@ int enqueue_search_cells(gcs_engine* e, const float4* src, int ni, double distan
     HIPCHK(hipMemcpyAsync(e->s_ctx, &e->s_ctx_host, sizeof(DevCtx), hipMemcpyHostToDevice, e->stream));
     ForceArgs sa{};
     sa.n = ni;
+    sa.prec = src64 ? 64 : 32;
     sa.pos0 = const_cast<float4*>(src);
     sa.pos1 = const_cast<float4*>(src);
+    sa.dpos0 = const_cast<double4*>(src64);
+    sa.dpos1 = const_cast<double4*>(src64);
     launch_prime(e->stream, e->s_ctx, sa, (float)distance, e->s_ncell_max, nullptr);
-    launch_cell_count(e->stream, e->s_ctx, src, src, ni, e->s_cell_of, e->s_slot, e->s_count);
+    if (src64)
+        launch_cell_count(e->stream, e->s_ctx, src64, src64, ni, e->s_cell_of, e->s_slot, e->s_count);
+    else
+        launch_cell_count(e->stream, e->s_ctx, src, src, ni, e->s_cell_of, e->s_slot, e->s_count);
     launch_cell_scan(e->stream, e->s_ctx, ni, e->s_count, e->s_cstart, e->s_tile, e->s_tile_range, false, nullptr, 0,
                      e->scan_mb ? e->s_scan_sync : nullptr, e->s_ncell_max);
     launch_cell_scatter(e->stream, ni, e->s_cell_of, e->s_slot, e->s_cstart, e->s_tmp, e->s_count);
-    launch_cell_sort(e->stream, e->s_ctx, src, src, nullptr, ni, e->s_tmp, e->s_cell_of, e->s_cstart, e->s_sidx,
-                     e->s_scell, e->s_spos, e->s_sb, 1);
+    if (src64)
+        launch_cell_sort(e->stream, e->s_ctx, src64, src64, (const double4*)nullptr, ni, e->s_tmp, e->s_cell_of,
+                         e->s_cstart, e->s_sidx, e->s_scell, e->s_spos, e->s_sb, 1);
+    else
+        launch_cell_sort(e->stream, e->s_ctx, src, src, nullptr, ni, e->s_tmp, e->s_cell_of, e->s_cstart, e->s_sidx,
+                         e->s_scell, e->s_spos, e->s_sb, 1);
     HIPCHK(hipGetLastError());
     return GCS_OK;
 }
@@ -1253,16 +1327,17 @@ int enqueue_search_cells(gcs_engine* e, const float4* src, int ni, double distan
 int contacts_insert_now(gcs_engine* e, double distance)
 {
     int rc;
-    if (e->fused == 2 && e->chain_valid) {
+    if (e->prec != 64 && e->fused == 2 && e->chain_valid) {
         // right after a rebuild-step run the engine's own cell list holds the current positions (k_rebuild built
         // it from the records the last force kernel filed): no cell build of our own
-        launch_contact_insert(e->stream, e->ctx, e->n, (float)distance, e->spos, e->sidx, e->scell, e->cstart,
+        launch_contact_insert(e->stream, e->ctx, e->n, distance, e->spos, e->sidx, e->scell, e->cstart,
                               e->c_keys, e->c_counts, e->c_bits, e->c_flags);
     } else {
         if ((rc = ensure_search(e, e->n))) return rc;
-        if ((rc = enqueue_search_cells(e, e->pos[e->parity], e->n, distance))) return rc;
-        launch_contact_insert(e->stream, e->s_ctx, e->n, (float)distance, e->s_spos, e->s_sidx, e->s_scell,
-                              e->s_cstart, e->c_keys, e->c_counts, e->c_bits, e->c_flags);
+        const double4* p64 = e->prec == 64 ? e->dpos[e->parity] : nullptr;
+        if ((rc = enqueue_search_cells(e, e->pos[e->parity], p64, e->n, distance))) return rc;
+        launch_contact_insert(e->stream, e->s_ctx, e->n, distance, e->s_spos, e->s_sidx, e->s_scell,
+                              e->s_cstart, e->c_keys, e->c_counts, e->c_bits, e->c_flags, p64);
     }
     HIPCHK(hipGetLastError());
     return GCS_OK;
@@ -1301,8 +1376,11 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
     *out = nullptr;
     if (d->particle_count <= 0 || d->particle_count > (int64_t)1 << 30)
         return fail(GCS_EINVAL, "particle_count must be in [1, 2^30]");
+    if (d->precision != GCS_PRECISION_DEFAULT && d->precision != GCS_PRECISION_F32 && d->precision != GCS_PRECISION_F64)
+        return fail(GCS_EINVAL, "precision must be 0 (default: fp64), 32 or 64");
     gcs_engine* e = new gcs_engine();
     e->device = d->device;
+    e->prec = d->precision == GCS_PRECISION_F32 ? 32 : 64;
     e->n = (int)d->particle_count;
     e->fa.chunk_mode = 1;  // strided candidate chunks (GCS_OPT_CHUNK_ORDER)
     e->fa.split = 0;       // split tiles (GCS_OPT_SPLIT_TILES): 1 and 2 measured slower on C2
@@ -1338,7 +1416,8 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
         (rc = dalloc(&e->ctx, 1)) || (rc = dalloc(&e->dsched, kSchedCount)) ||
         (rc = dalloc(&e->part_force, (size_t)(std::max(fb, ub) + 8) * kForcePartials)) ||  // + the list step's
         (rc = dalloc(&e->part_bbox, (size_t)(std::max(fb, ub) + 8) * kBBoxStride)) ||       // 8 group rows
-        (rc = dalloc(&e->part_energy, (size_t)fb * kEnergyKinds)) || (rc = dalloc(&e->force_out, n)) ||
+        (rc = dalloc(&e->part_energy, (size_t)std::max(fb, eval64_blocks(n)) * kEnergyKinds)) ||
+        (rc = dalloc(&e->force_out, n)) ||
         (rc = dalloc(&e->pbuf, (size_t)2 * std::max(force_grid(n), kMaxUnits) * kTile)) ||
         (rc = dalloc(&e->tcnt, std::max(force_grid(n), kMaxUnits))) || (rc = dalloc(&e->units, 2 * kMaxUnits)) ||
         (rc = dalloc(&e->scan_sync, scan_sync_words(e->ncell_max))) ||
@@ -1357,6 +1436,14 @@ int gcs_engine_create(const gcs_system_desc* d, gcs_engine** out)
     e->resident = std::min(force_step_resident(e->waves), kMaxUnits);
     if (he == hipSuccess) he = hipMemsetAsync(e->pos[0], 0, n * sizeof(float4), e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->pos[1], 0, n * sizeof(float4), e->stream);
+    if (e->prec == 64) {  // the fp64 state (the fp32 pos buffers above stay allocated but unused: a few MB)
+        if ((rc = dalloc(&e->dpos[0], n)) || (rc = dalloc(&e->dpos[1], n)) || (rc = dalloc(&e->dkmu, n)) ||
+            (rc = dalloc(&e->dforce_out, n)) || (rc = dalloc(&e->dpart, (size_t)eval64_blocks(n) * 8)) ||
+            (rc = dalloc(&e->dred, 8)))
+            return bail(rc);
+        if (he == hipSuccess) he = hipMemsetAsync(e->dpos[0], 0, n * sizeof(double4), e->stream);
+        if (he == hipSuccess) he = hipMemsetAsync(e->dpos[1], 0, n * sizeof(double4), e->stream);
+    }
     DevCtx c{};
     c.cs = 1.0;
     c.bs = 1.0;
@@ -1433,11 +1520,21 @@ int gcs_engine_destroy(gcs_engine* e)
     if (e->nccl) rccl_comm_destroy(e->nccl);
     dfree(e->dom_shared_idx);
     dfree(e->dom_shared_flag);
-    dfree(e->sm_list);
-    dfree(e->sm_lcount);
-    dfree(e->sm_bpos);
-    dfree(e->sm_cstart);
-    dfree(e->sm_cidx);
+    dfree(e->dpos[0]);
+    dfree(e->dpos[1]);
+    dfree(e->dkmu);
+    dfree(e->dforce_out);
+    dfree(e->dpart);
+    dfree(e->dred);
+    dfree(e->dbval);
+    dfree(e->dbend_eps);
+    dfree(e->dtent);
+    dfree(e->dtype_ab);
+    dfree(e->dpsort[0]);
+    dfree(e->dpsort[1]);
+    dfree(e->dskmu);
+    dfree(e->dnoise);
+    dfree(e->s_pts64);
     dfree(e->c_keys);
     dfree(e->c_counts);
     dfree(e->c_flags);
@@ -1477,6 +1574,13 @@ int gcs_engine_particle_count(const gcs_engine* e, int64_t* count)
 {
     if (!e || !count) return fail(GCS_EINVAL, "null argument");
     *count = e->n;
+    return GCS_OK;
+}
+
+int gcs_engine_precision(const gcs_engine* e, int32_t* bits)
+{
+    if (!e || !bits) return fail(GCS_EINVAL, "null argument");
+    *bits = e->prec;
     return GCS_OK;
 }
 
@@ -1618,9 +1722,15 @@ int gcs_engine_set_positions(gcs_engine* e, const double* xyz, int64_t n)
     if (!e || !xyz) return fail(GCS_EINVAL, "null argument");
     if (int rc = flush_contacts(e)) return rc;
     e->chain_valid = false;
-    e->small_cont = false;
     if (n != e->n) return fail(GCS_EINVAL, "position count does not match the particle count");
     HIPCHK(hipSetDevice(e->device));
+    if (e->prec == 64) {
+        std::vector<double4> h(n);
+        for (int64_t i = 0; i < n; ++i) h[i] = make_double4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], 0.0);
+        HIPCHK(hipMemcpyAsync(e->dpos[e->parity], h.data(), n * sizeof(double4), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        return GCS_OK;
+    }
     std::vector<float4> h(n);
     for (int64_t i = 0; i < n; ++i)
         h[i] = make_float4((float)xyz[3 * i], (float)xyz[3 * i + 1], (float)xyz[3 * i + 2], 0.f);
@@ -1634,6 +1744,17 @@ int gcs_engine_get_positions(gcs_engine* e, double* xyz, int64_t n)
     if (!e || !xyz) return fail(GCS_EINVAL, "null argument");
     if (n != e->n) return fail(GCS_EINVAL, "position count does not match the particle count");
     HIPCHK(hipSetDevice(e->device));
+    if (e->prec == 64) {
+        std::vector<double4> h(n);
+        HIPCHK(hipMemcpyAsync(h.data(), e->dpos[e->parity], n * sizeof(double4), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        for (int64_t i = 0; i < n; ++i) {
+            xyz[3 * i] = h[i].x;
+            xyz[3 * i + 1] = h[i].y;
+            xyz[3 * i + 2] = h[i].z;
+        }
+        return GCS_OK;
+    }
     std::vector<float4> h(n);
     HIPCHK(hipMemcpyAsync(h.data(), e->pos[e->parity], n * sizeof(float4), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
@@ -1671,7 +1792,6 @@ int gcs_engine_set_context(gcs_engine* e, const gcs_context* c)
     if (!e || !c) return fail(GCS_EINVAL, "null argument");
     if (int rc = flush_contacts(e)) return rc;
     e->chain_valid = false;
-    e->small_cont = false;
     HIPCHK(hipSetDevice(e->device));
     DevCtx d;
     HIPCHK(hipMemcpyAsync(&d, e->ctx, sizeof(d), hipMemcpyDeviceToHost, e->stream));
@@ -1696,7 +1816,6 @@ int gcs_engine_set_schedule(gcs_engine* e, const gcs_schedule* s)
     if (e) e->dom_cont = false;  // a decomposed run re-primes after any outside change
     if (!e || !s) return fail(GCS_EINVAL, "null argument");
     e->chain_valid = false;
-    e->small_cont = false;
     if ((s->update_scales && (!(s->core_scale_tau > 0) || !(s->bond_scale_tau > 0))))
         return fail(GCS_EINVAL, "scale time constants must be positive");
     HIPCHK(hipSetDevice(e->device));
@@ -1711,7 +1830,6 @@ int gcs_engine_apply_schedule(gcs_engine* e, int64_t step)
 {
     if (!e) return fail(GCS_EINVAL, "null argument");
     e->chain_valid = false;
-    e->small_cont = false;
     int rc = prepare(e);
     if (rc) return rc;
     long long st = step;
@@ -1730,12 +1848,18 @@ int gcs_engine_set_noise(gcs_engine* e, const double* normals, int64_t steps)
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     dfree(e->noise);
+    dfree(e->dnoise);
     const size_t cnt = (size_t)steps * (size_t)e->n * 3;
-    std::vector<float> h(cnt);
-    for (size_t k = 0; k < cnt; ++k) h[k] = (float)normals[k];
-    int rc = dalloc(&e->noise, cnt);
-    if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(e->noise, h.data(), cnt * sizeof(float), hipMemcpyHostToDevice, e->stream));
+    int rc;
+    std::vector<float> h(e->prec == 64 ? 0 : cnt);
+    if (e->prec == 64) {  // the normals as given
+        if ((rc = dalloc(&e->dnoise, cnt))) return rc;
+        HIPCHK(hipMemcpyAsync(e->dnoise, normals, cnt * sizeof(double), hipMemcpyHostToDevice, e->stream));
+    } else {
+        for (size_t k = 0; k < cnt; ++k) h[k] = (float)normals[k];
+        if ((rc = dalloc(&e->noise, cnt))) return rc;
+        HIPCHK(hipMemcpyAsync(e->noise, h.data(), cnt * sizeof(float), hipMemcpyHostToDevice, e->stream));
+    }
     long long zero = 0;
     if ((rc = set_ctx_field(e, offsetof(DevCtx, noise_cursor), &zero, sizeof(zero)))) return rc;
     HIPCHK(hipStreamSynchronize(e->stream));
@@ -1756,10 +1880,11 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
         return fail(GCS_ESTATE, "not enough injected noise for the requested steps");
     if (steps == 0) return prepare(e);
     const bool spacestep = cfg->spacestep > 0;
-    if (small_path(e, spacestep)) return run_small(e, cfg, first_step, steps);
-    e->small_cont = false;  // another step shape moves the state on: the small path rebuilds next time
     int rc = choose_shape(e, cfg, first_step);
     if (rc) return rc;
+    if (e->prec == 64 && !spacestep && !e->list_ok)
+        return fail(GCS_ESTATE, "the fp64 engine's fixed-timestep step is the list step: it needs a neighbor soft-core "
+                                "field, <= 256 (a, b) pair classes and < 2^24 particles (use GCS_PRECISION_F32)");
     if (!list_path(e, spacestep))
         if ((rc = flush_contacts(e))) return rc;
     if ((rc = begin_run(e, cfg, first_step))) return rc;
@@ -1785,7 +1910,8 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
             const bool ct = e->c_pending > 0;
             if (ct) {
                 const float d = (float)e->c_pending;
-                launch_set_contact(e->stream, e->ctx, d * d);  // fp32 product, as k_contact_insert forms it
+                // the products the predicates form: fp32 (k_contact_insert) and fp64
+                launch_set_contact(e->stream, e->ctx, d * d, e->c_pending * e->c_pending);
                 e->c_pending = 0;
                 e->rstats.fused_contact_steps++;
             }
@@ -1816,14 +1942,14 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
         const int len = (int)std::min<int64_t>(G, steps - done);
         hipGraphExec_t x = nullptr;
         rc = cached_graph(e, key, 0, 0, len, [&]() {
-            for (int k = 0; k < len; ++k) enqueue_step(e, spacestep, (float)cfg->spacestep, (float)cfg->timestep);
+            for (int k = 0; k < len; ++k) enqueue_step(e, spacestep, cfg->spacestep, cfg->timestep);
         }, &x);
         if (rc || (rc = launch_graph(e, x))) return rc;
         e->rstats.graph_steps += len;
         done += len;
     }
     for (; done < steps; ++done) {
-        enqueue_step(e, spacestep, (float)cfg->spacestep, (float)cfg->timestep);
+        enqueue_step(e, spacestep, cfg->spacestep, cfg->timestep);
         e->rstats.eager_steps++;
     }
     HIPCHK(hipGetLastError());
@@ -1850,6 +1976,20 @@ int gcs_engine_compute_forces(gcs_engine* e, double* forces, int64_t n)
     if (rc) return rc;
     launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max, e->dsched);
     enqueue_cells(e);
+    if (e->prec == 64) {
+        launch_eval64(e->stream, kModeForce, e->ctx, e->fa);
+        launch_red64(e->stream, e->ctx, e->fa, -1.0, 0.0, nullptr);  // reactions, drift, neighbours (dt untouched)
+        HIPCHK(hipGetLastError());
+        std::vector<double4> h(n);
+        HIPCHK(hipMemcpyAsync(h.data(), e->dforce_out, n * sizeof(double4), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        for (int64_t i = 0; i < n; ++i) {
+            forces[3 * i] = h[i].x;
+            forces[3 * i + 1] = h[i].y;
+            forces[3 * i + 2] = h[i].z;
+        }
+        return GCS_OK;
+    }
     launch_force(e->stream, kModeForce, e->waves, e->ctx, e->fa, false);
     launch_tail(e->stream, e->ctx, e->fa, force_grid(e->n), 0, 0, 0, e->ncell_max, e->dsched);
     HIPCHK(hipGetLastError());
@@ -1872,9 +2012,12 @@ int gcs_engine_compute_energy(gcs_engine* e, double* total, double* per_kind)
     if (rc) return rc;
     launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max, e->dsched);
     enqueue_cells(e);
-    launch_force(e->stream, kModeEnergy, e->waves, e->ctx, e->fa, false);
+    if (e->prec == 64)
+        launch_eval64(e->stream, kModeEnergy, e->ctx, e->fa);
+    else
+        launch_force(e->stream, kModeEnergy, e->waves, e->ctx, e->fa, false);
     HIPCHK(hipGetLastError());
-    const int fb = force_grid(e->n);
+    const int fb = e->prec == 64 ? eval64_blocks(e->n) : force_grid(e->n);
     std::vector<double> h((size_t)fb * kEnergyKinds);
     HIPCHK(hipMemcpyAsync(h.data(), e->part_energy, h.size() * sizeof(double), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
@@ -1904,17 +2047,29 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
     if ((rc = ensure_search(e, n))) return rc;
     const int ni = (int)n;
     const float4* src = e->s_pts;
+    const double4* src64 = nullptr;  // fp64 engine: the points in fp64, the fp64 predicate
     if (points) {
-        std::vector<float4> h(n);
-        for (int64_t i = 0; i < n; ++i)
-            h[i] = make_float4((float)points[3 * i], (float)points[3 * i + 1], (float)points[3 * i + 2], 0.f);
-        HIPCHK(hipMemcpyAsync(e->s_pts, h.data(), n * sizeof(float4), hipMemcpyHostToDevice, e->stream));
+        if (e->prec == 64) {
+            dfree(e->s_pts64);
+            if ((rc = dalloc(&e->s_pts64, n))) return rc;
+            std::vector<double4> h(n);
+            for (int64_t i = 0; i < n; ++i) h[i] = make_double4(points[3 * i], points[3 * i + 1], points[3 * i + 2], 0.0);
+            HIPCHK(hipMemcpyAsync(e->s_pts64, h.data(), n * sizeof(double4), hipMemcpyHostToDevice, e->stream));
+            src64 = e->s_pts64;
+        } else {
+            std::vector<float4> h(n);
+            for (int64_t i = 0; i < n; ++i)
+                h[i] = make_float4((float)points[3 * i], (float)points[3 * i + 1], (float)points[3 * i + 2], 0.f);
+            HIPCHK(hipMemcpyAsync(e->s_pts, h.data(), n * sizeof(float4), hipMemcpyHostToDevice, e->stream));
+        }
         HIPCHK(hipStreamSynchronize(e->stream));
     } else {
         src = e->pos[e->parity];
+        if (e->prec == 64) src64 = e->dpos[e->parity];
     }
-    if ((rc = enqueue_search_cells(e, src, ni, distance))) return rc;
-    launch_search_count(e->stream, e->s_ctx, ni, e->s_spos, e->s_sidx, e->s_scell, e->s_cstart, e->s_counts);
+    if ((rc = enqueue_search_cells(e, src, src64, ni, distance))) return rc;
+    launch_search_count(e->stream, e->s_ctx, ni, e->s_spos, e->s_sidx, e->s_scell, e->s_cstart, e->s_counts, src64,
+                        distance);
     launch_exclusive_scan_small(e->stream, e->s_counts, e->s_offsets, ni, e->s_total);
     HIPCHK(hipGetLastError());
     int total = 0;
@@ -1934,7 +2089,8 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
         HIPCHK(hipMalloc(&e->s_sort_temp, std::max<size_t>(e->s_sort_bytes, 16)));
         e->s_key_cap = total;
     }
-    launch_search_emit(e->stream, e->s_ctx, ni, e->s_spos, e->s_sidx, e->s_scell, e->s_cstart, e->s_offsets, e->s_keys);
+    launch_search_emit(e->stream, e->s_ctx, ni, e->s_spos, e->s_sidx, e->s_scell, e->s_cstart, e->s_offsets, e->s_keys,
+                       src64, distance);
     size_t bytes = sort_u64_temp_bytes(total);
     if (bytes > e->s_sort_bytes) {
         (void)hipFree(e->s_sort_temp);
@@ -2068,7 +2224,10 @@ int gcs_engine_sample_positions(gcs_engine* e, float* xyz, int64_t n, int32_t fr
     HIPCHK(hipSetDevice(e->device));
     int rc;
     if (!e->q_out && (rc = dalloc(&e->q_out, 3 * (size_t)e->n))) return rc;
-    launch_quantize(e->stream, e->pos[e->parity], e->q_out, e->n, fraction_bits);
+    if (e->prec == 64)
+        launch_quantize(e->stream, e->dpos[e->parity], e->q_out, e->n, fraction_bits);
+    else
+        launch_quantize(e->stream, e->pos[e->parity], e->q_out, e->n, fraction_bits);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(xyz, e->q_out, 3 * (size_t)n * sizeof(float), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
@@ -2112,6 +2271,8 @@ int gcs_engine_set_domain(gcs_engine* e, const double* box, double halo, const d
         return GCS_OK;
     }
     if (!box) return fail(GCS_EINVAL, "null argument");
+    if (e->prec == 64)
+        return fail(GCS_ESTATE, "spatial decomposition runs on fp32 engines (GCS_PRECISION_F32)");
     for (int k = 0; k < 3; ++k)
         if (!(box[k] < box[3 + k])) return fail(GCS_EINVAL, "domain box must have lo < hi on every axis");
     if (npeer < 0 || npeer > kMaxPeers || (npeer > 0 && !peer_boxes)) return fail(GCS_EINVAL, "bad peer list");
@@ -2213,7 +2374,7 @@ DomBox dom_region(const gcs_engine* e) { return region_of(e->dom_box, e->dom_hal
 // (cutoff + skin at cs = 1; the tail checks cutoff + largest displacement every step, kDomFlagMotion)
 bool dom_list_ok(const gcs_engine* e)
 {
-    return list_path(e, false) && e->fa.has_pair && e->dom_halo >= e->fa.pair_dist + list_skin(e);
+    return list_path(e, false) && e->fa.has_pair && e->dom_halo >= e->fa.pf.pair_dist + list_skin(e);
 }
 
 // the list-step half of a decomposed step before the allreduce: on a rebuild step the cells of this domain's region
@@ -2224,13 +2385,10 @@ void enqueue_dom_list_step(gcs_engine* e, int64_t st, double* red)
     const ForceArgs a = domain_args(e, red);
     if (e->l_need_build || st % e->list_every == 0) {
         const DomBox reg = dom_region(e);
-        launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], e->n, e->cell_of, e->slot, e->count, &reg,
-                          e->islot);
+        enqueue_count(e, &reg, e->islot);
         enqueue_scan(e, false);
         launch_cell_scatter(e->stream, e->n, e->cell_of, e->slot, e->cstart, e->tmp, e->count);
-        launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, e->n, e->tmp, e->cell_of, e->cstart,
-                         e->sidx, e->scell, e->spos, e->sb, e->fa.pair_mix, e->ptype, e->psort[0], e->psort[1], e->skmu,
-                         e->sbrow, e->fa.has_bonds ? e->boff : nullptr, e->islot);
+        enqueue_cell_order(e, true, e->islot);
         launch_list_build(e->stream, e->ctx, a);
         e->l_need_build = false;
     }
@@ -2268,7 +2426,6 @@ int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step
                               hipMemcpyDeviceToDevice, e->stream));
     }
     e->chain_valid = false;
-    e->small_cont = false;
     e->dom_next = step + 1;
     if (e->dom_list) {
         enqueue_dom_list_step(e, step, dev_reaction);
@@ -2278,7 +2435,7 @@ int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step
     const ForceArgs a = domain_args(e);
     const int n = e->n;
     const DomBox reg = dom_region(e);
-    launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count, &reg);
+    enqueue_count(e, &reg);
     enqueue_scan(e, false);
     enqueue_sort(e);
     launch_force(e->stream, kModeStep, e->waves, e->ctx, a, false);
@@ -2422,7 +2579,7 @@ int enqueue_rccl_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step)
     const ForceArgs a = domain_args(e);
     const int n = e->n;
     const DomBox reg = dom_region(e);
-    launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], n, e->cell_of, e->slot, e->count, &reg);
+    enqueue_count(e, &reg);
     enqueue_scan(e, false);
     enqueue_sort(e);
     launch_force(e->stream, kModeStep, e->waves, e->ctx, a, false);
@@ -2544,7 +2701,6 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
         e->dom_next = first_step + steps;
     }
     e->chain_valid = false;
-    e->small_cont = false;
     return GCS_OK;
 }
 
@@ -2669,8 +2825,8 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
     for (auto& x : ev) HIPCHK(hipEventCreate(&x));
     const int fb = step_grid(e);
     HIPCHK(hipEventRecord(ev[0], e->stream));
-    const bool fused = fused_path(e, false), rebuild = rebuild_path(e, false), lst = list_path(e, false);
-    // per step: [1] cells [2] force [3] fused: next-step scan / unfused: tail [4] fused: scatter + tail [5]
+    const bool rebuild = rebuild_path(e, false), lst = list_path(e, false);
+    // per step: [1] cells [2] force [3] unfused: tail [4] - [5]
     // (rebuild: [1] - [2] force [3] rebuild + tail [4] - [5]; list: [1] cells + list build on rebuild steps
     // [2] list step incl. its tail [3] - [4] - [5])
     for (int64_t k = 0; k < steps; ++k) {
@@ -2682,12 +2838,10 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
             ForceArgs la = list_args(e);
             if (build) {
                 la.dbg_build = dbgb;
-                launch_cell_count(e->stream, e->ctx, e->pos[0], e->pos[1], e->n, e->cell_of, e->slot, e->count);
+                enqueue_count(e);
                 enqueue_scan(e, false);
                 launch_cell_scatter(e->stream, e->n, e->cell_of, e->slot, e->cstart, e->tmp, e->count);
-                launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, e->n, e->tmp, e->cell_of, e->cstart,
-                                 e->sidx, e->scell, e->spos, e->sb, e->fa.pair_mix, e->ptype, e->psort[0], e->psort[1], e->skmu,
-                         e->sbrow, e->fa.has_bonds ? e->boff : nullptr);
+                enqueue_cell_order(e, true);
                 launch_list_build(e->stream, e->ctx, la);
                 la.dbg_build = nullptr;
             }
@@ -2699,26 +2853,18 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
             for (int q = 3; q <= 5; ++q) HIPCHK(hipEventRecord(ev[q + 5 * k], e->stream));
             continue;
         }
-        if (rebuild)
-            ;
-        else if (fused)
-            enqueue_cell_order(e);
-        else
-            enqueue_cells(e);
+        if (!rebuild) enqueue_cells(e);
         HIPCHK(hipEventRecord(ev[2 + 5 * k], e->stream));
         if (dbg && k == steps - 1) e->fa.dbg_times = dbg;
 
-        launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, fused);
+        launch_force(e->stream, kModeStep, e->waves, e->ctx, e->fa, rebuild);
         HIPCHK(hipEventRecord(ev[3 + 5 * k], e->stream));
         if (rebuild)
             launch_rebuild(e->stream, e->ctx, e->fa, e->tmp, e->rb_sync, fb, e->sched_flags != 0);
-        else if (fused)
-            enqueue_scan(e, true);
         else
             launch_tail(e->stream, e->ctx, e->fa, fb, fb, 1, e->sched_flags != 0, e->ncell_max, e->dsched);
         e->fa.dbg_times = nullptr;
         HIPCHK(hipEventRecord(ev[4 + 5 * k], e->stream));
-        if (fused && !rebuild) launch_scatter_tail(e->stream, e->ctx, e->fa, e->tmp, fb, e->sched_flags != 0, e->ncell_max);
         HIPCHK(hipEventRecord(ev[5 + 5 * k], e->stream));
     }
     HIPCHK(hipEventRecord(ev[ev.size() - 1], e->stream));
@@ -2734,9 +2880,6 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
             cell += t[0];  // cell list + list build (rebuild steps only)
         } else if (rebuild) {
             cell += t[2];  // rebuild kernel (its tail block runs beside the cell-list blocks)
-        } else if (fused) {
-            cell += t[0] + t[2];  // sort + scan
-            tail += t[3];         // scatter + tail
         } else {
             cell += t[0];
             tail += t[2] + t[3];
@@ -2859,7 +3002,6 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
 {
     if (!e) return fail(GCS_EINVAL, "null argument");
     e->chain_valid = false;
-    e->small_cont = false;
     if (option == GCS_OPT_CONTACT_BITS) {
         if (value != 0 && (value < 10 || value > 34)) return fail(GCS_EINVAL, "contact bits must be 0 or in [10, 34]");
         if (e->c_keys) return fail(GCS_ESTATE, "the contact map is already allocated");
@@ -2910,17 +3052,12 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         if (value < 0) return fail(GCS_EINVAL, "dense threshold must be >= 0");
         e->dense_opt = (int)value;
         e->chain_valid = false;
-        e->small_cont = false;
-        return GCS_OK;
-    }
-    if (option == GCS_OPT_SMALL_PATH) {
-        if (value != 0 && value != 1) return fail(GCS_EINVAL, "small path must be 0 (off) or 1 (auto)");
-        e->small_opt = (int)value;
-        e->small_cont = false;
         return GCS_OK;
     }
     if (option == GCS_OPT_FUSED_STEP) {
-        if (value < 0 || value > 3) return fail(GCS_EINVAL, "fused step must be 0, 1, 2 or 3");
+        if (value != 0 && value != 2 && value != 3) return fail(GCS_EINVAL, "fused step must be 0, 2 or 3");
+        if (e->prec == 64 && value != 3)
+            return fail(GCS_EINVAL, "the fp64 engine runs the list step (GCS_OPT_FUSED_STEP 3) only");
         e->fused = (int)value;
         drop_graph(e);
         return GCS_OK;

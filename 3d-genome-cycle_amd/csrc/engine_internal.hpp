@@ -102,6 +102,7 @@ struct DevCtx {
     long long lfallback;
     int lnslots;  // slots of the current lists (binned particles: N, or a decomposed domain's owned + ghosts)
     float contact_d2;  // the squared distance of the contact update a list step counts (k_set_contact, fp32 product)
+    double contact_d2_64;  // the same in fp64 (the fp64 list step's predicate; k_set_contact, fp64 product)
 };
 
 // an axis-aligned box [lo, hi) (a decomposed domain's own box, or a peer's region: its box extended by the halo)
@@ -117,21 +118,47 @@ enum BondType : int { kSemispring = 0, kHarmonic = 1, kSpring = 2, kSoftwell = 3
 
 struct BondParam {
     int type, mix, scaled, pad;
-    float ka, kb, la, lb;  // softwell: ka = energy, kb = 1/decay^2, la = cutoff^2
+    double ka, kb, la, lb;  // softwell: ka = energy, kb = 1/decay^2, la = cutoff^2
 };
 
-struct Tether {  // kinetochore fiber spring to a fixed pole
-    float px, py, pz, k, l, pad0, pad1, pad2;
-};
+// Arithmetic precision (gcs_system_desc::precision).  The reference computes in double (md::scalar; e.g.
+// stage_transition/transition_interphase.cpp:38 brace-inits md::point from doubles): GCS_PRECISION_F64 runs the list
+// step, the particle-local terms, the integrator, the force / energy evaluations, the neighbour predicate and the
+// contact map in fp64 on fp64 positions; GCS_PRECISION_F32 is the fp32 engine (and the only one with the tile-step
+// shapes).  Kernels shared by both are templated on the scalar R; real4<R> is the 16- or 32-byte position record.
+template <typename R> struct RealVec;
+template <> struct RealVec<float> { using v4 = float4; using v2 = float2; };
+template <> struct RealVec<double> { using v4 = double4; using v2 = double2; };
+template <typename R> using real4 = typename RealVec<R>::v4;
+template <typename R> using real2 = typename RealVec<R>::v2;
 
-struct PointSrc {
+template <typename R>
+struct TetherT {  // kinetochore fiber spring to a fixed pole
+    R px, py, pz, k, l, pad0, pad1, pad2;
+};
+using Tether = TetherT<float>;
+
+template <typename R>
+struct PointSrcT {
     int type;      // GCS_POT_*
-    float px, py, pz, k, l, f, b;
+    R px, py, pz, k, l, f, b;
 };
 
-struct WallIn {
-    float a_eps, a_sig, b_eps, b_sig, wall_a, wall_b, cx, cy, cz;
+template <typename R>
+struct WallInT {
+    R a_eps, a_sig, b_eps, b_sig, wall_a, wall_b, cx, cy, cz;
     int mix, scaled;
+};
+
+// every scalar parameter of the compiled force fields and the BD config, once per precision (ForceArgs::pf / pd)
+template <typename R>
+struct FieldPrm {
+    R pa_eps, pa_sig, pb_eps, pb_sig, pair_dist;  // neighbour soft-core
+    R sw_ka, sw_kb, sw_la;                        // droplet softwell: energy, 1 / decay^2, cutoff^2
+    PointSrcT<R> point[kMaxPointSources];
+    WallInT<R> win;
+    R wout_k, wout_cx, wout_cy, wout_cz;
+    R temperature, timestep;
 };
 
 enum Mode : int { kModeStep = 0, kModeForce = 1, kModeEnergy = 2, kModeList = 3 };  // kModeList: build the neighbour lists
@@ -150,7 +177,10 @@ struct ForceArgs {
     const int2* tile_range; // [tiles] sorted-slot range [begin, end) of each k_force tile (k_cell_scan)
     // neighbor soft-core pair field
     int has_pair, pair_mix, pair_scaled, chunk_mode;
-    float pa_eps, pa_sig, pb_eps, pb_sig, pair_dist;
+    // the fields' scalar parameters at each precision (the fp32 kernels read pf, the fp64 ones pd)
+    FieldPrm<float> pf;
+    FieldPrm<double> pd;
+    int prec;  // 32 or 64: which of the state pointers below hold the system (GCS_PRECISION_*)
     // bonded CSR (particle order)
     int has_bonds;
     const int* boff;
@@ -161,7 +191,6 @@ struct ForceArgs {
     // through the bond CSR; targets carry kmu[i].w = 1
     int sw_n;
     const int* sw_idx;
-    float sw_ka, sw_kb, sw_la;  // energy, 1 / decay^2, cutoff^2
     // bending
     int has_bend;
     const float* bend_eps;
@@ -171,13 +200,9 @@ struct ForceArgs {
     const Tether* tent;
     // point sources
     int n_point;
-    PointSrc point[kMaxPointSources];
     // ellipsoid walls
     int has_wall_in, has_wall_out;
-    WallIn win;
-    float wout_k, wout_cx, wout_cy, wout_cz;
     // Brownian dynamics
-    float temperature, timestep;
     unsigned seed_lo, seed_hi;
     int noise_mode;
     const float* noise;
@@ -259,12 +284,59 @@ struct ForceArgs {
     int* c_overflow;
     unsigned* lticket;      // list step arrival counters: [32 g] per group of workgroups (g < 8), [32 * 8] groups;
                             // then the launch accumulators (kListAccBase)
+    // fp64 state (prec == 64; the fp32 buffers above then hold only the cell lists and the fp32 sorted copies the
+    // list build bins): positions {x, y, z, 0} in particle order (ping-pong), per-particle {mu, a, b, target}, the
+    // slot-ordered positions (.w: the bits of particle | class << 24 as a 64-bit integer) and constants, the pair
+    // classes' (a, b), the bond CSR values, bending, tethers, injected normals, forces, and the partial rows of
+    // the fp64 force / energy evaluation ([blocks][8])
+    double4* dpos0;
+    double4* dpos1;
+    const double4* dkmu;
+    double4* dpsort0;
+    double4* dpsort1;
+    double4* dskmu;
+    const double2* dtype_ab;
+    const double4* dbval;
+    const double* dbend_eps;
+    const TetherT<double>* dtent;
+    const double* dnoise;
+    double4* dforce_out;
+    double* dpart;
+};
+
+// Precision-generic access to the state of ForceArgs (St<float>: the fp32 buffers, St<double>: the fp64 ones)
+template <typename R> struct St;
+template <> struct St<float> {
+    __host__ __device__ static float4* pos(const ForceArgs& a, int par) { return par ? a.pos1 : a.pos0; }
+    __host__ __device__ static float4* psort(const ForceArgs& a, int par) { return par ? a.psort1 : a.psort0; }
+    __host__ __device__ static const float4* kmu(const ForceArgs& a) { return a.kmu; }
+    __host__ __device__ static const float4* skmu(const ForceArgs& a) { return a.skmu; }
+    __host__ __device__ static const float2* type_ab(const ForceArgs& a) { return a.type_ab; }
+    __host__ __device__ static const float4* bval(const ForceArgs& a) { return a.bval; }
+    __host__ __device__ static const float* bend(const ForceArgs& a) { return a.bend_eps; }
+    __host__ __device__ static const TetherT<float>* tent(const ForceArgs& a) { return a.tent; }
+    __host__ __device__ static const float* noise(const ForceArgs& a) { return a.noise; }
+    __host__ __device__ static float4* force(const ForceArgs& a) { return a.force_out; }
+    __host__ __device__ static const FieldPrm<float>& prm(const ForceArgs& a) { return a.pf; }
+};
+template <> struct St<double> {
+    __host__ __device__ static double4* pos(const ForceArgs& a, int par) { return par ? a.dpos1 : a.dpos0; }
+    __host__ __device__ static double4* psort(const ForceArgs& a, int par) { return par ? a.dpsort1 : a.dpsort0; }
+    __host__ __device__ static const double4* kmu(const ForceArgs& a) { return a.dkmu; }
+    __host__ __device__ static const double4* skmu(const ForceArgs& a) { return a.dskmu; }
+    __host__ __device__ static const double2* type_ab(const ForceArgs& a) { return a.dtype_ab; }
+    __host__ __device__ static const double4* bval(const ForceArgs& a) { return a.dbval; }
+    __host__ __device__ static const double* bend(const ForceArgs& a) { return a.dbend_eps; }
+    __host__ __device__ static const TetherT<double>* tent(const ForceArgs& a) { return a.dtent; }
+    __host__ __device__ static const double* noise(const ForceArgs& a) { return a.dnoise; }
+    __host__ __device__ static double4* force(const ForceArgs& a) { return a.dforce_out; }
+    __host__ __device__ static const FieldPrm<double>& prm(const ForceArgs& a) { return a.pd; }
 };
 
 // list step launch accumulators behind the arrival counters in ForceArgs::lticket (unsigned words, 128 B per slot):
 // per group of workgroups (b % 8) kListAccSlots slots + one overflow flag (kernels.hip list_accumulate)
 constexpr int kListAccBase = 32 * 9;
-constexpr int kListAccSlots = 16;
+constexpr int kListAccSlots = 22;
 constexpr int kListTicketWords = kListAccBase + 8 * 32 * (kListAccSlots + 1);
 // identity of accumulator slot k (what list_accumulate starts from)
 __host__ __device__ inline unsigned long long list_acc_identity(int k)
@@ -304,10 +376,12 @@ __host__ __device__ inline void philox4x32_10(unsigned c[4], unsigned k0, unsign
     }
 }
 
-// launch wrappers (kernels.hip)
+// launch wrappers (kernels.hip); those taking a ForceArgs run the precision it names (a.prec)
 void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed, int ncell_max, const double* sched);
 // reg != nullptr: bin only the particles inside *reg (a decomposed domain's region); islot != nullptr: reset to -1
 void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n,
+                       int* cell_of, int* slot, int* count, const DomBox* reg = nullptr, int* islot = nullptr);
+void launch_cell_count(hipStream_t s, const DevCtx* ctx, const double4* pos0, const double4* pos1, int n,
                        int* cell_of, int* slot, int* count, const DomBox* reg = nullptr, int* islot = nullptr);
 void launch_cell_scan(hipStream_t s, DevCtx* ctx, int n, int* count, int* cstart, int* tile_start, int2* tile_range,
                       bool use_next = false, int4* units = nullptr, int resident = 0,
@@ -319,8 +393,6 @@ void launch_rebuild(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int* tmp, un
 int rebuild_sync_words(int ncell_max);
 int rebuild_blocks(int ncell_max);
 int force_step_resident(int waves);
-void launch_scatter_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int* tmp, int fblocks, int apply_sched,
-                         int ncell_max);
 void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* slot, const int* cstart, int* tmp,
                          int* count);
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, const float4* kmu,
@@ -328,43 +400,56 @@ void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, cons
                       float4* spos, float* sb, int pair_mix, const int* ptype = nullptr, float4* psort0 = nullptr,
                       float4* psort1 = nullptr, float4* skmu = nullptr, int2* sbrow = nullptr,
                       const int* boff = nullptr, int* islot = nullptr);
+// fp64 positions: the fp32 sorted copies (spos / sb, what the list build bins) are their roundings; psort / skmu
+// are the fp64 slot-ordered copies the fp64 list step reads
+void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const double4* pos0, const double4* pos1, const double4* kmu,
+                      int n, const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell,
+                      float4* spos, float* sb, int pair_mix, const int* ptype = nullptr, double4* psort0 = nullptr,
+                      double4* psort1 = nullptr, double4* skmu = nullptr, int2* sbrow = nullptr,
+                      const int* boff = nullptr, int* islot = nullptr);
 // list step: build the neighbour lists on the current cell list (grid rc = cutoff + skin); one step from them
 void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a);
 // flags: 1 apply the schedule, 2 the next step rebuilds (bounding box -> grid), 4 neighbour-count statistics,
 // 8 decomposed (a.dom_on): the owned slots only, the local reduction into a.dom_red instead of the tail
 void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags);
-void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2);
+void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2, double d2_64);
 // the decomposed list step's tail from the allreduced buffer glob (one workgroup), then the shared particles'
 // positions into both buffers (by index and by slot) and the send bands' header rows zeroed
 void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const double* glob, int flags,
                              const int* shared, int nshared, float4* bands, int npeer, int band_stride);
 int list_step_grid(int n);
-// small systems (N <= kSmallMax): `steps` steps in one single-workgroup launch (kernels.hip k_small); its list state
-// (list [kSmallCap][N] u16, lcount [N], build positions [N], the build's cells [kSmallCells + 1] + [N]) persists
-constexpr int kSmallMax = 2048;
-constexpr int kSmallCap = 256;
-constexpr int kSmallCells = 4096;
-void launch_small(hipStream_t s, DevCtx* ctx, const ForceArgs& a, long long first_step, int steps, int flags,
-                  int force_build, float skin, unsigned short* list, int* lcount, float4* bpos, int* cstart,
-                  unsigned short* cidx, unsigned long long* dbg = nullptr);
 bool list_u16(int n);  // list entries are 16-bit slot indices (N <= 65536)
 void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceArgs& a, bool fused);
+// fp64 force / energy evaluation on the current cell list (one thread per sorted slot; kernels.hip k_eval64):
+// kModeForce -> a.dforce_out + partial rows a.dpart [blocks][8] (reactions in[3], out[3], max mu|F|, neighbours),
+// kModeEnergy -> a.part_energy [blocks][kEnergyKinds]
+int eval64_blocks(int n);
+void launch_eval64(hipStream_t s, int mode, const DevCtx* ctx, const ForceArgs& a);
+// reduce the fp64 evaluation's rows (fixed order) into the context's reactions, max drift and neighbour count, and
+// into react_out[6] when given (the tail's ext_react); spacestep >= 0: also dt_used = min(timestep, spacestep /
+// max drift) (spacestep 0: timestep)
+void launch_red64(hipStream_t s, DevCtx* ctx, const ForceArgs& a, double spacestep, double timestep,
+                  double* react_out);
 void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a);
 void launch_adapt(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force_blocks, float spacestep, float timestep);
 void launch_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force_blocks, int bbox_blocks, int advance,
                  int apply_sched, int ncell_max, const double* sched /* device: gcs_schedule mirror */);
+// pos64 != nullptr: the pair predicate runs in fp64 on pos64[sidx[slot]] (strict: no contraction) instead of fp32 on
+// the sorted copies
 void launch_search_count(hipStream_t s, const DevCtx* ctx, int n, const float4* spos, const int* sidx,
-                         const int* scell, const int* cstart, int* counts);
+                         const int* scell, const int* cstart, int* counts, const double4* pos64 = nullptr,
+                         double d64 = 0.0);
 void launch_search_emit(hipStream_t s, const DevCtx* ctx, int n, const float4* spos, const int* sidx,
-                        const int* scell, const int* cstart, const int* offsets, unsigned long long* keys);
+                        const int* scell, const int* cstart, const int* offsets, unsigned long long* keys,
+                        const double4* pos64 = nullptr, double d64 = 0.0);
 void launch_exclusive_scan_small(hipStream_t s, const int* in, int* out, int n, int* total);
 void sort_u64_keys(hipStream_t s, unsigned long long* keys, unsigned long long* tmp, int n, void* temp, size_t temp_bytes);
 size_t sort_u64_temp_bytes(int n);
 
 // contacts.hip: contact map + sampled-position quantisation
-void launch_contact_insert(hipStream_t s, const DevCtx* ctx, int n, float dist, const float4* spos, const int* sidx,
+void launch_contact_insert(hipStream_t s, const DevCtx* ctx, int n, double dist, const float4* spos, const int* sidx,
                            const int* scell, const int* cstart, unsigned long long* keys, unsigned* counts, int bits,
-                           int* overflow);
+                           int* overflow, const double4* pos64 = nullptr);
 void launch_contact_compact(hipStream_t s, const unsigned long long* keys, const unsigned* counts, long long slots,
                             unsigned long long* out_k, unsigned* out_c, int* total);
 size_t sort_pairs_u64_u32_temp_bytes(int n);
@@ -373,6 +458,7 @@ void sort_pairs_u64_u32(hipStream_t s, const unsigned long long* k_in, unsigned 
                         unsigned* v_out, int n, void* temp, size_t temp_bytes, int end_bit = 64);
 void launch_contact_emit(hipStream_t s, const unsigned long long* k, const unsigned* c, int n, unsigned* out);
 void launch_quantize(hipStream_t s, const float4* pos, float* out, int n, int bits);
+void launch_quantize(hipStream_t s, const double4* pos, float* out, int n, int bits);
 // domain.hip: spatial decomposition (band pack / unpack) + the local partial reduction of a decomposed step
 constexpr int kMaxPeers = 32;
 constexpr int kMaxDomains = 256;

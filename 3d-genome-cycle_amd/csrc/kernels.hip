@@ -137,6 +137,48 @@ __device__ inline float wave_min(float v)
 __device__ inline int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ inline float uniform_f(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 
+// ---- precision-generic scalar helpers (R = float: exactly the fp32 builtins the fp32 kernels always used) ----
+template <typename R> __device__ __forceinline__ R r_sqrt(R x)
+{
+    if constexpr (sizeof(R) == 4) return sqrtf(x); else return sqrt(x);
+}
+template <typename R> __device__ __forceinline__ R r_rsqrt(R x)
+{
+    if constexpr (sizeof(R) == 4) return rsqrtf(x); else return rsqrt(x);
+}
+template <typename R> __device__ __forceinline__ R r_fma(R a, R b, R c)
+{
+    if constexpr (sizeof(R) == 4) return fmaf(a, b, c); else return fma(a, b, c);
+}
+template <typename R> __device__ __forceinline__ R r_fmax(R a, R b)
+{
+    if constexpr (sizeof(R) == 4) return fmaxf(a, b); else return fmax(a, b);
+}
+template <typename R> __device__ __forceinline__ R r_fabs(R x)
+{
+    if constexpr (sizeof(R) == 4) return fabsf(x); else return fabs(x);
+}
+template <typename R> __device__ __forceinline__ R r_atan2(R y, R x)
+{
+    if constexpr (sizeof(R) == 4) return atan2f(y, x); else return atan2(y, x);
+}
+template <typename R> __device__ __forceinline__ R wave_sum_r(R v)
+{
+    if constexpr (sizeof(R) == 4) return wave_sum(v); else return wave_sum_d(v);
+}
+// the integer a slot-ordered position record carries in .w (particle | class << 24): the float's bits in fp32, the
+// low word of the double's bits in fp64
+__device__ __forceinline__ int wbits(float w) { return __float_as_int(w); }
+__device__ __forceinline__ int wbits(double w) { return (int)__double_as_longlong(w); }
+template <typename R> __device__ __forceinline__ R wpack(int v)
+{
+    if constexpr (sizeof(R) == 4) return __int_as_float(v); else return __longlong_as_double((long long)(unsigned)v);
+}
+template <typename R> __device__ __forceinline__ real4<R> mk4(R x, R y, R z, R w)
+{
+    if constexpr (sizeof(R) == 4) return make_float4(x, y, z, w); else return make_double4(x, y, z, w);
+}
+
 
 __device__ inline int wave_max_int(int v)
 {
@@ -218,33 +260,47 @@ __device__ __forceinline__ Grid next_grid(const DevCtx* ctx, const ForceArgs& a,
         const double t = (flags & 1) ? (double)step * sched[kSchedDt] : ctx->time;
         cs = 1.0 - (1.0 - sched[kSchedCs0]) * exp(-(t / sched[kSchedCsTau]));
     }
-    const float rc = a.has_pair ? a.pair_dist * (a.pair_scaled ? (float)fmax(cs, ctx->cs) : 1.f) : 1.f;
+    const float rc = a.has_pair ? a.pf.pair_dist * (a.pair_scaled ? (float)fmax(cs, ctx->cs) : 1.f) : 1.f;
     return make_grid(lo, hi, rc, ncell_max, kPairFx);
 }
 
 __device__ inline float pair_cutoff(const ForceArgs& a, double cs)
 {
     if (!a.has_pair) return 1.f;
-    return a.pair_dist * (a.pair_scaled ? (float)cs : 1.f);
+    return a.pf.pair_dist * (a.pair_scaled ? (float)cs : 1.f);
+}
+// the pair cutoff in precision R (fp32: exactly pair_cutoff)
+template <typename R>
+__device__ inline R pair_cutoff_r(const ForceArgs& a, double cs)
+{
+    if constexpr (sizeof(R) == 4) {
+        return pair_cutoff(a, cs);
+    } else {
+        if (!a.has_pair) return 1.0;
+        return a.pd.pair_dist * (a.pair_scaled ? cs : 1.0);
+    }
 }
 
 // ----------------------------------------------------------------------------------------------------
 // cell list
 
+// R: the positions' precision (the bounding box is taken of their fp32 roundings, which is what the cells bin)
+template <typename R>
 __global__ __launch_bounds__(1024) void k_prime(DevCtx* ctx, ForceArgs a, float rc_fixed, int ncell_max,
                                                 const double* __restrict__ sched)
 {
     __shared__ float red[6][16];
-    const float4* pos = ctx->parity ? a.pos1 : a.pos0;
+    const real4<R>* pos = St<R>::pos(a, ctx->parity);
     float lo[3] = {3.0e38f, 3.0e38f, 3.0e38f}, hi[3] = {-3.0e38f, -3.0e38f, -3.0e38f};
     for (int i = threadIdx.x; i < a.n; i += blockDim.x) {
-        float4 p = pos[i];
-        lo[0] = fminf(lo[0], p.x);
-        lo[1] = fminf(lo[1], p.y);
-        lo[2] = fminf(lo[2], p.z);
-        hi[0] = fmaxf(hi[0], p.x);
-        hi[1] = fmaxf(hi[1], p.y);
-        hi[2] = fmaxf(hi[2], p.z);
+        const real4<R> p = pos[i];
+        const float px = (float)p.x, py = (float)p.y, pz = (float)p.z;
+        lo[0] = fminf(lo[0], px);
+        lo[1] = fminf(lo[1], py);
+        lo[2] = fminf(lo[2], pz);
+        hi[0] = fmaxf(hi[0], px);
+        hi[1] = fmaxf(hi[1], py);
+        hi[2] = fmaxf(hi[2], pz);
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int k = 0; k < 3; ++k) {
@@ -275,16 +331,18 @@ __global__ __launch_bounds__(1024) void k_prime(DevCtx* ctx, ForceArgs a, float 
 
 // dom != 0: bin only the particles inside reg (a domain's box extended by its halo); islot: reset to -1 (k_cell_sort
 // writes the binned particles' slots)
-__global__ __launch_bounds__(256) void k_cell_count(const DevCtx* __restrict__ ctx, const float4* __restrict__ p0,
-                                                    const float4* __restrict__ p1, int n, int* __restrict__ cell_of,
+template <typename P>
+__global__ __launch_bounds__(256) void k_cell_count(const DevCtx* __restrict__ ctx, const P* __restrict__ p0,
+                                                    const P* __restrict__ p1, int n, int* __restrict__ cell_of,
                                                     int* __restrict__ slot, int* __restrict__ count, int dom,
                                                     DomBox reg, int* __restrict__ islot)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float4* pos = ctx->parity ? p1 : p0;
+    const P* pos = ctx->parity ? p1 : p0;
     const Grid g = ctx->grid;
-    const float4 p = pos[i];
+    const P pr = pos[i];
+    const float4 p = make_float4((float)pr.x, (float)pr.y, (float)pr.z, 0.f);  // fp64 positions bin by their rounding
     const int c = cell_index(g, p.x, p.y, p.z);
     if (islot) islot[i] = -1;
     if (dom && !box_has(reg, p.x, p.y, p.z)) {  // domain: outside its region, not binned
@@ -840,28 +898,6 @@ __global__ __launch_bounds__(kMbThreads) void k_cell_scan_mb(DevCtx* __restrict_
     }
 }
 
-// fused step: the scatter of the next step's cells, and in one extra block the tail of the step just computed
-// (partials -> reactions, schedule, wall; grid <- grid_next and the grid after it).  The scatter blocks touch
-// no DevCtx field, so the tail block owns the context.
-__global__ __launch_bounds__(256) void k_scatter_tail(DevCtx* ctx, ForceArgs a, int n, int* __restrict__ tmp,
-                                                      int fblocks, int apply_sched, int ncell_max)
-{
-    if (blockIdx.x == gridDim.x - 1) {
-        const unsigned long long t0 = wall_clock64();
-        tail_body(ctx, a, fblocks, fblocks, 1, apply_sched, ncell_max, a.sched, true);
-        if (threadIdx.x == 0) {
-            ctx->t_tail[0] = t0;
-            ctx->t_tail[1] = wall_clock64();
-        }
-        return;
-    }
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int c = a.cell_of[i];
-    tmp[a.cstart_w[c] + a.slot[i]] = i;
-    a.count[c] = 0;  // every occupied cell has a particle here: count is all-zero again for the next binning
-}
-
 // Rebuild step (GCS_OPT_FUSED_STEP 2): everything between two force kernels in ONE launch.  Block 0 runs the
 // step's tail (tail_body: reductions, schedule, wall, grid <- grid_next).  Blocks 1.. rebuild the cell list the
 // force kernel filed into its per-cell buckets, each owning rows of the grid (R = max(1, kRbCells / nx) rows):
@@ -1183,36 +1219,40 @@ __global__ __launch_bounds__(256) void k_cell_scatter(int n, const int* __restri
     count[c] = 0;  // every occupied cell has a particle here: count is all-zero again for the next binning
 }
 
-__global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ctx, const float4* __restrict__ p0,
-                                                   const float4* __restrict__ p1, const float4* __restrict__ kmu, int n,
-                                                   const int* __restrict__ tmp, const int* __restrict__ cell_of,
+// R: the positions' precision.  spos / sb are fp32 always (the list build and the tile step read them: in fp64 the
+// roundings of the fp64 positions, which only place particles in cells and candidates in lists -- every pair force
+// and pair test of the fp64 step reads psort); psort / skmu are in the positions' precision
+template <typename R>
+__global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ctx, const real4<R>* __restrict__ p0,
+                                                   const real4<R>* __restrict__ p1, const real4<R>* __restrict__ kmu,
+                                                   int n, const int* __restrict__ tmp, const int* __restrict__ cell_of,
                                                    const int* __restrict__ cstart, int* __restrict__ sidx,
                                                    int* __restrict__ scell, float4* __restrict__ spos,
                                                    float* __restrict__ sb, int pair_mix,
-                                                   const int* __restrict__ ptype, float4* __restrict__ psort0,
-                                                   float4* __restrict__ psort1, float4* __restrict__ skmu,
+                                                   const int* __restrict__ ptype, real4<R>* __restrict__ psort0,
+                                                   real4<R>* __restrict__ psort1, real4<R>* __restrict__ skmu,
                                                    int2* __restrict__ sbrow, const int* __restrict__ boff,
                                                    int* __restrict__ islot)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n || s >= cstart[ctx->grid.ncell]) return;  // binned particles only (all of them, undecomposed)
-    const float4* pos = ctx->parity ? p1 : p0;
+    const real4<R>* pos = ctx->parity ? p1 : p0;
     const int i = tmp[s];
     const int c = cell_of[i];
     const int b = cstart[c], e = cstart[c + 1];
     int r = 0;
     for (int t = b; t < e; ++t) r += (tmp[t] < i) ? 1 : 0;
     const int d = b + r;
-    const float4 p = pos[i];
-    const float4 k = kmu ? kmu[i] : make_float4(1.f, 1.f, 0.f, 0.f);
+    const real4<R> p = pos[i];
+    const real4<R> k = kmu ? kmu[i] : mk4<R>(R(1), R(1), R(0), R(0));
     sidx[d] = i;
     scell[d] = c;
     // the pair field's factors: (a, b) when it mixes A/B (interphase), (1, 0) for plain softcore<2,3>
-    spos[d] = make_float4(p.x, p.y, p.z, pair_mix ? k.y : 1.f);
-    sb[d] = pair_mix ? k.z : 0.f;
+    spos[d] = make_float4((float)p.x, (float)p.y, (float)p.z, pair_mix ? (float)k.y : 1.f);
+    sb[d] = pair_mix ? (float)k.z : 0.f;
     if (psort0) {  // list path: the current positions in slot order, .w = particle | class << 24; the slot's
                    // constants and bond CSR row (the list step reads them by slot, not behind the particle index)
-        (ctx->parity ? psort1 : psort0)[d] = make_float4(p.x, p.y, p.z, __int_as_float(i | (ptype[i] << kListIndexBits)));
+        (ctx->parity ? psort1 : psort0)[d] = mk4<R>(p.x, p.y, p.z, wpack<R>(i | (ptype[i] << kListIndexBits)));
         skmu[d] = k;
         sbrow[d] = boff ? make_int2(boff[i], boff[i + 1]) : make_int2(0, 0);
         if (islot) islot[i] = d;
@@ -1222,57 +1262,69 @@ __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ct
 // ----------------------------------------------------------------------------------------------------
 // Brownian step helpers
 
-__device__ inline void philox_normal3(unsigned seed_lo, unsigned seed_hi, long long step, int i, float& n0, float& n1,
-                                      float& n2)
+// Philox4x32-10 normals of particle i at `step` (the oracle's gcso_philox_normals, oracle/rng.c): counter (i, step_lo,
+// step_hi, 'GCS1'), key (seed_lo, seed_hi), u = ((r >> 8) + 0.5) 2^-24 (exact in both precisions), Box-Muller on
+// (u0, u1) -> x, y and (u2, u3) -> z, evaluated in R
+template <typename R>
+__device__ inline void philox_normal3(unsigned seed_lo, unsigned seed_hi, long long step, int i, R& n0, R& n1, R& n2)
 {
     unsigned c[4] = {(unsigned)i, (unsigned)(unsigned long long)step, (unsigned)((unsigned long long)step >> 32),
                      0x47435331u};
     philox4x32_10(c, seed_lo, seed_hi);
-    const float k24 = 1.0f / 16777216.0f;
-    float u0 = ((float)(c[0] >> 8) + 0.5f) * k24;
-    float u1 = ((float)(c[1] >> 8) + 0.5f) * k24;
-    float u2 = ((float)(c[2] >> 8) + 0.5f) * k24;
-    float u3 = ((float)(c[3] >> 8) + 0.5f) * k24;
-    float r1 = sqrtf(-2.0f * logf(u0));
-    float r2 = sqrtf(-2.0f * logf(u2));
-    float s1, c1, s2, c2;
-    sincospif(2.0f * u1, &s1, &c1);
-    sincospif(2.0f * u3, &s2, &c2);
+    const R k24 = R(1) / R(16777216);
+    R u0 = ((R)(c[0] >> 8) + R(0.5)) * k24;
+    R u1 = ((R)(c[1] >> 8) + R(0.5)) * k24;
+    R u2 = ((R)(c[2] >> 8) + R(0.5)) * k24;
+    R u3 = ((R)(c[3] >> 8) + R(0.5)) * k24;
+    R s1, c1, s2, c2, r1, r2;
+    if constexpr (sizeof(R) == 4) {
+        r1 = sqrtf(-2.0f * logf(u0));
+        r2 = sqrtf(-2.0f * logf(u2));
+        sincospif(2.0f * u1, &s1, &c1);
+        sincospif(2.0f * u3, &s2, &c2);
+    } else {
+        r1 = sqrt(-2.0 * log(u0));
+        r2 = sqrt(-2.0 * log(u2));
+        sincospi(2.0 * u1, &s1, &c1);
+        sincospi(2.0 * u3, &s2, &c2);
+    }
     n0 = r1 * c1;
     n1 = r1 * s1;
     n2 = r2 * c2;
 }
 
-__device__ inline void noise3(const ForceArgs& a, const DevCtx* ctx, int i, float& n0, float& n1, float& n2)
+template <typename R>
+__device__ inline void noise3(const ForceArgs& a, const DevCtx* ctx, int i, R& n0, R& n1, R& n2)
 {
     if (a.noise_mode == GCS_NOISE_PHILOX) {
-        philox_normal3(a.seed_lo, a.seed_hi, ctx->step + 1, i, n0, n1, n2);
+        philox_normal3<R>(a.seed_lo, a.seed_hi, ctx->step + 1, i, n0, n1, n2);
     } else if (a.noise_mode == GCS_NOISE_INJECTED) {
         long long cur = ctx->noise_cursor;
         if (cur >= a.noise_steps) cur = a.noise_steps - 1;  // host checks the budget before launching
-        const float* p = a.noise + (cur * (long long)a.n + i) * 3;
+        const R* p = St<R>::noise(a) + (cur * (long long)a.n + i) * 3;
         n0 = p[0];
         n1 = p[1];
         n2 = p[2];
     } else {
-        n0 = n1 = n2 = 0.f;
+        n0 = n1 = n2 = R(0);
     }
 }
 
 // spring-type potential at separation vector r (|r|^2 = r2): returns force coefficient c (F = c r) and U
-__device__ inline float spring_coef(int type, float K, float l, float r2, float& U)
+template <typename R>
+__device__ inline R spring_coef(int type, R K, R l, R r2, R& U)
 {
     if (type == kHarmonic) {
-        U = 0.5f * K * r2;
+        U = R(0.5) * K * r2;
         return -K;
     }
-    float d = sqrtf(r2);
-    if ((type == kSemispring && d <= l) || d <= 0.f) {
-        U = (type == kSpring && d <= 0.f) ? 0.5f * K * l * l : 0.f;
-        return 0.f;
+    R d = r_sqrt(r2);
+    if ((type == kSemispring && d <= l) || d <= R(0)) {
+        U = (type == kSpring && d <= R(0)) ? R(0.5) * K * l * l : R(0);
+        return R(0);
     }
-    float dl = d - l;
-    U = 0.5f * K * dl * dl;
+    R dl = d - l;
+    U = R(0.5) * K * dl * dl;
     return -K * dl / d;
 }
 
@@ -1280,29 +1332,31 @@ __device__ inline float spring_coef(int type, float K, float l, float r2, float&
 // force / step kernel
 
 // Particle-local terms of particle i at (xi, yi, zi): bonded CSR (chain/loop/nucleolar bonds, droplet),
-// cosine bending, kinetochore fibers, point sources and the ellipsoid walls (+ their reactions).
+// cosine bending, kinetochore fibers, point sources and the ellipsoid walls (+ their reactions), in precision R.
 // BB: bonded entries whose loads are issued together (a row of the CSR is a chain of dependent loads per entry
 // otherwise: the nucleolar particles' ~20 droplet and bond partners made it the longest path of a step)
-template <int MODE, int BB = 1>
-__device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceArgs& a, int i, float xi, float yi,
-                                   float zi, float4 km, float& fx, float& fy, float& fz, float* en, float* rin,
-                                   float* rout, int2 erange = make_int2(-1, -1))
+template <int MODE, int BB = 1, typename R = float>
+__device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceArgs& a, int i, R xi, R yi, R zi,
+                                   real4<R> km, R& fx, R& fy, R& fz, R* en, R* rin, R* rout,
+                                   int2 erange = make_int2(-1, -1))
 {
     const int n = a.n;
-    const float4* __restrict__ posc = ctx->parity ? a.pos1 : a.pos0;
-    const float cs = (float)ctx->cs;
-    const float bs = (float)ctx->bs;
-    float e_sw = 0.f, e_bond = 0.f, e_bend = 0.f, e_win = 0.f, e_wout = 0.f, e_pt = 0.f, e_kf = 0.f;
+    const FieldPrm<R>& P = St<R>::prm(a);
+    const real4<R>* __restrict__ posc = St<R>::pos(a, ctx->parity);
+    const R cs = (R)ctx->cs;
+    const R bs = (R)ctx->bs;
+    R e_sw = 0, e_bond = 0, e_bend = 0, e_win = 0, e_wout = 0, e_pt = 0, e_kf = 0;
     if (a.has_bonds) {
         // erange: the particle's CSR row when the caller already has it (the list step's slot-ordered copy)
         const int eb = erange.x >= 0 ? erange.x : a.boff[i], ee = erange.x >= 0 ? erange.y : a.boff[i + 1];
+        const real4<R>* __restrict__ bval = St<R>::bval(a);
         for (int q0 = eb; q0 < ee; q0 += BB) {
           int2 enb[BB];
-          float4 bvb[BB], pjb[BB];
+          real4<R> bvb[BB], pjb[BB];
 #pragma unroll
           for (int u = 0; u < BB; ++u) {
               enb[u] = (q0 + u < ee) ? a.bent[q0 + u] : make_int2(i, kSemispring);
-              bvb[u] = (q0 + u < ee) ? a.bval[q0 + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+              bvb[u] = (q0 + u < ee) ? bval[q0 + u] : mk4<R>(R(0), R(0), R(0), R(0));
           }
 #pragma unroll
           for (int u = 0; u < BB; ++u) pjb[u] = posc[enb[u].x];
@@ -1310,30 +1364,30 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
           for (int u = 0; u < BB; ++u) {
             if (q0 + u >= ee) break;
             const int type = enb[u].y & 15;
-            const float4 bv = bvb[u];
-            const float4 pj = pjb[u];
-            const float rx = xi - pj.x, ry = yi - pj.y, rz = zi - pj.z;
-            const float r2 = fmaf(rz, rz, fmaf(ry, ry, rx * rx));
-            float c = 0.f, U = 0.f;
+            const real4<R> bv = bvb[u];
+            const real4<R> pj = pjb[u];
+            const R rx = xi - pj.x, ry = yi - pj.y, rz = zi - pj.z;
+            const R r2 = r_fma(rz, rz, r_fma(ry, ry, rx * rx));
+            R c = 0, U = 0;
             if (type == kSoftwell) {
                 if (r2 < bv.z) {
-                    const float u6 = r2 * bv.y;
-                    const float den = 1.f + u6 * u6 * u6;
-                    c = -6.f * bv.x * u6 * u6 * bv.y / (den * den);
-                    e_sw += -0.5f * bv.x / den;
+                    const R u6 = r2 * bv.y;
+                    const R den = R(1) + u6 * u6 * u6;
+                    c = R(-6) * bv.x * u6 * u6 * bv.y / (den * den);
+                    e_sw += R(-0.5) * bv.x / den;
                 }
             } else {
-                float K = bv.x, l = bv.y;
+                R K = bv.x, l = bv.y;
                 if (enb[u].y >> 4) {  // scaled by the bond scale
-                    K = K * (1.f / (bs * bs));
+                    K = K * (R(1) / (bs * bs));
                     l = l * bs;
                 }
-                c = spring_coef(type, K, l, r2, U);
-                e_bond += 0.5f * U;
+                c = spring_coef<R>(type, K, l, r2, U);
+                e_bond += R(0.5) * U;
             }
-            fx = fmaf(c, rx, fx);
-            fy = fmaf(c, ry, fy);
-            fz = fmaf(c, rz, fz);
+            fx = r_fma(c, rx, fx);
+            fy = r_fma(c, ry, fy);
+            fz = r_fma(c, rz, fz);
           }
         }
     }
@@ -1342,51 +1396,52 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
         // the droplet (simulation_driver_forcefield.cpp:164-185: softwell among the nucleolar targets, cut off at
         // apply_cutoff): every target interacts with every other; a wave holding a target loads all targets' positions
         // once (lane t: target t) and walks them by shuffles, in target order
-        const bool tgt = km.w != 0.f;
+        const bool tgt = km.w != R(0);
         if (__ballot(tgt)) {
             const int m = a.sw_n;
             const int jt = (__lane_id() < m) ? a.sw_idx[__lane_id()] : 0;
-            const float4 pt = posc[jt];
+            const real4<R> pt = posc[jt];
             for (int t = 0; t < m; ++t) {
                 const int j = __shfl(jt, t);
-                const float px = __shfl(pt.x, t), py = __shfl(pt.y, t), pz = __shfl(pt.z, t);
-                const float rx = xi - px, ry = yi - py, rz = zi - pz;
-                const float r2 = fmaf(rz, rz, fmaf(ry, ry, rx * rx));
-                if (tgt && j != i && r2 < a.sw_la) {
-                    const float u6 = r2 * a.sw_kb;
-                    const float den = 1.f + u6 * u6 * u6;
-                    const float c = -6.f * a.sw_ka * u6 * u6 * a.sw_kb / (den * den);
-                    e_sw += -0.5f * a.sw_ka / den;
-                    fx = fmaf(c, rx, fx);
-                    fy = fmaf(c, ry, fy);
-                    fz = fmaf(c, rz, fz);
+                const R px = __shfl(pt.x, t), py = __shfl(pt.y, t), pz = __shfl(pt.z, t);
+                const R rx = xi - px, ry = yi - py, rz = zi - pz;
+                const R r2 = r_fma(rz, rz, r_fma(ry, ry, rx * rx));
+                if (tgt && j != i && r2 < P.sw_la) {
+                    const R u6 = r2 * P.sw_kb;
+                    const R den = R(1) + u6 * u6 * u6;
+                    const R c = R(-6) * P.sw_ka * u6 * u6 * P.sw_kb / (den * den);
+                    e_sw += R(-0.5) * P.sw_ka / den;
+                    fx = r_fma(c, rx, fx);
+                    fy = r_fma(c, ry, fy);
+                    fz = r_fma(c, rz, fz);
                 }
             }
         }
     }
 
     if (a.has_bend) {
+        const R* __restrict__ bend = St<R>::bend(a);
         for (int role = 0; role < 3; ++role) {
             const int k0 = i - role;
             if (k0 < 0 || k0 + 2 >= n) continue;
-            const float eps = a.bend_eps[k0];
-            if (eps == 0.f) continue;
-            float4 q0 = (role == 0) ? make_float4(xi, yi, zi, 0.f) : posc[k0];
-            float4 q1 = (role == 1) ? make_float4(xi, yi, zi, 0.f) : posc[k0 + 1];
-            float4 q2 = (role == 2) ? make_float4(xi, yi, zi, 0.f) : posc[k0 + 2];
-            const float r1x = q1.x - q0.x, r1y = q1.y - q0.y, r1z = q1.z - q0.z;
-            const float r2x = q2.x - q1.x, r2y = q2.y - q1.y, r2z = q2.z - q1.z;
-            const float n1 = r1x * r1x + r1y * r1y + r1z * r1z;
-            const float n2 = r2x * r2x + r2y * r2y + r2z * r2z;
-            if (!(n1 > 0.f) || !(n2 > 0.f)) continue;
-            const float inv12 = rsqrtf(n1 * n2);
-            const float cv = (r1x * r2x + r1y * r2y + r1z * r2z) * inv12;
-            const float i1 = cv / n1, i2 = cv / n2;
-            const float d1x = r2x * inv12 - i1 * r1x, d1y = r2y * inv12 - i1 * r1y, d1z = r2z * inv12 - i1 * r1z;
-            const float d2x = r1x * inv12 - i2 * r2x, d2y = r1y * inv12 - i2 * r2y, d2z = r1z * inv12 - i2 * r2z;
+            const R eps = bend[k0];
+            if (eps == R(0)) continue;
+            real4<R> q0 = (role == 0) ? mk4<R>(xi, yi, zi, R(0)) : posc[k0];
+            real4<R> q1 = (role == 1) ? mk4<R>(xi, yi, zi, R(0)) : posc[k0 + 1];
+            real4<R> q2 = (role == 2) ? mk4<R>(xi, yi, zi, R(0)) : posc[k0 + 2];
+            const R r1x = q1.x - q0.x, r1y = q1.y - q0.y, r1z = q1.z - q0.z;
+            const R r2x = q2.x - q1.x, r2y = q2.y - q1.y, r2z = q2.z - q1.z;
+            const R n1 = r1x * r1x + r1y * r1y + r1z * r1z;
+            const R n2 = r2x * r2x + r2y * r2y + r2z * r2z;
+            if (!(n1 > R(0)) || !(n2 > R(0))) continue;
+            const R inv12 = r_rsqrt(n1 * n2);
+            const R cv = (r1x * r2x + r1y * r2y + r1z * r2z) * inv12;
+            const R i1 = cv / n1, i2 = cv / n2;
+            const R d1x = r2x * inv12 - i1 * r1x, d1y = r2y * inv12 - i1 * r1y, d1z = r2z * inv12 - i1 * r1z;
+            const R d2x = r1x * inv12 - i2 * r2x, d2y = r1y * inv12 - i2 * r2y, d2z = r1z * inv12 - i2 * r2z;
             if (role == 0) {
                 fx -= eps * d1x; fy -= eps * d1y; fz -= eps * d1z;
-                e_bend += eps * (1.f - cv);
+                e_bend += eps * (R(1) - cv);
             } else if (role == 2) {
                 fx += eps * d2x; fy += eps * d2y; fz += eps * d2z;
             } else {
@@ -1397,90 +1452,91 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
 
     if (a.has_tether) {
         const int tb = a.toff[i], te = a.toff[i + 1];
+        const TetherT<R>* __restrict__ tent = St<R>::tent(a);
         for (int q = tb; q < te; ++q) {
-            const Tether t = a.tent[q];
-            const float rx = xi - t.px, ry = yi - t.py, rz = zi - t.pz;
-            float U;
-            const float c = spring_coef(kSpring, t.k, t.l, rx * rx + ry * ry + rz * rz, U);
+            const TetherT<R> t = tent[q];
+            const R rx = xi - t.px, ry = yi - t.py, rz = zi - t.pz;
+            R U;
+            const R c = spring_coef<R>(kSpring, t.k, t.l, rx * rx + ry * ry + rz * rz, U);
             e_kf += U;
-            fx = fmaf(c, rx, fx);
-            fy = fmaf(c, ry, fy);
-            fz = fmaf(c, rz, fz);
+            fx = r_fma(c, rx, fx);
+            fy = r_fma(c, ry, fy);
+            fz = r_fma(c, rz, fz);
         }
     }
 
 #pragma unroll
     for (int q = 0; q < kMaxPointSources; ++q) {
         if (q >= a.n_point) break;
-        PointSrc p = a.point[q];
+        PointSrcT<R> p = P.point[q];
         // opaque to the optimizer: keeps the (rarely used, mitotic-only) point-source constants from being hoisted
         // to the kernel entry, where they would be spilled to scratch by every wave
         asm volatile("" : "+v"(p.b), "+v"(p.f), "+v"(p.k), "+v"(p.l));
-        const float rx = xi - p.px, ry = yi - p.py, rz = zi - p.pz;
-        const float r2 = rx * rx + ry * ry + rz * rz;
-        float c, U;
+        const R rx = xi - p.px, ry = yi - p.py, rz = zi - p.pz;
+        const R r2 = rx * rx + ry * ry + rz * rz;
+        R c, U;
         if (p.type == GCS_POT_FORCE_FLUX) {
             // common/potentials/force_flux_potential.hpp:24-37
-            const float r1 = sqrtf(r2), b2 = p.b * p.b;
-            c = (r1 > 0.f) ? p.f * b2 / (b2 * r1 + r1 * r2) : 0.f;
-            U = p.f * p.b * atan2f(p.b, r1);
+            const R r1 = r_sqrt(r2), b2 = p.b * p.b;
+            c = (r1 > R(0)) ? p.f * b2 / (b2 * r1 + r1 * r2) : R(0);
+            U = p.f * p.b * r_atan2(p.b, r1);
         } else {
-            c = spring_coef(p.type == GCS_POT_SEMISPRING ? kSemispring : (p.type == GCS_POT_HARMONIC ? kHarmonic : kSpring),
-                            p.k, p.l, r2, U);
+            c = spring_coef<R>(p.type == GCS_POT_SEMISPRING ? kSemispring : (p.type == GCS_POT_HARMONIC ? kHarmonic : kSpring),
+                               p.k, p.l, r2, U);
         }
         e_pt += U;
-        fx = fmaf(c, rx, fx);
-        fy = fmaf(c, ry, fy);
-        fz = fmaf(c, rz, fz);
+        fx = r_fma(c, rx, fx);
+        fy = r_fma(c, ry, fy);
+        fz = r_fma(c, rz, fz);
     }
 
     if (a.has_wall_in || a.has_wall_out) {
         // Sampson distance to the ellipsoid (DESIGN.md "ellipsoid wall"): rho = |r o 1/ax|,
         // g = r o 1/ax^2, d = |1 - rho| rho / |g|, normal n = g / |g|
-        const float ax = (float)ctx->wall[0], ay = (float)ctx->wall[1], az = (float)ctx->wall[2];
-        const float cx = a.has_wall_in ? a.win.cx : a.wout_cx;
-        const float cy = a.has_wall_in ? a.win.cy : a.wout_cy;
-        const float cz = a.has_wall_in ? a.win.cz : a.wout_cz;
-        const float rx = xi - cx, ry = yi - cy, rz = zi - cz;
-        const float qx = rx / ax, qy = ry / ay, qz = rz / az;
-        const float gx = qx / ax, gy = qy / ay, gz = qz / az;
-        const float g2 = gx * gx + gy * gy + gz * gz;
-        if (g2 > 0.f) {
-            const float rho = sqrtf(qx * qx + qy * qy + qz * qz);
-            const float ginv = rsqrtf(g2);
-            const float d = fabsf(1.f - rho) * rho * ginv;
-            const float nx_ = gx * ginv, ny_ = gy * ginv, nz_ = gz * ginv;
-            if (a.has_wall_in && rho < 1.f) {
-                const WallIn& w = a.win;
-                const float sc = w.scaled ? cs : 1.f;
-                const float A = w.mix ? 0.5f * (km.y + w.wall_a) : 1.f;
-                const float B = w.mix ? 0.5f * (km.z + w.wall_b) : 0.f;
-                const float d2 = d * d;
-                const float sa = w.a_sig * sc, sbw = w.b_sig * sc;
-                const float k2a = 1.f / (sa * sa), k2b = 1.f / (sbw * sbw);
-                const float ua = d2 * k2a, t = d2 * k2b;
-                float coef = 0.f, U = 0.f;
-                if (ua < 1.f) {
-                    const float ga = 1.f - ua;
-                    coef += A * 6.f * w.a_eps * k2a * ga * ga;
+        const R ax = (R)ctx->wall[0], ay = (R)ctx->wall[1], az = (R)ctx->wall[2];
+        const R cx = a.has_wall_in ? P.win.cx : P.wout_cx;
+        const R cy = a.has_wall_in ? P.win.cy : P.wout_cy;
+        const R cz = a.has_wall_in ? P.win.cz : P.wout_cz;
+        const R rx = xi - cx, ry = yi - cy, rz = zi - cz;
+        const R qx = rx / ax, qy = ry / ay, qz = rz / az;
+        const R gx = qx / ax, gy = qy / ay, gz = qz / az;
+        const R g2 = gx * gx + gy * gy + gz * gz;
+        if (g2 > R(0)) {
+            const R rho = r_sqrt(qx * qx + qy * qy + qz * qz);
+            const R ginv = r_rsqrt(g2);
+            const R d = r_fabs(R(1) - rho) * rho * ginv;
+            const R nx_ = gx * ginv, ny_ = gy * ginv, nz_ = gz * ginv;
+            if (a.has_wall_in && rho < R(1)) {
+                const WallInT<R>& w = P.win;
+                const R sc = w.scaled ? cs : R(1);
+                const R A = w.mix ? R(0.5) * (km.y + w.wall_a) : R(1);
+                const R B = w.mix ? R(0.5) * (km.z + w.wall_b) : R(0);
+                const R d2 = d * d;
+                const R sa = w.a_sig * sc, sbw = w.b_sig * sc;
+                const R k2a = R(1) / (sa * sa), k2b = R(1) / (sbw * sbw);
+                const R ua = d2 * k2a, t = d2 * k2b;
+                R coef = 0, U = 0;
+                if (ua < R(1)) {
+                    const R ga = R(1) - ua;
+                    coef += A * R(6) * w.a_eps * k2a * ga * ga;
                     U += A * w.a_eps * ga * ga * ga;
                 }
-                if (t < 1.f && B != 0.f) {
-                    const float t2 = t * t;
-                    const float gb = 1.f - t2 * t2;
-                    coef += B * 24.f * w.b_eps * k2b * gb * gb * t2 * t;
+                if (t < R(1) && B != R(0)) {
+                    const R t2 = t * t;
+                    const R gb = R(1) - t2 * t2;
+                    coef += B * R(24) * w.b_eps * k2b * gb * gb * t2 * t;
                     U += B * w.b_eps * gb * gb * gb;
                 }
-                const float wx = -coef * d * nx_, wy = -coef * d * ny_, wz = -coef * d * nz_;
+                const R wx = -coef * d * nx_, wy = -coef * d * ny_, wz = -coef * d * nz_;
                 fx += wx; fy += wy; fz += wz;
-                rin[0] = fabsf(wx); rin[1] = fabsf(wy); rin[2] = fabsf(wz);
+                rin[0] = r_fabs(wx); rin[1] = r_fabs(wy); rin[2] = r_fabs(wz);
                 e_win += U;
             }
-            if (a.has_wall_out && rho > 1.f) {
-                const float wx = -a.wout_k * d * nx_, wy = -a.wout_k * d * ny_, wz = -a.wout_k * d * nz_;
+            if (a.has_wall_out && rho > R(1)) {
+                const R wx = -P.wout_k * d * nx_, wy = -P.wout_k * d * ny_, wz = -P.wout_k * d * nz_;
                 fx += wx; fy += wy; fz += wz;
-                rout[0] = fabsf(wx); rout[1] = fabsf(wy); rout[2] = fabsf(wz);
-                e_wout += 0.5f * a.wout_k * d * d;
+                rout[0] = r_fabs(wx); rout[1] = r_fabs(wy); rout[2] = r_fabs(wz);
+                e_wout += R(0.5) * P.wout_k * d * d;
             }
         }
     }
@@ -1515,12 +1571,12 @@ __device__ inline void pair_forces(const DevCtx* __restrict__ ctx, const ForceAr
     const Grid g = ctx->grid;
     const float cs = (float)ctx->cs;
     const float scale = a.pair_scaled ? cs : 1.f;
-    const float sa = a.pa_sig * scale, sbb = a.pb_sig * scale;
+    const float sa = a.pf.pa_sig * scale, sbb = a.pf.pb_sig * scale;
     const float k2a = 1.f / (sa * sa), k2b = 1.f / (sbb * sbb);
     // F = coef * (x_i - x_j):  A * 6 eps_a k2a ga^2  +  B * 24 eps_b k2b gb^2 t^3   (A, B = pair means)
     // energy: 1/2 (mean) x 1/2 (each pair seen from both ends) x eps (A ga^3 + B gb^3)
-    const float kA = (MODE == kModeEnergy) ? 0.25f * a.pa_eps : 0.5f * 6.f * a.pa_eps * k2a;
-    const float kB = (MODE == kModeEnergy) ? 0.25f * a.pb_eps : 0.5f * 24.f * a.pb_eps * k2b;
+    const float kA = (MODE == kModeEnergy) ? 0.25f * a.pf.pa_eps : 0.5f * 6.f * a.pf.pa_eps * k2a;
+    const float kB = (MODE == kModeEnergy) ? 0.25f * a.pf.pb_eps : 0.5f * 24.f * a.pf.pb_eps * k2b;
     const float rc2 = g.rc2;
     const int nx = g.n[0], ny = g.n[1], nz = g.n[2], gfx = g.fx;
     const int c0 = uniform(a.scell[s_begin]), c1 = uniform(a.scell[s_end - 1]);
@@ -1774,10 +1830,10 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
     const Grid g = ctx->grid;
     const float cs = (float)ctx->cs;
     const float scale = a.pair_scaled ? cs : 1.f;
-    const float sa = a.pa_sig * scale, sbb = a.pb_sig * scale;
+    const float sa = a.pf.pa_sig * scale, sbb = a.pf.pb_sig * scale;
     const float k2a = 1.f / (sa * sa), k2b = 1.f / (sbb * sbb);
-    const float kA = (MODE == kModeEnergy) ? 0.25f * a.pa_eps : 0.5f * 6.f * a.pa_eps * k2a;
-    const float kB = (MODE == kModeEnergy) ? 0.25f * a.pb_eps : 0.5f * 24.f * a.pb_eps * k2b;
+    const float kA = (MODE == kModeEnergy) ? 0.25f * a.pf.pa_eps : 0.5f * 6.f * a.pf.pa_eps * k2a;
+    const float kB = (MODE == kModeEnergy) ? 0.25f * a.pf.pb_eps : 0.5f * 24.f * a.pf.pb_eps * k2b;
     const float rc2 = g.rc2;
     const int nx = g.n[0], ny = g.n[1], nz = g.n[2], gfx = g.fx;
     const int grp = lane / GL, gl = lane % GL;
@@ -2216,10 +2272,10 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(FUSE
                     // Euler-Maruyama: x += mu dt F + sqrt(2 T mu dt) xi
                     float4* __restrict__ posn = ctx->parity ? a.pos0 : a.pos1;
                     const float mu = km.x;
-                    const float dt = a.timestep;
+                    const float dt = a.pf.timestep;
                     float n0, n1, n2;
                     noise3(a, ctx, i, n0, n1, n2);
-                    const float amp = sqrtf(2.f * a.temperature * mu * dt);
+                    const float amp = sqrtf(2.f * a.pf.temperature * mu * dt);
                     const float mdt = mu * dt;
                     // ghosts (domain decomposition) keep their position: the owner's exchange refreshes both buffers
                     const float nxp = own ? pi.x + mdt * fx + amp * n0 : pi.x;
@@ -2300,6 +2356,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(FUSE
 }
 
 // spacestep path: update from stored forces with the adapted timestep (ctx->dt_used)
+template <typename R>
 __global__ __launch_bounds__(kUpdateBlock) void k_update(const DevCtx* __restrict__ ctx, ForceArgs a)
 {
     __shared__ float red[6][kUpdateBlock / 64];
@@ -2307,20 +2364,21 @@ __global__ __launch_bounds__(kUpdateBlock) void k_update(const DevCtx* __restric
     const bool valid = i < a.n;
     const int il = valid ? i : a.n - 1;
     const int par = ctx->parity;
-    const float4* posc = par ? a.pos1 : a.pos0;
-    float4* posn = par ? a.pos0 : a.pos1;
-    const float4 p = posc[il];
-    const float4 f = a.force_out[il];
-    const float mu = a.kmu[il].x;
-    const float dt = (float)ctx->dt_used;
-    float n0, n1, n2;
-    noise3(a, ctx, il, n0, n1, n2);
-    const float amp = sqrtf(2.f * a.temperature * mu * dt);
-    const float mdt = mu * dt;
-    const float x = p.x + mdt * f.x + amp * n0;
-    const float y = p.y + mdt * f.y + amp * n1;
-    const float z = p.z + mdt * f.z + amp * n2;
-    if (valid) posn[i] = make_float4(x, y, z, 0.f);
+    const real4<R>* posc = St<R>::pos(a, par);
+    real4<R>* posn = St<R>::pos(a, par ^ 1);
+    const real4<R> p = posc[il];
+    const real4<R> f = St<R>::force(a)[il];
+    const R mu = St<R>::kmu(a)[il].x;
+    const R dt = (R)ctx->dt_used;
+    R n0, n1, n2;
+    noise3<R>(a, ctx, il, n0, n1, n2);
+    const R amp = r_sqrt(R(2) * St<R>::prm(a).temperature * mu * dt);
+    const R mdt = mu * dt;
+    const R xr = p.x + mdt * f.x + amp * n0;
+    const R yr = p.y + mdt * f.y + amp * n1;
+    const R zr = p.z + mdt * f.z + amp * n2;
+    if (valid) posn[i] = mk4<R>(xr, yr, zr, R(0));
+    const float x = (float)xr, y = (float)yr, z = (float)zr;  // the bbox of the roundings (what the cells bin)
     const float big = 3.0e38f;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float v[6] = {wave_min(valid ? x : big),  wave_min(valid ? y : big),  wave_min(valid ? z : big),
@@ -2528,7 +2586,7 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
                 const double t = (flags & 1) ? (double)(step + 1) * s_dt : time;
                 csn = 1.0 - (1.0 - s_cs0) * exp(-(t / s_csTau));
             }
-            const float rc = a.has_pair ? a.pair_dist * (a.pair_scaled ? (float)fmax(csn, cs) : 1.f) : 1.f;
+            const float rc = a.has_pair ? a.pf.pair_dist * (a.pair_scaled ? (float)fmax(csn, cs) : 1.f) : 1.f;
 #pragma unroll
             for (int k = 0; k < kGridWords; ++k) reinterpret_cast<int*>(&ctx->grid)[k] = c_gn[k];
             ctx->grid_next = make_grid(lo, hi, rc, ncell_max, kPairFx);
@@ -2584,12 +2642,26 @@ __global__ __launch_bounds__(256) void k_tail(DevCtx* ctx, ForceArgs a, int fblo
 
 // the contact map's pair count (contacts.hip k_contact_insert: strict fp32 predicate, Fibonacci-hashed open
 // addressing, contact_count); i < j by particle index, so each pair counts once
-__device__ __forceinline__ void list_contact(const ForceArgs& a, float d2, float4 p, float4 q, int i, int j)
+// strict pair predicate of the neighbour search and the contact map: (dx^2 + dy^2) + dz^2 < d2, every operation
+// rounded on its own (no contraction), in the positions' precision -- the oracle's gcso_search_neighbors(64)
+__device__ __forceinline__ bool strict_lt(float px, float py, float pz, float qx, float qy, float qz, float d2)
+{
+    const float dx = __fsub_rn(px, qx), dy = __fsub_rn(py, qy), dz = __fsub_rn(pz, qz);
+    const float r2 = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
+    return r2 < d2;
+}
+__device__ __forceinline__ bool strict_lt(double px, double py, double pz, double qx, double qy, double qz, double d2)
+{
+    const double dx = __dsub_rn(px, qx), dy = __dsub_rn(py, qy), dz = __dsub_rn(pz, qz);
+    const double r2 = __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
+    return r2 < d2;
+}
+
+template <typename R>
+__device__ __forceinline__ void list_contact(const ForceArgs& a, R d2, real4<R> p, real4<R> q, int i, int j)
 {
     if (j <= i) return;
-    const float dx = __fsub_rn(p.x, q.x), dy = __fsub_rn(p.y, q.y), dz = __fsub_rn(p.z, q.z);
-    const float r2 = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
-    if (!(r2 < d2)) return;
+    if (!strict_lt(p.x, p.y, p.z, q.x, q.y, q.z, d2)) return;
     const unsigned long long key = ((unsigned long long)(unsigned)i << 32) | (unsigned)j;
     if (!contact_count(a.c_keys, a.c_counts, a.c_bits, key)) atomicOr(a.c_overflow, 1);
 }
@@ -2688,15 +2760,17 @@ __device__ void list_tail_apply(DevCtx* ctx, const ForceArgs& a, const ListTailI
 // launches), one set per group of workgroups g = b % 8 (a device-scope atomic word takes ~11 ns per arrival: a
 // single set would queue all ~1000 workgroups of a C2 launch on each word).  Integer atomics only: the totals do
 // not depend on the arrival order, so runs stay bitwise reproducible.
-//   0-5   wall reactions in[3], out[3]   int64 fixed point (2^-24), added
+//   0-5   wall reactions in[3], out[3]   high words: h = floor(r 2^20), int64, added
 //   6     neighbour count                integer, added (stats launches)
 //   7     max displacement from the build (>= 0): float bits, atomic max
 //   8     fallback particles             integer, added
 //   9-11  bbox lo, 12-14 bbox hi         order-preserving integer image of the float, atomic min / max (bbox launches)
 //   15    owned particles                integer, added (decomposed launches)
-//   16    a reaction whose fixed-point image would not fit (non-finite or > 2^38): the totals carry a NaN reaction, as
-//         a float sum would
-constexpr double kAccScale = 16777216.0;  // 2^24
+//   16-21 wall reactions, low words      l = round((r 2^20 - h) 2^32) in [0, 2^32], added: r = (h + l 2^-32) 2^-20
+//                                        exactly up to 2^-52 per term (the fp64 step's reactions keep fp64 resolution)
+//   22    a reaction whose fixed-point image would not fit (non-finite or >= 2^41): the totals carry a NaN reaction,
+//         as a float sum would
+constexpr int kAccReactLo = 16;
 constexpr int kAccWords = kListAccSlots + 1;  // slots + the overflow flag, per group
 __device__ __forceinline__ unsigned ordered_bits(float v)
 {
@@ -2712,25 +2786,31 @@ __device__ __forceinline__ unsigned long long* acc_slot(unsigned* base, int k)
     return reinterpret_cast<unsigned long long*>(base + 32 * k);
 }
 // fold one value into slot k of a group's accumulators (one lane per slot)
-__device__ __forceinline__ void acc_fold(unsigned* base, int k, float v)
+// (v: the slot's value; an fp32 value converts exactly, and slots 6..15 only ever receive fp32 or integer values)
+__device__ __forceinline__ void acc_fold(unsigned* base, int k, double v)
 {
     unsigned long long* w = acc_slot(base, k);
     unsigned* w32 = reinterpret_cast<unsigned*>(w);
     if (k < 6) {
-        const double d = (double)v * kAccScale;
-        if (fabs(d) < 0x1p62)
-            __hip_atomic_fetch_add(w, (unsigned long long)__double2ll_rn(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
+        const double sv = v * 0x1p20;
+        if (fabs(sv) < 0x1p61) {
+            const double h = floor(sv);
+            const long long l = __double2ll_rn((sv - h) * 0x1p32);
+            __hip_atomic_fetch_add(w, (unsigned long long)(long long)h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(acc_slot(base, kAccReactLo + k), (unsigned long long)l, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else {
             __hip_atomic_fetch_or(reinterpret_cast<unsigned*>(acc_slot(base, kListAccSlots)), 1u, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
     } else if (k == 6 || k == 8 || k == 15) {
         __hip_atomic_fetch_add(w, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (k == 7) {
-        __hip_atomic_fetch_max(w32, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(w32, __float_as_uint((float)v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (k < 12) {
-        __hip_atomic_fetch_min(w32, ordered_bits(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_min(w32, ordered_bits((float)v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-        __hip_atomic_fetch_max(w32, ordered_bits(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(w32, ordered_bits((float)v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 // the final workgroup (all threads): read every group's accumulators (device-coherent loads), combine them (integer
@@ -2746,20 +2826,28 @@ __device__ void list_totals(unsigned* base, int ngroups, ListTotals& t)
     }
     __syncthreads();
     if (tid != 0) return;
-    unsigned long long v[kAccWords];
-    for (int k = 0; k < kAccWords; ++k) v[k] = s_acc[k];
+    // two passes over the groups (slots 0..15, then the low reaction words and the flag), so no more than 16 words
+    // and their operands are live at once
+    unsigned long long v[kAccReactLo];
+    for (int k = 0; k < kAccReactLo; ++k) v[k] = s_acc[k];
     for (int g = 1; g < ngroups; ++g) {
         const unsigned long long* x = s_acc + g * kAccWords;
-        for (int k = 0; k < kAccWords; ++k) {
+        for (int k = 0; k < kAccReactLo; ++k) {
             if (k <= 6 || k == 8 || k == 15) v[k] += x[k];
             else if (k >= 9 && k < 12) v[k] = min((unsigned)v[k], (unsigned)x[k]);
-            else if (k == kListAccSlots) v[k] |= x[k];
             else v[k] = max((unsigned)v[k], (unsigned)x[k]);
         }
     }
-    const bool bad = (v[kListAccSlots] & 1ull) != 0;
-    for (int k = 0; k < 6; ++k) t.react[k] = bad ? __longlong_as_double(0x7ff8000000000000ll)
-                                                  : (double)(long long)v[k] / kAccScale;
+    unsigned long long lo[6], bad = 0;
+    for (int k = 0; k < 6; ++k) lo[k] = 0;
+    for (int g = 0; g < ngroups; ++g) {
+        const unsigned long long* x = s_acc + g * kAccWords;
+        for (int k = 0; k < 6; ++k) lo[k] += x[kAccReactLo + k];
+        bad |= x[kListAccSlots];
+    }
+    for (int k = 0; k < 6; ++k)
+        t.react[k] = (bad & 1ull) ? __longlong_as_double(0x7ff8000000000000ll)
+                                  : (double)(long long)v[k] * 0x1p-20 + (double)(long long)lo[k] * 0x1p-52;
     t.nbr = (double)v[6];
     t.ld = __uint_as_float((unsigned)v[7]);
     t.nfb = (long long)v[8];
@@ -2859,23 +2947,23 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
 }
 
 // the mixed soft-core pair force of one partner (the tile kernel's phase-2 arithmetic, in the global frame)
-__device__ __forceinline__ void list_pair(float xi, float yi, float zi, float4 q, float2 t, float ahi, float bhi,
-                                          float kA, float kB, float k2a, float k2b, float rc2, bool real, float& fx,
-                                          float& fy, float& fz, float& nbr)
+template <typename R>
+__device__ __forceinline__ void list_pair(R xi, R yi, R zi, real4<R> q, real2<R> t, R ahi, R bhi, R kA, R kB, R k2a,
+                                          R k2b, R rc2, bool real, R& fx, R& fy, R& fz, R& nbr)
 {
-    const float dx = xi - q.x, dy = yi - q.y, dz = zi - q.z;
-    const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-    const float ga = fmaxf(fmaf(-k2a, r2, 1.f), 0.f);
-    const float tt = r2 * k2b;
-    const float t2 = tt * tt;
-    const float gb = fmaxf(fmaf(-t2, t2, 1.f), 0.f);
-    const float A = fmaf(kA, t.x, ahi), B = fmaf(kB, t.y, bhi);
+    const R dx = xi - q.x, dy = yi - q.y, dz = zi - q.z;
+    const R r2 = r_fma(dz, dz, r_fma(dy, dy, dx * dx));
+    const R ga = r_fmax(r_fma(-k2a, r2, R(1)), R(0));
+    const R tt = r2 * k2b;
+    const R t2 = tt * tt;
+    const R gb = r_fmax(r_fma(-t2, t2, R(1)), R(0));
+    const R A = r_fma(kA, t.x, ahi), B = r_fma(kB, t.y, bhi);
     const bool in = real && r2 < rc2;
-    const float coef = in ? fmaf(A, ga * ga, B * (gb * gb * t2 * tt)) : 0.f;
-    fx = fmaf(coef, dx, fx);
-    fy = fmaf(coef, dy, fy);
-    fz = fmaf(coef, dz, fz);
-    nbr += in ? 1.f : 0.f;
+    const R coef = in ? r_fma(A, ga * ga, B * (gb * gb * t2 * tt)) : R(0);
+    fx = r_fma(coef, dx, fx);
+    fy = r_fma(coef, dy, fy);
+    fz = r_fma(coef, dz, fz);
+    nbr += in ? R(1) : R(0);
 }
 
 
@@ -2889,6 +2977,12 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 
 #ifndef GCS_LIST_WAVES_PER_EU_CT
 #define GCS_LIST_WAVES_PER_EU_CT 4  // the contact-step instantiation (CT, 1 launch in 20): 4 -> <= 128, no spills
+#endif
+#ifndef GCS_LIST_WAVES_PER_EU64
+#define GCS_LIST_WAVES_PER_EU64 4  // the fp64 step: every position / force register is a pair -> <= 128 VGPRs
+#endif
+#ifndef GCS_LIST_UNROLL64
+#define GCS_LIST_UNROLL64 8  // fp64 step: list entries per batch of the pair loop
 #endif
 // One list step: ONE tile of 64 consecutive slots per workgroup (the launch has one workgroup per tile), W waves.
 // Phases, with nothing but LDS carried from one to the next (every wave's registers are free for the next phase):
@@ -2904,12 +2998,18 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 // DOM (decomposed): a slot is integrated only when it belongs to this build (s < ctx->lnslots) and its
 // particle lies in the domain's box at the step start; the final workgroup writes the local reduction to a.dom_red
 // (the tail runs after the allreduce: k_ldom_tail)
-template <typename LE, int W, bool CT, bool DOM = false>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS_LIST_WAVES_PER_EU_CT : GCS_LIST_WAVES_PER_EU))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int flags)
+// R: the arithmetic precision (GCS_PRECISION_F32 / F64).  Positions, forces, the integration, the pair test and the
+// contact predicate are in R; the list bookkeeping (build positions, displacements, cell ranges, bbox) is fp32 with
+// margins (a partner within the cutoff in R is always in the list or found by the exact search: the skin test keeps
+// 0.1 % of the skin, ~1e-4, against fp32 roundings of ~1e-6 of the coordinates).
+template <typename LE, int W, bool CT, bool DOM = false, typename R = float>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS_LIST_WAVES_PER_EU_CT : (sizeof(R) == 8 ? GCS_LIST_WAVES_PER_EU64 : GCS_LIST_WAVES_PER_EU)))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int flags)
 {
-    __shared__ float red[W][4][kTile];
-    __shared__ float4 s_locf[kTile], s_locr[kTile], s_loco[kTile], s_noise[kTile];
-    __shared__ float2 s_tab[kMaxTypes];
+    using R4 = real4<R>;
+    using R2 = real2<R>;
+    __shared__ R red[W][4][kTile];
+    __shared__ R4 s_locf[kTile], s_locr[kTile], s_loco[kTile], s_noise[kTile];
+    __shared__ R2 s_tab[kMaxTypes];
     __shared__ int s_last, s_final;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = uniform(tid >> 6);
@@ -2918,15 +3018,16 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     unsigned long long* const dbg = a.dbg_times ? a.dbg_times + 8 * blockIdx.x : nullptr;
     if (dbg && tid == 0) dbg[0] = wall_clock64();
     const int n = a.n;
+    const FieldPrm<R>& P = St<R>::prm(a);
     const int tile = xcd_block(blockIdx.x, gridDim.x);
     const int s = tile * kTile + lane;
     const bool valid = s < n;
     const int sl = valid ? s : n - 1;
     const int par = a.par_hint >= 0 ? a.par_hint : ctx->parity;
-    const float4* __restrict__ qc = par ? a.psort1 : a.psort0;  // slot order (pair partners)
+    const R4* __restrict__ qc = St<R>::psort(a, par);  // slot order (pair partners)
     const int cap = a.list_cap;
     const size_t stride = (size_t)a.list_stride;
-    constexpr int kU = GCS_LIST_UNROLL;
+    constexpr int kU = sizeof(R) == 4 ? GCS_LIST_UNROLL : GCS_LIST_UNROLL64;
     constexpr int kE = 8 / (int)sizeof(LE);  // entries per 8-byte list word
     constexpr int kW = kU / kE;              // list words per batch
     static_assert(kU % kE == 0, "a batch is whole list words");
@@ -2934,54 +3035,60 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     const uint2* __restrict__ segw = reinterpret_cast<const uint2*>(a.list) + (size_t)wave * (cap / kE) * stride + sl;
 
     // 1. slot loads (one round trip; the type table's load beside them)
-    for (int t = tid; t < a.ntypes; t += blockDim.x) s_tab[t] = a.type_ab[t];
-    const float4 pi = qc[sl];
+    const R2* __restrict__ tab = St<R>::type_ab(a);
+    for (int t = tid; t < a.ntypes; t += blockDim.x) s_tab[t] = tab[t];
+    const R4 pi = qc[sl];
     const float4 pb = a.spos[sl];
     const int cw = a.lcount[(size_t)wave * stride + sl];
     uint2 e[kW];
 #pragma unroll
     for (int j = 0; j < kW; ++j) e[j] = segw[(size_t)j * stride];  // list_cap >= kU: in bounds
-    const float cs = (float)ctx->cs;
+    const R cs = (R)ctx->cs;
     const float D = ctx->ldisp;
     const float lrc_b = ctx->lrc_b;
     // the contact distance from the context (k_set_contact before the launch), so a captured graph serves any update
-    const float cd2 = CT ? ctx->contact_d2 : 0.f;
+    R cd2 = R(0);
+    if constexpr (CT) {
+        if constexpr (sizeof(R) == 4) cd2 = ctx->contact_d2; else cd2 = ctx->contact_d2_64;
+    }
     __syncthreads();  // s_tab
 
-    const int pk = __float_as_int(pi.w);
+    const int pk = wbits(pi.w);
     const int i = pk & kIdx;
-    const bool act = DOM ? (valid && s < ctx->lnslots && box_has(a.dom, pi.x, pi.y, pi.z)) : valid;
-    const float scale = a.pair_scaled ? cs : 1.f;
-    const float sa = a.pa_sig * scale, sbb = a.pb_sig * scale;
-    const float k2a = 1.f / (sa * sa), k2b = 1.f / (sbb * sbb);
-    const float kA = 0.5f * 6.f * a.pa_eps * k2a, kB = 0.5f * 24.f * a.pb_eps * k2b;
-    const float rc = pair_cutoff(a, (double)cs), rc2 = rc * rc;
+    const bool act = DOM ? (valid && s < ctx->lnslots && box_has(a.dom, (float)pi.x, (float)pi.y, (float)pi.z)) : valid;
+    const R scale = a.pair_scaled ? cs : R(1);
+    const R sa = P.pa_sig * scale, sbb = P.pb_sig * scale;
+    const R k2a = R(1) / (sa * sa), k2b = R(1) / (sbb * sbb);
+    const R kA = R(0.5) * R(6) * P.pa_eps * k2a, kB = R(0.5) * R(24) * P.pb_eps * k2b;
+    const R rc = pair_cutoff_r<R>(a, (double)cs), rc2 = rc * rc;
+    const float rcf = (float)rc;
     // a particle whose own displacement exceeds this may miss a partner in its list (0.999: fp32 margin)
-    const float slack = 0.999f * a.list_skin - D - fmaxf(rc - lrc_b, 0.f);
-    const float ex = pi.x - pb.x, ey = pi.y - pb.y, ez = pi.z - pb.z;
+    const float slack = 0.999f * a.list_skin - D - fmaxf(rcf - lrc_b, 0.f);
+    const float ex = (float)(pi.x - (R)pb.x), ey = (float)(pi.y - (R)pb.y), ez = (float)(pi.z - (R)pb.z);
     const float di = sqrtf(fmaf(ez, ez, fmaf(ey, ey, ex * ex)));
     const bool fb = act && (di > slack || (cw & kListOverflow) != 0);
     // contacts (CT): the lists must cover the contact distance; a particle whose list does not is searched for its
     // contacts only (its forces take exactly the path they take without contacts: identical bits)
-    const float rcc = CT ? fmaxf(rc, sqrtf(cd2)) : rc;
+    const float rcc = CT ? fmaxf(rcf, sqrtf((float)cd2)) : rcf;
     const bool fbc = CT && valid && (di > 0.999f * a.list_skin - D - fmaxf(rcc - lrc_b, 0.f) || (cw & kListOverflow) != 0);
 
     // 2. the particle-local terms (a dependent-gather chain: first, on the last wave), parked in LDS
     if (wave == W - 1) {
-        const float4 km = a.skmu[sl];
+        const R4 km = St<R>::skmu(a)[sl];
         const int2 erow = a.sbrow[sl];
-        float lfx = 0.f, lfy = 0.f, lfz = 0.f, en[kEnergyKinds];
-        float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
-        local_terms<kModeStep, GCS_LIST_BOND_BATCH>(ctx, a, i, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout, erow);
-        s_locf[lane] = make_float4(lfx, lfy, lfz, km.x);
-        s_locr[lane] = make_float4(act ? rin[0] : 0.f, act ? rin[1] : 0.f, act ? rin[2] : 0.f, 0.f);
-        s_loco[lane] = make_float4(act ? rout[0] : 0.f, act ? rout[1] : 0.f, act ? rout[2] : 0.f, 0.f);
+        R lfx = 0, lfy = 0, lfz = 0, en[kEnergyKinds];
+        R rin[3] = {0, 0, 0}, rout[3] = {0, 0, 0};
+        local_terms<kModeStep, GCS_LIST_BOND_BATCH, R>(ctx, a, i, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout,
+                                                       erow);
+        s_locf[lane] = mk4<R>(lfx, lfy, lfz, km.x);
+        s_locr[lane] = mk4<R>(act ? rin[0] : R(0), act ? rin[1] : R(0), act ? rin[2] : R(0), R(0));
+        s_loco[lane] = mk4<R>(act ? rout[0] : R(0), act ? rout[1] : R(0), act ? rout[2] : R(0), R(0));
     }
 
     // 3. the wave's list segment
-    float fx = 0.f, fy = 0.f, fz = 0.f, nbr = 0.f;
-    const float2 own = s_tab[(unsigned)pk >> kListIndexBits];
-    const float ahi = kA * own.x, bhi = kB * own.y;
+    R fx = 0, fy = 0, fz = 0, nbr = 0;
+    const R2 own = s_tab[(unsigned)pk >> kListIndexBits];
+    const R ahi = kA * own.x, bhi = kB * own.y;
     if (dbg && tid == 0) dbg[1] = wall_clock64();
     if (a.has_pair) {
         const int cnt = (act && !fb) ? min(cw & kListCountMask, cap) : 0;
@@ -2990,7 +3097,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         // return right behind the gathers, so each batch costs one round trip), then the pair forces (and contacts)
         const int klast = (cap / kU - 1) * kU;  // the segment's last batch (list_cap is a multiple of kU)
         for (int k0 = 0; k0 < kmax; k0 += kU) {
-            float4 q[kU];
+            R4 q[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) q[u] = qc[(k0 + u < cnt) ? list_entry<LE>(e, u) : sl];
             const int kn = min(k0 + kU, klast);
@@ -2999,12 +3106,12 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
             __builtin_amdgcn_sched_barrier(0);  // keep the entry loads here, ahead of the arithmetic
 #pragma unroll
             for (int u = 0; u < kU; ++u)
-                list_pair(pi.x, pi.y, pi.z, q[u], s_tab[(unsigned)__float_as_int(q[u].w) >> kListIndexBits], ahi, bhi,
-                          kA, kB, k2a, k2b, rc2, k0 + u < cnt, fx, fy, fz, nbr);
+                list_pair<R>(pi.x, pi.y, pi.z, q[u], s_tab[(unsigned)wbits(q[u].w) >> kListIndexBits], ahi, bhi, kA,
+                             kB, k2a, k2b, rc2, k0 + u < cnt, fx, fy, fz, nbr);
             if constexpr (CT) {
 #pragma unroll
                 for (int u = 0; u < kU; ++u)
-                    if (!fbc && k0 + u < cnt) list_contact(a, cd2, pi, q[u], i, __float_as_int(q[u].w) & kIdx);
+                    if (!fbc && k0 + u < cnt) list_contact<R>(a, cd2, pi, q[u], i, wbits(q[u].w) & kIdx);
             }
         }
         // exact search of the build's cell list for the particles the lists may not cover: a partner within rc
@@ -3014,17 +3121,18 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         unsigned long long fbm = __ballot(fb);
         if (fbm) {
             const Grid lg = ctx->lgrid;
-            const float R = rc + D + 1.0e-5f * (rc + D);
+            const float Rr = rcf + D + 1.0e-5f * (rcf + D);
             while (fbm) {
                 const int L = __ffsll((long long)fbm) - 1;
                 fbm &= fbm - 1ull;
-                const float px = __shfl(pi.x, L), py = __shfl(pi.y, L), pz = __shfl(pi.z, L);
-                const float pah = __shfl(ahi, L), pbh = __shfl(bhi, L);
+                const R px = __shfl(pi.x, L), py = __shfl(pi.y, L), pz = __shfl(pi.z, L);
+                const R pah = __shfl(ahi, L), pbh = __shfl(bhi, L);
                 const int sL = uniform(__shfl(s, L));
-                const int x0 = uniform(lgrid_cell(lg, 0, px - R)), x1 = uniform(lgrid_cell(lg, 0, px + R));
-                const int y0 = uniform(lgrid_cell(lg, 1, py - R)), y1 = uniform(lgrid_cell(lg, 1, py + R));
-                const int z0 = uniform(lgrid_cell(lg, 2, pz - R)), z1 = uniform(lgrid_cell(lg, 2, pz + R));
-                float gx = 0.f, gy = 0.f, gz = 0.f, gn = 0.f;
+                const float fpx = (float)px, fpy = (float)py, fpz = (float)pz;
+                const int x0 = uniform(lgrid_cell(lg, 0, fpx - Rr)), x1 = uniform(lgrid_cell(lg, 0, fpx + Rr));
+                const int y0 = uniform(lgrid_cell(lg, 1, fpy - Rr)), y1 = uniform(lgrid_cell(lg, 1, fpy + Rr));
+                const int z0 = uniform(lgrid_cell(lg, 2, fpz - Rr)), z1 = uniform(lgrid_cell(lg, 2, fpz + Rr));
+                R gx = 0, gy = 0, gz = 0, gn = 0;
                 int row = 0;
                 for (int z = z0; z <= z1; ++z)
                     for (int y = y0; y <= y1; ++y, ++row) {
@@ -3032,15 +3140,15 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
                         const int base = (z * lg.n[1] + y) * lg.n[0];
                         const int t0 = a.cstart[base + x0], t1 = a.cstart[base + x1 + 1];
                         for (int t = t0 + lane; t < t1; t += kTile) {
-                            const float4 q = qc[t];
-                            list_pair(px, py, pz, q, s_tab[(unsigned)__float_as_int(q.w) >> kListIndexBits], pah, pbh,
-                                      kA, kB, k2a, k2b, rc2, t != sL, gx, gy, gz, gn);
+                            const R4 q = qc[t];
+                            list_pair<R>(px, py, pz, q, s_tab[(unsigned)wbits(q.w) >> kListIndexBits], pah, pbh, kA, kB,
+                                         k2a, k2b, rc2, t != sL, gx, gy, gz, gn);
                         }
                     }
-                gx = wave_sum(gx);
-                gy = wave_sum(gy);
-                gz = wave_sum(gz);
-                gn = wave_sum(gn);
+                gx = wave_sum_r(gx);
+                gy = wave_sum_r(gy);
+                gz = wave_sum_r(gz);
+                gn = wave_sum_r(gn);
                 if (lane == L) {
                     fx += gx;
                     fy += gy;
@@ -3056,15 +3164,16 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         unsigned long long fcm = __ballot(fbc);
         if (fcm) {
             const Grid lg = ctx->lgrid;
-            const float R = rcc + D + 1.0e-5f * (rcc + D);
+            const float Rr = rcc + D + 1.0e-5f * (rcc + D);
             while (fcm) {
                 const int L = __ffsll((long long)fcm) - 1;
                 fcm &= fcm - 1ull;
-                const float4 pL = make_float4(__shfl(pi.x, L), __shfl(pi.y, L), __shfl(pi.z, L), 0.f);
+                const R4 pL = mk4<R>(__shfl(pi.x, L), __shfl(pi.y, L), __shfl(pi.z, L), R(0));
                 const int iL = __shfl(i, L), sL = uniform(__shfl(s, L));
-                const int x0 = uniform(lgrid_cell(lg, 0, pL.x - R)), x1 = uniform(lgrid_cell(lg, 0, pL.x + R));
-                const int y0 = uniform(lgrid_cell(lg, 1, pL.y - R)), y1 = uniform(lgrid_cell(lg, 1, pL.y + R));
-                const int z0 = uniform(lgrid_cell(lg, 2, pL.z - R)), z1 = uniform(lgrid_cell(lg, 2, pL.z + R));
+                const float fpx = (float)pL.x, fpy = (float)pL.y, fpz = (float)pL.z;
+                const int x0 = uniform(lgrid_cell(lg, 0, fpx - Rr)), x1 = uniform(lgrid_cell(lg, 0, fpx + Rr));
+                const int y0 = uniform(lgrid_cell(lg, 1, fpy - Rr)), y1 = uniform(lgrid_cell(lg, 1, fpy + Rr));
+                const int z0 = uniform(lgrid_cell(lg, 2, fpz - Rr)), z1 = uniform(lgrid_cell(lg, 2, fpz + Rr));
                 int row = 0;
                 for (int z = z0; z <= z1; ++z)
                     for (int y = y0; y <= y1; ++y, ++row) {
@@ -3072,8 +3181,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
                         const int base = (z * lg.n[1] + y) * lg.n[0];
                         const int t0 = a.cstart[base + x0], t1 = a.cstart[base + x1 + 1];
                         for (int t = t0 + lane; t < t1; t += kTile) {
-                            const float4 q = qc[t];
-                            if (t != sL) list_contact(a, cd2, pL, q, iL, __float_as_int(q.w) & kIdx);
+                            const R4 q = qc[t];
+                            if (t != sL) list_contact<R>(a, cd2, pL, q, iL, wbits(q.w) & kIdx);
                         }
                     }
             }
@@ -3085,9 +3194,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     red[wave][2][lane] = fz;
     red[wave][3][lane] = nbr;
     if (wave == (W > 1 ? 1 : 0)) {  // the noise (depends on the particle and the step only) off wave 0's path
-        float n0, n1, n2;
-        noise3(a, ctx, i, n0, n1, n2);
-        s_noise[lane] = make_float4(n0, n1, n2, 0.f);
+        R n0, n1, n2;
+        noise3<R>(a, ctx, i, n0, n1, n2);
+        s_noise[lane] = mk4<R>(n0, n1, n2, R(0));
     }
     __syncthreads();
     if (dbg && tid == 0) dbg[3] = wall_clock64();
@@ -3097,7 +3206,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     const int g = blockIdx.x % ngroups;
     unsigned* const acc = a.lticket + kListAccBase + 32 * kAccWords * g;
     if (wave == 0) {
-        float fsx = red[0][0][lane], fsy = red[0][1][lane], fsz = red[0][2][lane], ns = red[0][3][lane];
+        R fsx = red[0][0][lane], fsy = red[0][1][lane], fsz = red[0][2][lane], ns = red[0][3][lane];
 #pragma unroll
         for (int w = 1; w < W; ++w) {
             fsx += red[w][0][lane];
@@ -3105,41 +3214,42 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
             fsz += red[w][2][lane];
             ns += red[w][3][lane];
         }
-        const float4 lf = s_locf[lane];
+        const R4 lf = s_locf[lane];
         fsx += lf.x;
         fsy += lf.y;
         fsz += lf.z;
-        const float mu = lf.w;
+        const R mu = lf.w;
         // Euler-Maruyama: x += mu dt F + sqrt(2 T mu dt) xi
-        const float4 xi = s_noise[lane];
-        const float dt = a.timestep;
-        const float amp = sqrtf(2.f * a.temperature * mu * dt);
-        const float mdt = mu * dt;
-        const float nxp = pi.x + mdt * fsx + amp * xi.x;
-        const float nyp = pi.y + mdt * fsy + amp * xi.y;
-        const float nzp = pi.z + mdt * fsz + amp * xi.z;
+        const R4 xi = s_noise[lane];
+        const R dt = P.timestep;
+        const R amp = r_sqrt(R(2) * P.temperature * mu * dt);
+        const R mdt = mu * dt;
+        const R nxp = pi.x + mdt * fsx + amp * xi.x;
+        const R nyp = pi.y + mdt * fsy + amp * xi.y;
+        const R nzp = pi.z + mdt * fsz + amp * xi.z;
         if (act) {
-            float4* __restrict__ pn = par ? a.pos0 : a.pos1;  // particle order (bonded partners read ctx->parity's)
-            float4* __restrict__ qn = par ? a.psort0 : a.psort1;
-            pn[i] = make_float4(nxp, nyp, nzp, 0.f);
-            qn[s] = make_float4(nxp, nyp, nzp, pi.w);
+            R4* __restrict__ pn = St<R>::pos(a, par ^ 1);  // particle order (bonded partners read ctx->parity's)
+            R4* __restrict__ qn = St<R>::psort(a, par ^ 1);
+            pn[i] = mk4<R>(nxp, nyp, nzp, R(0));
+            qn[s] = mk4<R>(nxp, nyp, nzp, pi.w);
         }
         if (dbg && tid == 0) dbg[4] = wall_clock64();
-        const float gx = nxp - pb.x, gy = nyp - pb.y, gz = nzp - pb.z;
+        // the list bookkeeping in fp32: the displacement from the build and the bbox of the roundings
+        const float fnx = (float)nxp, fny = (float)nyp, fnz = (float)nzp;
+        const float gx = (float)(nxp - (R)pb.x), gy = (float)(nyp - (R)pb.y), gz = (float)(nzp - (R)pb.z);
         const float dmax = wave_max(act ? sqrtf(fmaf(gz, gz, fmaf(gy, gy, gx * gx))) : 0.f);
         const float nfb = (float)__popcll(__ballot(fb));
         const float nact = DOM ? (float)__popcll(__ballot(act)) : 0.f;  // (ballots outside the lane branches)
-        float v = 0.f;  // lane k: the value of accumulator slot k this wave owns
+        double v = 0.0;  // lane k: the value of accumulator slot k this wave owns
         if (flags & kLFlagStats) {
-            const float nt = wave_sum(act ? ns : 0.f);
-            if (lane == 6) v = nt;
+            const R nt = wave_sum_r(act ? ns : R(0));
+            if (lane == 6) v = (double)nt;
         }
         if (flags & kLFlagBBox) {
             const float big = 3.0e38f;
-            const float l0 = wave_min(act ? nxp : big), l1 = wave_min(act ? nyp : big),
-                        l2 = wave_min(act ? nzp : big);
-            const float h0 = wave_max(act ? nxp : -big), h1 = wave_max(act ? nyp : -big),
-                        h2 = wave_max(act ? nzp : -big);
+            const float l0 = wave_min(act ? fnx : big), l1 = wave_min(act ? fny : big), l2 = wave_min(act ? fnz : big);
+            const float h0 = wave_max(act ? fnx : -big), h1 = wave_max(act ? fny : -big),
+                        h2 = wave_max(act ? fnz : -big);
             v = lane == 9 ? l0 : lane == 10 ? l1 : lane == 11 ? l2 : lane == 12 ? h0 : lane == 13 ? h1 : lane == 14 ? h2 : v;
         }
         if (lane == 7) v = dmax;
@@ -3152,13 +3262,13 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         // the wall reactions: waves 1.. take the six components in turn (W = 4: wave 1 inward, wave 2 outward)
         const int c0 = W > 2 ? 3 * (wave - 1) : 0, c1 = W > 2 ? c0 + 3 : 6;
         if (c0 < 6) {
-            float v = 0.f;
+            R v = 0;
             for (int c = c0; c < c1; ++c) {
-                const float4 r = c < 3 ? s_locr[lane] : s_loco[lane];
-                const float x = wave_sum((c % 3) == 0 ? r.x : (c % 3) == 1 ? r.y : r.z);
+                const R4 r = c < 3 ? s_locr[lane] : s_loco[lane];
+                const R x = wave_sum_r((c % 3) == 0 ? r.x : (c % 3) == 1 ? r.y : r.z);
                 if (lane == c) v = x;
             }
-            if (lane >= c0 && lane < c1) acc_fold(acc, lane, v);
+            if (lane >= c0 && lane < c1) acc_fold(acc, lane, (double)v);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's accumulator atomics are performed
@@ -3273,18 +3383,24 @@ __device__ inline bool strict_pair(float4 p, float4 q, float rc2)
     return r2 < rc2;
 }
 
-template <bool EMIT>
+// F64: the predicate in fp64 on pos64 (the fp64 engine's positions, or fp64 query points) with d2 = d64 * d64; the
+// cells (fp32 roundings, edge >= distance * (1 + 1e-4)) still hold every candidate
+template <bool EMIT, bool F64>
 __global__ __launch_bounds__(256) void k_search(const DevCtx* __restrict__ ctx, int n, const float4* __restrict__ spos,
                                                 const int* __restrict__ sidx, const int* __restrict__ scell,
                                                 const int* __restrict__ cstart, int* __restrict__ counts,
-                                                const int* __restrict__ offsets, unsigned long long* __restrict__ keys)
+                                                const int* __restrict__ offsets, unsigned long long* __restrict__ keys,
+                                                const double4* __restrict__ pos64, double d64)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
     const Grid g = ctx->grid;
     const float rc2 = __fmul_rn(g.rc, g.rc);
+    const double d2 = __dmul_rn(d64, d64);
     const int i = sidx[s];
     const float4 p = spos[s];
+    double4 p64 = make_double4(0.0, 0.0, 0.0, 0.0);
+    if constexpr (F64) p64 = pos64[i];
     const int c = scell[s];
     const int nx = g.n[0], ny = g.n[1], nz = g.n[2];
     const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
@@ -3297,7 +3413,12 @@ __global__ __launch_bounds__(256) void k_search(const DevCtx* __restrict__ ctx, 
             for (int t = jb; t < je; ++t) {
                 const int j = sidx[t];
                 if (j <= i) continue;
-                if (!strict_pair(p, spos[t], rc2)) continue;
+                if constexpr (F64) {
+                    const double4 q = pos64[j];
+                    if (!strict_lt(p64.x, p64.y, p64.z, q.x, q.y, q.z, d2)) continue;
+                } else {
+                    if (!strict_pair(p, spos[t], rc2)) continue;
+                }
                 if (EMIT) keys[o++] = ((unsigned long long)(unsigned)i << 32) | (unsigned)j;
                 cnt++;
             }
@@ -3332,385 +3453,138 @@ __global__ __launch_bounds__(1024) void k_scan_small(const int* __restrict__ in,
     }
 }
 
+
 // ----------------------------------------------------------------------------------------------------
-// small systems (N <= kSmallMax: the mitotic stages' 586 / 1,172 particles of C3, the 1,002 of C1): ONE workgroup
-// runs a whole chunk of steps -- no kernel boundary, no grid-wide reduction, no atomics on the step path.  The
-// system lives in LDS (positions, per-particle constants, an LDS copy of the context); a step is: [list rebuild when
-// the skin is used up] -> forces of every particle from its neighbour list + the particle-local terms -> block
-// reductions (reactions, largest displacement) -> Euler-Maruyama update in LDS -> the schedule / wall ODE by thread
-// 0 (list_tail_apply on the LDS context).  At this size the multi-workgroup list step spends ~12 us per step on
-// launch, memory round trips and its cross-workgroup tail for ~10 workgroups of work.
-//
-// Neighbour lists (Verlet, the list step's skin): every partner within cutoff + skin of a particle at the build,
-// u16 particle indices in global memory [k][N], in the order of a cell scan of the build (cells ordered by
-// particle index: deterministic); rebuilt when 2 D + (cutoff growth) reaches 0.999 skin (D: the largest
-// displacement of any particle since the build, reduced every step), so a pair within the cutoff is always in the
-// lists -- the pair set is exact.  The build state (lists, build positions, the build's cell list, the context's
-// lgrid / lrc_b / ldisp) persists across launches: a chunked run rebuilds where one long run does (bitwise
-// identical).  A particle whose list overflowed kSmallCap is evaluated by a scan of the build's cells (exact by
-// the same bound).
+// fp64 force / energy evaluation (GCS_PRECISION_F64: md::system::compute_energy / the force pass of a spacestep
+// relaxation step, simulation_driver_relaxation.cpp:48-55, and gcs_engine_compute_forces).  Not on the fixed-timestep
+// step path (that is k_lstep<..., double>), so it is written for clarity: one thread per cell-sorted slot, a gather
+// of every candidate of the 3 x 3 neighbouring cell rows (x within +-fx cells) by particle index, the pair potential
+// in fp64 with the pair's mean (a, b) factors, then the fp64 particle-local terms.  Partial rows per block are
+// reduced in a fixed order (k_red64 / the host): bitwise reproducible.
+constexpr int kEval64Block = 256;
 
-struct SmallArgs {
-    long long first_step;
-    int steps;
-    int flags;          // kLFlagSched | kLFlagStats
-    int force_build;    // the chunk starts without continuity: build before its first step
-    float skin;
-    unsigned short* list;   // [kSmallCap][N]
-    int* lcount;            // [N] count | kListOverflow
-    float4* bpos;           // [N] positions at the build
-    int* cstart;            // [kSmallCells + 1] the build's cell starts
-    unsigned short* cidx;   // [N] particles ordered by cell (index order inside a cell)
-    unsigned long long* dbg;  // optional (GCS_DEBUG_SMALL): thread 0's wall-clock totals per phase
-};
-
-constexpr int kSmallThreads = 1024;
-constexpr int kSmallWaves = kSmallThreads / 64;
-
-// block totals in one pass: K values per thread, value k summed, or maxed (bit k of MAXM), or minned (bit k of
-// MINM) -> thread 0, in a fixed order (DPP wave reductions, waves in index order); one barrier
-template <int K, unsigned MAXM, unsigned MINM>
-__device__ __forceinline__ void small_totals(float* v, float (*s_tmp)[kSmallWaves])
+template <int MODE>
+__global__ __launch_bounds__(kEval64Block) void k_eval64(const DevCtx* __restrict__ ctx, ForceArgs a)
 {
+    __shared__ double s_red[kEnergyKinds][kEval64Block / 64];
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const Grid g = ctx->grid;
+    const bool valid = s < a.n && s < a.cstart[g.ncell];
+    const int sl = valid ? s : 0;
+    const int i = a.sidx[sl];
+    const double4* __restrict__ pos = St<double>::pos(a, ctx->parity);
+    const double4 p = pos[i];
+    const double4 km = a.dkmu[i];
+    const FieldPrm<double>& P = a.pd;
+    double fx = 0, fy = 0, fz = 0, ep = 0, nbr = 0;
+    if (valid && a.has_pair) {
+        const double cs = ctx->cs;
+        const double scale = a.pair_scaled ? cs : 1.0;
+        const double sa = P.pa_sig * scale, sbb = P.pb_sig * scale;
+        const double k2a = 1.0 / (sa * sa), k2b = 1.0 / (sbb * sbb);
+        const double rc = pair_cutoff_r<double>(a, cs), rc2 = rc * rc;
+        const double ai = a.pair_mix ? km.y : 1.0, bi = a.pair_mix ? km.z : 0.0;
+        const int c = a.scell[s];
+        const int nx = g.n[0], ny = g.n[1], nz = g.n[2];
+        const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
+        for (int z = max(cz - 1, 0); z <= min(cz + 1, nz - 1); ++z)
+            for (int y = max(cy - 1, 0); y <= min(cy + 1, ny - 1); ++y) {
+                const int base = (z * ny + y) * nx;
+                const int jb = a.cstart[base + max(cx - g.fx, 0)], je = a.cstart[base + min(cx + g.fx, nx - 1) + 1];
+                for (int t = jb; t < je; ++t) {
+                    if (t == s) continue;
+                    const int j = a.sidx[t];
+                    const double4 q = pos[j];
+                    const double dx = p.x - q.x, dy = p.y - q.y, dz = p.z - q.z;
+                    const double r2 = fma(dz, dz, fma(dy, dy, dx * dx));
+                    if (!(r2 < rc2)) continue;
+                    const double4 kj = a.dkmu[j];
+                    const double A = a.pair_mix ? 0.5 * (ai + kj.y) : 1.0, B = a.pair_mix ? 0.5 * (bi + kj.z) : 0.0;
+                    const double ga = fmax(1.0 - k2a * r2, 0.0);
+                    const double tt = r2 * k2b, t2 = tt * tt;
+                    const double gb = fmax(1.0 - t2 * t2, 0.0);
+                    if (MODE == kModeEnergy) {
+                        // each pair from both ends: half its energy here
+                        ep += 0.5 * (A * P.pa_eps * ga * ga * ga + B * P.pb_eps * gb * gb * gb);
+                    } else {
+                        const double coef = A * 6.0 * P.pa_eps * k2a * ga * ga + B * 24.0 * P.pb_eps * k2b * gb * gb * t2 * tt;
+                        fx = fma(coef, dx, fx);
+                        fy = fma(coef, dy, fy);
+                        fz = fma(coef, dz, fz);
+                        nbr += 1.0;
+                    }
+                }
+            }
+    }
+    double en[kEnergyKinds] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double rin[3] = {0, 0, 0}, rout[3] = {0, 0, 0};
+    // every lane calls it (the droplet term is wave-cooperative); invalid lanes' results are dropped below
+    local_terms<MODE, 1, double>(ctx, a, i, p.x, p.y, p.z, km, fx, fy, fz, en, rin, rout);
+    double v[kEnergyKinds];
+    if (MODE == kModeEnergy) {
+        en[0] = ep;
+        for (int k = 0; k < kEnergyKinds; ++k) v[k] = valid ? en[k] : 0.0;
+    } else {
+        if (valid) St<double>::force(a)[i] = make_double4(fx, fy, fz, 0.0);
+        for (int k = 0; k < 3; ++k) {
+            v[k] = valid ? rin[k] : 0.0;
+            v[3 + k] = valid ? rout[k] : 0.0;
+        }
+        v[6] = valid ? km.x * sqrt(fx * fx + fy * fy + fz * fz) : 0.0;  // mu |F| (spacestep)
+        v[7] = valid ? nbr : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < kEnergyKinds; ++k) {
+        const double w = (MODE != kModeEnergy && k == 6) ? wave_total_max_d(v[k]) : wave_total_sum_d(v[k]);
+        if (lane == 0) s_red[k][wave] = w;
+    }
+    __syncthreads();
+    if (threadIdx.x < kEnergyKinds) {
+        const int k = threadIdx.x;
+        double r = s_red[k][0];
+        for (int w = 1; w < kEval64Block / 64; ++w) r = (MODE != kModeEnergy && k == 6) ? fmax(r, s_red[k][w]) : r + s_red[k][w];
+        if (MODE == kModeEnergy)
+            a.part_energy[blockIdx.x * kEnergyKinds + k] = r;
+        else
+            a.dpart[blockIdx.x * 8 + k] = r;
+    }
+}
+
+// the fp64 evaluation's rows in a fixed order -> the context (reactions, max drift, neighbours), react_out[6] for
+// the tail's ext_react, and (spacestep >= 0) the step's adapted timestep; oracle/gcs_oracle.c gcso_run's spacestep
+__global__ __launch_bounds__(256) void k_red64(DevCtx* ctx, ForceArgs a, int rows, double spacestep, double timestep,
+                                               double* react_out)
+{
+    __shared__ double s_red[8][4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int b = tid; b < rows; b += blockDim.x)
+        for (int k = 0; k < 8; ++k) acc[k] = (k == 6) ? fmax(acc[k], a.dpart[b * 8 + k]) : acc[k] + a.dpart[b * 8 + k];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const float w = ((MAXM >> k) & 1) ? wave_max(v[k]) : (((MINM >> k) & 1) ? wave_min(v[k]) : wave_sum(v[k]));
-        if (lane == 0) s_tmp[k][wave] = w;
+    for (int k = 0; k < 8; ++k) {
+        const double w = (k == 6) ? wave_total_max_d(acc[k]) : wave_total_sum_d(acc[k]);
+        if (lane == 0) s_red[k][wave] = w;
     }
     __syncthreads();
-    if (tid == 0) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            float r = s_tmp[k][0];
-            for (int q = 1; q < kSmallWaves; ++q)
-                r = ((MAXM >> k) & 1) ? fmaxf(r, s_tmp[k][q]) : (((MINM >> k) & 1) ? fminf(r, s_tmp[k][q]) : r + s_tmp[k][q]);
-            v[k] = r;
-        }
+    if (tid != 0) return;
+    double tot[8];
+    for (int k = 0; k < 8; ++k) {
+        tot[k] = s_red[k][0];
+        for (int w = 1; w < (int)(blockDim.x / 64); ++w) tot[k] = (k == 6) ? fmax(tot[k], s_red[k][w]) : tot[k] + s_red[k][w];
     }
-}
-
-// the pair factors (a, b) particle j brings into a mixed pair (the list step's type_ab[class_j])
-__device__ __forceinline__ float2 small_ab(int pair_mix, float4 kj)
-{
-    return pair_mix ? make_float2(kj.y, kj.z) : make_float2(1.f, 0.f);
-}
-
-__global__ __launch_bounds__(kSmallThreads) void k_small(DevCtx* __restrict__ gctx, ForceArgs a, SmallArgs sa)
-{
-    __shared__ float4 s_pos[kSmallMax];
-    __shared__ float4 s_new[kSmallMax];
-    __shared__ float4 s_kmu[kSmallMax];
-    __shared__ int s_cnt[kSmallCells + 1];
-    __shared__ int s_fill[kSmallCells];
-    __shared__ unsigned short s_cidx[kSmallMax];
-    __shared__ unsigned short s_arr[kSmallMax];
-    __shared__ DevCtx s_ctx;
-    __shared__ double s_sched[kSchedCount];
-    __shared__ float s_red[10][kSmallWaves];
-    __shared__ int s_build;
-    const int tid = threadIdx.x;
-    const int n = a.n;
-    const int pair_mix = a.pair_mix;
-    const size_t N = (size_t)n;
-    const float skin = sa.skin;
-
-    // the system into LDS: the context, the schedule, the current positions, the per-particle constants
-    if (tid == 0) s_ctx = *gctx;
-    if (tid < kSchedCount) s_sched[tid] = a.sched[tid];
-    __syncthreads();
-    {
-        const float4* pcur = s_ctx.parity ? a.pos1 : a.pos0;
-        for (int i = tid; i < n; i += kSmallThreads) {
-            s_pos[i] = pcur[i];
-            s_kmu[i] = a.kmu[i];
-        }
+    for (int k = 0; k < 3; ++k) {
+        ctx->react_in[k] = tot[k];
+        ctx->react_out[k] = tot[3 + k];
     }
-    // the local terms read positions through ForceArgs and the context through a pointer: both point into LDS
-    ForceArgs la = a;
-    la.pos0 = s_pos;
-    la.pos1 = s_pos;
-    la.kmu = s_kmu;
-    __syncthreads();
-
-    unsigned long long ph[5] = {0, 0, 0, 0, 0};  // GCS_DEBUG_SMALL: build, forces, totals, tail+barrier, builds
-    for (int k = 0; k < sa.steps; ++k) {
-        const unsigned long long t0 = sa.dbg ? wall_clock64() : 0;
-        // ---- rebuild the lists when the skin may be used up (or at a chunk start without continuity)
-        if (tid == 0) {
-            const float rc = pair_cutoff(a, s_ctx.cs);
-            const bool used = 2.f * s_ctx.ldisp + fmaxf(rc - s_ctx.lrc_b, 0.f) > 0.999f * skin;
-            s_build = (a.has_pair && ((k == 0 && sa.force_build) || used)) ? 1 : 0;
-        }
-        __syncthreads();
-        if (s_build) {
-            const float rcb = pair_cutoff(a, s_ctx.cs) + skin;
-            float lo[3] = {3.0e38f, 3.0e38f, 3.0e38f}, hi[3] = {-3.0e38f, -3.0e38f, -3.0e38f};
-            for (int i = tid; i < n; i += kSmallThreads) {
-                const float4 p = s_pos[i];
-                lo[0] = fminf(lo[0], p.x);
-                lo[1] = fminf(lo[1], p.y);
-                lo[2] = fminf(lo[2], p.z);
-                hi[0] = fmaxf(hi[0], p.x);
-                hi[1] = fmaxf(hi[1], p.y);
-                hi[2] = fmaxf(hi[2], p.z);
-            }
-            {
-                float bb[6] = {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]};
-                small_totals<6, 0x38u, 0x07u>(bb, s_red);
-                if (tid == 0) {
-                    for (int d = 0; d < 3; ++d) {
-                        s_ctx.bbox_lo[d] = bb[d];
-                        s_ctx.bbox_hi[d] = bb[3 + d];
-                    }
-                    s_ctx.lgrid = make_grid(s_ctx.bbox_lo, s_ctx.bbox_hi, rcb, kSmallCells, 1);
-                }
-            }
-            __syncthreads();
-            const Grid g = s_ctx.lgrid;
-            for (int c = tid; c <= g.ncell; c += kSmallThreads) {
-                s_cnt[c] = 0;
-                if (c < g.ncell) s_fill[c] = 0;
-            }
-            __syncthreads();
-            for (int i = tid; i < n; i += kSmallThreads) {
-                const float4 p = s_pos[i];
-                atomicAdd(&s_cnt[cell_index(g, p.x, p.y, p.z)], 1);
-            }
-            __syncthreads();
-            {  // exclusive scan of the counts -> cell starts: 5 consecutive cells per thread, DPP wave scans, wave totals
-                constexpr int kC = (kSmallCells + 1 + kSmallThreads - 1) / kSmallThreads;
-                const int c0 = kC * tid;
-                int v[kC], sum = 0;
-#pragma unroll
-                for (int q = 0; q < kC; ++q) {
-                    v[q] = c0 + q <= g.ncell ? s_cnt[c0 + q] : 0;
-                    sum += v[q];
-                }
-                int incl = sum;
-                GCS_DPP_SCAN(dpp_i, add_i, 0, incl)
-                const int lane = tid & 63, wave = tid >> 6;
-                __shared__ int s_wsum[kSmallWaves];
-                if (lane == 63) s_wsum[wave] = incl;
-                __syncthreads();
-                int base = 0;
-                for (int w = 0; w < wave; ++w) base += s_wsum[w];
-                int run = base + incl - sum;
-#pragma unroll
-                for (int q = 0; q < kC; ++q) {
-                    if (c0 + q <= g.ncell) s_cnt[c0 + q] = run;
-                    run += v[q];
-                }
-            }
-            __syncthreads();
-            // file every particle under its cell in arrival order, then rank it by index inside the cell
-            for (int i = tid; i < n; i += kSmallThreads) {
-                const float4 p = s_pos[i];
-                const int c = cell_index(g, p.x, p.y, p.z);
-                s_arr[s_cnt[c] + atomicAdd(&s_fill[c], 1)] = (unsigned short)i;
-            }
-            __syncthreads();
-            for (int i = tid; i < n; i += kSmallThreads) {
-                const float4 p = s_pos[i];
-                const int c = cell_index(g, p.x, p.y, p.z);
-                const int b = s_cnt[c], e = s_cnt[c + 1];
-                int r = 0;
-                for (int t = b; t < e; ++t) r += (s_arr[t] < i) ? 1 : 0;
-                s_cidx[b + r] = (unsigned short)i;
-            }
-            __syncthreads();
-            for (int c = tid; c <= g.ncell; c += kSmallThreads) sa.cstart[c] = s_cnt[c];
-            for (int i = tid; i < n; i += kSmallThreads) sa.cidx[i] = s_cidx[i];
-            // the lists: every particle within rcb of each particle at the build (27 cells, cell order)
-            const float rcb2 = rcb * rcb;
-            const int nx = g.n[0], ny = g.n[1], nz = g.n[2];
-            for (int i = tid; i < n; i += kSmallThreads) {
-                const float4 p = s_pos[i];
-                const int c = cell_index(g, p.x, p.y, p.z);
-                const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
-                int cnt = 0;
-                for (int z = max(cz - 1, 0); z <= min(cz + 1, nz - 1); ++z)
-                    for (int y = max(cy - 1, 0); y <= min(cy + 1, ny - 1); ++y) {
-                        const int base = (z * ny + y) * nx;
-                        const int jb = s_cnt[base + max(cx - 1, 0)], je = s_cnt[base + min(cx + 1, nx - 1) + 1];
-                        for (int t = jb; t < je; ++t) {
-                            const int j = s_cidx[t];
-                            if (j == i) continue;
-                            const float4 q = s_pos[j];
-                            const float dx = p.x - q.x, dy = p.y - q.y, dz = p.z - q.z;
-                            if (fmaf(dz, dz, fmaf(dy, dy, dx * dx)) < rcb2) {
-                                if (cnt < kSmallCap) sa.list[(size_t)cnt * N + i] = (unsigned short)j;
-                                ++cnt;
-                            }
-                        }
-                    }
-                sa.lcount[i] = min(cnt, kSmallCap) | (cnt > kSmallCap ? kListOverflow : 0);
-                sa.bpos[i] = p;
-            }
-            if (tid == 0) {
-                s_ctx.lrc_b = pair_cutoff(a, s_ctx.cs);
-                s_ctx.ldisp = 0.f;
-                s_ctx.lbuilds += 1;
-            }
-            __threadfence_block();  // the lists and build positions are read back by this block below
-            __syncthreads();
-        }
-
-        const unsigned long long t1 = sa.dbg ? wall_clock64() : 0;
-        if (sa.dbg && s_build) ph[4] += 1;
-        // ---- forces + update (each thread: particles tid, tid + 1024, ...; every lane active, so the local terms'
-        // wave-cooperative droplet sees whole waves; the lanes past N compute particle N - 1 and discard it)
-        const float cs = (float)s_ctx.cs;
-        const float scale = a.pair_scaled ? cs : 1.f;
-        const float sga = a.pa_sig * scale, sgb = a.pb_sig * scale;
-        const float k2a = 1.f / (sga * sga), k2b = 1.f / (sgb * sgb);
-        const float kA = 0.5f * 6.f * a.pa_eps * k2a, kB = 0.5f * 24.f * a.pb_eps * k2b;
-        const float rc = pair_cutoff(a, s_ctx.cs), rc2 = rc * rc;
-        float rin_s[3] = {0.f, 0.f, 0.f}, rout_s[3] = {0.f, 0.f, 0.f};
-        float dmax = 0.f, nbr_s = 0.f, nfb = 0.f;
-#pragma unroll 1
-        for (int q = 0; q * kSmallThreads < n; ++q) {  // uniform trip count
-            const int i0 = q * kSmallThreads + tid;
-            const bool valid = i0 < n;
-            const int i = valid ? i0 : n - 1;
-            const float4 pi = s_pos[i];
-            const float4 km = s_kmu[i];
-            float fx = 0.f, fy = 0.f, fz = 0.f, nbr = 0.f;
-            if (a.has_pair) {
-                const float2 own = small_ab(pair_mix, km);
-                const float ahi = kA * own.x, bhi = kB * own.y;
-                const int cw = sa.lcount[i];
-                const bool ovf = (cw & kListOverflow) != 0;
-                // (every lane of the wave takes part in the maximum: overflowed lanes count 0 entries)
-                const int cnt = ovf ? 0 : min(cw & kListCountMask, kSmallCap);
-                const int cmax = uniform(wave_max_int(cnt));
-                if (!ovf) {
-                    // batches of 8 entries: their loads are independent (one round trip per batch); entries past
-                    // the count read a clamped in-bounds slot and are masked
-                    for (int t0 = 0; t0 < cmax; t0 += 8) {
-                        int ej[8];
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) ej[u] = sa.list[(size_t)min(t0 + u, kSmallCap - 1) * N + i];
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) {
-                            const int j = min(ej[u], n - 1);
-                            list_pair(pi.x, pi.y, pi.z, s_pos[j], small_ab(pair_mix, s_kmu[j]), ahi, bhi, kA, kB, k2a,
-                                      k2b, rc2, t0 + u < cnt, fx, fy, fz, nbr);
-                        }
-                    }
-                } else {  // overflowed list: the build's cells around the current position, radius rc + D
-                    nfb += valid ? 1.f : 0.f;
-                    const Grid lg = s_ctx.lgrid;
-                    const float D = s_ctx.ldisp;
-                    const float R = rc + D + 1.0e-5f * (rc + D);
-                    const int x0 = lgrid_cell(lg, 0, pi.x - R), x1 = lgrid_cell(lg, 0, pi.x + R);
-                    const int y0 = lgrid_cell(lg, 1, pi.y - R), y1 = lgrid_cell(lg, 1, pi.y + R);
-                    const int z0 = lgrid_cell(lg, 2, pi.z - R), z1 = lgrid_cell(lg, 2, pi.z + R);
-                    for (int z = z0; z <= z1; ++z)
-                        for (int y = y0; y <= y1; ++y) {
-                            const int base = (z * lg.n[1] + y) * lg.n[0];
-                            const int t0 = sa.cstart[base + x0], t1 = sa.cstart[base + x1 + 1];
-                            for (int t = t0; t < t1; ++t) {
-                                const int j = sa.cidx[t];
-                                list_pair(pi.x, pi.y, pi.z, s_pos[j], small_ab(pair_mix, s_kmu[j]), ahi, bhi, kA, kB,
-                                          k2a, k2b, rc2, j != i, fx, fy, fz, nbr);
-                            }
-                        }
-                }
-            }
-            float en[kEnergyKinds];
-            float rin[3] = {0.f, 0.f, 0.f}, rout[3] = {0.f, 0.f, 0.f};
-            local_terms<kModeStep, GCS_LIST_BOND_BATCH>(&s_ctx, la, i, pi.x, pi.y, pi.z, km, fx, fy, fz, en, rin, rout);
-            float n0, n1, n2;
-            noise3(a, &s_ctx, i, n0, n1, n2);
-            const float mu = km.x, dt = a.timestep;
-            const float amp = sqrtf(2.f * a.temperature * mu * dt);
-            const float mdt = mu * dt;
-            const float4 np = make_float4(pi.x + mdt * fx + amp * n0, pi.y + mdt * fy + amp * n1,
-                                          pi.z + mdt * fz + amp * n2, 0.f);
-            if (valid) {
-                s_new[i] = np;
-                for (int d = 0; d < 3; ++d) {
-                    rin_s[d] += rin[d];
-                    rout_s[d] += rout[d];
-                }
-                nbr_s += nbr;
-                if (a.has_pair) {
-                    const float4 b = sa.bpos[i];
-                    const float gx = np.x - b.x, gy = np.y - b.y, gz = np.z - b.z;
-                    dmax = fmaxf(dmax, sqrtf(fmaf(gz, gz, fmaf(gy, gy, gx * gx))));
-                }
-            }
-        }
-        // ---- the step's totals (fixed order; the barrier inside also orders every force's reads of the old
-        // positions before the copy below), then the positions, then the context (thread 0)
-        const unsigned long long t2 = sa.dbg ? wall_clock64() : 0;
-        float tot[9] = {rin_s[0], rin_s[1], rin_s[2], rout_s[0], rout_s[1], rout_s[2], nbr_s, nfb, dmax};
-        small_totals<9, 0x100u, 0u>(tot, s_red);
-        const unsigned long long t3 = sa.dbg ? wall_clock64() : 0;
-        for (int i = tid; i < n; i += kSmallThreads) s_pos[i] = s_new[i];
-        if (tid == 0) {
-            ListTailIn tin;
-            tin.s_flags = s_sched[kSchedFlags];
-            tin.s_dt = s_sched[kSchedDt];
-            tin.s_cs0 = s_sched[kSchedCs0];
-            tin.s_csTau = s_sched[kSchedCsTau];
-            tin.s_bs0 = s_sched[kSchedBs0];
-            tin.s_bsTau = s_sched[kSchedBsTau];
-            tin.s_muW = s_sched[kSchedMuW];
-            for (int d = 0; d < 3; ++d) tin.s_k[d] = s_sched[kSchedK0 + d];
-            tin.c_step = s_ctx.step;
-            tin.c_cursor = s_ctx.noise_cursor;
-            tin.c_fb = s_ctx.lfallback;
-            tin.c_parity = s_ctx.parity;
-            tin.c_time = s_ctx.time;
-            tin.c_cs = s_ctx.cs;
-            tin.c_bs = s_ctx.bs;
-            for (int d = 0; d < 3; ++d) tin.c_w[d] = s_ctx.wall[d];
-            ListTotals t;
-            for (int d = 0; d < 6; ++d) t.react[d] = (double)tot[d];
-            t.nbr = (double)tot[6];
-            t.nfb = (long long)tot[7];
-            t.ld = tot[8];
-            list_tail_apply(&s_ctx, a, tin, t, sa.flags & (kLFlagSched | kLFlagStats));
-        }
-        __syncthreads();
-        if (sa.dbg) {
-            const unsigned long long t4 = wall_clock64();
-            ph[0] += t1 - t0;
-            ph[1] += t2 - t1;
-            ph[2] += t3 - t2;
-            ph[3] += t4 - t3;
-        }
-    }
-    if (sa.dbg && tid == 0)
-        for (int q = 0; q < 5; ++q) sa.dbg[q] = ph[q];
-    // ---- the state back: positions into the buffer the context now names current, the context
-    {
-        float4* pout = s_ctx.parity ? a.pos1 : a.pos0;
-        for (int i = tid; i < n; i += kSmallThreads) pout[i] = s_pos[i];
-    }
-    if (tid == 0) {
-        const DevCtx& c = s_ctx;
-        gctx->step = c.step;
-        gctx->parity = c.parity;
-        gctx->time = c.time;
-        gctx->cs = c.cs;
-        gctx->bs = c.bs;
-        for (int d = 0; d < 3; ++d) {
-            gctx->wall[d] = c.wall[d];
-            gctx->react_in[d] = c.react_in[d];
-            gctx->react_out[d] = c.react_out[d];
-            gctx->bbox_lo[d] = c.bbox_lo[d];
-            gctx->bbox_hi[d] = c.bbox_hi[d];
-        }
-        gctx->noise_cursor = c.noise_cursor;
-        gctx->neighbors = c.neighbors;
-        gctx->lgrid = c.lgrid;
-        gctx->lrc_b = c.lrc_b;
-        gctx->ldisp = c.ldisp;
-        gctx->lbuilds = c.lbuilds;
-        gctx->lfallback = c.lfallback;
+    if (react_out)
+        for (int k = 0; k < 6; ++k) react_out[k] = tot[k];
+    ctx->max_drift = tot[6];
+    ctx->neighbors = tot[7] / (double)a.n;
+    if (spacestep >= 0.0) {
+        double dt = timestep;
+        if (spacestep > 0.0 && tot[6] * dt > spacestep) dt = spacestep / tot[6];
+        ctx->dt_used = dt;
     }
 }
 
@@ -3721,15 +3595,26 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(DevCtx* __restrict__ gc
 
 void launch_prime(hipStream_t s, DevCtx* ctx, const ForceArgs& a, float rc_fixed, int ncell_max, const double* sched)
 {
-    hipLaunchKernelGGL(k_prime, dim3(1), dim3(1024), 0, s, ctx, a, rc_fixed, ncell_max, sched);
+    if (a.prec == 64)
+        hipLaunchKernelGGL(k_prime<double>, dim3(1), dim3(1024), 0, s, ctx, a, rc_fixed, ncell_max, sched);
+    else
+        hipLaunchKernelGGL(k_prime<float>, dim3(1), dim3(1024), 0, s, ctx, a, rc_fixed, ncell_max, sched);
 }
 
 void launch_cell_count(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, int n, int* cell_of,
                        int* slot, int* count, const DomBox* reg, int* islot)
 {
     const DomBox r = reg ? *reg : DomBox{};
-    hipLaunchKernelGGL(k_cell_count, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, n, cell_of, slot, count,
-                       reg ? 1 : 0, r, islot);
+    hipLaunchKernelGGL(k_cell_count<float4>, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, n, cell_of, slot,
+                       count, reg ? 1 : 0, r, islot);
+}
+
+void launch_cell_count(hipStream_t s, const DevCtx* ctx, const double4* pos0, const double4* pos1, int n, int* cell_of,
+                       int* slot, int* count, const DomBox* reg, int* islot)
+{
+    const DomBox r = reg ? *reg : DomBox{};
+    hipLaunchKernelGGL(k_cell_count<double4>, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, n, cell_of, slot,
+                       count, reg ? 1 : 0, r, islot);
 }
 
 void launch_tail_reduce(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int fblocks, double* out)
@@ -3782,13 +3667,6 @@ int force_step_resident(int waves)
     return e == hipSuccess ? per * cus : 0;
 }
 
-void launch_scatter_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int* tmp, int fblocks, int apply_sched,
-                         int ncell_max)
-{
-    hipLaunchKernelGGL(k_scatter_tail, dim3((a.n + 255) / 256 + 1), dim3(256), 0, s, ctx, a, a.n, tmp, fblocks,
-                       apply_sched, ncell_max);
-}
-
 void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* slot, const int* cstart, int* tmp,
                          int* count)
 {
@@ -3800,8 +3678,17 @@ void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, cons
                       float* sb, int pair_mix, const int* ptype, float4* psort0, float4* psort1, float4* skmu,
                       int2* sbrow, const int* boff, int* islot)
 {
-    hipLaunchKernelGGL(k_cell_sort, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, kmu, n, tmp, cell_of,
-                       cstart, sidx, scell, spos, sb, pair_mix, ptype, psort0, psort1, skmu, sbrow, boff, islot);
+    hipLaunchKernelGGL(k_cell_sort<float>, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, kmu, n, tmp,
+                       cell_of, cstart, sidx, scell, spos, sb, pair_mix, ptype, psort0, psort1, skmu, sbrow, boff, islot);
+}
+
+void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const double4* pos0, const double4* pos1, const double4* kmu,
+                      int n, const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell, float4* spos,
+                      float* sb, int pair_mix, const int* ptype, double4* psort0, double4* psort1, double4* skmu,
+                      int2* sbrow, const int* boff, int* islot)
+{
+    hipLaunchKernelGGL(k_cell_sort<double>, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, kmu, n, tmp,
+                       cell_of, cstart, sidx, scell, spos, sb, pair_mix, ptype, psort0, psort1, skmu, sbrow, boff, islot);
 }
 
 template <int MODE, bool FUSED>
@@ -3857,30 +3744,31 @@ void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a)
     }
 }
 
-template <bool CT>
+template <bool CT, typename R>
 static void launch_list_step_ct(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)
 {
     const dim3 g(list_step_grid(a.n));
     if (list_u16(a.n)) {
         if (a.list_waves == 2)
-            hipLaunchKernelGGL((k_lstep<unsigned short, 2, CT>), g, dim3(128), 0, s, ctx, a, flags);
+            hipLaunchKernelGGL((k_lstep<unsigned short, 2, CT, false, R>), g, dim3(128), 0, s, ctx, a, flags);
         else
-            hipLaunchKernelGGL((k_lstep<unsigned short, 4, CT>), g, dim3(256), 0, s, ctx, a, flags);
+            hipLaunchKernelGGL((k_lstep<unsigned short, 4, CT, false, R>), g, dim3(256), 0, s, ctx, a, flags);
     } else {
         if (a.list_waves == 2)
-            hipLaunchKernelGGL((k_lstep<int, 2, CT>), g, dim3(128), 0, s, ctx, a, flags);
+            hipLaunchKernelGGL((k_lstep<int, 2, CT, false, R>), g, dim3(128), 0, s, ctx, a, flags);
         else
-            hipLaunchKernelGGL((k_lstep<int, 4, CT>), g, dim3(256), 0, s, ctx, a, flags);
+            hipLaunchKernelGGL((k_lstep<int, 4, CT, false, R>), g, dim3(256), 0, s, ctx, a, flags);
     }
 }
 
-__global__ void k_set_contact(DevCtx* ctx, float d2)
+__global__ void k_set_contact(DevCtx* ctx, float d2, double d2_64)
 {
     ctx->contact_d2 = d2;
+    ctx->contact_d2_64 = d2_64;
 }
-void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2)
+void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2, double d2_64)
 {
-    hipLaunchKernelGGL(k_set_contact, dim3(1), dim3(1), 0, s, ctx, d2);
+    hipLaunchKernelGGL(k_set_contact, dim3(1), dim3(1), 0, s, ctx, d2, d2_64);
 }
 
 void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)
@@ -3900,10 +3788,17 @@ void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)
         }
         return;
     }
-    if (a.contact_on)
-        launch_list_step_ct<true>(s, ctx, a, flags);
-    else
-        launch_list_step_ct<false>(s, ctx, a, flags);
+    if (a.prec == 64) {
+        if (a.contact_on)
+            launch_list_step_ct<true, double>(s, ctx, a, flags);
+        else
+            launch_list_step_ct<false, double>(s, ctx, a, flags);
+    } else {
+        if (a.contact_on)
+            launch_list_step_ct<true, float>(s, ctx, a, flags);
+        else
+            launch_list_step_ct<false, float>(s, ctx, a, flags);
+    }
 }
 
 void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const double* glob, int flags,
@@ -3913,28 +3808,28 @@ void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, con
                        band_stride);
 }
 
-void launch_small(hipStream_t s, DevCtx* ctx, const ForceArgs& a, long long first_step, int steps, int flags,
-                  int force_build, float skin, unsigned short* list, int* lcount, float4* bpos, int* cstart,
-                  unsigned short* cidx, unsigned long long* dbg)
-{
-    SmallArgs sa;
-    sa.first_step = first_step;
-    sa.steps = steps;
-    sa.flags = flags;
-    sa.force_build = force_build;
-    sa.skin = skin;
-    sa.list = list;
-    sa.lcount = lcount;
-    sa.bpos = bpos;
-    sa.cstart = cstart;
-    sa.cidx = cidx;
-    sa.dbg = dbg;
-    hipLaunchKernelGGL(k_small, dim3(1), dim3(kSmallThreads), 0, s, ctx, a, sa);
-}
-
 void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a)
 {
-    hipLaunchKernelGGL(k_update, dim3(update_blocks(a.n)), dim3(kUpdateBlock), 0, s, ctx, a);
+    if (a.prec == 64)
+        hipLaunchKernelGGL(k_update<double>, dim3(update_blocks(a.n)), dim3(kUpdateBlock), 0, s, ctx, a);
+    else
+        hipLaunchKernelGGL(k_update<float>, dim3(update_blocks(a.n)), dim3(kUpdateBlock), 0, s, ctx, a);
+}
+
+int eval64_blocks(int n) { return (n + kEval64Block - 1) / kEval64Block; }
+
+void launch_eval64(hipStream_t s, int mode, const DevCtx* ctx, const ForceArgs& a)
+{
+    const dim3 g(eval64_blocks(a.n));
+    if (mode == kModeEnergy)
+        hipLaunchKernelGGL(k_eval64<kModeEnergy>, g, dim3(kEval64Block), 0, s, ctx, a);
+    else
+        hipLaunchKernelGGL(k_eval64<kModeForce>, g, dim3(kEval64Block), 0, s, ctx, a);
+}
+
+void launch_red64(hipStream_t s, DevCtx* ctx, const ForceArgs& a, double spacestep, double timestep, double* react_out)
+{
+    hipLaunchKernelGGL(k_red64, dim3(1), dim3(256), 0, s, ctx, a, eval64_blocks(a.n), spacestep, timestep, react_out);
 }
 
 void launch_adapt(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int fblocks, float spacestep, float timestep)
@@ -3950,17 +3845,26 @@ void launch_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int fblocks, in
 }
 
 void launch_search_count(hipStream_t s, const DevCtx* ctx, int n, const float4* spos, const int* sidx, const int* scell,
-                         const int* cstart, int* counts)
+                         const int* cstart, int* counts, const double4* pos64, double d64)
 {
-    hipLaunchKernelGGL((k_search<false>), dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, spos, sidx, scell, cstart,
-                       counts, (const int*)nullptr, (unsigned long long*)nullptr);
+    if (pos64)
+        hipLaunchKernelGGL((k_search<false, true>), dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, spos, sidx, scell,
+                           cstart, counts, (const int*)nullptr, (unsigned long long*)nullptr, pos64, d64);
+    else
+        hipLaunchKernelGGL((k_search<false, false>), dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, spos, sidx, scell,
+                           cstart, counts, (const int*)nullptr, (unsigned long long*)nullptr, pos64, d64);
 }
 
 void launch_search_emit(hipStream_t s, const DevCtx* ctx, int n, const float4* spos, const int* sidx, const int* scell,
-                        const int* cstart, const int* offsets, unsigned long long* keys)
+                        const int* cstart, const int* offsets, unsigned long long* keys, const double4* pos64,
+                        double d64)
 {
-    hipLaunchKernelGGL((k_search<true>), dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, spos, sidx, scell, cstart,
-                       (int*)nullptr, offsets, keys);
+    if (pos64)
+        hipLaunchKernelGGL((k_search<true, true>), dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, spos, sidx, scell,
+                           cstart, (int*)nullptr, offsets, keys, pos64, d64);
+    else
+        hipLaunchKernelGGL((k_search<true, false>), dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, spos, sidx, scell,
+                           cstart, (int*)nullptr, offsets, keys, pos64, d64);
 }
 
 void launch_exclusive_scan_small(hipStream_t s, const int* in, int* out, int n, int* total)

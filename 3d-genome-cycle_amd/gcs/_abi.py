@@ -25,6 +25,10 @@ NOISE_PHILOX = 0
 NOISE_INJECTED = 1
 NOISE_NONE = 2
 
+PRECISION_DEFAULT = 0  # = PRECISION_F64
+PRECISION_F32 = 32
+PRECISION_F64 = 64
+
 OPT_GRAPH_STEPS = 1
 OPT_WAVES_PER_TILE = 2
 OPT_CHUNK_ORDER = 3
@@ -38,7 +42,6 @@ OPT_LIST_SKIN = 10
 OPT_LIST_EVERY = 11
 OPT_LIST_CAP = 12
 OPT_LIST_WAVES = 13
-OPT_SMALL_PATH = 14
 OPT_DENSE_NEIGHBORS = 15
 OPT_LIST_DEAL = 16
 
@@ -67,7 +70,7 @@ _pi64 = C.POINTER(C.c_int64)
 
 class SystemDesc(C.Structure):
     _fields_ = [("particle_count", _i64), ("mobilities", _pd), ("ab_factors", _pd), ("device", _i32),
-                ("reserved", _i32)]
+                ("precision", _i32)]
 
 
 class SoftcoreParams(C.Structure):
@@ -127,8 +130,7 @@ class ListStats(C.Structure):
 
 class RunStats(C.Structure):
     _fields_ = [("graph_launches", _i64), ("graph_steps", _i64), ("eager_steps", _i64), ("graphs_captured", _i64),
-                ("graphs_cached", _i64), ("small_launches", _i64), ("small_steps", _i64),
-                ("fused_contact_steps", _i64)]
+                ("graphs_cached", _i64), ("fused_contact_steps", _i64)]
 
 
 # name -> (restype, argtypes); the exported surface of include/gcs.h
@@ -139,6 +141,7 @@ PROTOTYPES = {
     "gcs_engine_create": (C.c_int, [C.POINTER(SystemDesc), C.POINTER(C.c_void_p)]),
     "gcs_engine_destroy": (C.c_int, [C.c_void_p]),
     "gcs_engine_particle_count": (C.c_int, [C.c_void_p, C.POINTER(_i64)]),
+    "gcs_engine_precision": (C.c_int, [C.c_void_p, C.POINTER(_i32)]),
     "gcs_add_neighbor_softcore": (C.c_int, [C.c_void_p, C.POINTER(SoftcoreParams), C.POINTER(_i32)]),
     "gcs_add_neighbor_softwell": (C.c_int, [C.c_void_p, C.POINTER(SoftwellParams), _pi64, _i64, C.POINTER(_i32)]),
     "gcs_add_bonded_pairwise": (C.c_int, [C.c_void_p, C.POINTER(BondParams), _pi64, _i64, _i32, _pi64, _i64,

@@ -99,12 +99,26 @@ def _close_live_engines():
         e.close()
 
 
-class Engine:
-    """One simulated system on one HIP device (md::system + md::simulate_brownian_dynamics)."""
+def precision_bits(precision) -> int:
+    """GCS_PRECISION_* of a precision given as 32 / 64 / "f32" / "f64" / "fp32" / "fp64" (None: the default, fp64)"""
+    if precision is None:
+        return A.PRECISION_F64
+    p = str(precision).lower().lstrip("f").lstrip("p")
+    if p in ("32", "64"):
+        return int(p)
+    raise ValueError(f"precision must be 32 or 64 (or 'f32' / 'f64'), not {precision!r}")
 
-    def __init__(self, n: int, mobilities=None, ab_factors=None, device: int = 0):
+
+class Engine:
+    """One simulated system on one HIP device (md::system + md::simulate_brownian_dynamics).
+
+    precision: 64 (default; md::scalar is double) or 32 (the fp32 engine: the tile-step shapes and the spatial
+    decomposition are fp32 only)."""
+
+    def __init__(self, n: int, mobilities=None, ab_factors=None, device: int = 0, precision=None):
         self._lib = A.load()
         self.n = int(n)
+        self.precision = precision_bits(precision)
         self._mu = _f64(mobilities, (self.n,)) if mobilities is not None else None
         self._ab = _f64(ab_factors, (self.n, 2)) if ab_factors is not None else None
         d = A.SystemDesc()
@@ -112,6 +126,7 @@ class Engine:
         d.mobilities = _pd(self._mu)
         d.ab_factors = _pd(self._ab)
         d.device = device
+        d.precision = self.precision
         h = C.c_void_p()
         A.check(self._lib.gcs_engine_create(C.byref(d), C.byref(h)))
         self._h = h

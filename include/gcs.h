@@ -51,8 +51,10 @@
  * Conventions: every function returns 0 (GCS_OK) on success or a positive GCS_E* code; the message of
  * the most recent failure on the calling thread is returned by gcs_last_error().  All arrays crossing
  * the boundary are plain host pointers owned by the caller and copied; device memory is engine-owned.
- * Positions are fp64 at the boundary (md::point is double) and fp32 on the device.  One engine per host
- * thread, bound to one HIP device and one stream; engines are not internally locked.
+ * Positions are fp64 at the boundary (md::point is double).  On the device the engine computes in fp64 like the
+ * reference (GCS_PRECISION_F64, the default: positions, forces, the integrator, the pair predicate) or, when
+ * asked, in fp32 (GCS_PRECISION_F32).  One engine per host thread, bound to one HIP device and one stream;
+ * engines are not internally locked.
  */
 #ifndef GCS_H
 #define GCS_H
@@ -63,8 +65,15 @@
 extern "C" {
 #endif
 
-/* 2: gcs_run_stats gained fused_contact_steps (an out-struct grew: callers built against 1 must rebuild) */
-#define GCS_ABI_VERSION 2
+/* 2: gcs_run_stats gained fused_contact_steps (an out-struct grew: callers built against 1 must rebuild)
+ * 3: gcs_system_desc.reserved became .precision (0 = fp64); gcs_run_stats lost the small-path counters;
+ *    GCS_OPT_SMALL_PATH and GCS_OPT_FUSED_STEP 1 are gone */
+#define GCS_ABI_VERSION 3
+
+/* arithmetic precision of an engine (gcs_system_desc.precision) */
+#define GCS_PRECISION_DEFAULT 0 /* = GCS_PRECISION_F64 */
+#define GCS_PRECISION_F32 32    /* fp32 positions and arithmetic (fastest; all step shapes, spatial decomposition) */
+#define GCS_PRECISION_F64 64    /* fp64 positions and arithmetic, as md::scalar = double; the list step */
 
 /* status codes */
 #define GCS_OK 0
@@ -94,7 +103,7 @@ typedef struct gcs_system_desc {
     const double* mobilities; /* [N]; NULL -> 1 (micromd default mobility) */
     const double* ab_factors; /* [N][2]; NULL -> (0, 0) */
     int32_t device;           /* HIP device ordinal */
-    int32_t reserved;
+    int32_t precision;        /* GCS_PRECISION_* (0: fp64) */
 } gcs_system_desc;
 
 /* Neighbor-pairwise soft-core repulsion: U_ij = a_ij*SC<2,3>(r) + b_ij*SC<8,3>(r),
@@ -218,6 +227,8 @@ int gcs_device_count(int32_t* count);
 int gcs_engine_create(const gcs_system_desc* desc, gcs_engine** out);
 int gcs_engine_destroy(gcs_engine* engine);
 int gcs_engine_particle_count(const gcs_engine* engine, int64_t* count);
+/* the engine's arithmetic precision in bits (32 or 64) */
+int gcs_engine_precision(const gcs_engine* engine, int32_t* bits);
 
 /* force fields; *handle receives an id usable with gcs_remove_forcefield */
 int gcs_add_neighbor_softcore(gcs_engine* e, const gcs_softcore_params* p, int32_t* handle);
@@ -261,8 +272,9 @@ int gcs_engine_compute_energy(gcs_engine* e, double* total, double* per_kind);
 /* Forces on every particle at the current positions/context ([N][3]); refreshes reaction stats. */
 int gcs_engine_compute_forces(gcs_engine* e, double* forces, int64_t n);
 
-/* Pairs (i < j) of `points` closer than `distance` (strict fp32 predicate), sorted by
- * (i, j).  points == NULL searches the engine's current positions. pairs receives [count][2]. */
+/* Pairs (i < j) of `points` closer than `distance` (the strict predicate (dx^2 + dy^2) + dz^2 < distance^2 with
+ * every operation rounded, in the engine's precision), sorted by (i, j).  points == NULL searches the
+ * engine's current positions. pairs receives [count][2]. */
 int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, double distance,
                                 uint32_t* pairs, int64_t capacity, int64_t* count);
 
@@ -271,7 +283,7 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
 
 /* Contact map (replaces contact_map::update / accumulate / clear, stage_interphase/contact_map.cpp:28-85, driven
  * from stage_interphase/simulation_driver_interphase.cpp:38-45).  update: count every pair i < j of the CURRENT positions closer
- * than `distance` (strict fp32 predicate, as gcs_engine_search_neighbors) into the engine's device hash map;
+ * than `distance` (the strict predicate of gcs_engine_search_neighbors) into the engine's device hash map;
  * enqueued on the engine stream, no host synchronisation (call it between gcs_engine_run chunks).
  * read: the accumulated (i, j, count) triples sorted by (i, j) into ijc[count][3] (count = distinct pairs;
  * GCS_ECAPACITY with *count set when capacity is too small, GCS_ECAPACITY without a count when the map
@@ -346,8 +358,8 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
 #define GCS_OPT_WAVES_PER_TILE 2 /* waves sharing one 64-particle tile of the pair loop: 1, 2, 4 or 8 */
 #define GCS_OPT_CHUNK_ORDER 3    /* pair-loop candidate chunks: 0 contiguous, 1 strided across stencil rows (default) */
 #define GCS_OPT_FUSED_STEP 4     /* 3 (default): neighbour-list step (1 launch per step + a list rebuild every few
-                                    steps; systems with > 256 pair classes or >= 2^24 particles run step 2);
-                                    2: 2 launches per step (force + cell-list rebuild); 1: 4 launches; 0: unfused */
+                                    steps; fp32 systems with > 256 pair classes or >= 2^24 particles run step 2);
+                                    fp32 only: 2 launches per step (force + cell-list rebuild), 0 unfused */
 #define GCS_OPT_SPLIT_TILES 5    /* step launches: 0 (default) off, 1 split every tile over two workgroups, 2 only the
                                     densest tiles, picked by the cell scan within the resident-workgroup budget */
 #define GCS_OPT_SUBTILES 7       /* pair-loop stencils per 64-particle tile: 1, 2 or 4 (default 2) */
@@ -359,10 +371,7 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
 #define GCS_OPT_LIST_CAP 12       /* list step: list entries per particle (default 1024; a longer list: exact search) */
 #define GCS_OPT_LIST_WAVES 13     /* list step: waves per 64-particle tile, 4 (default: lowest step latency) or 2 (more
                                      tiles resident: the better throughput when several trajectories share a GPU) */
-#define GCS_OPT_SMALL_PATH 14     /* 1: systems of <= 2,048 particles run every chunk of fixed-timestep steps in ONE
-                                     single-workgroup launch (Verlet lists rebuilt by displacement); 0 (default): the
-                                     list step's cached graphs (faster on C3's prometaphase / telophase) */
-#define GCS_OPT_DENSE_NEIGHBORS 15 /* list step (GCS_OPT_FUSED_STEP 3): a fresh run whose mean neighbour count within the
+#define GCS_OPT_DENSE_NEIGHBORS 15 /* fp32 list step (GCS_OPT_FUSED_STEP 3): a fresh run whose mean neighbour count within the
                                      cutoff, x 2 when list entries are 32-bit (N > 65,536), exceeds this takes the
                                      unfused tile step instead (default 48; 0: never) */
 #define GCS_OPT_LIST_DEAL 16      /* list build: which wave segment takes each candidate chunk; -1 (default) the tuned
@@ -398,8 +407,6 @@ typedef struct gcs_run_stats {
     int64_t eager_steps;      /* steps launched one by one */
     int64_t graphs_captured;  /* captures (a cache miss: new phase / parity / length, or changed settings) */
     int64_t graphs_cached;    /* captured sequences held now */
-    int64_t small_launches;   /* single-workgroup launches of the small-system path (GCS_OPT_SMALL_PATH) */
-    int64_t small_steps;      /* steps they ran */
     int64_t fused_contact_steps; /* list steps that counted a deferred contact update (gcs_engine_contacts_update) */
 } gcs_run_stats;
 int gcs_engine_get_run_stats(gcs_engine* e, gcs_run_stats* out);

@@ -59,6 +59,8 @@ void gcso_compute_forces(gcso_system* s, double* forces /* [N][3] */);
 /* strict-fp32 neighbor predicate (oracle/strict_f32.c): pairs (i<j) sorted, returns the count (may
  * exceed capacity; only the first `capacity` pairs are written). */
 int64_t gcso_search_neighbors(const double* xyz, int64_t n, double distance, uint32_t* pairs, int64_t capacity);
+/* the same in fp64 (the fp64 engine's predicate) on the points themselves */
+int64_t gcso_search_neighbors64(const double* xyz, int64_t n, double distance, uint32_t* pairs, int64_t capacity);
 
 /* random numbers */
 void gcso_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

@@ -58,6 +58,7 @@ def load():
             "gcso_compute_energy": (C.c_double, [vp, pd]),
             "gcso_compute_forces": (None, [vp, pd]),
             "gcso_search_neighbors": (C.c_int64, [pd, C.c_int64, C.c_double, C.POINTER(C.c_uint32), C.c_int64]),
+            "gcso_search_neighbors64": (C.c_int64, [pd, C.c_int64, C.c_double, C.POINTER(C.c_uint32), C.c_int64]),
             "gcso_philox4x32_10": (None, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
             "gcso_philox_normals": (None, [C.c_uint64, C.c_int64, C.c_int64, pd]),
             "gcso_seed_seq_generate": (None, [C.POINTER(C.c_uint32), C.c_int64, C.POINTER(C.c_uint32), C.c_int64]),
@@ -91,11 +92,13 @@ def _pi(a):
 
 
 class OracleSystem:
-    """fp64 single-threaded restatement with the Engine's method names."""
+    """fp64 single-threaded restatement with the Engine's method names.  `precision` (as Engine's: 64 default, or 32)
+    only selects the neighbour / contact predicate the engine it is checked against uses; the dynamics are fp64."""
 
-    def __init__(self, n, mobilities=None, ab_factors=None, **_):
+    def __init__(self, n, mobilities=None, ab_factors=None, precision=None, **_):
         self._lib = load()
         self.n = int(n)
+        self.precision = 32 if str(precision).lower().lstrip("fp") == "32" else 64
         mu = _f64(mobilities, (self.n,)) if mobilities is not None else None
         ab = _f64(ab_factors, (self.n, 2)) if ab_factors is not None else None
         d = A.SystemDesc()
@@ -218,7 +221,7 @@ class OracleSystem:
 
     def search_neighbors(self, distance, points=None):
         pts = _f64(points if points is not None else self.get_positions(), (-1, 3))
-        return search_neighbors(pts, distance)
+        return search_neighbors(pts, distance, self.precision)
 
 
     def set_domain(self, lo=None, hi=None):
@@ -236,7 +239,7 @@ class OracleSystem:
     def contacts_update(self, distance):
         if not hasattr(self, "_contacts"):
             self._contacts = {}
-        for i, j in search_neighbors(self.get_positions(), distance):
+        for i, j in search_neighbors(self.get_positions(), distance, self.precision):
             key = (int(i), int(j))
             self._contacts[key] = self._contacts.get(key, 0) + 1
 
@@ -253,14 +256,16 @@ class OracleSystem:
         return np.vectorize(lambda v: quantize(v, fraction_bits))(x).astype(np.float32)
 
 
-def search_neighbors(points, distance):
+def search_neighbors(points, distance, precision=32):
+    """pairs (i < j) closer than `distance` under the engine's strict predicate: fp32 (precision 32) or fp64"""
     lib = load()
+    fn = lib.gcso_search_neighbors64 if int(precision) == 64 else lib.gcso_search_neighbors
     pts = _f64(points, (-1, 3))
     n = pts.shape[0]
     cap = max(16, 8 * n)
     while True:
         buf = np.empty((cap, 2), dtype=np.uint32)
-        cnt = lib.gcso_search_neighbors(_pd(pts), n, float(distance), buf.ctypes.data_as(C.POINTER(C.c_uint32)), cap)
+        cnt = fn(_pd(pts), n, float(distance), buf.ctypes.data_as(C.POINTER(C.c_uint32)), cap)
         if cnt <= cap:
             return buf[:cnt].copy()
         cap = int(cnt)

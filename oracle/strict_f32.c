@@ -2,12 +2,15 @@
  * strict_f32.c -- TEST INFRASTRUCTURE ONLY.  Neighbor-set oracle for md::neighbor_searcher
  * (stage_interphase/contact_map.cpp:60-62): every pair (i < j) of points closer than `distance`.
  *
- * The predicate is evaluated in IEEE fp32 exactly as the device kernel evaluates it, so the two pair
- * sets are comparable bit for bit:  p = (float)x;  d = p_i - p_j (per axis, fp32);
+ * The predicate is evaluated exactly as the device kernels evaluate it, so the pair sets are comparable bit
+ * for bit.  fp32 engine (gcso_search_neighbors): p = (float)x;  d = p_i - p_j (per axis, fp32);
  * r2 = (dx*dx + dy*dy) + dz*dz (fp32, no contraction);  pair iff r2 < (float)distance * (float)distance.
+ * fp64 engine (gcso_search_neighbors64): the same expression in fp64 on x itself, pair iff
+ * r2 < distance * distance -- what md::neighbor_searcher's double arithmetic computes (INFERRED: the reference's
+ * squared-distance form; -funsafe-math-optimizations there may contract it, which moves only pairs at the cutoff).
  * This file is compiled with -ffp-contract=off and without -funsafe-math-optimizations (oracle/Makefile).
  * Candidate pairs come from a cell grid built in fp64 with a 1e-3 relative margin, so the grid never
- * decides membership; the fp32 predicate does.
+ * decides membership; the predicate does.
  */
 #include "gcs_oracle.h"
 
@@ -36,13 +39,26 @@ static inline int strict_pair(const float* p, int64_t i, int64_t j, float rc2)
     return r2 < rc2;
 }
 
-int64_t gcso_search_neighbors(const double* xyz, int64_t n, double distance, uint32_t* pairs, int64_t capacity)
+static inline int strict_pair64(const double* p, int64_t i, int64_t j, double rc2)
+{
+    double dx = p[3 * i] - p[3 * j];
+    double dy = p[3 * i + 1] - p[3 * j + 1];
+    double dz = p[3 * i + 2] - p[3 * j + 2];
+    double xx = dx * dx;
+    double yy = dy * dy;
+    double zz = dz * dz;
+    double r2 = (xx + yy) + zz;
+    return r2 < rc2;
+}
+
+static int64_t search(const double* xyz, int64_t n, double distance, uint32_t* pairs, int64_t capacity, int f64)
 {
     if (n < 2) return 0;
     float* p = (float*)malloc((size_t)(3 * n) * sizeof(float));
     for (int64_t k = 0; k < 3 * n; k++) p[k] = (float)xyz[k];
     float rcf = (float)distance;
     float rc2 = rcf * rcf;
+    double rc2_64 = distance * distance;
     double cell = (double)rcf * 1.001 + 1e-30;
     double lo[3], hi[3];
     for (int k = 0; k < 3; k++) lo[k] = hi[k] = p[k];
@@ -106,7 +122,7 @@ int64_t gcso_search_neighbors(const double* xyz, int64_t n, double distance, uin
                                 for (int64_t b = start[c2]; b < start[c2 + 1]; b++) {
                                     int64_t j = items[b];
                                     if (j <= i) continue;
-                                    if (!strict_pair(p, i, j, rc2)) continue;
+                                    if (f64 ? !strict_pair64(xyz, i, j, rc2_64) : !strict_pair(p, i, j, rc2)) continue;
                                     if (count < capacity) {
                                         pairs[2 * count] = (uint32_t)i;
                                         pairs[2 * count + 1] = (uint32_t)j;
@@ -122,4 +138,14 @@ int64_t gcso_search_neighbors(const double* xyz, int64_t n, double distance, uin
     free(items);
     free(p);
     return count;
+}
+
+int64_t gcso_search_neighbors(const double* xyz, int64_t n, double distance, uint32_t* pairs, int64_t capacity)
+{
+    return search(xyz, n, distance, pairs, capacity, 0);
+}
+
+int64_t gcso_search_neighbors64(const double* xyz, int64_t n, double distance, uint32_t* pairs, int64_t capacity)
+{
+    return search(xyz, n, distance, pairs, capacity, 1);
 }

@@ -35,7 +35,7 @@ def test_library_exports_every_symbol():
 
 
 def test_abi_version():
-    assert A.load().gcs_abi_version() == 2
+    assert A.load().gcs_abi_version() == 3
 
 
 STRUCTS = {
@@ -71,6 +71,18 @@ def test_errors_are_reported_not_crashed():
     assert lib.gcs_engine_create(C.byref(d), C.byref(h)) == A.GCS_EINVAL
     assert b"particle_count" in lib.gcs_last_error()
     assert lib.gcs_engine_create(None, C.byref(h)) == A.GCS_EINVAL
+    d.particle_count = 10
+    d.precision = 16  # neither 0, 32 nor 64
+    assert lib.gcs_engine_create(C.byref(d), C.byref(h)) == A.GCS_EINVAL
+    assert b"precision" in lib.gcs_last_error()
+
+
+def test_precision_names():
+    from gcs.engine import precision_bits
+    assert precision_bits(None) == 64 and precision_bits("f64") == 64 and precision_bits("fp32") == 32
+    assert precision_bits(32) == 32
+    with pytest.raises(ValueError):
+        precision_bits(16)
 
 
 def test_no_cpu_fallback_without_device():

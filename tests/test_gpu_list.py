@@ -1,8 +1,8 @@
 """GPU parity of the list step (GCS_OPT_FUSED_STEP 3: neighbour lists with a skin, one launch per step, exact
 cell search for any particle the skin no longer covers) against the fp64 oracle, through the C ABI.
 
-Bounds are the ones DESIGN.md §6 states for every step shape: positions within 2e-5 absolute after k steps,
-forces/energies through the same engine calls.  The list step changes only the order in which a particle's pair
+Bounds are the ones DESIGN.md §6 states for every step shape, per engine precision (tests/tolerances.py): positions
+within 1e-9 (fp64 engine) / 2e-5 (fp32 engine) absolute after k steps, forces/energies through the same engine calls.  The list step changes only the order in which a particle's pair
 forces are summed, never the pair set (k_lstep: a particle whose list may be incomplete is searched exactly), so
 the same bounds hold with the rebuild period forced far beyond what the skin covers, and with lists that overflow.
 """
@@ -13,12 +13,12 @@ from gcs import _abi as A
 from gcs import interphase, synthetic
 from gcs.config import InterphaseConfig, resolution_scaled
 from gcs.engine import Engine
+from tolerances import REACT, WALL_REL, X as TOL_X, precisions
 
 import oracle
 
 pytestmark = pytest.mark.gpu
 
-TOL_X = 2e-5
 LATE = {"step": 200000, "time": 2.0, "core_scale": 0.99, "bond_scale": 0.99, "wall_semiaxes": [1.5, 1.55, 1.6]}
 
 
@@ -26,19 +26,18 @@ def _f32(x):
     return np.asarray(x, dtype=np.float32).astype(np.float64)
 
 
-def _list_engine(design, cfg, **opts):
-    e, _ = interphase.build_interphase(Engine, design, cfg)
+def _list_engine(design, cfg, prec=64, **opts):
+    e, _ = interphase.build_interphase(Engine, design, cfg, precision=prec)
     e.set_option(A.OPT_FUSED_STEP, 3)
-    e.set_option(A.OPT_SMALL_PATH, 0)  # the multi-workgroup list step even at C1 size (tests/test_gpu_small.py: the other)
     e.set_option(A.OPT_DENSE_NEIGHBORS, 0)  # the list step at any density (test_dense_start_takes_tile_step: the switch)
     for k, v in opts.items():
         e.set_option(getattr(A, "OPT_" + k.upper()), v)
     return e
 
 
-def _pair(design, cfg, x=None, ctx=None, **opts):
-    e = _list_engine(design, cfg, **opts)
-    o, _ = interphase.build_interphase(oracle.OracleSystem, design, cfg)
+def _pair(design, cfg, x=None, ctx=None, prec=64, **opts):
+    e = _list_engine(design, cfg, prec, **opts)
+    o, _ = interphase.build_interphase(oracle.OracleSystem, design, cfg, precision=prec)
     for s in (e, o):
         s.set_schedule(**interphase.interphase_schedule(cfg))
         if x is not None:
@@ -55,66 +54,73 @@ def _run_both(e, o, steps, first, cfg, seed, **kw):
         s.run(steps, first_step=first, temperature=cfg.temperature, timestep=cfg.timestep, seed=seed, **kw)
 
 
-def test_list_trajectory_c1_from_step0(c1_design):
+@precisions
+def test_list_trajectory_c1_from_step0(c1_design, prec):
     """production start (core scale 0.5, growing cutoff), 60 steps, Philox noise"""
     cfg = InterphaseConfig()
-    e, o = _pair(c1_design, cfg)
+    e, o = _pair(c1_design, cfg, prec=prec)
     _run_both(e, o, 60, 0, cfg, 987654321)
     err = np.abs(e.get_positions() - o.get_positions()).max()
     st = e.list_stats()
     assert st["active"] == 1 and st["builds"] >= 60 // st["rebuild_every"], st
-    assert err <= TOL_X, (err, st)
+    assert err <= TOL_X[prec], (err, st)
 
 
-def test_list_trajectory_c1_wall_contact(c1_design):
+@precisions
+def test_list_trajectory_c1_wall_contact(c1_design, prec):
     cfg = InterphaseConfig()
-    e, o = _pair(c1_design, cfg, ctx=LATE)
+    e, o = _pair(c1_design, cfg, ctx=LATE, prec=prec)
     _run_both(e, o, 40, LATE["step"], cfg, 5)
-    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[prec]
     ce, co = e.get_context(), o.get_context()
     assert ce["step"] == co["step"] == LATE["step"] + 40
-    assert np.allclose(ce["wall_semiaxes"], co["wall_semiaxes"], rtol=1e-7)
-    assert np.allclose(ce["inward_reaction"], co["inward_reaction"], rtol=1e-3, atol=1e-2)
+    assert np.allclose(ce["wall_semiaxes"], co["wall_semiaxes"], rtol=WALL_REL[prec])
+    rt, at = REACT[prec]
+    assert np.allclose(ce["inward_reaction"], co["inward_reaction"], rtol=rt, atol=at)
 
 
-def test_list_injected_reference_noise(c1_design):
+@precisions
+def test_list_injected_reference_noise(c1_design, prec):
     cfg = InterphaseConfig()
     steps = 12
     xi = oracle.reference_normals(c1_design.seed, steps * c1_design.n * 3).reshape(steps, c1_design.n, 3)
-    e, o = _pair(c1_design, cfg)
+    e, o = _pair(c1_design, cfg, prec=prec)
     for s in (e, o):
         s.set_noise(xi)
     _run_both(e, o, steps, 0, cfg, 0, noise=A.NOISE_INJECTED)
-    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[prec]
 
 
+@precisions
 @pytest.mark.parametrize("skin,every", [(30, 200), (400, 64)])
-def test_list_exact_when_the_skin_is_outrun(c1_design, skin, every):
+def test_list_exact_when_the_skin_is_outrun(c1_design, skin, every, prec):
     """rebuild period far beyond the skin: particles outrun it and take the exact cell search; same bound"""
     cfg = InterphaseConfig()
-    e, o = _pair(c1_design, cfg, ctx=LATE, list_skin=skin, list_every=every)
+    e, o = _pair(c1_design, cfg, ctx=LATE, prec=prec, list_skin=skin, list_every=every)
     _run_both(e, o, 60, LATE["step"], cfg, 17)
     st = e.list_stats()
     assert st["fallback_particle_steps"] > 0, st
-    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[prec]
 
 
-def test_list_exact_when_lists_overflow(c1_design):
+@precisions
+def test_list_exact_when_lists_overflow(c1_design, prec):
     cfg = InterphaseConfig()
-    e, o = _pair(c1_design, cfg, ctx=LATE, list_cap=32)
+    e, o = _pair(c1_design, cfg, ctx=LATE, prec=prec, list_cap=32)
     _run_both(e, o, 30, LATE["step"], cfg, 23)
     st = e.list_stats()
     assert st["fallback_particle_steps"] > 0, st
-    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[prec]
 
 
+@precisions
 @pytest.mark.parametrize("every", [0, 1, 5])
-def test_list_graph_eager_and_chunks_bitwise_identical(c1_design, every):
+def test_list_graph_eager_and_chunks_bitwise_identical(c1_design, every, prec):
     """graph vs eager launches and one run vs chunks rebuild at the same steps: identical bits"""
     cfg = InterphaseConfig()
     runs = []
     for g, chunks in ((0, [70]), (8, [70]), (32, [70]), (32, [13, 40, 17])):
-        e = _list_engine(c1_design, cfg, list_every=every, graph_steps=g)
+        e = _list_engine(c1_design, cfg, prec, list_every=every, graph_steps=g)
         e.set_schedule(**interphase.interphase_schedule(cfg))
         e.set_context(LATE)
         first = LATE["step"]
@@ -128,9 +134,9 @@ def test_list_graph_eager_and_chunks_bitwise_identical(c1_design, every):
         assert c == runs[0][1]
 
 
-@pytest.mark.parametrize("small", [0, 1])
+@precisions
 @pytest.mark.parametrize("n", [1, 2, 63, 65, 200])
-def test_list_small_and_ragged_sizes(n, small):
+def test_list_small_and_ragged_sizes(n, prec):
     """random ab factors and mobilities (several pair classes, mixed), 20 steps at dt 1e-4"""
     rng = np.random.default_rng(n)
     x = rng.uniform(-0.5, 0.5, size=(n, 3))
@@ -138,7 +144,7 @@ def test_list_small_and_ragged_sizes(n, small):
     mu = rng.uniform(0.5, 1.5, size=n)
     sysd = {}
     for name, cls in (("e", Engine), ("o", oracle.OracleSystem)):
-        s = cls(n, mobilities=mu, ab_factors=ab)
+        s = cls(n, mobilities=mu, ab_factors=ab, precision=prec)
         s.add_neighbor_softcore(2.5, 0.3, 2.5, 0.24, 0.3, mix=True, scaled=True)
         if n > 1:
             s.add_bonded_pairwise(A.POT_SEMISPRING, a_spring=100.0, b_spring=50.0, mix=True, scaled=True,
@@ -147,43 +153,43 @@ def test_list_small_and_ragged_sizes(n, small):
         s.set_positions(x)
         if name == "e":
             s.set_option(A.OPT_FUSED_STEP, 3)
-            s.set_option(A.OPT_SMALL_PATH, small)
             s.set_option(A.OPT_DENSE_NEIGHBORS, 0)
         sysd[name] = s
     for s in sysd.values():
         s.run(20, seed=1, timestep=1e-4)
     assert sysd["e"].list_stats()["active"] == 1
-    assert (sysd["e"].run_stats()["small_steps"] == 20) == bool(small)
-    assert np.abs(sysd["e"].get_positions() - sysd["o"].get_positions()).max() <= TOL_X
+    assert np.abs(sysd["e"].get_positions() - sysd["o"].get_positions()).max() <= TOL_X[prec]
 
 
-def test_list_c2_trajectory_from_bench_state():
+@precisions
+def test_list_c2_trajectory_from_bench_state(prec):
     """C2 (60,662 beads) from benchdata (step 300,000): 1, 10, 50 steps vs the oracle"""
     from pathlib import Path
     z = np.load(Path(__file__).resolve().parents[1] / "benchdata" / "c2_interphase_step300000.npz")
     ctx = {"step": int(z["step"]), "time": float(z["time"]), "core_scale": float(z["core_scale"]),
            "bond_scale": float(z["bond_scale"]), "wall_semiaxes": [float(v) for v in z["wall_semiaxes"]]}
     design, cfg = synthetic.make_c2(), InterphaseConfig()
-    e, o = _pair(design, cfg, x=_f32(z["positions"]), ctx=ctx)
+    e, o = _pair(design, cfg, x=_f32(z["positions"]), ctx=ctx, prec=prec)
     first, done, errs = ctx["step"], 0, {}
     for k in (1, 10, 50):
         _run_both(e, o, k - done, first + done, cfg, 99)
         done = k
         errs[k] = float(np.abs(e.get_positions() - o.get_positions()).max())
     print({"list_c2_errors": errs, "stats": e.list_stats()})
-    assert all(v <= TOL_X for v in errs.values()), errs
+    assert all(v <= TOL_X[prec] for v in errs.values()), errs
     ce, co = e.get_context(), o.get_context()
-    assert np.allclose(ce["wall_semiaxes"], co["wall_semiaxes"], rtol=1e-7)
+    assert np.allclose(ce["wall_semiaxes"], co["wall_semiaxes"], rtol=WALL_REL[prec])
 
 
-def test_list_c5_trajectory():
+@precisions
+def test_list_c5_trajectory(prec):
     """C5 (606,248 beads, 10 kb, resolution-scaled timestep): 10 steps from the dense synthetic start"""
     design, cfg = synthetic.make_c5(), resolution_scaled(InterphaseConfig(), 10.0)
-    e, o = _pair(design, cfg, x=_f32(design.positions))
+    e, o = _pair(design, cfg, x=_f32(design.positions), prec=prec)
     _run_both(e, o, 10, 0, cfg, 99)
     err = float(np.abs(e.get_positions() - o.get_positions()).max())
     print({"list_c5_err": err, "stats": e.list_stats()})
-    assert err <= TOL_X
+    assert err <= TOL_X[prec]
 
 
 def test_dense_start_takes_tile_step():
@@ -192,15 +198,15 @@ def test_dense_start_takes_tile_step():
     the list step; a continuing chain keeps its verdict; the tile-step trajectory matches the fp64 oracle"""
     cfg5 = resolution_scaled(InterphaseConfig(), 10.0)
     d5 = synthetic.make_c5()
-    e, o = _pair(d5, cfg5, x=_f32(d5.positions), dense_neighbors=48)
+    e, o = _pair(d5, cfg5, x=_f32(d5.positions), prec=32, dense_neighbors=48)
     _run_both(e, o, 4, 0, cfg5, 99)
     st = e.list_stats()
     assert st["active"] == 0 and st["builds"] == 0, st
     err = float(np.abs(e.get_positions() - o.get_positions()).max())
-    assert err <= TOL_X, err
+    assert err <= TOL_X[32], err
     cfg2 = InterphaseConfig()
     d2 = synthetic.make_c2()
-    e2, _ = interphase.build_interphase(Engine, d2, cfg2)
+    e2, _ = interphase.build_interphase(Engine, d2, cfg2, precision=32)
     e2.set_schedule(**interphase.interphase_schedule(cfg2))
     e2.run(8, first_step=0, temperature=cfg2.temperature, timestep=cfg2.timestep, seed=1)
     e2.run(8, first_step=8, temperature=cfg2.temperature, timestep=cfg2.timestep, seed=1)
@@ -214,7 +220,7 @@ def test_list_and_rebuild_step_agree_on_neighbour_count():
     c2_design = synthetic.make_c2()
     vals = []
     for fused in (2, 3):
-        e, _ = interphase.build_interphase(Engine, c2_design, cfg)
+        e, _ = interphase.build_interphase(Engine, c2_design, cfg, precision=32)
         e.set_option(A.OPT_FUSED_STEP, fused)
         e.set_schedule(**interphase.interphase_schedule(cfg))
         e.set_context(LATE)
@@ -224,22 +230,26 @@ def test_list_and_rebuild_step_agree_on_neighbour_count():
     assert vals[0] > 0 and vals[1] == pytest.approx(vals[0], rel=1e-4), vals
 
 
-def test_list_two_waves_per_tile(c1_design):
+@precisions
+def test_list_two_waves_per_tile(c1_design, prec):
     """GCS_OPT_LIST_WAVES 2 (two list segments per particle): the same bound against the oracle"""
     cfg = InterphaseConfig()
-    e, o = _pair(c1_design, cfg, ctx=LATE, list_waves=2)
+    e, o = _pair(c1_design, cfg, ctx=LATE, prec=prec, list_waves=2)
     _run_both(e, o, 40, LATE["step"], cfg, 7)
-    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[prec]
 
 
-@pytest.mark.parametrize("waves,deal", [(4, ""), (4, "0120123"), (4, "3"), (2, "001"), (2, "1")])
+@pytest.mark.parametrize("waves,deal", [(4, ""), (4, "0120123"), (4, "3"), (2, "001"), (2, "1"),
+                                        (4, "012012013"), (4, "0120120123")])
 def test_list_deal_patterns(c1_design, waves, deal):
     """GCS_OPT_LIST_DEAL moves candidate chunks between a slot's list segments (even a single wave taking every
-    chunk): the pair set is unchanged, so the same bound against the oracle holds and the neighbour count is equal"""
+    chunk): the pair set is unchanged, so the same bound against the oracle holds and the neighbour count is equal.
+    Periods >= 8 set the top bit of the option word (a negative int64 at the ABI): the pattern is still applied
+    (the list build's segment counts differ from the default deal's)."""
     cfg = InterphaseConfig()
     e, o = _pair(c1_design, cfg, ctx=LATE, list_waves=waves, list_deal=A.list_deal(deal))
     _run_both(e, o, 40, LATE["step"], cfg, 7)
-    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[64]
     nb = []
     for d in (A.list_deal(deal), 0):  # from the same state
         s = _list_engine(c1_design, cfg, list_waves=waves, list_deal=d)
@@ -273,7 +283,7 @@ def test_c2_long_horizon_list_vs_rebuild_step():
     res = {3: [], 2: []}
     for fused in res:
         for k in range(nseed):
-            s, _ = interphase.build_interphase(Engine, design, cfg)
+            s, _ = interphase.build_interphase(Engine, design, cfg, precision=32)
             s.set_schedule(**interphase.interphase_schedule(cfg))
             s.set_option(A.OPT_FUSED_STEP, fused)
             s.set_positions(z["positions"])
@@ -303,15 +313,17 @@ def test_c2_long_horizon_list_vs_rebuild_step():
     assert (s3[:3] > 0).all() and (s2[:3] > 0).all()
 
 
-def test_second_neighbour_harmonic_nonzero_k(c1_design):
+@precisions
+def test_second_neighbour_harmonic_nonzero_k(c1_design, prec):
     """setup_loop_forcefield (simulation_driver_forcefield.cpp:100-136) with K != 0: the (i, i+2) harmonic bonds are
     compiled in (the default config's K = 0 drops them); forces and a 40-step list-step trajectory vs the oracle"""
     import dataclasses
     cfg = dataclasses.replace(InterphaseConfig(), a_core_2nd_bond_spring=40.0, b_core_2nd_bond_spring=15.0)
-    e, o = _pair(c1_design, cfg, ctx=LATE)
+    e, o = _pair(c1_design, cfg, ctx=LATE, prec=prec)
     fe, fo = e.compute_forces(), o.compute_forces()
-    assert np.abs(fe - fo).max() <= 1e-4 * np.abs(fo).max() + 1e-3
-    base, _ = _pair(c1_design, InterphaseConfig(), ctx=LATE)
+    from tolerances import assert_forces_close
+    assert_forces_close(fe, fo, prec)
+    base, _ = _pair(c1_design, InterphaseConfig(), ctx=LATE, prec=prec)
     assert np.abs(base.compute_forces() - fo).max() > 1e-2  # the field changes the forces
     _run_both(e, o, 40, LATE["step"], cfg, 7)
-    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[prec]
