@@ -78,6 +78,19 @@ __global__ __launch_bounds__(256) void k_contact_insert(const DevCtx* __restrict
         }
 }
 
+// occupied slots of the table (one atomic per wave): sizes the compaction's scratch before the compaction
+__global__ __launch_bounds__(256) void k_contact_occupied(const unsigned long long* __restrict__ keys, long long slots,
+                                                          int* __restrict__ total)
+{
+    const int lane = threadIdx.x & 63;
+    int c = 0;
+    for (long long h = (long long)blockIdx.x * blockDim.x + threadIdx.x; h < slots;
+         h += (long long)gridDim.x * blockDim.x)
+        c += keys[h] != kContactEmpty ? 1 : 0;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if (lane == 0 && c) atomicAdd(total, c);
+}
+
 // occupied slots -> (key, count) lists; output order is arbitrary (the sort that follows fixes it)
 __global__ __launch_bounds__(256) void k_contact_compact(const unsigned long long* __restrict__ keys,
                                                          const unsigned* __restrict__ counts, long long slots,
@@ -144,6 +157,12 @@ void launch_contact_insert(hipStream_t s, const DevCtx* ctx, int n, double dist,
     else
         hipLaunchKernelGGL(k_contact_insert<false>, dim3((n + 255) / 256), dim3(256), 0, s, ctx, n, (float)dist, spos,
                            sidx, scell, cstart, keys, counts, bits, overflow, pos64, dist);
+}
+
+void launch_contact_occupied(hipStream_t s, const unsigned long long* keys, long long slots, int* total)
+{
+    const long long blocks = std::min<long long>((slots + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_contact_occupied, dim3((unsigned)blocks), dim3(256), 0, s, keys, slots, total);
 }
 
 void launch_contact_compact(hipStream_t s, const unsigned long long* keys, const unsigned* counts, long long slots,

@@ -281,6 +281,9 @@ struct gcs_engine {
     // grid the next step expects, so a run that continues at chain_step skips re-priming (bitwise identical
     // to one longer run).  Anything that touches positions, context, schedule or cells clears it.
     bool chain_valid = false;
+    // a dense chain (the fp32 tile step picked by the density probe) keeps its verdict while it continues: the
+    // tile step leaves no fused state (chain_valid stays false), so the verdict has its own continuity record
+    bool dense_chain = false;
     int64_t chain_step = 0;
     double chain_dt = 0;  // the timestep begin_run last wrote to ctx->dt_used
     int chain_version = -1;
@@ -793,7 +796,7 @@ float list_skin(const gcs_engine* e) { return 1e-3f * (float)e->list_skin_pm * e
 // the list build's chunk deal (kernels.hip deal_nth): the option, or the default for the waves per tile
 unsigned long long list_deal(const gcs_engine* e)
 {
-    if (e->list_deal_opt >= 0) return (unsigned long long)e->list_deal_opt;
+    if (e->list_deal_opt != -1) return (unsigned long long)e->list_deal_opt;
     return e->list_waves == 2 ? kListDeal2 : kListDeal4;
 }
 // a deal pattern is valid for W waves when its period is 1..15 and every nibble of the period names a wave < W
@@ -802,7 +805,6 @@ bool deal_valid(long long d, int W)
     if (d == 0) return true;
     const int T = (int)((unsigned long long)d >> 60);
     if (T < 1 || T > 15) return false;
-    if ((unsigned long long)d & ~((1ull << 60) - 1ull) & ~(15ull << 60)) return false;
     for (int p = 0; p < 15; ++p) {
         const int w = (int)(((unsigned long long)d >> (4 * p)) & 15ull);
         if (p < T ? w >= W : w != 0) return false;
@@ -1050,10 +1052,12 @@ int choose_shape(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
         e->dense = false;
         return GCS_OK;
     }
-    const bool cont = e->chain_valid && e->chain_step == first_step && e->chain_version == e->topo_version;
+    const bool same = e->chain_step == first_step && e->chain_version == e->topo_version;
+    const bool cont = same && (e->chain_valid || (e->dense && e->dense_chain));
     if (e->dom || cfg->spacestep > 0 || cont) return GCS_OK;
     const bool was = e->dense;
     if ((rc = probe_density(e))) return rc;
+    e->rstats.density_probes++;
     if (e->dense != was) e->chain_valid = false;
     return GCS_OK;
 }
@@ -1180,6 +1184,7 @@ int flush_contacts(gcs_engine* e);  // (below)
 void end_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps)
 {
     e->chain_valid = fused_path(e, cfg->spacestep > 0);
+    e->dense_chain = dense_switch(e) && cfg->spacestep <= 0;
     e->chain_step = first_step + steps;
     e->chain_version = e->topo_version;
 }
@@ -1721,7 +1726,7 @@ int gcs_engine_set_positions(gcs_engine* e, const double* xyz, int64_t n)
     if (e) e->dom_cont = false;  // a decomposed run re-primes after any outside change
     if (!e || !xyz) return fail(GCS_EINVAL, "null argument");
     if (int rc = flush_contacts(e)) return rc;
-    e->chain_valid = false;
+    e->chain_valid = e->dense_chain = false;
     if (n != e->n) return fail(GCS_EINVAL, "position count does not match the particle count");
     HIPCHK(hipSetDevice(e->device));
     if (e->prec == 64) {
@@ -1791,7 +1796,7 @@ int gcs_engine_set_context(gcs_engine* e, const gcs_context* c)
     if (e) e->dom_cont = false;  // a decomposed run re-primes after any outside change
     if (!e || !c) return fail(GCS_EINVAL, "null argument");
     if (int rc = flush_contacts(e)) return rc;
-    e->chain_valid = false;
+    e->chain_valid = e->dense_chain = false;
     HIPCHK(hipSetDevice(e->device));
     DevCtx d;
     HIPCHK(hipMemcpyAsync(&d, e->ctx, sizeof(d), hipMemcpyDeviceToHost, e->stream));
@@ -1815,7 +1820,7 @@ int gcs_engine_set_schedule(gcs_engine* e, const gcs_schedule* s)
 {
     if (e) e->dom_cont = false;  // a decomposed run re-primes after any outside change
     if (!e || !s) return fail(GCS_EINVAL, "null argument");
-    e->chain_valid = false;
+    e->chain_valid = e->dense_chain = false;
     if ((s->update_scales && (!(s->core_scale_tau > 0) || !(s->bond_scale_tau > 0))))
         return fail(GCS_EINVAL, "scale time constants must be positive");
     HIPCHK(hipSetDevice(e->device));
@@ -1829,7 +1834,7 @@ int gcs_engine_set_schedule(gcs_engine* e, const gcs_schedule* s)
 int gcs_engine_apply_schedule(gcs_engine* e, int64_t step)
 {
     if (!e) return fail(GCS_EINVAL, "null argument");
-    e->chain_valid = false;
+    e->chain_valid = e->dense_chain = false;
     int rc = prepare(e);
     if (rc) return rc;
     long long st = step;
@@ -1971,7 +1976,7 @@ int gcs_engine_compute_forces(gcs_engine* e, double* forces, int64_t n)
 {
     if (!e || !forces) return fail(GCS_EINVAL, "null argument");
     if (n != e->n) return fail(GCS_EINVAL, "force array size does not match the particle count");
-    e->chain_valid = false;
+    e->chain_valid = e->dense_chain = false;
     int rc = prepare(e);
     if (rc) return rc;
     launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max, e->dsched);
@@ -2007,7 +2012,7 @@ int gcs_engine_compute_forces(gcs_engine* e, double* forces, int64_t n)
 int gcs_engine_compute_energy(gcs_engine* e, double* total, double* per_kind)
 {
     if (!e || !total) return fail(GCS_EINVAL, "null argument");
-    e->chain_valid = false;
+    e->chain_valid = e->dense_chain = false;
     int rc = prepare(e);
     if (rc) return rc;
     launch_prime(e->stream, e->ctx, e->fa, 0.f, e->ncell_max, e->dsched);
@@ -2037,7 +2042,7 @@ int gcs_engine_search_neighbors(gcs_engine* e, const double* points, int64_t n, 
 {
     if (!e || !count || (capacity > 0 && !pairs)) return fail(GCS_EINVAL, "null argument");
     if (!(distance > 0)) return fail(GCS_EINVAL, "search distance must be positive");
-    e->chain_valid = false;
+    e->chain_valid = e->dense_chain = false;
     if (!points && n != e->n) return fail(GCS_EINVAL, "point count does not match the particle count");
     if (n < 0 || n > (int64_t)1 << 30) return fail(GCS_EINVAL, "bad point count");
     *count = 0;
@@ -2174,12 +2179,10 @@ int gcs_engine_contacts_read(gcs_engine* e, uint32_t* ijc, int64_t capacity, int
     HIPCHK(hipMemcpyAsync(flags, e->c_flags, sizeof(flags), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     if (flags[0]) return fail(GCS_ECAPACITY, "contact map overflowed its hash table: raise GCS_OPT_CONTACT_BITS");
-    // compact into scratch of the table's size (the compaction writes at most the occupied slots), then radix-sort
-    // (key, count) by key; the scratch stays allocated for the next read
-    if (!e->c_ck) {
-        if ((rc = dalloc(&e->c_ck, (size_t)slots)) || (rc = dalloc(&e->c_cv, (size_t)slots))) return rc;
-    }
-    launch_contact_compact(e->stream, e->c_keys, e->c_counts, slots, e->c_ck, e->c_cv, e->c_flags + 1);
+    // count the occupied slots, then compact into scratch of that size and radix-sort (key, count) by key; the
+    // scratch (12 B + 12 B + 12 B per distinct pair) stays allocated for the next read, grown when a window holds more
+    // pairs (not sized to the table: at the 2^28-slot cap that would be 3 GB)
+    launch_contact_occupied(e->stream, e->c_keys, slots, e->c_flags + 1);
     int total = 0;
     HIPCHK(hipMemcpyAsync(&total, e->c_flags + 1, sizeof(int), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
@@ -2187,15 +2190,20 @@ int gcs_engine_contacts_read(gcs_engine* e, uint32_t* ijc, int64_t capacity, int
     if (total > capacity) return fail(GCS_ECAPACITY, "contact buffer too small; *count holds the required size");
     if (total == 0) return GCS_OK;
     if (total > e->c_sorted_cap) {
+        dfree(e->c_ck);
+        dfree(e->c_cv);
         dfree(e->c_ck2);
         dfree(e->c_cv2);
         dfree(e->c_rows);
         e->c_sorted_cap = 0;
-        if ((rc = dalloc(&e->c_ck2, (size_t)total)) || (rc = dalloc(&e->c_cv2, (size_t)total)) ||
-            (rc = dalloc(&e->c_rows, 3 * (size_t)total)))
+        const size_t cap = (size_t)total + (size_t)total / 4;  // headroom for the next windows
+        if ((rc = dalloc(&e->c_ck, cap)) || (rc = dalloc(&e->c_cv, cap)) || (rc = dalloc(&e->c_ck2, cap)) ||
+            (rc = dalloc(&e->c_cv2, cap)) || (rc = dalloc(&e->c_rows, 3 * cap)))
             return rc;
-        e->c_sorted_cap = total;
+        e->c_sorted_cap = (int64_t)cap;
     }
+    HIPCHK(hipMemsetAsync(e->c_flags + 1, 0, sizeof(int), e->stream));
+    launch_contact_compact(e->stream, e->c_keys, e->c_counts, slots, e->c_ck, e->c_cv, e->c_flags + 1);
     const size_t bytes = std::max<size_t>(sort_pairs_u64_u32_temp_bytes(total), 16);
     if (bytes > e->c_temp_bytes) {
         if (e->c_temp) (void)hipFree(e->c_temp);
@@ -2425,7 +2433,7 @@ int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step
         HIPCHK(hipMemcpyAsync(e->pos[e->parity ^ 1], e->pos[e->parity], (size_t)e->n * sizeof(float4),
                               hipMemcpyDeviceToDevice, e->stream));
     }
-    e->chain_valid = false;
+    e->chain_valid = e->dense_chain = false;
     e->dom_next = step + 1;
     if (e->dom_list) {
         enqueue_dom_list_step(e, step, dev_reaction);
@@ -2700,7 +2708,7 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
         e->dom_cont = true;
         e->dom_next = first_step + steps;
     }
-    e->chain_valid = false;
+    e->chain_valid = e->dense_chain = false;
     return GCS_OK;
 }
 
@@ -2987,6 +2995,7 @@ int gcs_engine_get_list_stats(gcs_engine* e, gcs_list_stats* out)
     out->pair_classes = e->ntypes;
     out->capacity = e->list_cap;
     out->sync_stalls = (int64_t)d.scan_stall;
+    out->deal = (int64_t)list_deal(e);
     return GCS_OK;
 }
 
@@ -3001,7 +3010,7 @@ int gcs_engine_get_run_stats(gcs_engine* e, gcs_run_stats* out)
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
 {
     if (!e) return fail(GCS_EINVAL, "null argument");
-    e->chain_valid = false;
+    e->chain_valid = e->dense_chain = false;
     if (option == GCS_OPT_CONTACT_BITS) {
         if (value != 0 && (value < 10 || value > 34)) return fail(GCS_EINVAL, "contact bits must be 0 or in [10, 34]");
         if (e->c_keys) return fail(GCS_ESTATE, "the contact map is already allocated");
@@ -3051,7 +3060,7 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
     if (option == GCS_OPT_DENSE_NEIGHBORS) {
         if (value < 0) return fail(GCS_EINVAL, "dense threshold must be >= 0");
         e->dense_opt = (int)value;
-        e->chain_valid = false;
+        e->chain_valid = e->dense_chain = false;
         return GCS_OK;
     }
     if (option == GCS_OPT_FUSED_STEP) {

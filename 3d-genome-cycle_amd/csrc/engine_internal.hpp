@@ -450,6 +450,7 @@ size_t sort_u64_temp_bytes(int n);
 void launch_contact_insert(hipStream_t s, const DevCtx* ctx, int n, double dist, const float4* spos, const int* sidx,
                            const int* scell, const int* cstart, unsigned long long* keys, unsigned* counts, int bits,
                            int* overflow, const double4* pos64 = nullptr);
+void launch_contact_occupied(hipStream_t s, const unsigned long long* keys, long long slots, int* total);
 void launch_contact_compact(hipStream_t s, const unsigned long long* keys, const unsigned* counts, long long slots,
                             unsigned long long* out_k, unsigned* out_c, int* total);
 size_t sort_pairs_u64_u32_temp_bytes(int n);

@@ -125,12 +125,12 @@ class Profile(C.Structure):
 class ListStats(C.Structure):
     _fields_ = [("active", _i32), ("rebuild_every", _i32), ("builds", _i64), ("fallback_particle_steps", _i64),
                 ("skin", _d), ("max_displacement", _d), ("pair_classes", _i32), ("capacity", _i32),
-                ("sync_stalls", _i64)]
+                ("sync_stalls", _i64), ("deal", _i64)]
 
 
 class RunStats(C.Structure):
     _fields_ = [("graph_launches", _i64), ("graph_steps", _i64), ("eager_steps", _i64), ("graphs_captured", _i64),
-                ("graphs_cached", _i64), ("fused_contact_steps", _i64)]
+                ("graphs_cached", _i64), ("fused_contact_steps", _i64), ("density_probes", _i64)]
 
 
 # name -> (restype, argtypes); the exported surface of include/gcs.h

@@ -5,7 +5,7 @@ reference's `prepare` reads TSV inputs instead).
 
     python -m gcs.cli prepare [-s seed] -o out.h5 config.json chains.tsv
     python -m gcs.cli prepare-synthetic out.h5 --config c1 [--master-seed 1]
-    python -m gcs.cli interphase out.h5 [--relaxation-steps N] [--steps N] [--device 0]
+    python -m gcs.cli interphase out.h5 [--relaxation-steps N] [--steps N] [--device 0] [--precision 64|32]
     python -m gcs.cli anatelophase out.h5 [--anaphase-steps N] [--telophase-steps N]
     python -m gcs.cli prometaphase out.h5 [--steps N]   (needs /stages/prometaphase/0/positions)
     python -m gcs.cli transition interphase|prometaphase out.h5
@@ -38,7 +38,7 @@ def cmd_interphase(a):
     with store.SimulationStore(a.path) as st:
         cfg = st.load_config().interphase
         design = st.load_interphase_design()
-        eng, _ = interphase.build_interphase(Engine, design, cfg, device=a.device)
+        eng, _ = interphase.build_interphase(Engine, design, cfg, device=a.device, precision=a.precision)
         drv = interphase.InterphaseDriver(eng, design, cfg, store=st, log=None if a.quiet else sys.stderr)
         # run_relaxation (simulation_driver_relaxation.cpp:10-23): stage, clear, initial structure from step 0
         st.set_stage("relaxation")
@@ -56,7 +56,7 @@ def cmd_anatelophase(a):
     with store.SimulationStore(a.path) as st:
         cfg = st.load_config().mitotic_phase
         design = st.load_anatelophase_design()
-        sys_, h = mitotic.build_anatelophase(Engine, design, cfg, device=a.device)
+        sys_, h = mitotic.build_anatelophase(Engine, design, cfg, device=a.device, precision=a.precision)
         drv = mitotic.AnatelophaseDriver(sys_, h, design, cfg, store=st, log=None if a.quiet else sys.stderr)
         st.set_stage("anaphase")  # run (stage_anatelophase/simulation_driver.cpp:193-203): clear_frames before set_stage
         st.clear_frames()
@@ -70,7 +70,7 @@ def cmd_prometaphase(a):
     with store.SimulationStore(a.path) as st:
         cfg = st.load_config().mitotic_phase
         design = st.load_prometaphase_design()
-        sys_, _ = mitotic.build_prometaphase(Engine, design, cfg, device=a.device)
+        sys_, _ = mitotic.build_prometaphase(Engine, design, cfg, device=a.device, precision=a.precision)
         st.set_stage("prometaphase")
         st.clear_frames()
         if not st.check_positions(0):
@@ -112,6 +112,8 @@ def main(argv=None):
         p = sub.add_parser(name)
         p.add_argument("path")
         p.add_argument("--device", type=int, default=0)
+        # the engine's arithmetic: 64 (default) is the reference's double; 32 the fp32 engine
+        p.add_argument("--precision", type=int, default=64, choices=[32, 64])
         p.add_argument("--quiet", action="store_true")
         if name == "interphase":
             p.add_argument("--relaxation-steps", type=int, default=None)

@@ -12,6 +12,7 @@ from __future__ import annotations
 import ctypes as C
 import json
 import os
+import sys
 from pathlib import Path
 
 import zlib
@@ -381,8 +382,19 @@ class AsyncWriter:
             raise err
 
     def close(self):
+        """Flush and stop.  A deferred write error is raised -- unless the caller is already propagating an exception
+        (close() called from a `finally` during an unwind): then it is chained onto that exception as a note and the
+        original exception survives."""
+        propagating = sys.exc_info()[1]
         try:
             self.flush()
+        except BaseException as err:
+            if propagating is None:
+                raise
+            if hasattr(propagating, "add_note"):
+                propagating.add_note(f"gcs.store.AsyncWriter: a deferred write also failed: {err!r}")
+            else:
+                print(f"gcs.store.AsyncWriter: a deferred write also failed: {err!r}", file=sys.stderr)
         finally:
             self.q.put(None)
             self.t.join()

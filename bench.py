@@ -3,7 +3,8 @@
 
 Workload (BASELINE.json configs[1]): C2 = synthetic female diploid hg38 at 100 kb, 60,662 particles, the full
 interphase force field (simulation_driver_forcefield.cpp:9-244) with the device-resident schedule and wall ODE,
-Philox noise.  A step = one force evaluation + Euler-Maruyama update of every particle (+ the cell-list rebuild
+Philox noise.  Arithmetic: fp64 (--precision 64, the default), the reference's own (md::scalar is double); the fp32
+engine's rate on the same window is reported beside it (config.f32).  A step = one force evaluation + Euler-Maruyama update of every particle (+ the cell-list rebuild
 and the schedule tail), i.e. one iteration of md::simulate_brownian_dynamics.  The timed window starts at step
 300,000 (t = 3, core_scale = 0.9988): the regime of >90 % of the reference's 700,000 production steps.
 Inputs are resident in HBM before the timed region.
@@ -44,7 +45,9 @@ sys.path.insert(0, str(ROOT / "3d-genome-cycle_amd"))
 
 import numpy as np  # noqa: E402
 
-BYTES_PER_UPDATE = 36  # algorithmic: 12 B position read + 12 B position write + 12 B {mu, a, b}
+# algorithmic bytes per bead-update: position read + position write + {mu, a, b}, 3 scalars each:
+# 36 B in fp32, 72 B in fp64
+BYTES_PER_UPDATE = {32: 36, 64: 72}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md "Chip-level parameters")
 WINDOW_START = 300_000
 STATE_FILE = ROOT / "benchdata" / "c2_interphase_step300000.npz"
@@ -145,10 +148,10 @@ def load_state():
     return z["positions"].astype(np.float64), ctx
 
 
-def make_engine(design, cfg, device, start_step, state=None):
+def make_engine(design, cfg, device, start_step, state=None, precision=64):
     from gcs import interphase
     from gcs.engine import Engine
-    e, _ = interphase.build_interphase(Engine, design, cfg, device=device)
+    e, _ = interphase.build_interphase(Engine, design, cfg, device=device, precision=precision)
     e.set_schedule(**interphase.interphase_schedule(cfg))
     if os.environ.get("GCS_BENCH_DENSE") is not None:  # (experiments) the dense-start threshold of every engine
         from gcs import _abi as A
@@ -316,13 +319,14 @@ def _cpu_model():
     return None
 
 
-STEP_KERNEL = {3: ("k_lstep", "pmc_lstep_traffic.json"), 2: ("k_force<kModeStep, FUSED>", "pmc_force_traffic.json"),
-               1: ("k_force<kModeStep, FUSED>", None), 0: ("k_force<kModeStep>", None)}
+STEP_KERNEL = {(3, 64): ("k_lstep<..., double>", "pmc_lstep64_traffic.json"),
+               (3, 32): ("k_lstep<..., float>", "pmc_lstep_traffic.json"),
+               (2, 32): ("k_force<kModeStep, FUSED>", "pmc_force_traffic.json"), (0, 32): ("k_force<kModeStep>", None)}
 
 
-def read_traffic(fused=3):
+def read_traffic(fused=3, precision=64):
     """HBM bytes per launch of the step's dominant kernel from the committed rocprofv3 PMC pass (profiles/)."""
-    name = STEP_KERNEL.get(fused, (None, None))[1]
+    name = STEP_KERNEL.get((fused, precision), (None, None))[1]
     if name is None:
         return None
     p = ROOT / "profiles" / name
@@ -338,19 +342,22 @@ def read_traffic(fused=3):
 # secondary legs of the default line: C5 on one GPU, the C3 cell cycle
 
 
-def c5_leg(local, seed, steps, log=sys.stderr):
+def c5_leg(local, seed, steps, precision=64, log=sys.stderr):
     """C5 (606,248 particles, BASELINE configs[4]'s system) as ONE trajectory on this GPU, from its synthetic start
-    (step 0, core_scale 0.5 and growing; gcs.config.resolution_scaled force field): the engine's default step and
-    the explicit step shapes (list step, 2-launch rebuild step, 6-launch unfused tile step), each warmed by 64 steps
-    (graphs captured)."""
+    (step 0, core_scale 0.5 and growing; gcs.config.resolution_scaled force field): the fp64 engine (its list step),
+    and the fp32 engine's default step and explicit step shapes (list step, 2-launch rebuild step, 6-launch unfused
+    tile step), each warmed by 64 steps (graphs captured)."""
     from gcs import _abi as A
     from gcs import synthetic
     cfg = bench_config("c5")
     d = synthetic.make_c5(master_seed=1)
     bd = {"temperature": cfg.temperature, "timestep": cfg.timestep, "seed": seed}
     out = {"particles": d.n, "window": f"steps 64..{64 + steps} from the synthetic start", "steps": steps}
-    for name, fused in (("default", None), ("list_step", 3), ("rebuild_step", 2), ("unfused_tile_step", 0)):
-        e = make_engine(d, cfg, local, 0)
+    legs = [("default", None, precision)] + [(f"f32_{n}", f, 32) for n, f in
+                                              (("default", None), ("list_step", 3), ("rebuild_step", 2),
+                                               ("unfused_tile_step", 0))]
+    for name, fused, prec in legs:
+        e = make_engine(d, cfg, local, 0, precision=prec)
         if fused is not None:
             e.set_option(A.OPT_FUSED_STEP, fused)
         e.run(64, first_step=0, **bd)
@@ -359,9 +366,10 @@ def c5_leg(local, seed, steps, log=sys.stderr):
         e.run(steps, first_step=64, **bd)
         e.synchronize()
         out[name] = d.n * steps / (time.perf_counter() - t0)
-        if name == "default":
-            # the engine's density verdict (GCS_OPT_DENSE_NEIGHBORS): list step, or the unfused tile step when dense
-            out["default_step"] = "list" if e.list_stats()["active"] else "unfused tile (dense start)"
+        if name.endswith("default"):
+            # the engine's density verdict (fp32, GCS_OPT_DENSE_NEIGHBORS): list step, or the unfused tile step when
+            # dense; the fp64 engine runs the list step
+            out[name + "_step"] = "list" if e.list_stats()["active"] else "unfused tile (dense start)"
         e.close()
         print(f"bench: C5 {name} {out[name]:.3e} bead-updates/s", file=log, flush=True)
     return out
@@ -436,7 +444,7 @@ def decomp_main(args):
     cfg = bench_config(args.config)
     state = load_state() if args.config == "c2" else None
     design = design_maker(args.config)(master_seed=1)
-    ndom = world if world > 1 else args.decomp
+    ndom = world if world > 1 else args.decomp  # (the decomposition runs on fp32 engines)
     halo = D.domain_halo(cfg)
     x0 = state[0] if state is not None else design.positions
     boxes = D.plan_slabs(x0[:, 2], ndom) if args.slabs else D.plan_boxes(x0, ndom)
@@ -445,7 +453,7 @@ def decomp_main(args):
     window = window_start(args.config)
     cap = max(D.band_capacity(x0, boxes, halo, d) for d in range(ndom))  # one size: bands move between domains
     for d in mine:
-        e = make_engine(design, cfg, local, window, state)
+        e = make_engine(design, cfg, local, window, state, precision=32)
         if args.fused is not None:
             e.set_option(A.OPT_FUSED_STEP, args.fused)  # e.g. 0: the decomposed tile step
         doms.append(D.EngineDomain(e, d, boxes, halo, cap=cap, shared=D.shared_particles(design)))
@@ -470,7 +478,7 @@ def decomp_main(args):
             "metric": "bead-updates/sec (whole node), decomposed single trajectory",
             "value": n * args.steps / el_max, "unit": "bead-updates/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": el_max * 1e3 / args.steps, "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",  # fp32 engines
             "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, one trajectory in "
                                    f"{ndom} {'z-slab' if args.slabs else 'box'} domains "
                                    f"({'RCCL from the engine' if rccl else 'in-process, one GPU'})",
@@ -488,6 +496,55 @@ def decomp_main(args):
 
 # ---------------------------------------------------------------------------------------------------------------
 # replicas (C2 / C4): the headline
+
+
+def f32_leg(args, maker, cfg, bd, local, state, window, R, K, G, list_waves, rank, log=sys.stderr):
+    """The fp32 engine on the headline's workload (same window, replicas, options), timed the same way for about half
+    the headline's window: the rate the fp32 arithmetic buys (a secondary line item, not the headline)."""
+    from gcs import _abi as A
+    engines, seeds, nxt = [], [], []
+    for k in range(R):
+        rid = rank * R + k
+        d = maker(master_seed=1 if state is not None else replica_master_seed(rid))
+        e = make_engine(d, cfg, local, window, state, precision=32)
+        e.set_option(A.OPT_GRAPH_STEPS, G)
+        e.set_option(A.OPT_LIST_WAVES, list_waves)
+        engines.append(e)
+        seeds.append(replica_noise_seed(rid))
+        nxt.append(window)
+    n = engines[0].n
+
+    def enqueue_all(steps):
+        chunk = G if G > 0 else 64
+        for s0 in range(0, steps, chunk):
+            c = min(chunk, steps - s0)
+            for k, (e, sd) in enumerate(zip(engines, seeds)):
+                e.run(c, first_step=nxt[k], seed=sd, **bd)
+                nxt[k] += c
+
+    def sync_all():
+        for e in engines:
+            e.synchronize()
+
+    for _ in range(3):
+        enqueue_all(K)
+    sync_all()
+    t0 = time.perf_counter()
+    enqueue_all(K)
+    sync_all()
+    per_pass = time.perf_counter() - t0
+    passes = max(1, math.ceil(0.5 * args.min_window_s / max(per_pass, 1e-9)))
+    t0 = time.perf_counter()
+    for _ in range(passes):
+        enqueue_all(K)
+    sync_all()
+    value = n * R * passes * K / (time.perf_counter() - t0)
+    prof = engines[0].profile(args.profile_steps, first_step=nxt[0], seed=seeds[0], **bd)
+    for e in engines:
+        e.close()
+    print(f"bench: f32 engine {value:.3e} bead-updates/s ({R} trajectories)", file=log, flush=True)
+    return {"value": value, "replicas_per_gpu": R, "steps": passes * K, "k_lstep_ms": prof["force_ms"],
+            "roofline_frac": n * BYTES_PER_UPDATE[32] / (prof["force_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
 def replica_main(args):
@@ -522,12 +579,13 @@ def replica_main(args):
             e = StubEngine(d.n)
         else:
             from gcs import _abi as A
-            e = make_engine(d, cfg, local, window, state)
-            for opt, v in ((A.OPT_GRAPH_STEPS, G), (A.OPT_WAVES_PER_TILE, args.waves),
-                           (A.OPT_CHUNK_ORDER, args.chunk_order), (A.OPT_FUSED_STEP, args.fused),
-                           (A.OPT_SPLIT_TILES, args.split), (A.OPT_TILE_PRIORITY, args.prio),
-                           (A.OPT_SUBTILES, args.subtiles), (A.OPT_SCAN_BLOCKS, args.scan_mb),
-                           (A.OPT_LIST_WAVES, list_waves)):
+            e = make_engine(d, cfg, local, window, state, precision=args.precision)
+            opts = [(A.OPT_GRAPH_STEPS, G), (A.OPT_SCAN_BLOCKS, args.scan_mb), (A.OPT_LIST_WAVES, list_waves)]
+            if args.precision == 32:  # the fp32 engine's tile-step shapes and their options
+                opts += [(A.OPT_WAVES_PER_TILE, args.waves), (A.OPT_CHUNK_ORDER, args.chunk_order),
+                         (A.OPT_FUSED_STEP, args.fused), (A.OPT_SPLIT_TILES, args.split),
+                         (A.OPT_TILE_PRIORITY, args.prio), (A.OPT_SUBTILES, args.subtiles)]
+            for opt, v in opts:
                 e.set_option(opt, v)
             for kv in args.engine_opt:  # experiments: --engine-opt list_skin=300 (gcs._abi OPT_<NAME>)
                 name, v = kv.split("=")  # list_deal=d:0120123 -> a deal pattern (gcs._abi.list_deal)
@@ -623,7 +681,8 @@ def replica_main(args):
     # per-kernel durations with HIP events on the engine's stream (replica 0 alone, after the timed region)
     prof = eng.profile(args.profile_steps, first_step=after, seed=seed, **bd)
     force_ms = prof["force_ms"]
-    achieved = n * BYTES_PER_UPDATE / (force_ms * 1e-3) / 1e9
+    bpu = BYTES_PER_UPDATE[args.precision]
+    achieved = n * bpu / (force_ms * 1e-3) / 1e9
     ctx = eng.get_context()
     lst = eng.list_stats() if hasattr(eng, "list_stats") else None
     if lst is not None:  # the list step's rebuild cadence and exact-search fallbacks (DESIGN.md "The list step")
@@ -661,7 +720,7 @@ def replica_main(args):
 
         # secondary: the production start window (step 0, core_scale 0.5, ~7x fewer neighbours), one replica
         if rank == 0 and not args.no_start_window:
-            e0 = make_engine(design, cfg, local, 0)
+            e0 = make_engine(design, cfg, local, 0, precision=args.precision)
             e0.set_option(A.OPT_GRAPH_STEPS, G)
             e0.run(max(64, 2 * G), first_step=0, seed=seed, **bd)
             e0.synchronize()
@@ -681,10 +740,12 @@ def replica_main(args):
     for e in engines[1:]:
         e.close()  # (replica 0 stays for the line's context)
 
-    c5 = cycle = None
+    c5 = cycle = f32 = None
     if world == 1 and not args.stub_engine:
+        if args.precision == 64 and args.f32_leg:
+            f32 = f32_leg(args, maker, cfg, bd, local, state, window, R, K, G, list_waves, rank)
         if args.c5_steps > 0:
-            c5 = c5_leg(local, seed, args.c5_steps)
+            c5 = c5_leg(local, seed, args.c5_steps, args.precision)
         if args.cycle_scale > 0:
             cycle = cycle_leg(local, args.cycle_scale)
 
@@ -704,7 +765,7 @@ def replica_main(args):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f64" if args.precision == 64 else "f32",
         "data": "synthetic" if not args.stub_engine else "stub",
         "steps_requested": K,
         "passes": passes,
@@ -726,11 +787,13 @@ def replica_main(args):
                    "contacts_update_ms": contacts_ms, "contacts_distinct_pairs_22_updates": contacts_distinct,
                    "list_step": lst, "list_waves_per_tile": list_waves,
                    "c5_value": c5["default"] if c5 else None, "c5": c5,
-                   "c3_cycle_wall_s": cycle["cycle_wall_s"] if cycle else None, "c3_cycle": cycle},
+                   "c3_cycle_wall_s": cycle["cycle_wall_s"] if cycle else None, "c3_cycle": cycle,
+                   "precision": args.precision, "f32_value": f32["value"] if f32 else None, "f32": f32},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(args.fused),
-                     "kernel": STEP_KERNEL.get(args.fused, ("?",))[0], "force_ms": force_ms, "cell_ms": prof["cell_ms"],
-                     "tail_ms": prof["tail_ms"], "bytes_per_launch": n * BYTES_PER_UPDATE},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(args.fused, args.precision),
+                     "kernel": STEP_KERNEL.get((args.fused, args.precision), ("?",))[0], "force_ms": force_ms,
+                     "cell_ms": prof["cell_ms"], "tail_ms": prof["tail_ms"], "bytes_per_launch": n * bpu,
+                     "bytes_per_update": bpu},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
@@ -747,6 +810,10 @@ def parse_args(argv=None):
     ap.add_argument("--min-window-s", type=float, default=0.5,
                     help="the timed region repeats passes of --steps until it lasts this long")
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c5"])
+    ap.add_argument("--precision", type=int, default=64, choices=[32, 64],
+                    help="engine arithmetic: 64 (default; the reference's double) or 32")
+    ap.add_argument("--no-f32-leg", dest="f32_leg", action="store_false",
+                    help="skip the secondary fp32-engine window of an fp64 run")
     ap.add_argument("--graph-steps", type=int, default=32)
     ap.add_argument("--waves", type=int, default=4)
     ap.add_argument("--chunk-order", type=int, default=1)
@@ -762,7 +829,7 @@ def parse_args(argv=None):
     ap.add_argument("--list-waves", type=int, default=0,
                     help="list step waves per tile: 2 or 4 (0: 2 with several replicas per GPU, else 4)")
     ap.add_argument("--fused", type=int, default=3,
-                    help="3: list step (default), 2: 2-launch rebuild step, 1: 4-launch step, 0: unfused")
+                    help="3: list step (default); fp32 engines only: 2 the 2-launch rebuild step, 0 unfused")
     ap.add_argument("--profile-steps", type=int, default=50)
     ap.add_argument("--replicas-per-gpu", type=int, default=4,
                     help="independent trajectories per GPU, each its own engine + stream (1 = single trajectory)")

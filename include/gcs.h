@@ -66,8 +66,8 @@ extern "C" {
 #endif
 
 /* 2: gcs_run_stats gained fused_contact_steps (an out-struct grew: callers built against 1 must rebuild)
- * 3: gcs_system_desc.reserved became .precision (0 = fp64); gcs_run_stats lost the small-path counters;
- *    GCS_OPT_SMALL_PATH and GCS_OPT_FUSED_STEP 1 are gone */
+ * 3: gcs_system_desc.reserved became .precision (0 = fp64); gcs_run_stats lost the small-path counters and
+ *    gained density_probes; gcs_list_stats gained deal; GCS_OPT_SMALL_PATH and GCS_OPT_FUSED_STEP 1 are gone */
 #define GCS_ABI_VERSION 3
 
 /* arithmetic precision of an engine (gcs_system_desc.precision) */
@@ -393,6 +393,7 @@ typedef struct gcs_list_stats {
     int32_t pair_classes;             /* distinct (a, b) pair-factor classes */
     int32_t capacity;                 /* list entries per particle */
     int64_t sync_stalls;              /* multi-block cell-scan look-backs that gave up waiting; must stay 0 */
+    int64_t deal;                     /* the chunk deal the list build applies (GCS_OPT_LIST_DEAL resolved) */
 } gcs_list_stats;
 int gcs_engine_get_list_stats(gcs_engine* e, gcs_list_stats* out);
 
@@ -408,6 +409,7 @@ typedef struct gcs_run_stats {
     int64_t graphs_captured;  /* captures (a cache miss: new phase / parity / length, or changed settings) */
     int64_t graphs_cached;    /* captured sequences held now */
     int64_t fused_contact_steps; /* list steps that counted a deferred contact update (gcs_engine_contacts_update) */
+    int64_t density_probes;   /* fresh fp32 chains whose mean neighbour count was probed (GCS_OPT_DENSE_NEIGHBORS) */
 } gcs_run_stats;
 int gcs_engine_get_run_stats(gcs_engine* e, gcs_run_stats* out);
 

@@ -4,7 +4,7 @@
     python tests/golden/gen_oracle_fixtures.py        # from the repo root; builds the oracle if needed
 
 Items: two-particle KATs (energy, x force) of softcore A/B, semispring, softwell and force flux at 16 radii; the C1
-pair sets within 0.24 and 0.30 (strict fp32 predicate, i < j); the C1 interphase forces, energy per kind and
+pair sets within 0.24 and 0.30 (strict fp32 predicate and strict fp64 predicate, i < j); the C1 interphase forces, energy per kind and
 reactions at the step-0 schedule; C1 positions and context after 1 and 10 BD steps with injected reference-order
 noise (seed 123); a quantize table."""
 import sys
@@ -28,7 +28,8 @@ def main(out=ROOT / "tests" / "golden" / "oracle_golden.npz"):
     x0 = np.asarray(design.positions, dtype=np.float64)
     rec["c1_x0"] = x0
     for d in G.PAIR_DISTANCES:
-        rec[f"c1_pairs_{int(round(d * 100)):03d}"] = oracle.search_neighbors(x0, d).astype(np.int32)
+        rec[f"c1_pairs_{int(round(d * 100)):03d}"] = oracle.search_neighbors(x0, d, 32).astype(np.int32)
+        rec[f"c1_pairs64_{int(round(d * 100)):03d}"] = oracle.search_neighbors(x0, d, 64).astype(np.int32)
     rec["c1_forces"] = s.compute_forces()
     tot, parts = s.compute_energy()
     rec["c1_energy"] = np.array([tot]) if np.isscalar(tot) else np.asarray(tot)

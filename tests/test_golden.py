@@ -53,7 +53,9 @@ def test_oracle_reproduces_c1():
     assert np.array_equal(np.asarray(design.positions, dtype=np.float64), GOLD["c1_x0"])
     for d in G.PAIR_DISTANCES:
         exp = GOLD[f"c1_pairs_{int(round(d * 100)):03d}"]
-        assert np.array_equal(oracle.search_neighbors(GOLD["c1_x0"], d), exp)
+        assert np.array_equal(oracle.search_neighbors(GOLD["c1_x0"], d, 32), exp)
+        exp64 = GOLD[f"c1_pairs64_{int(round(d * 100)):03d}"]
+        assert np.array_equal(oracle.search_neighbors(GOLD["c1_x0"], d, 64), exp64)
     assert np.allclose(s.compute_forces(), GOLD["c1_forces"], rtol=1e-9, atol=1e-9)
     tot, parts = s.compute_energy()
     assert tot == pytest.approx(float(GOLD["c1_energy"][0]), rel=1e-10)

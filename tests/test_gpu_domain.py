@@ -5,6 +5,7 @@ host-staged over gloo: RCCL refuses two ranks on one GPU), and the engine-issued
 engine, each other and the fp64 oracle.  Both decomposed step shapes: the list step (k_lstep<..., DOM>, the default)
 and the tile step (GCS_OPT_FUSED_STEP 0); both geometries: z-slabs and recursive-bisection boxes (2 x 2 x 2 at 8).
 
+The decomposition runs on fp32 engines (GCS_PRECISION_F32; the fp64 engine rejects set_domain).
 Tolerances: positions |dx| <= 2e-5 after 30 steps (fp32; the domains' cell lists order the pair sums differently
 from the single engine's), wall semiaxes relative 1e-7; the protocol flags (bond beyond the halo, band over
 capacity, lost particle, displacement beyond the halo) must stay clear."""
@@ -31,7 +32,7 @@ SEED = 99
 
 
 def _engine(design, cfg, fused=None):
-    e, _ = interphase.build_interphase(Engine, design, cfg, device=0)
+    e, _ = interphase.build_interphase(Engine, design, cfg, device=0, precision=32)
     e.set_schedule(**interphase.interphase_schedule(cfg))
     if fused is not None:
         e.set_option(A.OPT_FUSED_STEP, fused)
@@ -193,7 +194,7 @@ def _rank_main(rank, world, port, out_dir, config):
     from gcs.engine import Engine as E
     dist.init_process_group("gloo", rank=rank, world_size=world)
     design, cfg = (S.make_c1() if config == "c1" else S.make_c2()), IC()
-    e, _ = I.build_interphase(E, design, cfg, device=0)
+    e, _ = I.build_interphase(E, design, cfg, device=0, precision=32)
     e.set_schedule(**I.interphase_schedule(cfg))
     boxes = (D.plan_slabs(design.positions[:, 2], world) if config == "c1"
              else D.plan_boxes(design.positions, world))

@@ -214,6 +214,27 @@ def test_dense_start_takes_tile_step():
     assert st2["active"] == 1 and st2["builds"] >= 1, st2  # (one build at the start: the period exceeds 16 steps)
 
 
+def test_dense_chain_keeps_its_verdict_across_chunks():
+    """a dense fp32 chain (C5's synthetic start: the tile step) run as two chunks equals one run bit for bit and
+    probes its density once: the verdict holds while the chain continues"""
+    cfg5 = resolution_scaled(InterphaseConfig(), 10.0)
+    d5 = synthetic.make_c5()
+    runs = []
+    for chunks in ([6], [2, 4]):
+        e, _ = interphase.build_interphase(Engine, d5, cfg5, precision=32)
+        e.set_schedule(**interphase.interphase_schedule(cfg5))
+        e.set_option(A.OPT_DENSE_NEIGHBORS, 48)
+        first = 0
+        for c in chunks:
+            e.run(c, first_step=first, temperature=cfg5.temperature, timestep=cfg5.timestep, seed=99)
+            first += c
+        runs.append((e.get_positions(), e.run_stats()["density_probes"], e.list_stats()["active"]))
+        e.close()
+    assert runs[0][2] == 0 and runs[1][2] == 0  # the tile step
+    assert runs[0][1] == 1 and runs[1][1] == 1, (runs[0][1], runs[1][1])
+    assert np.array_equal(runs[0][0], runs[1][0])
+
+
 def test_list_and_rebuild_step_agree_on_neighbour_count():
     """the pair set is the same: the mean neighbour count the list step reports equals the tile kernel's"""
     cfg = InterphaseConfig()
@@ -250,6 +271,7 @@ def test_list_deal_patterns(c1_design, waves, deal):
     e, o = _pair(c1_design, cfg, ctx=LATE, list_waves=waves, list_deal=A.list_deal(deal))
     _run_both(e, o, 40, LATE["step"], cfg, 7)
     assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[64]
+    assert e.list_stats()["deal"] == A.list_deal(deal)  # the pattern the build applied (not the default's)
     nb = []
     for d in (A.list_deal(deal), 0):  # from the same state
         s = _list_engine(c1_design, cfg, list_waves=waves, list_deal=d)
