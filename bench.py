@@ -59,10 +59,13 @@ STATE_FILE = ROOT / "benchdata" / "c2_interphase_step300000.npz"
 
 def dist_setup(backend="gloo"):
     """gloo on CPU tensors: the barrier, the max over ranks and (decomposed runs) the RCCL id hand-out; the
-    decomposed runs' data path (reaction allreduce, band exchange) is RCCL issued by the engine itself."""
+    decomposed runs' data path (reaction allreduce, band exchange) is RCCL issued by the engine itself.
+    GCS_BENCH_SAME_DEVICE=1 (tests on a one-GPU box): every rank on device 0."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if os.environ.get("GCS_BENCH_SAME_DEVICE") == "1":
+        local = 0
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -631,6 +634,9 @@ def replica_main(args):
     # (3 passes at least: the first pass of a run starts with an eager forced rebuild, which shifts its graphs by a
     # step, so the timed passes' first shape appears in the warm-up's second pass at the earliest)
     warm_passes = max(3, math.ceil(warm / K))
+    if os.environ.get("GCS_MAPS_OUT"):  # (diagnostics) this process's mappings before its first graph launch
+        with open("/proc/self/maps") as src, open(os.environ["GCS_MAPS_OUT"], "w") as dst:
+            dst.write(src.read())
     enqueue_all(K)
     sync_all()
     t0 = time.perf_counter()
@@ -676,6 +682,7 @@ def replica_main(args):
     steps = passes * K
     el_max = max_over_ranks(dist, el)
     rank_values = gather_over_ranks(dist, n * R * steps / el)
+    rank_seeds = gather_over_ranks(dist, float(seed))  # every rank's first trajectory's noise seed (all distinct)
     after = nxt[0]
 
     # per-kernel durations with HIP events on the engine's stream (replica 0 alone, after the timed region)
@@ -774,6 +781,7 @@ def replica_main(args):
         "timed_runs": timed_runs,
         "timed_s": el_max,
         "per_rank_values": rank_values,
+        "per_rank_seeds": rank_seeds,
         "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, {R} independent "
                                f"trajectories per GPU, window from step {window} "
                                f"(core_scale {ctx['core_scale']:.4f})",

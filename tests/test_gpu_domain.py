@@ -213,7 +213,7 @@ def _steps(config):
     return STEPS if config == "c1" else 20
 
 
-@pytest.mark.parametrize("config,world", [("c1", 2), ("c2", 4)])
+@pytest.mark.parametrize("config,world", [("c1", 2), ("c2", 4), ("c2", 8)])
 def test_engine_domains_processes_host_staged(tmp_path, config, world):
     """`world` processes, one engine domain each (device 0), reaction allreduce and bands over gloo: within 2e-5 of
     the single engine; with two domains also bit for bit the in-process run (the same kernels; a two-term sum is
