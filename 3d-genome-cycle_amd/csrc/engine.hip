@@ -264,7 +264,6 @@ struct gcs_engine {
     int list_cap = 1024;        // GCS_OPT_LIST_CAP: list entries per particle (split over the tile's waves)
     size_t list_alloc = 0;      // allocated entries
     int list_skin_pm = 500;     // GCS_OPT_LIST_SKIN: skin in 1/1000 of the pair cutoff
-    bool list_skin_set = false; // the option was given (else the resident step takes its own default, kResSkinPm)
     int list_every_opt = 0;     // GCS_OPT_LIST_EVERY: rebuild period in steps (0: from the noise amplitude)
     int list_every = 1;         // the period of the current run
     int list_waves = 4;         // GCS_OPT_LIST_WAVES: waves per tile (2: more tiles resident, for replica runs)
@@ -289,20 +288,6 @@ struct gcs_engine {
     double chain_dt = 0;  // the timestep begin_run last wrote to ctx->dt_used
     int chain_version = -1;
 
-    // resident small systems (GCS_OPT_RESIDENT, kernels.hip k_resident): one launch of one workgroup per run chunk
-    // for N <= kResMax; its list state persists here between launches (res_chain: the chain's lists are the
-    // resident kernel's, so a continuing resident run restores them instead of rebuilding)
-    int res_opt = 1;
-    bool res_active = false;  // the current (last) run takes the resident step
-    int res_cap = 0;  // list entries per particle the LDS budget allows (0: not computed / not eligible)
-    int res_n = 0;    // the particle count the buffers were sized for
-    unsigned short* r_list = nullptr;
-    int* r_lcount = nullptr;
-    float4* r_bpos = nullptr;
-    int* r_cstart = nullptr;
-    unsigned short* r_cidx = nullptr;
-    unsigned long long* r_dbg = nullptr;
-    bool res_chain = false;
 };
 
 namespace {
@@ -807,13 +792,7 @@ bool list_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) == 3 &
 bool fused_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) != 0 && !spacestep; }
 bool rebuild_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) == 2 && !spacestep; }
 
-// the skin of the current run's lists: the option, or the default of the step shape (the resident step rebuilds
-// in LDS at little cost, so it takes a thinner skin: shorter lists that fit its LDS budget)
-float list_skin(const gcs_engine* e)
-{
-    const int pm = (e->res_active && !e->dom && !e->list_skin_set) ? kResSkinPm : e->list_skin_pm;
-    return 1e-3f * (float)pm * e->fa.pf.pair_dist;
-}
+float list_skin(const gcs_engine* e) { return 1e-3f * (float)e->list_skin_pm * e->fa.pf.pair_dist; }
 
 // the list build's chunk deal (kernels.hip deal_nth): the option, or the default for the waves per tile
 unsigned long long list_deal(const gcs_engine* e)
@@ -1206,88 +1185,9 @@ int flush_contacts(gcs_engine* e);  // (below)
 void end_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps)
 {
     e->chain_valid = fused_path(e, cfg->spacestep > 0);
-    e->res_chain = false;
     e->dense_chain = dense_switch(e) && cfg->spacestep <= 0;
     e->chain_step = first_step + steps;
     e->chain_version = e->topo_version;
-}
-
-// the resident step's list capacity: what the dynamic LDS budget leaves for the lists (0: the system does not fit)
-int res_capacity(const gcs_engine* e)
-{
-    const size_t fixed = res_lds_bytes(e->n, 0, e->prec);
-    if (e->n < 1 || e->n > kResMax || fixed >= kResLdsLimit) return 0;
-    const size_t room = (kResLdsLimit - fixed - 16) / (2 * (size_t)e->n);
-    const int cap = (int)std::min<size_t>(std::min(kResCapMax, e->list_cap), room);
-    return cap >= kResCapMin ? cap : 0;
-}
-// a fixed-timestep list-step run of an undecomposed system of <= kResMax particles takes the resident step
-bool resident_path(const gcs_engine* e, bool spacestep)
-{
-    return e->res_opt != 0 && list_path(e, spacestep) && !e->dom && res_capacity(e) > 0;
-}
-int ensure_resident(gcs_engine* e)
-{
-    const int cap = res_capacity(e);
-    if (e->r_list && e->res_n == e->n && e->res_cap == cap) return GCS_OK;
-    dfree(e->r_list);
-    dfree(e->r_lcount);
-    dfree(e->r_bpos);
-    dfree(e->r_cstart);
-    dfree(e->r_cidx);
-    e->res_chain = false;
-    int rc;
-    if ((rc = dalloc(&e->r_list, (size_t)cap * e->n)) || (rc = dalloc(&e->r_lcount, e->n)) ||
-        (rc = dalloc(&e->r_bpos, e->n)) || (rc = dalloc(&e->r_cstart, kResCells + 1)) || (rc = dalloc(&e->r_cidx, e->n)))
-        return rc;
-    e->res_n = e->n;
-    e->res_cap = cap;
-    return GCS_OK;
-}
-// The steps of a resident run: launches of up to kResChunk steps, each restoring the list state the last one left
-// (a run start without continuity rebuilds first, as the list step does)
-int run_resident(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps, bool cont)
-{
-    int rc = ensure_resident(e);
-    if (rc) return rc;
-    const ForceArgs a = list_args(e);
-    ResArgs ra;
-    ra.flags = (e->sched_flags != 0 ? 1 : 0) | 4;  // the schedule; neighbour statistics (ctx->neighbors)
-    ra.period = e->list_every;
-    ra.cap = e->res_cap;
-    ra.list = e->r_list;
-    ra.lcount = e->r_lcount;
-    ra.bpos = e->r_bpos;
-    ra.cstart = e->r_cstart;
-    ra.cidx = e->r_cidx;
-    ra.force_build = cont ? 0 : 1;
-    ra.dbg = nullptr;
-    unsigned long long hd[5] = {0, 0, 0, 0, 0};
-    const bool times = std::getenv("GCS_RES_TIMES") != nullptr;
-    if (times) {
-        if (!e->r_dbg && (rc = dalloc(&e->r_dbg, 5))) return rc;
-        HIPCHK(hipMemsetAsync(e->r_dbg, 0, 5 * sizeof(unsigned long long), e->stream));
-        ra.dbg = e->r_dbg;
-    }
-    for (int64_t done = 0; done < steps;) {
-        ra.steps = (int)std::min<int64_t>(kResChunk, steps - done);
-        launch_resident(e->stream, e->ctx, a, ra);
-        HIPCHK(hipGetLastError());
-        ra.force_build = 0;
-        done += ra.steps;
-        e->rstats.resident_launches++;
-        e->rstats.resident_steps += ra.steps;
-    }
-    if (times) {  // (diagnostics: synchronous)
-        HIPCHK(hipMemcpyAsync(hd, e->r_dbg, sizeof(hd), hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(hipStreamSynchronize(e->stream));
-        const double k = hd[4] ? 1e-2 / (double)hd[4] : 0.0;  // 100 MHz ticks -> us per step
-        std::fprintf(stderr, "resident n=%d prec=%d cap=%d steps=%llu us/step: build %.2f forces %.2f barrier1 %.2f "
-                     "tail+barrier2 %.2f\n", e->n, e->prec, e->res_cap, hd[4], hd[0] * k, hd[1] * k, hd[2] * k, hd[3] * k);
-    }
-    (void)cfg;
-    (void)first_step;
-    return GCS_OK;
 }
 
 }  // namespace
@@ -1578,12 +1478,6 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->psort[0]);
     dfree(e->psort[1]);
     dfree(e->skmu);
-    dfree(e->r_list);
-    dfree(e->r_lcount);
-    dfree(e->r_bpos);
-    dfree(e->r_cstart);
-    dfree(e->r_cidx);
-    dfree(e->r_dbg);
     dfree(e->sbrow);
     dfree(e->lticket);
     dfree(e->ptype);
@@ -1997,23 +1891,9 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
     if (e->prec == 64 && !spacestep && !e->list_ok)
         return fail(GCS_ESTATE, "the fp64 engine's fixed-timestep step is the list step: it needs a neighbor soft-core "
                                 "field, <= 256 (a, b) pair classes and < 2^24 particles (use GCS_PRECISION_F32)");
-    const bool res = resident_path(e, spacestep);
-    // a resident chain continues when the last run was resident and ended where this one starts
-    const bool res_cont = res && e->res_chain && e->chain_valid && e->chain_step == first_step &&
-                          e->chain_version == e->topo_version;
-    if (!list_path(e, spacestep) || res)
+    if (!list_path(e, spacestep))
         if ((rc = flush_contacts(e))) return rc;
-    if (!res && e->res_chain) e->chain_valid = false;  // the list step's state is not the resident kernel's
-    e->res_active = res;
     if ((rc = begin_run(e, cfg, first_step))) return rc;
-    if (res) {
-        if ((rc = run_resident(e, cfg, first_step, steps, res_cont))) return rc;
-        end_run(e, cfg, first_step, steps);
-        e->res_chain = true;
-        if (steps & 1) e->parity ^= 1;
-        if (cfg->noise == GCS_NOISE_INJECTED) e->noise_cursor += steps;
-        return GCS_OK;
-    }
 
     const int G = e->graph_steps;
     const GraphKey key = run_key(e, cfg, spacestep);
@@ -3147,7 +3027,6 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
     if (option == GCS_OPT_LIST_SKIN) {
         if (value < 1 || value > 4000) return fail(GCS_EINVAL, "list skin must be in [1, 4000] per mille of the cutoff");
         e->list_skin_pm = (int)value;
-        e->list_skin_set = true;
         drop_graph(e);
         return GCS_OK;
     }
@@ -3221,11 +3100,6 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         if (value < 0 || value > 2) return fail(GCS_EINVAL, "split tiles must be 0, 1 or 2");
         e->fa.split = (int)value;
         drop_graph(e);
-        return GCS_OK;
-    }
-    if (option == GCS_OPT_RESIDENT) {
-        if (value != 0 && value != 1) return fail(GCS_EINVAL, "resident must be 0 (off) or 1 (on for N <= 2048)");
-        e->res_opt = (int)value;
         return GCS_OK;
     }
     if (option == GCS_OPT_WAVES_PER_TILE) {

@@ -419,39 +419,6 @@ void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, con
                              const int* shared, int nshared, float4* bands, int npeer, int band_stride);
 int list_step_grid(int n);
 bool list_u16(int n);  // list entries are 16-bit slot indices (N <= 65536)
-// resident small systems (N <= kResMax; kernels.hip k_resident): every fixed-timestep step of a run chunk in ONE launch of
-// one workgroup holding the system in LDS.  Its list state (lists [cap][N] u16, counts, build positions, the build's
-// cell list) persists in global memory between launches, so a chunked run rebuilds where one run does.
-constexpr int kResThreads = 1024;
-constexpr int kResMax = 2048;   // particles (two per thread)
-constexpr int kResCells = 2048; // cells of the in-LDS list build
-constexpr size_t kResLdsLimit = 160 * 1024 - 12 * 1024;  // dynamic LDS budget (the rest: the kernel's static LDS)
-constexpr int kResCapMin = 16;   // fewer list entries per particle than this: the system does not take the path
-constexpr int kResCapMax = 128;
-constexpr int kResChunk = 8192;  // steps per launch
-constexpr int kResSkinPm = 200;  // default skin of the resident step's lists, 1/1000 of the pair cutoff
-__host__ __device__ inline size_t res_align(size_t b) { return (b + 15) & ~(size_t)15; }
-// dynamic LDS bytes of k_resident: positions (16 or 32 B), lists (cap x 2 B), counts (4 B), classes (1 B) per
-// particle, the build's cell starts (4 B x (kResCells + 1)) and particles by cell (2 B per particle)
-__host__ __device__ inline size_t res_lds_bytes(int n, int cap, int prec)
-{
-    return res_align((size_t)n * (prec == 64 ? 32 : 16)) + res_align((size_t)cap * n * 2) + res_align((size_t)n * 4) +
-           res_align((size_t)(kResCells + 1) * 4) + res_align((size_t)n * 2) + res_align((size_t)n);
-}
-struct ResArgs {
-    int steps;         // steps of this launch
-    int flags;         // kLFlagSched | kLFlagStats (list_tail_apply)
-    int force_build;   // no continuity: build before the first step (else the persisted lists are restored)
-    int period;        // rebuild period M: the step that starts at s rebuilds when s % M == 0 (as the list step)
-    int cap;           // list entries per particle
-    unsigned short* list;  // [cap][N]
-    int* lcount;           // [N] count | kListOverflow
-    float4* bpos;          // [N] build positions (fp32 roundings; read by the steps from global memory)
-    int* cstart;           // [kResCells + 1]
-    unsigned short* cidx;  // [N]
-    unsigned long long* dbg;  // GCS_RES_TIMES: [5] wall-clock sums per phase + steps (nullptr: off)
-};
-void launch_resident(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const ResArgs& ra);
 void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceArgs& a, bool fused);
 // fp64 force / energy evaluation on the current cell list (one thread per sorted slot; kernels.hip k_eval64):
 // kModeForce -> a.dforce_out + partial rows a.dpart [blocks][8] (reactions in[3], out[3], max mu|F|, neighbours),

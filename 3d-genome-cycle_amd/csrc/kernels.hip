@@ -3595,398 +3595,6 @@ __global__ __launch_bounds__(256) void k_red64(DevCtx* ctx, ForceArgs a, int row
     }
 }
 
-// ----------------------------------------------------------------------------------------------------
-// resident small systems (N <= kResMax: C3's mitotic stages, 586 / 1,172 particles, and C1's 1,002): every step of a
-// run chunk inside ONE launch of ONE workgroup (1024 threads) that holds the positions (the step reads them, then
-// overwrites them after a barrier), the neighbour lists, the build's cell list and the context in LDS.  At this size
-// the multi-workgroup list step is ~14 us of launch, memory round trips and cross-workgroup tail per step for ~10
-// workgroups of work; here a step is the pair loop over LDS lists, the particle-local terms (bond tables from L2),
-// the noise, the update, one fixed-order block reduction and the context update by thread 0, between two barriers.
-//
-// Lists are Verlet lists by particle index at cutoff + skin, built in LDS at steps = 0 (mod M) and at a chunk start
-// without continuity (as the list step, so a chunked run rebuilds where one run does; the lists, counts and cell
-// list go back to global memory at the end of a launch and are restored by the next; the build positions live in
-// global memory).  A particle whose displacement since the build could let a partner escape its list, or whose list
-// overflowed, is evaluated by an exact search of the build's cell list with radius cutoff + largest displacement:
-// the pair set is exact.  Reductions are DPP wave totals combined in wave order by thread 0: bitwise reproducible.
-// Per particle only the new position is carried in registers across the barrier (the 128 VGPRs of a 1024-thread
-// workgroup hold one particle's step): build positions, constants and bond rows come from global memory (L2).
-
-constexpr int kResWaves = kResThreads / 64;
-constexpr int kResPer = kResMax / kResThreads;  // particles per thread
-
-template <typename R>
-__global__ __launch_bounds__(kResThreads) void k_resident(DevCtx* __restrict__ gctx, ForceArgs a, ResArgs ra)
-{
-    using R4 = real4<R>;
-    using R2 = real2<R>;
-    extern __shared__ __align__(16) unsigned char res_smem[];
-    __shared__ DevCtx s_ctx;
-    __shared__ double s_sched[kSchedCount];
-    __shared__ R2 s_tab[kMaxTypes];
-    __shared__ double s_red[9][kResWaves];
-    __shared__ int s_wsum[kResWaves];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int n = a.n, cap = ra.cap;
-    const FieldPrm<R>& P = St<R>::prm(a);
-    unsigned char* sp = res_smem;
-    R4* const s_pos = reinterpret_cast<R4*>(sp);
-    sp += res_align((size_t)n * sizeof(R4));
-    unsigned short* s_list = reinterpret_cast<unsigned short*>(sp);
-    sp += res_align((size_t)cap * n * 2);
-    int* s_lcount = reinterpret_cast<int*>(sp);
-    sp += res_align((size_t)n * 4);
-    int* s_cstart = reinterpret_cast<int*>(sp);
-    sp += res_align((size_t)(kResCells + 1) * 4);
-    unsigned short* s_cidx = reinterpret_cast<unsigned short*>(sp);
-    sp += res_align((size_t)n * 2);
-    unsigned char* s_cls = sp;
-
-    // the system into LDS: context, schedule, class table, positions, classes; the persisted list state
-    if (tid == 0) s_ctx = *gctx;
-    if (tid < kSchedCount) s_sched[tid] = a.sched[tid];
-    for (int t = tid; t < a.ntypes; t += kResThreads) s_tab[t] = St<R>::type_ab(a)[t];
-    __syncthreads();
-    {
-        const R4* pcur = St<R>::pos(a, s_ctx.parity);
-        for (int i = tid; i < n; i += kResThreads) {
-            s_pos[i] = pcur[i];
-            s_cls[i] = a.ptype ? (unsigned char)a.ptype[i] : 0;
-        }
-        if (!ra.force_build) {
-            for (int q = tid; q < cap * n; q += kResThreads) s_list[q] = ra.list[q];
-            for (int i = tid; i < n; i += kResThreads) {
-                s_lcount[i] = ra.lcount[i];
-                s_cidx[i] = ra.cidx[i];
-            }
-            for (int c = tid; c <= kResCells; c += kResThreads) s_cstart[c] = ra.cstart[c];
-        }
-    }
-    // the particle-local terms read bonded partners through the position pointers: point them at LDS (flat addresses)
-    ForceArgs la = a;
-    if constexpr (sizeof(R) == 4) {
-        la.pos0 = la.pos1 = reinterpret_cast<float4*>(s_pos);
-    } else {
-        la.dpos0 = la.dpos1 = reinterpret_cast<double4*>(s_pos);
-    }
-    __syncthreads();
-
-    // GCS_RES_TIMES: thread 0's wall clock summed per phase (build, forces + update, after the first barrier,
-    // after the second) over the launch
-    unsigned long long tb = 0, tf = 0, t1 = 0, t2 = 0;
-    for (int k = 0; k < ra.steps; ++k) {
-        const R4* __restrict__ cur = s_pos;
-        const unsigned long long c0 = ra.dbg ? wall_clock64() : 0ull;
-        // ---- rebuild (uniform decision: every thread reads the same context)
-        if (a.has_pair && ((k == 0 && ra.force_build) || (s_ctx.step % ra.period) == 0)) {
-            const float rcb = pair_cutoff(a, s_ctx.cs) + a.list_skin;
-            float l0 = 3.0e38f, l1 = 3.0e38f, l2 = 3.0e38f, h0 = -3.0e38f, h1 = -3.0e38f, h2 = -3.0e38f;
-            for (int i = tid; i < n; i += kResThreads) {
-                const R4 p = cur[i];
-                const float x = (float)p.x, y = (float)p.y, z = (float)p.z;
-                l0 = fminf(l0, x);
-                l1 = fminf(l1, y);
-                l2 = fminf(l2, z);
-                h0 = fmaxf(h0, x);
-                h1 = fmaxf(h1, y);
-                h2 = fmaxf(h2, z);
-            }
-            l0 = wave_total_min_f(l0);
-            l1 = wave_total_min_f(l1);
-            l2 = wave_total_min_f(l2);
-            h0 = wave_total_max_f(h0);
-            h1 = wave_total_max_f(h1);
-            h2 = wave_total_max_f(h2);
-            if (lane == 0) {
-                s_red[0][wave] = l0;
-                s_red[1][wave] = l1;
-                s_red[2][wave] = l2;
-                s_red[3][wave] = h0;
-                s_red[4][wave] = h1;
-                s_red[5][wave] = h2;
-            }
-            for (int c = tid; c <= kResCells; c += kResThreads) s_cstart[c] = 0;
-            __syncthreads();
-            if (tid == 0) {
-                float blo[3], bhi[3];
-#pragma unroll
-                for (int d = 0; d < 3; ++d) {
-                    float lo = (float)s_red[d][0], hi = (float)s_red[3 + d][0];
-#pragma unroll
-                    for (int w = 1; w < kResWaves; ++w) {
-                        lo = fminf(lo, (float)s_red[d][w]);
-                        hi = fmaxf(hi, (float)s_red[3 + d][w]);
-                    }
-                    blo[d] = lo;
-                    bhi[d] = hi;
-                }
-                s_ctx.lgrid = make_grid(blo, bhi, rcb, kResCells, 1);
-                s_ctx.lrc_b = pair_cutoff(a, s_ctx.cs);
-                s_ctx.ldisp = 0.f;
-                s_ctx.lbuilds += 1;
-            }
-            __syncthreads();
-            const Grid g = s_ctx.lgrid;
-            for (int i = tid; i < n; i += kResThreads) {
-                const R4 p = cur[i];
-                atomicAdd(&s_cstart[cell_index(g, (float)p.x, (float)p.y, (float)p.z)], 1);
-            }
-            __syncthreads();
-            {  // inclusive scan of the counts (the cell ends): kC cells per thread, DPP wave scans + wave totals
-                constexpr int kC = (kResCells + 1 + kResThreads - 1) / kResThreads;
-                const int c0 = kC * tid;
-                int v[kC], sum = 0;
-#pragma unroll
-                for (int q = 0; q < kC; ++q) {
-                    v[q] = c0 + q <= g.ncell ? s_cstart[c0 + q] : 0;
-                    sum += v[q];
-                }
-                int incl = sum;
-                GCS_DPP_SCAN(dpp_i, add_i, 0, incl)
-                if (lane == 63) s_wsum[wave] = incl;
-                __syncthreads();
-                int run = incl - sum;
-                for (int w = 0; w < wave; ++w) run += s_wsum[w];
-#pragma unroll
-                for (int q = 0; q < kC; ++q) {
-                    run += v[q];
-                    if (c0 + q <= g.ncell) s_cstart[c0 + q] = run;
-                }
-            }
-            __syncthreads();
-            // arrival-order filing (the ends count down to the starts) into row 0 of the lists (rewritten below),
-            // then each particle's rank by index inside its cell: the cell list is independent of the arrival order
-            unsigned short* const arr = s_list;
-            for (int i = tid; i < n; i += kResThreads) {
-                const R4 p = cur[i];
-                arr[atomicSub(&s_cstart[cell_index(g, (float)p.x, (float)p.y, (float)p.z)], 1) - 1] = (unsigned short)i;
-            }
-            __syncthreads();
-            for (int i = tid; i < n; i += kResThreads) {
-                const R4 p = cur[i];
-                const int c = cell_index(g, (float)p.x, (float)p.y, (float)p.z);
-                const int b = s_cstart[c], e = s_cstart[c + 1];
-                int r = 0;
-                for (int t = b; t < e; ++t) r += arr[t] < i ? 1 : 0;
-                s_cidx[b + r] = (unsigned short)i;
-            }
-            __syncthreads();
-            // the lists: every particle within rcb in the 27 neighbouring cells, in cell order.  The test is fp32 with
-            // a 1e-5 margin (the roundings of the coordinates are ~1e-7 of them): a superset of the pairs within rcb
-            const float rcb2 = (rcb * 1.00001f) * (rcb * 1.00001f);
-            const int nx = g.n[0], ny = g.n[1], nz = g.n[2];
-            for (int i = tid; i < n; i += kResThreads) {
-                const R4 p = cur[i];
-                const float px = (float)p.x, py = (float)p.y, pz = (float)p.z;
-                const int c = cell_index(g, px, py, pz);
-                const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
-                int cnt = 0;
-                for (int z = max(cz - 1, 0); z <= min(cz + 1, nz - 1); ++z)
-                    for (int y = max(cy - 1, 0); y <= min(cy + 1, ny - 1); ++y) {
-                        const int base = (z * ny + y) * nx;
-                        const int jb = s_cstart[base + max(cx - 1, 0)], je = s_cstart[base + min(cx + 1, nx - 1) + 1];
-                        for (int t = jb; t < je; ++t) {
-                            const int j = s_cidx[t];
-                            const R4 o = cur[j];
-                            const float dx = px - (float)o.x, dy = py - (float)o.y, dz = pz - (float)o.z;
-                            if (j != i && fmaf(dz, dz, fmaf(dy, dy, dx * dx)) < rcb2) {
-                                if (cnt < cap) s_list[cnt * n + i] = (unsigned short)j;
-                                ++cnt;
-                            }
-                        }
-                    }
-                s_lcount[i] = min(cnt, cap) | (cnt > cap ? kListOverflow : 0);
-                ra.bpos[i] = make_float4(px, py, pz, 0.f);
-            }
-            __syncthreads();
-        }
-
-        const unsigned long long c1 = ra.dbg ? wall_clock64() : 0ull;
-        // ---- forces, particle-local terms, noise, update
-        // (the step's constants from the LDS context: wave-uniform, moved to scalar registers)
-        const R cs = uniform((R)s_ctx.cs);
-        const R scale = a.pair_scaled ? cs : R(1);
-        const R sa = P.pa_sig * scale, sbb = P.pb_sig * scale;
-        const R k2a = uniform(R(1) / (sa * sa)), k2b = uniform(R(1) / (sbb * sbb));
-        const R kA = uniform(R(0.5) * R(6) * P.pa_eps * k2a), kB = uniform(R(0.5) * R(24) * P.pb_eps * k2b);
-        const R rc = pair_cutoff_r<R>(a, (double)cs), rc2 = uniform(rc * rc);
-        const float rcf = uniform((float)rc);
-        const float D = uniform(s_ctx.ldisp);
-        const float slack = uniform(0.999f * a.list_skin - D - fmaxf(rcf - s_ctx.lrc_b, 0.f));
-        double ri0 = 0, ri1 = 0, ri2 = 0, ro0 = 0, ro1 = 0, ro2 = 0, tn = 0, tf = 0;
-        float tmax = 0.f;
-        // the new positions until the barrier (a thread's second particle: N > 1024): a private array, not unrolled
-        // (one copy of the step's code: unrolled, the two particles' steps spill far more than these 6 words)
-        R nx_[kResPer], ny_[kResPer], nz_[kResPer];
-#pragma unroll 1
-        for (int q = 0; q < kResPer; ++q) {
-            if (q * kResThreads >= n) break;  // (uniform)
-            const int i = tid + q * kResThreads;
-            if (i >= n) break;
-            // global loads first (L2: build position, constants, bond row), the LDS pair loop under them
-            const float4 bp = ra.bpos[i];
-            const R4 km = St<R>::kmu(a)[i];
-            const int2 er = a.has_bonds ? make_int2(a.boff[i], a.boff[i + 1]) : make_int2(0, 0);
-            const R4 pi = cur[i];
-            R fx = 0, fy = 0, fz = 0, nbr = 0;
-            bool fb = false;
-            if (a.has_pair) {
-                const R2 own = s_tab[s_cls[i]];
-                const R ahi = kA * own.x, bhi = kB * own.y;
-                const int cw = s_lcount[i];
-                const int cnt = (cw & kListOverflow) ? 0 : min(cw & kListCountMask, cap);
-                for (int t = 0; t < cnt; ++t) {
-                    const int j = s_list[t * n + i];
-                    list_pair<R>(pi.x, pi.y, pi.z, cur[j], s_tab[s_cls[j]], ahi, bhi, kA, kB, k2a, k2b, rc2, true, fx,
-                                 fy, fz, nbr);
-                }
-                const float ex = (float)(pi.x - (R)bp.x), ey = (float)(pi.y - (R)bp.y), ez = (float)(pi.z - (R)bp.z);
-                fb = sqrtf(fmaf(ez, ez, fmaf(ey, ey, ex * ex))) > slack || (cw & kListOverflow) != 0;
-                if (fb) {  // the build's cells around the current position, radius rc + D
-                    fx = fy = fz = nbr = R(0);
-                    const Grid lg = s_ctx.lgrid;
-                    const float Rr = rcf + D + 1.0e-5f * (rcf + D);
-                    const float px = (float)pi.x, py = (float)pi.y, pz = (float)pi.z;
-                    const int x0 = lgrid_cell(lg, 0, px - Rr), x1 = lgrid_cell(lg, 0, px + Rr);
-                    const int y0 = lgrid_cell(lg, 1, py - Rr), y1 = lgrid_cell(lg, 1, py + Rr);
-                    const int z0 = lgrid_cell(lg, 2, pz - Rr), z1 = lgrid_cell(lg, 2, pz + Rr);
-                    for (int z = z0; z <= z1; ++z)
-                        for (int y = y0; y <= y1; ++y) {
-                            const int base = (z * lg.n[1] + y) * lg.n[0];
-                            const int t0 = s_cstart[base + x0], t1 = s_cstart[base + x1 + 1];
-                            for (int t = t0; t < t1; ++t) {
-                                const int j = s_cidx[t];
-                                list_pair<R>(pi.x, pi.y, pi.z, cur[j], s_tab[s_cls[j]], ahi, bhi, kA, kB, k2a, k2b,
-                                             rc2, j != i, fx, fy, fz, nbr);
-                            }
-                        }
-                }
-            }
-            R en[kEnergyKinds];
-            R rin[3] = {0, 0, 0}, rout[3] = {0, 0, 0};
-            local_terms<kModeStep, GCS_LIST_BOND_BATCH, R>(&s_ctx, la, i, pi.x, pi.y, pi.z, km, fx, fy, fz, en, rin,
-                                                           rout, a.has_bonds ? er : make_int2(-1, -1));
-            R n0, n1, n2;
-            noise3<R>(a, &s_ctx, i, n0, n1, n2);
-            const R mu = km.x, dt = P.timestep;
-            const R amp = r_sqrt(R(2) * P.temperature * mu * dt);
-            const R mdt = mu * dt;
-            const R nxp = pi.x + mdt * fx + amp * n0, nyp = pi.y + mdt * fy + amp * n1, nzp = pi.z + mdt * fz + amp * n2;
-            nx_[q] = nxp;
-            ny_[q] = nyp;
-            nz_[q] = nzp;
-            ri0 += (double)rin[0];
-            ri1 += (double)rin[1];
-            ri2 += (double)rin[2];
-            ro0 += (double)rout[0];
-            ro1 += (double)rout[1];
-            ro2 += (double)rout[2];
-            tn += (double)nbr;
-            tf += fb ? 1.0 : 0.0;
-            if (a.has_pair) {
-                const float gx = (float)(nxp - (R)bp.x), gy = (float)(nyp - (R)bp.y), gz = (float)(nzp - (R)bp.z);
-                tmax = fmaxf(tmax, sqrtf(fmaf(gz, gz, fmaf(gy, gy, gx * gx))));
-            }
-        }
-        // ---- the step's totals: wave totals (DPP), combined in wave order by thread 0, which advances the context
-        ri0 = wave_total_sum_d(ri0);
-        ri1 = wave_total_sum_d(ri1);
-        ri2 = wave_total_sum_d(ri2);
-        ro0 = wave_total_sum_d(ro0);
-        ro1 = wave_total_sum_d(ro1);
-        ro2 = wave_total_sum_d(ro2);
-        tn = wave_total_sum_d(tn);
-        tf = wave_total_sum_d(tf);
-        tmax = wave_total_max_f(tmax);
-        if (lane == 0) {
-            s_red[0][wave] = ri0;
-            s_red[1][wave] = ri1;
-            s_red[2][wave] = ri2;
-            s_red[3][wave] = ro0;
-            s_red[4][wave] = ro1;
-            s_red[5][wave] = ro2;
-            s_red[6][wave] = tn;
-            s_red[7][wave] = tf;
-            s_red[8][wave] = tmax;
-        }
-        const unsigned long long c2 = ra.dbg ? wall_clock64() : 0ull;
-        __syncthreads();  // every read of the step's positions is done
-        const unsigned long long c3 = ra.dbg ? wall_clock64() : 0ull;
-#pragma unroll
-        for (int q = 0; q < kResPer; ++q) {
-            const int i = tid + q * kResThreads;
-            if (i < n) s_pos[i] = mk4<R>(nx_[q], ny_[q], nz_[q], R(0));
-        }
-        if (tid == 0) {
-            ListTotals t;
-#pragma unroll
-            for (int v = 0; v < 8; ++v) {
-                double x = s_red[v][0];
-#pragma unroll
-                for (int w = 1; w < kResWaves; ++w) x += s_red[v][w];
-                if (v < 6) t.react[v] = x;
-                else if (v == 6) t.nbr = x;
-                else t.nfb = (long long)x;
-            }
-            float m = (float)s_red[8][0];
-#pragma unroll
-            for (int w = 1; w < kResWaves; ++w) m = fmaxf(m, (float)s_red[8][w]);
-            t.ld = m;
-            t.nown = 0;
-            ListTailIn tin;
-            tin.s_flags = s_sched[kSchedFlags];
-            tin.s_dt = s_sched[kSchedDt];
-            tin.s_cs0 = s_sched[kSchedCs0];
-            tin.s_csTau = s_sched[kSchedCsTau];
-            tin.s_bs0 = s_sched[kSchedBs0];
-            tin.s_bsTau = s_sched[kSchedBsTau];
-            tin.s_muW = s_sched[kSchedMuW];
-            tin.s_k[0] = s_sched[kSchedK0];
-            tin.s_k[1] = s_sched[kSchedK0 + 1];
-            tin.s_k[2] = s_sched[kSchedK0 + 2];
-            tin.c_step = s_ctx.step;
-            tin.c_cursor = s_ctx.noise_cursor;
-            tin.c_fb = s_ctx.lfallback;
-            tin.c_parity = s_ctx.parity;
-            tin.c_time = s_ctx.time;
-            tin.c_cs = s_ctx.cs;
-            tin.c_bs = s_ctx.bs;
-            tin.c_w[0] = s_ctx.wall[0];
-            tin.c_w[1] = s_ctx.wall[1];
-            tin.c_w[2] = s_ctx.wall[2];
-            list_tail_apply(&s_ctx, a, tin, t, ra.flags & (kLFlagSched | kLFlagStats));
-        }
-        __syncthreads();
-        if (ra.dbg) {
-            const unsigned long long c4 = wall_clock64();
-            tb += c1 - c0;
-            tf += c2 - c1;
-            t1 += c3 - c2;
-            t2 += c4 - c3;
-        }
-    }
-    if (ra.dbg && tid == 0) {
-        ra.dbg[0] += tb;
-        ra.dbg[1] += tf;
-        ra.dbg[2] += t1;
-        ra.dbg[3] += t2;
-        ra.dbg[4] += (unsigned long long)ra.steps;
-    }
-
-    // ---- the state back: positions (the buffer the context now names current), the context, the list state
-    {
-        R4* pout = St<R>::pos(a, s_ctx.parity);
-        for (int i = tid; i < n; i += kResThreads) pout[i] = s_pos[i];
-        for (int q = tid; q < cap * n; q += kResThreads) ra.list[q] = s_list[q];
-        for (int i = tid; i < n; i += kResThreads) {
-            ra.lcount[i] = s_lcount[i];
-            ra.cidx[i] = s_cidx[i];
-        }
-        for (int c = tid; c <= kResCells; c += kResThreads) ra.cstart[c] = s_cstart[c];
-    }
-    if (tid == 0) *gctx = s_ctx;
-}
-
 }  // namespace
 
 // ----------------------------------------------------------------------------------------------------
@@ -4216,22 +3824,6 @@ void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a)
 }
 
 int eval64_blocks(int n) { return (n + kEval64Block - 1) / kEval64Block; }
-
-void launch_resident(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const ResArgs& ra)
-{
-    const size_t lds = res_lds_bytes(a.n, ra.cap, a.prec);
-    if (a.prec == 64) {
-        static bool attr = hipFuncSetAttribute((const void*)k_resident<double>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResLdsLimit) == hipSuccess;
-        (void)attr;
-        hipLaunchKernelGGL(k_resident<double>, dim3(1), dim3(kResThreads), lds, s, ctx, a, ra);
-    } else {
-        static bool attr = hipFuncSetAttribute((const void*)k_resident<float>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResLdsLimit) == hipSuccess;
-        (void)attr;
-        hipLaunchKernelGGL(k_resident<float>, dim3(1), dim3(kResThreads), lds, s, ctx, a, ra);
-    }
-}
 
 void launch_eval64(hipStream_t s, int mode, const DevCtx* ctx, const ForceArgs& a)
 {

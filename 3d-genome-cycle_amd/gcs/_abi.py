@@ -44,7 +44,6 @@ OPT_LIST_CAP = 12
 OPT_LIST_WAVES = 13
 OPT_DENSE_NEIGHBORS = 15
 OPT_LIST_DEAL = 16
-OPT_RESIDENT = 17
 
 
 def list_deal(pattern: str) -> int:
@@ -131,8 +130,7 @@ class ListStats(C.Structure):
 
 class RunStats(C.Structure):
     _fields_ = [("graph_launches", _i64), ("graph_steps", _i64), ("eager_steps", _i64), ("graphs_captured", _i64),
-                ("graphs_cached", _i64), ("fused_contact_steps", _i64), ("density_probes", _i64),
-                ("resident_launches", _i64), ("resident_steps", _i64)]
+                ("graphs_cached", _i64), ("fused_contact_steps", _i64), ("density_probes", _i64)]
 
 
 # name -> (restype, argtypes); the exported surface of include/gcs.h

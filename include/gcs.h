@@ -67,8 +67,7 @@ extern "C" {
 
 /* 2: gcs_run_stats gained fused_contact_steps (an out-struct grew: callers built against 1 must rebuild)
  * 3: gcs_system_desc.reserved became .precision (0 = fp64); gcs_run_stats lost the small-path counters and
- *    gained density_probes and the resident-step counters; gcs_list_stats gained deal; GCS_OPT_SMALL_PATH and
- *    GCS_OPT_FUSED_STEP 1 are gone; GCS_OPT_RESIDENT is new */
+ *    gained density_probes; gcs_list_stats gained deal; GCS_OPT_SMALL_PATH and GCS_OPT_FUSED_STEP 1 are gone */
 #define GCS_ABI_VERSION 3
 
 /* arithmetic precision of an engine (gcs_system_desc.precision) */
@@ -380,10 +379,6 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
                                      wave (< waves per tile) of chunk p of each period in nibble p.  Only the split of
                                      a slot's list over the segments changes (the list step's last wave also carries
                                      the particle-local terms); the pair set and the results do not */
-#define GCS_OPT_RESIDENT 17       /* small systems: 1 (default) a fixed-timestep list-step run of N <= 2048 particles
-                                     (undecomposed, its positions, lists and cell list within the LDS of one
-                                     workgroup) runs every step of a chunk of up to 8192 steps in ONE launch
-                                     (kernels.hip k_resident); 0 off (the list step) */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
 
 /* List-step diagnostics (the neighbour lists md::neighbor_searcher keeps between rebuilds; micromd, called at
@@ -415,8 +410,6 @@ typedef struct gcs_run_stats {
     int64_t graphs_cached;    /* captured sequences held now */
     int64_t fused_contact_steps; /* list steps that counted a deferred contact update (gcs_engine_contacts_update) */
     int64_t density_probes;   /* fresh fp32 chains whose mean neighbour count was probed (GCS_OPT_DENSE_NEIGHBORS) */
-    int64_t resident_launches; /* launches of the resident small-system step (GCS_OPT_RESIDENT) */
-    int64_t resident_steps;   /* steps inside them */
 } gcs_run_stats;
 int gcs_engine_get_run_stats(gcs_engine* e, gcs_run_stats* out);
 

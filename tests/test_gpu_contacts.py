@@ -179,7 +179,6 @@ def _fused_contacts(design, cfg, ctx, distance, updates, seed, x=None, prec=64, 
     e = engine_for(design, cfg, prec)
     e.set_option(A.OPT_FUSED_STEP, 3)
     e.set_option(A.OPT_DENSE_NEIGHBORS, 0)  # at any density (C1 at core scale 0.99 is dense)
-    e.set_option(A.OPT_RESIDENT, opts.pop("resident", 0))  # the multi-workgroup list step (fused contact counting)
     for k, v in opts.items():
         e.set_option(getattr(A, "OPT_" + k.upper()), v)
     if x is not None:
@@ -262,20 +261,7 @@ def test_fused_contacts_leave_the_trajectory_unchanged(c1_design, prec):
     b = engine_for(c1_design, cfg, prec)
     b.set_option(A.OPT_FUSED_STEP, 3)
     b.set_option(A.OPT_DENSE_NEIGHBORS, 0)
-    b.set_option(A.OPT_RESIDENT, 0)
     b.set_context(LATE)
     b.run(4 * STEPS_PER_UPDATE, first_step=LATE["step"], seed=53)
     assert np.array_equal(a.get_positions(), b.get_positions())
 
-
-@precisions
-@pytest.mark.parametrize("frac", [0.24, 0.5])
-def test_resident_contacts_match_oracle(c1_design, frac, prec):
-    """the resident step (C1: 1,002 particles, one launch per run) counts a deferred update from the positions at
-    the next run's start, as the list step does (there with a separate insert before the launch): the same table"""
-    cfg = InterphaseConfig()
-    d = frac * LATE["core_scale"]
-    e, got, snaps, st, runs = _fused_contacts(c1_design, cfg, LATE, d, 5, 31, prec=prec, resident=1)
-    exp = expected_table(snaps, d, prec)
-    assert runs["resident_steps"] == 5 * STEPS_PER_UPDATE and runs["fused_contact_steps"] == 0, runs
-    assert got.shape == exp.shape and np.array_equal(got, exp)

@@ -26,20 +26,17 @@ def _f32(x):
     return np.asarray(x, dtype=np.float32).astype(np.float64)
 
 
-def _list_engine(design, cfg, prec=64, resident=0, **opts):
+def _list_engine(design, cfg, prec=64, **opts):
     e, _ = interphase.build_interphase(Engine, design, cfg, precision=prec)
     e.set_option(A.OPT_FUSED_STEP, 3)
     e.set_option(A.OPT_DENSE_NEIGHBORS, 0)  # the list step at any density (test_dense_start_takes_tile_step: the switch)
-    # resident 1: systems of <= 2048 particles take the resident step (GCS_OPT_RESIDENT, the default); 0: the
-    # multi-workgroup list step these tests are about unless they ask for both
-    e.set_option(A.OPT_RESIDENT, resident)
     for k, v in opts.items():
         e.set_option(getattr(A, "OPT_" + k.upper()), v)
     return e
 
 
-def _pair(design, cfg, x=None, ctx=None, prec=64, resident=0, **opts):
-    e = _list_engine(design, cfg, prec, resident, **opts)
+def _pair(design, cfg, x=None, ctx=None, prec=64, **opts):
+    e = _list_engine(design, cfg, prec, **opts)
     o, _ = interphase.build_interphase(oracle.OracleSystem, design, cfg, precision=prec)
     for s in (e, o):
         s.set_schedule(**interphase.interphase_schedule(cfg))
@@ -57,36 +54,23 @@ def _run_both(e, o, steps, first, cfg, seed, **kw):
         s.run(steps, first_step=first, temperature=cfg.temperature, timestep=cfg.timestep, seed=seed, **kw)
 
 
-def _check_shape(e, resident, steps):
-    """the run took the step shape the test asked for"""
-    r = e.run_stats()
-    assert r["resident_steps"] == (steps if resident else 0), r
-
-
-RESIDENT = pytest.mark.parametrize("resident", [0, 1], ids=["list", "resident"])
-
-
 @precisions
-@RESIDENT
-def test_list_trajectory_c1_from_step0(c1_design, prec, resident):
+def test_list_trajectory_c1_from_step0(c1_design, prec):
     """production start (core scale 0.5, growing cutoff), 60 steps, Philox noise"""
     cfg = InterphaseConfig()
-    e, o = _pair(c1_design, cfg, prec=prec, resident=resident)
+    e, o = _pair(c1_design, cfg, prec=prec)
     _run_both(e, o, 60, 0, cfg, 987654321)
     err = np.abs(e.get_positions() - o.get_positions()).max()
     st = e.list_stats()
     assert st["active"] == 1 and st["builds"] >= 60 // st["rebuild_every"], st
     assert err <= TOL_X[prec], (err, st)
-    _check_shape(e, resident, 60)
 
 
 @precisions
-@RESIDENT
-def test_list_trajectory_c1_wall_contact(c1_design, prec, resident):
+def test_list_trajectory_c1_wall_contact(c1_design, prec):
     cfg = InterphaseConfig()
-    e, o = _pair(c1_design, cfg, ctx=LATE, prec=prec, resident=resident)
+    e, o = _pair(c1_design, cfg, ctx=LATE, prec=prec)
     _run_both(e, o, 40, LATE["step"], cfg, 5)
-    _check_shape(e, resident, 40)
     assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[prec]
     ce, co = e.get_context(), o.get_context()
     assert ce["step"] == co["step"] == LATE["step"] + 40
@@ -96,12 +80,11 @@ def test_list_trajectory_c1_wall_contact(c1_design, prec, resident):
 
 
 @precisions
-@RESIDENT
-def test_list_injected_reference_noise(c1_design, prec, resident):
+def test_list_injected_reference_noise(c1_design, prec):
     cfg = InterphaseConfig()
     steps = 12
     xi = oracle.reference_normals(c1_design.seed, steps * c1_design.n * 3).reshape(steps, c1_design.n, 3)
-    e, o = _pair(c1_design, cfg, prec=prec, resident=resident)
+    e, o = _pair(c1_design, cfg, prec=prec)
     for s in (e, o):
         s.set_noise(xi)
     _run_both(e, o, steps, 0, cfg, 0, noise=A.NOISE_INJECTED)
@@ -109,12 +92,11 @@ def test_list_injected_reference_noise(c1_design, prec, resident):
 
 
 @precisions
-@RESIDENT
 @pytest.mark.parametrize("skin,every", [(30, 200), (400, 64)])
-def test_list_exact_when_the_skin_is_outrun(c1_design, skin, every, prec, resident):
+def test_list_exact_when_the_skin_is_outrun(c1_design, skin, every, prec):
     """rebuild period far beyond the skin: particles outrun it and take the exact cell search; same bound"""
     cfg = InterphaseConfig()
-    e, o = _pair(c1_design, cfg, ctx=LATE, prec=prec, resident=resident, list_skin=skin, list_every=every)
+    e, o = _pair(c1_design, cfg, ctx=LATE, prec=prec, list_skin=skin, list_every=every)
     _run_both(e, o, 60, LATE["step"], cfg, 17)
     st = e.list_stats()
     assert st["fallback_particle_steps"] > 0, st
@@ -122,11 +104,9 @@ def test_list_exact_when_the_skin_is_outrun(c1_design, skin, every, prec, reside
 
 
 @precisions
-@RESIDENT
-def test_list_exact_when_lists_overflow(c1_design, prec, resident):
-    """32 entries per particle (the list step: 8 per wave segment; the resident step: 32) overflow at C1's density"""
+def test_list_exact_when_lists_overflow(c1_design, prec):
     cfg = InterphaseConfig()
-    e, o = _pair(c1_design, cfg, ctx=LATE, prec=prec, resident=resident, list_cap=32)
+    e, o = _pair(c1_design, cfg, ctx=LATE, prec=prec, list_cap=32)
     _run_both(e, o, 30, LATE["step"], cfg, 23)
     st = e.list_stats()
     assert st["fallback_particle_steps"] > 0, st
@@ -134,15 +114,13 @@ def test_list_exact_when_lists_overflow(c1_design, prec, resident):
 
 
 @precisions
-@RESIDENT
 @pytest.mark.parametrize("every", [0, 1, 5])
-def test_list_graph_eager_and_chunks_bitwise_identical(c1_design, every, prec, resident):
-    """graph vs eager launches and one run vs chunks rebuild at the same steps: identical bits (the resident step:
-    one launch per run, so only the chunking varies; its lists persist between the chunks' launches)"""
+def test_list_graph_eager_and_chunks_bitwise_identical(c1_design, every, prec):
+    """graph vs eager launches and one run vs chunks rebuild at the same steps: identical bits"""
     cfg = InterphaseConfig()
     runs = []
     for g, chunks in ((0, [70]), (8, [70]), (32, [70]), (32, [13, 40, 17]), (32, [1, 1, 3, 65])):
-        e = _list_engine(c1_design, cfg, prec, resident, list_every=every, graph_steps=g)
+        e = _list_engine(c1_design, cfg, prec, list_every=every, graph_steps=g)
         e.set_schedule(**interphase.interphase_schedule(cfg))
         e.set_context(LATE)
         first = LATE["step"]
@@ -157,9 +135,8 @@ def test_list_graph_eager_and_chunks_bitwise_identical(c1_design, every, prec, r
 
 
 @precisions
-@RESIDENT
 @pytest.mark.parametrize("n", [1, 2, 63, 65, 200, 1025, 1500])
-def test_list_small_and_ragged_sizes(n, prec, resident):
+def test_list_small_and_ragged_sizes(n, prec):
     """random ab factors and mobilities (several pair classes, mixed), 20 steps at dt 1e-4"""
     rng = np.random.default_rng(n)
     x = rng.uniform(-0.5, 0.5, size=(n, 3))
@@ -177,12 +154,10 @@ def test_list_small_and_ragged_sizes(n, prec, resident):
         if name == "e":
             s.set_option(A.OPT_FUSED_STEP, 3)
             s.set_option(A.OPT_DENSE_NEIGHBORS, 0)
-            s.set_option(A.OPT_RESIDENT, resident)
         sysd[name] = s
     for s in sysd.values():
         s.run(20, seed=1, timestep=1e-4)
     assert sysd["e"].list_stats()["active"] == 1
-    _check_shape(sysd["e"], resident, 20)
     assert np.abs(sysd["e"].get_positions() - sysd["o"].get_positions()).max() <= TOL_X[prec]
 
 
@@ -360,29 +335,13 @@ def test_c2_long_horizon_list_vs_rebuild_step():
     assert (s3[:3] > 0).all() and (s2[:3] > 0).all()
 
 
-def test_resident_eligibility():
-    """the resident step takes N <= 2048 when the LDS holds >= 16 list entries per particle: fp32 up to 2048
-    particles, fp64 up to ~1,900 (fp64 positions are 32 B); larger systems and GCS_OPT_RESIDENT 0 take the list step"""
-    for n, prec, opt, exp in ((2048, 32, 1, 1), (1800, 64, 1, 1), (2048, 64, 1, 0), (2049, 32, 1, 0), (500, 64, 0, 0)):
-        rng = np.random.default_rng(n)
-        e = Engine(n, precision=prec)
-        e.add_neighbor_softcore(2.5, 0.3, 2.5, 0.24, 0.03, mix=False, scaled=False)
-        e.set_positions(rng.uniform(-1, 1, size=(n, 3)))
-        e.set_option(A.OPT_RESIDENT, opt)
-        e.run(3, seed=1, timestep=1e-5)
-        assert e.run_stats()["resident_steps"] == 3 * exp, (n, prec, opt)
-        assert e.list_stats()["active"] == 1
-        e.close()
-
-
 @precisions
-@RESIDENT
-def test_second_neighbour_harmonic_nonzero_k(c1_design, prec, resident):
+def test_second_neighbour_harmonic_nonzero_k(c1_design, prec):
     """setup_loop_forcefield (simulation_driver_forcefield.cpp:100-136) with K != 0: the (i, i+2) harmonic bonds are
     compiled in (the default config's K = 0 drops them); forces and a 40-step list-step trajectory vs the oracle"""
     import dataclasses
     cfg = dataclasses.replace(InterphaseConfig(), a_core_2nd_bond_spring=40.0, b_core_2nd_bond_spring=15.0)
-    e, o = _pair(c1_design, cfg, ctx=LATE, prec=prec, resident=resident)
+    e, o = _pair(c1_design, cfg, ctx=LATE, prec=prec)
     fe, fo = e.compute_forces(), o.compute_forces()
     from tolerances import assert_forces_close
     assert_forces_close(fe, fo, prec)

@@ -470,34 +470,24 @@ def _c3():
     return mitotic, cfg, a, p
 
 
-RESIDENT = pytest.mark.parametrize("resident", [0, 1], ids=["list", "resident"])
-
-
 @precisions
-@RESIDENT
-def test_c3_anatelophase_stages_match_oracle(prec, resident):
+def test_c3_anatelophase_stages_match_oracle(prec):
     """586 beads: rods init (same mt19937_64 draws), 40 anaphase steps with kinetochore fibers, field swap,
-    40 telophase steps with the packing well; positions and energies within the precision's bounds (the list step
-    and the resident step, GCS_OPT_RESIDENT)."""
+    40 telophase steps with the packing well; positions and energies within the precision's bounds."""
     mitotic, cfg, a, _ = _c3()
     res = []
     for cls in (Engine, oracle.OracleSystem):
         s, h = mitotic.build_anatelophase(cls, a, cfg, precision=prec)
-        if cls is Engine:
-            s.set_option(A.OPT_RESIDENT, resident)
         drv = mitotic.AnatelophaseDriver(s, h, a, cfg, log=None)
         drv.run(anaphase_steps=40, telophase_steps=40)
         res.append((s.get_positions(), s.compute_energy()[0], s.compute_forces()))
-        if cls is Engine:
-            assert s.run_stats()["resident_steps"] == (80 if resident else 0)
     assert np.abs(res[0][0] - res[1][0]).max() <= X[prec]
     assert res[0][1] == pytest.approx(res[1][1], rel=E_REL[prec])
     assert_forces_close(res[0][2], res[1][2], prec)
 
 
 @precisions
-@RESIDENT
-def test_c3_prometaphase_matches_oracle(prec, resident):
+def test_c3_prometaphase_matches_oracle(prec):
     """1,172 beads: sister bonds, fibers to both poles, force-flux point sources (polar ejection switched on)."""
     import dataclasses
     mitotic, cfg, a, p = _c3()
@@ -516,11 +506,7 @@ def test_c3_prometaphase_matches_oracle(prec, resident):
     res = []
     for cls in (Engine, oracle.OracleSystem):
         s, _ = mitotic.build_prometaphase(cls, p, cfg, precision=prec)
-        if cls is Engine:
-            s.set_option(A.OPT_RESIDENT, resident)
         mitotic.PrometaphaseDriver(s, p, cfg, log=None).run(x0, steps=50)
-        if cls is Engine:
-            assert s.run_stats()["resident_steps"] == (50 if resident else 0)
         res.append((s.get_positions(), s.compute_forces()))
     assert np.abs(res[0][0] - res[1][0]).max() <= X[prec]
     assert_forces_close(res[0][1], res[1][1], prec)
