@@ -788,8 +788,14 @@ int eff_fused(const gcs_engine* e)
     if (!e->list_ok) return 2;
     return dense_switch(e) ? 0 : 3;
 }
-bool list_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) == 3 && !spacestep; }
-bool fused_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) != 0 && !spacestep; }
+// the list step, and the relaxation (spacestep) step on the same lists (k_lstep<..., RLX> + k_lupdate) when the
+// system admits lists; other spacestep runs take the cell-list evaluation (fp32: k_force + k_adapt + k_update, fp64:
+// k_eval64 + k_red64 + k_update)
+bool list_path(const gcs_engine* e, bool spacestep)
+{
+    return eff_fused(e) == 3 && e->list_ok && (!spacestep || !e->dom);
+}
+bool fused_path(const gcs_engine* e, bool spacestep) { return spacestep ? list_path(e, true) : eff_fused(e) != 0; }
 bool rebuild_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) == 2 && !spacestep; }
 
 float list_skin(const gcs_engine* e) { return 1e-3f * (float)e->list_skin_pm * e->fa.pf.pair_dist; }
@@ -914,10 +920,15 @@ int list_flags(const gcs_engine* e, int64_t st)
 // one list step: on a rebuild step the cell list at cutoff + skin (ctx->grid, set by the prime or the last
 // bounding-box step's tail), the lists, then the step itself (forces + local terms + update + tail in the final
 // workgroup)
-void enqueue_list_step(gcs_engine* e, bool build, int lflags, double contact = 0, int parity = -1)
+void enqueue_list_step(gcs_engine* e, bool build, int lflags, double contact = 0, int parity = -1,
+                       const gcs_bd_config* relax = nullptr)
 {
     ForceArgs la = list_args(e);
     la.par_hint = parity;
+    if (relax) {
+        la.relax_spacestep = relax->spacestep;
+        la.relax_timestep = relax->timestep;
+    }
     if (contact > 0) {  // the pending contact update, counted from this step's start positions (its distance: ctx)
         la.contact_on = 1;
         la.c_keys = e->c_keys;
@@ -932,7 +943,10 @@ void enqueue_list_step(gcs_engine* e, bool build, int lflags, double contact = 0
         enqueue_cell_order(e, true);
         launch_list_build(e->stream, e->ctx, la);
     }
-    launch_list_step(e->stream, e->ctx, la, lflags);
+    if (relax)  // neighbour statistics from the force launch; the schedule and the next build's grid from the update
+        launch_list_relax(e->stream, e->ctx, la, lflags & 4, lflags & (1 | 2));
+    else
+        launch_list_step(e->stream, e->ctx, la, lflags);
 }
 int step_grid(const gcs_engine* e) { return e->fa.split ? force_grid_split(e->n) : force_grid(e->n); }
 
@@ -1891,7 +1905,7 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
     if (e->prec == 64 && !spacestep && !e->list_ok)
         return fail(GCS_ESTATE, "the fp64 engine's fixed-timestep step is the list step: it needs a neighbor soft-core "
                                 "field, <= 256 (a, b) pair classes and < 2^24 particles (use GCS_PRECISION_F32)");
-    if (!list_path(e, spacestep))
+    if (!list_path(e, spacestep) || spacestep)  // (contact updates are fused into fixed-timestep list steps only)
         if ((rc = flush_contacts(e))) return rc;
     if ((rc = begin_run(e, cfg, first_step))) return rc;
 
@@ -1921,9 +1935,10 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
                 e->c_pending = 0;
                 e->rstats.fused_contact_steps++;
             }
+            const gcs_bd_config* rx = spacestep ? cfg : nullptr;  // the relaxation step
             if (e->l_need_build || G == 0) {
                 // a run start's rebuild, or no graphs
-                enqueue_list_step(e, e->l_need_build || phase == 0, list_flags(e, st), ct ? 1.0 : 0.0, par(done));
+                enqueue_list_step(e, e->l_need_build || phase == 0, list_flags(e, st), ct ? 1.0 : 0.0, par(done), rx);
                 e->l_need_build = false;
                 ++done;
                 e->rstats.eager_steps++;
@@ -1936,7 +1951,7 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
             rc = cached_graph(e, key, phase | (ct ? 1 << 20 : 0), p0, len, [&]() {
                 for (int k = 0; k < len; ++k)
                     enqueue_list_step(e, (phase + k) % M == 0, list_flags(e, st + k), (ct && k == 0) ? 1.0 : 0.0,
-                                      p0 ^ (k & 1));
+                                      p0 ^ (k & 1), rx);
             }, &x);
             if (rc || (rc = launch_graph(e, x))) return rc;
             e->rstats.graph_steps += len;
@@ -1960,6 +1975,7 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
     }
     HIPCHK(hipGetLastError());
     end_run(e, cfg, first_step, steps);
+    if (spacestep) e->chain_dt = -1.0;  // ctx->dt_used holds an adapted timestep: the next run rewrites it
     if (steps & 1) e->parity ^= 1;
     if (cfg->noise == GCS_NOISE_INJECTED) e->noise_cursor += steps;
     return GCS_OK;
@@ -2442,7 +2458,6 @@ int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step
         return GCS_OK;
     }
     const ForceArgs a = domain_args(e);
-    const int n = e->n;
     const DomBox reg = dom_region(e);
     enqueue_count(e, &reg);
     enqueue_scan(e, false);
@@ -2586,7 +2601,6 @@ int enqueue_rccl_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step)
         return GCS_OK;
     }
     const ForceArgs a = domain_args(e);
-    const int n = e->n;
     const DomBox reg = dom_region(e);
     enqueue_count(e, &reg);
     enqueue_scan(e, false);

@@ -275,6 +275,9 @@ struct ForceArgs {
     unsigned long long list_deal;  // list build: candidate chunk -> wave segment pattern (GCS_OPT_LIST_DEAL; 0: round robin)
     int par_hint;           // >= 0: ctx->parity of this launch, known to the host at enqueue (the slot loads need not
                             // wait for the context); -1: read it
+    // the relaxation list step (k_lstep<..., RLX> + k_lupdate): the run's spacestep and the largest timestep
+    double relax_spacestep;
+    double relax_timestep;
     // the contact-map update fused into a list step (stage_interphase/contact_map.cpp:33-63): every pair i < j of
     // the step's START positions closer than sqrt(DevCtx::contact_d2) (strict fp32 predicate) is counted into the table
     int contact_on;
@@ -336,7 +339,7 @@ template <> struct St<double> {
 // list step launch accumulators behind the arrival counters in ForceArgs::lticket (unsigned words, 128 B per slot):
 // per group of workgroups (b % 8) kListAccSlots slots + one overflow flag (kernels.hip list_accumulate)
 constexpr int kListAccBase = 32 * 9;
-constexpr int kListAccSlots = 22;
+constexpr int kListAccSlots = 23;
 constexpr int kListTicketWords = kListAccBase + 8 * 32 * (kListAccSlots + 1);
 // identity of accumulator slot k (what list_accumulate starts from)
 __host__ __device__ inline unsigned long long list_acc_identity(int k)
@@ -412,6 +415,9 @@ void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a);
 // flags: 1 apply the schedule, 2 the next step rebuilds (bounding box -> grid), 4 neighbour-count statistics,
 // 8 decomposed (a.dom_on): the owned slots only, the local reduction into a.dom_red instead of the tail
 void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags);
+// the relaxation (spacestep) step on the lists: forces + the adapted timestep (k_lstep<..., RLX>: forces into
+// a.force_out / a.dforce_out in slot order, its final workgroup sets ctx->dt_used), then the update (k_lupdate)
+void launch_list_relax(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force_flags, int update_flags);
 void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2, double d2_64);
 // the decomposed list step's tail from the allreduced buffer glob (one workgroup), then the shared particles'
 // positions into both buffers (by index and by slot) and the send bands' header rows zeroed

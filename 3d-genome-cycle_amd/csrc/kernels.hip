@@ -135,13 +135,6 @@ __device__ inline float wave_min(float v)
 }
 
 __device__ inline int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ inline float uniform(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
-__device__ inline double uniform(double v)
-{
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readfirstlane((int)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
-}
 __device__ inline float uniform_f(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 
 // ---- precision-generic scalar helpers (R = float: exactly the fp32 builtins the fp32 kernels always used) ----
@@ -2715,6 +2708,7 @@ struct ListTotals {
     long long nown;   // owned particles (decomposed launches)
     float ld;         // largest displacement from the build
     float bb[6];      // bbox lo[3], hi[3] (bbox launches)
+    double drift;     // largest mu |F| (relaxation force launches)
 };
 
 // launch flags of k_lstep
@@ -2775,9 +2769,11 @@ __device__ void list_tail_apply(DevCtx* ctx, const ForceArgs& a, const ListTailI
 //   15    owned particles                integer, added (decomposed launches)
 //   16-21 wall reactions, low words      l = round((r 2^20 - h) 2^32) in [0, 2^32], added: r = (h + l 2^-32) 2^-20
 //                                        exactly up to 2^-52 per term (the fp64 step's reactions keep fp64 resolution)
-//   22    a reaction whose fixed-point image would not fit (non-finite or >= 2^41): the totals carry a NaN reaction,
+//   22    largest mu |F| (relaxation force launches): the fp64 bits of a value >= 0, atomic max
+//   23    a reaction whose fixed-point image would not fit (non-finite or >= 2^41): the totals carry a NaN reaction,
 //         as a float sum would
 constexpr int kAccReactLo = 16;
+constexpr int kAccDrift = 22;
 constexpr int kAccWords = kListAccSlots + 1;  // slots + the overflow flag, per group
 __device__ __forceinline__ unsigned ordered_bits(float v)
 {
@@ -2812,6 +2808,8 @@ __device__ __forceinline__ void acc_fold(unsigned* base, int k, double v)
         }
     } else if (k == 6 || k == 8 || k == 15) {
         __hip_atomic_fetch_add(w, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (k == kAccDrift) {
+        __hip_atomic_fetch_max(w, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (k == 7) {
         __hip_atomic_fetch_max(w32, __float_as_uint((float)v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (k < 12) {
@@ -2845,13 +2843,15 @@ __device__ void list_totals(unsigned* base, int ngroups, ListTotals& t)
             else v[k] = max((unsigned)v[k], (unsigned)x[k]);
         }
     }
-    unsigned long long lo[6], bad = 0;
+    unsigned long long lo[6], bad = 0, drift = 0;
     for (int k = 0; k < 6; ++k) lo[k] = 0;
     for (int g = 0; g < ngroups; ++g) {
         const unsigned long long* x = s_acc + g * kAccWords;
         for (int k = 0; k < 6; ++k) lo[k] += x[kAccReactLo + k];
+        drift = max(drift, x[kAccDrift]);
         bad |= x[kListAccSlots];
     }
+    t.drift = __longlong_as_double((long long)drift);
     for (int k = 0; k < 6; ++k)
         t.react[k] = (bad & 1ull) ? __longlong_as_double(0x7ff8000000000000ll)
                                   : (double)(long long)v[k] * 0x1p-20 + (double)(long long)lo[k] * 0x1p-52;
@@ -3009,7 +3009,10 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 // contact predicate are in R; the list bookkeeping (build positions, displacements, cell ranges, bbox) is fp32 with
 // margins (a partner within the cutoff in R is always in the list or found by the exact search: the skin test keeps
 // 0.1 % of the skin, ~1e-4, against fp32 roundings of ~1e-6 of the coordinates).
-template <typename LE, int W, bool CT, bool DOM = false, typename R = float>
+// RLX (the relaxation step's force launch, simulation_driver_relaxation.cpp:48-55): wave 0 stores the force (slot
+// order, .w = mu) instead of integrating and folds max mu |F| into the accumulators; the final workgroup sets the
+// adapted timestep ctx->dt_used (k_red64's arithmetic) and the reactions; k_lupdate then moves the particles.
+template <typename LE, int W, bool CT, bool DOM = false, typename R = float, bool RLX = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS_LIST_WAVES_PER_EU_CT : (sizeof(R) == 8 ? GCS_LIST_WAVES_PER_EU64 : GCS_LIST_WAVES_PER_EU)))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int flags)
 {
     using R4 = real4<R>;
@@ -3200,7 +3203,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     red[wave][1][lane] = fy;
     red[wave][2][lane] = fz;
     red[wave][3][lane] = nbr;
-    if (wave == (W > 1 ? 1 : 0)) {  // the noise (depends on the particle and the step only) off wave 0's path
+    if (!RLX && wave == (W > 1 ? 1 : 0)) {  // the noise (depends on the particle and the step only) off wave 0's path
         R n0, n1, n2;
         noise3<R>(a, ctx, i, n0, n1, n2);
         s_noise[lane] = mk4<R>(n0, n1, n2, R(0));
@@ -3226,6 +3229,21 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         fsy += lf.y;
         fsz += lf.z;
         const R mu = lf.w;
+        if constexpr (RLX) {
+            // the force for k_lupdate, the drift for the adapted timestep (k_eval64's expression)
+            if (act) St<R>::force(a)[s] = mk4<R>(fsx, fsy, fsz, mu);
+            const double drift =
+                wave_total_max_d(act ? (double)(mu * r_sqrt(fsx * fsx + fsy * fsy + fsz * fsz)) : 0.0);
+            const float nfb = (float)__popcll(__ballot(fb));
+            double v = 0.0;
+            if (flags & kLFlagStats) {
+                const R nt = wave_sum_r(act ? ns : R(0));
+                if (lane == 6) v = (double)nt;
+            }
+            if (lane == 8) v = nfb;
+            if (lane == kAccDrift) v = drift;
+            if (lane == 8 || lane == kAccDrift || ((flags & kLFlagStats) && lane == 6)) acc_fold(acc, lane, v);
+        } else {
         // Euler-Maruyama: x += mu dt F + sqrt(2 T mu dt) xi
         const R4 xi = s_noise[lane];
         const R dt = P.timestep;
@@ -3265,6 +3283,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         const bool mine = lane == 7 || lane == 8 || ((flags & kLFlagStats) && lane == 6) ||
                           ((flags & kLFlagBBox) && lane >= 9 && lane < 15) || (DOM && lane == 15);
         if (mine) acc_fold(acc, lane, v);
+        }
     } else {
         // the wall reactions: waves 1.. take the six components in turn (W = 4: wave 1 inward, wave 2 outward)
         const int c0 = W > 2 ? 3 * (wave - 1) : 0, c1 = W > 2 ? c0 + 3 : 6;
@@ -3305,12 +3324,26 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     unsigned long long* const dbt = a.dbg_times ? a.dbg_times + 8 * gridDim.x : nullptr;
     if (dbt && tid == 0) dbt[0] = wall_clock64();
     ListTailIn tin;
-    if (!DOM && tid == 0) tin = list_tail_load(ctx, a);  // in flight during the accumulator reads
+    if (!DOM && !RLX && tid == 0) tin = list_tail_load(ctx, a);  // in flight during the accumulator reads
     ListTotals tot;
     list_totals(a.lticket + kListAccBase, ngroups, tot);
     if (tid != 0) return;
     if (dbt) dbt[1] = wall_clock64();
     a.lticket[32 * 8] = 0u;
+    if constexpr (RLX) {
+        // the force launch's part of the tail: reactions, neighbours, fallbacks, the drift -> the adapted timestep
+        for (int k = 0; k < 3; ++k) {
+            ctx->react_in[k] = tot.react[k];
+            ctx->react_out[k] = tot.react[3 + k];
+        }
+        if (flags & kLFlagStats) ctx->neighbors = tot.nbr / (double)a.n;
+        ctx->lfallback += tot.nfb;
+        ctx->max_drift = tot.drift;
+        double dt = a.relax_timestep;
+        if (a.relax_spacestep > 0.0 && tot.drift * dt > a.relax_spacestep) dt = a.relax_spacestep / tot.drift;
+        ctx->dt_used = dt;
+        return;
+    }
     if constexpr (DOM) {
         // the local reduction (layout kDomainRed); this domain's largest displacement in its own slot
         double* r = a.dom_red;
@@ -3329,6 +3362,91 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     }
     list_tail_apply(ctx, a, tin, tot, flags);
     if (dbg) dbg[7] = wall_clock64();
+}
+
+// The relaxation step's update (after k_lstep<..., RLX>): one thread per slot moves its particle with the adapted
+// timestep ctx->dt_used, x += mu dt F + sqrt(2 T mu dt) xi (k_update's arithmetic, from the slot-ordered force), into
+// both position buffers of the next parity; the largest displacement from the build and, before a rebuild, the
+// bounding box go to the launch accumulators, and the final workgroup advances the context (list_tail_apply, with
+// the reactions of the force launch).
+constexpr int kLUpdateBlock = 256;
+template <typename R>
+__global__ __launch_bounds__(kLUpdateBlock) void k_lupdate(DevCtx* __restrict__ ctx, ForceArgs a, int flags)
+{
+    using R4 = real4<R>;
+    __shared__ int s_last, s_final;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int n = a.n;
+    const int s = blockIdx.x * kLUpdateBlock + tid;
+    const bool valid = s < n;
+    const int sl = valid ? s : n - 1;
+    const int par = a.par_hint >= 0 ? a.par_hint : ctx->parity;
+    constexpr int kIdx = (1 << kListIndexBits) - 1;
+    const R4 pi = St<R>::psort(a, par)[sl];
+    const R4 f = St<R>::force(a)[sl];
+    const float4 pb = a.spos[sl];
+    const int i = wbits(pi.w) & kIdx;
+    const R dt = (R)ctx->dt_used;
+    R n0, n1, n2;
+    noise3<R>(a, ctx, i, n0, n1, n2);
+    const R mu = f.w;
+    const R amp = r_sqrt(R(2) * St<R>::prm(a).temperature * mu * dt);
+    const R mdt = mu * dt;
+    const R nxp = pi.x + mdt * f.x + amp * n0;
+    const R nyp = pi.y + mdt * f.y + amp * n1;
+    const R nzp = pi.z + mdt * f.z + amp * n2;
+    if (valid) {
+        St<R>::pos(a, par ^ 1)[i] = mk4<R>(nxp, nyp, nzp, R(0));
+        St<R>::psort(a, par ^ 1)[s] = mk4<R>(nxp, nyp, nzp, pi.w);
+    }
+    // the list bookkeeping in fp32 (as k_lstep's): displacement from the build, bbox of the roundings
+    const float fnx = (float)nxp, fny = (float)nyp, fnz = (float)nzp;
+    const float gx = (float)(nxp - (R)pb.x), gy = (float)(nyp - (R)pb.y), gz = (float)(nzp - (R)pb.z);
+    const float dmax = wave_max(valid ? sqrtf(fmaf(gz, gz, fmaf(gy, gy, gx * gx))) : 0.f);
+    const int ngroups = min((int)gridDim.x, 8);
+    const int g = blockIdx.x % ngroups;
+    unsigned* const acc = a.lticket + kListAccBase + 32 * kAccWords * g;
+    double v = lane == 7 ? (double)dmax : 0.0;
+    if (flags & kLFlagBBox) {
+        const float big = 3.0e38f;
+        const float l0 = wave_min(valid ? fnx : big), l1 = wave_min(valid ? fny : big), l2 = wave_min(valid ? fnz : big);
+        const float h0 = wave_max(valid ? fnx : -big), h1 = wave_max(valid ? fny : -big), h2 = wave_max(valid ? fnz : -big);
+        v = lane == 9 ? l0 : lane == 10 ? l1 : lane == 11 ? l2 : lane == 12 ? h0 : lane == 13 ? h1 : lane == 14 ? h2 : v;
+    }
+    if (lane == 7 || ((flags & kLFlagBBox) && lane >= 9 && lane < 15)) acc_fold(acc, lane, v);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's accumulator atomics are performed
+    __syncthreads();
+    // the two-level ticket (as k_lstep)
+    const int gsize = ((int)gridDim.x - g + ngroups - 1) / ngroups;
+    if (tid == 0) {
+        const unsigned old = atomicAdd(&a.lticket[32 * g], 1u);
+        s_last = (old == (unsigned)gsize - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (tid == 0) {
+        a.lticket[32 * g] = 0u;
+        const unsigned old = atomicAdd(&a.lticket[32 * 8], 1u);
+        s_final = (old == (unsigned)ngroups - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!s_final) return;
+    ListTailIn tin;
+    double react[6];
+    if (tid == 0) {
+        tin = list_tail_load(ctx, a);
+        for (int k = 0; k < 3; ++k) {
+            react[k] = ctx->react_in[k];
+            react[3 + k] = ctx->react_out[k];
+        }
+    }
+    ListTotals tot;
+    list_totals(a.lticket + kListAccBase, ngroups, tot);
+    if (tid != 0) return;
+    a.lticket[32 * 8] = 0u;
+    for (int k = 0; k < 6; ++k) tot.react[k] = react[k];  // (the force launch's; list_tail_apply rewrites them)
+    tot.nfb = 0;  // (counted by the force launch)
+    list_tail_apply(ctx, a, tin, tot, flags & (kLFlagSched | kLFlagBBox));
 }
 
 // The decomposed list step's tail (one workgroup, after the allreduce of every domain's k_lstep<..., DOM> reduction):
@@ -3776,6 +3894,32 @@ __global__ void k_set_contact(DevCtx* ctx, float d2, double d2_64)
 void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2, double d2_64)
 {
     hipLaunchKernelGGL(k_set_contact, dim3(1), dim3(1), 0, s, ctx, d2, d2_64);
+}
+
+template <typename R>
+static void launch_list_relax_r(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force_flags, int update_flags)
+{
+    const dim3 g(list_step_grid(a.n));
+    if (list_u16(a.n)) {
+        if (a.list_waves == 2)
+            hipLaunchKernelGGL((k_lstep<unsigned short, 2, false, false, R, true>), g, dim3(128), 0, s, ctx, a, force_flags);
+        else
+            hipLaunchKernelGGL((k_lstep<unsigned short, 4, false, false, R, true>), g, dim3(256), 0, s, ctx, a, force_flags);
+    } else {
+        if (a.list_waves == 2)
+            hipLaunchKernelGGL((k_lstep<int, 2, false, false, R, true>), g, dim3(128), 0, s, ctx, a, force_flags);
+        else
+            hipLaunchKernelGGL((k_lstep<int, 4, false, false, R, true>), g, dim3(256), 0, s, ctx, a, force_flags);
+    }
+    hipLaunchKernelGGL(k_lupdate<R>, dim3((a.n + kLUpdateBlock - 1) / kLUpdateBlock), dim3(kLUpdateBlock), 0, s, ctx, a,
+                       update_flags);
+}
+void launch_list_relax(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force_flags, int update_flags)
+{
+    if (a.prec == 64)
+        launch_list_relax_r<double>(s, ctx, a, force_flags, update_flags);
+    else
+        launch_list_relax_r<float>(s, ctx, a, force_flags, update_flags);
 }
 
 void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)

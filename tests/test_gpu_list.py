@@ -349,3 +349,70 @@ def test_second_neighbour_harmonic_nonzero_k(c1_design, prec):
     assert np.abs(base.compute_forces() - fo).max() > 1e-2  # the field changes the forces
     _run_both(e, o, 40, LATE["step"], cfg, 7)
     assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[prec]
+
+
+def _relax_engine(design, cfg, prec, **opts):
+    e = _list_engine(design, cfg, prec, **opts)
+    e.set_schedule(update_time=0, update_scales=0, update_wall=0, timestep=cfg.timestep)
+    return e
+
+
+@precisions
+def test_list_relaxation_matches_oracle(c1_design, prec):
+    """the relaxation stage's step (spacestep 1e-3, simulation_driver_relaxation.cpp:48-55) on the lists:
+    k_lstep<..., RLX> stores the forces and adapts the timestep in its final workgroup, k_lupdate moves the
+    particles.  From C1's start (core scale 0.5, fast motion: several rebuilds), 60 steps, Philox noise, then 5 more
+    from there: positions within the precision's bound, the adapted timestep equal"""
+    cfg = InterphaseConfig()
+    e = _relax_engine(c1_design, cfg, prec, list_every=5)
+    o, _ = interphase.build_interphase(oracle.OracleSystem, c1_design, cfg, precision=prec)
+    o.set_schedule(update_time=0, update_scales=0, update_wall=0, timestep=cfg.timestep)
+    for s in (e, o):
+        s.apply_schedule(0)
+    for first, k in ((0, 60), (60, 5)):
+        for s in (e, o):
+            s.run(k, first_step=first, temperature=cfg.temperature, timestep=cfg.timestep,
+                  spacestep=cfg.relaxation_spacestep, seed=4242)
+        assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[prec]
+        assert e.get_context()["last_timestep"] == pytest.approx(o.get_context()["last_timestep"],
+                                                                 rel={64: 1e-10, 32: 1e-4}[prec])
+    st, rs = e.list_stats(), e.run_stats()
+    assert st["active"] == 1 and st["builds"] >= 65 // 5, st
+    assert rs["graph_steps"] > 0, rs
+    assert e.get_context()["last_timestep"] < cfg.timestep  # the spacestep limit is active at this start
+
+
+@precisions
+def test_list_relaxation_graph_eager_and_chunks_bitwise_identical(c1_design, prec):
+    cfg = InterphaseConfig()
+    runs = []
+    for g, chunks in ((0, [40]), (32, [40]), (8, [7, 20, 13])):
+        e = _relax_engine(c1_design, cfg, prec, list_every=6, graph_steps=g)
+        e.apply_schedule(0)
+        first = 0
+        for c in chunks:
+            e.run(c, first_step=first, temperature=cfg.temperature, timestep=cfg.timestep,
+                  spacestep=cfg.relaxation_spacestep, seed=3)
+            first += c
+        runs.append((e.get_positions(), e.get_context()))
+        e.close()
+    for x, c in runs[1:]:
+        assert np.array_equal(x, runs[0][0])
+        assert c == runs[0][1]
+
+
+@precisions
+def test_list_relaxation_then_fixed_timestep(c1_design, prec):
+    """a relaxation run followed by a fixed-timestep run continuing at its last step: the lists carry over, and the
+    context reports the fixed timestep again (the relaxation's adapted one does not leak)"""
+    cfg = InterphaseConfig()
+    e = _relax_engine(c1_design, cfg, prec)
+    o, _ = interphase.build_interphase(oracle.OracleSystem, c1_design, cfg, precision=prec)
+    o.set_schedule(update_time=0, update_scales=0, update_wall=0, timestep=cfg.timestep)
+    for s in (e, o):
+        s.apply_schedule(0)
+        s.run(20, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, spacestep=cfg.relaxation_spacestep,
+              seed=8)
+        s.run(20, first_step=20, temperature=cfg.temperature, timestep=cfg.timestep, seed=9)
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[prec]
+    assert e.get_context()["last_timestep"] == o.get_context()["last_timestep"] == cfg.timestep

@@ -129,9 +129,15 @@ def test_trajectory_philox_c1_wall_contact(c1_design, interphase_cfg, prec):
 
 
 @precisions
-def test_relaxation_spacestep(c1_design, interphase_cfg, prec):
+@pytest.mark.parametrize("fused", [3, 0], ids=["list", "cells"])
+def test_relaxation_spacestep(c1_design, interphase_cfg, prec, fused):
+    """spacestep 1e-3 (simulation_driver_relaxation.cpp:48-55), injected reference noise: the relaxation step on the
+    lists (default) and, on the fp32 engine, on a fresh cell list every step (GCS_OPT_FUSED_STEP 0)"""
+    if prec == 64 and fused != 3:
+        pytest.skip("the fp64 engine has the list step only")
     cfg = interphase_cfg
     e, o = both(c1_design, cfg, prec)
+    e.set_option(A.OPT_FUSED_STEP, fused)
     steps = 10
     xi = oracle.reference_normals(7, steps * c1_design.n * 3).reshape(steps, c1_design.n, 3)
     for s in (e, o):
@@ -141,6 +147,7 @@ def test_relaxation_spacestep(c1_design, interphase_cfg, prec):
     assert np.abs(e.get_positions() - o.get_positions()).max() <= X[prec]
     assert e.get_context()["last_timestep"] == pytest.approx(o.get_context()["last_timestep"],
                                                              rel={64: 1e-10, 32: 1e-4}[prec])
+    assert e.list_stats()["builds"] == (1 if fused == 3 else 0)
 
 
 @precisions
