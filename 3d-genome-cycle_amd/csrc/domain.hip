@@ -87,8 +87,12 @@ __global__ __launch_bounds__(256) void k_domain_pack(const DevCtx* __restrict__ 
 // (slots != 0: also the record's list slot in both slot-order buffers, when the current lists have one)
 __global__ __launch_bounds__(256) void k_domain_unpack(ForceArgs a, const float4* __restrict__ in,
                                                        const int* __restrict__ counts, int nbuf, int cap, int istride,
-                                                       int cstride, int slots)
+                                                       int cstride, int slots, float4* __restrict__ send, int nsend,
+                                                       int sstride)
 {
+    // the send bands' header rows for the next step's fused pack (this step's sends are done: stream order)
+    if (blockIdx.x == 0)
+        for (int p = threadIdx.x; p < nsend; p += blockDim.x) send[(size_t)p * sstride] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int b = 0; b < nbuf; ++b) {
         const int c = min(counts[(size_t)b * cstride], cap);
         for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < c; k += gridDim.x * blockDim.x) {
@@ -166,11 +170,11 @@ void launch_domain_shared_in(hipStream_t s, const ForceArgs& a, const int* idx, 
 }
 
 void launch_domain_unpack(hipStream_t s, const ForceArgs& a, const float4* in, const int* counts, int nbuf, int cap,
-                          int istride, int cstride, int slots)
+                          int istride, int cstride, int slots, float4* send, int nsend, int sstride)
 {
     const int blocks = std::max(1, std::min(1024, (cap + 255) / 256));
     hipLaunchKernelGGL(k_domain_unpack, dim3(blocks), dim3(256), 0, s, a, in, counts, nbuf, cap,
-                       istride > 0 ? istride : cap, cstride, slots);
+                       istride > 0 ? istride : cap, cstride, slots, send, send ? nsend : 0, sstride);
 }
 
 // zero the header rows (counts) of npeer bands of `stride` rows

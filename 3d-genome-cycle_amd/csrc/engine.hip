@@ -207,7 +207,8 @@ struct gcs_engine {
     int* islot = nullptr;   // [n] particle -> slot of the current lists (-1: not binned), decomposed list step
     bool dom_cont = false;  // the next domain step continues the previous one (no re-priming)
     int* dom_shared_idx = nullptr;   // shared particles (gcs_engine_set_domain_shared) [nshared]
-    int* dom_shared_flag = nullptr;  // [n] 1 = shared
+    int* dom_shared_flag = nullptr;  // [n] k + 1 for the k-th shared particle, 0 = not shared
+    bool dom_fused = false;          // the last decomposed step packed its bands itself (k_lstep<..., DOM>)
     int dom_nshared = 0;
     int64_t dom_next = 0;
     // engine-owned decomposed-run exchange (gcs_engine_domain_buffers) and its RCCL transport
@@ -2340,7 +2341,7 @@ int gcs_engine_set_domain_shared(gcs_engine* e, const int64_t* idx, int32_t coun
     for (int k = 0; k < count; ++k) {
         if (!valid_index(e, idx[k])) return fail(GCS_EINVAL, "shared particle index out of range");
         h[k] = (int)idx[k];
-        flag[h[k]] = 1;
+        flag[h[k]] = k + 1;  // (nonzero: shared; k + 1: its row in the allreduce buffer's shared block)
     }
     drop_domain_graph(e);
     if (e->dom_red && kDomainRed + 3 * count + e->dom_ndom != e->dom_nred) {
@@ -2405,9 +2406,17 @@ bool dom_list_ok(const gcs_engine* e)
 // the list-step half of a decomposed step before the allreduce: on a rebuild step the cells of this domain's region
 // (owned + ghosts) and the lists, then k_lstep<..., DOM> (owned slots; local reduction -> red), then the shared
 // particles' new positions into red
-void enqueue_dom_list_step(gcs_engine* e, int64_t st, double* red)
+void enqueue_dom_list_step(gcs_engine* e, int64_t st, double* red, bool fused_pack = false)
 {
-    const ForceArgs a = domain_args(e, red);
+    ForceArgs a = domain_args(e, red);
+    if (fused_pack) {  // the engine's bands (header rows zeroed by the last unpack) and reduction buffer
+        a.dom_bands = e->dom_send;
+        a.dom_bstride = e->dom_cap + 1;
+        a.dom_cap = e->dom_cap;
+        a.dom_npeer = e->dom_npeer;
+        a.dom_regions = e->dom_regions;
+        a.dom_shared = e->dom_shared_flag;
+    }
     if (e->l_need_build || st % e->list_every == 0) {
         const DomBox reg = dom_region(e);
         enqueue_count(e, &reg, e->islot);
@@ -2419,18 +2428,21 @@ void enqueue_dom_list_step(gcs_engine* e, int64_t st, double* red)
     }
     e->dom_flags_step = list_flags(e, st) | 8;  // 8: kLFlagDomain
     launch_list_step(e->stream, e->ctx, a, e->dom_flags_step);
-    launch_domain_shared_out(e->stream, e->ctx, a, e->dom_shared_idx, e->dom_nshared, red);
+    if (!fused_pack) launch_domain_shared_out(e->stream, e->ctx, a, e->dom_shared_idx, e->dom_nshared, red);
 }
 
 // after the allreduce: the tail from the global sums, the shared particles in, the send bands' headers zeroed
 void enqueue_dom_list_finish(gcs_engine* e, const double* glob, float4* bands, int npeer)
 {
-    launch_list_domain_tail(e->stream, e->ctx, domain_args(e), glob, e->dom_flags_step & ~8, e->dom_shared_idx,
-                            e->dom_nshared, bands, npeer, e->dom_cap + 1);
+    // (with the engine's reduction buffer: its shared block is zeroed for the next step's fused pack)
+    launch_list_domain_tail(e->stream, e->ctx, domain_args(e, e->dom_red), glob, e->dom_flags_step & ~8,
+                            e->dom_shared_idx, e->dom_nshared, bands, npeer, e->dom_cap + 1);
 }
 }  // namespace
 
-int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step, double* dev_reaction)
+// fused: the engine's own bands and reduction buffer take the step's band pack and shared particles from
+// k_lstep<..., DOM> itself (gcs_engine_domain_step_host; the pack then only copies); otherwise the separate pack
+static int domain_step_impl(gcs_engine* e, const gcs_bd_config* cfg, int64_t step, double* dev_reaction, bool fused)
 {
     if (!e || !cfg || !dev_reaction) return fail(GCS_EINVAL, "null argument");
     if (!e->dom) return fail(GCS_ESTATE, "gcs_engine_set_domain first");
@@ -2449,11 +2461,15 @@ int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step
         // buffer the first step writes must already carry every other particle's copy
         HIPCHK(hipMemcpyAsync(e->pos[e->parity ^ 1], e->pos[e->parity], (size_t)e->n * sizeof(float4),
                               hipMemcpyDeviceToDevice, e->stream));
+        // the fused pack's starting state: empty send bands, an empty shared block in the reduction buffer
+        if (e->dom_send) launch_band_headers_zero(e->stream, e->dom_send, e->dom_npeer, e->dom_cap + 1);
+        if (e->dom_red) HIPCHK(hipMemsetAsync(e->dom_red, 0, (size_t)e->dom_nred * sizeof(double), e->stream));
     }
     e->chain_valid = e->dense_chain = false;
     e->dom_next = step + 1;
+    e->dom_fused = fused && e->dom_list && e->dom_send && dev_reaction == e->dom_red;
     if (e->dom_list) {
-        enqueue_dom_list_step(e, step, dev_reaction);
+        enqueue_dom_list_step(e, step, dev_reaction, e->dom_fused);
         HIPCHK(hipGetLastError());
         return GCS_OK;
     }
@@ -2467,6 +2483,11 @@ int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step
     launch_domain_shared_out(e->stream, e->ctx, a, e->dom_shared_idx, e->dom_nshared, dev_reaction);
     HIPCHK(hipGetLastError());
     return GCS_OK;
+}
+
+int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step, double* dev_reaction)
+{
+    return domain_step_impl(e, cfg, step, dev_reaction, false);
 }
 
 int gcs_engine_domain_finish(gcs_engine* e, const double* dev_reaction)
@@ -2508,7 +2529,7 @@ int gcs_engine_domain_unpack(gcs_engine* e, const float* dev_in, const int32_t* 
     if (nbuf <= 0) return GCS_OK;
     HIPCHK(hipSetDevice(e->device));
     launch_domain_unpack(e->stream, domain_args(e), (const float4*)dev_in, dev_counts, nbuf, cap, 0, 1,
-                         e->dom_list ? 1 : 0);
+                         e->dom_list ? 1 : 0, e->dom_send, e->dom_send ? e->dom_npeer : 0, e->dom_cap + 1);
     HIPCHK(hipGetLastError());
     return GCS_OK;
 }
@@ -2560,9 +2581,10 @@ void enqueue_band_pack(gcs_engine* e, bool headers_zeroed = false)
 void enqueue_band_unpack(gcs_engine* e)
 {
     const int stride = e->dom_cap + 1;
-    if (e->dom_npeer > 0)
+    if (e->dom_npeer > 0)  // (and the send bands' headers zeroed for the next step's fused pack)
         launch_domain_unpack(e->stream, domain_args(e), e->dom_recv + 1, reinterpret_cast<const int*>(e->dom_recv),
-                             e->dom_npeer, e->dom_cap, stride, 4 * stride, e->dom_list ? 1 : 0);
+                             e->dom_npeer, e->dom_cap, stride, 4 * stride, e->dom_list ? 1 : 0, e->dom_send,
+                             e->dom_npeer, stride);
 }
 
 // one grouped send/recv of every peer's band (the count in its header row)
@@ -2588,12 +2610,11 @@ int enqueue_rccl_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step)
 {
     const RcclApi* r = rccl();
     if (e->dom_list) {
-        // list step: k_lstep<DOM> (+ rebuild) + shared out, allreduce, tail + shared in + headers, pack, exchange,
-        // unpack: 5 launches and 2 collectives per step
-        enqueue_dom_list_step(e, step, e->dom_red);
+        // list step: k_lstep<DOM> (+ rebuild) with the band pack and the shared particles fused, allreduce, tail +
+        // shared in, exchange, unpack (+ the send headers zeroed): 3 launches and 2 collectives per step
+        enqueue_dom_list_step(e, step, e->dom_red, true);
         NCCLCHK(r->allReduce(e->dom_red, e->dom_glob, e->dom_nred, ncclDouble, ncclSum, e->nccl, e->stream));
-        enqueue_dom_list_finish(e, e->dom_glob, e->dom_send, e->dom_npeer);
-        enqueue_band_pack(e, true);
+        enqueue_dom_list_finish(e, e->dom_glob, nullptr, 0);
         if (int rc = enqueue_band_exchange(e)) return rc;
         enqueue_band_unpack(e);
         HIPCHK(hipGetLastError());
@@ -2734,7 +2755,7 @@ int gcs_engine_domain_step_host(gcs_engine* e, const gcs_bd_config* cfg, int64_t
     if (!e || !red) return fail(GCS_EINVAL, "null argument");
     if (!e->dom_red) return fail(GCS_ESTATE, "gcs_engine_domain_buffers first");
     if (nred != e->dom_nred) return fail(GCS_EINVAL, "reaction buffer size does not match");
-    int rc = gcs_engine_domain_step(e, cfg, step, e->dom_red);
+    int rc = domain_step_impl(e, cfg, step, e->dom_red, true);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(red, e->dom_red, nred * sizeof(double), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
@@ -2756,7 +2777,7 @@ int gcs_engine_domain_pack_host(gcs_engine* e, float* bands)
     if (!e) return fail(GCS_EINVAL, "null argument");
     if (!e->dom_send) return fail(GCS_ESTATE, "gcs_engine_domain_buffers first");
     HIPCHK(hipSetDevice(e->device));
-    enqueue_band_pack(e);
+    if (!e->dom_fused) enqueue_band_pack(e);  // (a fused step packed its bands already)
     HIPCHK(hipGetLastError());
     if (!bands) return GCS_OK;  // packed on the device only (in-process transport: gcs_engine_domain_receive)
     if (e->dom_npeer > 0)

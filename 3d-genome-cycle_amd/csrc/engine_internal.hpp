@@ -254,6 +254,17 @@ struct ForceArgs {
     int dom_dbase, dom_index, dom_ndom;
     int* dom_flags;
     int* islot;
+    // the band pack and the shared particles' positions fused into k_lstep<..., DOM> (the engine's RCCL run;
+    // dom_bands == nullptr: the separate k_domain_pack / k_domain_shared_out launches): each owned particle's record
+    // {new x, y, z, index} goes to every peer p whose region holds its old or new position (band p's records at
+    // dom_bands[p * dom_bstride + 1 + k], k < cap, its count in the header row p * dom_bstride, zeroed by the previous
+    // step's unpack), an owned shared particle's new position into its row of dom_red's shared block (k_ldom_tail
+    // zeroes the block for the next step), and a bond of an owned particle reaching beyond the halo raises
+    // dom_flags bit 0 (the local-terms wave)
+    float4* dom_bands;
+    int dom_bstride, dom_cap, dom_npeer;
+    const DomBox* dom_regions;
+    const int* dom_shared;  // [N] k + 1 for the k-th shared particle, 0 otherwise
     // list step (GCS_OPT_FUSED_STEP 3; DESIGN.md "The list step"): per sorted slot s and wave w (w < 4) the
     // sorted slots of the pair partners found within build cutoff + list_skin are
     // list[(w * list_cap + k) * list_stride + s], k < count, count = lcount[w * list_stride + s] & kListCountMask
@@ -488,7 +499,8 @@ void launch_domain_shared_out(hipStream_t s, const DevCtx* ctx, const ForceArgs&
 void launch_domain_shared_in(hipStream_t s, const ForceArgs& a, const int* idx, int nshared, const double* buf);
 // slots != 0 also refreshes the records' list slots (both psort buffers)
 void launch_domain_unpack(hipStream_t s, const ForceArgs& a, const float4* in, const int* counts, int nbuf, int cap,
-                          int istride = 0, int cstride = 1, int slots = 0);
+                          int istride = 0, int cstride = 1, int slots = 0, float4* send = nullptr, int nsend = 0,
+                          int sstride = 0);
 void launch_tail_reduce(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int fblocks, double* out);
 
 inline int force_blocks(int n) { return (n + kTile - 1) / kTile; }

@@ -3090,6 +3090,24 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         R rin[3] = {0, 0, 0}, rout[3] = {0, 0, 0};
         local_terms<kModeStep, GCS_LIST_BOND_BATCH, R>(ctx, a, i, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout,
                                                        erow);
+        if constexpr (DOM) {
+            // the fused pack's bond check (k_domain_pack's): a bond of an owned particle longer than the halo (its
+            // partner may be a stale ghost); the cut-off droplet and shared particles excepted
+            if (a.dom_bands && act && a.has_bonds && !(a.dom_shared && a.dom_shared[i])) {
+                const R4* __restrict__ pc = St<R>::pos(a, par);
+                const float h2 = a.dom_halo * a.dom_halo;
+                bool far = false;
+                for (int q = erow.x; q < erow.y; ++q) {
+                    const int2 en2 = a.bent[q];
+                    if ((en2.y & 15) == kSoftwell || (a.dom_shared && a.dom_shared[en2.x])) continue;
+                    const R4 pj = pc[en2.x];
+                    const float dx = (float)pi.x - (float)pj.x, dy = (float)pi.y - (float)pj.y,
+                                dz = (float)pi.z - (float)pj.z;
+                    far |= dx * dx + dy * dy + dz * dz >= h2;
+                }
+                if (far) atomicOr(a.dom_flags, 1);
+            }
+        }
         s_locf[lane] = mk4<R>(lfx, lfy, lfz, km.x);
         s_locr[lane] = mk4<R>(act ? rin[0] : R(0), act ? rin[1] : R(0), act ? rin[2] : R(0), R(0));
         s_loco[lane] = mk4<R>(act ? rout[0] : R(0), act ? rout[1] : R(0), act ? rout[2] : R(0), R(0));
@@ -3257,6 +3275,48 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
             R4* __restrict__ qn = St<R>::psort(a, par ^ 1);
             pn[i] = mk4<R>(nxp, nyp, nzp, R(0));
             qn[s] = mk4<R>(nxp, nyp, nzp, pi.w);
+        }
+        if constexpr (DOM) {
+            if (a.dom_bands) {
+                // the fused band pack (k_domain_pack's rule: owned at the step start, old or new position in the
+                // peer's region) and the owned shared particles' new positions (k_domain_shared_out's)
+                const float ox = (float)pi.x, oy = (float)pi.y, oz = (float)pi.z;
+                const float nx = (float)nxp, ny = (float)nyp, nz = (float)nzp;
+                if (act && a.dom_shared) {
+                    const int k = a.dom_shared[i];
+                    if (k > 0) {
+                        double* r = a.dom_red + kDomainRed + 3 * (k - 1);
+                        r[0] = (double)nxp;
+                        r[1] = (double)nyp;
+                        r[2] = (double)nzp;
+                    }
+                }
+                int* const counts = reinterpret_cast<int*>(a.dom_bands);
+                const size_t cstride = (size_t)4 * a.dom_bstride;
+                // every peer's ballot first, then one counter atomic per peer, all in flight together (lane p)
+                int mine = 0;
+                for (int p = 0; p < a.dom_npeer; ++p) {
+                    const DomBox r = a.dom_regions[p];
+                    const bool send = act && (box_has(r, ox, oy, oz) || box_has(r, nx, ny, nz));
+                    const int c = __popcll(__ballot(send));
+                    if (lane == p) mine = c;
+                }
+                int base = 0;
+                if (lane < a.dom_npeer && mine > 0) base = atomicAdd(&counts[(size_t)lane * cstride], mine);
+                for (int p = 0; p < a.dom_npeer; ++p) {
+                    const DomBox r = a.dom_regions[p];
+                    const bool send = act && (box_has(r, ox, oy, oz) || box_has(r, nx, ny, nz));
+                    const unsigned long long m = __ballot(send);
+                    const int at = __shfl(base, p);
+                    if (send) {
+                        const int o = at + __popcll(m & ((1ull << lane) - 1ull));
+                        if (o < a.dom_cap)
+                            a.dom_bands[(size_t)p * a.dom_bstride + 1 + o] = make_float4(nx, ny, nz, __int_as_float(i));
+                        else
+                            atomicOr(a.dom_flags, 2);
+                    }
+                }
+            }
         }
         if (dbg && tid == 0) dbg[4] = wall_clock64();
         // the list bookkeeping in fp32: the displacement from the build and the bbox of the roundings
@@ -3496,6 +3556,10 @@ __global__ __launch_bounds__(64) void k_ldom_tail(DevCtx* __restrict__ ctx, Forc
         }
     }
     for (int p = tid; p < npeer; p += blockDim.x) bands[(size_t)p * bstride] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // the shared block of this domain's reduction buffer for the next step's owners (the fused pack writes only
+    // the owned particles' rows; the allreduce of this step has consumed it)
+    if (a.dom_red)
+        for (int k = tid; k < 3 * nshared; k += blockDim.x) a.dom_red[kDomainRed + k] = 0.0;
 }
 
 // ----------------------------------------------------------------------------------------------------

@@ -6,7 +6,7 @@ src=$(cd "$(dirname "$0")/../3d-genome-cycle_amd/csrc" && pwd)
 /opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC --offload-arch=gfx950 -fno-slp-vectorize -Wno-unused-result "$@" \
   --cuda-device-only -S -o /tmp/gcs_kernels_scratch.s "$src/kernels.hip"
 awk '
-/^_ZN3gcs12_GLOBAL__N_1[0-9]+k_(force|lstep|lbuild|small)[^:]*:/ {name=$1; n=0; next}
+/^_ZN3gcs12_GLOBAL__N_1[0-9]+k_(force|lstep|lbuild|lupdate|eval64)[^:]*:/ {name=$1; n=0; next}
 name!="" && /scratch_(load|store)/ {n++}
 name!="" && /^\.Lfunc_end/ {cnt[name]=n; name=""}
 /\.amdhsa_kernel / {k=$2}
