@@ -1041,7 +1041,9 @@ int probe_density(gcs_engine* e)
     // its copies and kernels; profiling runs turn the probe off: GCS_OPT_DENSE_NEIGHBORS 0, tools/profile.sh)
     double cs = 1.0;
     HIPCHK(hipStreamSynchronize(e->stream));
-    HIPCHK(hipMemcpy(&cs, (const char*)e->ctx + offsetof(DevCtx, cs), sizeof(cs), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(&cs, (const char*)e->ctx + offsetof(DevCtx, cs), sizeof(cs), hipMemcpyDeviceToHost,
+                          e->stream));  // (the engine's stream: no legacy null-stream work anywhere in the library)
+    HIPCHK(hipStreamSynchronize(e->stream));
     const double rc = (double)e->fa.pf.pair_dist * (e->fa.pair_scaled ? cs : 1.0);
     int rc_;
     if (!(rc > 0) || e->n < 2) return GCS_OK;
@@ -1052,7 +1054,8 @@ int probe_density(gcs_engine* e)
     HIPCHK(hipGetLastError());
     int pairs = 0;
     HIPCHK(hipStreamSynchronize(e->stream));
-    HIPCHK(hipMemcpy(&pairs, e->s_total, sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(&pairs, e->s_total, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
     e->dense_mean = 2.0 * pairs / (double)e->n;
     e->dense = e->dense_mean * (list_u16(e->n) ? 1.0 : 2.0) > (double)e->dense_opt;
     return GCS_OK;

@@ -328,14 +328,15 @@ STEP_KERNEL = {(3, 64): ("k_lstep<..., double>", "pmc_lstep64_traffic.json"),
 
 
 def read_traffic(fused=3, precision=64):
-    """HBM bytes per launch of the step's dominant kernel from the committed rocprofv3 PMC pass (profiles/)."""
+    """The committed rocprofv3 record of the step's dominant kernel (profiles/): HBM bytes per launch from the PMC
+    passes (2 x FETCH_SIZE + WRITE_SIZE: reads and writes) and the kernel-trace average duration of the same run."""
     name = STEP_KERNEL.get((fused, precision), (None, None))[1]
     if name is None:
         return None
     p = ROOT / "profiles" / name
     if p.exists():
         try:
-            return json.loads(p.read_text()).get("bytes_per_launch")
+            return json.loads(p.read_text())
         except Exception:
             return None
     return None
@@ -476,6 +477,19 @@ def decomp_main(args):
     el_max = max_over_ranks(dist, el)
     run.check()
     n = design.n
+    ref = None
+    if world == 1:
+        # the same trajectory undecomposed (one engine, same window, steps and shape): what the decomposition costs
+        e = make_engine(design, cfg, local, window, state, precision=32)
+        if args.fused is not None:
+            e.set_option(A.OPT_FUSED_STEP, args.fused)
+        e.run(args.warmup, first_step=window, seed=seed, timestep=cfg.timestep)
+        e.synchronize()
+        t0 = time.perf_counter()
+        e.run(args.steps, first_step=window + args.warmup, seed=seed, timestep=cfg.timestep)
+        e.synchronize()
+        ref = n * args.steps / (time.perf_counter() - t0)
+        e.close()
     if rank == 0:
         line = {
             "metric": "bead-updates/sec (whole node), decomposed single trajectory",
@@ -488,7 +502,9 @@ def decomp_main(args):
                        "particles": n, "domains": ndom, "halo": halo, "parallelism": f"domains{ndom}",
                        "band_capacity_rank0": doms[0].cap, "peers_rank0": doms[0].peers,
                        "bytes_per_peer_per_step": 16 * (doms[0].cap + 1),
-                       "step_shape": "list" if doms[0].e.list_stats()["builds"] > 0 else "tile"},
+                       "step_shape": "list" if doms[0].e.list_stats()["builds"] > 0 else "tile",
+                       "undecomposed_value": ref,
+                       "decomposed_over_undecomposed": (n * args.steps / el_max / ref) if ref else None},
         }
         print(json.dumps(line), flush=True)
     for d in doms:
@@ -690,6 +706,7 @@ def replica_main(args):
     force_ms = prof["force_ms"]
     bpu = BYTES_PER_UPDATE[args.precision]
     achieved = n * bpu / (force_ms * 1e-3) / 1e9
+    tr = read_traffic(args.fused, args.precision)
     ctx = eng.get_context()
     lst = eng.list_stats() if hasattr(eng, "list_stats") else None
     if lst is not None:  # the list step's rebuild cadence and exact-search fallbacks (DESIGN.md "The list step")
@@ -798,10 +815,15 @@ def replica_main(args):
                    "c3_cycle_wall_s": cycle["cycle_wall_s"] if cycle else None, "c3_cycle": cycle,
                    "precision": args.precision, "f32_value": f32["value"] if f32 else None, "f32": f32},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(args.fused, args.precision),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": tr.get("bytes_per_launch") if tr else None,
                      "kernel": STEP_KERNEL.get((args.fused, args.precision), ("?",))[0], "force_ms": force_ms,
                      "cell_ms": prof["cell_ms"], "tail_ms": prof["tail_ms"], "bytes_per_launch": n * bpu,
-                     "bytes_per_update": bpu},
+                     "bytes_per_update": bpu,
+                     # the same accounting on the committed rocprofv3 kernel trace (profiles/, R = 1 bench)
+                     "rocprof_avg_us": tr.get("avg_us") if tr else None,
+                     "frac_rocprof": (n * bpu / (tr["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS)
+                     if tr and tr.get("avg_us") else None,
+                     "traffic_source": tr.get("source") if tr else None},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
