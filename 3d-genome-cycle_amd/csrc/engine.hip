@@ -2380,12 +2380,25 @@ int gcs_engine_stream(gcs_engine* e, void** stream)
 namespace {
 // the decomposed step's argument block: the list step's (dom_list) or the tile step's, with the domain geometry, the
 // reduction layout (dom_red: the caller's buffer) and the flags
+bool dom_list_ok(const gcs_engine* e);
+// The ghosts a decomposed step BINS: the list step needs a particle's partners within its list radius (cutoff at
+// cs = 1 + skin) of the box, plus the displacement since the build, so it bins the ghosts within list radius + one
+// more skin (the motion check flags cutoff + largest displacement beyond it); the exchange halo itself is the
+// chain bonds' reach (C5: 0.54 against a list radius of 0.21), which only the bonded partners need, and they are
+// read by index from the position buffers the unpack refreshes, binned or not.  The tile step bins the whole halo.
+float dom_bin_halo(const gcs_engine* e)
+{
+    if (!dom_list_ok(e)) return e->dom_halo;
+    return std::min(e->dom_halo, e->fa.pf.pair_dist + 2.f * list_skin(e));
+}
+
 ForceArgs domain_args(const gcs_engine* e, double* red = nullptr)
 {
     ForceArgs a = e->dom_list ? list_args(e) : e->fa;
     a.dom_on = 1;
     a.dom = e->dom_box;
     a.dom_halo = e->dom_halo;
+    a.dom_bin_halo = dom_bin_halo(e);
     a.bucket_p = nullptr;
     a.dom_red = red;
     a.dom_dbase = kDomainRed + 3 * e->dom_nshared;
@@ -2396,7 +2409,7 @@ ForceArgs domain_args(const gcs_engine* e, double* red = nullptr)
     return a;
 }
 
-DomBox dom_region(const gcs_engine* e) { return region_of(e->dom_box, e->dom_halo); }
+DomBox dom_region(const gcs_engine* e) { return region_of(e->dom_box, dom_bin_halo(e)); }
 
 // the decomposed run takes the list step when the engine would (list step selected, lists admitted) and the halo
 // holds the list radius: a partner within the cutoff of an owned particle must have been binned at the build

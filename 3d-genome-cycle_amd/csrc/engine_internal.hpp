@@ -245,7 +245,9 @@ struct ForceArgs {
     // dom_halo of the box (owned + ghosts, refreshed every step by the owners' band exchange).  dom_on == 0: off.
     int dom_on;
     DomBox dom;
-    float dom_halo;
+    float dom_halo;      // the exchange halo: a peer receives the owned particles within it of its box (bond reach)
+    float dom_bin_halo;  // the binning halo (<= dom_halo): the decomposed list step bins only the ghosts within the
+                         // list radius + a skin of the box; the motion check holds cutoff + displacement below it
     const double* ext_react;  // != nullptr: the step's wall reaction summed over all domains (allreduced), [6]
     // decomposed list step: the local reduction goes to dom_red (layout kDomainRed), the per-domain slot of the
     // largest displacement at dom_red[dom_dbase + dom_index] (dom_ndom slots: a sum-allreduce carries the max);

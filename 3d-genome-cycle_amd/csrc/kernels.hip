@@ -3533,12 +3533,12 @@ __global__ __launch_bounds__(64) void k_ldom_tail(DevCtx* __restrict__ ctx, Forc
         for (int q = 0; q < a.dom_ndom; ++q) ld = fmaxf(ld, (float)glob[a.dom_dbase + q]);
         t.ld = ld;
         for (int k = 0; k < 3; ++k) {
-            t.bb[k] = ctx->bbox_lo[k] - a.dom_halo;
-            t.bb[3 + k] = ctx->bbox_hi[k] + a.dom_halo;
+            t.bb[k] = ctx->bbox_lo[k] - a.dom_bin_halo;
+            t.bb[3 + k] = ctx->bbox_hi[k] + a.dom_bin_halo;
         }
         list_tail_apply(ctx, a, tin, t, flags);
         int fl = nown != (long long)a.n ? kDomFlagLost : 0;
-        if (pair_cutoff(a, ctx->cs) + ld > a.dom_halo) fl |= kDomFlagMotion;
+        if (pair_cutoff(a, ctx->cs) + ld > a.dom_bin_halo) fl |= kDomFlagMotion;
         if (fl) atomicOr(a.dom_flags, fl);
     }
     constexpr int kIdx = (1 << kListIndexBits) - 1;

@@ -1,6 +1,6 @@
 """Decomposition geometry of a configuration (no GPU): per rank the owned beads, the region's binned beads (owned +
 ghosts), the peers, the band records per peer (owned beads inside the peer's region: what the owner sends each step,
-16 B each) and the halo's share of the binned set, for recursive-bisection boxes and for z-slabs.  The numbers
+16 B each) and the binning halo's share of the binned set, for recursive-bisection boxes and for z-slabs.  The numbers
 DESIGN.md §8 quotes for 8 ranks.
 
 usage: python tools/decomp_plan.py [c2|c5] [ranks...]"""
@@ -23,14 +23,17 @@ else:
 x = design.positions
 n = x.shape[0]
 halo = domain.domain_halo(cfg)
-print(f"{config}: {n} beads, halo {halo:.3f} (list radius {max(cfg.a_core_diameter, cfg.b_core_diameter) * (1 + domain.LIST_SKIN):.3f})")
+rc = max(cfg.a_core_diameter, cfg.b_core_diameter)
+bin_halo = min(halo, rc * (1 + 2 * domain.LIST_SKIN))  # the engine's binning halo (engine.hip dom_bin_halo)
+print(f"{config}: {n} beads, exchange halo {halo:.3f}, binning halo {bin_halo:.3f} (list radius "
+      f"{rc * (1 + domain.LIST_SKIN):.3f})")
 for kind in ("boxes", "slabs"):
     for k in ranks:
         boxes = domain.plan_boxes(x, k) if kind == "boxes" else domain.plan_slabs(x[:, 2], k)
         rows = []
         for d in range(k):
             own = domain.in_box(x, boxes[d])
-            binned = domain.in_box(x, domain.region(boxes[d], halo))
+            binned = domain.in_box(x, domain.region(boxes[d], bin_halo))
             peers = domain.peers_of(d, boxes, halo)
             bands = [int((own & domain.in_box(x, domain.region(boxes[p], halo))).sum()) for p in peers]
             rows.append((int(own.sum()), int(binned.sum()), len(peers), sum(bands), max(bands, default=0)))
