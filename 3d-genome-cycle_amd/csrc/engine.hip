@@ -212,8 +212,9 @@ struct gcs_engine {
     int dom_nshared = 0;
     int64_t dom_next = 0;
     // engine-owned decomposed-run exchange (gcs_engine_domain_buffers) and its RCCL transport
-    float4* dom_send = nullptr;  // [npeer][cap + 1] rows: row 0 of a band = {count bits, 0, 0, 0}, then records
-    float4* dom_recv = nullptr;
+    // [npeer][cap + 1] records of band_record_bytes(prec): row 0 of a band = {count bits, 0, 0, 0}, then records
+    unsigned char* dom_send = nullptr;
+    unsigned char* dom_recv = nullptr;
     int dom_cap = 0;
     double* dom_red = nullptr;   // [nred]: local reduction + shared positions; dom_glob: the sum over domains
     double* dom_glob = nullptr;
@@ -2300,8 +2301,6 @@ int gcs_engine_set_domain(gcs_engine* e, const double* box, double halo, const d
         return GCS_OK;
     }
     if (!box) return fail(GCS_EINVAL, "null argument");
-    if (e->prec == 64)
-        return fail(GCS_ESTATE, "spatial decomposition runs on fp32 engines (GCS_PRECISION_F32)");
     for (int k = 0; k < 3; ++k)
         if (!(box[k] < box[3 + k])) return fail(GCS_EINVAL, "domain box must have lo < hi on every axis");
     if (npeer < 0 || npeer > kMaxPeers || (npeer > 0 && !peer_boxes)) return fail(GCS_EINVAL, "bad peer list");
@@ -2448,7 +2447,7 @@ void enqueue_dom_list_step(gcs_engine* e, int64_t st, double* red, bool fused_pa
 }
 
 // after the allreduce: the tail from the global sums, the shared particles in, the send bands' headers zeroed
-void enqueue_dom_list_finish(gcs_engine* e, const double* glob, float4* bands, int npeer)
+void enqueue_dom_list_finish(gcs_engine* e, const double* glob, void* bands, int npeer)
 {
     // (with the engine's reduction buffer: its shared block is zeroed for the next step's fused pack)
     launch_list_domain_tail(e->stream, e->ctx, domain_args(e, e->dom_red), glob, e->dom_flags_step & ~8,
@@ -2470,15 +2469,22 @@ static int domain_step_impl(gcs_engine* e, const gcs_bd_config* cfg, int64_t ste
         int rc = prepare(e);
         if (rc) return rc;
         e->dom_list = dom_list_ok(e);
+        if (e->prec == 64 && !e->dom_list)
+            return fail(GCS_ESTATE, "an fp64 decomposed run takes the list step: it needs a neighbor soft-core field "
+                                    "and a halo of at least the list radius (cutoff x (1 + skin))");
         if (e->dom_list && !e->islot && (rc = dalloc(&e->islot, e->n))) return rc;
         drop_domain_graph(e);  // captured for the other step shape, or another rebuild phase
         if ((rc = begin_run(e, cfg, step))) return rc;
         // both position buffers hold the start state: a domain writes only what it owns or receives, so the
         // buffer the first step writes must already carry every other particle's copy
-        HIPCHK(hipMemcpyAsync(e->pos[e->parity ^ 1], e->pos[e->parity], (size_t)e->n * sizeof(float4),
-                              hipMemcpyDeviceToDevice, e->stream));
+        if (e->prec == 64)
+            HIPCHK(hipMemcpyAsync(e->dpos[e->parity ^ 1], e->dpos[e->parity], (size_t)e->n * sizeof(double4),
+                                  hipMemcpyDeviceToDevice, e->stream));
+        else
+            HIPCHK(hipMemcpyAsync(e->pos[e->parity ^ 1], e->pos[e->parity], (size_t)e->n * sizeof(float4),
+                                  hipMemcpyDeviceToDevice, e->stream));
         // the fused pack's starting state: empty send bands, an empty shared block in the reduction buffer
-        if (e->dom_send) launch_band_headers_zero(e->stream, e->dom_send, e->dom_npeer, e->dom_cap + 1);
+        if (e->dom_send) launch_band_headers_zero(e->stream, e->dom_send, e->dom_npeer, e->dom_cap + 1, e->prec);
         if (e->dom_red) HIPCHK(hipMemsetAsync(e->dom_red, 0, (size_t)e->dom_nred * sizeof(double), e->stream));
     }
     e->chain_valid = e->dense_chain = false;
@@ -2526,25 +2532,25 @@ int gcs_engine_domain_finish(gcs_engine* e, const double* dev_reaction)
     return GCS_OK;
 }
 
-int gcs_engine_domain_pack(gcs_engine* e, float* dev_out, int32_t* dev_counts, int32_t cap, int32_t* dev_flags)
+int gcs_engine_domain_pack(gcs_engine* e, void* dev_out, int32_t* dev_counts, int32_t cap, int32_t* dev_flags)
 {
     if (!e || (e->dom_npeer > 0 && (!dev_out || !dev_counts)) || !dev_flags) return fail(GCS_EINVAL, "null argument");
     if (!e->dom) return fail(GCS_ESTATE, "gcs_engine_set_domain first");
     if (cap < 1) return fail(GCS_EINVAL, "band capacity must be positive");
     HIPCHK(hipSetDevice(e->device));
     if (e->dom_npeer > 0) HIPCHK(hipMemsetAsync(dev_counts, 0, e->dom_npeer * sizeof(int), e->stream));
-    launch_domain_pack(e->stream, e->ctx, domain_args(e), e->dom_regions, e->dom_npeer, (float4*)dev_out, dev_counts,
+    launch_domain_pack(e->stream, e->ctx, domain_args(e), e->dom_regions, e->dom_npeer, dev_out, dev_counts,
                        cap, dev_flags, e->dom_shared_flag, 0, 1, e->dom_list ? 1 : 0);
     HIPCHK(hipGetLastError());
     return GCS_OK;
 }
 
-int gcs_engine_domain_unpack(gcs_engine* e, const float* dev_in, const int32_t* dev_counts, int32_t nbuf, int32_t cap)
+int gcs_engine_domain_unpack(gcs_engine* e, const void* dev_in, const int32_t* dev_counts, int32_t nbuf, int32_t cap)
 {
     if (!e || (nbuf > 0 && (!dev_in || !dev_counts))) return fail(GCS_EINVAL, "null argument");
     if (nbuf <= 0) return GCS_OK;
     HIPCHK(hipSetDevice(e->device));
-    launch_domain_unpack(e->stream, domain_args(e), (const float4*)dev_in, dev_counts, nbuf, cap, 0, 1,
+    launch_domain_unpack(e->stream, domain_args(e), dev_in, dev_counts, nbuf, cap, 0, 1,
                          e->dom_list ? 1 : 0, e->dom_send, e->dom_send ? e->dom_npeer : 0, e->dom_cap + 1);
     HIPCHK(hipGetLastError());
     return GCS_OK;
@@ -2565,12 +2571,13 @@ int gcs_engine_domain_buffers(gcs_engine* e, int32_t cap, int32_t* nred)
     const size_t rows = (size_t)std::max(e->dom_npeer, 1) * (cap + 1);
     const int nr = kDomainRed + 3 * e->dom_nshared + e->dom_ndom;
     int rc;
-    if ((rc = dalloc(&e->dom_send, rows)) || (rc = dalloc(&e->dom_recv, rows)) || (rc = dalloc(&e->dom_red, nr)) ||
+    const size_t rb = band_record_bytes(e->prec);
+    if ((rc = dalloc(&e->dom_send, rows * rb)) || (rc = dalloc(&e->dom_recv, rows * rb)) || (rc = dalloc(&e->dom_red, nr)) ||
         (rc = dalloc(&e->dom_glob, nr)))
         return rc;
     if (!e->dom_flags && (rc = dalloc(&e->dom_flags, 1))) return rc;
-    HIPCHK(hipMemsetAsync(e->dom_send, 0, rows * sizeof(float4), e->stream));
-    HIPCHK(hipMemsetAsync(e->dom_recv, 0, rows * sizeof(float4), e->stream));
+    HIPCHK(hipMemsetAsync(e->dom_send, 0, rows * rb, e->stream));
+    HIPCHK(hipMemsetAsync(e->dom_recv, 0, rows * rb, e->stream));
     HIPCHK(hipMemsetAsync(e->dom_red, 0, nr * sizeof(double), e->stream));
     HIPCHK(hipMemsetAsync(e->dom_glob, 0, nr * sizeof(double), e->stream));
     HIPCHK(hipMemsetAsync(e->dom_flags, 0, sizeof(int), e->stream));
@@ -2588,18 +2595,20 @@ namespace {
 void enqueue_band_pack(gcs_engine* e, bool headers_zeroed = false)
 {
     const int stride = e->dom_cap + 1;
-    if (!headers_zeroed) launch_band_headers_zero(e->stream, e->dom_send, e->dom_npeer, stride);
-    launch_domain_pack(e->stream, e->ctx, domain_args(e), e->dom_regions, e->dom_npeer, e->dom_send + 1,
+    const size_t rb = band_record_bytes(e->prec);
+    if (!headers_zeroed) launch_band_headers_zero(e->stream, e->dom_send, e->dom_npeer, stride, e->prec);
+    launch_domain_pack(e->stream, e->ctx, domain_args(e), e->dom_regions, e->dom_npeer, e->dom_send + rb,
                        reinterpret_cast<int*>(e->dom_send), e->dom_cap, e->dom_flags, e->dom_shared_flag, stride,
-                       4 * stride, e->dom_list ? 1 : 0);
+                       stride * (int)(rb / sizeof(int)), e->dom_list ? 1 : 0);
 }
 
 void enqueue_band_unpack(gcs_engine* e)
 {
     const int stride = e->dom_cap + 1;
     if (e->dom_npeer > 0)  // (and the send bands' headers zeroed for the next step's fused pack)
-        launch_domain_unpack(e->stream, domain_args(e), e->dom_recv + 1, reinterpret_cast<const int*>(e->dom_recv),
-                             e->dom_npeer, e->dom_cap, stride, 4 * stride, e->dom_list ? 1 : 0, e->dom_send,
+        launch_domain_unpack(e->stream, domain_args(e), e->dom_recv + band_record_bytes(e->prec),
+                             reinterpret_cast<const int*>(e->dom_recv), e->dom_npeer, e->dom_cap, stride,
+                             stride * (int)(band_record_bytes(e->prec) / sizeof(int)), e->dom_list ? 1 : 0, e->dom_send,
                              e->dom_npeer, stride);
 }
 
@@ -2608,13 +2617,11 @@ int enqueue_band_exchange(gcs_engine* e)
 {
     if (e->dom_npeer == 0) return GCS_OK;
     const RcclApi* r = rccl();
-    const size_t cnt = (size_t)4 * (e->dom_cap + 1);
+    const size_t bytes = band_record_bytes(e->prec) * (e->dom_cap + 1);  // one band: header row + records
     NCCLCHK(r->groupStart());
     for (int p = 0; p < e->dom_npeer; ++p) {
-        NCCLCHK(r->send(e->dom_send + (size_t)p * (e->dom_cap + 1), cnt, ncclFloat, e->dom_peer_rank[p], e->nccl,
-                        e->stream));
-        NCCLCHK(r->recv(e->dom_recv + (size_t)p * (e->dom_cap + 1), cnt, ncclFloat, e->dom_peer_rank[p], e->nccl,
-                        e->stream));
+        NCCLCHK(r->send(e->dom_send + (size_t)p * bytes, bytes, ncclUint8, e->dom_peer_rank[p], e->nccl, e->stream));
+        NCCLCHK(r->recv(e->dom_recv + (size_t)p * bytes, bytes, ncclUint8, e->dom_peer_rank[p], e->nccl, e->stream));
     }
     NCCLCHK(r->groupEnd());
     return GCS_OK;
@@ -2788,7 +2795,7 @@ int gcs_engine_domain_finish_host(gcs_engine* e, const double* glob, int32_t nre
     return gcs_engine_domain_finish(e, e->dom_glob);
 }
 
-int gcs_engine_domain_pack_host(gcs_engine* e, float* bands)
+int gcs_engine_domain_pack_host(gcs_engine* e, void* bands)
 {
     if (!e) return fail(GCS_EINVAL, "null argument");
     if (!e->dom_send) return fail(GCS_ESTATE, "gcs_engine_domain_buffers first");
@@ -2797,19 +2804,19 @@ int gcs_engine_domain_pack_host(gcs_engine* e, float* bands)
     HIPCHK(hipGetLastError());
     if (!bands) return GCS_OK;  // packed on the device only (in-process transport: gcs_engine_domain_receive)
     if (e->dom_npeer > 0)
-        HIPCHK(hipMemcpyAsync(bands, e->dom_send, (size_t)e->dom_npeer * (e->dom_cap + 1) * sizeof(float4),
+        HIPCHK(hipMemcpyAsync(bands, e->dom_send, (size_t)e->dom_npeer * (e->dom_cap + 1) * band_record_bytes(e->prec),
                               hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     return GCS_OK;
 }
 
-int gcs_engine_domain_unpack_host(gcs_engine* e, const float* bands)
+int gcs_engine_domain_unpack_host(gcs_engine* e, const void* bands)
 {
     if (!e || (e->dom_npeer > 0 && !bands)) return fail(GCS_EINVAL, "null argument");
     if (!e->dom_recv) return fail(GCS_ESTATE, "gcs_engine_domain_buffers first");
     if (e->dom_npeer == 0) return GCS_OK;
     HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipMemcpyAsync(e->dom_recv, bands, (size_t)e->dom_npeer * (e->dom_cap + 1) * sizeof(float4),
+    HIPCHK(hipMemcpyAsync(e->dom_recv, bands, (size_t)e->dom_npeer * (e->dom_cap + 1) * band_record_bytes(e->prec),
                           hipMemcpyHostToDevice, e->stream));
     enqueue_band_unpack(e);
     HIPCHK(hipGetLastError());
@@ -2831,8 +2838,10 @@ int gcs_engine_domain_receive(gcs_engine* dst, int32_t dst_slot, gcs_engine* src
     HIPCHK(hipEventRecord(ev, src->stream));
     HIPCHK(hipStreamWaitEvent(dst->stream, ev, 0));
     const size_t rows = (size_t)dst->dom_cap + 1;
-    HIPCHK(hipMemcpyAsync(dst->dom_recv + (size_t)dst_slot * rows, src->dom_send + (size_t)src_slot * rows,
-                          rows * sizeof(float4), hipMemcpyDeviceToDevice, dst->stream));
+    if (dst->prec != src->prec) return fail(GCS_EINVAL, "band records differ in precision");
+    const size_t rb = band_record_bytes(dst->prec);
+    HIPCHK(hipMemcpyAsync(dst->dom_recv + (size_t)dst_slot * rows * rb, src->dom_send + (size_t)src_slot * rows * rb,
+                          rows * rb, hipMemcpyDeviceToDevice, dst->stream));
     HIPCHK(hipEventDestroy(ev));
     return GCS_OK;
 }

@@ -131,6 +131,17 @@ template <> struct RealVec<float> { using v4 = float4; using v2 = float2; };
 template <> struct RealVec<double> { using v4 = double4; using v2 = double2; };
 template <typename R> using real4 = typename RealVec<R>::v4;
 template <typename R> using real2 = typename RealVec<R>::v2;
+// the .w word of a slot-ordered position or a band record: an integer's bits (fp64: in the low word of the double)
+__device__ __forceinline__ int wbits(float w) { return __float_as_int(w); }
+__device__ __forceinline__ int wbits(double w) { return (int)__double_as_longlong(w); }
+template <typename R> __device__ __forceinline__ R wpack(int v)
+{
+    if constexpr (sizeof(R) == 4) return __int_as_float(v); else return __longlong_as_double((long long)(unsigned)v);
+}
+template <typename R> __device__ __forceinline__ real4<R> mk4(R x, R y, R z, R w)
+{
+    if constexpr (sizeof(R) == 4) return make_float4(x, y, z, w); else return make_double4(x, y, z, w);
+}
 
 template <typename R>
 struct TetherT {  // kinetochore fiber spring to a fixed pole
@@ -263,7 +274,7 @@ struct ForceArgs {
     // step's unpack), an owned shared particle's new position into its row of dom_red's shared block (k_ldom_tail
     // zeroes the block for the next step), and a bond of an owned particle reaching beyond the halo raises
     // dom_flags bit 0 (the local-terms wave)
-    float4* dom_bands;
+    void* dom_bands;  // real4<R> records
     int dom_bstride, dom_cap, dom_npeer;
     const DomBox* dom_regions;
     const int* dom_shared;  // [N] k + 1 for the k-th shared particle, 0 otherwise
@@ -435,7 +446,7 @@ void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2, double d2_64);
 // the decomposed list step's tail from the allreduced buffer glob (one workgroup), then the shared particles'
 // positions into both buffers (by index and by slot) and the send bands' header rows zeroed
 void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const double* glob, int flags,
-                             const int* shared, int nshared, float4* bands, int npeer, int band_stride);
+                             const int* shared, int nshared, void* bands, int npeer, int band_stride);
 int list_step_grid(int n);
 bool list_u16(int n);  // list entries are 16-bit slot indices (N <= 65536)
 void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceArgs& a, bool fused);
@@ -482,6 +493,8 @@ void launch_quantize(hipStream_t s, const double4* pos, float* out, int n, int b
 // domain.hip: spatial decomposition (band pack / unpack) + the local partial reduction of a decomposed step
 constexpr int kMaxPeers = 32;
 constexpr int kMaxDomains = 256;
+// band records: {x, y, z, index bits} in the engine's precision (16 B fp32, 32 B fp64)
+inline size_t band_record_bytes(int prec) { return prec == 64 ? 32 : 16; }
 // allreduce buffer: [0, kDomainRed) the local reduction (reactions in[3] out[3]; tile step: max drift, neighbours;
 // list step: neighbours, owned particles, fallback particles), then 3 doubles per shared particle, then (list step)
 // one slot per domain for the largest displacement from the build
@@ -493,15 +506,15 @@ constexpr int kDomFlagLost = 4;      // a particle owned by no domain's lists (m
 constexpr int kDomFlagMotion = 8;    // cutoff + largest displacement since the build exceeds the halo
 // pack: slots != 0 packs from the list slots (the decomposed list step), else by particle index
 void launch_domain_pack(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const DomBox* regions, int npeer,
-                        float4* out, int* counts, int cap, int* flags, const int* shared, int ostride = 0,
+                        void* out, int* counts, int cap, int* flags, const int* shared = nullptr, int ostride = 0,
                         int cstride = 1, int slots = 0);
-void launch_band_headers_zero(hipStream_t s, float4* bands, int npeer, int stride);
+void launch_band_headers_zero(hipStream_t s, void* bands, int npeer, int stride, int prec);
 void launch_domain_shared_out(hipStream_t s, const DevCtx* ctx, const ForceArgs& a, const int* idx, int nshared,
                               double* buf);
 void launch_domain_shared_in(hipStream_t s, const ForceArgs& a, const int* idx, int nshared, const double* buf);
 // slots != 0 also refreshes the records' list slots (both psort buffers)
-void launch_domain_unpack(hipStream_t s, const ForceArgs& a, const float4* in, const int* counts, int nbuf, int cap,
-                          int istride = 0, int cstride = 1, int slots = 0, float4* send = nullptr, int nsend = 0,
+void launch_domain_unpack(hipStream_t s, const ForceArgs& a, const void* in, const int* counts, int nbuf, int cap,
+                          int istride = 0, int cstride = 1, int slots = 0, void* send = nullptr, int nsend = 0,
                           int sstride = 0);
 void launch_tail_reduce(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int fblocks, double* out);
 

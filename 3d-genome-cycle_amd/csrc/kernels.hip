@@ -168,16 +168,6 @@ template <typename R> __device__ __forceinline__ R wave_sum_r(R v)
 }
 // the integer a slot-ordered position record carries in .w (particle | class << 24): the float's bits in fp32, the
 // low word of the double's bits in fp64
-__device__ __forceinline__ int wbits(float w) { return __float_as_int(w); }
-__device__ __forceinline__ int wbits(double w) { return (int)__double_as_longlong(w); }
-template <typename R> __device__ __forceinline__ R wpack(int v)
-{
-    if constexpr (sizeof(R) == 4) return __int_as_float(v); else return __longlong_as_double((long long)(unsigned)v);
-}
-template <typename R> __device__ __forceinline__ real4<R> mk4(R x, R y, R z, R w)
-{
-    if constexpr (sizeof(R) == 4) return make_float4(x, y, z, w); else return make_double4(x, y, z, w);
-}
 
 
 __device__ inline int wave_max_int(int v)
@@ -2989,7 +2979,10 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 #define GCS_LIST_WAVES_PER_EU64 4  // the fp64 step: every position / force register is a pair -> <= 128 VGPRs
 #endif
 #ifndef GCS_LIST_UNROLL64
-#define GCS_LIST_UNROLL64 8  // fp64 step: list entries per batch of the pair loop
+// fp64 step: list entries per batch of the pair loop.  Same-box A/B (tools/gpu_r04b.sh, profiles/r04_variants.txt):
+// 4 entries 3.92e9 (single trajectory 1.95e9, k_lstep 29.0 us) vs 8 entries 3.84e9 (1.80e9, 31.2 us); at 5 waves
+// per SIMD either spills (3.74e9 / 1.15e9)
+#define GCS_LIST_UNROLL64 4
 #endif
 // One list step: ONE tile of 64 consecutive slots per workgroup (the launch has one workgroup per tile), W waves.
 // Phases, with nothing but LDS carried from one to the next (every wave's registers are free for the next phase):
@@ -3291,8 +3284,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
                         r[2] = (double)nzp;
                     }
                 }
+                R4* const bands = reinterpret_cast<R4*>(a.dom_bands);
                 int* const counts = reinterpret_cast<int*>(a.dom_bands);
-                const size_t cstride = (size_t)4 * a.dom_bstride;
+                const size_t cstride = (size_t)a.dom_bstride * (sizeof(R4) / sizeof(int));  // (ints per band)
                 // every peer's ballot first, then one counter atomic per peer, all in flight together (lane p)
                 int mine = 0;
                 for (int p = 0; p < a.dom_npeer; ++p) {
@@ -3311,7 +3305,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
                     if (send) {
                         const int o = at + __popcll(m & ((1ull << lane) - 1ull));
                         if (o < a.dom_cap)
-                            a.dom_bands[(size_t)p * a.dom_bstride + 1 + o] = make_float4(nx, ny, nz, __int_as_float(i));
+                            bands[(size_t)p * a.dom_bstride + 1 + o] = mk4<R>(nxp, nyp, nzp, wpack<R>(i));
                         else
                             atomicOr(a.dom_flags, 2);
                     }
@@ -3516,9 +3510,10 @@ __global__ __launch_bounds__(kLUpdateBlock) void k_lupdate(DevCtx* __restrict__ 
 // particle owned by some domain's lists (kDomFlagLost), cutoff + largest displacement within the halo
 // (kDomFlagMotion).  Then the shared particles' allreduced positions into both buffers, by index and by slot, and the
 // send bands' header rows zeroed for the pack.
+template <typename R>
 __global__ __launch_bounds__(64) void k_ldom_tail(DevCtx* __restrict__ ctx, ForceArgs a, const double* __restrict__ glob,
                                                   int flags, const int* __restrict__ shared, int nshared,
-                                                  float4* __restrict__ bands, int npeer, int bstride)
+                                                  real4<R>* __restrict__ bands, int npeer, int bstride)
 {
     const int tid = threadIdx.x;
     if (tid == 0) {
@@ -3544,18 +3539,17 @@ __global__ __launch_bounds__(64) void k_ldom_tail(DevCtx* __restrict__ ctx, Forc
     constexpr int kIdx = (1 << kListIndexBits) - 1;
     for (int k = tid; k < nshared; k += blockDim.x) {
         const int i = shared[k];
-        const float x = (float)glob[kDomainRed + 3 * k], y = (float)glob[kDomainRed + 3 * k + 1],
-                    z = (float)glob[kDomainRed + 3 * k + 2];
-        a.pos0[i] = make_float4(x, y, z, 0.f);
-        a.pos1[i] = make_float4(x, y, z, 0.f);
+        const R x = (R)glob[kDomainRed + 3 * k], y = (R)glob[kDomainRed + 3 * k + 1], z = (R)glob[kDomainRed + 3 * k + 2];
+        St<R>::pos(a, 0)[i] = mk4<R>(x, y, z, R(0));
+        St<R>::pos(a, 1)[i] = mk4<R>(x, y, z, R(0));
         const int sl = a.islot[i];
         if (sl >= 0) {
-            const float4 q = make_float4(x, y, z, __int_as_float((i & kIdx) | (a.ptype[i] << kListIndexBits)));
-            a.psort0[sl] = q;
-            a.psort1[sl] = q;
+            const real4<R> q = mk4<R>(x, y, z, wpack<R>((i & kIdx) | (a.ptype[i] << kListIndexBits)));
+            St<R>::psort(a, 0)[sl] = q;
+            St<R>::psort(a, 1)[sl] = q;
         }
     }
-    for (int p = tid; p < npeer; p += blockDim.x) bands[(size_t)p * bstride] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int p = tid; p < npeer; p += blockDim.x) bands[(size_t)p * bstride] = mk4<R>(R(0), R(0), R(0), R(0));
     // the shared block of this domain's reduction buffer for the next step's owners (the fused pack writes only
     // the owned particles' rows; the allreduce of this step has consumed it)
     if (a.dom_red)
@@ -3986,21 +3980,30 @@ void launch_list_relax(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force
         launch_list_relax_r<float>(s, ctx, a, force_flags, update_flags);
 }
 
+template <typename R>
+static void launch_list_step_dom(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)
+{
+    const dim3 g(list_step_grid(a.n));
+    if (list_u16(a.n)) {
+        if (a.list_waves == 2)
+            hipLaunchKernelGGL((k_lstep<unsigned short, 2, false, true, R>), g, dim3(128), 0, s, ctx, a, flags);
+        else
+            hipLaunchKernelGGL((k_lstep<unsigned short, 4, false, true, R>), g, dim3(256), 0, s, ctx, a, flags);
+    } else {
+        if (a.list_waves == 2)
+            hipLaunchKernelGGL((k_lstep<int, 2, false, true, R>), g, dim3(128), 0, s, ctx, a, flags);
+        else
+            hipLaunchKernelGGL((k_lstep<int, 4, false, true, R>), g, dim3(256), 0, s, ctx, a, flags);
+    }
+}
+
 void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)
 {
     if (flags & kLFlagDomain) {  // decomposed (no fused contacts: the engine flushes them before a decomposed step)
-        const dim3 g(list_step_grid(a.n));
-        if (list_u16(a.n)) {
-            if (a.list_waves == 2)
-                hipLaunchKernelGGL((k_lstep<unsigned short, 2, false, true>), g, dim3(128), 0, s, ctx, a, flags);
-            else
-                hipLaunchKernelGGL((k_lstep<unsigned short, 4, false, true>), g, dim3(256), 0, s, ctx, a, flags);
-        } else {
-            if (a.list_waves == 2)
-                hipLaunchKernelGGL((k_lstep<int, 2, false, true>), g, dim3(128), 0, s, ctx, a, flags);
-            else
-                hipLaunchKernelGGL((k_lstep<int, 4, false, true>), g, dim3(256), 0, s, ctx, a, flags);
-        }
+        if (a.prec == 64)
+            launch_list_step_dom<double>(s, ctx, a, flags);
+        else
+            launch_list_step_dom<float>(s, ctx, a, flags);
         return;
     }
     if (a.prec == 64) {
@@ -4017,10 +4020,14 @@ void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)
 }
 
 void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const double* glob, int flags,
-                             const int* shared, int nshared, float4* bands, int npeer, int band_stride)
+                             const int* shared, int nshared, void* bands, int npeer, int band_stride)
 {
-    hipLaunchKernelGGL(k_ldom_tail, dim3(1), dim3(64), 0, s, ctx, a, glob, flags, shared, nshared, bands, npeer,
-                       band_stride);
+    if (a.prec == 64)
+        hipLaunchKernelGGL(k_ldom_tail<double>, dim3(1), dim3(64), 0, s, ctx, a, glob, flags, shared, nshared,
+                           (double4*)bands, npeer, band_stride);
+    else
+        hipLaunchKernelGGL(k_ldom_tail<float>, dim3(1), dim3(64), 0, s, ctx, a, glob, flags, shared, nshared,
+                           (float4*)bands, npeer, band_stride);
 }
 
 void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a)

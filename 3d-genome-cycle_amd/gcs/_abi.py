@@ -187,8 +187,8 @@ PROTOTYPES = {
     "gcs_engine_domain_run": (C.c_int, [C.c_void_p, C.POINTER(BDConfig), _i64, _i64]),
     "gcs_engine_domain_step_host": (C.c_int, [C.c_void_p, C.POINTER(BDConfig), _i64, _pd, _i32]),
     "gcs_engine_domain_finish_host": (C.c_int, [C.c_void_p, _pd, _i32]),
-    "gcs_engine_domain_pack_host": (C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
-    "gcs_engine_domain_unpack_host": (C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
+    "gcs_engine_domain_pack_host": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gcs_engine_domain_unpack_host": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gcs_engine_domain_receive": (C.c_int, [C.c_void_p, _i32, C.c_void_p, _i32]),
     "gcs_engine_domain_unpack_received": (C.c_int, [C.c_void_p]),
     "gcs_engine_domain_flags": (C.c_int, [C.c_void_p, C.POINTER(_i32)]),

@@ -204,7 +204,8 @@ class EngineDomain(_Domain):
         # local reduction (10) + shared particles' positions + one displacement slot per domain (csrc/domain.hip)
         self.red = np.zeros(self.nred)
         self.glob = np.zeros(self.nred)  # its sum over domains
-        self.out = np.zeros((npeer, self.cap + 1, 4), dtype=np.float32)  # host staging: [peer][header + cap][4]
+        # host staging: [peer][header + cap][4] records in the engine's precision (csrc/domain.hip)
+        self.out = np.zeros((npeer, self.cap + 1, 4), dtype=np.float64 if engine.precision == 64 else np.float32)
         self.inb = np.zeros_like(self.out)
 
     def step(self, st, bd):

@@ -364,10 +364,10 @@ class Engine:
 
     def domain_pack_host(self, bands):
         A.check(self._lib.gcs_engine_domain_pack_host(
-            self._h, bands.ctypes.data_as(C.POINTER(C.c_float)) if bands is not None else None))
+            self._h, C.c_void_p(bands.ctypes.data) if bands is not None else None))
 
     def domain_unpack_host(self, bands):
-        A.check(self._lib.gcs_engine_domain_unpack_host(self._h, bands.ctypes.data_as(C.POINTER(C.c_float))))
+        A.check(self._lib.gcs_engine_domain_unpack_host(self._h, C.c_void_p(bands.ctypes.data)))
 
     def domain_receive(self, slot, src, src_slot):
         A.check(self._lib.gcs_engine_domain_receive(self._h, int(slot), src._h, int(src_slot)))

@@ -448,7 +448,7 @@ def decomp_main(args):
     cfg = bench_config(args.config)
     state = load_state() if args.config == "c2" else None
     design = design_maker(args.config)(master_seed=1)
-    ndom = world if world > 1 else args.decomp  # (the decomposition runs on fp32 engines)
+    ndom = world if world > 1 else args.decomp
     halo = D.domain_halo(cfg)
     x0 = state[0] if state is not None else design.positions
     boxes = D.plan_slabs(x0[:, 2], ndom) if args.slabs else D.plan_boxes(x0, ndom)
@@ -457,9 +457,9 @@ def decomp_main(args):
     window = window_start(args.config)
     cap = max(D.band_capacity(x0, boxes, halo, d) for d in range(ndom))  # one size: bands move between domains
     for d in mine:
-        e = make_engine(design, cfg, local, window, state, precision=32)
+        e = make_engine(design, cfg, local, window, state, precision=args.precision)
         if args.fused is not None:
-            e.set_option(A.OPT_FUSED_STEP, args.fused)  # e.g. 0: the decomposed tile step
+            e.set_option(A.OPT_FUSED_STEP, args.fused)  # e.g. 0: the decomposed tile step (fp32)
         doms.append(D.EngineDomain(e, d, boxes, halo, cap=cap, shared=D.shared_particles(design)))
     rccl = world > 1 or (args.rccl and ndom == 1)
     run = D.RcclRun(doms[0], dist) if rccl else D.DecomposedRun(doms, D.LocalTransport(doms))
@@ -480,7 +480,7 @@ def decomp_main(args):
     ref = None
     if world == 1:
         # the same trajectory undecomposed (one engine, same window, steps and shape): what the decomposition costs
-        e = make_engine(design, cfg, local, window, state, precision=32)
+        e = make_engine(design, cfg, local, window, state, precision=args.precision)
         if args.fused is not None:
             e.set_option(A.OPT_FUSED_STEP, args.fused)
         e.run(args.warmup, first_step=window, seed=seed, timestep=cfg.timestep)
@@ -495,7 +495,8 @@ def decomp_main(args):
             "metric": "bead-updates/sec (whole node), decomposed single trajectory",
             "value": n * args.steps / el_max, "unit": "bead-updates/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": el_max * 1e3 / args.steps, "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",  # fp32 engines
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64" if args.precision == 64 else "f32",
+            "data": "synthetic",
             "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, one trajectory in "
                                    f"{ndom} {'z-slab' if args.slabs else 'box'} domains "
                                    f"({'RCCL from the engine' if rccl else 'in-process, one GPU'})",
@@ -590,6 +591,12 @@ def replica_main(args):
     # (tools/make_bench_state.py); other configs start from their synthetic state at the window's context
     state = load_state() if args.config == "c2" and not args.stub_engine else None
     window = window_start(args.config)
+    # the fp32 leg first, before this process has created any other stream: HIP hands streams the hardware queues
+    # (4 per process here) in creation order, and measured after the headline's engines and the secondary legs its
+    # 4 trajectories shared queues (4.2e9 against 6.44e9 for the same workload as the headline of its own process)
+    f32 = None
+    if world == 1 and not args.stub_engine and args.precision == 64 and args.f32_leg:
+        f32 = f32_leg(args, maker, cfg, bd, local, state, window, R, K, G, list_waves, rank)
     designs, engines, seeds = [], [], []
     for k in range(R):
         rid = rank * R + k
@@ -764,10 +771,8 @@ def replica_main(args):
     for e in engines[1:]:
         e.close()  # (replica 0 stays for the line's context)
 
-    c5 = cycle = f32 = None
+    c5 = cycle = None
     if world == 1 and not args.stub_engine:
-        if args.precision == 64 and args.f32_leg:
-            f32 = f32_leg(args, maker, cfg, bd, local, state, window, R, K, G, list_waves, rank)
         if args.c5_steps > 0:
             c5 = c5_leg(local, seed, args.c5_steps, args.precision)
         if args.cycle_scale > 0:

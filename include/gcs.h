@@ -299,17 +299,20 @@ int gcs_engine_sample_positions(gcs_engine* e, float* xyz, int64_t n, int32_t fr
 /* Spatial domain decomposition (C5: one trajectory over several GPUs; SURVEY.md 8e, DESIGN.md "Multi-GPU").
  * Every engine holds all N particles by global index and integrates those that lie in its box
  * box = {lo[3], hi[3]} ([lo, hi) per axis; the domains' boxes tile space, outer faces at +-inf) at the start of a
- * step; it bins only the particles within `halo` of the box (its region).  `peer_boxes` [npeer][6] are the boxes of
+ * step; the particles within `halo` of the box (its region) are kept fresh by the owners' bands, and the list step
+ * bins those within list radius + one skin of the box (the tile step the whole region).  `peer_boxes` [npeer][6] are the boxes of
  * the domains whose regions overlap this one's: after each step the band of owned particles whose old or new
  * position lies in a peer's region (its box extended by `halo`) is packed for that peer.  Every engine derives the
  * regions with one fp32 formula, so membership is bit-identical on both sides.  `index` / `ndomains`: this domain's number and the domain
  * count (one slot each in the allreduce buffer).  halo <= 0 turns decomposition off.
  * The step shape follows the engine's: the list step (GCS_OPT_FUSED_STEP 3, the default) when the halo holds the
- * list radius (cutoff + skin at core scale 1), the tile step otherwise.
+ * list radius (cutoff + skin at core scale 1), the tile step (fp32 engines only) otherwise.  Band records are in the
+ * engine's precision: {x, y, z, index bits} as 4 floats (fp32 engine) or 4 doubles (fp64; the index in the low word
+ * of the fourth), the count of a band in the first int of its header row.
  * One step = gcs_engine_domain_step (force + update of the owned particles, local reduction into
  * dev_reaction[nred] on the device) -> the caller's allreduce(sum) of dev_reaction over all domains ->
  * gcs_engine_domain_finish(allreduced buffer: wall ODE + schedule) -> gcs_engine_domain_pack (band records
- * {x, y, z, index bits} into dev_out[npeer][cap][4], counts per peer; dev_flags[0] |= 1 a bond longer than the
+ * {x, y, z, index bits} into dev_out[npeer][cap][4] floats or doubles, counts per peer; dev_flags[0] |= 1 a bond longer than the
  * halo, |= 2 a band over cap, |= 4 a particle owned by no domain's lists, |= 8 cutoff + largest displacement since
  * the last list build beyond the halo) -> exchange -> gcs_engine_domain_unpack(received buffers).  All calls only
  * enqueue on the engine stream (gcs_engine_stream), so the caller's collectives can be ordered on it too.
@@ -324,8 +327,8 @@ int gcs_engine_set_domain_shared(gcs_engine* e, const int64_t* idx, int32_t coun
 int gcs_engine_stream(gcs_engine* e, void** stream);
 int gcs_engine_domain_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step, double* dev_reaction);
 int gcs_engine_domain_finish(gcs_engine* e, const double* dev_reaction);
-int gcs_engine_domain_pack(gcs_engine* e, float* dev_out, int32_t* dev_counts, int32_t cap, int32_t* dev_flags);
-int gcs_engine_domain_unpack(gcs_engine* e, const float* dev_in, const int32_t* dev_counts, int32_t nbuf,
+int gcs_engine_domain_pack(gcs_engine* e, void* dev_out, int32_t* dev_counts, int32_t cap, int32_t* dev_flags);
+int gcs_engine_domain_unpack(gcs_engine* e, const void* dev_in, const int32_t* dev_counts, int32_t nbuf,
                              int32_t cap);
 
 /* Engine-owned exchange of a decomposed run (C5): band buffers of `cap` records per peer (the band's first row
@@ -342,11 +345,12 @@ int gcs_engine_domain_rccl(gcs_engine* e, const uint8_t* id, int32_t nranks, int
  * of the band with each peer and the unpack; chunks of GCS_OPT_GRAPH_STEPS steps are captured in a hipGraph. */
 int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps);
 /* Host-staged transport (tests; any process layout, e.g. several processes on one device): a step's halves with
- * host buffers -- the local reduction out, the summed one in; the bands out ([npeer][cap + 1][4] floats) and in. */
+ * host buffers -- the local reduction out, the summed one in; the bands out ([npeer][cap + 1][4] floats, doubles for
+ * an fp64 engine) and in.  With these engine-owned buffers the list step packs its bands itself (k_lstep). */
 int gcs_engine_domain_step_host(gcs_engine* e, const gcs_bd_config* cfg, int64_t step, double* red, int32_t nred);
 int gcs_engine_domain_finish_host(gcs_engine* e, const double* glob, int32_t nred);
-int gcs_engine_domain_pack_host(gcs_engine* e, float* bands /* NULL: pack on the device only */);
-int gcs_engine_domain_unpack_host(gcs_engine* e, const float* bands);
+int gcs_engine_domain_pack_host(gcs_engine* e, void* bands /* NULL: pack on the device only */);
+int gcs_engine_domain_unpack_host(gcs_engine* e, const void* bands);
 /* In-process transport (several domains on one device): copy src's band src_slot into dst's received band
  * dst_slot (ordered after src's stream), then unpack everything received. */
 int gcs_engine_domain_receive(gcs_engine* dst, int32_t dst_slot, gcs_engine* src, int32_t src_slot);

@@ -11,9 +11,11 @@ out=$root/gpurun_out/prof_$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
 bench=(python3 "$root/bench.py" --steps "$steps" --warmup 50 --cpu-budget 0 --profile-steps 10 --no-start-window --replicas-per-gpu "${REPLICAS:-1}" --c5-steps 0 --cycle-scale 0 --precision "${PREC:-64}" --no-f32-leg)
-# the engines' density probe (GCS_OPT_DENSE_NEIGHBORS) makes rocprofv3 --kernel-trace segfault in the first graph
-# launch (engine.hip probe_density); the C2 window is list-step territory either way (25 neighbours)
-export GCS_BENCH_DENSE=0
+# rocprofv3 --kernel-trace segfaults inside hipGraphLaunch when HIP dispatches a graph's pre-captured AQL packets
+# (the default graph packet capture): the fault is in librocprofiler-sdk's queue-write interceptor, which reads a
+# packet header one page past the array it is handed (profiles/r04_rocprof_crash.txt).  Profiling runs
+# turn the capture off (every graph node dispatched on its own); GCS_PROFILE_PACKET_CAPTURE=1 keeps it.
+export DEBUG_CLR_GRAPH_PACKET_CAPTURE=${GCS_PROFILE_PACKET_CAPTURE:-0}
 # (GCS_MAPS_OUT: the process's memory map before the first warm-up step, to symbolise a crash trace's PCs)
 GCS_MAPS_OUT=$out/maps.txt timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- "${bench[@]}" > "$out/trace.log" 2>&1 || exit $?
 i=0
