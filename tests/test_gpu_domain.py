@@ -5,10 +5,11 @@ host-staged over gloo: RCCL refuses two ranks on one GPU), and the engine-issued
 engine, each other and the fp64 oracle.  Both decomposed step shapes: the list step (k_lstep<..., DOM>, the default)
 and the tile step (GCS_OPT_FUSED_STEP 0); both geometries: z-slabs and recursive-bisection boxes (2 x 2 x 2 at 8).
 
-The decomposition runs on fp32 engines (GCS_PRECISION_F32; the fp64 engine rejects set_domain).
-Tolerances: positions |dx| <= 2e-5 after 30 steps (fp32; the domains' cell lists order the pair sums differently
-from the single engine's), wall semiaxes relative 1e-7; the protocol flags (bond beyond the halo, band over
-capacity, lost particle, displacement beyond the halo) must stay clear."""
+Both precisions: the fp64 engine (the default) decomposes on its list step; the tile-step cases are fp32 only.
+Tolerances (tests/tolerances.py, per precision): positions vs the single engine and the fp64 oracle 1e-9 (fp64) /
+2e-5 (fp32) after 30 steps (the domains' cell lists order the pair sums differently from the single engine's), wall
+semiaxes relative 1e-12 / 1e-7; the protocol flags (bond beyond the halo, band over capacity, lost particle,
+displacement beyond the halo) must stay clear."""
 import json
 import os
 import socket
@@ -22,6 +23,7 @@ from gcs import _abi as A
 from gcs import domain, interphase, synthetic
 from gcs.config import InterphaseConfig
 from gcs.engine import Engine
+from tolerances import WALL_REL, X
 
 import oracle
 
@@ -31,8 +33,8 @@ STEPS = 30
 SEED = 99
 
 
-def _engine(design, cfg, fused=None):
-    e, _ = interphase.build_interphase(Engine, design, cfg, device=0, precision=32)
+def _engine(design, cfg, fused=None, prec=32):
+    e, _ = interphase.build_interphase(Engine, design, cfg, device=0, precision=prec)
     e.set_schedule(**interphase.interphase_schedule(cfg))
     if fused is not None:
         e.set_option(A.OPT_FUSED_STEP, fused)
@@ -44,56 +46,57 @@ def _plan(kind, design, ndom):
     return domain.plan_slabs(x[:, 2], ndom) if kind == "slabs" else domain.plan_boxes(x, ndom)
 
 
-def _decomposed(design, cfg, ndom, steps, cap=None, halo=None, kind="slabs", fused=None):
+def _decomposed(design, cfg, ndom, steps, cap=None, halo=None, kind="slabs", fused=None, prec=32):
     halo = halo or domain.domain_halo(cfg)
     boxes = _plan(kind, design, ndom)
     sh = domain.shared_particles(design)
-    doms = [domain.EngineDomain(_engine(design, cfg, fused), d, boxes, halo, cap=cap, shared=sh)
+    doms = [domain.EngineDomain(_engine(design, cfg, fused, prec), d, boxes, halo, cap=cap, shared=sh)
             for d in range(ndom)]
     run = domain.DecomposedRun(doms, domain.LocalTransport(doms))
     run.run(steps, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     return run, doms, boxes
 
 
-@pytest.mark.parametrize("kind,ndom,halo,fused", [("slabs", 2, None, None), ("slabs", 4, None, None),
-                                                  ("slabs", 3, 0.5, None), ("boxes", 4, None, None),
-                                                  ("boxes", 8, None, None), ("slabs", 2, None, 0),
-                                                  ("boxes", 4, None, 0)])
-def test_decomposed_engines_match_single_engine_c1(c1_design, kind, ndom, halo, fused):
+@pytest.mark.parametrize("kind,ndom,halo,fused,prec", [
+    ("slabs", 2, None, None, 32), ("slabs", 4, None, None, 32), ("slabs", 3, 0.5, None, 32),
+    ("boxes", 4, None, None, 32), ("boxes", 8, None, None, 32), ("slabs", 2, None, 0, 32), ("boxes", 4, None, 0, 32),
+    ("slabs", 2, None, None, 64), ("slabs", 3, 0.5, None, 64), ("boxes", 4, None, None, 64),
+    ("boxes", 8, None, None, 64)])
+def test_decomposed_engines_match_single_engine_c1(c1_design, kind, ndom, halo, fused, prec):
     cfg = InterphaseConfig()
-    single = _engine(c1_design, cfg)
+    single = _engine(c1_design, cfg, prec=prec)
     single.run(STEPS, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     x1, c1 = single.get_positions(), single.get_context()
-    run, doms, boxes = _decomposed(c1_design, cfg, ndom, STEPS, halo=halo, kind=kind, fused=fused)
+    run, doms, boxes = _decomposed(c1_design, cfg, ndom, STEPS, halo=halo, kind=kind, fused=fused, prec=prec)
     run.check()
     # the list step ran decomposed (its builds), or the tile step (no lists)
     st = doms[0].e.list_stats()
     builds = st["builds"]
     assert (builds >= 1 + (STEPS - 1) // st["rebuild_every"]) if fused is None else builds == 0, st
     x = domain.gather_positions(run, c1_design.n)
-    assert np.abs(x - x1).max() <= 2e-5
+    assert np.abs(x - x1).max() <= X[prec]
     for d in doms:
         c = d.context()
         assert c["step"] == c1["step"]
-        assert np.allclose(c["wall_semiaxes"], c1["wall_semiaxes"], rtol=1e-7, atol=0)
-    # and against the fp64 oracle's undecomposed run
-    o, _ = interphase.build_interphase(oracle.OracleSystem, c1_design, cfg)
+        assert np.allclose(c["wall_semiaxes"], c1["wall_semiaxes"], rtol=WALL_REL[prec], atol=0)
+    # and against the fp64 oracle's undecomposed run (the oracle's predicate in the engine's precision)
+    o, _ = interphase.build_interphase(oracle.OracleSystem, c1_design, cfg, precision=prec)
     o.set_schedule(**interphase.interphase_schedule(cfg))
     o.run(STEPS, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
-    assert np.abs(x - o.get_positions()).max() <= 2e-5
+    assert np.abs(x - o.get_positions()).max() <= X[prec]
 
 
-@pytest.mark.parametrize("kind,ndom", [("slabs", 4), ("boxes", 8)])
-def test_decomposed_engines_c2(kind, ndom):
+@pytest.mark.parametrize("kind,ndom,prec", [("slabs", 4, 32), ("boxes", 8, 32), ("boxes", 8, 64)])
+def test_decomposed_engines_c2(kind, ndom, prec):
     cfg = InterphaseConfig()
     design = synthetic.make_c2()
-    single = _engine(design, cfg)
+    single = _engine(design, cfg, prec=prec)
     single.run(20, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     x1 = single.get_positions()
-    run, doms, _ = _decomposed(design, cfg, ndom, 20, kind=kind)
+    run, doms, _ = _decomposed(design, cfg, ndom, 20, kind=kind, prec=prec)
     run.check()
     x = domain.gather_positions(run, design.n)
-    assert np.abs(x - x1).max() <= 2e-5
+    assert np.abs(x - x1).max() <= X[prec]
 
 
 def test_motion_beyond_halo_is_reported(c1_design):
@@ -152,8 +155,8 @@ def test_decomposed_c5_scaled_two_domains():
     assert e_single <= 2e-5 and e_dec <= 2e-5, (e_dec, e_single)
 
 
-@pytest.mark.parametrize("fused", [None, 0])
-def test_rccl_run_one_rank_equals_host_driven(c1_design, fused):
+@pytest.mark.parametrize("fused,prec", [(None, 32), (0, 32), (None, 64)])
+def test_rccl_run_one_rank_equals_host_driven(c1_design, fused, prec):
     """gcs_engine_domain_run with one rank (RCCL allreduce on the engine stream; 70 steps = a priming step, two
     captured 32-step graphs (list step: whole rebuild periods, recaptured for the second call's phase) and eager
     steps) equals the host-driven step sequence of the same domain bit for bit"""
@@ -162,10 +165,10 @@ def test_rccl_run_one_rank_equals_host_driven(c1_design, fused):
     halo = domain.domain_halo(cfg)
     slabs = domain.plan_slabs(c1_design.positions[:, 2], 1)
     sh = domain.shared_particles(c1_design)
-    ref = domain.EngineDomain(_engine(c1_design, cfg, fused), 0, slabs, halo, shared=sh)
+    ref = domain.EngineDomain(_engine(c1_design, cfg, fused, prec), 0, slabs, halo, shared=sh)
     run = domain.DecomposedRun([ref], domain.LocalTransport([ref]))
     run.run(70, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
-    d = domain.EngineDomain(_engine(c1_design, cfg, fused), 0, slabs, halo, shared=sh)
+    d = domain.EngineDomain(_engine(c1_design, cfg, fused, prec), 0, slabs, halo, shared=sh)
     d.e.domain_rccl(rccl_unique_id(), 1, 0, [])
     d.e.domain_run(30, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     d.e.domain_run(40, first_step=30, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
@@ -182,7 +185,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, out_dir, config):
+def _rank_main(rank, world, port, out_dir, config, prec=32):
     """one domain per process, all on device 0, host-staged over gloo (C1: z-slabs; C2: boxes)"""
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
                        "MASTER_PORT": str(port)})
@@ -194,7 +197,7 @@ def _rank_main(rank, world, port, out_dir, config):
     from gcs.engine import Engine as E
     dist.init_process_group("gloo", rank=rank, world_size=world)
     design, cfg = (S.make_c1() if config == "c1" else S.make_c2()), IC()
-    e, _ = I.build_interphase(E, design, cfg, device=0, precision=32)
+    e, _ = I.build_interphase(E, design, cfg, device=0, precision=prec)
     e.set_schedule(**I.interphase_schedule(cfg))
     boxes = (D.plan_slabs(design.positions[:, 2], world) if config == "c1"
              else D.plan_boxes(design.positions, world))
@@ -213,8 +216,9 @@ def _steps(config):
     return STEPS if config == "c1" else 20
 
 
-@pytest.mark.parametrize("config,world", [("c1", 2), ("c2", 4), ("c2", 8)])
-def test_engine_domains_processes_host_staged(tmp_path, config, world):
+@pytest.mark.parametrize("config,world,prec", [("c1", 2, 32), ("c2", 4, 32), ("c2", 8, 32), ("c1", 2, 64),
+                                               ("c2", 4, 64)])
+def test_engine_domains_processes_host_staged(tmp_path, config, world, prec):
     """`world` processes, one engine domain each (device 0), reaction allreduce and bands over gloo: within 2e-5 of
     the single engine; with two domains also bit for bit the in-process run (the same kernels; a two-term sum is
     order-free; gloo's 4-term sum may associate differently from the host's)"""
@@ -223,7 +227,7 @@ def test_engine_domains_processes_host_staged(tmp_path, config, world):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, str(tmp_path), config)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, str(tmp_path), config, prec)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -235,11 +239,11 @@ def test_engine_domains_processes_host_staged(tmp_path, config, world):
     design = synthetic.make_c1() if config == "c1" else synthetic.make_c2()
     steps = _steps(config)
     if world == 2:
-        run, doms, _ = _decomposed(design, cfg, world, steps)
+        run, doms, _ = _decomposed(design, cfg, world, steps, prec=prec)
         xl = domain.gather_positions(run, design.n)
         assert np.array_equal(x, xl)
         assert ctx["wall_semiaxes"] == doms[0].context()["wall_semiaxes"]
-    single = _engine(design, cfg)
+    single = _engine(design, cfg, prec=prec)
     single.run(steps, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
-    assert np.abs(x - single.get_positions()).max() <= 2e-5
-    assert np.allclose(ctx["wall_semiaxes"], single.get_context()["wall_semiaxes"], rtol=1e-7, atol=0)
+    assert np.abs(x - single.get_positions()).max() <= X[prec]
+    assert np.allclose(ctx["wall_semiaxes"], single.get_context()["wall_semiaxes"], rtol=WALL_REL[prec], atol=0)
