@@ -689,7 +689,8 @@ def replica_main(args):
         single_rate = n * k1 * reps / el1
 
     # passes of K steps so the timed window lasts >= min_window_s (estimated from the warm-up, agreed by all ranks)
-    passes = max(1, math.ceil(args.min_window_s / max(per_pass, 1e-9)))
+    # (x 1.25: the warm-up's pass estimate runs a little slow, so the window still lasts min_window_s)
+    passes = max(1, math.ceil(1.25 * args.min_window_s / max(per_pass, 1e-9)))
     passes = int(max_over_ranks(dist, float(passes)))
     barrier(dist)
     sync_all()
