@@ -2832,17 +2832,22 @@ int gcs_engine_domain_receive(gcs_engine* dst, int32_t dst_slot, gcs_engine* src
     if (dst_slot < 0 || dst_slot >= dst->dom_npeer || src_slot < 0 || src_slot >= src->dom_npeer)
         return fail(GCS_EINVAL, "bad band slot");
     if (dst->device != src->device) return fail(GCS_EINVAL, "in-process bands move within one device");
+    if (dst->prec != src->prec) return fail(GCS_EINVAL, "band records differ in precision");
     HIPCHK(hipSetDevice(dst->device));
-    hipEvent_t ev;
+    hipEvent_t ev, done;
     HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
     HIPCHK(hipEventRecord(ev, src->stream));
     HIPCHK(hipStreamWaitEvent(dst->stream, ev, 0));
     const size_t rows = (size_t)dst->dom_cap + 1;
-    if (dst->prec != src->prec) return fail(GCS_EINVAL, "band records differ in precision");
     const size_t rb = band_record_bytes(dst->prec);
     HIPCHK(hipMemcpyAsync(dst->dom_recv + (size_t)dst_slot * rows * rb, src->dom_send + (size_t)src_slot * rows * rb,
                           rows * rb, hipMemcpyDeviceToDevice, dst->stream));
+    // and src's stream waits for the copy: its unpack zeroes the band's header row for the next step's fused pack
+    HIPCHK(hipEventRecord(done, dst->stream));
+    HIPCHK(hipStreamWaitEvent(src->stream, done, 0));
     HIPCHK(hipEventDestroy(ev));
+    HIPCHK(hipEventDestroy(done));
     return GCS_OK;
 }
 
