@@ -2626,6 +2626,9 @@ __global__ __launch_bounds__(256) void k_tail(DevCtx* ctx, ForceArgs a, int fblo
 #ifndef GCS_LIST_WAVES_PER_EU
 #define GCS_LIST_WAVES_PER_EU 5  // k_lstep occupancy target (VGPR cap 512 / waves): 5 -> <= 96, no spills
 #endif
+#ifndef GCS_LIST_BOND_BATCH64
+#define GCS_LIST_BOND_BATCH64 4  // the fp64 step's bond batch (each entry holds a 32-B parameter and position record)
+#endif
 #ifndef GCS_LIST_BOND_BATCH
 #define GCS_LIST_BOND_BATCH 4  // bond CSR entries whose loads are issued together in the particle-local terms
 #endif
@@ -3081,7 +3084,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         const int2 erow = a.sbrow[sl];
         R lfx = 0, lfy = 0, lfz = 0, en[kEnergyKinds];
         R rin[3] = {0, 0, 0}, rout[3] = {0, 0, 0};
-        local_terms<kModeStep, GCS_LIST_BOND_BATCH, R>(ctx, a, i, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout,
+        local_terms<kModeStep, sizeof(R) == 8 ? GCS_LIST_BOND_BATCH64 : GCS_LIST_BOND_BATCH, R>(ctx, a, i, pi.x, pi.y,
+                                                                                             pi.z, km, lfx, lfy, lfz, en, rin, rout,
                                                        erow);
         if constexpr (DOM) {
             // the fused pack's bond check (k_domain_pack's): a bond of an owned particle longer than the halo (its

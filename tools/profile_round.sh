@@ -2,7 +2,7 @@
 # tools/profile.sh for R = 1 and R = 4, summarised on the box (raw rocprofv3 output exceeds what gpurun copies back)
 set -u
 tag=${1:?tag}
-for R in 1 4; do
+for R in ${PROFILE_REPLICAS:-1 4}; do
   t=$tag; [ $R -gt 1 ] && t=${tag}_r$R
   REPLICAS=$R bash tools/profile.sh $t || { d=gpurun_out/prof_$t; cp $d/trace.log gpurun_out/${t}_trace.log; cp $d/maps.txt gpurun_out/${t}_maps.txt; rm -rf $d/trace $d/pmc*; exit 1; }
   d=gpurun_out/prof_$t
