@@ -265,7 +265,7 @@ struct gcs_engine {
     bool list_ok = false;       // the system admits the list step (a pair field, <= 256 classes, N < 2^24)
     int list_cap = 1024;        // GCS_OPT_LIST_CAP: list entries per particle (split over the tile's waves)
     size_t list_alloc = 0;      // allocated entries
-    int list_skin_pm = 500;     // GCS_OPT_LIST_SKIN: skin in 1/1000 of the pair cutoff
+    int list_skin_pm = 0;       // GCS_OPT_LIST_SKIN: skin in 1/1000 of the pair cutoff (0: the precision's default)
     int list_every_opt = 0;     // GCS_OPT_LIST_EVERY: rebuild period in steps (0: from the noise amplitude)
     int list_every = 1;         // the period of the current run
     int list_waves = 4;         // GCS_OPT_LIST_WAVES: waves per tile (2: more tiles resident, for replica runs)
@@ -800,7 +800,14 @@ bool list_path(const gcs_engine* e, bool spacestep)
 bool fused_path(const gcs_engine* e, bool spacestep) { return spacestep ? list_path(e, true) : eff_fused(e) != 0; }
 bool rebuild_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) == 2 && !spacestep; }
 
-float list_skin(const gcs_engine* e) { return 1e-3f * (float)e->list_skin_pm * e->fa.pf.pair_dist; }
+// the list skin: the option, or the precision's default.  The fp64 step gathers 32-B partners, so shorter lists pay
+// for more frequent rebuilds sooner than at fp32 (4-replica bench sweeps: fp32 profiles/r03_skin_sweep.txt, 500 per
+// mille / 16 steps best; fp64 profiles/r04_skin_sweep_f64*.txt)
+float list_skin(const gcs_engine* e)
+{
+    const int pm = e->list_skin_pm > 0 ? e->list_skin_pm : (e->prec == 64 ? kListSkinPm64 : kListSkinPm32);
+    return 1e-3f * (float)pm * e->fa.pf.pair_dist;
+}
 
 // the list build's chunk deal (kernels.hip deal_nth): the option, or the default for the waves per tile
 unsigned long long list_deal(const gcs_engine* e)
@@ -3090,7 +3097,8 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         return GCS_OK;
     }
     if (option == GCS_OPT_LIST_SKIN) {
-        if (value < 1 || value > 4000) return fail(GCS_EINVAL, "list skin must be in [1, 4000] per mille of the cutoff");
+        if (value < 0 || value > 4000)
+            return fail(GCS_EINVAL, "list skin must be in [1, 4000] per mille of the cutoff (0: the default)");
         e->list_skin_pm = (int)value;
         drop_graph(e);
         return GCS_OK;

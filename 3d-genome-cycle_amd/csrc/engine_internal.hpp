@@ -375,6 +375,8 @@ __host__ __device__ inline unsigned long long list_acc_identity(int k)
 // (tools/deal_sweep.sh, profiles/r03c_deal_sweep.txt): 4 replicas 5.85-6.21 -> 6.24-6.26e9, single 2.52-2.53 -> 2.60-2.61e9
 constexpr unsigned long long kListDeal2 = (3ull << 60) | 0x100ull;
 constexpr unsigned long long kListDeal4 = (7ull << 60) | 0x3210210ull;
+constexpr int kListSkinPm32 = 500;  // default list skin, 1/1000 of the pair cutoff (GCS_OPT_LIST_SKIN 0)
+constexpr int kListSkinPm64 = 350;
 constexpr int kMaxListWaves = 4;  // waves per tile of the list kernels (each owns one list segment): 2 or 4
 constexpr int kMaxTypes = 256;          // pair-factor classes (8 bits of a list entry)
 constexpr int kListIndexBits = 24;      // particle index bits of a list entry

@@ -109,7 +109,7 @@ def plan_boxes(x, ndom: int):
 BOND_SIGMAS = 7.5  # a chain bond stretched beyond this many thermal widths: ~1e-11 per bond-step
 
 
-LIST_SKIN = 0.5  # the list step's skin / pair cutoff (GCS_OPT_LIST_SKIN default 500 per mille)
+LIST_SKIN = 0.5  # the list step's largest default skin / pair cutoff (GCS_OPT_LIST_SKIN: 500 per mille fp32, 350 fp64)
 
 
 def domain_halo(cfg: InterphaseConfig, margin: float = 0.05, list_skin: float = LIST_SKIN) -> float:
