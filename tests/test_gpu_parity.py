@@ -147,7 +147,8 @@ def test_relaxation_spacestep(c1_design, interphase_cfg, prec, fused):
     assert np.abs(e.get_positions() - o.get_positions()).max() <= X[prec]
     assert e.get_context()["last_timestep"] == pytest.approx(o.get_context()["last_timestep"],
                                                              rel={64: 1e-10, 32: 1e-4}[prec])
-    assert e.list_stats()["builds"] == (1 if fused == 3 else 0)
+    builds = e.list_stats()["builds"]
+    assert (builds >= 1) if fused == 3 else (builds == 0)  # (the rebuild period depends on the precision's skin)
 
 
 @precisions
