@@ -416,3 +416,18 @@ def test_list_relaxation_then_fixed_timestep(c1_design, prec):
         s.run(20, first_step=20, temperature=cfg.temperature, timestep=cfg.timestep, seed=9)
     assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[prec]
     assert e.get_context()["last_timestep"] == o.get_context()["last_timestep"] == cfg.timestep
+
+
+@pytest.mark.parametrize("prec,pm", [(64, 350), (32, 500)])
+def test_default_skin_per_precision(c1_design, prec, pm):
+    """GCS_OPT_LIST_SKIN 0 (the default): 350 per mille of the cutoff at fp64 (its 32-B gathers favour shorter lists),
+    500 at fp32; an explicit value applies to both"""
+    cfg = InterphaseConfig()
+    e = _list_engine(c1_design, cfg, prec)
+    e.set_schedule(**interphase.interphase_schedule(cfg))
+    e.set_context(LATE)
+    e.run(2, first_step=LATE["step"], seed=1)
+    assert e.list_stats()["skin"] == pytest.approx(pm * 1e-3 * cfg.a_core_diameter, rel=1e-6)
+    e.set_option(A.OPT_LIST_SKIN, 420)
+    e.run(2, first_step=LATE["step"] + 2, seed=1)
+    assert e.list_stats()["skin"] == pytest.approx(0.42 * cfg.a_core_diameter, rel=1e-6)
