@@ -24,7 +24,8 @@ cfg = bench.bench_config(name)
 start = int(opts.pop("start", 0)) or name != "c2"  # 1: the production start window (step 0, core_scale 0.5)
 st = None if start else bench.load_state()
 w0 = 0 if start else bench.WINDOW_START
-e = bench.make_engine(bench.design_maker(name)(), cfg, 0, w0, st)
+e = bench.make_engine(bench.design_maker(name)(), cfg, 0, w0, st,
+                      precision=int(os.environ.get("GCS_PROBE_PRECISION", "64")))
 e.set_option(A.OPT_FUSED_STEP, int(opts.pop("fused", 3)))
 for k, v in opts.items():
     e.set_option(getattr(A, "OPT_" + k.upper()), int(v))
