@@ -10,7 +10,7 @@ root=$(pwd)
 out=$root/gpurun_out/prof_$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
-bench=(python3 "$root/bench.py" --steps "$steps" --warmup 50 --cpu-budget 0 --profile-steps 10 --no-start-window --replicas-per-gpu "${REPLICAS:-1}" --c5-steps 0 --cycle-scale 0 --precision "${PREC:-64}" --no-f32-leg)
+bench=(python3 "$root/bench.py" --steps "$steps" --warmup 50 --cpu-budget 0 --profile-steps 10 --no-start-window --replicas-per-gpu "${REPLICAS:-1}" --c5-steps 0 --cycle-scale 0 --precision "${PREC:-64}" --no-f32-leg --config "${CONFIG:-c2}")
 # rocprofv3 --kernel-trace segfaults inside hipGraphLaunch when HIP dispatches a graph's pre-captured AQL packets
 # (the default graph packet capture): the fault is in librocprofiler-sdk's queue-write interceptor, which reads a
 # packet header one page past the array it is handed (profiles/r04_rocprof_crash.txt).  Profiling runs
