@@ -431,3 +431,32 @@ def test_default_skin_per_precision(c1_design, prec, pm):
     e.set_option(A.OPT_LIST_SKIN, 420)
     e.run(2, first_step=LATE["step"] + 2, seed=1)
     assert e.list_stats()["skin"] == pytest.approx(0.42 * cfg.a_core_diameter, rel=1e-6)
+
+
+@precisions
+@pytest.mark.parametrize("n", [1, 2, 65, 1025])
+def test_list_relaxation_small_and_ragged_sizes(n, prec):
+    """the relaxation step on the lists (k_lstep<..., RLX> + k_lupdate) at ragged sizes: random particles, several
+    pair classes, a chain; spacestep 2e-3 with dt 1e-4 (the limit active), 15 steps vs the oracle"""
+    rng = np.random.default_rng(100 + n)
+    x = rng.uniform(-0.5, 0.5, size=(n, 3))
+    ab = rng.choice([0.0, 0.5, 1.0], size=(n, 2))
+    mu = rng.uniform(0.5, 1.5, size=n)
+    sysd = {}
+    for name, cls in (("e", Engine), ("o", oracle.OracleSystem)):
+        s = cls(n, mobilities=mu, ab_factors=ab, precision=prec)
+        s.add_neighbor_softcore(2.5, 0.3, 2.5, 0.24, 0.3, mix=True, scaled=True)
+        if n > 1:
+            s.add_bonded_pairwise(A.POT_SEMISPRING, a_spring=100.0, b_spring=50.0, mix=True, scaled=True,
+                                  ranges=[(0, n)])
+        s.set_context({"core_scale": 0.8, "bond_scale": 0.7, "wall_semiaxes": [1, 1, 1]})
+        s.set_positions(x)
+        if name == "e":
+            s.set_option(A.OPT_FUSED_STEP, 3)
+            s.set_option(A.OPT_DENSE_NEIGHBORS, 0)
+        sysd[name] = s
+    for s in sysd.values():
+        s.run(15, seed=2, timestep=1e-4, spacestep=2e-3)
+    assert np.abs(sysd["e"].get_positions() - sysd["o"].get_positions()).max() <= TOL_X[prec]
+    assert sysd["e"].get_context()["last_timestep"] == pytest.approx(sysd["o"].get_context()["last_timestep"],
+                                                                    rel={64: 1e-10, 32: 1e-4}[prec])
