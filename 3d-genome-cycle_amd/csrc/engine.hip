@@ -851,7 +851,6 @@ ForceArgs list_args(const gcs_engine* e)
     a.list_stride = (e->n + 63) & ~63;
     a.list_skin = list_skin(e);
     a.list_waves = e->list_waves;
-    a.list_rel = e->n > 65536 ? 1 : 0;
     a.list_deal = list_deal(e);
     a.par_hint = -1;
     return a;

@@ -296,7 +296,6 @@ struct ForceArgs {
     int list_stride;        // >= N
     float list_skin;        // > 0 only in the list path's own argument block
     int list_waves;         // waves per tile (list segments): 4, or 2 (GCS_OPT_LIST_WAVES)
-    int list_rel;           // 16-bit entries hold (partner slot - own slot + 2^15) (N > 65,536), else the slot
     unsigned long long list_deal;  // list build: candidate chunk -> wave segment pattern (GCS_OPT_LIST_DEAL; 0: round robin)
     int par_hint;           // >= 0: ctx->parity of this launch, known to the host at enqueue (the slot loads need not
                             // wait for the context); -1: read it
@@ -451,7 +450,7 @@ void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2, double d2_64);
 void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const double* glob, int flags,
                              const int* shared, int nshared, void* bands, int npeer, int band_stride);
 int list_step_grid(int n);
-bool list_u16(int n);  // 16-bit list entries (absolute slots for N <= 65536, relative beyond: ForceArgs::list_rel)
+bool list_u16(int n);  // list entries are 16-bit slot indices (N <= 65536)
 void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceArgs& a, bool fused);
 // fp64 force / energy evaluation on the current cell list (one thread per sorted slot; kernels.hip k_eval64):
 // kModeForce -> a.dforce_out + partial rows a.dpart [blocks][8] (reactions in[3], out[3], max mu|F|, neighbours),

@@ -2004,16 +2004,12 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                     const int e = reinterpret_cast<const int*>(my_cand)[4 * kSub + k];  // the partner's sorted slot
                     if (e != s) {
                         const int kk = *lcnt;
-                        // relative entries (N > 65,536): the partner's slot offset from this slot + 2^15; a partner
-                        // further than that in the sorted order marks the list overflowed (exact search instead)
-                        const int ev = a.list_rel ? e - s + 32768 : e;
-                        const bool fits = !a.list_rel || (unsigned)ev <= 65535u;
-                        if (kk < a.list_cap && fits) {
-                            *lpend = (*lpend >> EB) | ((unsigned long long)(LE)ev << (64 - EB));
+                        if (kk < a.list_cap) {
+                            *lpend = (*lpend >> EB) | ((unsigned long long)(LE)e << (64 - EB));
                             if (kk % E == E - 1)
                                 lw[((size_t)wv * (a.list_cap / E) + kk / E) * a.list_stride + s] = *lpend;
                         }
-                        *lcnt = fits ? kk + 1 : max(kk + 1, a.list_cap + 1);
+                        *lcnt = kk + 1;
                     }
                 }
             }
@@ -3122,14 +3118,13 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     if (a.has_pair) {
         const int cnt = (act && !fb) ? min(cw & kListCountMask, cap) : 0;
         const int kmax = uniform(wave_max_int(cnt));
-        const int rbase = a.list_rel ? s - 32768 : 0;  // relative 16-bit entries (N > 65,536)
         // batches of kU entries: the partners' gathers are issued first, then the next batch's entry words (they
         // return right behind the gathers, so each batch costs one round trip), then the pair forces (and contacts)
         const int klast = (cap / kU - 1) * kU;  // the segment's last batch (list_cap is a multiple of kU)
         for (int k0 = 0; k0 < kmax; k0 += kU) {
             R4 q[kU];
 #pragma unroll
-            for (int u = 0; u < kU; ++u) q[u] = qc[(k0 + u < cnt) ? list_entry<LE>(e, u) + rbase : sl];
+            for (int u = 0; u < kU; ++u) q[u] = qc[(k0 + u < cnt) ? list_entry<LE>(e, u) : sl];
             const int kn = min(k0 + kU, klast);
 #pragma unroll
             for (int j = 0; j < kW; ++j) e[j] = segw[(size_t)(kn / kE + j) * stride];
@@ -3918,9 +3913,7 @@ void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceAr
 
 int list_step_grid(int n) { return force_blocks(n); }
 
-// 16-bit entries: absolute slots for N <= 65,536, relative to the own slot beyond (ForceArgs::list_rel); every system
-// the list step admits (N < 2^24) takes them.  (The 32-bit instantiations remain for list_rel == 0 beyond 2^16 only.)
-bool list_u16(int n) { return n < (1 << kListIndexBits); }
+bool list_u16(int n) { return n <= 65536; }
 
 void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a)
 {

@@ -460,28 +460,3 @@ def test_list_relaxation_small_and_ragged_sizes(n, prec):
     assert np.abs(sysd["e"].get_positions() - sysd["o"].get_positions()).max() <= TOL_X[prec]
     assert sysd["e"].get_context()["last_timestep"] == pytest.approx(sysd["o"].get_context()["last_timestep"],
                                                                     rel={64: 1e-10, 32: 1e-4}[prec])
-
-
-@precisions
-def test_relative_entries_beyond_65536_with_escapes(prec):
-    """N > 65,536: 16-bit entries hold the partner's slot relative to the particle's own (list_rel).  A 70,000-particle
-    slab two list cells thick puts ~35,000 slots between a particle and its partners across the middle plane, beyond
-    the 16-bit range: those lists are marked overflowed and the particles searched exactly.  Same bound vs the
-    oracle (softcore only, 5 steps), and the exact searches happened."""
-    n = 70000
-    rng = np.random.default_rng(7)
-    x = np.column_stack([rng.uniform(0, 20, n), rng.uniform(0, 20, n), rng.uniform(0, 1.0, n)])
-    sysd = {}
-    for name, cls in (("e", Engine), ("o", oracle.OracleSystem)):
-        s = cls(n, precision=prec)
-        s.add_neighbor_softcore(2.5, 0.3, 2.5, 0.24, 0.3, mix=False, scaled=False)
-        s.set_positions(x)
-        if name == "e":
-            s.set_option(A.OPT_FUSED_STEP, 3)
-            s.set_option(A.OPT_DENSE_NEIGHBORS, 0)
-        sysd[name] = s
-    for s in sysd.values():
-        s.run(5, seed=3, timestep=1e-5)
-    st = sysd["e"].list_stats()
-    assert st["active"] == 1 and st["fallback_particle_steps"] > 0, st
-    assert np.abs(sysd["e"].get_positions() - sysd["o"].get_positions()).max() <= TOL_X[prec]
