@@ -255,6 +255,7 @@ struct gcs_engine {
     // list step (GCS_OPT_FUSED_STEP 3): neighbour lists, pair-factor classes, rebuild period
     int* list = nullptr;
     int* lcount = nullptr;
+    int4* lbase = nullptr;
     float4* psort[2] = {nullptr, nullptr};
     float4* skmu = nullptr;  // list step: slot-ordered kmu and bond CSR rows
     int2* sbrow = nullptr;
@@ -269,6 +270,7 @@ struct gcs_engine {
     int list_every_opt = 0;     // GCS_OPT_LIST_EVERY: rebuild period in steps (0: from the noise amplitude)
     int list_every = 1;         // the period of the current run
     int list_waves = 4;         // GCS_OPT_LIST_WAVES: waves per tile (2: more tiles resident, for replica runs)
+    int list_fmt_opt = 0;       // GCS_OPT_LIST_FORMAT: 0 auto, 1 plane-relative 16-bit, 2 absolute 32-bit
     long long list_deal_opt = -1;  // GCS_OPT_LIST_DEAL: chunk -> wave pattern of the list build (-1: the default for
                                    // list_waves, 0: round robin)
     bool l_need_build = true;   // the next list step must rebuild (run start without continuity)
@@ -809,6 +811,15 @@ float list_skin(const gcs_engine* e)
     return 1e-3f * (float)pm * e->fa.pf.pair_dist;
 }
 
+// the list entry format (GCS_OPT_LIST_FORMAT): absolute 16-bit slots up to 65,536 particles, plane-relative 16-bit
+// slots beyond (kernels.hip ListRel16), or the form the option names
+int list_format(const gcs_engine* e)
+{
+    if (e->list_fmt_opt == 2) return kListFmtInt;
+    if (e->list_fmt_opt == 1) return kListFmtRel16;
+    return e->n <= 65536 ? kListFmtAbs16 : kListFmtRel16;
+}
+
 // the list build's chunk deal (kernels.hip deal_nth): the option, or the default for the waves per tile
 unsigned long long list_deal(const gcs_engine* e)
 {
@@ -851,6 +862,8 @@ ForceArgs list_args(const gcs_engine* e)
     a.list_stride = (e->n + 63) & ~63;
     a.list_skin = list_skin(e);
     a.list_waves = e->list_waves;
+    a.list_fmt = list_format(e);
+    a.lbase = e->lbase;
     a.list_deal = list_deal(e);
     a.par_hint = -1;
     return a;
@@ -863,6 +876,7 @@ int ensure_list(gcs_engine* e)
     if (need <= e->list_alloc && e->lcount) return GCS_OK;
     dfree(e->list);
     dfree(e->lcount);
+    dfree(e->lbase);
     dfree(e->psort[0]);
     dfree(e->psort[1]);
     dfree(e->skmu);
@@ -873,7 +887,7 @@ int ensure_list(gcs_engine* e)
     e->list_alloc = 0;
     int rc;
     if ((rc = dalloc(&e->list, need)) || (rc = dalloc(&e->lcount, stride * kMaxListWaves)) ||
-        (rc = dalloc(&e->sbrow, stride)))
+        (rc = dalloc(&e->lbase, stride)) || (rc = dalloc(&e->sbrow, stride)))
         return rc;
     if (e->prec == 64) {  // the slot-ordered copies in the engine's precision only
         if ((rc = dalloc(&e->dpsort[0], stride)) || (rc = dalloc(&e->dpsort[1], stride)) || (rc = dalloc(&e->dskmu, stride)))
@@ -1065,7 +1079,7 @@ int probe_density(gcs_engine* e)
     HIPCHK(hipMemcpyAsync(&pairs, e->s_total, sizeof(int), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     e->dense_mean = 2.0 * pairs / (double)e->n;
-    e->dense = e->dense_mean * (list_u16(e->n) ? 1.0 : 2.0) > (double)e->dense_opt;
+    e->dense = e->dense_mean * (list_format(e) == kListFmtInt ? 2.0 : 1.0) > (double)e->dense_opt;
     return GCS_OK;
 }
 
@@ -1501,6 +1515,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->sw_idx);
     dfree(e->list);
     dfree(e->lcount);
+    dfree(e->lbase);
     dfree(e->psort[0]);
     dfree(e->psort[1]);
     dfree(e->skmu);
@@ -3120,6 +3135,14 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         if (value != -1 && !deal_valid(value, e->list_waves))
             return fail(GCS_EINVAL, "list deal must be -1, 0 or (period << 60 | wave nibbles < waves per tile)");
         e->list_deal_opt = value;
+        drop_graph(e);
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_LIST_FORMAT) {
+        if (value != 0 && value != 1 && value != 2)
+            return fail(GCS_EINVAL, "list format must be 0 (default), 1 (plane-relative 16-bit) or 2 (32-bit)");
+        e->list_fmt_opt = (int)value;
+        e->l_need_build = true;
         drop_graph(e);
         return GCS_OK;
     }

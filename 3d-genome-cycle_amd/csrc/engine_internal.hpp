@@ -285,6 +285,7 @@ struct ForceArgs {
     // (ping-pong with ctx->parity), .w = particle | class << 24 (class: the (a, b) pair factors, type_ab[class]).
     int* list;
     int* lcount;
+    int4* lbase;            // list_fmt kListFmtRel16: per slot the partner planes' first slots (kernels.hip ListRel16)
     const int* ptype;       // [N] pair-factor class of each particle
     float4* psort0;
     float4* psort1;
@@ -296,6 +297,7 @@ struct ForceArgs {
     int list_stride;        // >= N
     float list_skin;        // > 0 only in the list path's own argument block
     int list_waves;         // waves per tile (list segments): 4, or 2 (GCS_OPT_LIST_WAVES)
+    int list_fmt;           // list entries: kListFmtAbs16 / kListFmtInt / kListFmtRel16 (list_format)
     unsigned long long list_deal;  // list build: candidate chunk -> wave segment pattern (GCS_OPT_LIST_DEAL; 0: round robin)
     int par_hint;           // >= 0: ctx->parity of this launch, known to the host at enqueue (the slot loads need not
                             // wait for the context); -1: read it
@@ -380,6 +382,11 @@ constexpr int kListSkinPm64 = 350;
 constexpr int kMaxListWaves = 4;  // waves per tile of the list kernels (each owns one list segment): 2 or 4
 constexpr int kMaxTypes = 256;          // pair-factor classes (8 bits of a list entry)
 constexpr int kListIndexBits = 24;      // particle index bits of a list entry
+// list entry formats (GCS_OPT_LIST_FORMAT): 16-bit absolute slots (N <= 65,536), 32-bit absolute slots, 16-bit
+// slots relative to the slot's plane bases (kernels.hip ListRel16: the default beyond 65,536 particles)
+constexpr int kListFmtAbs16 = 0;
+constexpr int kListFmtInt = 1;
+constexpr int kListFmtRel16 = 2;
 constexpr int kListCountMask = (1 << 30) - 1;
 constexpr int kListOverflow = 1 << 30;
 
@@ -450,7 +457,6 @@ void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2, double d2_64);
 void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const double* glob, int flags,
                              const int* shared, int nshared, void* bands, int npeer, int band_stride);
 int list_step_grid(int n);
-bool list_u16(int n);  // list entries are 16-bit slot indices (N <= 65536)
 void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceArgs& a, bool fused);
 // fp64 force / energy evaluation on the current cell list (one thread per sorted slot; kernels.hip k_eval64):
 // kModeForce -> a.dforce_out + partial rows a.dpart [blocks][8] (reactions in[3], out[3], max mu|F|, neighbours),

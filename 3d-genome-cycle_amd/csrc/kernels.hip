@@ -16,6 +16,7 @@
 #include "engine_internal.hpp"
 
 #include <hipcub/hipcub.hpp>
+#include <type_traits>
 
 #include "../../include/gcs.h"
 
@@ -1766,6 +1767,37 @@ __device__ __forceinline__ size_t list_at(int w, int cap, int k, int s, size_t s
     constexpr int E = 8 / (int)sizeof(LE);
     return (((size_t)w * (size_t)(cap / E) + (size_t)(k / E)) * stride + (size_t)s) * E + (size_t)(k % E);
 }
+// ListRel16 (ForceArgs::list_fmt kListFmtRel16, the default beyond 65,536 particles): 16-bit entries p << 14 | u
+// relative to the slot's plane bases lbase[s] = {b0, b1, b2}: the partner's slot is b_p + u.  p = 0, 1, 2 is the
+// partner's z plane (the slot's build cell z - 1, z, z + 1) and b_p the first slot of cell (x - fx, y - 1) in that
+// plane: a partner lies in the plane's rows y - 1 .. y + 1 and cells x - fx .. x + fx, so u spans at most two cell rows
+// plus 2 fx + 1 cells -- below 2^14 slots even at C5's densest start (11,231: profiles/r04_c5_plane_spans.txt).  A
+// partner outside [b_p, b_p + 2^14) marks the list overflowed (exact search).  Absolute slots would need 32 bits past
+// 2^16 particles; an offset from the slot's own index would span a whole z layer of cells (tens of thousands).
+struct ListRel16 {
+    unsigned short v;
+};
+template <typename LE>
+struct ListFmt {
+    static constexpr bool rel = false;
+};
+template <>
+struct ListFmt<ListRel16> {
+    static constexpr bool rel = true;
+};
+constexpr int kRelBits = 14;
+// the partner slot of a list entry (x: its raw bits)
+template <typename LE>
+__device__ __forceinline__ int list_slot(int x, int4 lb)
+{
+    if constexpr (ListFmt<LE>::rel) {
+        const int p = x >> kRelBits;
+        return (p == 0 ? lb.x : (p == 1 ? lb.y : lb.z)) + (x & ((1 << kRelBits) - 1));
+    } else {
+        (void)lb;
+        return x;
+    }
+}
 // entry u of a batch held as 8-byte words
 template <typename LE>
 __device__ __forceinline__ int list_entry(const uint2* w, int u)
@@ -1807,7 +1839,7 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                                        int s_begin, int s_end, float4 pi, float bi, float& fx, float& fy, float& fz,
                                        float& acc, int* s_rowV, int* s_rowJ, float4* s_cand, int* s_candj, int& ntot,
                                        int wv, int nwv, int self = -1, bool lvalid = false, int* lcnt = nullptr,
-                                       unsigned long long* lpend = nullptr)
+                                       unsigned long long* lpend = nullptr, int4* plb = nullptr)
 {
     // kModeList: phase 2 appends each hit (other than the particle itself) to the lane's list segment wv
     // instead of evaluating the pair force (the lists of the list step, built at the grid's rc = cutoff + skin)
@@ -1848,6 +1880,18 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 }
             }
         }
+        if constexpr (MODE == kModeList && ListFmt<LE>::rel) {
+            // this lane's plane bases (ListRel16): first slot of cell (x - fx, y - 1) in planes z - 1, z, z + 1
+            const int cx = a.scell[min(s, s_end - 1)] % nx;
+            const int xb = max(cx - gfx, 0), yb = max(y0 - 1, 0);
+            int b[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const int z = z0 + p - 1;
+                b[p] = (z >= 0 && z < nz) ? a.cstart[(z * ny + yb) * nx + xb] : 0;
+            }
+            *plb = make_int4(b[0], b[1], b[2], 0);
+        }
         int incl = len;
         GCS_DPP_SCAN(dpp_i, add_i, 0, incl)
         const int gbase = __shfl(incl, max(9 * h - 1, 0));
@@ -1887,7 +1931,7 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
 
     float4 np[FPL];
     float nb[FPL];
-    int nj[FPL];
+    int nj[FPL], npl[FPL];
     auto fetch = [&](int c) {
         const int cg = deal ? deal_nth(deal, dT, dkw, wv, c) : wv + c * nwv;  // chunk index within every group
 #pragma unroll
@@ -1901,6 +1945,7 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 for (int step = 8; step > 0; step >>= 1)
                     if (rowV[lo + step] <= v) lo += step;
                 nj[f] = rowJ[lo] + (v - rowV[lo]);
+                npl[f] = lo / 3;  // the stencil row's z plane (rows q = 0..8: z = z0 + q / 3 - 1)
                 np[f] = a.spos[nj[f]];
                 nb[f] = a.sb[nj[f]];
             }
@@ -1922,7 +1967,9 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 P[h8 + 2] = -2.f * py;
                 P[h8 + 4] = -2.f * pz;
                 P[h8 + 6] = fmaf(pz, pz, fmaf(py, py, px * px));
-                reinterpret_cast<int*>(my_cand)[4 * kSub + i] = real ? nj[f] : -1;
+                // the partner's slot (< 2^24) and, for ListRel16, its plane in bits 28..29
+                reinterpret_cast<int*>(my_cand)[4 * kSub + i] =
+                    real ? (ListFmt<LE>::rel ? (nj[f] | (npl[f] << 28)) : nj[f]) : -1;
                 continue;
             }
             my_cand[2 * i] = make_float4(-2.f * px, -2.f * py, -2.f * pz, fmaf(pz, pz, fmaf(py, py, px * px)));
@@ -2001,15 +2048,24 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 const unsigned k = min(b ^ 7u, (unsigned)kSub);
                 m &= m - 1u;
                 if (k < (unsigned)kSub && lvalid) {
-                    const int e = reinterpret_cast<const int*>(my_cand)[4 * kSub + k];  // the partner's sorted slot
+                    const int er = reinterpret_cast<const int*>(my_cand)[4 * kSub + k];
+                    const int e = er & 0x0fffffff;  // the partner's sorted slot
                     if (e != s) {
                         const int kk = *lcnt;
-                        if (kk < a.list_cap) {
-                            *lpend = (*lpend >> EB) | ((unsigned long long)(LE)e << (64 - EB));
+                        unsigned code = (unsigned)e;
+                        bool fits = true;
+                        if constexpr (ListFmt<LE>::rel) {
+                            const int p = er >> 28;
+                            const int u = e - (p == 0 ? plb->x : (p == 1 ? plb->y : plb->z));
+                            fits = (unsigned)u < (1u << kRelBits);
+                            code = ((unsigned)p << kRelBits) | (unsigned)u;
+                        }
+                        if (kk < a.list_cap && fits) {
+                            *lpend = (*lpend >> EB) | ((unsigned long long)code << (64 - EB));
                             if (kk % E == E - 1)
                                 lw[((size_t)wv * (a.list_cap / E) + kk / E) * a.list_stride + s] = *lpend;
                         }
-                        *lcnt = kk + 1;
+                        *lcnt = fits ? kk + 1 : max(kk + 1, a.list_cap + 1);  // out of range: overflowed
                     }
                 }
             }
@@ -2919,9 +2975,11 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
         float fx = 0.f, fy = 0.f, fz = 0.f, acc = 0.f;
         int cnt = 0;
         unsigned long long pend = 0ull;
+        int4 lb = make_int4(0, 0, 0, 0);
         pair_forces_sub<kModeList, GCS_LBUILD_GROUPS, LE>(ctx, a, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
                                       s_rowJ[wave], s_cand[wave], nullptr, ntot, wave, kListWaves, self, valid, &cnt,
-                                      &pend);
+                                      &pend, &lb);
+        if (ListFmt<LE>::rel && valid && wave == 0) a.lbase[s] = lb;
         {  // the last, partial word of the lane's segment (its r entries sit in the top r slots: shift them down)
             constexpr int E = 8 / (int)sizeof(LE);
             const int r = cnt % E;
@@ -3008,6 +3066,22 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 // RLX (the relaxation step's force launch, simulation_driver_relaxation.cpp:48-55): wave 0 stores the force (slot
 // order, .w = mu) instead of integrating and folds max mu |F| into the accumulators; the final workgroup sets the
 // adapted timestep ctx->dt_used (k_red64's arithmetic) and the reactions; k_lupdate then moves the particles.
+#ifndef GCS_LIST_NT
+#define GCS_LIST_NT 2  // list words read with the non-temporal hint: 0 never, 1 always, 2 beyond absolute 16-bit lists
+#endif
+// one 8-byte list word of the list step (read once per step: with the non-temporal hint it should not displace the
+// gathered positions from the XCD's L2).  Same-box A/B (profiles/r04_list_format_ab.txt): C5 fp64 +3-5 %, C2 fp64
+// with 4 trajectories -16 % when applied to its absolute 16-bit lists (which the L2 / Infinity Cache would keep)
+template <typename LE>
+__device__ __forceinline__ uint2 list_word(const uint2* p)
+{
+    if constexpr (GCS_LIST_NT == 1 || (GCS_LIST_NT == 2 && !std::is_same<LE, unsigned short>::value)) {
+        const unsigned long long v = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(p));
+        return make_uint2((unsigned)v, (unsigned)(v >> 32));
+    } else {
+        return *p;
+    }
+}
 template <typename LE, int W, bool CT, bool DOM = false, typename R = float, bool RLX = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS_LIST_WAVES_PER_EU_CT : (sizeof(R) == 8 ? GCS_LIST_WAVES_PER_EU64 : GCS_LIST_WAVES_PER_EU)))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int flags)
 {
@@ -3046,9 +3120,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     const R4 pi = qc[sl];
     const float4 pb = a.spos[sl];
     const int cw = a.lcount[(size_t)wave * stride + sl];
+    int4 lb = make_int4(0, 0, 0, 0);
+    if constexpr (ListFmt<LE>::rel) lb = a.lbase[sl];
     uint2 e[kW];
 #pragma unroll
-    for (int j = 0; j < kW; ++j) e[j] = segw[(size_t)j * stride];  // list_cap >= kU: in bounds
+    for (int j = 0; j < kW; ++j) e[j] = list_word<LE>(segw + (size_t)j * stride);  // list_cap >= kU: in bounds
     const R cs = (R)ctx->cs;
     const float D = ctx->ldisp;
     const float lrc_b = ctx->lrc_b;
@@ -3124,10 +3200,10 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         for (int k0 = 0; k0 < kmax; k0 += kU) {
             R4 q[kU];
 #pragma unroll
-            for (int u = 0; u < kU; ++u) q[u] = qc[(k0 + u < cnt) ? list_entry<LE>(e, u) : sl];
+            for (int u = 0; u < kU; ++u) q[u] = qc[(k0 + u < cnt) ? list_slot<LE>(list_entry<LE>(e, u), lb) : sl];
             const int kn = min(k0 + kU, klast);
 #pragma unroll
-            for (int j = 0; j < kW; ++j) e[j] = segw[(size_t)(kn / kE + j) * stride];
+            for (int j = 0; j < kW; ++j) e[j] = list_word<LE>(segw + (size_t)(kn / kE + j) * stride);
             __builtin_amdgcn_sched_barrier(0);  // keep the entry loads here, ahead of the arithmetic
 #pragma unroll
             for (int u = 0; u < kU; ++u)
@@ -3913,39 +3989,41 @@ void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceAr
 
 int list_step_grid(int n) { return force_blocks(n); }
 
-bool list_u16(int n) { return n <= 65536; }
+// the entry type of the launch's list format (ForceArgs::list_fmt), handed to fn as a value of that type
+template <typename Fn>
+static void with_list_entry(const ForceArgs& a, Fn&& fn)
+{
+    if (a.list_fmt == kListFmtAbs16)
+        fn((unsigned short)0);
+    else if (a.list_fmt == kListFmtRel16)
+        fn(ListRel16{});
+    else
+        fn((int)0);
+}
 
 void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a)
 {
     const dim3 g(force_grid(a.n));
-    if (list_u16(a.n)) {
+    with_list_entry(a, [&](auto tag) {
+        using LE = decltype(tag);
         if (a.list_waves == 2)
-            hipLaunchKernelGGL((k_lbuild<unsigned short, 2>), g, dim3(128), 0, s, ctx, a);
+            hipLaunchKernelGGL((k_lbuild<LE, 2>), g, dim3(128), 0, s, ctx, a);
         else
-            hipLaunchKernelGGL((k_lbuild<unsigned short, 4>), g, dim3(256), 0, s, ctx, a);
-    } else {
-        if (a.list_waves == 2)
-            hipLaunchKernelGGL((k_lbuild<int, 2>), g, dim3(128), 0, s, ctx, a);
-        else
-            hipLaunchKernelGGL((k_lbuild<int, 4>), g, dim3(256), 0, s, ctx, a);
-    }
+            hipLaunchKernelGGL((k_lbuild<LE, 4>), g, dim3(256), 0, s, ctx, a);
+    });
 }
 
 template <bool CT, typename R>
 static void launch_list_step_ct(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)
 {
     const dim3 g(list_step_grid(a.n));
-    if (list_u16(a.n)) {
+    with_list_entry(a, [&](auto tag) {
+        using LE = decltype(tag);
         if (a.list_waves == 2)
-            hipLaunchKernelGGL((k_lstep<unsigned short, 2, CT, false, R>), g, dim3(128), 0, s, ctx, a, flags);
+            hipLaunchKernelGGL((k_lstep<LE, 2, CT, false, R>), g, dim3(128), 0, s, ctx, a, flags);
         else
-            hipLaunchKernelGGL((k_lstep<unsigned short, 4, CT, false, R>), g, dim3(256), 0, s, ctx, a, flags);
-    } else {
-        if (a.list_waves == 2)
-            hipLaunchKernelGGL((k_lstep<int, 2, CT, false, R>), g, dim3(128), 0, s, ctx, a, flags);
-        else
-            hipLaunchKernelGGL((k_lstep<int, 4, CT, false, R>), g, dim3(256), 0, s, ctx, a, flags);
-    }
+            hipLaunchKernelGGL((k_lstep<LE, 4, CT, false, R>), g, dim3(256), 0, s, ctx, a, flags);
+    });
 }
 
 __global__ void k_set_contact(DevCtx* ctx, float d2, double d2_64)
@@ -3962,17 +4040,13 @@ template <typename R>
 static void launch_list_relax_r(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force_flags, int update_flags)
 {
     const dim3 g(list_step_grid(a.n));
-    if (list_u16(a.n)) {
+    with_list_entry(a, [&](auto tag) {
+        using LE = decltype(tag);
         if (a.list_waves == 2)
-            hipLaunchKernelGGL((k_lstep<unsigned short, 2, false, false, R, true>), g, dim3(128), 0, s, ctx, a, force_flags);
+            hipLaunchKernelGGL((k_lstep<LE, 2, false, false, R, true>), g, dim3(128), 0, s, ctx, a, force_flags);
         else
-            hipLaunchKernelGGL((k_lstep<unsigned short, 4, false, false, R, true>), g, dim3(256), 0, s, ctx, a, force_flags);
-    } else {
-        if (a.list_waves == 2)
-            hipLaunchKernelGGL((k_lstep<int, 2, false, false, R, true>), g, dim3(128), 0, s, ctx, a, force_flags);
-        else
-            hipLaunchKernelGGL((k_lstep<int, 4, false, false, R, true>), g, dim3(256), 0, s, ctx, a, force_flags);
-    }
+            hipLaunchKernelGGL((k_lstep<LE, 4, false, false, R, true>), g, dim3(256), 0, s, ctx, a, force_flags);
+    });
     hipLaunchKernelGGL(k_lupdate<R>, dim3((a.n + kLUpdateBlock - 1) / kLUpdateBlock), dim3(kLUpdateBlock), 0, s, ctx, a,
                        update_flags);
 }
@@ -3988,17 +4062,13 @@ template <typename R>
 static void launch_list_step_dom(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)
 {
     const dim3 g(list_step_grid(a.n));
-    if (list_u16(a.n)) {
+    with_list_entry(a, [&](auto tag) {
+        using LE = decltype(tag);
         if (a.list_waves == 2)
-            hipLaunchKernelGGL((k_lstep<unsigned short, 2, false, true, R>), g, dim3(128), 0, s, ctx, a, flags);
+            hipLaunchKernelGGL((k_lstep<LE, 2, false, true, R>), g, dim3(128), 0, s, ctx, a, flags);
         else
-            hipLaunchKernelGGL((k_lstep<unsigned short, 4, false, true, R>), g, dim3(256), 0, s, ctx, a, flags);
-    } else {
-        if (a.list_waves == 2)
-            hipLaunchKernelGGL((k_lstep<int, 2, false, true, R>), g, dim3(128), 0, s, ctx, a, flags);
-        else
-            hipLaunchKernelGGL((k_lstep<int, 4, false, true, R>), g, dim3(256), 0, s, ctx, a, flags);
-    }
+            hipLaunchKernelGGL((k_lstep<LE, 4, false, true, R>), g, dim3(256), 0, s, ctx, a, flags);
+    });
 }
 
 void launch_list_step(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)

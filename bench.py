@@ -151,6 +151,14 @@ def load_state():
     return z["positions"].astype(np.float64), ctx
 
 
+def apply_engine_opts(e, args):
+    """experiments: --engine-opt list_skin=300 (gcs._abi OPT_<NAME>); list_deal=d:0120123 -> a deal pattern"""
+    from gcs import _abi as A
+    for kv in args.engine_opt:
+        name, v = kv.split("=")
+        e.set_option(getattr(A, "OPT_" + name.upper()), A.list_deal(v[2:]) if v.startswith("d:") else int(v))
+
+
 def make_engine(design, cfg, device, start_step, state=None, precision=64):
     from gcs import interphase
     from gcs.engine import Engine
@@ -613,9 +621,7 @@ def replica_main(args):
                          (A.OPT_TILE_PRIORITY, args.prio), (A.OPT_SUBTILES, args.subtiles)]
             for opt, v in opts:
                 e.set_option(opt, v)
-            for kv in args.engine_opt:  # experiments: --engine-opt list_skin=300 (gcs._abi OPT_<NAME>)
-                name, v = kv.split("=")  # list_deal=d:0120123 -> a deal pattern (gcs._abi.list_deal)
-                e.set_option(getattr(A, "OPT_" + name.upper()), A.list_deal(v[2:]) if v.startswith("d:") else int(v))
+            apply_engine_opts(e, args)
             if args.cu_split and R > 1:
                 # replica k on CUs c with (c mod R) == k ("interleave") or a contiguous R-th of them ("block")
                 ncu = args.cu_count
@@ -754,6 +760,7 @@ def replica_main(args):
         if rank == 0 and not args.no_start_window:
             e0 = make_engine(design, cfg, local, 0, precision=args.precision)
             e0.set_option(A.OPT_GRAPH_STEPS, G)
+            apply_engine_opts(e0, args)
             e0.run(max(64, 2 * G), first_step=0, seed=seed, **bd)
             e0.synchronize()
             k0 = max(256, K // 4)

@@ -376,13 +376,17 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
 #define GCS_OPT_LIST_WAVES 13     /* list step: waves per 64-particle tile, 4 (default: lowest step latency) or 2 (more
                                      tiles resident: the better throughput when several trajectories share a GPU) */
 #define GCS_OPT_DENSE_NEIGHBORS 15 /* fp32 list step (GCS_OPT_FUSED_STEP 3): a fresh run whose mean neighbour count within the
-                                     cutoff, x 2 when list entries are 32-bit (N > 65,536), exceeds this takes the
+                                     cutoff, x 2 when list entries are 32-bit (GCS_OPT_LIST_FORMAT 2), exceeds this takes the
                                      unfused tile step instead (default 48; 0: never) */
 #define GCS_OPT_LIST_DEAL 16      /* list build: which wave segment takes each candidate chunk; -1 (default) the tuned
                                      pattern for the waves per tile, 0 round robin, else period T (1..15) << 60 | the
                                      wave (< waves per tile) of chunk p of each period in nibble p.  Only the split of
                                      a slot's list over the segments changes (the list step's last wave also carries
                                      the particle-local terms); the pair set and the results do not */
+#define GCS_OPT_LIST_FORMAT 17    /* list entries: 0 (default) 16-bit absolute slots up to 65,536 particles, 16-bit slots
+                                     relative to the particle's cell planes beyond (an entry out of their range sends the
+                                     particle to the exact search); 1 the relative form at any size; 2 32-bit absolute
+                                     slots.  Every form holds the same pairs in the same order: the results do not change */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
 
 /* List-step diagnostics (the neighbour lists md::neighbor_searcher keeps between rebuilds; micromd, called at

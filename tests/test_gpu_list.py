@@ -460,3 +460,64 @@ def test_list_relaxation_small_and_ragged_sizes(n, prec):
     assert np.abs(sysd["e"].get_positions() - sysd["o"].get_positions()).max() <= TOL_X[prec]
     assert sysd["e"].get_context()["last_timestep"] == pytest.approx(sysd["o"].get_context()["last_timestep"],
                                                                     rel={64: 1e-10, 32: 1e-4}[prec])
+
+
+def _format_run(design, cfg, prec, fmt, steps, ctx=LATE, seed=11, **opts):
+    e = _list_engine(design, cfg, prec, list_format=fmt, **opts)
+    e.set_schedule(**interphase.interphase_schedule(cfg))
+    e.set_context(ctx)
+    e.run(steps, first_step=ctx["step"], temperature=cfg.temperature, timestep=cfg.timestep, seed=seed)
+    return e.get_positions(), e.list_stats()
+
+
+@precisions
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_list_formats_bitwise_c1(c1_design, prec, fmt):
+    """GCS_OPT_LIST_FORMAT: plane-relative 16-bit entries (1, kernels.hip ListRel16) and 32-bit entries (2) hold the
+    same pairs in the same order as the default absolute 16-bit entries: the trajectory (list rebuilds included) is
+    bitwise the same, with the same particles searched exactly"""
+    cfg = InterphaseConfig()
+    x0, s0 = _format_run(c1_design, cfg, prec, 0, 60)
+    x1, s1 = _format_run(c1_design, cfg, prec, fmt, 60)
+    assert s0["builds"] == s1["builds"] and s0["builds"] >= 2, (s0, s1)
+    assert s0["fallback_particle_steps"] == s1["fallback_particle_steps"]
+    assert np.array_equal(x0, x1)
+
+
+@precisions
+def test_relative_entries_c5_bitwise(prec):
+    """N > 65,536 (C5, 606,248 particles, its dense synthetic start): the default plane-relative 16-bit entries against
+    32-bit entries -- every partner within the plane span (no escape to the exact search), so bitwise the same"""
+    cfg = resolution_scaled(InterphaseConfig(), 10.0)
+    design = synthetic.make_c5()
+    ctx = {"step": 0, "time": 0.0, "core_scale": 1.0, "bond_scale": 1.0, "wall_semiaxes": LATE["wall_semiaxes"]}
+    x0, s0 = _format_run(design, cfg, prec, 0, 20, ctx=ctx)
+    x2, s2 = _format_run(design, cfg, prec, 2, 20, ctx=ctx)
+    assert s0["fallback_particle_steps"] == s2["fallback_particle_steps"], (s0, s2)
+    assert np.array_equal(x0, x2)
+
+
+@precisions
+def test_relative_entries_escape_to_exact_search(prec):
+    """A 100,000-particle rod (cross-section of two or three list cells: cell rows of ~11,000-25,000 slots) puts a
+    particle's partners in the row above up to ~22,000 slots past its plane base, beyond the 14-bit offset: those
+    lists are marked overflowed and the particles searched exactly.  Same bound vs the oracle (softcore only, 5
+    steps), and the exact searches happened.  (Lengths at a tenth of the nucleus' scale -- cutoff 0.03, rod 10 long
+    -- so coordinates stay below 10, where the fp32 bound applies; timestep scaled to move particles alike.)"""
+    n = 100000
+    rng = np.random.default_rng(7)
+    x = np.column_stack([rng.uniform(0, 10, n), rng.uniform(0, 0.13, n), rng.uniform(0, 0.13, n)])
+    sysd = {}
+    for name, cls in (("e", Engine), ("o", oracle.OracleSystem)):
+        s = cls(n, precision=prec)
+        s.add_neighbor_softcore(2.5, 0.03, 2.5, 0.024, 0.03, mix=False, scaled=False)
+        s.set_positions(x)
+        if name == "e":
+            s.set_option(A.OPT_FUSED_STEP, 3)
+            s.set_option(A.OPT_DENSE_NEIGHBORS, 0)
+        sysd[name] = s
+    for s in sysd.values():
+        s.run(5, seed=3, timestep=1e-7)
+    st = sysd["e"].list_stats()
+    assert st["active"] == 1 and st["fallback_particle_steps"] > 0, st
+    assert np.abs(sysd["e"].get_positions() - sysd["o"].get_positions()).max() <= TOL_X[prec]
