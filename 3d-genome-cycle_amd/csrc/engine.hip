@@ -60,14 +60,14 @@ struct FieldRec {
 // What a captured step sequence depends on beyond its (phase, parity, length) key: anything else that changes
 // drops every cached graph before the next capture.
 struct GraphKey {
-    int topo_version, fused, list_every, sched_flags, waves, chunk, spacestep, list_waves;
+    int topo_version, fused, list_every, sched_flags, waves, chunk, spacestep, list_waves, skin_pm;
     gcs_bd_config cfg;
 };
 bool same_key(const GraphKey& x, const GraphKey& y)
 {
     return x.topo_version == y.topo_version && x.fused == y.fused && x.list_every == y.list_every &&
            x.sched_flags == y.sched_flags && x.waves == y.waves && x.chunk == y.chunk && x.spacestep == y.spacestep &&
-           x.list_waves == y.list_waves && x.cfg.temperature == y.cfg.temperature &&
+           x.list_waves == y.list_waves && x.skin_pm == y.skin_pm && x.cfg.temperature == y.cfg.temperature &&
            x.cfg.timestep == y.cfg.timestep && x.cfg.spacestep == y.cfg.spacestep && x.cfg.seed == y.cfg.seed &&
            x.cfg.noise == y.cfg.noise;
 }
@@ -267,6 +267,7 @@ struct gcs_engine {
     int list_cap = 1024;        // GCS_OPT_LIST_CAP: list entries per particle (split over the tile's waves)
     size_t list_alloc = 0;      // allocated entries
     int list_skin_pm = 0;       // GCS_OPT_LIST_SKIN: skin in 1/1000 of the pair cutoff (0: the precision's default)
+    int skin_level_pm = 0;      // the skin (1/1000 of the pair cutoff) of the current undecomposed list run (skin_level)
     int list_every_opt = 0;     // GCS_OPT_LIST_EVERY: rebuild period in steps (0: from the noise amplitude)
     int list_every = 1;         // the period of the current run
     int list_waves = 4;         // GCS_OPT_LIST_WAVES: waves per tile (2: more tiles resident, for replica runs)
@@ -805,10 +806,43 @@ bool rebuild_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) == 
 // the list skin: the option, or the precision's default.  The fp64 step gathers 32-B partners, so shorter lists pay
 // for more frequent rebuilds sooner than at fp32 (4-replica bench sweeps: fp32 profiles/r03_skin_sweep.txt, 500 per
 // mille / 16 steps best; fp64 profiles/r04_skin_sweep_f64*.txt)
+int default_skin_pm(const gcs_engine* e) { return e->prec == 64 ? kListSkinPm64 : kListSkinPm32; }
+
 float list_skin(const gcs_engine* e)
 {
-    const int pm = e->list_skin_pm > 0 ? e->list_skin_pm : (e->prec == 64 ? kListSkinPm64 : kListSkinPm32);
+    const int pm = e->list_skin_pm > 0                  ? e->list_skin_pm
+                   : (e->skin_level_pm > 0 && !e->dom) ? e->skin_level_pm
+                                                       : default_skin_pm(e);
     return 1e-3f * (float)pm * e->fa.pf.pair_dist;
+}
+
+// The core scale the schedule gives step st (the closed form the tails evaluate, stage_interphase/
+// simulation_driver_interphase.cpp:67-76), or -1 when the host cannot know it: no scale schedule on step time, or a
+// cutoff that does not scale
+double sched_cs(const gcs_engine* e, int64_t st)
+{
+    if ((e->sched_flags & 3) != 3 || !e->fa.pair_scaled || !(e->sched.core_scale_tau > 0)) return -1.0;
+    const double t = (double)st * e->sched.timestep;
+    return 1.0 - (1.0 - e->sched.core_scale_init) * std::exp(-(t / e->sched.core_scale_tau));
+}
+
+// The list skin of step st (1/1000 of the pair cutoff at core scale 1) when GCS_OPT_LIST_SKIN is 0: the precision's
+// default s1 x sqrt(cs), rounded to 10 per mille.  The list radius is rc(cs) + skin: per step a list costs
+// ~ (rc + skin)^3, a rebuild (every M ~ kappa skin^2 steps, auto_list_every) some beta steps' worth, and at the
+// production start (cs 0.5) a skin sized for cs = 1 makes the lists (0.5 + 0.35)^3 / 0.5^3 = 4.9 x the pairs they
+// hold.  Minimising (cs + s)^3 (1 + beta / (kappa s^2)) with beta fixed by s1 being the optimum at cs = 1 gives
+// u = s / s1 = 0.76 at cs 0.5; the sweeps put the optimum lower (C5 start fp64: 250 best of 150..350, C2 start window
+// 250 > 270 > 350; profiles/r04_skin_cs.txt: the build's cost grows with the list too), which sqrt(cs) meets (0.71).
+// The scheduled core scale is a closed form of the step, so the skin changes at steps the schedule fixes (a few
+// times while cs grows; each change re-primes and rebuilds, gcs_engine_run), and a run split into chunks changes it
+// where the whole run does.
+int skin_level(const gcs_engine* e, int64_t st)
+{
+    if (e->list_skin_pm > 0) return e->list_skin_pm;
+    const int s1 = default_skin_pm(e);
+    const double cs = sched_cs(e, st);
+    if (!(cs > 0.0) || cs >= 1.0) return s1;
+    return std::max(50, (int)std::lround(s1 * std::sqrt(cs) / 10.0) * 10);
 }
 
 // the list entry format (GCS_OPT_LIST_FORMAT): absolute 16-bit slots up to 65,536 particles, plane-relative 16-bit
@@ -1215,6 +1249,7 @@ GraphKey run_key(const gcs_engine* e, const gcs_bd_config* cfg, bool spacestep)
     k.chunk = e->fa.chunk_mode;
     k.spacestep = spacestep ? 1 : 0;
     k.list_waves = e->list_waves;
+    k.skin_pm = e->skin_level_pm;
     k.cfg = *cfg;
     return k;
 }
@@ -1934,10 +1969,18 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
                                 "field, <= 256 (a, b) pair classes and < 2^24 particles (use GCS_PRECISION_F32)");
     if (!list_path(e, spacestep) || spacestep)  // (contact updates are fused into fixed-timestep list steps only)
         if ((rc = flush_contacts(e))) return rc;
+    // the list skin of the run's first step (skin_level); a change from the last run's re-primes and rebuilds
+    const int lv0 = list_path(e, spacestep) ? skin_level(e, first_step) : e->skin_level_pm;
+    const bool lv_changed = lv0 != e->skin_level_pm;
+    e->skin_level_pm = lv0;
     if ((rc = begin_run(e, cfg, first_step))) return rc;
+    if (lv_changed && list_path(e, spacestep)) {
+        launch_prime(e->stream, e->ctx, list_args(e), 0.f, e->ncell_max, e->dsched);
+        e->l_need_build = true;
+    }
 
     const int G = e->graph_steps;
-    const GraphKey key = run_key(e, cfg, spacestep);
+    GraphKey key = run_key(e, cfg, spacestep);
     int64_t done = 0;
     if (list_path(e, spacestep)) {
         // rebuilds at the steps k with (first_step + k) % M == 0 and at a run start without continuity, so a run
@@ -1945,12 +1988,22 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
         // is replayed from a graph captured once per (first step mod M, starting parity, length): a run of any
         // length, from any step, replays graphs (only the forced rebuild of a run start and a pending contact
         // update run eagerly)
-        const int M = e->list_every;
         // the host knows every step's position-buffer parity (the kernels' slot loads then need no context read);
         // a captured graph bakes its steps' parities in
         auto par = [&](int64_t k) { return e->parity ^ (int)(k & 1); };
         while (done < steps) {
             const int64_t st = first_step + done;
+            const int lv = skin_level(e, st);
+            if (lv != e->skin_level_pm) {
+                // the skin changes at this step (the core scale grew): the grid at the new list radius, a rebuild,
+                // the period for the new skin, graphs under the new key
+                e->skin_level_pm = lv;
+                e->list_every = auto_list_every(e, cfg);
+                launch_prime(e->stream, e->ctx, list_args(e), 0.f, e->ncell_max, e->dsched);
+                e->l_need_build = true;
+                key = run_key(e, cfg, spacestep);
+            }
+            const int M = e->list_every;
             const int phase = (int)(((st % M) + M) % M);
             // the contact update the host asked for after the last step: counted by this stretch's first step, its
             // distance set in the context (so the stretch's graph does not depend on it)
@@ -1971,7 +2024,12 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
                 e->rstats.eager_steps++;
                 continue;
             }
-            const int len = (int)std::min<int64_t>(G, steps - done);
+            int len = (int)std::min<int64_t>(G, steps - done);
+            for (int k = 1; k < len; ++k)  // a stretch ends where the skin changes
+                if (skin_level(e, st + k) != lv) {
+                    len = k;
+                    break;
+                }
             const int p0 = par(done);
             hipGraphExec_t x = nullptr;
             // cache slot: rebuild phase, and whether the first step counts contacts

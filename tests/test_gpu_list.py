@@ -521,3 +521,35 @@ def test_relative_entries_escape_to_exact_search(prec):
     st = sysd["e"].list_stats()
     assert st["active"] == 1 and st["fallback_particle_steps"] > 0, st
     assert np.abs(sysd["e"].get_positions() - sysd["o"].get_positions()).max() <= TOL_X[prec]
+
+
+@precisions
+def test_skin_follows_core_scale(c1_design, prec):
+    """GCS_OPT_LIST_SKIN 0: the skin follows the scheduled core scale (engine.hip skin_level: s1 sqrt(cs), 250 per mille
+    at core scale 0.5 for fp64's 350, 350 for fp32's 500), changing at steps fixed by the schedule -- each change re-primes
+    and rebuilds.  A fast core-scale schedule (0.5 -> 0.93 over 120 steps) crosses several skin levels: the run in
+    three chunks is bitwise the run in one, both within the bound of the oracle, and the skin ends larger"""
+    cfg = InterphaseConfig()
+    sched = dict(interphase.interphase_schedule(cfg), core_scale_tau=100 * cfg.timestep / 2.0)
+    ctx0 = interphase.initial_context(cfg)
+    runs = []
+    for chunks in ((120,), (37, 50, 33)):
+        e = _list_engine(c1_design, cfg, prec)
+        e.set_schedule(**sched)
+        e.set_context(ctx0)
+        e.run(1, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=21)
+        skin0 = e.list_stats()["skin"]
+        first = 1
+        for c in chunks:
+            e.run(c, first_step=first, temperature=cfg.temperature, timestep=cfg.timestep, seed=21)
+            first += c
+        runs.append((e.get_positions(), skin0, e.list_stats()))
+    (x1, skin0, st1), (x3, _, st3) = runs
+    assert skin0 == pytest.approx({64: 0.250, 32: 0.350}[prec] * cfg.a_core_diameter, rel=1e-6)
+    assert st1["skin"] > skin0 and st1["skin"] == st3["skin"] and st1["builds"] == st3["builds"], (st1, st3)
+    assert np.array_equal(x1, x3)
+    o, _ = interphase.build_interphase(oracle.OracleSystem, c1_design, cfg, precision=prec)
+    o.set_schedule(**sched)
+    o.set_context(ctx0)
+    o.run(121, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=21)
+    assert np.abs(x1 - o.get_positions()).max() <= TOL_X[prec]
