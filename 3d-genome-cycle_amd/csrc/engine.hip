@@ -277,7 +277,7 @@ struct gcs_engine {
     bool l_need_build = true;   // the next list step must rebuild (run start without continuity)
     // dense systems: mean neighbours within the cutoff above which a fresh run takes the 2-launch tile step instead
     // of the list step (GCS_OPT_DENSE_NEIGHBORS; 0: never), and the current chain's verdict
-    int dense_opt = 48;
+    int dense_opt = 96;
     bool dense = false;
     double dense_mean = -1.0;  // the last probe's mean neighbour count
     double c_pending = 0;      // a contact update fused into the next list step (its distance; 0: none)
@@ -827,12 +827,13 @@ double sched_cs(const gcs_engine* e, int64_t st)
 }
 
 // The list skin of step st (1/1000 of the pair cutoff at core scale 1) when GCS_OPT_LIST_SKIN is 0: the precision's
-// default s1 x sqrt(cs), rounded to 10 per mille.  The list radius is rc(cs) + skin: per step a list costs
-// ~ (rc + skin)^3, a rebuild (every M ~ kappa skin^2 steps, auto_list_every) some beta steps' worth, and at the
-// production start (cs 0.5) a skin sized for cs = 1 makes the lists (0.5 + 0.35)^3 / 0.5^3 = 4.9 x the pairs they
-// hold.  Minimising (cs + s)^3 (1 + beta / (kappa s^2)) with beta fixed by s1 being the optimum at cs = 1 gives
-// u = s / s1 = 0.76 at cs 0.5; the sweeps put the optimum lower (C5 start fp64: 250 best of 150..350, C2 start window
-// 250 > 270 > 350; profiles/r04_skin_cs.txt: the build's cost grows with the list too), which sqrt(cs) meets (0.71).
+// default s1 (the optimum at cs = 1) x sqrt(cs) at fp64, x cs at fp32, rounded to 10 per mille.  The list radius is
+// rc(cs) + skin: per step a list costs ~ (rc + skin)^3, a rebuild (every M ~ kappa skin^2 steps, auto_list_every) some
+// beta steps' worth, and at the production start (cs 0.5) a skin sized for cs = 1 makes the lists
+// (0.5 + 0.35)^3 / 0.5^3 = 4.9 x the pairs they hold.  Minimising (cs + s)^3 (1 + beta / (kappa s^2)) with beta
+// fixed by s1 being the optimum at cs = 1 gives u = s / s1 = 0.76 at cs 0.5; the sweeps put it lower
+// (profiles/r04_skin_cs.txt; the build's cost grows with the list too): fp64 250 of 150..350 at C5's start (u 0.71),
+// fp32 250 of 250..370 there (u 0.5; its C2 start window 370 > 500).
 // The scheduled core scale is a closed form of the step, so the skin changes at steps the schedule fixes (a few
 // times while cs grows; each change re-primes and rebuilds, gcs_engine_run), and a run split into chunks changes it
 // where the whole run does.
@@ -842,7 +843,8 @@ int skin_level(const gcs_engine* e, int64_t st)
     const int s1 = default_skin_pm(e);
     const double cs = sched_cs(e, st);
     if (!(cs > 0.0) || cs >= 1.0) return s1;
-    return std::max(50, (int)std::lround(s1 * std::sqrt(cs) / 10.0) * 10);
+    const double u = e->prec == 64 ? std::sqrt(cs) : cs;
+    return std::max(50, (int)std::lround(s1 * u / 10.0) * 10);
 }
 
 // the list entry format (GCS_OPT_LIST_FORMAT): absolute 16-bit slots up to 65,536 particles, plane-relative 16-bit

@@ -371,14 +371,14 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
 #define GCS_OPT_TILE_PRIORITY 6  /* n > 0: pair-loop wave priority min(3, tile candidates / n); 0 = off (default 700) */
 #define GCS_OPT_CONTACT_BITS 9   /* contact map: 2^bits hash slots (0 = default, >= 2 N slots sized at first update) */
 #define GCS_OPT_LIST_SKIN 10      /* list step: skin in 1/1000 of the pair cutoff (0 = default: 500 fp32, 350 fp64 at core
-                                     scale 1; x sqrt(core scale) while a schedule grows it: 350 / 250 at 0.5) */
+                                     scale 1; x core scale (fp32) / sqrt(core scale) (fp64) while a schedule grows it: 250 / 250 at 0.5) */
 #define GCS_OPT_LIST_EVERY 11     /* list step: rebuild period in steps (0 = default: from the noise amplitude) */
 #define GCS_OPT_LIST_CAP 12       /* list step: list entries per particle (default 1024; a longer list: exact search) */
 #define GCS_OPT_LIST_WAVES 13     /* list step: waves per 64-particle tile, 4 (default: lowest step latency) or 2 (more
                                      tiles resident: the better throughput when several trajectories share a GPU) */
 #define GCS_OPT_DENSE_NEIGHBORS 15 /* fp32 list step (GCS_OPT_FUSED_STEP 3): a fresh run whose mean neighbour count within the
                                      cutoff, x 2 when list entries are 32-bit (GCS_OPT_LIST_FORMAT 2), exceeds this takes the
-                                     unfused tile step instead (default 48; 0: never) */
+                                     unfused tile step instead (default 96; 0: never) */
 #define GCS_OPT_LIST_DEAL 16      /* list build: which wave segment takes each candidate chunk; -1 (default) the tuned
                                      pattern for the waves per tile, 0 round robin, else period T (1..15) << 60 | the
                                      wave (< waves per tile) of chunk p of each period in nibble p.  Only the split of

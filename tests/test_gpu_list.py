@@ -193,9 +193,9 @@ def test_list_c5_trajectory(prec):
 
 
 def test_dense_start_takes_tile_step():
-    """the default engine (GCS_OPT_DENSE_NEIGHBORS 48) probes a fresh chain's density: C5's synthetic start (64
-    neighbours within the cutoff at core scale 0.5, 32-bit entries) runs the unfused tile step, C2's start (41, 16-bit)
-    the list step; a continuing chain keeps its verdict; the tile-step trajectory matches the fp64 oracle"""
+    """a threshold of 48 (GCS_OPT_DENSE_NEIGHBORS; the default is 96) probes a fresh chain's density: C5's synthetic
+    start (64 neighbours within the cutoff at core scale 0.5) runs the unfused tile step, C2's start (41) the list
+    step; a continuing chain keeps its verdict; the tile-step trajectory matches the fp64 oracle"""
     cfg5 = resolution_scaled(InterphaseConfig(), 10.0)
     d5 = synthetic.make_c5()
     e, o = _pair(d5, cfg5, x=_f32(d5.positions), prec=32, dense_neighbors=48)
@@ -525,8 +525,8 @@ def test_relative_entries_escape_to_exact_search(prec):
 
 @precisions
 def test_skin_follows_core_scale(c1_design, prec):
-    """GCS_OPT_LIST_SKIN 0: the skin follows the scheduled core scale (engine.hip skin_level: s1 sqrt(cs), 250 per mille
-    at core scale 0.5 for fp64's 350, 350 for fp32's 500), changing at steps fixed by the schedule -- each change re-primes
+    """GCS_OPT_LIST_SKIN 0: the skin follows the scheduled core scale (engine.hip skin_level: 250 per mille at core
+    scale 0.5 for fp64's 350 (x sqrt(cs)) and for fp32's 500 (x cs)), changing at steps fixed by the schedule -- each change re-primes
     and rebuilds.  A fast core-scale schedule (0.5 -> 0.93 over 120 steps) crosses several skin levels: the run in
     three chunks is bitwise the run in one, both within the bound of the oracle, and the skin ends larger"""
     cfg = InterphaseConfig()
@@ -545,7 +545,7 @@ def test_skin_follows_core_scale(c1_design, prec):
             first += c
         runs.append((e.get_positions(), skin0, e.list_stats()))
     (x1, skin0, st1), (x3, _, st3) = runs
-    assert skin0 == pytest.approx({64: 0.250, 32: 0.350}[prec] * cfg.a_core_diameter, rel=1e-6)
+    assert skin0 == pytest.approx({64: 0.250, 32: 0.250}[prec] * cfg.a_core_diameter, rel=1e-6)
     assert st1["skin"] > skin0 and st1["skin"] == st3["skin"] and st1["builds"] == st3["builds"], (st1, st3)
     assert np.array_equal(x1, x3)
     o, _ = interphase.build_interphase(oracle.OracleSystem, c1_design, cfg, precision=prec)
