@@ -4,7 +4,8 @@
 //   gather32 / gather16 / gather2: 32 Mi random records of 32 / 16 / 2 B from a 2 GiB buffer (far beyond the L2 and the
 //   256 MB Infinity Cache: every record is its own line), the indices from a hash (no index traffic)
 //   write16: 1 GiB written, 16 B per lane
-// Every kernel folds what it reads into a value that is stored only when impossible, so no load is dropped.
+// Every kernel folds what it reads into a value stored only when it equals a constant the data never produces (but
+// the compiler cannot rule out: a 16-bit pattern, since 2-B reads fold to 16 bits), so no load is dropped.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -30,7 +31,7 @@ __global__ __launch_bounds__(256) void k_stream(const T* __restrict__ p, size_t 
             acc ^= (unsigned)v;
         }
     }
-    if (acc == 0x9e3779b9u) out[threadIdx.x] = acc;
+    if (acc == 0x1234u) out[threadIdx.x] = acc;  // (a value XOR-folded 16-bit reads can reach: the loads stay)
 }
 
 template <typename T>
@@ -46,7 +47,7 @@ __global__ __launch_bounds__(256) void k_gather(const T* __restrict__ p, size_t 
             acc ^= (unsigned)v;
         }
     }
-    if (acc == 0x9e3779b9u) out[threadIdx.x] = acc;
+    if (acc == 0x1234u) out[threadIdx.x] = acc;  // (a value XOR-folded 16-bit reads can reach: the loads stay)
 }
 
 __global__ __launch_bounds__(256) void k_write16(uint4* __restrict__ p, size_t n)
