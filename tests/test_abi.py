@@ -91,3 +91,11 @@ def test_no_cpu_fallback_without_device():
         pytest.skip("a GPU is visible")
     with pytest.raises(A.GcsError):
         Engine(10)
+
+
+def test_option_numbers_match_header():
+    """every GCS_OPT_* the header defines has the same number in the ctypes mirror (gcs._abi.OPT_*)"""
+    opts = dict((k, int(v)) for k, v in re.findall(r"^#define GCS_OPT_(\w+)\s+(\d+)", HEADER.read_text(), flags=re.M))
+    assert "LIST_FORMAT" in opts and len(opts) >= 15
+    for name, num in opts.items():
+        assert getattr(A, "OPT_" + name) == num, name
