@@ -803,10 +803,13 @@ bool list_path(const gcs_engine* e, bool spacestep)
 bool fused_path(const gcs_engine* e, bool spacestep) { return spacestep ? list_path(e, true) : eff_fused(e) != 0; }
 bool rebuild_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) == 2 && !spacestep; }
 
-// the list skin: the option, or the precision's default.  The fp64 step gathers 32-B partners, so shorter lists pay
-// for more frequent rebuilds sooner than at fp32 (4-replica bench sweeps: fp32 profiles/r03_skin_sweep.txt, 500 per
-// mille / 16 steps best; fp64 profiles/r04_skin_sweep_f64*.txt)
+// the precision's default skin at core scale 1.  The fp64 step gathers 32-B partners, so shorter lists pay for more
+// frequent rebuilds sooner than at fp32 (4-replica bench sweeps: fp32 profiles/r03_skin_sweep.txt, 500 per mille / 16
+// steps best; fp64 profiles/r04_skin_sweep_f64*.txt)
 int default_skin_pm(const gcs_engine* e) { return e->prec == 64 ? kListSkinPm64 : kListSkinPm32; }
+
+// the list skin: the option, the current undecomposed run's level (skin_level), or the default (decomposed runs:
+// their binning halo is sized from it)
 
 float list_skin(const gcs_engine* e)
 {
