@@ -227,7 +227,7 @@ struct gcs_engine {
     hipGraph_t dgraph = nullptr;
     int dg_steps = 0;
     gcs_bd_config dg_cfg{};
-    int dg_version = -1, dg_sched_flags = -1, dg_phase = -1;
+    int dg_version = -1, dg_sched_flags = -1, dg_phase = -1, dg_skin = -1;
 
     ForceArgs fa{};
     gcs_schedule sched{};
@@ -808,15 +808,17 @@ bool rebuild_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) == 
 // steps best; fp64 profiles/r04_skin_sweep_f64*.txt)
 int default_skin_pm(const gcs_engine* e) { return e->prec == 64 ? kListSkinPm64 : kListSkinPm32; }
 
-// the list skin: the option, the current undecomposed run's level (skin_level), or the default (decomposed runs:
-// their binning halo is sized from it)
-
+// the list skin: the option, the current run's level (skin_level), or the default
 float list_skin(const gcs_engine* e)
 {
-    const int pm = e->list_skin_pm > 0                  ? e->list_skin_pm
-                   : (e->skin_level_pm > 0 && !e->dom) ? e->skin_level_pm
-                                                       : default_skin_pm(e);
+    const int pm = e->list_skin_pm > 0 ? e->list_skin_pm : e->skin_level_pm > 0 ? e->skin_level_pm : default_skin_pm(e);
     return 1e-3f * (float)pm * e->fa.pf.pair_dist;
+}
+// the largest skin any level takes (the option, or the default at core scale 1): what a decomposed run's binning halo
+// is sized from, so a level change never needs a wider region
+float list_skin_max(const gcs_engine* e)
+{
+    return 1e-3f * (float)(e->list_skin_pm > 0 ? e->list_skin_pm : default_skin_pm(e)) * e->fa.pf.pair_dist;
 }
 
 // The core scale the schedule gives step st (the closed form the tails evaluate, stage_interphase/
@@ -959,12 +961,12 @@ int ensure_list(gcs_engine* e)
 // 6.17e9, 0.45 / 14 6.33e9, 0.5 / 13 6.27e9, 0.5 / 16 6.32e9, 0.5 / 18 6.1e9, 0.55 / 18 6.13e9, 0.6 / 20 5.97e9
 // (C2's largest mobility 1, dt 1e-5: (0.075 / (4.15 sigma))^2 = 16.3 -> 16; 3.95 sigma gave 18, whose fallbacks
 // reach 1.7e-3 of the particle-steps over 20,000 C2 steps)
-int auto_list_every(const gcs_engine* e, const gcs_bd_config* cfg)
+int auto_list_every(const gcs_engine* e, double temperature, double timestep)
 {
     if (e->list_every_opt > 0) return e->list_every_opt;
     double mu = 0;
     for (double m : e->mu) mu = std::max(mu, m);
-    const double sigma = std::sqrt(2.0 * std::max(cfg->temperature, 0.0) * mu * cfg->timestep);
+    const double sigma = std::sqrt(2.0 * std::max(temperature, 0.0) * mu * timestep);
     const double half = 0.5 * (double)list_skin(e);
     if (!(sigma > 0)) return 64;
     const double m = std::floor((half / (4.15 * sigma)) * (half / (4.15 * sigma)));
@@ -1170,7 +1172,7 @@ int begin_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step)
     e->chain_valid = false;
     if (list_path(e, cfg->spacestep > 0)) {
         if ((rc = ensure_list(e))) return rc;
-        e->list_every = auto_list_every(e, cfg);
+        e->list_every = auto_list_every(e, cfg->temperature, cfg->timestep);
         if (!cont) {
             launch_prime(e->stream, e->ctx, list_args(e), 0.f, e->ncell_max, e->dsched);
             e->l_need_build = true;
@@ -2003,7 +2005,7 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
                 // the skin changes at this step (the core scale grew): the grid at the new list radius, a rebuild,
                 // the period for the new skin, graphs under the new key
                 e->skin_level_pm = lv;
-                e->list_every = auto_list_every(e, cfg);
+                e->list_every = auto_list_every(e, cfg->temperature, cfg->timestep);
                 launch_prime(e->stream, e->ctx, list_args(e), 0.f, e->ncell_max, e->dsched);
                 e->l_need_build = true;
                 key = run_key(e, cfg, spacestep);
@@ -2473,7 +2475,7 @@ bool dom_list_ok(const gcs_engine* e);
 float dom_bin_halo(const gcs_engine* e)
 {
     if (!dom_list_ok(e)) return e->dom_halo;
-    return std::min(e->dom_halo, e->fa.pf.pair_dist + 2.f * list_skin(e));
+    return std::min(e->dom_halo, e->fa.pf.pair_dist + 2.f * list_skin_max(e));
 }
 
 ForceArgs domain_args(const gcs_engine* e, double* red = nullptr)
@@ -2500,7 +2502,7 @@ DomBox dom_region(const gcs_engine* e) { return region_of(e->dom_box, dom_bin_ha
 // (cutoff + skin at cs = 1; the tail checks cutoff + largest displacement every step, kDomFlagMotion)
 bool dom_list_ok(const gcs_engine* e)
 {
-    return list_path(e, false) && e->fa.has_pair && e->dom_halo >= e->fa.pf.pair_dist + list_skin(e);
+    return list_path(e, false) && e->fa.has_pair && e->dom_halo >= e->fa.pf.pair_dist + list_skin_max(e);
 }
 
 // the list-step half of a decomposed step before the allreduce: on a rebuild step the cells of this domain's region
@@ -2508,6 +2510,16 @@ bool dom_list_ok(const gcs_engine* e)
 // particles' new positions into red
 void enqueue_dom_list_step(gcs_engine* e, int64_t st, double* red, bool fused_pack = false)
 {
+    const int lv = skin_level(e, st);
+    if (lv != e->skin_level_pm) {
+        // the skin changes at this step (skin_level): the grid at the new list radius over this domain's local box
+        // (padded by the binning halo, sized for the largest skin), a rebuild, the period for the new skin.  Never
+        // inside a capture: gcs_engine_domain_run runs a stretch with a change eagerly
+        e->skin_level_pm = lv;
+        e->list_every = auto_list_every(e, e->fa.pd.temperature, e->fa.pd.timestep);
+        launch_dom_grid(e->stream, e->ctx, domain_args(e, red));
+        e->l_need_build = true;
+    }
     ForceArgs a = domain_args(e, red);
     if (fused_pack) {  // the engine's bands (header rows zeroed by the last unpack) and reduction buffer
         a.dom_bands = e->dom_send;
@@ -2809,15 +2821,19 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
         k = k0 = 1;  // gcs_engine_domain_finish flipped the host parity of this step
     }
     // the rest: G-step chunks captured once into a graph (kernels and collectives), the remainder eagerly.  The list
-    // step rebuilds at steps = 0 (mod M): its chunks are whole periods, captured for the rebuild phase they start at
+    // step rebuilds at steps = 0 (mod M): its chunks are whole periods, captured for the rebuild phase they start at.
+    // A run whose steps change the list skin (skin_level; a few times while the core scale grows) runs eagerly
+    bool skin_change = false;
+    if (e->dom_list)
+        for (int64_t q = k; q < steps && !skin_change; ++q) skin_change = skin_level(e, first_step + q) != e->skin_level_pm;
     const int M = e->dom_list ? e->list_every : 1;
-    const int G = e->graph_steps > 0 ? (e->graph_steps + M - 1) / M * M : 0;
+    const int G = e->graph_steps > 0 && !skin_change ? (e->graph_steps + M - 1) / M * M : 0;
     const int phase = e->dom_list ? (int)((first_step + k) % M) : 0;
     if (G > 0 && steps - k >= G) {
         // (geometry, buffers, communicator and options drop the graph when they change: drop_domain_graph)
         const bool same = e->dgexec && e->dg_steps == G && std::memcmp(&e->dg_cfg, cfg, sizeof(*cfg)) == 0 &&
                           e->dg_version == e->topo_version && e->dg_sched_flags == e->sched_flags &&
-                          e->dg_phase == phase;
+                          e->dg_phase == phase && e->dg_skin == e->skin_level_pm;
         if (!same) {
             drop_domain_graph(e);
             HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
@@ -2836,6 +2852,7 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
             e->dg_version = e->topo_version;
             e->dg_sched_flags = e->sched_flags;
             e->dg_phase = phase;
+            e->dg_skin = e->skin_level_pm;
             e->rstats.graphs_captured++;
         }
         for (; steps - k >= G; k += G) {

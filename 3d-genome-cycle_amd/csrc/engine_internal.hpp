@@ -454,6 +454,9 @@ void launch_list_relax(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force
 void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2, double d2_64);
 // the decomposed list step's tail from the allreduced buffer glob (one workgroup), then the shared particles'
 // positions into both buffers (by index and by slot) and the send bands' header rows zeroed
+// a decomposed list run's cell grid at the current list radius over the domain's local box padded by the binning
+// halo (the skin changed: engine.hip enqueue_dom_list_step)
+void launch_dom_grid(hipStream_t s, DevCtx* ctx, const ForceArgs& a);
 void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const double* glob, int flags,
                              const int* shared, int nshared, void* bands, int npeer, int band_stride);
 int list_step_grid(int n);

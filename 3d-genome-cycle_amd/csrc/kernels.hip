@@ -3590,6 +3590,19 @@ __global__ __launch_bounds__(kLUpdateBlock) void k_lupdate(DevCtx* __restrict__ 
 // particle owned by some domain's lists (kDomFlagLost), cutoff + largest displacement within the halo
 // (kDomFlagMotion).  Then the shared particles' allreduced positions into both buffers, by index and by slot, and the
 // send bands' header rows zeroed for the pack.
+// the grid k_ldom_tail computes before a rebuild (ctx->bbox: this domain's owned box at its last bounding-box step,
+// padded by the binning halo; any box is exact, particles outside it are clamped into the border cells), for a
+// skin that changed since
+__global__ void k_dom_grid(DevCtx* __restrict__ ctx, ForceArgs a)
+{
+    float bb[6];
+    for (int k = 0; k < 3; ++k) {
+        bb[k] = ctx->bbox_lo[k] - a.dom_bin_halo;
+        bb[3 + k] = ctx->bbox_hi[k] + a.dom_bin_halo;
+    }
+    ctx->grid = make_grid(bb, bb + 3, pair_cutoff(a, ctx->cs) + a.list_skin, a.ncell_max, kPairFx);
+}
+
 template <typename R>
 __global__ __launch_bounds__(64) void k_ldom_tail(DevCtx* __restrict__ ctx, ForceArgs a, const double* __restrict__ glob,
                                                   int flags, const int* __restrict__ shared, int nshared,
@@ -4050,6 +4063,11 @@ static void launch_list_relax_r(hipStream_t s, DevCtx* ctx, const ForceArgs& a, 
     hipLaunchKernelGGL(k_lupdate<R>, dim3((a.n + kLUpdateBlock - 1) / kLUpdateBlock), dim3(kLUpdateBlock), 0, s, ctx, a,
                        update_flags);
 }
+void launch_dom_grid(hipStream_t s, DevCtx* ctx, const ForceArgs& a)
+{
+    hipLaunchKernelGGL(k_dom_grid, dim3(1), dim3(1), 0, s, ctx, a);
+}
+
 void launch_list_relax(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force_flags, int update_flags)
 {
     if (a.prec == 64)

@@ -247,3 +247,40 @@ def test_engine_domains_processes_host_staged(tmp_path, config, world, prec):
     single.run(steps, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     assert np.abs(x - single.get_positions()).max() <= X[prec]
     assert np.allclose(ctx["wall_semiaxes"], single.get_context()["wall_semiaxes"], rtol=WALL_REL[prec], atol=0)
+
+
+@pytest.mark.parametrize("prec", [64, 32])
+def test_decomposed_skin_follows_core_scale(c1_design, prec):
+    """the decomposed list step's skin follows the scheduled core scale as the single engine's does (engine.hip
+    enqueue_dom_list_step: a re-gridded rebuild at each level change; gcs_engine_domain_run runs a stretch with a
+    change eagerly).  A fast core-scale schedule crosses several levels in 70 steps: the one-rank RCCL run in two
+    calls equals the host-driven sequence bit for bit, both within the precision's bound of the single engine, flags
+    clear"""
+    from gcs.engine import rccl_unique_id
+    cfg = InterphaseConfig()
+    sched = dict(interphase.interphase_schedule(cfg), core_scale_tau=100 * cfg.timestep / 2.0)
+    halo = domain.domain_halo(cfg)
+    slabs = domain.plan_slabs(c1_design.positions[:, 2], 1)
+    sh = domain.shared_particles(c1_design)
+
+    def eng():
+        e = _engine(c1_design, cfg, None, prec)
+        e.set_schedule(**sched)
+        return e
+
+    ref = domain.EngineDomain(eng(), 0, slabs, halo, shared=sh)
+    run = domain.DecomposedRun([ref], domain.LocalTransport([ref]))
+    run.run(70, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    run.check()
+    d = domain.EngineDomain(eng(), 0, slabs, halo, shared=sh)
+    d.e.domain_rccl(rccl_unique_id(), 1, 0, [])
+    d.e.domain_run(30, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    d.e.domain_run(40, first_step=30, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    assert d.flag_bits() == 0
+    xd, skin = d.positions(), d.e.list_stats()["skin"]
+    d.e.close()
+    assert np.array_equal(xd, ref.positions())
+    assert skin > 0.25 * cfg.a_core_diameter * (1 + 1e-6)  # the skin grew with the core scale
+    single = eng()
+    single.run(70, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+    assert np.abs(single.get_positions() - xd).max() <= X[prec]
