@@ -67,7 +67,8 @@ extern "C" {
 
 /* 2: gcs_run_stats gained fused_contact_steps (an out-struct grew: callers built against 1 must rebuild)
  * 3: gcs_system_desc.reserved became .precision (0 = fp64); gcs_run_stats lost the small-path counters and
- *    gained density_probes; gcs_list_stats gained deal; GCS_OPT_SMALL_PATH and GCS_OPT_FUSED_STEP 1 are gone */
+ *    gained density_probes; gcs_list_stats gained deal; GCS_OPT_SMALL_PATH and GCS_OPT_FUSED_STEP 1 are gone;
+ *    later in 3 (additive, no layout change): GCS_OPT_LIST_FORMAT; the default list skin follows the core scale */
 #define GCS_ABI_VERSION 3
 
 /* arithmetic precision of an engine (gcs_system_desc.precision) */
