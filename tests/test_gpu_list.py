@@ -335,6 +335,49 @@ def test_c2_long_horizon_list_vs_rebuild_step():
     assert (s3[:3] > 0).all() and (s2[:3] > 0).all()
 
 
+def test_c2_production_start_list_vs_rebuild_step():
+    """The production start (C2 synthetic design, step 0, core scale 0.5 growing to ~0.67 over the window): 20,000
+    steps per trajectory, 6 seeds, fp32, through the list step -- whose skin follows the core scale, changing level
+    ~4 times (engine.hip skin_level: a re-primed grid and a rebuild at each change) -- and through the rebuild step (no
+    lists): the time-averaged <|r_i,i+1|>, Rg, E/N and wall semiaxes agree within 3.5 standard errors of the difference
+    of the seed means, every state stays finite, fallbacks stay rare"""
+    design, cfg = synthetic.make_c2(), InterphaseConfig()
+    nseed, steps, every, skip = 6, 20000, 2000, 4000
+    res = {3: [], 2: []}
+    skins = []
+    for fused in res:
+        for k in range(nseed):
+            s, _ = interphase.build_interphase(Engine, design, cfg, precision=32)
+            s.set_schedule(**interphase.interphase_schedule(cfg))
+            s.set_option(A.OPT_FUSED_STEP, fused)
+            s.set_option(A.OPT_DENSE_NEIGHBORS, 0)
+            s.set_context(interphase.initial_context(cfg))
+            samples, done = [], 0
+            while done < steps:
+                s.run(every, first_step=done, temperature=cfg.temperature, timestep=cfg.timestep,
+                      seed=8000 + 10 * k + fused)
+                done += every
+                if fused == 3 and done == every:
+                    skins.append(s.list_stats()["skin"])
+                if done > skip:
+                    samples.append(_c2_observables(s, design))
+            assert np.isfinite(s.get_positions()).all()
+            if fused == 3:
+                st = s.list_stats()
+                assert st["active"] == 1
+                assert st["skin"] > skins[-1], (st, skins[-1])  # the skin grew with the core scale
+                assert st["fallback_particle_steps"] < 1e-3 * design.n * steps, st
+            res[fused].append(np.mean(samples, axis=0))
+            s.close()
+    m3, m2 = np.mean(res[3], axis=0), np.mean(res[2], axis=0)
+    s3 = np.std(res[3], axis=0, ddof=1) / np.sqrt(nseed)
+    s2 = np.std(res[2], axis=0, ddof=1) / np.sqrt(nseed)
+    zs = np.abs(m3 - m2) / np.sqrt(s3 ** 2 + s2 ** 2 + 1e-30)
+    names = ["bond", "rg", "energy_per_bead", "wall_x", "wall_y", "wall_z"]
+    print({n: (float(a), float(b), float(c)) for n, a, b, c in zip(names, m3, m2, zs)})
+    assert (zs <= 3.5).all(), dict(zip(names, zs.tolist()))
+
+
 @precisions
 def test_second_neighbour_harmonic_nonzero_k(c1_design, prec):
     """setup_loop_forcefield (simulation_driver_forcefield.cpp:100-136) with K != 0: the (i, i+2) harmonic bonds are
