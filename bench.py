@@ -378,6 +378,14 @@ def c5_leg(local, seed, steps, precision=64, log=sys.stderr):
         e.run(steps, first_step=64, **bd)
         e.synchronize()
         out[name] = d.n * steps / (time.perf_counter() - t0)
+        if name == "default":
+            # the same trajectory over the next 8 x `steps` steps: past the synthetic start's densest stretch (the
+            # particles spread, the core scale grows), closer to what a production run sees on average
+            t0 = time.perf_counter()
+            e.run(8 * steps, first_step=64 + steps, **bd)
+            e.synchronize()
+            out["default_long"] = d.n * 8 * steps / (time.perf_counter() - t0)
+            out["default_long_window"] = f"steps {64 + steps}..{64 + 9 * steps}"
         if name.endswith("default"):
             # the engine's density verdict (fp32, GCS_OPT_DENSE_NEIGHBORS): list step, or the unfused tile step when
             # dense; the fp64 engine runs the list step
