@@ -256,6 +256,7 @@ struct gcs_engine {
     int* list = nullptr;
     int* lcount = nullptr;
     int4* lbase = nullptr;
+    int* ltile = nullptr;  // ListTile16 tile table (ForceArgs::ltile)
     float4* psort[2] = {nullptr, nullptr};
     float4* skmu = nullptr;  // list step: slot-ordered kmu and bond CSR rows
     int2* sbrow = nullptr;
@@ -271,7 +272,8 @@ struct gcs_engine {
     int list_every_opt = 0;     // GCS_OPT_LIST_EVERY: rebuild period in steps (0: from the noise amplitude)
     int list_every = 1;         // the period of the current run
     int list_waves = 4;         // GCS_OPT_LIST_WAVES: waves per tile (2: more tiles resident, for replica runs)
-    int list_fmt_opt = 0;       // GCS_OPT_LIST_FORMAT: 0 auto, 1 plane-relative 16-bit, 2 absolute 32-bit
+    int list_fmt_opt = 0;       // GCS_OPT_LIST_FORMAT: 0 tile-staged 16-bit (default), 1 plane-relative 16-bit, 2 absolute
+                                // 32-bit, 3 the slot entries of round 4 (absolute 16-bit up to 65,536, plane-relative beyond)
     long long list_deal_opt = -1;  // GCS_OPT_LIST_DEAL: chunk -> wave pattern of the list build (-1: the default for
                                    // list_waves, 0: round robin)
     bool l_need_build = true;   // the next list step must rebuild (run start without continuity)
@@ -788,7 +790,7 @@ bool dense_switch(const gcs_engine* e) { return e->dense && !e->dom && e->prec !
 // rebuild step (2) when the system does not admit lists, and hands a dense chain to the unfused tile step (0)
 int eff_fused(const gcs_engine* e)
 {
-    if (e->prec == 64) return 3;  // the fp64 engine has the list step only (run() checks that the system admits it)
+    if (e->prec == 64) return 3;  // the fp64 engine: the list step, or (list_ok false) its cell-list step
     if (e->fused != 3) return e->fused;
     if (!e->list_ok) return 2;
     return dense_switch(e) ? 0 : 3;
@@ -852,14 +854,19 @@ int skin_level(const gcs_engine* e, int64_t st)
     return std::max(50, (int)std::lround(s1 * u / 10.0) * 10);
 }
 
-// the list entry format (GCS_OPT_LIST_FORMAT): absolute 16-bit slots up to 65,536 particles, plane-relative 16-bit
-// slots beyond (kernels.hip ListRel16), or the form the option names
+// the list entry format (GCS_OPT_LIST_FORMAT): 16-bit indices into the step tile's LDS image of its partner rows
+// (kernels.hip ListTile16, the default), or the slot entries the option names: absolute 16-bit slots up to 65,536
+// particles and plane-relative 16-bit slots beyond (ListRel16), or absolute 32-bit slots.  Every format holds the
+// same pairs in the same order: the trajectories are bitwise the same
 int list_format(const gcs_engine* e)
 {
     if (e->list_fmt_opt == 2) return kListFmtInt;
     if (e->list_fmt_opt == 1) return kListFmtRel16;
-    return e->n <= 65536 ? kListFmtAbs16 : kListFmtRel16;
+    if (e->list_fmt_opt == 3 || e->ntypes > kTileTypes) return e->n <= 65536 ? kListFmtAbs16 : kListFmtRel16;
+    return kListFmtTile16;  // (its LDS class table holds kTileTypes classes)
 }
+// window-table entries: one per step workgroup (64 slots)
+size_t ltile_entries(const gcs_engine* e) { return (size_t)force_blocks(e->n); }
 
 // the list build's chunk deal (kernels.hip deal_nth): the option, or the default for the waves per tile
 unsigned long long list_deal(const gcs_engine* e)
@@ -905,6 +912,10 @@ ForceArgs list_args(const gcs_engine* e)
     a.list_waves = e->list_waves;
     a.list_fmt = list_format(e);
     a.lbase = e->lbase;
+    a.ltile = e->ltile;
+    // the non-temporal hint beyond 16-bit absolute lists that the L2s keep (kernels.hip k_lstep)
+    a.list_nt = (a.list_fmt == kListFmtRel16 || a.list_fmt == kListFmtInt || (a.list_fmt == kListFmtTile16 && e->n > 65536))
+                    ? 1 : 0;
     a.list_deal = list_deal(e);
     a.par_hint = -1;
     return a;
@@ -918,6 +929,7 @@ int ensure_list(gcs_engine* e)
     dfree(e->list);
     dfree(e->lcount);
     dfree(e->lbase);
+    dfree(e->ltile);
     dfree(e->psort[0]);
     dfree(e->psort[1]);
     dfree(e->skmu);
@@ -928,7 +940,8 @@ int ensure_list(gcs_engine* e)
     e->list_alloc = 0;
     int rc;
     if ((rc = dalloc(&e->list, need)) || (rc = dalloc(&e->lcount, stride * kMaxListWaves)) ||
-        (rc = dalloc(&e->lbase, stride)) || (rc = dalloc(&e->sbrow, stride)))
+        (rc = dalloc(&e->lbase, stride)) || (rc = dalloc(&e->sbrow, stride)) ||
+        (rc = dalloc(&e->ltile, ltile_entries(e) * kListTileWords)))
         return rc;
     if (e->prec == 64) {  // the slot-ordered copies in the engine's precision only
         if ((rc = dalloc(&e->dpsort[0], stride)) || (rc = dalloc(&e->dpsort[1], stride)) || (rc = dalloc(&e->dskmu, stride)))
@@ -1025,8 +1038,9 @@ int step_grid(const gcs_engine* e) { return e->fa.split ? force_grid_split(e->n)
 void enqueue_step(gcs_engine* e, bool spacestep, double spacestep_v, double timestep)
 {
     if (e->prec == 64) {
-        // fp64 (the spacestep relaxation step; fixed-timestep runs take the list step): cells, the fp64 force pass,
-        // its reduction (reactions, max drift -> the adapted dt), the update, the tail with those reactions
+        // fp64 without the list step (spacestep relaxation off the lists; any run of a system the list step does not
+        // admit: no pair field, > 256 pair classes): cells, the fp64 force pass, its reduction (reactions, max drift
+        // -> the adapted dt; spacestep 0: the fixed timestep), the update, the tail with those reactions
         enqueue_cells(e);
         launch_eval64(e->stream, kModeForce, e->ctx, e->fa);
         launch_red64(e->stream, e->ctx, e->fa, spacestep ? spacestep_v : 0.0, timestep, e->dred);
@@ -1558,6 +1572,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->list);
     dfree(e->lcount);
     dfree(e->lbase);
+    dfree(e->ltile);
     dfree(e->psort[0]);
     dfree(e->psort[1]);
     dfree(e->skmu);
@@ -1971,9 +1986,8 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
     const bool spacestep = cfg->spacestep > 0;
     int rc = choose_shape(e, cfg, first_step);
     if (rc) return rc;
-    if (e->prec == 64 && !spacestep && !e->list_ok)
-        return fail(GCS_ESTATE, "the fp64 engine's fixed-timestep step is the list step: it needs a neighbor soft-core "
-                                "field, <= 256 (a, b) pair classes and < 2^24 particles (use GCS_PRECISION_F32)");
+    // (the fp64 engine's fixed-timestep step is the list step when the system admits it -- a neighbor soft-core field,
+    // <= 256 (a, b) pair classes, < 2^24 particles -- and otherwise its cell-list step: enqueue_step, prec 64)
     if (!list_path(e, spacestep) || spacestep)  // (contact updates are fused into fixed-timestep list steps only)
         if ((rc = flush_contacts(e))) return rc;
     // the list skin of the run's first step (skin_level); a change from the last run's re-primes and rebuilds
@@ -3219,8 +3233,9 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         return GCS_OK;
     }
     if (option == GCS_OPT_LIST_FORMAT) {
-        if (value != 0 && value != 1 && value != 2)
-            return fail(GCS_EINVAL, "list format must be 0 (default), 1 (plane-relative 16-bit) or 2 (32-bit)");
+        if (value < 0 || value > 3)
+            return fail(GCS_EINVAL, "list format must be 0 (tile-staged, default), 1 (plane-relative 16-bit), 2 (32-bit) or "
+                                    "3 (16-bit slots: absolute up to 65,536 particles, plane-relative beyond)");
         e->list_fmt_opt = (int)value;
         e->l_need_build = true;
         drop_graph(e);

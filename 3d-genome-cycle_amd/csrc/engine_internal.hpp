@@ -297,7 +297,11 @@ struct ForceArgs {
     int list_stride;        // >= N
     float list_skin;        // > 0 only in the list path's own argument block
     int list_waves;         // waves per tile (list segments): 4, or 2 (GCS_OPT_LIST_WAVES)
-    int list_fmt;           // list entries: kListFmtAbs16 / kListFmtInt / kListFmtRel16 (list_format)
+    int list_fmt;           // list entries: kListFmtTile16 / kListFmtAbs16 / kListFmtInt / kListFmtRel16 (list_format)
+    int list_nt;            // read the list words with the non-temporal hint (lists far beyond the L2s)
+    // kListFmtTile16 (kernels.hip ListTile16): per step window (64 slots) kListTileWords ints written by the build,
+    // the staged rows of its (up to two) row parts (layout: kernels.hip stage_slot)
+    int* ltile;
     unsigned long long list_deal;  // list build: candidate chunk -> wave segment pattern (GCS_OPT_LIST_DEAL; 0: round robin)
     int par_hint;           // >= 0: ctx->parity of this launch, known to the host at enqueue (the slot loads need not
                             // wait for the context); -1: read it
@@ -387,6 +391,10 @@ constexpr int kListIndexBits = 24;      // particle index bits of a list entry
 constexpr int kListFmtAbs16 = 0;
 constexpr int kListFmtInt = 1;
 constexpr int kListFmtRel16 = 2;
+// 16-bit indices into the step tile's LDS image of its partners (kernels.hip ListTile16: the default at any size)
+constexpr int kListFmtTile16 = 3;
+constexpr int kListTileWords = 64;  // ints per window-table entry (kernels.hip stage_slot: 38 used)
+constexpr int kTileTypes = 64;      // pair-factor classes of the ListTile16 step (its LDS class table; more: slot entries)
 constexpr int kListCountMask = (1 << 30) - 1;
 constexpr int kListOverflow = 1 << 30;
 
@@ -459,7 +467,7 @@ void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2, double d2_64);
 void launch_dom_grid(hipStream_t s, DevCtx* ctx, const ForceArgs& a);
 void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const double* glob, int flags,
                              const int* shared, int nshared, void* bands, int npeer, int band_stride);
-int list_step_grid(int n);
+int list_step_grid(const ForceArgs& a);
 void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceArgs& a, bool fused);
 // fp64 force / energy evaluation on the current cell list (one thread per sorted slot; kernels.hip k_eval64):
 // kModeForce -> a.dforce_out + partial rows a.dpart [blocks][8] (reactions in[3], out[3], max mu|F|, neighbours),

@@ -1777,14 +1777,67 @@ __device__ __forceinline__ size_t list_at(int w, int cap, int k, int s, size_t s
 struct ListRel16 {
     unsigned short v;
 };
+// ListTile16 (kListFmtTile16, the default): 16-bit indices into the step tile's LDS image of its partner rows.  The
+// list build and the step share their tiles (<= 64 consecutive slots of one cell row, k_cell_scan's tile table); a
+// tile's partners lie in 9 stencil rows, each a contiguous slot range [cell (x_first - fx), cell (x_last + fx)] of
+// rows y - 1 .. y + 1 in planes z - 1 .. z + 1 at the build.  The build concatenates those ranges (the staged rows,
+// kStageRow order: the tile's own row first, corner rows last) and an entry is the partner's position in that
+// concatenation; the step copies the ranges' CURRENT positions into LDS with LDS-DMA (coalesced rows), so a list entry
+// costs an LDS read instead of an L2/HBM gather.  Slots are fixed between builds, so the same index holds across the
+// period.  Entries beyond the LDS image (tiles whose staged rows exceed kStageBytes) are gathered from global memory
+// through the same row table.  The entry order, hence every sum, is that of the slot formats: bitwise the same.
+struct ListTile16 {
+    unsigned short v;
+};
 template <typename LE>
 struct ListFmt {
     static constexpr bool rel = false;
+    static constexpr bool tile = false;
 };
 template <>
 struct ListFmt<ListRel16> {
     static constexpr bool rel = true;
+    static constexpr bool tile = false;
 };
+template <>
+struct ListFmt<ListTile16> {
+    static constexpr bool rel = false;
+    static constexpr bool tile = true;
+};
+// the staged rows in order: stencil row q = (dz + 1) * 3 + (dy + 1) of staged position k (the tile's own row first,
+// then the 4 edge-adjacent rows, the corner rows last: what an LDS image too small for all 9 keeps is the rows
+// holding most partners)
+__device__ __forceinline__ int stage_row(int k)
+{
+    return (int)((0x862075314ull >> (4 * k)) & 15ull);  // k = 0..8: rows 4, 1, 3, 5, 7, 0, 2, 6, 8
+}
+// A window's table entry (ForceArgs::ltile, kListTileWords ints): part p (0, 1) of the window has staged rows k = 0..8
+// whose first slot is t[18 p + k] and first staged index t[18 p + 9 + k] (non-decreasing over p, k); t[36] = part 1's
+// first index (= part 0's staged total), t[37] = the total.  The slot of staged index v < t[37]: the last row of its
+// part starting at or before v.  From the LDS copy of the entry:
+__device__ __forceinline__ int stage_slot(int v, const int* t)
+{
+    const int b = v >= t[36] ? 18 : 0;
+    int d = t[b] - t[b + 9];
+#pragma unroll
+    for (int k = 1; k < 9; ++k) d = (v >= t[b + 9 + k]) ? t[b + k] - t[b + 9 + k] : d;
+    return v + d;
+}
+// ... and from the entry held one int per lane (tw = t[lane], wave-uniform reads)
+__device__ __forceinline__ int stage_slot_w(int v, int tw)
+{
+    const bool p1 = v >= __builtin_amdgcn_readlane(tw, 36);
+    int d = p1 ? __builtin_amdgcn_readlane(tw, 18) - __builtin_amdgcn_readlane(tw, 27)
+               : __builtin_amdgcn_readlane(tw, 0) - __builtin_amdgcn_readlane(tw, 9);
+#pragma unroll
+    for (int k = 1; k < 9; ++k) {
+        const int v0 = __builtin_amdgcn_readlane(tw, 9 + k), v1 = __builtin_amdgcn_readlane(tw, 27 + k);
+        const int j0 = __builtin_amdgcn_readlane(tw, k), j1 = __builtin_amdgcn_readlane(tw, 18 + k);
+        const int th = p1 ? v1 : v0;
+        if (v >= th) d = p1 ? j1 - v1 : j0 - v0;
+    }
+    return v + d;
+}
 constexpr int kRelBits = 14;
 // the partner slot of a list entry (x: its raw bits)
 template <typename LE>
@@ -1839,7 +1892,7 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                                        int s_begin, int s_end, float4 pi, float bi, float& fx, float& fy, float& fz,
                                        float& acc, int* s_rowV, int* s_rowJ, float4* s_cand, int* s_candj, int& ntot,
                                        int wv, int nwv, int self = -1, bool lvalid = false, int* lcnt = nullptr,
-                                       unsigned long long* lpend = nullptr, int4* plb = nullptr)
+                                       unsigned long long* lpend = nullptr, int4* plb = nullptr, int* s_tile = nullptr)
 {
     // kModeList: phase 2 appends each hit (other than the particle itself) to the lane's list segment wv
     // instead of evaluating the pair force (the lists of the list step, built at the grid's rc = cutoff + skin)
@@ -1891,6 +1944,54 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 b[p] = (z >= 0 && z < nz) ? a.cstart[(z * ny + yb) * nx + xb] : 0;
             }
             *plb = make_int4(b[0], b[1], b[2], 0);
+        }
+        if constexpr (MODE == kModeList && ListFmt<LE>::tile) {
+            // the staged rows of the step windows this tile meets (ListTile16; windows of 64 slots, each in up to
+            // two row parts): lane wi * 32 + p * 16 + k, k < 9, takes staged row k (stencil row stage_row(k)) of part
+            // p of window (s_begin >> 6) + wi.  Outputs: the window's table entry (ltile, wave 0; identical from every
+            // workgroup that meets the window), s_tile[(2 wi + p) * 9 + q] = staged index - slot of stencil row q,
+            // s_tile[36 + 2 wi + p] = the end slot of part p
+            const int wA = s_begin >> 6, wi = lane >> 5, p = (lane >> 4) & 1, k = lane & 15;
+            const int w = wA + wi;
+            const int nsl = a.cstart[g.ncell];  // binned slots
+            const int wb = w * kTile, we = min(wb + kTile, nsl);
+            int tl = 0, tj = 0, pend = wb;
+            const bool wok = w <= ((s_end - 1) >> 6) && wb < we;
+            if (wok) {
+                const int r0 = a.scell[wb] / nx;
+                const int p0e = min(we, a.cstart[(r0 + 1) * nx]);
+                int first = wb, last = p0e - 1, r = r0;
+                pend = p0e;
+                if (p == 1) {
+                    first = p0e;
+                    r = first < we ? a.scell[first] / nx : r0;
+                    pend = first < we ? min(we, a.cstart[(r + 1) * nx]) : p0e;
+                    last = pend - 1;
+                }
+                if (k < 9 && first <= last) {
+                    const int q = stage_row(k);
+                    const int x0 = a.scell[first] % nx, x1 = a.scell[last] % nx;
+                    const int xlo = max(x0 - gfx, 0), xhi = min(x1 + gfx, nx - 1);
+                    const int y = r % ny + q % 3 - 1, z = r / ny + q / 3 - 1;
+                    if (y >= 0 && y < ny && z >= 0 && z < nz) {
+                        const int base = (z * ny + y) * nx;
+                        tj = a.cstart[base + xlo];
+                        tl = a.cstart[base + xhi + 1] - tj;
+                    }
+                }
+            }
+            int tincl = tl;
+            GCS_DPP_SCAN(dpp_i, add_i, 0, tincl)
+            const int wbase = __shfl(tincl, 31);
+            const int tv = tincl - tl - (wi ? wbase : 0);  // first staged index of the row within its window
+            if (k < 9) s_tile[(2 * wi + p) * 9 + stage_row(k)] = tv - tj;
+            if (k == 0) s_tile[36 + 2 * wi + p] = pend;
+            if (wv == 0 && wok && k < 9) {
+                int* const t = a.ltile + (size_t)w * kListTileWords;
+                t[18 * p + k] = tj;
+                t[18 * p + 9 + k] = tv;
+                if (k == 8) t[36 + p] = tv + tl;  // [36] part 0's end = part 1's first index, [37] the total
+            }
         }
         int incl = len;
         GCS_DPP_SCAN(dpp_i, add_i, 0, incl)
@@ -1945,7 +2046,8 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 for (int step = 8; step > 0; step >>= 1)
                     if (rowV[lo + step] <= v) lo += step;
                 nj[f] = rowJ[lo] + (v - rowV[lo]);
-                npl[f] = lo / 3;  // the stencil row's z plane (rows q = 0..8: z = z0 + q / 3 - 1)
+                // ListRel16: the stencil row's z plane (rows q = 0..8: z = z0 + q / 3 - 1); ListTile16: the row
+                npl[f] = ListFmt<LE>::tile ? lo : lo / 3;
                 np[f] = a.spos[nj[f]];
                 nb[f] = a.sb[nj[f]];
             }
@@ -1969,7 +2071,7 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 P[h8 + 6] = fmaf(pz, pz, fmaf(py, py, px * px));
                 // the partner's slot (< 2^24) and, for ListRel16, its plane in bits 28..29
                 reinterpret_cast<int*>(my_cand)[4 * kSub + i] =
-                    real ? (ListFmt<LE>::rel ? (nj[f] | (npl[f] << 28)) : nj[f]) : -1;
+                    real ? ((ListFmt<LE>::rel || ListFmt<LE>::tile) ? (nj[f] | (npl[f] << 28)) : nj[f]) : -1;
                 continue;
             }
             my_cand[2 * i] = make_float4(-2.f * px, -2.f * py, -2.f * pz, fmaf(pz, pz, fmaf(py, py, px * px)));
@@ -2042,6 +2144,13 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
             constexpr int E = 8 / (int)sizeof(LE);
             constexpr int EB = 8 * (int)sizeof(LE);  // bits per entry
             unsigned long long* const lw = reinterpret_cast<unsigned long long*>(a.list);
+            // ListTile16: the lane's window part -> its row of s_tile (-1: a third row part of the window, which
+            // has no staged rows: the lane's list is marked overflowed, the step searches it exactly)
+            int tpart = -1;
+            if constexpr (ListFmt<LE>::tile) {
+                const int wi = (s >> 6) != (s_begin >> 6) ? 1 : 0;
+                tpart = s < s_tile[36 + 2 * wi] ? 2 * wi : s < s_tile[37 + 2 * wi] ? 2 * wi + 1 : -1;
+            }
             for (int t = 0; t < mh; ++t) {
                 unsigned b;
                 asm("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(m));
@@ -2054,7 +2163,11 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                         const int kk = *lcnt;
                         unsigned code = (unsigned)e;
                         bool fits = true;
-                        if constexpr (ListFmt<LE>::rel) {
+                        if constexpr (ListFmt<LE>::tile) {
+                            const int x = tpart >= 0 ? e + s_tile[9 * tpart + (int)((unsigned)er >> 28)] : -1;
+                            fits = (unsigned)x < (1u << 16);
+                            code = (unsigned)x;
+                        } else if constexpr (ListFmt<LE>::rel) {
                             const int p = er >> 28;
                             const int u = e - (p == 0 ? plb->x : (p == 1 ? plb->y : plb->z));
                             fits = (unsigned)u < (1u << kRelBits);
@@ -2947,14 +3060,11 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
     const int lane = threadIdx.x & 63;
     const int wave = uniform((int)(threadIdx.x >> 6));
     const int ntiles = ctx->ntiles;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        // read by the list steps that follow (next launches); every block here reads ctx->grid only
-        ctx->lgrid = ctx->grid;
-        ctx->lrc_b = pair_cutoff(a, ctx->cs);
-        ctx->lnslots = a.cstart[ctx->grid.ncell];  // binned particles (N undecomposed)
-        ctx->ldisp = 0.f;
-        ctx->lbuilds += 1;
-        ctx->nactive = 0;  // the list step's tail reads every workgroup's partial row
+    if constexpr (ListFmt<LE>::tile) {
+        // windows past the binned slots (a decomposed domain's build) stage nothing
+        const int w0 = (a.cstart[ctx->grid.ncell] + kTile - 1) / kTile, wn = (a.n + kTile - 1) / kTile;
+        for (int w = w0 + (int)blockIdx.x; w < wn; w += gridDim.x)
+            if (threadIdx.x < 2) a.ltile[(size_t)w * kListTileWords + 36 + threadIdx.x] = 0;
     }
     int ntot = 0;
     unsigned long long* const dbg = a.dbg_build ? a.dbg_build + 8 * blockIdx.x : nullptr;
@@ -2978,7 +3088,7 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
         int4 lb = make_int4(0, 0, 0, 0);
         pair_forces_sub<kModeList, GCS_LBUILD_GROUPS, LE>(ctx, a, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
                                       s_rowJ[wave], s_cand[wave], nullptr, ntot, wave, kListWaves, self, valid, &cnt,
-                                      &pend, &lb);
+                                      &pend, &lb, s_ovf[wave]);  // (ListTile16 tables: s_ovf's row, free until the tile's end)
         if (ListFmt<LE>::rel && valid && wave == 0) a.lbase[s] = lb;
         {  // the last, partial word of the lane's segment (its r entries sit in the top r slots: shift them down)
             constexpr int E = 8 / (int)sizeof(LE);
@@ -3045,13 +3155,17 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 // per SIMD either spills (3.74e9 / 1.15e9)
 #define GCS_LIST_UNROLL64 4
 #endif
-// One list step: ONE tile of 64 consecutive slots per workgroup (the launch has one workgroup per tile), W waves.
-// Phases, with nothing but LDS carried from one to the next (every wave's registers are free for the next phase):
+// One list step.  A workgroup takes ONE tile (W waves): ListTile16 the build's tile (<= 64 consecutive slots of one
+// cell row) from its table entry, the slot formats 64 consecutive slots.  Phases, with nothing but LDS carried from
+// one to the next (every wave's registers are free for the next phase):
 //   1. slot loads: current position (.w = particle | class << 24), build position, list count, the first kU
-//      entries of the wave's segment; the local-terms wave (W - 1) also the slot's constants and bond row
+//      entries of the wave's segment; the local-terms wave (W - 1) also the slot's constants and bond row.
+//      ListTile16: first the staged rows' current positions into the LDS image (LDS-DMA)
 //   2. wave W - 1: the particle-local terms (bond CSR, droplet, bending, tethers, point sources, walls) -> LDS
-//   3. every wave: its list segment, kU entries per batch (the next batch's entries in flight), the exact search
-//      for the lanes the lists may not cover; forces + neighbour counts -> LDS.  Wave 1: the Philox noise -> LDS
+//   3. every wave: its list segment, kU entries per batch (ListTile16: partners from the LDS image, the entries of
+//      the next two batches in flight; slot formats: one gather per entry, the next batch's entries in flight), the
+//      exact search for the lanes the lists may not cover; forces + neighbour counts -> LDS.  Wave 1: the Philox
+//      noise -> LDS
 //   4. (barrier) wave 0: sum the waves' forces, integrate, store; the launch statistics it owns (largest
 //      displacement, fallbacks; bbox / neighbour count on flagged launches) into the group's accumulators.
 //      Waves 1.. (in parallel): the wall reactions into the accumulators
@@ -3066,31 +3180,42 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 // RLX (the relaxation step's force launch, simulation_driver_relaxation.cpp:48-55): wave 0 stores the force (slot
 // order, .w = mu) instead of integrating and folds max mu |F| into the accumulators; the final workgroup sets the
 // adapted timestep ctx->dt_used (k_red64's arithmetic) and the reactions; k_lupdate then moves the particles.
-#ifndef GCS_LIST_NT
-#define GCS_LIST_NT 2  // list words read with the non-temporal hint: 0 never, 1 always, 2 beyond absolute 16-bit lists
+// List words are read once per step, with the non-temporal hint (ForceArgs::list_nt) when the lists are far beyond the
+// L2s, so they do not displace the partners (same-box A/B, profiles/r04_list_format_ab.txt: C5 fp64 +3-5 %, C2 fp64
+// with 4 trajectories -16 % when applied to its 16-bit lists, which the L2 / Infinity Cache keep).
+#ifndef GCS_STAGE_BYTES
+// ListTile16: bytes of the step window's LDS image of its partner rows (1,056 fp64 / 2,112 fp32 records; the image
+// also holds the waves' force partials after the pair loop).  With the rest of the kernel's LDS (< 7 KB) a workgroup
+// stays within 40 KB: 4 per CU, so C2's 948 windows are resident at once (a second round of workgroups doubles the
+// latency-bound step: profiles/r05b_probe_f0.log)
+#define GCS_STAGE_BYTES 33792
 #endif
-// one 8-byte list word of the list step (read once per step: with the non-temporal hint it should not displace the
-// gathered positions from the XCD's L2).  Same-box A/B (profiles/r04_list_format_ab.txt): C5 fp64 +3-5 %, C2 fp64
-// with 4 trajectories -16 % when applied to its absolute 16-bit lists (which the L2 / Infinity Cache would keep)
-template <typename LE>
-__device__ __forceinline__ uint2 list_word(const uint2* p)
-{
-    if constexpr (GCS_LIST_NT == 1 || (GCS_LIST_NT == 2 && !std::is_same<LE, unsigned short>::value)) {
-        const unsigned long long v = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(p));
-        return make_uint2((unsigned)v, (unsigned)(v >> 32));
-    } else {
-        return *p;
-    }
-}
+#ifndef GCS_LIST_WAVES_PER_EU_TILE
+#define GCS_LIST_WAVES_PER_EU_TILE 4  // ListTile16: 4 workgroups of 4 waves per CU -> <= 128 VGPRs
+#endif
+#ifndef GCS_LIST_UNROLL_TILE
+#define GCS_LIST_UNROLL_TILE 8  // ListTile16: list entries per batch (partners read from LDS; 2 batches of words ahead)
+#endif
+#ifndef GCS_LIST_UNROLL_TILE64
+#define GCS_LIST_UNROLL_TILE64 4  // the same at fp64
+#endif
 template <typename LE, int W, bool CT, bool DOM = false, typename R = float, bool RLX = false>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS_LIST_WAVES_PER_EU_CT : (sizeof(R) == 8 ? GCS_LIST_WAVES_PER_EU64 : GCS_LIST_WAVES_PER_EU)))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int flags)
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(ListFmt<LE>::tile ? GCS_LIST_WAVES_PER_EU_TILE : CT ? GCS_LIST_WAVES_PER_EU_CT : (sizeof(R) == 8 ? GCS_LIST_WAVES_PER_EU64 : GCS_LIST_WAVES_PER_EU)))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int flags)
 {
     using R4 = real4<R>;
     using R2 = real2<R>;
-    __shared__ R red[W][4][kTile];
-    __shared__ R4 s_locf[kTile], s_locr[kTile], s_loco[kTile], s_noise[kTile];
-    __shared__ R2 s_tab[kMaxTypes];
+    constexpr bool TL = ListFmt<LE>::tile;
+    constexpr int kStageRec = TL ? GCS_STAGE_BYTES / (int)sizeof(R4) : 1;
+    static_assert(!TL || (kStageRec * (int)sizeof(R4)) % 1024 == 0, "the image is whole 1-KiB LDS-DMA pieces");
+    static_assert(!TL || kStageRec * (int)sizeof(R4) >= W * 4 * kTile * (int)sizeof(R), "the partials fit the image");
+    __shared__ R4 s_stage[kStageRec];
+    __shared__ R s_red[TL ? 1 : W][4][TL ? 1 : kTile];
+    // ListTile16: the force partials reuse the image once every wave's pair loop is done (a barrier apart)
+    R(*const red)[4][kTile] = reinterpret_cast<R(*)[4][kTile]>(TL ? (void*)s_stage : (void*)s_red);
+    __shared__ R4 s_locf[kTile], s_noise[kTile];
+    __shared__ R2 s_tab[TL ? kTileTypes : kMaxTypes];
     __shared__ int s_last, s_final;
+    __shared__ int s_ttab[TL ? 40 : 1];  // ListTile16: the window's table entry (row lookups of entries past the image)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = uniform(tid >> 6);
     // GCS_DEBUG_TIMES: per workgroup 8 wall-clock stamps (start, wave 0: pair loop start / end, reduced, integrated,
@@ -3107,14 +3232,27 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     const R4* __restrict__ qc = St<R>::psort(a, par);  // slot order (pair partners)
     const int cap = a.list_cap;
     const size_t stride = (size_t)a.list_stride;
-    constexpr int kU = sizeof(R) == 4 ? GCS_LIST_UNROLL : GCS_LIST_UNROLL64;
+    constexpr int kU = TL ? (sizeof(R) == 4 ? GCS_LIST_UNROLL_TILE : GCS_LIST_UNROLL_TILE64)
+                          : (sizeof(R) == 4 ? GCS_LIST_UNROLL : GCS_LIST_UNROLL64);
     constexpr int kE = 8 / (int)sizeof(LE);  // entries per 8-byte list word
     constexpr int kW = kU / kE;              // list words per batch
     static_assert(kU % kE == 0, "a batch is whole list words");
     constexpr int kIdx = (1 << kListIndexBits) - 1;
+    const int klast = (cap / kU - 1) * kU;  // the segment's last batch (list_cap is a multiple of kU)
+    const bool lnt = a.list_nt != 0;
+    auto word = [&](const uint2* p) -> uint2 {
+        if (lnt) {
+            const unsigned long long v = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(p));
+            return make_uint2((unsigned)v, (unsigned)(v >> 32));
+        }
+        return *p;
+    };
     const uint2* __restrict__ segw = reinterpret_cast<const uint2*>(a.list) + (size_t)wave * (cap / kE) * stride + sl;
 
-    // 1. slot loads (one round trip; the type table's load beside them)
+    // 1. slot loads (one round trip; ListTile16: the window's table first, then the staged rows' current positions
+    // into the LDS image, LDS-DMA in 1-KiB pieces of consecutive records: a second round trip, under the first)
+    int tw = 0, T = 0, nst = 0;
+    if constexpr (TL) tw = lane < 38 ? a.ltile[(size_t)tile * kListTileWords + lane] : 0;
     const R2* __restrict__ tab = St<R>::type_ab(a);
     for (int t = tid; t < a.ntypes; t += blockDim.x) s_tab[t] = tab[t];
     const R4 pi = qc[sl];
@@ -3122,9 +3260,25 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     const int cw = a.lcount[(size_t)wave * stride + sl];
     int4 lb = make_int4(0, 0, 0, 0);
     if constexpr (ListFmt<LE>::rel) lb = a.lbase[sl];
-    uint2 e[kW];
+    uint2 e[kW], e1[kW];
 #pragma unroll
-    for (int j = 0; j < kW; ++j) e[j] = list_word<LE>(segw + (size_t)j * stride);  // list_cap >= kU: in bounds
+    for (int j = 0; j < kW; ++j) e[j] = word(segw + (size_t)j * stride);  // list_cap >= kU: in bounds
+    if constexpr (TL) {
+#pragma unroll
+        for (int j = 0; j < kW; ++j) e1[j] = word(segw + (size_t)(min(kU, klast) / kE + j) * stride);
+        T = __builtin_amdgcn_readlane(tw, 37);
+        nst = min(T, kStageRec);
+        if (wave == 0 && lane < 40) s_ttab[lane] = tw;
+        constexpr int kLpr = (int)sizeof(R4) / 16;  // lanes per record
+        constexpr int kRpc = 64 / kLpr;             // records per piece
+        const int npc = (nst + kRpc - 1) / kRpc;
+        for (int c = wave; c < npc; c += W) {
+            const int v = min(c * kRpc + lane / kLpr, T - 1);
+            const char* src = reinterpret_cast<const char*>(qc + stage_slot_w(v, tw)) + 16 * (lane % kLpr);
+            __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(s_stage + c * kRpc), 16,
+                                             0, 0);
+        }
+    }
     const R cs = (R)ctx->cs;
     const float D = ctx->ldisp;
     const float lrc_b = ctx->lrc_b;
@@ -3133,7 +3287,10 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     if constexpr (CT) {
         if constexpr (sizeof(R) == 4) cd2 = ctx->contact_d2; else cd2 = ctx->contact_d2_64;
     }
-    __syncthreads();  // s_tab
+    __syncthreads();  // s_tab, the LDS image
+    const int ngroups = min((int)gridDim.x, 8);
+    const int g = blockIdx.x % ngroups;
+    unsigned* const acc = a.lticket + kListAccBase + 32 * kAccWords * g;
 
     const int pk = wbits(pi.w);
     const int i = pk & kIdx;
@@ -3182,8 +3339,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
             }
         }
         s_locf[lane] = mk4<R>(lfx, lfy, lfz, km.x);
-        s_locr[lane] = mk4<R>(act ? rin[0] : R(0), act ? rin[1] : R(0), act ? rin[2] : R(0), R(0));
-        s_loco[lane] = mk4<R>(act ? rout[0] : R(0), act ? rout[1] : R(0), act ? rout[2] : R(0), R(0));
+        // the wall reactions straight into the launch accumulators (lane c: component c, inward then outward)
+        R rv = 0;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            const R x = wave_sum_r(act ? (c < 3 ? rin[c] : rout[c - 3]) : R(0));
+            if (lane == c) rv = x;
+        }
+        if (lane < 6) acc_fold(acc, lane, (double)rv);
     }
 
     // 3. the wave's list segment
@@ -3194,16 +3357,55 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     if (a.has_pair) {
         const int cnt = (act && !fb) ? min(cw & kListCountMask, cap) : 0;
         const int kmax = uniform(wave_max_int(cnt));
+        if constexpr (TL) {
+            // partners from the LDS image (an entry past the image: gathered through the row table); the entry
+            // words of the next two batches in flight
+            auto walk = [&](auto spill) {
+                constexpr bool SP = decltype(spill)::value;
+                for (int k0 = 0; k0 < kmax; k0 += kU) {
+                    uint2 e2[kW];
+                    const int kn = min(k0 + 2 * kU, klast);
+#pragma unroll
+                    for (int j = 0; j < kW; ++j) e2[j] = word(segw + (size_t)(kn / kE + j) * stride);
+                    R4 q[kU];
+#pragma unroll
+                    for (int u = 0; u < kU; ++u) {
+                        const int x = (k0 + u < cnt) ? list_entry<LE>(e, u) : 0;
+                        if constexpr (SP)
+                            q[u] = x < nst ? s_stage[x] : qc[stage_slot(x, s_ttab)];
+                        else
+                            q[u] = s_stage[x];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kU; ++u)
+                        list_pair<R>(pi.x, pi.y, pi.z, q[u], s_tab[(unsigned)wbits(q[u].w) >> kListIndexBits], ahi, bhi,
+                                     kA, kB, k2a, k2b, rc2, k0 + u < cnt, fx, fy, fz, nbr);
+                    if constexpr (CT) {
+#pragma unroll
+                        for (int u = 0; u < kU; ++u)
+                            if (!fbc && k0 + u < cnt) list_contact<R>(a, cd2, pi, q[u], i, wbits(q[u].w) & kIdx);
+                    }
+#pragma unroll
+                    for (int j = 0; j < kW; ++j) {
+                        e[j] = e1[j];
+                        e1[j] = e2[j];
+                    }
+                }
+            };
+            if (T <= kStageRec)
+                walk(std::false_type{});
+            else
+                walk(std::true_type{});
+        } else {
         // batches of kU entries: the partners' gathers are issued first, then the next batch's entry words (they
         // return right behind the gathers, so each batch costs one round trip), then the pair forces (and contacts)
-        const int klast = (cap / kU - 1) * kU;  // the segment's last batch (list_cap is a multiple of kU)
         for (int k0 = 0; k0 < kmax; k0 += kU) {
             R4 q[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) q[u] = qc[(k0 + u < cnt) ? list_slot<LE>(list_entry<LE>(e, u), lb) : sl];
             const int kn = min(k0 + kU, klast);
 #pragma unroll
-            for (int j = 0; j < kW; ++j) e[j] = list_word<LE>(segw + (size_t)(kn / kE + j) * stride);
+            for (int j = 0; j < kW; ++j) e[j] = word(segw + (size_t)(kn / kE + j) * stride);
             __builtin_amdgcn_sched_barrier(0);  // keep the entry loads here, ahead of the arithmetic
 #pragma unroll
             for (int u = 0; u < kU; ++u)
@@ -3214,6 +3416,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
                 for (int u = 0; u < kU; ++u)
                     if (!fbc && k0 + u < cnt) list_contact<R>(a, cd2, pi, q[u], i, wbits(q[u].w) & kIdx);
             }
+        }
         }
         // exact search of the build's cell list for the particles the lists may not cover: a partner within rc
         // now was within rc + D at the build.  Wave-cooperative: the wave takes its fallback lanes one at a time,
@@ -3290,22 +3493,20 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         }
     }
     if (dbg && tid == 0) dbg[2] = wall_clock64();
-    red[wave][0][lane] = fx;
-    red[wave][1][lane] = fy;
-    red[wave][2][lane] = fz;
-    red[wave][3][lane] = nbr;
     if (!RLX && wave == (W > 1 ? 1 : 0)) {  // the noise (depends on the particle and the step only) off wave 0's path
         R n0, n1, n2;
         noise3<R>(a, ctx, i, n0, n1, n2);
         s_noise[lane] = mk4<R>(n0, n1, n2, R(0));
     }
+    if constexpr (TL) __syncthreads();  // every wave is done with the image: the partials may take its place
+    red[wave][0][lane] = fx;
+    red[wave][1][lane] = fy;
+    red[wave][2][lane] = fz;
+    red[wave][3][lane] = nbr;
     __syncthreads();
     if (dbg && tid == 0) dbg[3] = wall_clock64();
 
     // 4. integrate (wave 0) / the reactions (waves 1..)
-    const int ngroups = min((int)gridDim.x, 8);
-    const int g = blockIdx.x % ngroups;
-    unsigned* const acc = a.lticket + kListAccBase + 32 * kAccWords * g;
     if (wave == 0) {
         R fsx = red[0][0][lane], fsy = red[0][1][lane], fsz = red[0][2][lane], ns = red[0][3][lane];
 #pragma unroll
@@ -3418,23 +3619,10 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
                           ((flags & kLFlagBBox) && lane >= 9 && lane < 15) || (DOM && lane == 15);
         if (mine) acc_fold(acc, lane, v);
         }
-    } else {
-        // the wall reactions: waves 1.. take the six components in turn (W = 4: wave 1 inward, wave 2 outward)
-        const int c0 = W > 2 ? 3 * (wave - 1) : 0, c1 = W > 2 ? c0 + 3 : 6;
-        if (c0 < 6) {
-            R v = 0;
-            for (int c = c0; c < c1; ++c) {
-                const R4 r = c < 3 ? s_locr[lane] : s_loco[lane];
-                const R x = wave_sum_r((c % 3) == 0 ? r.x : (c % 3) == 1 ? r.y : r.z);
-                if (lane == c) v = x;
-            }
-            if (lane >= c0 && lane < c1) acc_fold(acc, lane, (double)v);
-        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's accumulator atomics are performed
     __syncthreads();
     if (dbg && tid == 0) dbg[5] = wall_clock64();
-
     // 5. the two-level ticket (one counter per group of workgroups b % 8, then one over the groups; a single
     // counter serialises ~1000 returning atomics); the final workgroup reads the totals and advances the context
     const int gsize = ((int)gridDim.x - g + ngroups - 1) / ngroups;
@@ -4000,13 +4188,16 @@ void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceAr
     }
 }
 
-int list_step_grid(int n) { return force_blocks(n); }
+// the list step's launch: one workgroup per 64 consecutive slots (ListTile16: per window of the table)
+int list_step_grid(const ForceArgs& a) { return force_blocks(a.n); }
 
 // the entry type of the launch's list format (ForceArgs::list_fmt), handed to fn as a value of that type
 template <typename Fn>
 static void with_list_entry(const ForceArgs& a, Fn&& fn)
 {
-    if (a.list_fmt == kListFmtAbs16)
+    if (a.list_fmt == kListFmtTile16)
+        fn(ListTile16{});
+    else if (a.list_fmt == kListFmtAbs16)
         fn((unsigned short)0);
     else if (a.list_fmt == kListFmtRel16)
         fn(ListRel16{});
@@ -4029,7 +4220,7 @@ void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a)
 template <bool CT, typename R>
 static void launch_list_step_ct(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)
 {
-    const dim3 g(list_step_grid(a.n));
+    const dim3 g(list_step_grid(a));
     with_list_entry(a, [&](auto tag) {
         using LE = decltype(tag);
         if (a.list_waves == 2)
@@ -4052,7 +4243,7 @@ void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2, double d2_64)
 template <typename R>
 static void launch_list_relax_r(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force_flags, int update_flags)
 {
-    const dim3 g(list_step_grid(a.n));
+    const dim3 g(list_step_grid(a));
     with_list_entry(a, [&](auto tag) {
         using LE = decltype(tag);
         if (a.list_waves == 2)
@@ -4079,7 +4270,7 @@ void launch_list_relax(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force
 template <typename R>
 static void launch_list_step_dom(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int flags)
 {
-    const dim3 g(list_step_grid(a.n));
+    const dim3 g(list_step_grid(a));
     with_list_entry(a, [&](auto tag) {
         using LE = decltype(tag);
         if (a.list_waves == 2)

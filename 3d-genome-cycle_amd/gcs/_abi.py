@@ -44,7 +44,7 @@ OPT_LIST_CAP = 12
 OPT_LIST_WAVES = 13
 OPT_DENSE_NEIGHBORS = 15
 OPT_LIST_DEAL = 16
-OPT_LIST_FORMAT = 17  # 0 default, 1 plane-relative 16-bit entries at any size, 2 32-bit entries
+OPT_LIST_FORMAT = 17  # 0 default (tile-staged 16-bit), 1 plane-relative 16-bit, 2 32-bit, 3 16-bit slots (round 4)
 
 
 def list_deal(pattern: str) -> int:

@@ -104,9 +104,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def launch_ranks(n: int, argv) -> int:
+def launch_ranks(n: int, argv, poll_s: float = 0.05, grace_s: float = 5.0) -> int:
     """`bench.py --gpus N` without WORLD_SIZE: start N child ranks of this same script (one per GPU) and wait.
-    This process touches no device: the children load the engine after their own environment is set."""
+    This process touches no device: the children load the engine after their own environment is set.  The children
+    are polled together: the first one to exit non-zero ends the run (the others would wait in their next collective
+    until the gloo timeout), so they are terminated -- killed after `grace_s` -- and its exit code returned."""
     port = _free_port()
     procs = []
     for r in range(n):
@@ -114,13 +116,28 @@ def launch_ranks(n: int, argv) -> int:
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, str(ROOT / "bench.py")] + list(argv), env=env))
     rc = 0
-    for p in procs:
-        code = p.wait()
-        if code != 0 and rc == 0:
-            rc = code
-            for q in procs:  # one rank failed: the others would wait forever in the next collective
-                if q.poll() is None:
-                    q.terminate()
+    live = list(procs)
+    while live and rc == 0:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = code
+                break
+        if live and rc == 0:
+            time.sleep(poll_s)
+    if rc != 0:
+        for q in live:  # a rank failed: stop the rest
+            q.terminate()
+        deadline = time.monotonic() + grace_s
+        for q in live:
+            try:
+                q.wait(timeout=max(0.0, deadline - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                q.kill()
+                q.wait()
     return rc
 
 
@@ -585,6 +602,9 @@ def f32_leg(args, maker, cfg, bd, local, state, window, R, K, G, list_waves, ran
 
 def replica_main(args):
     world, rank, local, dist = dist_setup()
+    if os.environ.get("GCS_BENCH_FAIL_RANK") == str(rank):  # launcher tests: this rank dies before the first barrier
+        print(f"bench: rank {rank} failing on purpose (GCS_BENCH_FAIL_RANK)", file=sys.stderr, flush=True)
+        os._exit(3)
     if not args.stub_engine:
         from gcs import _abi as A
         A.load()  # this rank's engine runtime (no torch HIP runtime in replica runs)
@@ -735,6 +755,9 @@ def replica_main(args):
         lst = {k: lst[k] for k in ("active", "rebuild_every", "skin", "builds", "fallback_particle_steps",
                                    "pair_classes", "capacity")}
     finite = all(bool(np.isfinite(e.get_positions()).all()) for e in engines)
+    # every rank's trajectories: all finite, and a position checksum of its first one (distinct seeds: distinct sums)
+    rank_finite = gather_over_ranks(dist, 1.0 if finite else 0.0)
+    rank_sums = gather_over_ranks(dist, float(np.asarray(engines[0].get_positions(), dtype=np.float64).sum()))
     at = after + args.profile_steps
 
     contacts_ms, contacts_distinct = None, None
@@ -820,6 +843,8 @@ def replica_main(args):
         "timed_s": el_max,
         "per_rank_values": rank_values,
         "per_rank_seeds": rank_seeds,
+        "per_rank_finite": rank_finite,
+        "per_rank_checksums": rank_sums,
         "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, {R} independent "
                                f"trajectories per GPU, window from step {window} "
                                f"(core_scale {ctx['core_scale']:.4f})",

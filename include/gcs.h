@@ -385,10 +385,12 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
                                      wave (< waves per tile) of chunk p of each period in nibble p.  Only the split of
                                      a slot's list over the segments changes (the list step's last wave also carries
                                      the particle-local terms); the pair set and the results do not */
-#define GCS_OPT_LIST_FORMAT 17    /* list entries: 0 (default) 16-bit absolute slots up to 65,536 particles, 16-bit slots
-                                     relative to the particle's cell planes beyond (an entry out of their range sends the
-                                     particle to the exact search); 1 the relative form at any size; 2 32-bit absolute
-                                     slots.  Every form holds the same pairs in the same order: the results do not change */
+#define GCS_OPT_LIST_FORMAT 17    /* list entries: 0 (default) 16-bit indices into the step tile's LDS image of its partner
+                                     rows (the partners are read from LDS, not gathered); 1 16-bit slots relative to the
+                                     particle's cell planes (an entry out of their range sends the particle to the exact
+                                     search); 2 32-bit absolute slots; 3 16-bit absolute slots up to 65,536 particles, the
+                                     relative form beyond.  Every form holds the same pairs in the same order: the results
+                                     do not change */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
 
 /* List-step diagnostics (the neighbour lists md::neighbor_searcher keeps between rebuilds; micromd, called at

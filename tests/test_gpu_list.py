@@ -554,11 +554,12 @@ def _format_run(design, cfg, prec, fmt, steps, ctx=LATE, seed=11, **opts):
 
 
 @precisions
-@pytest.mark.parametrize("fmt", [1, 2])
+@pytest.mark.parametrize("fmt", [1, 2, 3])
 def test_list_formats_bitwise_c1(c1_design, prec, fmt):
-    """GCS_OPT_LIST_FORMAT: plane-relative 16-bit entries (1, kernels.hip ListRel16) and 32-bit entries (2) hold the
-    same pairs in the same order as the default absolute 16-bit entries: the trajectory (list rebuilds included) is
-    bitwise the same, with the same particles searched exactly"""
+    """GCS_OPT_LIST_FORMAT: plane-relative 16-bit slots (1, kernels.hip ListRel16), 32-bit slots (2) and absolute
+    16-bit slots (3) hold the same pairs in the same order as the default tile-staged entries (0, ListTile16: indices
+    into the step tile's LDS image): the trajectory (list rebuilds included) is bitwise the same, with the same
+    particles searched exactly"""
     cfg = InterphaseConfig()
     x0, s0 = _format_run(c1_design, cfg, prec, 0, 60)
     x1, s1 = _format_run(c1_design, cfg, prec, fmt, 60)
@@ -569,15 +570,18 @@ def test_list_formats_bitwise_c1(c1_design, prec, fmt):
 
 @precisions
 def test_relative_entries_c5_bitwise(prec):
-    """N > 65,536 (C5, 606,248 particles, its dense synthetic start): the default plane-relative 16-bit entries against
-    32-bit entries -- every partner within the plane span (no escape to the exact search), so bitwise the same"""
+    """N > 65,536 (C5, 606,248 particles, its dense synthetic start): the default tile-staged entries (many tiles'
+    partner rows exceed the LDS image there: those entries are gathered through the row table) and the plane-relative
+    16-bit slots against 32-bit slots -- every partner within the plane span (no escape to the exact search), so
+    bitwise the same"""
     cfg = resolution_scaled(InterphaseConfig(), 10.0)
     design = synthetic.make_c5()
     ctx = {"step": 0, "time": 0.0, "core_scale": 1.0, "bond_scale": 1.0, "wall_semiaxes": LATE["wall_semiaxes"]}
-    x0, s0 = _format_run(design, cfg, prec, 0, 20, ctx=ctx)
     x2, s2 = _format_run(design, cfg, prec, 2, 20, ctx=ctx)
-    assert s0["fallback_particle_steps"] == s2["fallback_particle_steps"], (s0, s2)
-    assert np.array_equal(x0, x2)
+    for fmt in (0, 1):
+        x0, s0 = _format_run(design, cfg, prec, fmt, 20, ctx=ctx)
+        assert s0["fallback_particle_steps"] == s2["fallback_particle_steps"], (fmt, s0, s2)
+        assert np.array_equal(x0, x2), fmt
 
 
 @precisions
@@ -598,12 +602,40 @@ def test_relative_entries_escape_to_exact_search(prec):
         if name == "e":
             s.set_option(A.OPT_FUSED_STEP, 3)
             s.set_option(A.OPT_DENSE_NEIGHBORS, 0)
+            s.set_option(A.OPT_LIST_FORMAT, 1)
         sysd[name] = s
     for s in sysd.values():
         s.run(5, seed=3, timestep=1e-7)
     st = sysd["e"].list_stats()
     assert st["active"] == 1 and st["fallback_particle_steps"] > 0, st
     assert np.abs(sysd["e"].get_positions() - sysd["o"].get_positions()).max() <= TOL_X[prec]
+
+
+@precisions
+def test_tile_entries_beyond_the_lds_image(prec):
+    """The default tile-staged entries (ListTile16) on a dense rod (100,000 particles, 4 x 0.13 x 0.13, ~400-560
+    list entries each) whose tiles' partner rows exceed the LDS image (GCS_STAGE_BYTES) in ~98 % of the tiles at
+    either precision (tools estimate: staged rows ~1,900 fp64 / ~3,000 fp32 records per tile against 1,248 / 2,496):
+    the entries past the image are gathered through the tile's row table.  The same particles searched exactly as
+    with 32-bit slots, bitwise the same trajectory, and the same bound vs the oracle"""
+    n = 100000
+    rng = np.random.default_rng(7)
+    x = np.column_stack([rng.uniform(0, 4, n), rng.uniform(0, 0.13, n), rng.uniform(0, 0.13, n)])
+    runs = {}
+    for name, cls, fmt in (("t", Engine, 0), ("i", Engine, 2), ("o", oracle.OracleSystem, None)):
+        s = cls(n, precision=prec)
+        s.add_neighbor_softcore(2.5, 0.03, 2.5, 0.024, 0.03, mix=False, scaled=False)
+        s.set_positions(x)
+        if fmt is not None:
+            s.set_option(A.OPT_FUSED_STEP, 3)
+            s.set_option(A.OPT_DENSE_NEIGHBORS, 0)
+            s.set_option(A.OPT_LIST_FORMAT, fmt)
+        s.run(5, seed=3, timestep=1e-7)
+        runs[name] = s
+    st = runs["t"].list_stats()
+    assert st["active"] == 1 and st["fallback_particle_steps"] == runs["i"].list_stats()["fallback_particle_steps"], st
+    assert np.array_equal(runs["t"].get_positions(), runs["i"].get_positions())
+    assert np.abs(runs["t"].get_positions() - runs["o"].get_positions()).max() <= TOL_X[prec]
 
 
 @precisions
@@ -636,3 +668,51 @@ def test_skin_follows_core_scale(c1_design, prec):
     o.set_context(ctx0)
     o.run(121, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=21)
     assert np.abs(x1 - o.get_positions()).max() <= TOL_X[prec]
+
+
+def _classes_system(cls, n, nclass, prec, rng_seed=5, **opts):
+    """n particles in a cube at ~C2's density, softcore A/B with `nclass` distinct (a, b) factor pairs (continuous
+    values, as chains TSVs give: stage_prepare/chains.cpp:55-56) and an ellipsoid wall"""
+    rng = np.random.default_rng(rng_seed)
+    side = (n / 220.0) ** (1.0 / 3.0)
+    x = rng.uniform(0, side, (n, 3))
+    table = rng.uniform(0.4, 1.6, (nclass, 2))
+    ab = table[rng.integers(0, nclass, n)]
+    ab[:nclass] = table  # every class present
+    s = cls(n, ab_factors=ab, precision=prec)
+    s.add_neighbor_softcore(2.0, 0.3, 1.5, 0.24, 0.3, mix=True, scaled=False)
+    s.add_ellipsoid_inward(5.0, 0.3, 0.0, 1.0, center=(side / 2,) * 3)
+    s.set_context({"core_scale": 1.0, "bond_scale": 1.0, "wall_semiaxes": [0.45 * side] * 3})
+    s.set_positions(x)
+    for k, v in opts.items():
+        s.set_option(getattr(A, "OPT_" + k.upper()), v)
+    return s
+
+
+@precisions
+def test_many_pair_classes_take_the_cell_list_step(prec):
+    """More than 256 distinct (a, b) pair classes (1,500 continuous factor pairs): the list step does not admit the
+    system; the default engine then runs its cell-list step (fp64: k_eval64 + k_red64 + k_update + k_tail; fp32: the
+    rebuild step) instead of failing, within the precision's bound of the oracle"""
+    n = 1500
+    e = _classes_system(Engine, n, 1500, prec)
+    o = _classes_system(oracle.OracleSystem, n, 1500, prec)
+    for s in (e, o):
+        s.run(25, seed=9, timestep=1e-5, temperature=1.0)
+    assert e.list_stats()["active"] == 0
+    assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[prec]
+
+
+@precisions
+def test_pair_classes_beyond_the_tile_table(prec):
+    """65-256 pair classes (100 here): the list step with 16-bit slot entries (the tile-staged entries' LDS class
+    table holds 64), bitwise the explicit slot format, and within the bound of the oracle"""
+    n = 1500
+    runs = [_classes_system(Engine, n, 100, prec, fused_step=3, dense_neighbors=0, list_format=f) for f in (0, 3)]
+    o = _classes_system(oracle.OracleSystem, n, 100, prec)
+    for s in runs + [o]:
+        s.run(25, seed=9, timestep=1e-5, temperature=1.0)
+    st = runs[0].list_stats()
+    assert st["active"] == 1 and st["pair_classes"] == 100
+    assert np.array_equal(runs[0].get_positions(), runs[1].get_positions())
+    assert np.abs(runs[0].get_positions() - o.get_positions()).max() <= TOL_X[prec]

@@ -79,3 +79,24 @@ def test_single_gpu_stub_engine_defaults_to_one_rank():
                         "--replicas-per-gpu", "1", "--profile-steps", "2", "--min-window-s", "0.05"])
     assert line["n_gpus"] == 1 and line["steps_requested"] == 16 and line["steps"] % 16 == 0
     assert line["warmup_steps_run"] >= 32  # G = min(graph_steps, steps) = 16, two chunks
+
+
+@pytest.mark.parametrize("fail_rank", [0, 1])
+def test_launcher_ends_when_a_rank_fails(fail_rank):
+    """`bench.py --gpus 2` when one rank dies (GCS_BENCH_FAIL_RANK: exit 3 right after the rendezvous, before the
+    first barrier): the launcher polls every child, so it returns that exit code within seconds -- it does not sit
+    in rank 0's wait while the survivor blocks in its barrier until the gloo timeout -- and no child is left
+    running."""
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["GCS_BENCH_FAIL_RANK"] = str(fail_rank)
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--stub-engine", "--config", "c1",
+                        "--steps", "16", "--warmup", "2", "--cpu-budget", "0", "--replicas-per-gpu", "1",
+                        "--profile-steps", "2", "--min-window-s", "0.05"],
+                       capture_output=True, text=True, env=env, timeout=120, cwd=str(ROOT))
+    elapsed = time.monotonic() - t0
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert "failing on purpose" in p.stderr
+    assert elapsed < 60, elapsed  # (gloo's own timeout is 30 min)
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]  # no bench line
