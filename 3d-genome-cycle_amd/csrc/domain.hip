@@ -99,23 +99,8 @@ __global__ __launch_bounds__(256) void k_domain_unpack(ForceArgs a, const real4<
     // the send bands' header rows for the next step's fused pack (this step's sends are done: stream order)
     if (blockIdx.x == 0)
         for (int p = threadIdx.x; p < nsend; p += blockDim.x) send[(size_t)p * sstride] = mk4<R>(R(0), R(0), R(0), R(0));
-    for (int b = 0; b < nbuf; ++b) {
-        const int c = min(counts[(size_t)b * cstride], cap);
-        for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < c; k += gridDim.x * blockDim.x) {
-            const R4 r = in[(size_t)b * istride + k];
-            const int i = wbits(r.w);
-            if (i < 0 || i >= a.n) continue;
-            const R4 p = mk4<R>(r.x, r.y, r.z, R(0));
-            St<R>::pos(a, 0)[i] = p;
-            St<R>::pos(a, 1)[i] = p;
-            const int sl = slots ? a.islot[i] : -1;
-            if (sl >= 0) {
-                const R4 q = mk4<R>(r.x, r.y, r.z, wpack<R>(i | (a.ptype[i] << kListIndexBits)));
-                St<R>::psort(a, 0)[sl] = q;
-                St<R>::psort(a, 1)[sl] = q;
-            }
-        }
-    }
+    dom_unpack_records<R>(a, in, counts, nbuf, cap, istride, cstride, slots, blockIdx.x * blockDim.x + threadIdx.x,
+                          gridDim.x * blockDim.x);
 }
 
 // Shared particles (the nucleolar beads and their NOR beads: their bonds are far softer than the chain's, so no

@@ -257,6 +257,9 @@ struct gcs_engine {
     int* lcount = nullptr;
     int4* lbase = nullptr;
     int* ltile = nullptr;  // ListTile16 tile table (ForceArgs::ltile)
+    unsigned* psync = nullptr;  // the persistent small-system step's barrier counter and accumulator sets
+    int small_opt = 1;          // GCS_OPT_SMALL_STEP
+    bool fused_explicit = false;  // GCS_OPT_FUSED_STEP was set: the step shape it names, never the small step
     float4* psort[2] = {nullptr, nullptr};
     float4* skmu = nullptr;  // list step: slot-ordered kmu and bond CSR rows
     int2* sbrow = nullptr;
@@ -790,7 +793,8 @@ bool dense_switch(const gcs_engine* e) { return e->dense && !e->dom && e->prec !
 // rebuild step (2) when the system does not admit lists, and hands a dense chain to the unfused tile step (0)
 int eff_fused(const gcs_engine* e)
 {
-    if (e->prec == 64) return 3;  // the fp64 engine: the list step, or (list_ok false) its cell-list step
+    // the fp64 engine: the list step, or its cell-list step (list_ok false, or GCS_OPT_FUSED_STEP 0)
+    if (e->prec == 64) return e->fused == 0 ? 0 : 3;
     if (e->fused != 3) return e->fused;
     if (!e->list_ok) return 2;
     return dense_switch(e) ? 0 : 3;
@@ -1573,6 +1577,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->lcount);
     dfree(e->lbase);
     dfree(e->ltile);
+    dfree(e->psync);
     dfree(e->psort[0]);
     dfree(e->psort[1]);
     dfree(e->skmu);
@@ -1973,6 +1978,40 @@ int gcs_engine_set_noise(gcs_engine* e, const double* normals, int64_t steps)
     return GCS_OK;
 }
 
+namespace {
+// the persistent small-system step (kernels.hip k_pstep): fixed-timestep runs of <= kPMax particles, undecomposed,
+// unless a step shape was asked for (GCS_OPT_FUSED_STEP) or the option is off
+bool small_path(const gcs_engine* e, bool spacestep)
+{
+    return e->small_opt != 0 && !e->fused_explicit && !spacestep && !e->dom && e->n >= 1 && e->n <= kPMax;
+}
+constexpr int kPChunk = 2048;  // steps per cooperative launch (a launch then lasts ~10 ms)
+
+int run_small(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps)
+{
+    int rc;
+    if ((rc = flush_contacts(e))) return rc;
+    if ((rc = begin_run(e, cfg, first_step))) return rc;
+    if (!e->psync && (rc = dalloc(&e->psync, kPSyncWords))) return rc;
+    ForceArgs a = e->fa;
+    a.psync = e->psync;
+    for (int64_t done = 0; done < steps;) {
+        const int len = (int)std::min<int64_t>(kPChunk, steps - done);
+        HIPCHK(hipMemsetAsync(e->psync, 0, kPSyncWords * sizeof(unsigned), e->stream));
+        if (launch_pstep(e->stream, e->ctx, a, len, e->sched_flags != 0 ? 1 : 0))
+            return fail(GCS_EHIP, "the persistent small-system step could not be launched cooperatively");
+        e->rstats.eager_steps += len;
+        done += len;
+    }
+    HIPCHK(hipGetLastError());
+    end_run(e, cfg, first_step, steps);
+    e->chain_valid = false;  // no cell or neighbour lists of these positions
+    if (steps & 1) e->parity ^= 1;
+    if (cfg->noise == GCS_NOISE_INJECTED) e->noise_cursor += steps;
+    return GCS_OK;
+}
+}  // namespace
+
 int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps)
 {
     if (e) e->dom_cont = false;  // a decomposed run re-primes after any outside change
@@ -1988,6 +2027,7 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
     if (rc) return rc;
     // (the fp64 engine's fixed-timestep step is the list step when the system admits it -- a neighbor soft-core field,
     // <= 256 (a, b) pair classes, < 2^24 particles -- and otherwise its cell-list step: enqueue_step, prec 64)
+    if (small_path(e, spacestep)) return run_small(e, cfg, first_step, steps);
     if (!list_path(e, spacestep) || spacestep)  // (contact updates are fused into fixed-timestep list steps only)
         if ((rc = flush_contacts(e))) return rc;
     // the list skin of the run's first step (skin_level); a change from the last run's re-primes and rebuilds
@@ -2744,13 +2784,19 @@ int enqueue_rccl_step(gcs_engine* e, const gcs_bd_config* cfg, int64_t step)
 {
     const RcclApi* r = rccl();
     if (e->dom_list) {
-        // list step: k_lstep<DOM> (+ rebuild) with the band pack and the shared particles fused, allreduce, tail +
-        // shared in, exchange, unpack (+ the send headers zeroed): 3 launches and 2 collectives per step
+        // list step: k_lstep<DOM> (+ rebuild) with the band pack and the shared particles fused, allreduce, exchange,
+        // tail + shared in + unpack (+ the send headers zeroed): 2 launches and 2 collectives per step
         enqueue_dom_list_step(e, step, e->dom_red, true);
         NCCLCHK(r->allReduce(e->dom_red, e->dom_glob, e->dom_nred, ncclDouble, ncclSum, e->nccl, e->stream));
-        enqueue_dom_list_finish(e, e->dom_glob, nullptr, 0);
         if (int rc = enqueue_band_exchange(e)) return rc;
-        enqueue_band_unpack(e);
+        // the tail and the unpack in one launch (k_ldom_finish; the exchange does not depend on the tail)
+        const int stride = e->dom_cap + 1;
+        const size_t rb = band_record_bytes(e->prec);
+        launch_list_domain_finish(e->stream, e->ctx, domain_args(e, e->dom_red), e->dom_glob, e->dom_flags_step & ~8,
+                                  e->dom_shared_idx, e->dom_nshared, e->dom_recv + rb,
+                                  reinterpret_cast<const int*>(e->dom_recv), e->dom_npeer, e->dom_cap, stride,
+                                  stride * (int)(rb / sizeof(int)), e->dom_npeer > 0 ? e->dom_send : nullptr,
+                                  e->dom_npeer, stride);
         HIPCHK(hipGetLastError());
         (void)cfg;
         return GCS_OK;
@@ -3255,11 +3301,17 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         e->chain_valid = e->dense_chain = false;
         return GCS_OK;
     }
+    if (option == GCS_OPT_SMALL_STEP) {
+        if (value != 0 && value != 1) return fail(GCS_EINVAL, "small step must be 0 or 1");
+        e->small_opt = (int)value;
+        return GCS_OK;
+    }
     if (option == GCS_OPT_FUSED_STEP) {
         if (value != 0 && value != 2 && value != 3) return fail(GCS_EINVAL, "fused step must be 0, 2 or 3");
-        if (e->prec == 64 && value != 3)
-            return fail(GCS_EINVAL, "the fp64 engine runs the list step (GCS_OPT_FUSED_STEP 3) only");
+        if (e->prec == 64 && value == 2)
+            return fail(GCS_EINVAL, "the fp64 engine runs the list step (3) or its cell-list step (0)");
         e->fused = (int)value;
+        e->fused_explicit = true;
         drop_graph(e);
         return GCS_OK;
     }

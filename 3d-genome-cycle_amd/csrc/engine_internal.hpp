@@ -302,6 +302,8 @@ struct ForceArgs {
     // kListFmtTile16 (kernels.hip ListTile16): per step window (64 slots) kListTileWords ints written by the build,
     // the staged rows of its (up to two) row parts (layout: kernels.hip stage_slot)
     int* ltile;
+    // the persistent small-system step (kernels.hip k_pstep): [0] the grid-barrier counter, then three accumulator sets
+    unsigned* psync;
     unsigned long long list_deal;  // list build: candidate chunk -> wave segment pattern (GCS_OPT_LIST_DEAL; 0: round robin)
     int par_hint;           // >= 0: ctx->parity of this launch, known to the host at enqueue (the slot loads need not
                             // wait for the context); -1: read it
@@ -393,10 +395,41 @@ constexpr int kListFmtInt = 1;
 constexpr int kListFmtRel16 = 2;
 // 16-bit indices into the step tile's LDS image of its partners (kernels.hip ListTile16: the default at any size)
 constexpr int kListFmtTile16 = 3;
+constexpr int kPMax = 2048;         // particles of the persistent small-system step (kernels.hip k_pstep: LDS images)
+constexpr int kPSyncWords = 64 + 3 * 32 * (kListAccSlots + 1);  // its psync buffer
 constexpr int kListTileWords = 64;  // ints per window-table entry (kernels.hip stage_slot: 38 used)
 constexpr int kTileTypes = 64;      // pair-factor classes of the ListTile16 step (its LDS class table; more: slot entries)
 constexpr int kListCountMask = (1 << 30) - 1;
 constexpr int kListOverflow = 1 << 30;
+
+// the decomposed runs' band unpack (domain.hip k_domain_unpack, kernels.hip k_ldom_finish): received records
+// {x, y, z, index bits} of nbuf bands (band b's records at in[b * istride + k], k < counts[b * cstride] <= cap) into
+// both position buffers by index and, with slots, into both slot-order buffers at the particle's list slot (islot);
+// thread t of nt, grid-stride
+template <typename R>
+__device__ __forceinline__ void dom_unpack_records(const ForceArgs& a, const real4<R>* __restrict__ in,
+                                                   const int* __restrict__ counts, int nbuf, int cap, int istride,
+                                                   int cstride, int slots, int t, int nt)
+{
+    using R4 = real4<R>;
+    for (int b = 0; b < nbuf; ++b) {
+        const int c = min(counts[(size_t)b * cstride], cap);
+        for (int k = t; k < c; k += nt) {
+            const R4 r = in[(size_t)b * istride + k];
+            const int i = wbits(r.w);
+            if (i < 0 || i >= a.n) continue;
+            const R4 p = mk4<R>(r.x, r.y, r.z, R(0));
+            St<R>::pos(a, 0)[i] = p;
+            St<R>::pos(a, 1)[i] = p;
+            const int sl = slots ? a.islot[i] : -1;
+            if (sl >= 0) {
+                const R4 q = mk4<R>(r.x, r.y, r.z, wpack<R>(i | (a.ptype[i] << kListIndexBits)));
+                St<R>::psort(a, 0)[sl] = q;
+                St<R>::psort(a, 1)[sl] = q;
+            }
+        }
+    }
+}
 
 // ---- Philox4x32-10 + Box-Muller: the production noise stream (identical on host for the oracle) ----
 __host__ __device__ inline void philox4x32_10(unsigned c[4], unsigned k0, unsigned k1)
@@ -467,7 +500,15 @@ void launch_set_contact(hipStream_t s, DevCtx* ctx, float d2, double d2_64);
 void launch_dom_grid(hipStream_t s, DevCtx* ctx, const ForceArgs& a);
 void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const double* glob, int flags,
                              const int* shared, int nshared, void* bands, int npeer, int band_stride);
+// the engine-issued RCCL list step's finish, ONE launch after both collectives: the tail of launch_list_domain_tail
+// (block 0) beside the band unpack of launch_domain_unpack with slots (every block; the send bands' headers zeroed)
+void launch_list_domain_finish(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const double* glob, int flags,
+                               const int* shared, int nshared, const void* in, const int* counts, int nbuf, int cap,
+                               int istride, int cstride, void* send, int nsend, int sstride);
 int list_step_grid(const ForceArgs& a);
+// the persistent small-system step: `steps` steps of n <= kPMax particles in ONE cooperative launch (a.psync zeroed
+// by the caller first); flags: kernels.hip kLFlagSched when the schedule applies
+int launch_pstep(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int steps, int flags);
 void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceArgs& a, bool fused);
 // fp64 force / energy evaluation on the current cell list (one thread per sorted slot; kernels.hip k_eval64):
 // kModeForce -> a.dforce_out + partial rows a.dpart [blocks][8] (reactions in[3], out[3], max mu|F|, neighbours),

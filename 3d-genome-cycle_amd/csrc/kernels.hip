@@ -1329,11 +1329,12 @@ __device__ inline R spring_coef(int type, R K, R l, R r2, R& U)
 template <int MODE, int BB = 1, typename R = float>
 __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceArgs& a, int i, R xi, R yi, R zi,
                                    real4<R> km, R& fx, R& fy, R& fz, R* en, R* rin, R* rout,
-                                   int2 erange = make_int2(-1, -1))
+                                   int2 erange = make_int2(-1, -1), const real4<R>* posv = nullptr)
 {
     const int n = a.n;
     const FieldPrm<R>& P = St<R>::prm(a);
-    const real4<R>* __restrict__ posc = St<R>::pos(a, ctx->parity);
+    // the step-start positions of the partners: the context's buffer, or posv (k_pstep: its LDS image)
+    const real4<R>* __restrict__ posc = posv ? posv : St<R>::pos(a, ctx->parity);
     const R cs = (R)ctx->cs;
     const R bs = (R)ctx->bs;
     R e_sw = 0, e_bond = 0, e_bend = 0, e_win = 0, e_wout = 0, e_pt = 0, e_kf = 0;
@@ -3771,6 +3772,256 @@ __global__ __launch_bounds__(kLUpdateBlock) void k_lupdate(DevCtx* __restrict__ 
     list_tail_apply(ctx, a, tin, tot, flags & (kLFlagSched | kLFlagBBox));
 }
 
+// ----------------------------------------------------------------------------------------------------
+// The persistent small-system step (the mitotic stages: 586 / 1,172 particles; any system of <= kPMax particles).
+// At these sizes a step of the list step is ~10-19 workgroups and its cost is latency: a launch, a chain of dependent
+// round trips, a cross-workgroup tail (~16 us per step).  Here ONE cooperative launch runs a chunk
+// of steps with one workgroup per 64 particles (all resident, each on a CU of its own), and every workgroup holds the
+// WHOLE system's positions in LDS:
+//   * pairs: all N candidates per particle, a fp32 prefilter on the LDS image with a margin (every pair within the
+//     cutoff in R passes), then the exact pair in R (list_pair, the list step's arithmetic: the same pair set).  No
+//     cell list, no neighbour lists, no rebuilds, no skin: exact at every step by construction;
+//   * particle-local terms on the LDS image (local_terms with the image as its positions);
+//   * one grid barrier per step: each workgroup stores its particles' new positions write-through (sc1), drains,
+//     and ONE lane adds to a counter; the workgroups poll it (sc1 loads), then load the new positions with sc1
+//     loads into LDS (MI355X_MICROARCH.md "inter-workgroup visibility", the counter row of the valid forms: sc1
+//     stores and loads, one workgroup per CU);
+//   * the tail (reactions -> wall ODE, schedule, step / parity / noise cursor) computed REDUNDANTLY by every
+//     workgroup from the step's accumulator set (fixed-point integer sums: order-free, so every copy is the same)
+//     on its own LDS copy of the context; workgroup 0 writes the context back at the end.  Accumulator sets rotate
+//     over three (step k accumulates into set k % 3, workgroup 0 clears set (k + 1) % 3 during step k: every
+//     workgroup read it after barrier k - 2, before arriving at barrier k - 1).
+// The force on a particle sums its partners in index order (wave w takes candidates [w N / 4, (w + 1) N / 4)):
+// bitwise reproducible, and independent of how a run is chunked.  The sum order differs from the list step's, so
+// the two agree to rounding (tests: both within the oracle's bound).
+#ifndef GCS_PSTEP_SPIN
+#define GCS_PSTEP_SPIN (1 << 22)  // grid-barrier polls before a workgroup gives up (DevCtx::scan_stall; the host fails)
+#endif
+constexpr int kPWaves = 4;
+constexpr int kPSyncSet = 64;                  // psync: [0] the barrier counter, the sets from word 64
+constexpr int kPSetWords = 32 * kAccWords;     // one accumulator set (acc_fold's layout: 128 B per slot)
+
+// the totals of one accumulator set (the slots the persistent step folds: reactions, neighbours), read-only
+__device__ __forceinline__ void pset_totals(unsigned* base, ListTotals& t)
+{
+    unsigned long long v[7], lo[6];
+    for (int k = 0; k < 7; ++k) v[k] = __hip_atomic_load(acc_slot(base, k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < 6; ++k)
+        lo[k] = __hip_atomic_load(acc_slot(base, kAccReactLo + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned bad = __hip_atomic_load(reinterpret_cast<unsigned*>(acc_slot(base, kListAccSlots)), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < 6; ++k)
+        t.react[k] = (bad & 1u) ? __longlong_as_double(0x7ff8000000000000ll)
+                                : (double)(long long)v[k] * 0x1p-20 + (double)(long long)lo[k] * 0x1p-52;
+    t.nbr = (double)v[6];
+    t.ld = 0.f;
+    t.nfb = 0;
+    t.nown = 0;
+    for (int k = 0; k < 6; ++k) t.bb[k] = 0.f;
+    t.drift = 0.0;
+}
+
+template <typename R>
+__global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx, ForceArgs a, int steps, int flags)
+{
+    using R4 = real4<R>;
+    using R2 = real2<R>;
+    constexpr int W = kPWaves;
+    __shared__ R4 s_pos[kPMax];      // every particle's position at the step start (particle order)
+    __shared__ float4 s_pf[kPMax];   // its fp32 rounding (the prefilter)
+    __shared__ R2 s_ab[kPMax];       // its pair factors (a, b)
+    __shared__ R red[W][4][kTile];
+    __shared__ R4 s_locf[kTile], s_noise[kTile];
+    __shared__ DevCtx s_ctx;
+    // (fp32: pad the workgroup beyond half a CU's LDS -- one workgroup per CU, the hand-off's validated form)
+    __shared__ char s_pad[sizeof(R) == 4 ? 48 * 1024 : 16];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = uniform(tid >> 6);
+    const int n = a.n;
+    const int G = gridDim.x;
+    const int i = blockIdx.x * kTile + lane;
+    const bool valid = i < n;
+    const int il = valid ? i : n - 1;
+    unsigned* const sync = a.psync;
+    if (tid == 0) s_pad[0] = 0;
+    const FieldPrm<R>& P = St<R>::prm(a);
+    const R4* __restrict__ kmu = St<R>::kmu(a);
+
+    // launch start: the context, the pair factors and the run's positions (earlier launches wrote them: the launch
+    // boundary orders them), the particle's constants for every step
+    if (tid == 0) s_ctx = *ctx;
+    for (int j = tid; j < n; j += blockDim.x) {
+        const R4 k = kmu[j];
+        R2 t;
+        t.x = a.pair_mix ? k.y : R(1);
+        t.y = a.pair_mix ? k.z : R(0);
+        s_ab[j] = t;
+    }
+    __syncthreads();
+    int par = s_ctx.parity;
+    for (int j = tid; j < n; j += blockDim.x) {
+        const R4 p = St<R>::pos(a, par)[j];
+        s_pos[j] = p;
+        s_pf[j] = make_float4((float)p.x, (float)p.y, (float)p.z, 0.f);
+    }
+    R4 km = mk4<R>(R(0), R(0), R(0), R(0));
+    int2 erow = make_int2(0, 0);
+    if (wave == W - 1) {
+        km = kmu[il];
+        erow = a.has_bonds ? make_int2(a.boff[il], a.boff[il + 1]) : make_int2(0, 0);
+    }
+    const R2 own = s_ab[il];  // (s_ab was filled before the barrier above)
+    const int j0 = wave * n / W, j1 = (wave + 1) * n / W;  // this wave's candidates
+
+    for (int k = 0; k < steps; ++k) {
+        unsigned* const acc = sync + kPSyncSet + (k % 3) * kPSetWords;
+        if (blockIdx.x == 0 && tid < kListAccSlots + 1) {  // clear the set of step k + 1
+            unsigned long long* w = acc_slot(sync + kPSyncSet + ((k + 1) % 3) * kPSetWords, tid);
+            __hip_atomic_store(w, list_acc_identity(tid), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();  // s_pos / s_pf of this step, s_ctx
+        const R4 pi = s_pos[il];
+        const R cs = (R)s_ctx.cs;
+        const R scale = a.pair_scaled ? cs : R(1);
+        const R sa = P.pa_sig * scale, sbb = P.pb_sig * scale;
+        const R k2a = R(1) / (sa * sa), k2b = R(1) / (sbb * sbb);
+        const R kA = R(0.5) * R(6) * P.pa_eps * k2a, kB = R(0.5) * R(24) * P.pb_eps * k2b;
+        const R rc = pair_cutoff_r<R>(a, (double)cs), rc2 = rc * rc;
+        const R ahi = kA * own.x, bhi = kB * own.y;
+
+        // the particle-local terms first on the last wave (image positions), the reactions into the set
+        if (wave == W - 1) {
+            R lfx = 0, lfy = 0, lfz = 0, en[kEnergyKinds];
+            R rin[3] = {0, 0, 0}, rout[3] = {0, 0, 0};
+            local_terms<kModeStep, sizeof(R) == 8 ? GCS_LIST_BOND_BATCH64 : GCS_LIST_BOND_BATCH, R>(
+                &s_ctx, a, il, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout, erow, s_pos);
+            s_locf[lane] = mk4<R>(lfx, lfy, lfz, km.x);
+            R rv = 0;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                const R x = wave_sum_r(valid ? (c < 3 ? rin[c] : rout[c - 3]) : R(0));
+                if (lane == c) rv = x;
+            }
+            if (lane < 6) acc_fold(acc, lane, (double)rv);
+        }
+
+        // pairs: this wave's quarter of the candidates, 32 at a time: the fp32 prefilter -> a hit mask, then the
+        // exact pair in R for each hit in index order
+        R fx = 0, fy = 0, fz = 0, nbr = 0;
+        if (a.has_pair) {
+            const float pxf = (float)pi.x, pyf = (float)pi.y, pzf = (float)pi.z;
+            // margin: the fp32 roundings of the coordinates (|x| < ~400) move r^2 by far less than this
+            const float thr = (float)rc2 * 1.001f + 1.0e-4f * (float)rc;
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            const f2 PX = {pxf, pxf}, PY = {pyf, pyf}, PZ = {pzf, pzf};
+            for (int c0 = j0; c0 < j1; c0 += 32) {
+                unsigned m = 0u;
+#pragma unroll
+                for (int h = 0; h < 16; ++h) {
+                    const int ja = min(c0 + 2 * h, kPMax - 1), jb = min(c0 + 2 * h + 1, kPMax - 1);
+                    const float4 A = s_pf[ja], B = s_pf[jb];
+                    const f2 dx = f2{A.x, B.x} - PX, dy = f2{A.y, B.y} - PY, dz = f2{A.z, B.z} - PZ;
+                    const f2 r2 = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+                    m |= (r2.x < thr ? 1u : 0u) << (2 * h);
+                    m |= (r2.y < thr ? 1u : 0u) << (2 * h + 1);
+                }
+                const int rem = j1 - c0;
+                if (rem < 32) m &= (1u << rem) - 1u;
+                if ((unsigned)(i - c0) < 32u) m &= ~(1u << (i - c0));  // not itself
+                if (!valid) m = 0u;
+                while (__ballot(m != 0u)) {
+                    const int b = m ? __ffs(m) - 1 : 0;
+                    const bool real = m != 0u;
+                    m &= m - 1u;
+                    const int j = c0 + b;
+                    list_pair<R>(pi.x, pi.y, pi.z, s_pos[j], s_ab[j], ahi, bhi, kA, kB, k2a, k2b, rc2, real, fx, fy, fz,
+                                 nbr);
+                }
+            }
+        }
+        if (wave == (W > 1 ? 1 : 0)) {  // the noise (depends on the particle and the step only)
+            R n0, n1, n2;
+            noise3<R>(a, &s_ctx, il, n0, n1, n2);
+            s_noise[lane] = mk4<R>(n0, n1, n2, R(0));
+        }
+        red[wave][0][lane] = fx;
+        red[wave][1][lane] = fy;
+        red[wave][2][lane] = fz;
+        red[wave][3][lane] = nbr;
+        __syncthreads();
+
+        // integrate (wave 0): the new position, stored write-through for the other workgroups
+        if (wave == 0) {
+            R fsx = red[0][0][lane], fsy = red[0][1][lane], fsz = red[0][2][lane], ns = red[0][3][lane];
+#pragma unroll
+            for (int w = 1; w < W; ++w) {
+                fsx += red[w][0][lane];
+                fsy += red[w][1][lane];
+                fsz += red[w][2][lane];
+                ns += red[w][3][lane];
+            }
+            const R4 lf = s_locf[lane];
+            fsx += lf.x;
+            fsy += lf.y;
+            fsz += lf.z;
+            const R mu = lf.w;
+            const R4 xi = s_noise[lane];
+            const R dt = P.timestep;
+            const R amp = r_sqrt(R(2) * P.temperature * mu * dt);
+            const R mdt = mu * dt;
+            const R4 np = mk4<R>(pi.x + mdt * fsx + amp * xi.x, pi.y + mdt * fsy + amp * xi.y,
+                                 pi.z + mdt * fsz + amp * xi.z, R(0));
+            if (valid) {
+                const auto rp = __builtin_amdgcn_make_buffer_rsrc((void*)St<R>::pos(a, par ^ 1), 0, n * (int)sizeof(R4),
+                                                                  0x00020000);
+                const float4* pv = reinterpret_cast<const float4*>(&np);
+#pragma unroll
+                for (int h = 0; h < (int)sizeof(R4) / 16; ++h) st_sc1_f4(rp, i * (int)sizeof(R4) + 16 * h, pv[h]);
+            }
+            const R nt = wave_sum_r(valid ? ns : R(0));
+            if (lane == 6) acc_fold(acc, 6, (double)nt);
+        }
+
+        // the grid barrier: every wave's stores and folds are performed, ONE lane adds, then polls the counter
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned target = (unsigned)G * (unsigned)(k + 1);
+            for (int spin = 0; __hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
+                if (spin >= GCS_PSTEP_SPIN) {  // (never with every workgroup resident: counted, the host fails)
+                    s_ctx.scan_stall += 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+        par ^= 1;
+        // the next step's image (sc1 loads: the other workgroups' write-through stores), and the tail on this
+        // workgroup's context from the step's set
+        {
+            const auto rp = __builtin_amdgcn_make_buffer_rsrc((void*)St<R>::pos(a, par), 0, n * (int)sizeof(R4), 0x00020000);
+            for (int j = tid; j < n; j += blockDim.x) {
+                R4 p;
+                float4* pv = reinterpret_cast<float4*>(&p);
+#pragma unroll
+                for (int h = 0; h < (int)sizeof(R4) / 16; ++h) pv[h] = ld_sc1_f4(rp, j * (int)sizeof(R4) + 16 * h);
+                s_pos[j] = p;
+                s_pf[j] = make_float4((float)p.x, (float)p.y, (float)p.z, 0.f);
+            }
+        }
+        if (tid == 0) {
+            ListTotals t;
+            pset_totals(acc, t);
+            const ListTailIn tin = list_tail_load(&s_ctx, a);
+            list_tail_apply(&s_ctx, a, tin, t, flags | (k == steps - 1 ? kLFlagStats : 0));
+        }
+    }
+    __syncthreads();
+    if (blockIdx.x == 0 && tid == 0) *ctx = s_ctx;
+}
+
 // The decomposed list step's tail (one workgroup, after the allreduce of every domain's k_lstep<..., DOM> reduction):
 // the same context update as the undecomposed step's final workgroup from the global sums (reactions, neighbours,
 // fallbacks) and the largest of the domains' displacement slots; the next build's grid is this domain's owned bbox
@@ -3791,12 +4042,15 @@ __global__ void k_dom_grid(DevCtx* __restrict__ ctx, ForceArgs a)
     ctx->grid = make_grid(bb, bb + 3, pair_cutoff(a, ctx->cs) + a.list_skin, a.ncell_max, kPairFx);
 }
 
+// the tail of a decomposed list step from the allreduced buffer glob (thread tid of nt >= 1 in one workgroup; the
+// context by thread 0): the undecomposed tail arithmetic on the global sums, the checks, the shared particles in
+// (by index and slot), the send bands' headers zeroed (bands != nullptr), the shared block of the reduction buffer
+// zeroed for the next step's owners
 template <typename R>
-__global__ __launch_bounds__(64) void k_ldom_tail(DevCtx* __restrict__ ctx, ForceArgs a, const double* __restrict__ glob,
-                                                  int flags, const int* __restrict__ shared, int nshared,
-                                                  real4<R>* __restrict__ bands, int npeer, int bstride)
+__device__ __forceinline__ void ldom_tail_body(DevCtx* __restrict__ ctx, const ForceArgs& a, const double* __restrict__ glob,
+                                               int flags, const int* __restrict__ shared, int nshared,
+                                               real4<R>* __restrict__ bands, int npeer, int bstride, int tid, int nt)
 {
-    const int tid = threadIdx.x;
     if (tid == 0) {
         const ListTailIn tin = list_tail_load(ctx, a);
         ListTotals t;
@@ -3818,7 +4072,7 @@ __global__ __launch_bounds__(64) void k_ldom_tail(DevCtx* __restrict__ ctx, Forc
         if (fl) atomicOr(a.dom_flags, fl);
     }
     constexpr int kIdx = (1 << kListIndexBits) - 1;
-    for (int k = tid; k < nshared; k += blockDim.x) {
+    for (int k = tid; k < nshared; k += nt) {
         const int i = shared[k];
         const R x = (R)glob[kDomainRed + 3 * k], y = (R)glob[kDomainRed + 3 * k + 1], z = (R)glob[kDomainRed + 3 * k + 2];
         St<R>::pos(a, 0)[i] = mk4<R>(x, y, z, R(0));
@@ -3830,11 +4084,37 @@ __global__ __launch_bounds__(64) void k_ldom_tail(DevCtx* __restrict__ ctx, Forc
             St<R>::psort(a, 1)[sl] = q;
         }
     }
-    for (int p = tid; p < npeer; p += blockDim.x) bands[(size_t)p * bstride] = mk4<R>(R(0), R(0), R(0), R(0));
+    if (bands)
+        for (int p = tid; p < npeer; p += nt) bands[(size_t)p * bstride] = mk4<R>(R(0), R(0), R(0), R(0));
     // the shared block of this domain's reduction buffer for the next step's owners (the fused pack writes only
     // the owned particles' rows; the allreduce of this step has consumed it)
     if (a.dom_red)
-        for (int k = tid; k < 3 * nshared; k += blockDim.x) a.dom_red[kDomainRed + k] = 0.0;
+        for (int k = tid; k < 3 * nshared; k += nt) a.dom_red[kDomainRed + k] = 0.0;
+}
+
+template <typename R>
+__global__ __launch_bounds__(64) void k_ldom_tail(DevCtx* __restrict__ ctx, ForceArgs a, const double* __restrict__ glob,
+                                                  int flags, const int* __restrict__ shared, int nshared,
+                                                  real4<R>* __restrict__ bands, int npeer, int bstride)
+{
+    ldom_tail_body<R>(ctx, a, glob, flags, shared, nshared, bands, npeer, bstride, threadIdx.x, blockDim.x);
+}
+
+// The engine-issued RCCL list step's finish after BOTH collectives (the band exchange does not depend on the tail,
+// only the next step does): workgroup 0's first wave runs the tail, every thread of every workgroup unpacks the
+// received bands (k_domain_unpack's scatter, slots on) -- one launch per step instead of two.  The tail's shared
+// particles and a band record of the same particle carry the same new position, so their order does not matter.
+template <typename R>
+__global__ __launch_bounds__(256) void k_ldom_finish(DevCtx* __restrict__ ctx, ForceArgs a, const double* __restrict__ glob,
+                                                     int flags, const int* __restrict__ shared, int nshared,
+                                                     const real4<R>* __restrict__ in, const int* __restrict__ counts,
+                                                     int nbuf, int cap, int istride, int cstride,
+                                                     real4<R>* __restrict__ send, int nsend, int sstride)
+{
+    if (blockIdx.x == 0 && threadIdx.x < 64)
+        ldom_tail_body<R>(ctx, a, glob, flags, shared, nshared, send, nsend, sstride, threadIdx.x, 64);
+    dom_unpack_records<R>(a, in, counts, nbuf, cap, istride, cstride, 1, blockIdx.x * blockDim.x + threadIdx.x,
+                          gridDim.x * blockDim.x);
 }
 
 // ----------------------------------------------------------------------------------------------------
@@ -4259,6 +4539,16 @@ void launch_dom_grid(hipStream_t s, DevCtx* ctx, const ForceArgs& a)
     hipLaunchKernelGGL(k_dom_grid, dim3(1), dim3(1), 0, s, ctx, a);
 }
 
+int launch_pstep(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int steps, int flags)
+{
+    const dim3 g((a.n + kTile - 1) / kTile), b(64 * kPWaves);
+    ForceArgs args = a;
+    void* kargs[] = {(void*)&ctx, (void*)&args, (void*)&steps, (void*)&flags};
+    // cooperative: the runtime launches the grid only if every workgroup can be resident at once (the grid barrier)
+    const void* fn = a.prec == 64 ? (const void*)k_pstep<double> : (const void*)k_pstep<float>;
+    return hipLaunchCooperativeKernel(fn, g, b, kargs, 0, s) == hipSuccess ? 0 : -1;
+}
+
 void launch_list_relax(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int force_flags, int update_flags)
 {
     if (a.prec == 64)
@@ -4311,6 +4601,19 @@ void launch_list_domain_tail(hipStream_t s, DevCtx* ctx, const ForceArgs& a, con
     else
         hipLaunchKernelGGL(k_ldom_tail<float>, dim3(1), dim3(64), 0, s, ctx, a, glob, flags, shared, nshared,
                            (float4*)bands, npeer, band_stride);
+}
+
+void launch_list_domain_finish(hipStream_t s, DevCtx* ctx, const ForceArgs& a, const double* glob, int flags,
+                               const int* shared, int nshared, const void* in, const int* counts, int nbuf, int cap,
+                               int istride, int cstride, void* send, int nsend, int sstride)
+{
+    const int blocks = nbuf > 0 ? std::max(1, std::min(1024, (cap + 255) / 256)) : 1;
+    if (a.prec == 64)
+        hipLaunchKernelGGL(k_ldom_finish<double>, dim3(blocks), dim3(256), 0, s, ctx, a, glob, flags, shared, nshared,
+                           (const double4*)in, counts, nbuf, cap, istride, cstride, (double4*)send, nsend, sstride);
+    else
+        hipLaunchKernelGGL(k_ldom_finish<float>, dim3(blocks), dim3(256), 0, s, ctx, a, glob, flags, shared, nshared,
+                           (const float4*)in, counts, nbuf, cap, istride, cstride, (float4*)send, nsend, sstride);
 }
 
 void launch_update(hipStream_t s, const DevCtx* ctx, const ForceArgs& a)

@@ -68,7 +68,8 @@ extern "C" {
 /* 2: gcs_run_stats gained fused_contact_steps (an out-struct grew: callers built against 1 must rebuild)
  * 3: gcs_system_desc.reserved became .precision (0 = fp64); gcs_run_stats lost the small-path counters and
  *    gained density_probes; gcs_list_stats gained deal; GCS_OPT_SMALL_PATH and GCS_OPT_FUSED_STEP 1 are gone;
- *    later in 3 (additive, no layout change): GCS_OPT_LIST_FORMAT; the default list skin follows the core scale */
+ *    later in 3 (additive, no layout change): GCS_OPT_LIST_FORMAT; the default list skin follows the core scale;
+ *    GCS_OPT_LIST_FORMAT 3, GCS_OPT_SMALL_STEP */
 #define GCS_ABI_VERSION 3
 
 /* arithmetic precision of an engine (gcs_system_desc.precision) */
@@ -363,8 +364,9 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
 #define GCS_OPT_WAVES_PER_TILE 2 /* waves sharing one 64-particle tile of the pair loop: 1, 2, 4 or 8 */
 #define GCS_OPT_CHUNK_ORDER 3    /* pair-loop candidate chunks: 0 contiguous, 1 strided across stencil rows (default) */
 #define GCS_OPT_FUSED_STEP 4     /* 3 (default): neighbour-list step (1 launch per step + a list rebuild every few
-                                    steps; fp32 systems with > 256 pair classes or >= 2^24 particles run step 2);
-                                    fp32 only: 2 launches per step (force + cell-list rebuild), 0 unfused */
+                                    steps; systems with > 256 pair classes or >= 2^24 particles: fp32 step 2, fp64
+                                    step 0); 0 unfused (a fresh cell list every step; fp64: k_eval64 + k_red64 +
+                                    k_update + k_tail); fp32 only: 2 launches per step (force + cell-list rebuild) */
 #define GCS_OPT_SPLIT_TILES 5    /* step launches: 0 (default) off, 1 split every tile over two workgroups, 2 only the
                                     densest tiles, picked by the cell scan within the resident-workgroup budget */
 #define GCS_OPT_SUBTILES 7       /* pair-loop stencils per 64-particle tile: 1, 2 or 4 (default 2) */
@@ -391,6 +393,9 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
                                      search); 2 32-bit absolute slots; 3 16-bit absolute slots up to 65,536 particles, the
                                      relative form beyond.  Every form holds the same pairs in the same order: the results
                                      do not change */
+#define GCS_OPT_SMALL_STEP 18     /* systems of <= 2,048 particles (the mitotic stages): 1 (default) one cooperative launch
+                                     per chunk of steps, every workgroup holding the whole system in LDS (all pairs, a
+                                     grid barrier per step), unless GCS_OPT_FUSED_STEP was set; 0 the step shapes above */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
 
 /* List-step diagnostics (the neighbour lists md::neighbor_searcher keeps between rebuilds; micromd, called at

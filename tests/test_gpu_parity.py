@@ -132,9 +132,8 @@ def test_trajectory_philox_c1_wall_contact(c1_design, interphase_cfg, prec):
 @pytest.mark.parametrize("fused", [3, 0], ids=["list", "cells"])
 def test_relaxation_spacestep(c1_design, interphase_cfg, prec, fused):
     """spacestep 1e-3 (simulation_driver_relaxation.cpp:48-55), injected reference noise: the relaxation step on the
-    lists (default) and, on the fp32 engine, on a fresh cell list every step (GCS_OPT_FUSED_STEP 0)"""
-    if prec == 64 and fused != 3:
-        pytest.skip("the fp64 engine has the list step only")
+    lists (default) and on a fresh cell list every step (GCS_OPT_FUSED_STEP 0: fp32 k_force + k_adapt + k_update, fp64
+    k_eval64 + k_red64 + k_update)"""
     cfg = interphase_cfg
     e, o = both(c1_design, cfg, prec)
     e.set_option(A.OPT_FUSED_STEP, fused)
