@@ -3067,6 +3067,15 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
         for (int w = w0 + (int)blockIdx.x; w < wn; w += gridDim.x)
             if (threadIdx.x < 2) a.ltile[(size_t)w * kListTileWords + 36 + threadIdx.x] = 0;
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // read by the list steps that follow (next launches); every block here reads ctx->grid only
+        ctx->lgrid = ctx->grid;
+        ctx->lrc_b = pair_cutoff(a, ctx->cs);
+        ctx->lnslots = a.cstart[ctx->grid.ncell];  // binned particles (N undecomposed)
+        ctx->ldisp = 0.f;
+        ctx->lbuilds += 1;
+        ctx->nactive = 0;  // the list step's tail reads every workgroup's partial row
+    }
     int ntot = 0;
     unsigned long long* const dbg = a.dbg_build ? a.dbg_build + 8 * blockIdx.x : nullptr;
     if (dbg && threadIdx.x == 0) dbg[0] = wall_clock64();
