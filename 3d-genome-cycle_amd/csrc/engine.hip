@@ -257,6 +257,7 @@ struct gcs_engine {
     int* lcount = nullptr;
     int4* lbase = nullptr;
     int* ltile = nullptr;  // ListTile16 tile table (ForceArgs::ltile)
+    int* lstage = nullptr;  // ListTile16 image sources (ForceArgs::lstage)
     unsigned* psync = nullptr;  // the persistent small-system step's barrier counter and accumulator sets
     int small_opt = 1;          // GCS_OPT_SMALL_STEP
     bool fused_explicit = false;  // GCS_OPT_FUSED_STEP was set: the step shape it names, never the small step
@@ -917,6 +918,7 @@ ForceArgs list_args(const gcs_engine* e)
     a.list_fmt = list_format(e);
     a.lbase = e->lbase;
     a.ltile = e->ltile;
+    a.lstage = e->lstage;
     // the non-temporal hint beyond 16-bit absolute lists that the L2s keep (kernels.hip k_lstep)
     a.list_nt = (a.list_fmt == kListFmtRel16 || a.list_fmt == kListFmtInt || (a.list_fmt == kListFmtTile16 && e->n > 65536))
                     ? 1 : 0;
@@ -934,6 +936,7 @@ int ensure_list(gcs_engine* e)
     dfree(e->lcount);
     dfree(e->lbase);
     dfree(e->ltile);
+    dfree(e->lstage);
     dfree(e->psort[0]);
     dfree(e->psort[1]);
     dfree(e->skmu);
@@ -945,7 +948,8 @@ int ensure_list(gcs_engine* e)
     int rc;
     if ((rc = dalloc(&e->list, need)) || (rc = dalloc(&e->lcount, stride * kMaxListWaves)) ||
         (rc = dalloc(&e->lbase, stride)) || (rc = dalloc(&e->sbrow, stride)) ||
-        (rc = dalloc(&e->ltile, ltile_entries(e) * kListTileWords)))
+        (rc = dalloc(&e->ltile, ltile_entries(e) * kListTileWords)) ||
+        (rc = dalloc(&e->lstage, ltile_entries(e) * (size_t)stage_capacity(e->prec))))
         return rc;
     if (e->prec == 64) {  // the slot-ordered copies in the engine's precision only
         if ((rc = dalloc(&e->dpsort[0], stride)) || (rc = dalloc(&e->dpsort[1], stride)) || (rc = dalloc(&e->dskmu, stride)))
@@ -1577,6 +1581,7 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->lcount);
     dfree(e->lbase);
     dfree(e->ltile);
+    dfree(e->lstage);
     dfree(e->psync);
     dfree(e->psort[0]);
     dfree(e->psort[1]);

@@ -302,6 +302,7 @@ struct ForceArgs {
     // kListFmtTile16 (kernels.hip ListTile16): per step window (64 slots) kListTileWords ints written by the build,
     // the staged rows of its (up to two) row parts (layout: kernels.hip stage_slot)
     int* ltile;
+    int* lstage;  // per window stage_capacity(prec) ints: the slot of each record of the step's LDS image
     // the persistent small-system step (kernels.hip k_pstep): [0] the grid-barrier counter, then three accumulator sets
     unsigned* psync;
     unsigned long long list_deal;  // list build: candidate chunk -> wave segment pattern (GCS_OPT_LIST_DEAL; 0: round robin)
@@ -397,8 +398,11 @@ constexpr int kListFmtRel16 = 2;
 constexpr int kListFmtTile16 = 3;
 constexpr int kPMax = 2048;         // particles of the persistent small-system step (kernels.hip k_pstep: LDS images)
 constexpr int kPSyncWords = 64 + 3 * 32 * (kListAccSlots + 1);  // its psync buffer
-constexpr int kListTileWords = 64;  // ints per window-table entry (kernels.hip stage_slot: 38 used)
-constexpr int kTileTypes = 64;      // pair-factor classes of the ListTile16 step (its LDS class table; more: slot entries)
+constexpr int kListTileWords = 128;  // ints per window-table entry (kernels.hip stage_slot_w: 73 used)
+constexpr int kTileTypes = 64;
+// records of the ListTile16 step's LDS image (kernels.hip k_lstep: 33,792 B; fp64 28 B per record in three arrays, fp32
+// whole 16-B records)
+__host__ __device__ constexpr int stage_capacity(int prec) { return prec == 64 ? 1152 : 2112; }      // pair-factor classes of the ListTile16 step (its LDS class table; more: slot entries)
 constexpr int kListCountMask = (1 << 30) - 1;
 constexpr int kListOverflow = 1 << 30;
 

@@ -1812,32 +1812,24 @@ __device__ __forceinline__ int stage_row(int k)
 {
     return (int)((0x862075314ull >> (4 * k)) & 15ull);  // k = 0..8: rows 4, 1, 3, 5, 7, 0, 2, 6, 8
 }
-// A window's table entry (ForceArgs::ltile, kListTileWords ints): part p (0, 1) of the window has staged rows k = 0..8
-// whose first slot is t[18 p + k] and first staged index t[18 p + 9 + k] (non-decreasing over p, k); t[36] = part 1's
-// first index (= part 0's staged total), t[37] = the total.  The slot of staged index v < t[37]: the last row of its
-// part starting at or before v.  From the LDS copy of the entry:
-__device__ __forceinline__ int stage_slot(int v, const int* t)
+// A window's table entry (ForceArgs::ltile, kListTileWords ints): staged row r = 9 p + k (part p < kWinParts of the
+// window, its staged row k) starts at staged index t[r] (non-decreasing in r; rows of absent parts start at the
+// total) and holds the slots from t[36 + r] on; t[72] = the total.  The slot of staged index v < t[72]: that of the
+// last row starting at or before v, found by a binary search over the 36 row starts held one per lane (tw0 = t[lane],
+// tw1 = t[64 + lane]; lane-indexed reads of them are ds_bpermute)
+constexpr int kWinParts = 4;
+__device__ __forceinline__ int stage_slot_w(int v, int tw0, int tw1)
 {
-    const int b = v >= t[36] ? 18 : 0;
-    int d = t[b] - t[b + 9];
+    int lo = 0;
 #pragma unroll
-    for (int k = 1; k < 9; ++k) d = (v >= t[b + 9 + k]) ? t[b + k] - t[b + 9 + k] : d;
-    return v + d;
-}
-// ... and from the entry held one int per lane (tw = t[lane], wave-uniform reads)
-__device__ __forceinline__ int stage_slot_w(int v, int tw)
-{
-    const bool p1 = v >= __builtin_amdgcn_readlane(tw, 36);
-    int d = p1 ? __builtin_amdgcn_readlane(tw, 18) - __builtin_amdgcn_readlane(tw, 27)
-               : __builtin_amdgcn_readlane(tw, 0) - __builtin_amdgcn_readlane(tw, 9);
-#pragma unroll
-    for (int k = 1; k < 9; ++k) {
-        const int v0 = __builtin_amdgcn_readlane(tw, 9 + k), v1 = __builtin_amdgcn_readlane(tw, 27 + k);
-        const int j0 = __builtin_amdgcn_readlane(tw, k), j1 = __builtin_amdgcn_readlane(tw, 18 + k);
-        const int th = p1 ? v1 : v0;
-        if (v >= th) d = p1 ? j1 - v1 : j0 - v0;
+    for (int st = 32; st > 0; st >>= 1) {
+        const int c = min(lo + st, 35);
+        const int t = __shfl(tw0, c);
+        lo = (lo + st < 36 && t <= v) ? lo + st : lo;
     }
-    return v + d;
+    const int tv = __shfl(tw0, lo);
+    const int j0 = __shfl(tw0, min(36 + lo, 63)), j1 = __shfl(tw1, max(lo - 28, 0));
+    return v - tv + (lo < 28 ? j0 : j1);
 }
 constexpr int kRelBits = 14;
 // the partner slot of a list entry (x: its raw bits)
@@ -1948,50 +1940,69 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
         }
         if constexpr (MODE == kModeList && ListFmt<LE>::tile) {
             // the staged rows of the step windows this tile meets (ListTile16; windows of 64 slots, each in up to
-            // two row parts): lane wi * 32 + p * 16 + k, k < 9, takes staged row k (stencil row stage_row(k)) of part
-            // p of window (s_begin >> 6) + wi.  Outputs: the window's table entry (ltile, wave 0; identical from every
-            // workgroup that meets the window), s_tile[(2 wi + p) * 9 + q] = staged index - slot of stencil row q,
-            // s_tile[36 + 2 wi + p] = the end slot of part p
-            const int wA = s_begin >> 6, wi = lane >> 5, p = (lane >> 4) & 1, k = lane & 15;
-            const int w = wA + wi;
+            // kWinParts row parts), one window at a time: the window's slots' cells (one coalesced load), a ballot of
+            // the row changes = the parts' first slots, then lane p * 16 + k, k < 9, takes staged row k (stencil row
+            // stage_row(k)) of part p.  Outputs: the window's table entry (wave 0; identical from every workgroup
+            // that meets the window: kernels.hip stage_slot_w's layout), s_tile[(4 wi + p) * 9 + q] = staged index -
+            // slot of stencil row q of part p of window wi, s_tile[72 + 2 wi], [73 + 2 wi] = its part-start mask
             const int nsl = a.cstart[g.ncell];  // binned slots
-            const int wb = w * kTile, we = min(wb + kTile, nsl);
-            int tl = 0, tj = 0, pend = wb;
-            const bool wok = w <= ((s_end - 1) >> 6) && wb < we;
-            if (wok) {
-                const int r0 = a.scell[wb] / nx;
-                const int p0e = min(we, a.cstart[(r0 + 1) * nx]);
-                int first = wb, last = p0e - 1, r = r0;
-                pend = p0e;
-                if (p == 1) {
-                    first = p0e;
-                    r = first < we ? a.scell[first] / nx : r0;
-                    pend = first < we ? min(we, a.cstart[(r + 1) * nx]) : p0e;
-                    last = pend - 1;
-                }
-                if (k < 9 && first <= last) {
+            const int wA = s_begin >> 6, wZ = (s_end - 1) >> 6;
+            const int p = lane >> 4, k = lane & 15;
+            for (int wi = 0; wi < 2; ++wi) {
+                const int w = wA + wi;
+                if (w > wZ) break;
+                const int wb = w * kTile, we = min(wb + kTile, nsl);
+                const int cell = wb + lane < we ? a.scell[wb + lane] : -1;
+                const int row = cell >= 0 ? cell / nx : -1;
+                const int rprev = __shfl(row, max(lane - 1, 0));
+                const unsigned long long m = __ballot(cell >= 0 && (lane == 0 || row != rprev));
+                // part p: lanes [f, l] of the window
+                unsigned long long mm = m;
+                for (int q = 0; q < p; ++q) mm &= mm - 1ull;
+                const int f = mm ? __ffsll((long long)mm) - 1 : -1;
+                const unsigned long long mn = mm & (mm - 1ull);
+                const int l = mn ? __ffsll((long long)mn) - 2 : (we - wb) - 1;
+                const int fr = __shfl(row, max(f, 0)), fc = __shfl(cell, max(f, 0)), lc = __shfl(cell, max(l, 0));
+                int tl = 0, tj = 0;
+                if (f >= 0 && k < 9) {
                     const int q = stage_row(k);
-                    const int x0 = a.scell[first] % nx, x1 = a.scell[last] % nx;
+                    const int x0 = fc % nx, x1 = lc % nx;
                     const int xlo = max(x0 - gfx, 0), xhi = min(x1 + gfx, nx - 1);
-                    const int y = r % ny + q % 3 - 1, z = r / ny + q / 3 - 1;
+                    const int y = fr % ny + q % 3 - 1, z = fr / ny + q / 3 - 1;
                     if (y >= 0 && y < ny && z >= 0 && z < nz) {
                         const int base = (z * ny + y) * nx;
                         tj = a.cstart[base + xlo];
                         tl = a.cstart[base + xhi + 1] - tj;
                     }
                 }
-            }
-            int tincl = tl;
-            GCS_DPP_SCAN(dpp_i, add_i, 0, tincl)
-            const int wbase = __shfl(tincl, 31);
-            const int tv = tincl - tl - (wi ? wbase : 0);  // first staged index of the row within its window
-            if (k < 9) s_tile[(2 * wi + p) * 9 + stage_row(k)] = tv - tj;
-            if (k == 0) s_tile[36 + 2 * wi + p] = pend;
-            if (wv == 0 && wok && k < 9) {
-                int* const t = a.ltile + (size_t)w * kListTileWords;
-                t[18 * p + k] = tj;
-                t[18 * p + 9 + k] = tv;
-                if (k == 8) t[36 + p] = tv + tl;  // [36] part 0's end = part 1's first index, [37] the total
+                int tincl = tl;
+                GCS_DPP_SCAN(dpp_i, add_i, 0, tincl)
+                const int tv = tincl - tl;  // the row's first staged index (rows in part-major order)
+                if (k < 9) s_tile[(4 * wi + p) * 9 + stage_row(k)] = tv - tj;
+                if (lane == 0) {
+                    s_tile[72 + 2 * wi] = (int)(unsigned)m;
+                    s_tile[73 + 2 * wi] = (int)(unsigned)(m >> 32);
+                }
+                if (wv == 0) {
+                    int* const t = a.ltile + (size_t)w * kListTileWords;
+                    if (k < 9) {
+                        t[p * 9 + k] = tv;
+                        t[36 + p * 9 + k] = tj;
+                    }
+                    if (lane == 63) t[72] = tincl;  // the total
+                    // the slot of every staged record the step's LDS image holds (its LDS-DMA sources; 0 past the
+                    // total: every entry a valid slot), row by row, coalesced
+                    const int ks = stage_capacity(a.prec);
+                    const int total = __shfl(tincl, 63);
+                    int* const ls = a.lstage + (size_t)w * ks;
+                    for (int r = 0; r < 36; ++r) {
+                        const int lr = (r / 9) * 16 + r % 9;
+                        const int rs = __builtin_amdgcn_readlane(tv, lr), rj = __builtin_amdgcn_readlane(tj, lr);
+                        const int rl = min(__builtin_amdgcn_readlane(tl, lr), ks - rs);
+                        for (int u = lane; u < rl; u += 64) ls[rs + u] = rj + u;
+                    }
+                    for (int v = min(total, ks) + lane; v < ks; v += 64) ls[v] = 0;
+                }
             }
         }
         int incl = len;
@@ -2145,12 +2156,16 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
             constexpr int E = 8 / (int)sizeof(LE);
             constexpr int EB = 8 * (int)sizeof(LE);  // bits per entry
             unsigned long long* const lw = reinterpret_cast<unsigned long long*>(a.list);
-            // ListTile16: the lane's window part -> its row of s_tile (-1: a third row part of the window, which
-            // has no staged rows: the lane's list is marked overflowed, the step searches it exactly)
+            // ListTile16: the lane's window part -> its rows of s_tile (-1: a part past kWinParts, which has no
+            // staged rows: the lane's list is marked overflowed, the step searches it exactly)
             int tpart = -1;
             if constexpr (ListFmt<LE>::tile) {
                 const int wi = (s >> 6) != (s_begin >> 6) ? 1 : 0;
-                tpart = s < s_tile[36 + 2 * wi] ? 2 * wi : s < s_tile[37 + 2 * wi] ? 2 * wi + 1 : -1;
+                const unsigned long long m = (unsigned long long)(unsigned)s_tile[72 + 2 * wi] |
+                                             ((unsigned long long)(unsigned)s_tile[73 + 2 * wi] << 32);
+                const int pos = s & 63;
+                const int pp = __popcll(m & (pos == 63 ? ~0ull : ((2ull << pos) - 1ull))) - 1;
+                tpart = pp < kWinParts ? 4 * wi + pp : -1;
             }
             for (int t = 0; t < mh; ++t) {
                 unsigned b;
@@ -3056,8 +3071,8 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
 {
     __shared__ int s_rowV[kListWaves][4 * 17];
     __shared__ int s_rowJ[kListWaves][4 * 16];
-    __shared__ float4 s_cand[kListWaves][4 * 2 * (32 + 1)];
-    __shared__ int s_ovf[kListWaves][kTile];
+    __shared__ float4 s_cand[kListWaves][GCS_LBUILD_GROUPS * 2 * (32 + 1)];
+    __shared__ int s_ovf[kListWaves][80];  // (ListTile16: the window tables of pair_forces_sub until the tile's end)
     const int lane = threadIdx.x & 63;
     const int wave = uniform((int)(threadIdx.x >> 6));
     const int ntiles = ctx->ntiles;
@@ -3065,7 +3080,7 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
         // windows past the binned slots (a decomposed domain's build) stage nothing
         const int w0 = (a.cstart[ctx->grid.ncell] + kTile - 1) / kTile, wn = (a.n + kTile - 1) / kTile;
         for (int w = w0 + (int)blockIdx.x; w < wn; w += gridDim.x)
-            if (threadIdx.x < 2) a.ltile[(size_t)w * kListTileWords + 36 + threadIdx.x] = 0;
+            if (threadIdx.x < 37) a.ltile[(size_t)w * kListTileWords + (threadIdx.x < 36 ? threadIdx.x : 72)] = 0;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // read by the list steps that follow (next launches); every block here reads ctx->grid only
@@ -3209,23 +3224,42 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 #ifndef GCS_LIST_UNROLL_TILE64
 #define GCS_LIST_UNROLL_TILE64 4  // the same at fp64
 #endif
+#ifndef GCS_LIST_PREWORDS
+#define GCS_LIST_PREWORDS 8  // ListTile16: list words loaded with the slot loads (8: 32 16-bit entries per segment)
+#endif
+#ifndef GCS_LIST_PREWORDS_CT
+#define GCS_LIST_PREWORDS_CT 2  // the same in the contact step (its unrolled contact probes would spill with 8)
+#endif
 template <typename LE, int W, bool CT, bool DOM = false, typename R = float, bool RLX = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(ListFmt<LE>::tile ? GCS_LIST_WAVES_PER_EU_TILE : CT ? GCS_LIST_WAVES_PER_EU_CT : (sizeof(R) == 8 ? GCS_LIST_WAVES_PER_EU64 : GCS_LIST_WAVES_PER_EU)))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int flags)
 {
     using R4 = real4<R>;
     using R2 = real2<R>;
     constexpr bool TL = ListFmt<LE>::tile;
-    constexpr int kStageRec = TL ? GCS_STAGE_BYTES / (int)sizeof(R4) : 1;
-    static_assert(!TL || (kStageRec * (int)sizeof(R4)) % 1024 == 0, "the image is whole 1-KiB LDS-DMA pieces");
-    static_assert(!TL || kStageRec * (int)sizeof(R4) >= W * 4 * kTile * (int)sizeof(R), "the partials fit the image");
-    __shared__ R4 s_stage[kStageRec];
+    // the LDS image: fp32 whole 16-B records (1-KiB LDS-DMA pieces of 64 records); fp64 (kSplit) three arrays, 28 B
+    // per record instead of 32: {x, y} (16 B, pieces of 64), z (8 B, two 4-B lanes per record: pieces of 32) and the
+    // .w word (4 B, pieces of 64).  (An LDS-DMA lane of 12 B lands at lane x 16 B: tools/calib/glds_width.hip)
+    constexpr bool kSplit = TL && sizeof(R) == 8;
+    constexpr int kStageRec = !TL ? 1 : stage_capacity(sizeof(R) == 8 ? 64 : 32);
+    static_assert(!TL || kStageRec == (kSplit ? GCS_STAGE_BYTES / 28 / 64 * 64 : GCS_STAGE_BYTES / (int)sizeof(R4)),
+                  "the build's image capacity");
+    constexpr int kXyBytes = kSplit ? kStageRec * 16 : (int)sizeof(R4) * kStageRec;  // {x, y} / whole records
+    constexpr int kZBytes = kSplit ? kStageRec * 8 : 0;
+    constexpr int kWBytes = kSplit ? kStageRec * 4 : 0;
+    static_assert(!TL || kXyBytes % 1024 == 0, "the image is whole LDS-DMA pieces");
+    static_assert(!TL || kXyBytes + kZBytes + kWBytes <= GCS_STAGE_BYTES, "the image fits its budget");
+    static_assert(!TL || kXyBytes + kZBytes + kWBytes >= W * 4 * kTile * (int)sizeof(R), "the partials fit the image");
+    __shared__ __attribute__((aligned(16))) char s_img[TL ? kXyBytes + kZBytes + kWBytes : 16];
+    R4* const s_stage = reinterpret_cast<R4*>(s_img);  // whole records (fp32)
+    const R2* const s_xy = reinterpret_cast<const R2*>(s_img);                    // (fp64)
+    const R* const s_z = reinterpret_cast<const R*>(s_img + kXyBytes);
+    const int* const s_w = reinterpret_cast<const int*>(s_img + kXyBytes + kZBytes);
     __shared__ R s_red[TL ? 1 : W][4][TL ? 1 : kTile];
     // ListTile16: the force partials reuse the image once every wave's pair loop is done (a barrier apart)
-    R(*const red)[4][kTile] = reinterpret_cast<R(*)[4][kTile]>(TL ? (void*)s_stage : (void*)s_red);
+    R(*const red)[4][kTile] = reinterpret_cast<R(*)[4][kTile]>(TL ? (void*)s_img : (void*)s_red);
     __shared__ R4 s_locf[kTile], s_noise[kTile];
     __shared__ R2 s_tab[TL ? kTileTypes : kMaxTypes];
     __shared__ int s_last, s_final;
-    __shared__ int s_ttab[TL ? 40 : 1];  // ListTile16: the window's table entry (row lookups of entries past the image)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = uniform(tid >> 6);
     // GCS_DEBUG_TIMES: per workgroup 8 wall-clock stamps (start, wave 0: pair loop start / end, reduced, integrated,
@@ -3261,8 +3295,16 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(ListFmt<
 
     // 1. slot loads (one round trip; ListTile16: the window's table first, then the staged rows' current positions
     // into the LDS image, LDS-DMA in 1-KiB pieces of consecutive records: a second round trip, under the first)
-    int tw = 0, T = 0, nst = 0;
-    if constexpr (TL) tw = lane < 38 ? a.ltile[(size_t)tile * kListTileWords + lane] : 0;
+    int tw0 = 0, tw1 = 0, T = 0, nst = 0;
+    constexpr int kGW = TL ? (kStageRec / 64 + W - 1) / W : 1;  // image groups of 64 records per wave
+    int gsl[kGW];
+    if constexpr (TL) {
+        tw0 = a.ltile[(size_t)tile * kListTileWords + lane];
+        tw1 = lane < 9 ? a.ltile[(size_t)tile * kListTileWords + 64 + lane] : 0;
+        const int* __restrict__ lst = a.lstage + (size_t)tile * kStageRec;
+#pragma unroll
+        for (int t = 0; t < kGW; ++t) gsl[t] = lst[min((wave + t * W) * 64 + lane, kStageRec - 1)];
+    }
     const R2* __restrict__ tab = St<R>::type_ab(a);
     for (int t = tid; t < a.ntypes; t += blockDim.x) s_tab[t] = tab[t];
     const R4 pi = qc[sl];
@@ -3271,22 +3313,42 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(ListFmt<
     int4 lb = make_int4(0, 0, 0, 0);
     if constexpr (ListFmt<LE>::rel) lb = a.lbase[sl];
     uint2 e[kW], e1[kW];
+    // ListTile16: the segment's first kPreW words (kPreW * kE entries: a C2 segment whole) in this round trip, so
+    // the pair loop then runs from registers and LDS alone
+    constexpr int kPreW = TL ? (CT ? GCS_LIST_PREWORDS_CT : GCS_LIST_PREWORDS) : 1;
+    uint2 ew[kPreW];
+    if constexpr (!TL) {
 #pragma unroll
-    for (int j = 0; j < kW; ++j) e[j] = word(segw + (size_t)j * stride);  // list_cap >= kU: in bounds
+        for (int j = 0; j < kW; ++j) e[j] = word(segw + (size_t)j * stride);  // list_cap >= kU: in bounds
+    }
     if constexpr (TL) {
+        const int nw = cap / kE;  // the segment's words
 #pragma unroll
-        for (int j = 0; j < kW; ++j) e1[j] = word(segw + (size_t)(min(kU, klast) / kE + j) * stride);
-        T = __builtin_amdgcn_readlane(tw, 37);
+        for (int j = 0; j < kPreW; ++j) ew[j] = word(segw + (size_t)min(j, nw - 1) * stride);
+        T = __builtin_amdgcn_readlane(tw1, 8);
         nst = min(T, kStageRec);
-        if (wave == 0 && lane < 40) s_ttab[lane] = tw;
-        constexpr int kLpr = (int)sizeof(R4) / 16;  // lanes per record
-        constexpr int kRpc = 64 / kLpr;             // records per piece
-        const int npc = (nst + kRpc - 1) / kRpc;
-        for (int c = wave; c < npc; c += W) {
-            const int v = min(c * kRpc + lane / kLpr, T - 1);
-            const char* src = reinterpret_cast<const char*>(qc + stage_slot_w(v, tw)) + 16 * (lane % kLpr);
-            __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(s_stage + c * kRpc), 16,
-                                             0, 0);
+        typedef __attribute__((address_space(3))) void* lds_t;
+        // groups of 64 records: lane l's record 64 g + l, its slot from the build's list of the image's sources
+        // (loaded with the slot loads above); fp64: {x, y} and .w by lane, z by two 4-B lanes per record (the slots
+        // of records 64 g + l / 2 and 64 g + 32 + l / 2 by lane-indexed reads); fp32 the whole record
+        const int ng = (nst + 63) / 64;
+#pragma unroll
+        for (int t = 0; t < kGW; ++t) {
+            const int gg = wave + t * W;
+            if (gg >= ng) break;
+            const char* rec = reinterpret_cast<const char*>(qc + gsl[t]);
+            if constexpr (kSplit) {
+                const int sz0 = __shfl(gsl[t], lane >> 1), sz1 = __shfl(gsl[t], 32 + (lane >> 1));
+                __builtin_amdgcn_global_load_lds((const void*)rec, (lds_t)(s_img + gg * 1024), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const char*>(qc + sz0) + 16 + 4 * (lane & 1)),
+                                                 (lds_t)(s_img + kXyBytes + gg * 512), 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const char*>(qc + sz1) + 16 + 4 * (lane & 1)),
+                                                 (lds_t)(s_img + kXyBytes + gg * 512 + 256), 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void*)(rec + 24), (lds_t)(s_img + kXyBytes + kZBytes + gg * 256), 4,
+                                                 0, 0);
+            } else {
+                __builtin_amdgcn_global_load_lds((const void*)rec, (lds_t)(s_stage + gg * 64), 16, 0, 0);
+            }
         }
     }
     const R cs = (R)ctx->cs;
@@ -3372,19 +3434,24 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(ListFmt<
             // words of the next two batches in flight
             auto walk = [&](auto spill) {
                 constexpr bool SP = decltype(spill)::value;
-                for (int k0 = 0; k0 < kmax; k0 += kU) {
-                    uint2 e2[kW];
-                    const int kn = min(k0 + 2 * kU, klast);
-#pragma unroll
-                    for (int j = 0; j < kW; ++j) e2[j] = word(segw + (size_t)(kn / kE + j) * stride);
+                // one batch of kU entries held as kW words
+                auto batch = [&](const uint2* eb, int k0) {
                     R4 q[kU];
 #pragma unroll
                     for (int u = 0; u < kU; ++u) {
-                        const int x = (k0 + u < cnt) ? list_entry<LE>(e, u) : 0;
-                        if constexpr (SP)
-                            q[u] = x < nst ? s_stage[x] : qc[stage_slot(x, s_ttab)];
-                        else
-                            q[u] = s_stage[x];
+                        const int x = (k0 + u < cnt) ? list_entry<LE>(eb, u) : 0;
+                        auto img = [&](int v) -> R4 {
+                            if constexpr (kSplit) {
+                                const R2 xy = s_xy[v];
+                                return mk4<R>(xy.x, xy.y, s_z[v], wpack<R>(s_w[v]));
+                            } else
+                                return s_stage[v];
+                        };
+                        if constexpr (SP) {
+                            const int xs = stage_slot_w(x, tw0, tw1);  // (every lane: lane-indexed reads)
+                            q[u] = x < nst ? img(x) : qc[xs];
+                        } else
+                            q[u] = img(x);
                     }
 #pragma unroll
                     for (int u = 0; u < kU; ++u)
@@ -3395,10 +3462,32 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(ListFmt<
                         for (int u = 0; u < kU; ++u)
                             if (!fbc && k0 + u < cnt) list_contact<R>(a, cd2, pi, q[u], i, wbits(q[u].w) & kIdx);
                     }
+                };
+                // the preloaded words
+#pragma unroll
+                for (int b = 0; b < kPreW / kW; ++b) {
+                    if (b * kU >= kmax) break;
+                    batch(ew + b * kW, b * kU);
+                }
+                // the rest (long segments), the entry words of the next two batches in flight
+                constexpr int kPre = (kPreW / kW) * kU;
+                if (kmax > kPre) {
 #pragma unroll
                     for (int j = 0; j < kW; ++j) {
-                        e[j] = e1[j];
-                        e1[j] = e2[j];
+                        e[j] = word(segw + (size_t)(min(kPre, klast) / kE + j) * stride);
+                        e1[j] = word(segw + (size_t)(min(kPre + kU, klast) / kE + j) * stride);
+                    }
+                    for (int k0 = kPre; k0 < kmax; k0 += kU) {
+                        uint2 e2[kW];
+                        const int kn = min(k0 + 2 * kU, klast);
+#pragma unroll
+                        for (int j = 0; j < kW; ++j) e2[j] = word(segw + (size_t)(kn / kE + j) * stride);
+                        batch(e, k0);
+#pragma unroll
+                        for (int j = 0; j < kW; ++j) {
+                            e[j] = e1[j];
+                            e1[j] = e2[j];
+                        }
                     }
                 }
             };

@@ -570,18 +570,23 @@ def test_list_formats_bitwise_c1(c1_design, prec, fmt):
 
 @precisions
 def test_relative_entries_c5_bitwise(prec):
-    """N > 65,536 (C5, 606,248 particles, its dense synthetic start): the default tile-staged entries (many tiles'
-    partner rows exceed the LDS image there: those entries are gathered through the row table) and the plane-relative
-    16-bit slots against 32-bit slots -- every partner within the plane span (no escape to the exact search), so
-    bitwise the same"""
+    """N > 65,536 (C5, 606,248 particles, its dense synthetic start): the plane-relative 16-bit slots against 32-bit
+    slots -- every partner within the plane span (no escape to the exact search), so bitwise the same; the default
+    tile-staged entries (many windows' partner rows exceed the LDS image there: those entries are gathered through
+    the window table) within the precision's bound of them"""
     cfg = resolution_scaled(InterphaseConfig(), 10.0)
     design = synthetic.make_c5()
     ctx = {"step": 0, "time": 0.0, "core_scale": 1.0, "bond_scale": 1.0, "wall_semiaxes": LATE["wall_semiaxes"]}
     x2, s2 = _format_run(design, cfg, prec, 2, 20, ctx=ctx)
-    for fmt in (0, 1):
-        x0, s0 = _format_run(design, cfg, prec, fmt, 20, ctx=ctx)
-        assert s0["fallback_particle_steps"] == s2["fallback_particle_steps"], (fmt, s0, s2)
-        assert np.array_equal(x0, x2), fmt
+    x1, s1 = _format_run(design, cfg, prec, 1, 20, ctx=ctx)
+    assert s1["fallback_particle_steps"] == s2["fallback_particle_steps"], (s1, s2)
+    assert np.array_equal(x1, x2)
+    # the tile-staged entries: the same pairs, except that the rare particle in a 5th+ cell-row part of its
+    # 64-slot window (kernels.hip kWinParts) is searched exactly (its sum in another order): within the bound
+    x0, s0 = _format_run(design, cfg, prec, 0, 20, ctx=ctx)
+    extra = s0["fallback_particle_steps"] - s2["fallback_particle_steps"]
+    assert 0 <= extra < 1e-4 * design.n * 20, (s0, s2)
+    assert np.abs(x0 - x2).max() <= TOL_X[prec]
 
 
 @precisions
