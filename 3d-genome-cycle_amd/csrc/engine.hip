@@ -1990,6 +1990,7 @@ bool small_path(const gcs_engine* e, bool spacestep)
 {
     return e->small_opt != 0 && !e->fused_explicit && !spacestep && !e->dom && e->n >= 1 && e->n <= kPMax;
 }
+constexpr int kPDebugWords = 1024 + 64 * 128;  // GCS_DEBUG_PSTEP: kernels.hip k_pstep's stamps
 constexpr int kPChunk = 2048;  // steps per cooperative launch (a launch then lasts ~10 ms)
 
 int run_small(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64_t steps)
@@ -2000,6 +2001,14 @@ int run_small(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64
     if (!e->psync && (rc = dalloc(&e->psync, kPSyncWords))) return rc;
     ForceArgs a = e->fa;
     a.psync = e->psync;
+    // GCS_DEBUG_PSTEP=<file>: workgroup 0's phase stamps of the first 64 steps of the call's first launch
+    const char* dbg_path = std::getenv("GCS_DEBUG_PSTEP");
+    unsigned long long* dbg = nullptr;
+    if (dbg_path) {
+        HIPCHK(hipMalloc(&dbg, kPDebugWords * sizeof(unsigned long long)));
+        HIPCHK(hipMemsetAsync(dbg, 0, kPDebugWords * sizeof(unsigned long long), e->stream));
+        a.dbg_times = dbg;
+    }
     for (int64_t done = 0; done < steps;) {
         const int len = (int)std::min<int64_t>(kPChunk, steps - done);
         HIPCHK(hipMemsetAsync(e->psync, 0, kPSyncWords * sizeof(unsigned), e->stream));
@@ -2007,8 +2016,19 @@ int run_small(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64
             return fail(GCS_EHIP, "the persistent small-system step could not be launched cooperatively");
         e->rstats.eager_steps += len;
         done += len;
+        a.dbg_times = nullptr;
     }
     HIPCHK(hipGetLastError());
+    if (dbg) {
+        std::vector<unsigned long long> h(kPDebugWords);
+        HIPCHK(hipMemcpyAsync(h.data(), dbg, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipFree(dbg));
+        if (FILE* f = std::fopen(dbg_path, "wb")) {
+            std::fwrite(h.data(), sizeof(h[0]), h.size(), f);
+            std::fclose(f);
+        }
+    }
     end_run(e, cfg, first_step, steps);
     e->chain_valid = false;  // no cell or neighbour lists of these positions
     if (steps & 1) e->parity ^= 1;

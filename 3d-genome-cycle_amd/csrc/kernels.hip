@@ -1285,12 +1285,14 @@ __device__ inline void philox_normal3(unsigned seed_lo, unsigned seed_hi, long l
 }
 
 template <typename R>
-__device__ inline void noise3(const ForceArgs& a, const DevCtx* ctx, int i, R& n0, R& n1, R& n2)
+__device__ inline void noise3(const ForceArgs& a, const DevCtx* ctx, int i, R& n0, R& n1, R& n2, int ahead = 0)
 {
+    // ahead: the noise of the step that many steps after the context's next one (k_pstep: the next step's, before
+    // the tail has advanced the context)
     if (a.noise_mode == GCS_NOISE_PHILOX) {
-        philox_normal3<R>(a.seed_lo, a.seed_hi, ctx->step + 1, i, n0, n1, n2);
+        philox_normal3<R>(a.seed_lo, a.seed_hi, ctx->step + 1 + ahead, i, n0, n1, n2);
     } else if (a.noise_mode == GCS_NOISE_INJECTED) {
-        long long cur = ctx->noise_cursor;
+        long long cur = ctx->noise_cursor + ahead;
         if (cur >= a.noise_steps) cur = a.noise_steps - 1;  // host checks the budget before launching
         const R* p = St<R>::noise(a) + (cur * (long long)a.n + i) * 3;
         n0 = p[0];
@@ -1329,8 +1331,11 @@ __device__ inline R spring_coef(int type, R K, R l, R r2, R& U)
 template <int MODE, int BB = 1, typename R = float>
 __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceArgs& a, int i, R xi, R yi, R zi,
                                    real4<R> km, R& fx, R& fy, R& fz, R* en, R* rin, R* rout,
-                                   int2 erange = make_int2(-1, -1), const real4<R>* posv = nullptr)
+                                   int2 erange = make_int2(-1, -1), const real4<R>* posv = nullptr, int lq = 0,
+                                   int nq = 1)
 {
+    // lq / nq: this lane's share when nq lanes hold the same particle (k_pstep): bonded entries, droplet targets,
+    // bending roles and tethers strided over them, the point sources and walls on lq == 0; the caller sums the lanes
     const int n = a.n;
     const FieldPrm<R>& P = St<R>::prm(a);
     // the step-start positions of the partners: the context's buffer, or posv (k_pstep: its LDS image)
@@ -1342,7 +1347,7 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
         // erange: the particle's CSR row when the caller already has it (the list step's slot-ordered copy)
         const int eb = erange.x >= 0 ? erange.x : a.boff[i], ee = erange.x >= 0 ? erange.y : a.boff[i + 1];
         const real4<R>* __restrict__ bval = St<R>::bval(a);
-        for (int q0 = eb; q0 < ee; q0 += BB) {
+        for (int q0 = eb + lq * BB; q0 < ee; q0 += nq * BB) {
           int2 enb[BB];
           real4<R> bvb[BB], pjb[BB];
 #pragma unroll
@@ -1393,7 +1398,7 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
             const int m = a.sw_n;
             const int jt = (__lane_id() < m) ? a.sw_idx[__lane_id()] : 0;
             const real4<R> pt = posc[jt];
-            for (int t = 0; t < m; ++t) {
+            for (int t = lq; t < m; t += nq) {
                 const int j = __shfl(jt, t);
                 const R px = __shfl(pt.x, t), py = __shfl(pt.y, t), pz = __shfl(pt.z, t);
                 const R rx = xi - px, ry = yi - py, rz = zi - pz;
@@ -1413,7 +1418,7 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
 
     if (a.has_bend) {
         const R* __restrict__ bend = St<R>::bend(a);
-        for (int role = 0; role < 3; ++role) {
+        for (int role = lq; role < 3; role += nq) {
             const int k0 = i - role;
             if (k0 < 0 || k0 + 2 >= n) continue;
             const R eps = bend[k0];
@@ -1445,7 +1450,7 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
     if (a.has_tether) {
         const int tb = a.toff[i], te = a.toff[i + 1];
         const TetherT<R>* __restrict__ tent = St<R>::tent(a);
-        for (int q = tb; q < te; ++q) {
+        for (int q = tb + lq; q < te; q += nq) {
             const TetherT<R> t = tent[q];
             const R rx = xi - t.px, ry = yi - t.py, rz = zi - t.pz;
             R U;
@@ -1459,7 +1464,7 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
 
 #pragma unroll
     for (int q = 0; q < kMaxPointSources; ++q) {
-        if (q >= a.n_point) break;
+        if (q >= a.n_point || lq != 0) break;
         PointSrcT<R> p = P.point[q];
         // opaque to the optimizer: keeps the (rarely used, mitotic-only) point-source constants from being hoisted
         // to the kernel entry, where they would be spilled to scratch by every wave
@@ -1482,7 +1487,7 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
         fz = r_fma(c, rz, fz);
     }
 
-    if (a.has_wall_in || a.has_wall_out) {
+    if ((a.has_wall_in || a.has_wall_out) && lq == 0) {
         // Sampson distance to the ellipsoid (DESIGN.md "ellipsoid wall"): rho = |r o 1/ax|,
         // g = r o 1/ax^2, d = |1 - rho| rho / |g|, normal n = g / |g|
         const R ax = (R)ctx->wall[0], ay = (R)ctx->wall[1], az = (R)ctx->wall[2];
@@ -3896,29 +3901,131 @@ __global__ __launch_bounds__(kLUpdateBlock) void k_lupdate(DevCtx* __restrict__ 
 #define GCS_PSTEP_SPIN (1 << 22)  // grid-barrier polls before a workgroup gives up (DevCtx::scan_stall; the host fails)
 #endif
 constexpr int kPWaves = 4;
-constexpr int kPSyncSet = 64;                  // psync: [0] the barrier counter, the sets from word 64
-constexpr int kPSetWords = 32 * kAccWords;     // one accumulator set (acc_fold's layout: 128 B per slot)
+constexpr int kPP = 16;          // particles per workgroup; a wave's lanes are kPP particles x (64 / kPP) segments
+constexpr int kHitCap = 64;      // prefilter hits listed per lane before a flush
+// the hand-off (a.psync, zeroed before every launch): two halves, step k writes half k & 1 with tag k + 1.  A half:
+// every particle's record (fp64: 3 chunks, fp32: 2), then every workgroup's 8 chunks of partial totals (6 reactions,
+// the neighbour count).  A chunk is 16 B = two 8-B granules {data word, tag}: written by one sc1 store, read by sc1
+// loads, each granule checked by its own tag (MI355X_MICROARCH.md, the tagged-granule hand-off: no fence, no
+// counter, no ordering between granules).  Step k + 2 overwrites half k & 1 only after every workgroup has read it:
+// a workgroup writes step k + 2's records after it read all of step k + 1's, which every workgroup wrote after it
+// had read step k's.
+template <typename R> constexpr int kPRecBytes = sizeof(R) == 8 ? 48 : 32;
+// a workgroup's totals: records kPMax + TR g .. (TR = 3 fp64 / 4 fp32 records: 9 / 8 chunks, 7 used, one double each)
+template <typename R> constexpr int kPTotRecs = sizeof(R) == 8 ? 3 : 4;
+template <typename R> constexpr int kPTotChunks = kPTotRecs<R> * kPRecBytes<R> / 16;
+template <typename R> constexpr int kPTotOff = kPMax * kPRecBytes<R>;
+template <typename R> constexpr int kPTotBytes = kPTotRecs<R> * kPRecBytes<R>;
+constexpr int kPGroups = (kPMax + kPP - 1) / kPP;
+static_assert(kPTotOff<double> + kPTotBytes<double> * kPGroups <= kPHalfBytes, "psync half");
+static_assert(kPTotOff<float> + kPTotBytes<float> * kPGroups <= kPHalfBytes, "psync half");
 
-// the totals of one accumulator set (the slots the persistent step folds: reactions, neighbours), read-only
-__device__ __forceinline__ void pset_totals(unsigned* base, ListTotals& t)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t phalf_rsrc(char* half, int bytes)
 {
-    unsigned long long v[7], lo[6];
-    for (int k = 0; k < 7; ++k) v[k] = __hip_atomic_load(acc_slot(base, k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int k = 0; k < 6; ++k)
-        lo[k] = __hip_atomic_load(acc_slot(base, kAccReactLo + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned bad = __hip_atomic_load(reinterpret_cast<unsigned*>(acc_slot(base, kListAccSlots)), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-    for (int k = 0; k < 6; ++k)
-        t.react[k] = (bad & 1u) ? __longlong_as_double(0x7ff8000000000000ll)
-                                : (double)(long long)v[k] * 0x1p-20 + (double)(long long)lo[k] * 0x1p-52;
-    t.nbr = (double)v[6];
-    t.ld = 0.f;
-    t.nfb = 0;
-    t.nown = 0;
-    for (int k = 0; k < 6; ++k) t.bb[k] = 0.f;
-    t.drift = 0.0;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)half, 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ void pput_chunk(char* half, int off, unsigned d0, unsigned d1, unsigned tag)
+{
+    st_sc1_f4(phalf_rsrc(half, kPHalfBytes), off,
+              make_float4(__uint_as_float(d0), __uint_as_float(tag), __uint_as_float(d1), __uint_as_float(tag)));
+}
+__device__ __forceinline__ void pput_double(char* half, int off, double v, unsigned tag)
+{
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    pput_chunk(half, off, (unsigned)b, (unsigned)(b >> 32), tag);
+}
+template <typename R>
+__device__ __forceinline__ void pput_record(char* half, int i, const real4<R>& p, unsigned tag)
+{
+    const int o = i * kPRecBytes<R>;
+    if constexpr (sizeof(R) == 8) {
+        pput_double(half, o, p.x, tag);
+        pput_double(half, o + 16, p.y, tag);
+        pput_double(half, o + 32, p.z, tag);
+    } else {
+        pput_chunk(half, o, __float_as_uint(p.x), __float_as_uint(p.y), tag);
+        pput_chunk(half, o + 16, __float_as_uint(p.z), 0u, tag);
+    }
+}
+__device__ __forceinline__ bool pchunk_ok(const int4& v, unsigned tag)
+{
+    return (unsigned)v.y == tag && (unsigned)v.w == tag;
+}
+__device__ __forceinline__ double pchunk_double(const int4& v)
+{
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)v.z << 32) | (unsigned)v.x));
 }
 
+// the image of step tag and the G workgroups' partial totals: thread t of T walks u = t, t + T, ... over the n
+// records and then the G kPTotRecs totals records (record kPMax + u - n), a batch's loads issued together, polls
+// until every granule carries the tag (a stall after GCS_PSTEP_SPIN polls: counted, the host fails); records into
+// s_pos and the fp32 coordinate arrays s_pfx / s_pfy / s_pfz, totals chunks (one double each) into s_tot
+template <typename R, typename Mid>
+__device__ __forceinline__ void pget_image(char* half, int n, int G, int t, int T, unsigned tag, real4<R>* s_pos,
+                                           float* s_pfx, float* s_pfy, float* s_pfz, double* s_tot,
+                                           volatile int* stall, Mid&& mid, unsigned long long* dbg = nullptr)
+{
+    // mid(): work of the caller's that runs while the first batch's loads are in flight
+    constexpr int C = sizeof(R) == 8 ? 3 : 2, RB = sizeof(R) == 8 ? 4 : 6, RBY = kPRecBytes<R>;
+    const int nu = n + G * kPTotRecs<R>;
+    const auto rp = phalf_rsrc(half, kPHalfBytes);
+    auto rec = [&](int u) { return u < n ? u : kPMax + (u - n); };
+    for (int u0 = 0; u0 < nu; u0 += RB * T) {
+        int4 v[RB][C];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            const int u = u0 + t + r * T;
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[r][c] = u < nu ? ld_sc1_i4(rp, rec(u) * RBY + 16 * c) : int4{};
+        }
+        if (u0 == 0) mid();
+        for (int spin = 0;; ++spin) {
+            bool ok = true;
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+#pragma unroll
+                for (int c = 0; c < C; ++c) ok = ok && (u0 + t + r * T >= nu || pchunk_ok(v[r][c], tag));
+            if (dbg && u0 == 0) {
+                if (spin == 0) dbg[0] = wall_clock64();
+                dbg[1] = spin;
+            }
+            if (ok) break;
+            if (*stall || spin >= GCS_PSTEP_SPIN) {
+                *stall = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+                const int u = u0 + t + r * T;
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+                    if (u < nu && !pchunk_ok(v[r][c], tag)) v[r][c] = ld_sc1_i4(rp, rec(u) * RBY + 16 * c);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            const int u = u0 + t + r * T;
+            if (u < n) {
+                real4<R> p;
+                if constexpr (sizeof(R) == 8) {
+                    p = mk4<R>(pchunk_double(v[r][0]), pchunk_double(v[r][1]), pchunk_double(v[r][2]), R(0));
+                } else {
+                    p = mk4<R>(__int_as_float(v[r][0].x), __int_as_float(v[r][0].z), __int_as_float(v[r][1].x), R(0));
+                }
+                s_pos[u] = p;
+                s_pfx[u] = (float)p.x;
+                s_pfy[u] = (float)p.y;
+                s_pfz[u] = (float)p.z;
+            } else if (u < nu) {
+#pragma unroll
+                for (int c = 0; c < C; ++c) s_tot[(u - n) * C + c] = pchunk_double(v[r][c]);
+            }
+        }
+    }
+}
+
+constexpr int kPDbgSteps = 32;  // GCS_DEBUG_PSTEP: the steps stamped (the first of the launch)
 template <typename R>
 __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx, ForceArgs a, int steps, int flags)
 {
@@ -3926,22 +4033,34 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
     using R2 = real2<R>;
     constexpr int W = kPWaves;
     __shared__ R4 s_pos[kPMax];      // every particle's position at the step start (particle order)
-    __shared__ float4 s_pf[kPMax];   // its fp32 rounding (the prefilter)
+    // its fp32 rounding (the prefilter), by coordinate (a b128 read: 4 candidates; padded for the last chunk's reads)
+    __shared__ __attribute__((aligned(16))) float s_pfx[kPMax + 32], s_pfy[kPMax + 32], s_pfz[kPMax + 32];
     __shared__ R2 s_ab[kPMax];       // its pair factors (a, b)
+    constexpr int Q = kTile / kPP;   // candidate segments per wave (lane group q = lane / kPP)
     __shared__ R red[W][4][kTile];
-    __shared__ R4 s_locf[kTile], s_noise[kTile];
+    __shared__ R4 s_locf[kPP], s_noise[2][kPP];  // (the noise by step parity: the next step's is made early)
+    __shared__ int s_stall;
+    __shared__ unsigned long long s_dbg[kPDbgSteps][16], s_dbw[kPDbgSteps];  // GCS_DEBUG_PSTEP stamps
+    __shared__ double s_react[6];  // the workgroup's wall reactions of the step (wave W - 1 -> wave 0)
+    __shared__ double s_tot[kPGroups * kPTotChunks<R>];  // the step's partial totals, by workgroup
     __shared__ DevCtx s_ctx;
+    __shared__ unsigned short s_hit[kPWaves][kHitCap][kTile];  // per wave: each lane's prefilter hits (column)
     // (fp32: pad the workgroup beyond half a CU's LDS -- one workgroup per CU, the hand-off's validated form)
-    __shared__ char s_pad[sizeof(R) == 4 ? 48 * 1024 : 16];
+    __shared__ char s_pad[sizeof(R) == 4 ? 32 * 1024 : 16];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = uniform(tid >> 6);
     const int n = a.n;
     const int G = gridDim.x;
-    const int i = blockIdx.x * kTile + lane;
+    const int pl = lane & (kPP - 1), lq = lane / kPP;
+    const int i = blockIdx.x * kPP + pl;
     const bool valid = i < n;
+    const bool lead = valid && lq == 0;  // the lane that stores / folds particle i (the others hold copies)
     const int il = valid ? i : n - 1;
-    unsigned* const sync = a.psync;
-    if (tid == 0) s_pad[0] = 0;
+    unsigned* const sync = a.psync;  // the hand-off halves
+    if (tid == 0) {
+        s_pad[0] = 0;
+        s_stall = 0;
+    }
     const FieldPrm<R>& P = St<R>::prm(a);
     const R4* __restrict__ kmu = St<R>::kmu(a);
 
@@ -3960,7 +4079,9 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
     for (int j = tid; j < n; j += blockDim.x) {
         const R4 p = St<R>::pos(a, par)[j];
         s_pos[j] = p;
-        s_pf[j] = make_float4((float)p.x, (float)p.y, (float)p.z, 0.f);
+        s_pfx[j] = (float)p.x;
+        s_pfy[j] = (float)p.y;
+        s_pfz[j] = (float)p.z;
     }
     R4 km = mk4<R>(R(0), R(0), R(0), R(0));
     int2 erow = make_int2(0, 0);
@@ -3969,15 +4090,32 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
         erow = a.has_bonds ? make_int2(a.boff[il], a.boff[il + 1]) : make_int2(0, 0);
     }
     const R2 own = s_ab[il];  // (s_ab was filled before the barrier above)
-    const int j0 = wave * n / W, j1 = (wave + 1) * n / W;  // this wave's candidates
+    // this lane's candidates [cj0, cj1): the wave's share of the candidates in 1/64, split evenly over its Q lane
+    // groups.  The local-terms wave (W - 1) takes a share that grows with n from none at ~600 particles (its terms
+    // then take about as long as the others' pairs: 2.6 us against ~3.1 us at 586) to 4/64 at ~1,100 (3.8 us
+    // against ~5.7 at 1,172), waves 0..2 split the rest.  Static: the sum order is the same at every step and chunk.
+    int cj0, cj1;
+    {
+        static_assert(kPWaves == 4, "four waves");
+        const int s3 = min(8, max(0, (n - 600) / 128));
+        const int rest = 64 - s3;
+        int sh[4] = {rest / 3 + (rest % 3 > 0), rest / 3 + (rest % 3 > 1), rest / 3, s3};
+        int b = 0;
+        for (int w = 0; w < wave; ++w) b += sh[w];
+        cj0 = (int)((long long)n * (b * Q + lq * sh[wave]) / (64 * Q));
+        cj1 = (int)((long long)n * (b * Q + (lq + 1) * sh[wave]) / (64 * Q));
+    }
 
     for (int k = 0; k < steps; ++k) {
-        unsigned* const acc = sync + kPSyncSet + (k % 3) * kPSetWords;
-        if (blockIdx.x == 0 && tid < kListAccSlots + 1) {  // clear the set of step k + 1
-            unsigned long long* w = acc_slot(sync + kPSyncSet + ((k + 1) % 3) * kPSetWords, tid);
-            __hip_atomic_store(w, list_acc_identity(tid), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();  // s_pos / s_pf of this step, s_ctx
+        __syncthreads();  // s_pos / s_pf* of this step, s_ctx
+        const unsigned tag = (unsigned)k + 1u;  // step k's hand-off: half k & 1, tag k + 1
+        char* const half = reinterpret_cast<char*>(sync) + (k & 1) * kPHalfBytes;
+        // debug stamps (GCS_DEBUG_PSTEP): workgroup 0's phases of the first 64 steps ([16 k ...]), every workgroup's
+        // hand-off time ([1024 + 128 k + workgroup])
+        // (kept in LDS and written out at the end: a global store would hold the storing wave's next vmcnt wait)
+        unsigned long long* const dbs = (a.dbg_times && blockIdx.x == 0 && k < kPDbgSteps) ? s_dbg[k] : nullptr;
+        unsigned long long* const dbw = (a.dbg_times && k < kPDbgSteps) ? &s_dbw[k] : nullptr;
+        if (dbs && tid == 0) dbs[0] = wall_clock64();
         const R4 pi = s_pos[il];
         const R cs = (R)s_ctx.cs;
         const R scale = a.pair_scaled ? cs : R(1);
@@ -3987,24 +4125,41 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
         const R rc = pair_cutoff_r<R>(a, (double)cs), rc2 = rc * rc;
         const R ahi = kA * own.x, bhi = kB * own.y;
 
-        // the particle-local terms first on the last wave (image positions), the reactions into the set
+        if (k == 0 && wave == 1) {  // the first step's noise (the later steps': while the previous hand-off lands)
+            R n0, n1, n2;
+            noise3<R>(a, &s_ctx, il, n0, n1, n2);
+            if (lq == 0) s_noise[0][pl] = mk4<R>(n0, n1, n2, R(0));
+        }
+        // the particle-local terms first on the last wave (image positions); the workgroup's reaction partials out
         if (wave == W - 1) {
             R lfx = 0, lfy = 0, lfz = 0, en[kEnergyKinds];
             R rin[3] = {0, 0, 0}, rout[3] = {0, 0, 0};
             local_terms<kModeStep, sizeof(R) == 8 ? GCS_LIST_BOND_BATCH64 : GCS_LIST_BOND_BATCH, R>(
-                &s_ctx, a, il, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout, erow, s_pos);
-            s_locf[lane] = mk4<R>(lfx, lfy, lfz, km.x);
+                &s_ctx, a, il, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout, erow, s_pos, lq, Q);
+#pragma unroll
+            for (int o = kPP; o < kTile; o <<= 1) {  // the lane groups' shares, in a fixed order
+                lfx += __shfl_down(lfx, o);
+                lfy += __shfl_down(lfy, o);
+                lfz += __shfl_down(lfz, o);
+            }
+            if (lq == 0) s_locf[pl] = mk4<R>(lfx, lfy, lfz, km.x);
             R rv = 0;
 #pragma unroll
             for (int c = 0; c < 6; ++c) {
-                const R x = wave_sum_r(valid ? (c < 3 ? rin[c] : rout[c - 3]) : R(0));
+                const R x = wave_sum_r(lead ? (c < 3 ? rin[c] : rout[c - 3]) : R(0));
                 if (lane == c) rv = x;
             }
-            if (lane < 6) acc_fold(acc, lane, (double)rv);
+            // (published by wave 0 with its hand-off: a store here would hold this wave's next vmcnt wait -- loads
+            // and stores share the counter -- until the write-through store is acknowledged, ~1 us)
+            if (lane < 6) s_react[lane] = (double)rv;
+            if (dbs && lane == 0) dbs[1] = wall_clock64();
         }
 
-        // pairs: this wave's quarter of the candidates, 32 at a time: the fp32 prefilter -> a hit mask, then the
-        // exact pair in R for each hit in index order
+        // pairs: this wave's share of the candidates (the local-terms wave a smaller one), 32 at a time through the
+        // fp32 prefilter; each lane appends its hits (ascending index) to its column of the wave's hit list, and the
+        // exact pairs in R run over the list -- wave-max(hits) iterations instead of one per hit of the chunk's
+        // densest lane, chunk after chunk (the candidates of a chunk are a chain segment: its hits bunch on a few
+        // lanes).  A list that could overflow is flushed first.
         R fx = 0, fy = 0, fz = 0, nbr = 0;
         if (a.has_pair) {
             const float pxf = (float)pi.x, pyf = (float)pi.y, pzf = (float)pi.z;
@@ -4012,109 +4167,162 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
             const float thr = (float)rc2 * 1.001f + 1.0e-4f * (float)rc;
             typedef float f2 __attribute__((ext_vector_type(2)));
             const f2 PX = {pxf, pxf}, PY = {pyf, pyf}, PZ = {pzf, pzf};
-            for (int c0 = j0; c0 < j1; c0 += 32) {
+            unsigned short* const hl = &s_hit[wave][0][0];
+            int cnt = 0;
+            auto flush = [&]() {
+                const int kmax = uniform(wave_max_int(cnt));
+                for (int q = 0; q < kmax; ++q) {
+                    const bool real = q < cnt;
+                    const int j = real ? hl[q * kTile + lane] : il;
+                    list_pair<R>(pi.x, pi.y, pi.z, s_pos[j], s_ab[j], ahi, bhi, kA, kB, k2a, k2b, rc2, real, fx, fy,
+                                 fz, nbr);
+                }
+                cnt = 0;
+            };
+            const float4* const X4 = reinterpret_cast<const float4*>(s_pfx);
+            const float4* const Y4 = reinterpret_cast<const float4*>(s_pfy);
+            const float4* const Z4 = reinterpret_cast<const float4*>(s_pfz);
+            // chunks from cj0 rounded down to 4 (b128 reads of 4 candidates a coordinate; the 16 candidates of a half
+            // chunk loaded together), the candidates outside [cj0, cj1) masked
+            for (int c0 = cj0 & ~3; c0 < cj1; c0 += 32) {
                 unsigned m = 0u;
 #pragma unroll
-                for (int h = 0; h < 16; ++h) {
-                    const int ja = min(c0 + 2 * h, kPMax - 1), jb = min(c0 + 2 * h + 1, kPMax - 1);
-                    const float4 A = s_pf[ja], B = s_pf[jb];
-                    const f2 dx = f2{A.x, B.x} - PX, dy = f2{A.y, B.y} - PY, dz = f2{A.z, B.z} - PZ;
-                    const f2 r2 = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
-                    m |= (r2.x < thr ? 1u : 0u) << (2 * h);
-                    m |= (r2.y < thr ? 1u : 0u) << (2 * h + 1);
+                for (int hh = 0; hh < 2; ++hh) {
+                    float4 X[4], Y[4], Z[4];
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int q = (c0 >> 2) + 4 * hh + g;
+                        X[g] = X4[q];
+                        Y[g] = Y4[q];
+                        Z[g] = Z4[q];
+                    }
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const f2 dx0 = f2{X[g].x, X[g].y} - PX, dx1 = f2{X[g].z, X[g].w} - PX;
+                        const f2 dy0 = f2{Y[g].x, Y[g].y} - PY, dy1 = f2{Y[g].z, Y[g].w} - PY;
+                        const f2 dz0 = f2{Z[g].x, Z[g].y} - PZ, dz1 = f2{Z[g].z, Z[g].w} - PZ;
+                        const f2 r0 = __builtin_elementwise_fma(dz0, dz0, __builtin_elementwise_fma(dy0, dy0, dx0 * dx0));
+                        const f2 r1 = __builtin_elementwise_fma(dz1, dz1, __builtin_elementwise_fma(dy1, dy1, dx1 * dx1));
+                        const int b = 16 * hh + 4 * g;
+                        m |= (r0.x < thr ? 1u : 0u) << b;
+                        m |= (r0.y < thr ? 1u : 0u) << (b + 1);
+                        m |= (r1.x < thr ? 1u : 0u) << (b + 2);
+                        m |= (r1.y < thr ? 1u : 0u) << (b + 3);
+                    }
                 }
-                const int rem = j1 - c0;
+                if (c0 < cj0) m &= ~((1u << (cj0 - c0)) - 1u);
+                const int rem = cj1 - c0;
                 if (rem < 32) m &= (1u << rem) - 1u;
                 if ((unsigned)(i - c0) < 32u) m &= ~(1u << (i - c0));  // not itself
                 if (!valid) m = 0u;
-                while (__ballot(m != 0u)) {
-                    const int b = m ? __ffs(m) - 1 : 0;
-                    const bool real = m != 0u;
+                if (__ballot(cnt + __popc(m) > kHitCap)) flush();
+                while (m) {
+                    hl[cnt * kTile + lane] = (unsigned short)(c0 + __ffs(m) - 1);
+                    ++cnt;
                     m &= m - 1u;
-                    const int j = c0 + b;
-                    list_pair<R>(pi.x, pi.y, pi.z, s_pos[j], s_ab[j], ahi, bhi, kA, kB, k2a, k2b, rc2, real, fx, fy, fz,
-                                 nbr);
                 }
             }
+            if (dbs && lane == 0 && wave == 0) dbs[8] = wall_clock64();
+            flush();
         }
-        if (wave == (W > 1 ? 1 : 0)) {  // the noise (depends on the particle and the step only)
-            R n0, n1, n2;
-            noise3<R>(a, &s_ctx, il, n0, n1, n2);
-            s_noise[lane] = mk4<R>(n0, n1, n2, R(0));
+        if (dbs && lane == 0) dbs[wave == 0 ? 2 : 8 + wave] = wall_clock64();
+        // the lane groups' sums in a fixed order ((q0 + q1) + (q2 + q3)), lanes of group 0 keep them
+#pragma unroll
+        for (int o = kPP; o < kTile; o <<= 1) {
+            fx += __shfl_down(fx, o);
+            fy += __shfl_down(fy, o);
+            fz += __shfl_down(fz, o);
+            nbr += __shfl_down(nbr, o);
         }
-        red[wave][0][lane] = fx;
-        red[wave][1][lane] = fy;
-        red[wave][2][lane] = fz;
-        red[wave][3][lane] = nbr;
+        if (lq == 0) {
+            red[wave][0][pl] = fx;
+            red[wave][1][pl] = fy;
+            red[wave][2][pl] = fz;
+            red[wave][3][pl] = nbr;
+        }
         __syncthreads();
 
-        // integrate (wave 0): the new position, stored write-through for the other workgroups
         if (wave == 0) {
-            R fsx = red[0][0][lane], fsy = red[0][1][lane], fsz = red[0][2][lane], ns = red[0][3][lane];
+            // integrate: the new position (the waves' sums in wave order), handed off as tagged granules
+            R fsx = red[0][0][pl], fsy = red[0][1][pl], fsz = red[0][2][pl], ns = red[0][3][pl];
 #pragma unroll
             for (int w = 1; w < W; ++w) {
-                fsx += red[w][0][lane];
-                fsy += red[w][1][lane];
-                fsz += red[w][2][lane];
-                ns += red[w][3][lane];
+                fsx += red[w][0][pl];
+                fsy += red[w][1][pl];
+                fsz += red[w][2][pl];
+                ns += red[w][3][pl];
             }
-            const R4 lf = s_locf[lane];
+            if (dbs && lane == 0) dbs[13] = wall_clock64();
+            const R4 lf = s_locf[pl];
             fsx += lf.x;
             fsy += lf.y;
             fsz += lf.z;
             const R mu = lf.w;
-            const R4 xi = s_noise[lane];
+            const R4 xi = s_noise[k & 1][pl];
             const R dt = P.timestep;
             const R amp = r_sqrt(R(2) * P.temperature * mu * dt);
             const R mdt = mu * dt;
             const R4 np = mk4<R>(pi.x + mdt * fsx + amp * xi.x, pi.y + mdt * fsy + amp * xi.y,
                                  pi.z + mdt * fsz + amp * xi.z, R(0));
-            if (valid) {
-                const auto rp = __builtin_amdgcn_make_buffer_rsrc((void*)St<R>::pos(a, par ^ 1), 0, n * (int)sizeof(R4),
-                                                                  0x00020000);
-                const float4* pv = reinterpret_cast<const float4*>(&np);
-#pragma unroll
-                for (int h = 0; h < (int)sizeof(R4) / 16; ++h) st_sc1_f4(rp, i * (int)sizeof(R4) + 16 * h, pv[h]);
+            if (lead) {
+                pput_record<R>(half, i, np, tag);
+                if (k == steps - 1) St<R>::pos(a, par ^ 1)[i] = np;  // the launch's result (the launch end orders it)
             }
-            const R nt = wave_sum_r(valid ? ns : R(0));
-            if (lane == 6) acc_fold(acc, 6, (double)nt);
+            if (dbs && lane == 0) dbs[14] = wall_clock64();
+            const R nt = wave_sum_r(lead ? ns : R(0));
+            if (lane < kPTotChunks<R>)  // reactions, neighbours (the unused chunks tagged too: all are polled)
+                pput_double(half, kPTotOff<R> + blockIdx.x * kPTotBytes<R> + 16 * lane,
+                            lane < 6 ? s_react[min(lane, 5)] : lane == 6 ? (double)nt : 0.0, tag);
+            if (dbs && lane == 0) dbs[3] = wall_clock64();
+            if (dbw && lane == 0) *dbw = wall_clock64();
         }
-
-        // the grid barrier: every wave's stores and folds are performed, ONE lane adds, then polls the counter
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // the next step's image and every workgroup's partial totals, from the granules (all waves); wave 1 makes
+        // the next step's noise (the particle and the step only) while its first loads are in flight
+        pget_image<R>(half, n, G, tid, blockDim.x, tag, s_pos, s_pfx, s_pfy, s_pfz, s_tot, &s_stall, [&]() {
+            if (wave == 1 && k + 1 < steps) {
+                R n0, n1, n2;
+                noise3<R>(a, &s_ctx, il, n0, n1, n2, 1);
+                if (lq == 0) s_noise[(k + 1) & 1][pl] = mk4<R>(n0, n1, n2, R(0));
+            }
+        }, dbs && tid == 0 ? dbs + 4 : nullptr);
+        if (dbs && tid == 0) dbs[12] = wall_clock64();
         __syncthreads();
-        if (tid == 0) {
-            __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned target = (unsigned)G * (unsigned)(k + 1);
-            for (int spin = 0; __hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
-                if (spin >= GCS_PSTEP_SPIN) {  // (never with every workgroup resident: counted, the host fails)
-                    s_ctx.scan_stall += 1;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        __syncthreads();
-        par ^= 1;
-        // the next step's image (sc1 loads: the other workgroups' write-through stores), and the tail on this
-        // workgroup's context from the step's set
-        {
-            const auto rp = __builtin_amdgcn_make_buffer_rsrc((void*)St<R>::pos(a, par), 0, n * (int)sizeof(R4), 0x00020000);
-            for (int j = tid; j < n; j += blockDim.x) {
-                R4 p;
-                float4* pv = reinterpret_cast<float4*>(&p);
+        if (wave == 0) {
+            // the step's totals, in a fixed order (the same totals in every workgroup, bitwise): lane 8 c + p sums
+            // quantity c over workgroups p, p + 8, ..., then the 8 lanes of c pairwise
+            const int tc = lane >> 3, tp = lane & 7;
+            double s = 0.0;
+            if (tc < 7)
+                for (int g = tp; g < G; g += 8) s += s_tot[g * kPTotChunks<R> + tc];
+            s += __shfl_xor(s, 1);
+            s += __shfl_xor(s, 2);
+            s += __shfl_xor(s, 4);
+            double tot[7];
 #pragma unroll
-                for (int h = 0; h < (int)sizeof(R4) / 16; ++h) pv[h] = ld_sc1_f4(rp, j * (int)sizeof(R4) + 16 * h);
-                s_pos[j] = p;
-                s_pf[j] = make_float4((float)p.x, (float)p.y, (float)p.z, 0.f);
-            }
-        }
-        if (tid == 0) {
+            for (int c = 0; c < 7; ++c) tot[c] = __shfl(s, 8 * c);
+            if (dbs && lane == 0) dbs[7] = wall_clock64();
             ListTotals t;
-            pset_totals(acc, t);
-            const ListTailIn tin = list_tail_load(&s_ctx, a);
-            list_tail_apply(&s_ctx, a, tin, t, flags | (k == steps - 1 ? kLFlagStats : 0));
+            for (int c = 0; c < 6; ++c) t.react[c] = tot[c];
+            t.nbr = tot[6];
+            t.ld = 0.f;
+            t.nfb = 0;
+            t.nown = 0;
+            for (int c = 0; c < 6; ++c) t.bb[c] = 0.f;
+            t.drift = 0.0;
+            if (tid == 0) {
+                const ListTailIn tin = list_tail_load(&s_ctx, a);
+                list_tail_apply(&s_ctx, a, tin, t, flags | (k == steps - 1 ? kLFlagStats : 0));
+                if (dbs) dbs[6] = wall_clock64();
+            }
         }
+        par ^= 1;
+    }
+    __syncthreads();
+    if (tid == 0 && s_stall) s_ctx.scan_stall += 1;
+    if (a.dbg_times && tid < kPDbgSteps) {  // the stamps: workgroup 0's phases, every workgroup's hand-off
+        if (blockIdx.x == 0)
+            for (int c = 0; c < 16; ++c) a.dbg_times[16 * tid + c] = tid < steps ? s_dbg[tid][c] : 0ull;
+        if (blockIdx.x < 128) a.dbg_times[1024 + 128 * tid + blockIdx.x] = tid < steps ? s_dbw[tid] : 0ull;
     }
     __syncthreads();
     if (blockIdx.x == 0 && tid == 0) *ctx = s_ctx;
@@ -4639,7 +4847,7 @@ void launch_dom_grid(hipStream_t s, DevCtx* ctx, const ForceArgs& a)
 
 int launch_pstep(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int steps, int flags)
 {
-    const dim3 g((a.n + kTile - 1) / kTile), b(64 * kPWaves);
+    const dim3 g((a.n + kPP - 1) / kPP), b(64 * kPWaves);
     ForceArgs args = a;
     void* kargs[] = {(void*)&ctx, (void*)&args, (void*)&steps, (void*)&flags};
     // cooperative: the runtime launches the grid only if every workgroup can be resident at once (the grid barrier)
