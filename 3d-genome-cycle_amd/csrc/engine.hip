@@ -2907,14 +2907,23 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
     }
     // the rest: G-step chunks captured once into a graph (kernels and collectives), the remainder eagerly.  The list
     // step rebuilds at steps = 0 (mod M): its chunks are whole periods, captured for the rebuild phase they start at.
-    // A run whose steps change the list skin (skin_level; a few times while the core scale grows) runs eagerly
-    bool skin_change = false;
-    if (e->dom_list)
-        for (int64_t q = k; q < steps && !skin_change; ++q) skin_change = skin_level(e, first_step + q) != e->skin_level_pm;
-    const int M = e->dom_list ? e->list_every : 1;
-    const int G = e->graph_steps > 0 && !skin_change ? (e->graph_steps + M - 1) / M * M : 0;
-    const int phase = e->dom_list ? (int)((first_step + k) % M) : 0;
-    if (G > 0 && steps - k >= G) {
+    // A step that changes the list skin (skin_level; a few times while the core scale grows: a new grid, a rebuild,
+    // the period of the new skin) runs eagerly, as do the steps of a chunk that would hold one; the graph is then
+    // captured again for the new skin, period and phase
+    while (k < steps) {
+        const int64_t st = first_step + k;
+        const bool change = e->dom_list && skin_level(e, st) != e->skin_level_pm;
+        const int M = e->dom_list ? e->list_every : 1;
+        const int G = e->graph_steps > 0 ? (e->graph_steps + M - 1) / M * M : 0;
+        bool whole = !change && G > 0 && steps - k >= G;
+        for (int q = 1; whole && e->dom_list && q < G; ++q) whole = skin_level(e, st + q) == e->skin_level_pm;
+        if (!whole) {
+            if ((rc = enqueue_rccl_step(e, cfg, st))) return rc;
+            e->rstats.eager_steps++;
+            ++k;
+            continue;
+        }
+        const int phase = e->dom_list ? (int)(st % M) : 0;
         // (geometry, buffers, communicator and options drop the graph when they change: drop_domain_graph)
         const bool same = e->dgexec && e->dg_steps == G && std::memcmp(&e->dg_cfg, cfg, sizeof(*cfg)) == 0 &&
                           e->dg_version == e->topo_version && e->dg_sched_flags == e->sched_flags &&
@@ -2923,7 +2932,7 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
             drop_domain_graph(e);
             HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
             for (int q = 0; q < G; ++q) {
-                if ((rc = enqueue_rccl_step(e, cfg, first_step + k + q))) {
+                if ((rc = enqueue_rccl_step(e, cfg, st + q))) {
                     hipGraph_t g = nullptr;
                     (void)hipStreamEndCapture(e->stream, &g);
                     if (g) (void)hipGraphDestroy(g);
@@ -2940,14 +2949,9 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
             e->dg_skin = e->skin_level_pm;
             e->rstats.graphs_captured++;
         }
-        for (; steps - k >= G; k += G) {
-            if ((rc = launch_graph(e, e->dgexec))) return rc;
-            e->rstats.graph_steps += G;
-        }
-    }
-    for (; k < steps; ++k) {
-        if ((rc = enqueue_rccl_step(e, cfg, first_step + k))) return rc;
-        e->rstats.eager_steps++;
+        if ((rc = launch_graph(e, e->dgexec))) return rc;
+        e->rstats.graph_steps += G;
+        k += G;
     }
     if ((steps - k0) & 1) e->parity ^= 1;
     if (steps > 0) {

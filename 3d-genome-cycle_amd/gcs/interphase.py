@@ -111,10 +111,10 @@ class InterphaseDriver:
             self._writer = AsyncWriter(self.store)
         return self._writer
 
-    def _close_out(self):
+    def _close_out(self, propagating=None):
         if self._writer is not None:
             w, self._writer = self._writer, None
-            w.close()
+            w.close(propagating)
 
     def _progress(self, phase, step):
         if self.log is None:
@@ -143,7 +143,10 @@ class InterphaseDriver:
                              spacestep=cfg.relaxation_spacestep, seed=self.relaxation_seed)
                 done += k
                 self._callback_relax(done)
-        finally:
+        except BaseException as exc:
+            self._close_out(exc)
+            raise
+        else:
             self._close_out()
 
     def _callback_relax(self, step):
@@ -198,7 +201,10 @@ class InterphaseDriver:
                              seed=self.interphase_seed)
                 done += k
                 self._callback_sim(done, contacts)
-        finally:
+        except BaseException as exc:
+            self._close_out(exc)
+            raise
+        else:
             self._close_out()
 
     def _callback_sim(self, step, contacts=True):

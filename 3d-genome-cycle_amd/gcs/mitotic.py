@@ -209,7 +209,11 @@ class AnatelophaseDriver:
                 self.sys.run(k, first_step=done, temperature=cfg.temperature, timestep=cfg.timestep, seed=seed)
                 done += k
                 self._callback(name, done)
-        finally:
+        except BaseException as exc:
+            if self._writer is not None:
+                self._writer.close(exc)
+            raise
+        else:
             if self._writer is not None:
                 self._writer.close()
 
@@ -309,7 +313,11 @@ class PrometaphaseDriver:
                 self.sys.run(k, first_step=done, temperature=cfg.temperature, timestep=cfg.timestep, seed=seed)
                 done += k
                 self._callback(done)
-        finally:
+        except BaseException as exc:
+            if self._writer is not None:
+                self._writer.close(exc)
+            raise
+        else:
             if self._writer is not None:
                 self._writer.close()
 

@@ -381,11 +381,10 @@ class AsyncWriter:
             err, self.err = self.err, None
             raise err
 
-    def close(self):
-        """Flush and stop.  A deferred write error is raised -- unless the caller is already propagating an exception
-        (close() called from a `finally` during an unwind): then it is chained onto that exception as a note and the
-        original exception survives."""
-        propagating = sys.exc_info()[1]
+    def close(self, propagating=None):
+        """Flush and stop.  A deferred write error is raised -- unless the caller passes the exception it is already
+        propagating (`propagating`: close() on an unwind, as __exit__ does): then the write error is added to that
+        exception as a note and the original exception survives.  A plain close() always raises it."""
         try:
             self.flush()
         except BaseException as err:
@@ -399,6 +398,13 @@ class AsyncWriter:
             self.q.put(None)
             self.t.join()
             self.pool.shutdown(wait=True)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        self.close(propagating=exc)
+        return False
 
 
 def sampled_positions(system):

@@ -535,7 +535,7 @@ def decomp_main(args):
                                    f"({'RCCL from the engine' if rccl else 'in-process, one GPU'})",
                        "particles": n, "domains": ndom, "halo": halo, "parallelism": f"domains{ndom}",
                        "band_capacity_rank0": doms[0].cap, "peers_rank0": doms[0].peers,
-                       "bytes_per_peer_per_step": 16 * (doms[0].cap + 1),
+                       "bytes_per_peer_per_step": (32 if args.precision == 64 else 16) * (doms[0].cap + 1),
                        "step_shape": "list" if doms[0].e.list_stats()["builds"] > 0 else "tile",
                        "undecomposed_value": ref,
                        "decomposed_over_undecomposed": (n * args.steps / el_max / ref) if ref else None},

@@ -170,6 +170,9 @@ def test_rccl_run_one_rank_equals_host_driven(c1_design, fused, prec):
     run.run(70, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     d = domain.EngineDomain(_engine(c1_design, cfg, fused, prec), 0, slabs, halo, shared=sh)
     d.e.domain_rccl(rccl_unique_id(), 1, 0, [])
+    if graph is not None:  # 4-step graphs between the level changes (the changes' stretches eager)
+        from gcs import _abi as A
+        d.e.set_option(A.OPT_GRAPH_STEPS, graph)
     d.e.domain_run(30, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     d.e.domain_run(40, first_step=30, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     assert d.flag_bits() == 0
@@ -249,8 +252,9 @@ def test_engine_domains_processes_host_staged(tmp_path, config, world, prec):
     assert np.allclose(ctx["wall_semiaxes"], single.get_context()["wall_semiaxes"], rtol=WALL_REL[prec], atol=0)
 
 
+@pytest.mark.parametrize("graph", [None, 4])
 @pytest.mark.parametrize("prec", [64, 32])
-def test_decomposed_skin_follows_core_scale(c1_design, prec):
+def test_decomposed_skin_follows_core_scale(c1_design, prec, graph):
     """the decomposed list step's skin follows the scheduled core scale as the single engine's does (engine.hip
     enqueue_dom_list_step: a re-gridded rebuild at each level change; gcs_engine_domain_run runs a stretch with a
     change eagerly).  A fast core-scale schedule crosses several levels in 70 steps: the one-rank RCCL run in two
@@ -274,6 +278,9 @@ def test_decomposed_skin_follows_core_scale(c1_design, prec):
     run.check()
     d = domain.EngineDomain(eng(), 0, slabs, halo, shared=sh)
     d.e.domain_rccl(rccl_unique_id(), 1, 0, [])
+    if graph is not None:  # 4-step graphs between the level changes (the changes' stretches eager)
+        from gcs import _abi as A
+        d.e.set_option(A.OPT_GRAPH_STEPS, graph)
     d.e.domain_run(30, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     d.e.domain_run(40, first_step=30, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     assert d.flag_bits() == 0

@@ -177,6 +177,31 @@ def test_async_writer_keeps_order_and_raises(prepared):
             w.close()
 
 
+def test_async_writer_close_inside_a_handler_still_raises(prepared):
+    """a plain close() raises a failed deferred write even when it runs inside an unrelated, handled `except` block
+    (sys.exc_info() is set there); only close(propagating=exc) / the context manager's unwind adds it as a note"""
+    p, _ = prepared
+
+    def bad():
+        raise store.StoreError("write failed")
+    with store.SimulationStore(p) as s:
+        w = store.AsyncWriter(s, depth=2)
+        w._put(bad)
+        try:
+            raise KeyError("handled elsewhere")
+        except KeyError:
+            with pytest.raises(store.StoreError):
+                w.close()
+        w = store.AsyncWriter(s, depth=2)
+        with pytest.raises(ValueError) as info:
+            with w:
+                w._put(bad)
+                w.q.join()
+                raise ValueError("the stage failed")
+        notes = getattr(info.value, "__notes__", [])
+        assert any("deferred write also failed" in n for n in notes) or not hasattr(info.value, "add_note")
+
+
 def test_deflated_frames_equal_the_filter_path(prepared):
     """gcs_store_write_deflated (the async writer's frames, deflated on a thread pool): the chunk stored is byte for
     byte the one HDF5's deflate-6 filter stores for the same positions, and the dataset reads back the same"""
