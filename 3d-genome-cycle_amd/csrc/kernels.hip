@@ -3904,28 +3904,17 @@ constexpr int kPWaves = 4;
 constexpr int kPP = 16;          // particles per workgroup; a wave's lanes are kPP particles x (64 / kPP) segments
 constexpr int kHitCap = 64;      // prefilter hits listed per lane before a flush
 // the hand-off (a.psync, zeroed before every launch): two halves, step k writes half k & 1 with tag k + 1.  A half:
-// every particle's record, then every workgroup's 8 chunks of partial totals (6 reactions, the neighbour count, one
-// unused; one double a chunk).  A chunk is 16 B written by one sc1 store and read by sc1 loads (MI355X_MICROARCH.md,
-// the tagged hand-off: no fence, no counter, no ordering between chunks):
-//   GCS_PSTEP_CHECKED 1 (default): 3 data words + a check word (the tag mixed with the data words): a chunk is taken
-//     when its check word matches its data and this step's tag -- a stale chunk, or one read torn between two steps'
-//     stores, fails the match (but for a 2^-32 collision) and is polled again; a record is 6 (fp64) / 3 (fp32) words:
-//     2 / 1 chunks;
-//   GCS_PSTEP_CHECKED 0: two 8-B granules {data word, tag}, each checked by its own tag (8-B atomicity only); 3 / 2
-//     chunks a record.
-// Step k + 2 overwrites half k & 1 only after every workgroup has read it: a workgroup writes step k + 2's records
-// after it read all of step k + 1's, which every workgroup wrote after it had read step k's.
-#ifndef GCS_PSTEP_CHECKED
-#define GCS_PSTEP_CHECKED 1
-#endif
-constexpr bool kPChk = GCS_PSTEP_CHECKED != 0;
-constexpr int kPDW = kPChk ? 3 : 2;  // data words a chunk
-template <typename R> constexpr int kPRecWords = sizeof(R) == 8 ? 6 : 3;
-template <typename R> constexpr int kPRecChunks = (kPRecWords<R> + kPDW - 1) / kPDW;
-template <typename R> constexpr int kPRecBytes = 16 * kPRecChunks<R>;
-// a workgroup's totals: records kPMax + TR g .. (8 chunks or more: the records' chunks, all written, all polled)
-template <typename R> constexpr int kPTotRecs = (8 + kPRecChunks<R> - 1) / kPRecChunks<R>;
-template <typename R> constexpr int kPTotChunks = kPTotRecs<R> * kPRecChunks<R>;
+// every particle's record (fp64: 3 chunks, fp32: 2), then every workgroup's 8 chunks of partial totals (6 reactions,
+// the neighbour count).  A chunk is 16 B = two 8-B granules {data word, tag}: written by one sc1 store, read by sc1
+// loads, each granule checked by its own tag (MI355X_MICROARCH.md, the tagged-granule hand-off: no fence, no
+// counter, no ordering between granules).  Step k + 2 overwrites half k & 1 only after every workgroup has read it:
+// a workgroup writes step k + 2's records after it read all of step k + 1's, which every workgroup wrote after it
+// had read step k's.  (Measured and not kept: 16-B chunks of three data words and a check word mixing the tag with
+// them -- 2 / 1 chunks a record instead of 3 / 2 -- took 8.0 against 6.9 us per fp64 anatelophase step, same box.)
+template <typename R> constexpr int kPRecBytes = sizeof(R) == 8 ? 48 : 32;
+// a workgroup's totals: records kPMax + TR g .. (TR = 3 fp64 / 4 fp32 records: 9 / 8 chunks, 7 used, one double each)
+template <typename R> constexpr int kPTotRecs = sizeof(R) == 8 ? 3 : 4;
+template <typename R> constexpr int kPTotChunks = kPTotRecs<R> * kPRecBytes<R> / 16;
 template <typename R> constexpr int kPTotOff = kPMax * kPRecBytes<R>;
 template <typename R> constexpr int kPTotBytes = kPTotRecs<R> * kPRecBytes<R>;
 constexpr int kPGroups = (kPMax + kPP - 1) / kPP;
@@ -3936,79 +3925,36 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t phalf_rsrc(char* half, int byt
 {
     return __builtin_amdgcn_make_buffer_rsrc((void*)half, 0, bytes, 0x00020000);
 }
-__device__ __forceinline__ unsigned pchk(unsigned tag, unsigned d0, unsigned d1, unsigned d2)
+__device__ __forceinline__ void pput_chunk(char* half, int off, unsigned d0, unsigned d1, unsigned tag)
 {
-    return tag ^ 0x5bd1e995u ^ (d0 * 0x9e3779b1u) ^ (d1 * 0x85ebca77u) ^ (d2 * 0xc2b2ae3du);
-}
-__device__ __forceinline__ void pput_chunk(char* half, int off, unsigned d0, unsigned d1, unsigned d2, unsigned tag)
-{
-    const float4 v = kPChk ? make_float4(__uint_as_float(d0), __uint_as_float(d1), __uint_as_float(d2),
-                                         __uint_as_float(pchk(tag, d0, d1, d2)))
-                           : make_float4(__uint_as_float(d0), __uint_as_float(tag), __uint_as_float(d1),
-                                         __uint_as_float(tag));
-    st_sc1_f4(phalf_rsrc(half, kPHalfBytes), off, v);
-}
-__device__ __forceinline__ bool pchunk_ok(const int4& v, unsigned tag)
-{
-    if constexpr (kPChk) return (unsigned)v.w == pchk(tag, (unsigned)v.x, (unsigned)v.y, (unsigned)v.z);
-    return (unsigned)v.y == tag && (unsigned)v.w == tag;
-}
-__device__ __forceinline__ unsigned pchunk_word(const int4& v, int w)  // data word w of a chunk
-{
-    if constexpr (kPChk) return (unsigned)(w == 0 ? v.x : w == 1 ? v.y : v.z);
-    return (unsigned)(w == 0 ? v.x : v.z);
+    st_sc1_f4(phalf_rsrc(half, kPHalfBytes), off,
+              make_float4(__uint_as_float(d0), __uint_as_float(tag), __uint_as_float(d1), __uint_as_float(tag)));
 }
 __device__ __forceinline__ void pput_double(char* half, int off, double v, unsigned tag)
 {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    pput_chunk(half, off, (unsigned)b, (unsigned)(b >> 32), 0u, tag);
-}
-__device__ __forceinline__ double pchunk_double(const int4& v)
-{
-    return __longlong_as_double(
-        (long long)(((unsigned long long)pchunk_word(v, 1) << 32) | (unsigned long long)pchunk_word(v, 0)));
+    pput_chunk(half, off, (unsigned)b, (unsigned)(b >> 32), tag);
 }
 template <typename R>
 __device__ __forceinline__ void pput_record(char* half, int i, const real4<R>& p, unsigned tag)
 {
-    constexpr int NW = kPRecChunks<R> * kPDW;
-    unsigned w[NW];
-    for (int q = 0; q < NW; ++q) w[q] = 0u;
+    const int o = i * kPRecBytes<R>;
     if constexpr (sizeof(R) == 8) {
-        const double c[3] = {p.x, p.y, p.z};
-        for (int q = 0; q < 3; ++q) {
-            const unsigned long long b = (unsigned long long)__double_as_longlong(c[q]);
-            w[2 * q] = (unsigned)b;
-            w[2 * q + 1] = (unsigned)(b >> 32);
-        }
+        pput_double(half, o, p.x, tag);
+        pput_double(half, o + 16, p.y, tag);
+        pput_double(half, o + 32, p.z, tag);
     } else {
-        w[0] = __float_as_uint(p.x);
-        w[1] = __float_as_uint(p.y);
-        w[2] = __float_as_uint(p.z);
+        pput_chunk(half, o, __float_as_uint(p.x), __float_as_uint(p.y), tag);
+        pput_chunk(half, o + 16, __float_as_uint(p.z), 0u, tag);
     }
-#pragma unroll
-    for (int c = 0; c < kPRecChunks<R>; ++c)
-        pput_chunk(half, i * kPRecBytes<R> + 16 * c, w[kPDW * c], w[kPDW * c + 1], kPDW > 2 ? w[kPDW * c + kPDW - 1] : 0u,
-                   tag);
 }
-template <typename R>
-__device__ __forceinline__ real4<R> pchunks_record(const int4* v)
+__device__ __forceinline__ bool pchunk_ok(const int4& v, unsigned tag)
 {
-    constexpr int NW = kPRecChunks<R> * kPDW;
-    unsigned w[NW];
-#pragma unroll
-    for (int c = 0; c < kPRecChunks<R>; ++c)
-#pragma unroll
-        for (int q = 0; q < kPDW; ++q) w[kPDW * c + q] = pchunk_word(v[c], q);
-    if constexpr (sizeof(R) == 8) {
-        double c[3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-            c[q] = __longlong_as_double((long long)(((unsigned long long)w[2 * q + 1] << 32) | w[2 * q]));
-        return mk4<R>(c[0], c[1], c[2], R(0));
-    } else {
-        return mk4<R>(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]), R(0));
-    }
+    return (unsigned)v.y == tag && (unsigned)v.w == tag;
+}
+__device__ __forceinline__ double pchunk_double(const int4& v)
+{
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)v.z << 32) | (unsigned)v.x));
 }
 
 // the image of step tag and the G workgroups' partial totals: thread t of T walks u = t, t + T, ... over the n
@@ -4021,7 +3967,7 @@ __device__ __forceinline__ void pget_image(char* half, int n, int G, int t, int 
                                            volatile int* stall, Mid&& mid, unsigned long long* dbg = nullptr)
 {
     // mid(): work of the caller's that runs while the first batch's loads are in flight
-    constexpr int C = kPRecChunks<R>, RB = 12 / C, RBY = kPRecBytes<R>;  // (12 chunk loads in flight a thread)
+    constexpr int C = sizeof(R) == 8 ? 3 : 2, RB = sizeof(R) == 8 ? 4 : 6, RBY = kPRecBytes<R>;
     const int nu = n + G * kPTotRecs<R>;
     const auto rp = phalf_rsrc(half, kPHalfBytes);
     auto rec = [&](int u) { return u < n ? u : kPMax + (u - n); };
@@ -4062,7 +4008,12 @@ __device__ __forceinline__ void pget_image(char* half, int n, int G, int t, int 
         for (int r = 0; r < RB; ++r) {
             const int u = u0 + t + r * T;
             if (u < n) {
-                const real4<R> p = pchunks_record<R>(v[r]);
+                real4<R> p;
+                if constexpr (sizeof(R) == 8) {
+                    p = mk4<R>(pchunk_double(v[r][0]), pchunk_double(v[r][1]), pchunk_double(v[r][2]), R(0));
+                } else {
+                    p = mk4<R>(__int_as_float(v[r][0].x), __int_as_float(v[r][0].z), __int_as_float(v[r][1].x), R(0));
+                }
                 s_pos[u] = p;
                 s_pfx[u] = (float)p.x;
                 s_pfy[u] = (float)p.y;
