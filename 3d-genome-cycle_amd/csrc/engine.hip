@@ -2009,6 +2009,17 @@ int run_small(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64
         HIPCHK(hipMemsetAsync(dbg, 0, kPDebugWords * sizeof(unsigned long long), e->stream));
         a.dbg_times = dbg;
     }
+    // GCS_DEBUG_PSTEP_OFF=<mask>: timing probes only (wrong physics): drop bonds 1, bending 2, tethers 4, point
+    // sources 8, walls 16, droplet 32 from the particle-local terms
+    if (const char* off = std::getenv("GCS_DEBUG_PSTEP_OFF")) {
+        const int m = std::atoi(off);
+        if (m & 1) a.has_bonds = 0;
+        if (m & 2) a.has_bend = 0;
+        if (m & 4) a.has_tether = 0;
+        if (m & 8) a.n_point = 0;
+        if (m & 16) a.has_wall_in = a.has_wall_out = 0;
+        if (m & 32) a.sw_n = 0;
+    }
     for (int64_t done = 0; done < steps;) {
         const int len = (int)std::min<int64_t>(kPChunk, steps - done);
         HIPCHK(hipMemsetAsync(e->psync, 0, kPSyncWords * sizeof(unsigned), e->stream));

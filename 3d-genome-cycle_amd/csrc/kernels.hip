@@ -1328,18 +1328,31 @@ __device__ inline R spring_coef(int type, R K, R l, R r2, R& U)
 // cosine bending, kinetochore fibers, point sources and the ellipsoid walls (+ their reactions), in precision R.
 // BB: bonded entries whose loads are issued together (a row of the CSR is a chain of dependent loads per entry
 // otherwise: the nucleolar particles' ~20 droplet and bond partners made it the longest path of a step)
-template <int MODE, int BB = 1, typename R = float>
+// A lane's constants of the particle-local terms, loaded once per launch by k_pstep (whose lanes keep their particle
+// and share for a whole launch): its first bonded entry, its bending triple's eps, its tether row and first tether
+template <typename R>
+struct LocalPre {
+    int2 enb;      // the first bonded entry of the lane's share (its CSR index: erange.x + lq)
+    real4<R> bv;
+    R beps;        // bend eps of the triple that starts at i - lq (lq < 3)
+    int tb, te;    // the particle's tether row
+    TetherT<R> tt; // its entry tb + lq
+};
+template <int MODE, int BB = 1, typename R = float, bool PL = false>
 __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceArgs& a, int i, R xi, R yi, R zi,
                                    real4<R> km, R& fx, R& fy, R& fz, R* en, R* rin, R* rout,
                                    int2 erange = make_int2(-1, -1), const real4<R>* posv = nullptr, int lq = 0,
-                                   int nq = 1)
+                                   int nq = 1, const LocalPre<R>* pre = nullptr)
 {
+    static_assert(!PL || BB == 1, "the preloaded first entry assumes one bonded entry per batch");
     // lq / nq: this lane's share when nq lanes hold the same particle (k_pstep): bonded entries, droplet targets,
     // bending roles and tethers strided over them, the point sources and walls on lq == 0; the caller sums the lanes
     const int n = a.n;
     const FieldPrm<R>& P = St<R>::prm(a);
-    // the step-start positions of the partners: the context's buffer, or posv (k_pstep: its LDS image)
-    const real4<R>* __restrict__ posc = posv ? posv : St<R>::pos(a, ctx->parity);
+    // the step-start positions of the partners: the context's buffer, or posv (PL: k_pstep's LDS image, selected
+    // statically so the compiler sees the LDS pointer and reads it with ds_read, not with flat loads that also count
+    // against vmcnt)
+    const real4<R>* __restrict__ posc = PL ? posv : St<R>::pos(a, ctx->parity);
     const R cs = (R)ctx->cs;
     const R bs = (R)ctx->bs;
     R e_sw = 0, e_bond = 0, e_bend = 0, e_win = 0, e_wout = 0, e_pt = 0, e_kf = 0;
@@ -1347,22 +1360,8 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
         // erange: the particle's CSR row when the caller already has it (the list step's slot-ordered copy)
         const int eb = erange.x >= 0 ? erange.x : a.boff[i], ee = erange.x >= 0 ? erange.y : a.boff[i + 1];
         const real4<R>* __restrict__ bval = St<R>::bval(a);
-        for (int q0 = eb + lq * BB; q0 < ee; q0 += nq * BB) {
-          int2 enb[BB];
-          real4<R> bvb[BB], pjb[BB];
-#pragma unroll
-          for (int u = 0; u < BB; ++u) {
-              enb[u] = (q0 + u < ee) ? a.bent[q0 + u] : make_int2(i, kSemispring);
-              bvb[u] = (q0 + u < ee) ? bval[q0 + u] : mk4<R>(R(0), R(0), R(0), R(0));
-          }
-#pragma unroll
-          for (int u = 0; u < BB; ++u) pjb[u] = posc[enb[u].x];
-#pragma unroll
-          for (int u = 0; u < BB; ++u) {
-            if (q0 + u >= ee) break;
-            const int type = enb[u].y & 15;
-            const real4<R> bv = bvb[u];
-            const real4<R> pj = pjb[u];
+        auto bond = [&](const int2 e, const real4<R>& bv, const real4<R>& pj) {
+            const int type = e.y & 15;
             const R rx = xi - pj.x, ry = yi - pj.y, rz = zi - pj.z;
             const R r2 = r_fma(rz, rz, r_fma(ry, ry, rx * rx));
             R c = 0, U = 0;
@@ -1375,7 +1374,7 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
                 }
             } else {
                 R K = bv.x, l = bv.y;
-                if (enb[u].y >> 4) {  // scaled by the bond scale
+                if (e.y >> 4) {  // scaled by the bond scale
                     K = K * (R(1) / (bs * bs));
                     l = l * bs;
                 }
@@ -1385,6 +1384,26 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
             fx = r_fma(c, rx, fx);
             fy = r_fma(c, ry, fy);
             fz = r_fma(c, rz, fz);
+        };
+        int q0 = eb + lq * BB;
+        if constexpr (PL) {  // the lane's first entry from the launch's preload
+            if (q0 < ee) bond(pre->enb, pre->bv, posc[pre->enb.x]);
+            q0 += nq;
+        }
+        for (; q0 < ee; q0 += nq * BB) {
+          int2 enb[BB];
+          real4<R> bvb[BB], pjb[BB];
+#pragma unroll
+          for (int u = 0; u < BB; ++u) {
+              enb[u] = (q0 + u < ee) ? a.bent[q0 + u] : make_int2(i, kSemispring);
+              bvb[u] = (q0 + u < ee) ? bval[q0 + u] : mk4<R>(R(0), R(0), R(0), R(0));
+          }
+#pragma unroll
+          for (int u = 0; u < BB; ++u) pjb[u] = posc[enb[u].x];
+#pragma unroll
+          for (int u = 0; u < BB; ++u) {
+            if (q0 + u >= ee) break;
+            bond(enb[u], bvb[u], pjb[u]);
           }
         }
     }
@@ -1421,7 +1440,7 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
         for (int role = lq; role < 3; role += nq) {
             const int k0 = i - role;
             if (k0 < 0 || k0 + 2 >= n) continue;
-            const R eps = bend[k0];
+            const R eps = (PL && role == lq) ? pre->beps : bend[k0];
             if (eps == R(0)) continue;
             real4<R> q0 = (role == 0) ? mk4<R>(xi, yi, zi, R(0)) : posc[k0];
             real4<R> q1 = (role == 1) ? mk4<R>(xi, yi, zi, R(0)) : posc[k0 + 1];
@@ -1448,10 +1467,10 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
     }
 
     if (a.has_tether) {
-        const int tb = a.toff[i], te = a.toff[i + 1];
+        const int tb = PL ? pre->tb : a.toff[i], te = PL ? pre->te : a.toff[i + 1];
         const TetherT<R>* __restrict__ tent = St<R>::tent(a);
         for (int q = tb + lq; q < te; q += nq) {
-            const TetherT<R> t = tent[q];
+            const TetherT<R> t = (PL && q == tb + lq) ? pre->tt : tent[q];
             const R rx = xi - t.px, ry = yi - t.py, rz = zi - t.pz;
             R U;
             const R c = spring_coef<R>(kSpring, t.k, t.l, rx * rx + ry * ry + rz * rz, U);
@@ -4086,9 +4105,18 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
     }
     R4 km = mk4<R>(R(0), R(0), R(0), R(0));
     int2 erow = make_int2(0, 0);
+    LocalPre<R> pre{};
     if (wave == W - 1) {
         km = kmu[il];
         erow = a.has_bonds ? make_int2(a.boff[il], a.boff[il + 1]) : make_int2(0, 0);
+        // this lane's constants of the particle-local terms for the whole launch (local_terms, LocalPre)
+        const int qb = erow.x + lq;
+        pre.enb = qb < erow.y ? a.bent[qb] : make_int2(il, 0);
+        pre.bv = qb < erow.y ? St<R>::bval(a)[qb] : mk4<R>(R(0), R(0), R(0), R(0));
+        pre.beps = (a.has_bend && lq < 3 && il - lq >= 0 && il - lq + 2 < n) ? St<R>::bend(a)[il - lq] : R(0);
+        pre.tb = a.has_tether ? a.toff[il] : 0;
+        pre.te = a.has_tether ? a.toff[il + 1] : 0;
+        if (pre.tb + lq < pre.te) pre.tt = St<R>::tent(a)[pre.tb + lq];
     }
     const R2 own = s_ab[il];  // (s_ab was filled before the barrier above)
     // this lane's candidates [cj0, cj1): the wave's share of the candidates in 1/64, split evenly over its Q lane
@@ -4135,8 +4163,8 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
         if (wave == W - 1) {
             R lfx = 0, lfy = 0, lfz = 0, en[kEnergyKinds];
             R rin[3] = {0, 0, 0}, rout[3] = {0, 0, 0};
-            local_terms<kModeStep, sizeof(R) == 8 ? GCS_LIST_BOND_BATCH64 : GCS_LIST_BOND_BATCH, R>(
-                &s_ctx, a, il, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout, erow, s_pos, lq, Q);
+            local_terms<kModeStep, 1, R, true>(&s_ctx, a, il, pi.x, pi.y, pi.z, km, lfx, lfy, lfz, en, rin, rout, erow,
+                                               s_pos, lq, Q, &pre);
 #pragma unroll
             for (int o = kPP; o < kTile; o <<= 1) {  // the lane groups' shares, in a fixed order
                 lfx += __shfl_down(lfx, o);
