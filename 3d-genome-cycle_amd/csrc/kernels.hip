@@ -1285,14 +1285,13 @@ __device__ inline void philox_normal3(unsigned seed_lo, unsigned seed_hi, long l
 }
 
 template <typename R>
-__device__ inline void noise3(const ForceArgs& a, const DevCtx* ctx, int i, R& n0, R& n1, R& n2, int ahead = 0)
+__device__ inline void noise3_at(const ForceArgs& a, long long step, long long cursor, int i, R& n0, R& n1, R& n2)
 {
-    // ahead: the noise of the step that many steps after the context's next one (k_pstep: the next step's, before
-    // the tail has advanced the context)
+    // the noise of the step after `step` (the context's last completed step), injected noise at `cursor`
     if (a.noise_mode == GCS_NOISE_PHILOX) {
-        philox_normal3<R>(a.seed_lo, a.seed_hi, ctx->step + 1 + ahead, i, n0, n1, n2);
+        philox_normal3<R>(a.seed_lo, a.seed_hi, step + 1, i, n0, n1, n2);
     } else if (a.noise_mode == GCS_NOISE_INJECTED) {
-        long long cur = ctx->noise_cursor + ahead;
+        long long cur = cursor;
         if (cur >= a.noise_steps) cur = a.noise_steps - 1;  // host checks the budget before launching
         const R* p = St<R>::noise(a) + (cur * (long long)a.n + i) * 3;
         n0 = p[0];
@@ -1301,6 +1300,11 @@ __device__ inline void noise3(const ForceArgs& a, const DevCtx* ctx, int i, R& n
     } else {
         n0 = n1 = n2 = R(0);
     }
+}
+template <typename R>
+__device__ inline void noise3(const ForceArgs& a, const DevCtx* ctx, int i, R& n0, R& n1, R& n2)
+{
+    noise3_at<R>(a, ctx->step, ctx->noise_cursor, i, n0, n1, n2);
 }
 
 // spring-type potential at separation vector r (|r|^2 = r2): returns force coefficient c (F = c r) and U
@@ -3976,12 +3980,13 @@ __device__ __forceinline__ double pchunk_double(const int4& v)
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)v.z << 32) | (unsigned)v.x));
 }
 
-// the image of step tag and the G workgroups' partial totals: thread t of T walks u = t, t + T, ... over the n
-// records and then the G kPTotRecs totals records (record kPMax + u - n), a batch's loads issued together, polls
+// the image of step tag and the G workgroups' partial totals: units u < n are the records, u in [n, n + G TR) the
+// totals records (record kPMax + u - n); thread t of T walks u = ub + t, ub + t + T, ... < ue, a batch's loads issued
+// together, polls
 // until every granule carries the tag (a stall after GCS_PSTEP_SPIN polls: counted, the host fails); records into
 // s_pos and the fp32 coordinate arrays s_pfx / s_pfy / s_pfz, totals chunks (one double each) into s_tot
 template <typename R, typename Mid>
-__device__ __forceinline__ void pget_image(char* half, int n, int G, int t, int T, unsigned tag, real4<R>* s_pos,
+__device__ __forceinline__ void pget_image(char* half, int n, int G, int ub, int ue, int t, int T, unsigned tag, real4<R>* s_pos,
                                            float* s_pfx, float* s_pfy, float* s_pfz, double* s_tot,
                                            volatile int* stall, Mid&& mid, unsigned long long* dbg = nullptr)
 {
@@ -3990,22 +3995,22 @@ __device__ __forceinline__ void pget_image(char* half, int n, int G, int t, int 
     const int nu = n + G * kPTotRecs<R>;
     const auto rp = phalf_rsrc(half, kPHalfBytes);
     auto rec = [&](int u) { return u < n ? u : kPMax + (u - n); };
-    for (int u0 = 0; u0 < nu; u0 += RB * T) {
+    for (int u0 = ub; u0 < ue; u0 += RB * T) {
         int4 v[RB][C];
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
             const int u = u0 + t + r * T;
 #pragma unroll
-            for (int c = 0; c < C; ++c) v[r][c] = u < nu ? ld_sc1_i4(rp, rec(u) * RBY + 16 * c) : int4{};
+            for (int c = 0; c < C; ++c) v[r][c] = u < ue ? ld_sc1_i4(rp, rec(u) * RBY + 16 * c) : int4{};
         }
-        if (u0 == 0) mid();
+        if (u0 == ub) mid();
         for (int spin = 0;; ++spin) {
             bool ok = true;
 #pragma unroll
             for (int r = 0; r < RB; ++r)
 #pragma unroll
-                for (int c = 0; c < C; ++c) ok = ok && (u0 + t + r * T >= nu || pchunk_ok(v[r][c], tag));
-            if (dbg && u0 == 0) {
+                for (int c = 0; c < C; ++c) ok = ok && (u0 + t + r * T >= ue || pchunk_ok(v[r][c], tag));
+            if (dbg && u0 == ub) {
                 if (spin == 0) dbg[0] = wall_clock64();
                 dbg[1] = spin;
             }
@@ -4020,7 +4025,7 @@ __device__ __forceinline__ void pget_image(char* half, int n, int G, int t, int 
                 const int u = u0 + t + r * T;
 #pragma unroll
                 for (int c = 0; c < C; ++c)
-                    if (u < nu && !pchunk_ok(v[r][c], tag)) v[r][c] = ld_sc1_i4(rp, rec(u) * RBY + 16 * c);
+                    if (u < ue && !pchunk_ok(v[r][c], tag)) v[r][c] = ld_sc1_i4(rp, rec(u) * RBY + 16 * c);
             }
         }
 #pragma unroll
@@ -4037,7 +4042,7 @@ __device__ __forceinline__ void pget_image(char* half, int n, int G, int t, int 
                 s_pfx[u] = (float)p.x;
                 s_pfy[u] = (float)p.y;
                 s_pfz[u] = (float)p.z;
-            } else if (u < nu) {
+            } else if (u < ue) {
 #pragma unroll
                 for (int c = 0; c < C; ++c) s_tot[(u - n) * C + c] = pchunk_double(v[r][c]);
             }
@@ -4145,6 +4150,7 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
         unsigned long long* const dbs = (a.dbg_times && blockIdx.x == 0 && k < kPDbgSteps) ? s_dbg[k] : nullptr;
         unsigned long long* const dbw = (a.dbg_times && k < kPDbgSteps) ? &s_dbw[k] : nullptr;
         if (dbs && tid == 0) dbs[0] = wall_clock64();
+        const long long c_step = s_ctx.step, c_cursor = s_ctx.noise_cursor;  // (the tail advances s_ctx mid-step)
         const R4 pi = s_pos[il];
         const R cs = (R)s_ctx.cs;
         const R scale = a.pair_scaled ? cs : R(1);
@@ -4305,20 +4311,25 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
             if (dbs && lane == 0) dbs[3] = wall_clock64();
             if (dbw && lane == 0) *dbw = wall_clock64();
         }
-        // the next step's image and every workgroup's partial totals, from the granules (all waves); wave 1 makes
-        // the next step's noise (the particle and the step only) while its first loads are in flight
-        pget_image<R>(half, n, G, tid, blockDim.x, tag, s_pos, s_pfx, s_pfy, s_pfz, s_tot, &s_stall, [&]() {
-            if (wave == 1 && k + 1 < steps) {
-                R n0, n1, n2;
-                noise3<R>(a, &s_ctx, il, n0, n1, n2, 1);
-                if (lq == 0) s_noise[(k + 1) & 1][pl] = mk4<R>(n0, n1, n2, R(0));
-            }
-        }, dbs && tid == 0 ? dbs + 4 : nullptr);
-        if (dbs && tid == 0) dbs[12] = wall_clock64();
-        __syncthreads();
-        if (wave == 0) {
+        // the next step's image (waves 1..) and every workgroup's partial totals (wave 0), from the granules: wave 0
+        // sums the totals and runs the tail while the image lands; wave 1 makes the next step's noise (the particle
+        // and the step only: the step and cursor as of the step start, the tail may advance the context meanwhile)
+        // while its first loads are in flight
+        if (wave > 0) {
+            pget_image<R>(half, n, G, 0, n, tid - 64, 64 * (W - 1), tag, s_pos, s_pfx, s_pfy, s_pfz, s_tot, &s_stall,
+                          [&]() {
+                if (wave == 1 && k + 1 < steps) {
+                    R n0, n1, n2;
+                    noise3_at<R>(a, c_step + 1, c_cursor + 1, il, n0, n1, n2);
+                    if (lq == 0) s_noise[(k + 1) & 1][pl] = mk4<R>(n0, n1, n2, R(0));
+                }
+            });
+            if (dbs && tid == 64) dbs[12] = wall_clock64();
+        } else {
+            pget_image<R>(half, n, G, n, n + G * kPTotRecs<R>, lane, 64, tag, s_pos, s_pfx, s_pfy, s_pfz, s_tot,
+                          &s_stall, [] {}, dbs && tid == 0 ? dbs + 4 : nullptr);
             // the step's totals, in a fixed order (the same totals in every workgroup, bitwise): lane 8 c + p sums
-            // quantity c over workgroups p, p + 8, ..., then the 8 lanes of c pairwise
+            // quantity c over workgroups p, p + 8, ..., then the 8 lanes of c pairwise (this wave's own LDS writes)
             const int tc = lane >> 3, tp = lane & 7;
             double s = 0.0;
             if (tc < 7)
