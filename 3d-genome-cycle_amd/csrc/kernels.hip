@@ -4019,7 +4019,7 @@ __device__ __forceinline__ void pget_image(char* half, int n, int G, int ub, int
                 *stall = 1;
                 break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(1);  // (longer backoffs measured slower: 2 / 4 / 8 x 64 clocks)
 #pragma unroll
             for (int r = 0; r < RB; ++r) {
                 const int u = u0 + t + r * T;
@@ -4288,6 +4288,12 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
                 ns += red[w][3][pl];
             }
             if (dbs && lane == 0) dbs[13] = wall_clock64();
+            // the workgroup's totals out first (wave 0 of every workgroup waits on them before its tail), then the
+            // records
+            const R nt = wave_sum_r(lead ? ns : R(0));
+            if (lane < kPTotChunks<R>)  // reactions, neighbours (the unused chunks tagged too: all are polled)
+                pput_double(half, kPTotOff<R> + blockIdx.x * kPTotBytes<R> + 16 * lane,
+                            lane < 6 ? s_react[min(lane, 5)] : lane == 6 ? (double)nt : 0.0, tag);
             const R4 lf = s_locf[pl];
             fsx += lf.x;
             fsy += lf.y;
@@ -4304,10 +4310,6 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
                 if (k == steps - 1) St<R>::pos(a, par ^ 1)[i] = np;  // the launch's result (the launch end orders it)
             }
             if (dbs && lane == 0) dbs[14] = wall_clock64();
-            const R nt = wave_sum_r(lead ? ns : R(0));
-            if (lane < kPTotChunks<R>)  // reactions, neighbours (the unused chunks tagged too: all are polled)
-                pput_double(half, kPTotOff<R> + blockIdx.x * kPTotBytes<R> + 16 * lane,
-                            lane < 6 ? s_react[min(lane, 5)] : lane == 6 ? (double)nt : 0.0, tag);
             if (dbs && lane == 0) dbs[3] = wall_clock64();
             if (dbw && lane == 0) *dbw = wall_clock64();
         }
@@ -4326,6 +4328,8 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
             });
             if (dbs && tid == 64) dbs[12] = wall_clock64();
         } else {
+            ListTailIn tin;
+            if (tid == 0) tin = list_tail_load(&s_ctx, a);  // (the tail's inputs that do not need the totals)
             pget_image<R>(half, n, G, n, n + G * kPTotRecs<R>, lane, 64, tag, s_pos, s_pfx, s_pfy, s_pfz, s_tot,
                           &s_stall, [] {}, dbs && tid == 0 ? dbs + 4 : nullptr);
             // the step's totals, in a fixed order (the same totals in every workgroup, bitwise): lane 8 c + p sums
@@ -4350,7 +4354,6 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
             for (int c = 0; c < 6; ++c) t.bb[c] = 0.f;
             t.drift = 0.0;
             if (tid == 0) {
-                const ListTailIn tin = list_tail_load(&s_ctx, a);
                 list_tail_apply(&s_ctx, a, tin, t, flags | (k == steps - 1 ? kLFlagStats : 0));
                 if (dbs) dbs[6] = wall_clock64();
             }
