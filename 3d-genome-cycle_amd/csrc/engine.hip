@@ -867,8 +867,10 @@ int list_format(const gcs_engine* e)
 {
     if (e->list_fmt_opt == 2) return kListFmtInt;
     if (e->list_fmt_opt == 1) return kListFmtRel16;
-    if (e->list_fmt_opt == 3 || e->ntypes > kTileTypes) return e->n <= 65536 ? kListFmtAbs16 : kListFmtRel16;
-    return kListFmtTile16;  // (its LDS class table holds kTileTypes classes)
+    // 3: the tile-staged entries (an experiment: slower than the slot entries at C2 and C5 on MI355X, DESIGN.md §4
+    // "List entry formats"; its LDS class table holds kTileTypes classes; undecomposed runs only)
+    if (e->list_fmt_opt == 3 && e->ntypes <= kTileTypes && !e->dom) return kListFmtTile16;
+    return e->n <= 65536 ? kListFmtAbs16 : kListFmtRel16;
 }
 // window-table entries: one per step workgroup (64 slots)
 size_t ltile_entries(const gcs_engine* e) { return (size_t)force_blocks(e->n); }

@@ -387,15 +387,17 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
                                      wave (< waves per tile) of chunk p of each period in nibble p.  Only the split of
                                      a slot's list over the segments changes (the list step's last wave also carries
                                      the particle-local terms); the pair set and the results do not */
-#define GCS_OPT_LIST_FORMAT 17    /* list entries: 0 (default) 16-bit indices into the step tile's LDS image of its partner
-                                     rows (the partners are read from LDS, not gathered); 1 16-bit slots relative to the
-                                     particle's cell planes (an entry out of their range sends the particle to the exact
-                                     search); 2 32-bit absolute slots; 3 16-bit absolute slots up to 65,536 particles, the
-                                     relative form beyond.  Every form holds the same pairs in the same order: the results
-                                     do not change */
-#define GCS_OPT_SMALL_STEP 18     /* systems of <= 2,048 particles (the mitotic stages): 1 (default) one cooperative launch
-                                     per chunk of steps, every workgroup holding the whole system in LDS (all pairs, a
-                                     grid barrier per step), unless GCS_OPT_FUSED_STEP was set; 0 the step shapes above */
+#define GCS_OPT_LIST_FORMAT 17    /* list entries: 0 (default) 16-bit absolute slots up to 65,536 particles, the relative
+                                     form beyond; 1 16-bit slots relative to the particle's cell planes (an entry out of
+                                     their range sends the particle to the exact search); 2 32-bit absolute slots; 3
+                                     16-bit indices into the step workgroup's LDS image of its partner rows (the partners
+                                     read from LDS; undecomposed runs with <= 64 pair classes, else the default).  Every
+                                     form holds the same pairs in the same order: the results do not change, but for the
+                                     rare particle the tile-staged form searches exactly */
+#define GCS_OPT_SMALL_STEP 18     /* systems of <= 1,536 particles (the mitotic stages): 1 (default) one cooperative launch
+                                     per chunk of steps, every workgroup holding the whole system in LDS (all pairs; the
+                                     new positions handed between workgroups as tagged granules every step), unless
+                                     GCS_OPT_FUSED_STEP was set; 0 the step shapes above */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
 
 /* List-step diagnostics (the neighbour lists md::neighbor_searcher keeps between rebuilds; micromd, called at

@@ -170,9 +170,6 @@ def test_rccl_run_one_rank_equals_host_driven(c1_design, fused, prec):
     run.run(70, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     d = domain.EngineDomain(_engine(c1_design, cfg, fused, prec), 0, slabs, halo, shared=sh)
     d.e.domain_rccl(rccl_unique_id(), 1, 0, [])
-    if graph is not None:  # 4-step graphs between the level changes (the changes' stretches eager)
-        from gcs import _abi as A
-        d.e.set_option(A.OPT_GRAPH_STEPS, graph)
     d.e.domain_run(30, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     d.e.domain_run(40, first_step=30, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     assert d.flag_bits() == 0
