@@ -397,7 +397,7 @@ constexpr int kListFmtRel16 = 2;
 // 16-bit indices into the step tile's LDS image of its partners (kernels.hip ListTile16: the default at any size)
 constexpr int kListFmtTile16 = 3;
 constexpr int kPMax = 1536;         // particles of the persistent small-system step (kernels.hip k_pstep: LDS images)
-constexpr int kPHalfBytes = kPMax * 48 + 128 * 128;  // its hand-off buffer (psync): two halves (kernels.hip k_pstep)
+constexpr int kPHalfBytes = kPMax * 48 + 256 * 144;  // its hand-off buffer (psync): two halves (kernels.hip k_pstep)
 constexpr int kPSyncWords = 2 * kPHalfBytes / 4;
 constexpr int kListTileWords = 128;  // ints per window-table entry (kernels.hip stage_slot_w: 73 used)
 constexpr int kTileTypes = 64;

@@ -3924,7 +3924,10 @@ __global__ __launch_bounds__(kLUpdateBlock) void k_lupdate(DevCtx* __restrict__ 
 #define GCS_PSTEP_SPIN (1 << 22)  // grid-barrier polls before a workgroup gives up (DevCtx::scan_stall; the host fails)
 #endif
 constexpr int kPWaves = 4;
-constexpr int kPP = 16;          // particles per workgroup; a wave's lanes are kPP particles x (64 / kPP) segments
+#ifndef GCS_PSTEP_PP
+#define GCS_PSTEP_PP 16
+#endif
+constexpr int kPP = GCS_PSTEP_PP;  // particles per workgroup; a wave's lanes are kPP particles x (64 / kPP) segments
 constexpr int kHitCap = 64;      // prefilter hits listed per lane before a flush
 // the hand-off (a.psync, zeroed before every launch): two halves, step k writes half k & 1 with tag k + 1.  A half:
 // every particle's record (fp64: 3 chunks, fp32: 2), then every workgroup's 8 chunks of partial totals (6 reactions,
