@@ -195,6 +195,7 @@ struct gcs_engine {
     int c_bits_opt = 0;      // GCS_OPT_CONTACT_BITS (0: sized from N at the first update)
     // sampled positions (store quantisation)
     float* q_out = nullptr;
+    float* q_host = nullptr;  // pinned staging of the quantised sample (a pageable D2H copy stages through the runtime)
     // spatial domain decomposition (gcs_engine_set_domain): own box, halo, peer regions, domain index / count
     bool dom = false;
     DomBox dom_box{};
@@ -1661,6 +1662,8 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->c_rows);
     if (e->c_temp) (void)hipFree(e->c_temp);
     dfree(e->q_out);
+    if (e->q_host) (void)hipHostFree(e->q_host);
+    e->q_host = nullptr;
     dfree(e->s_pts);
     dfree(e->s_spos);
     dfree(e->s_sb);
@@ -2433,13 +2436,15 @@ int gcs_engine_sample_positions(gcs_engine* e, float* xyz, int64_t n, int32_t fr
     HIPCHK(hipSetDevice(e->device));
     int rc;
     if (!e->q_out && (rc = dalloc(&e->q_out, 3 * (size_t)e->n))) return rc;
+    if (!e->q_host) HIPCHK(hipHostMalloc(&e->q_host, 3 * (size_t)e->n * sizeof(float), hipHostMallocDefault));
     if (e->prec == 64)
         launch_quantize(e->stream, e->dpos[e->parity], e->q_out, e->n, fraction_bits);
     else
         launch_quantize(e->stream, e->pos[e->parity], e->q_out, e->n, fraction_bits);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(xyz, e->q_out, 3 * (size_t)n * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(e->q_host, e->q_out, 3 * (size_t)n * sizeof(float), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
+    std::memcpy(xyz, e->q_host, 3 * (size_t)n * sizeof(float));
     return GCS_OK;
 }
 

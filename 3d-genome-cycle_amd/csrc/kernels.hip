@@ -4222,7 +4222,7 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
             const float4* const Z4 = reinterpret_cast<const float4*>(s_pfz);
             // chunks from cj0 rounded down to 4 (b128 reads of 4 candidates a coordinate; the 16 candidates of a half
             // chunk loaded together), the candidates outside [cj0, cj1) masked
-            for (int c0 = cj0 & ~3; c0 < cj1; c0 += 32) {
+            for (int c0 = cj0 < cj1 ? (cj0 & ~3) : cj1; c0 < cj1; c0 += 32) {  // (an empty share: no chunk)
                 unsigned m = 0u;
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh) {
