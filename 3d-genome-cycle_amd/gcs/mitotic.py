@@ -202,13 +202,19 @@ class AnatelophaseDriver:
         every = math.gcd(cfg.sampling_interval, cfg.logging_interval)
         self._writer = _writer(self.store)
         try:
-            self._callback(name, 0)
+            # a sample's frame is handed to the writer after the next run is enqueued (the device then computes
+            # while the host queues the write; the frames and their order are unchanged)
+            pending = self._callback(name, 0)
             done = 0
             while done < steps:
                 k = min(every - done % every, steps - done)
                 self.sys.run(k, first_step=done, temperature=cfg.temperature, timestep=cfg.timestep, seed=seed)
+                if pending is not None:
+                    pending()
                 done += k
-                self._callback(name, done)
+                pending = self._callback(name, done)
+            if pending is not None:
+                pending()
         except BaseException as exc:
             if self._writer is not None:
                 self._writer.close(exc)
@@ -218,14 +224,18 @@ class AnatelophaseDriver:
                 self._writer.close()
 
     def _callback(self, name, step):
+        """the step's sample and log line; returns the frame write (or None), for the caller to hand over once the
+        next run is enqueued"""
         cfg = self.cfg
+        write = None
         if step % cfg.sampling_interval == 0 and self.store is not None:
             x, q = sampled_positions(self.sys)
-            self._writer.save_frame(name, step, x, None, quantized=q)
+            write = lambda: self._writer.save_frame(name, step, x, None, quantized=q)  # noqa: E731
         if step % cfg.logging_interval == 0 and self.log is not None:
             e, _ = self.sys.compute_energy()
             stamp = _time.strftime("%Y-%m-%d %H:%M:%S")
             print(f"[{name}] {stamp}\t{step}\tE: {e / self.design.n:g}", file=self.log)
+        return write
 
     def run_dragging_stage(self, steps=None):
         """:232-262: kinetochore fibers to the pole at anaphase_spindle_shift"""
@@ -305,14 +315,18 @@ class PrometaphaseDriver:
         every = math.gcd(cfg.sampling_interval, cfg.logging_interval)
         self._writer = _writer(self.store)
         try:
-            self._callback(0)
+            pending = self._callback(0)  # (frame writes handed over after the next run is enqueued, as above)
             seed = self.random()  # .seed = _random() (:230; callback(0) draws nothing)
             done = 0
             while done < steps:
                 k = min(every - done % every, steps - done)
                 self.sys.run(k, first_step=done, temperature=cfg.temperature, timestep=cfg.timestep, seed=seed)
+                if pending is not None:
+                    pending()
                 done += k
-                self._callback(done)
+                pending = self._callback(done)
+            if pending is not None:
+                pending()
         except BaseException as exc:
             if self._writer is not None:
                 self._writer.close(exc)
@@ -330,4 +344,5 @@ class PrometaphaseDriver:
             print(f"[prometaphase] {stamp}\t{step}\tE: {e:g}", file=self.log)
         if step % cfg.sampling_interval == 0 and self.store is not None:
             x, q = sampled_positions(self.sys)
-            self._writer.save_frame("prometaphase", step, x, None, quantized=q)
+            return lambda: self._writer.save_frame("prometaphase", step, x, None, quantized=q)
+        return None
