@@ -189,9 +189,13 @@ __device__ inline int cell_index(const Grid& g, float x, float y, float z)
     return cx + g.n[0] * (cy + g.n[1] * cz);
 }
 
-// Cell grid over the box [lo, hi]; cell edge >= rc (1e-4 margin; x edge rc / fx) so any pair closer than rc lies
-// in the same or an adjacent cell (+-fx in x).  Particles outside the box are clamped into the border cells,
-// which keeps that property because clamping never increases a per-axis cell distance.
+// Cell grid over the box [lo, hi]; cell edge >= rc (x edge rc / fx) plus a margin, so any pair closer than rc lies
+// in the same or an adjacent cell (+-fx in x).  The margin covers the binning's fp32 arithmetic: 1e-4 of the edge,
+// plus, in length units, the roundings of a particle's coordinate (2^-24 |x|, the fp32 copy of an fp64 position)
+// and of (x - lo) * inv (2^-24 of the extent each), for both particles of a pair, with a factor 2 to spare:
+// 2.5e-7 (max(|lo|, |hi|) + 2 extent) -- which matters far from the origin and at the 1,024-cell cap.
+// Particles outside the box are clamped into the border cells, which keeps that property because clamping never
+// increases a per-axis cell distance.
 __device__ __forceinline__ Grid make_grid(const float* lo, const float* hi, float rc, int ncell_max, int fx)
 {
     Grid g;
@@ -203,7 +207,8 @@ __device__ __forceinline__ Grid make_grid(const float* lo, const float* hi, floa
         if (!(e > 0.f) || !(e < 3.0e38f)) e = 0.f;
         ext[k] = e;
         const float edge = (k == 0) ? rc / (float)fx : rc;
-        float q = (rc > 0.f) ? e / (edge * 1.0001f) : 0.f;
+        const float mag = (e > 0.f) ? fmaxf(fabsf(lo[k]), fabsf(hi[k])) : 0.f;
+        float q = (rc > 0.f) ? e / (edge * 1.0001f + 2.5e-7f * (mag + 2.f * e)) : 0.f;
         int m = (q >= 1.f) ? (int)fminf(q, 1024.f) : 1;
         n[k] = m;
         total *= m;

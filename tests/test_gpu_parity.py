@@ -281,6 +281,26 @@ def test_chunked_runs_equal_one_run(c1_design, interphase_cfg, prec, fused):
 
 
 @precisions
+def test_neighbor_search_near_cutoff_far_from_origin(prec):
+    """Pairs just inside the cutoff (d (1 - 1e-6) along a coordinate axis) in a box 1,000 away from the origin,
+    where the fp32 roundings the binning works on (~6e-5) exceed 1e-4 of the cell edge (d = 0.1): without a margin
+    that scales with the coordinates some such pairs bin two cells apart and are lost (kernels.hip make_grid; ADVICE
+    r4).  The pair set is bit-exact vs the oracle predicate"""
+    rng = np.random.default_rng(13)
+    d = 0.1
+    m = 20000
+    a = 1000.0 + rng.uniform(0, 3.0, size=(m, 3))
+    u = np.zeros((m, 3))
+    u[np.arange(m), rng.integers(0, 3, m)] = rng.choice([-1.0, 1.0], m)
+    pts = np.concatenate([a, a + u * d * (1 - 1e-6)])
+    e = Engine(4, precision=prec)
+    got = e.search_neighbors(d, points=pts)
+    exp = oracle.search_neighbors(pts, d, prec)
+    assert exp.shape[0] >= m // 2  # (most placed pairs are within d in the engine's precision)
+    assert got.shape == exp.shape and np.array_equal(got, exp)
+
+
+@precisions
 def test_neighbor_search_bitexact_c1(c1_design, prec):
     e = Engine(c1_design.n, precision=prec)
     e.set_positions(c1_design.positions)
