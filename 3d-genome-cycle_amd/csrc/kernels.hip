@@ -2928,7 +2928,24 @@ constexpr int kLFlagBBox = 2;   // the next step rebuilds: reduce the bounding b
 constexpr int kLFlagStats = 4;  // reduce the neighbour count (diagnostics: ctx->neighbors)
 constexpr int kLFlagDomain = 8;  // decomposed (k_lstep<..., DOM>): owned slots only, local reduction -> a.dom_red
 
-__device__ void list_tail_apply(DevCtx* ctx, const ForceArgs& a, const ListTailIn& in, const ListTotals& t, int flags)
+// the schedule's closed forms of the next step (time, core and bond scale): they need no totals, so k_pstep
+// evaluates them while the step's totals are still landing and hands them to list_tail_apply (the same expressions)
+struct TailSched {
+    double time, cs, bs;
+};
+__device__ __forceinline__ TailSched list_tail_sched(const ListTailIn& in)
+{
+    TailSched s{in.c_time, in.c_cs, 0.0};
+    const int sf = (int)in.s_flags;
+    if (sf & 1) s.time = (double)(in.c_step + 1) * in.s_dt;
+    if (sf & 2) {
+        s.cs = 1.0 - (1.0 - in.s_cs0) * exp(-(s.time / in.s_csTau));
+        s.bs = 1.0 - (1.0 - in.s_bs0) * exp(-(s.time / in.s_bsTau));
+    }
+    return s;
+}
+__device__ void list_tail_apply(DevCtx* ctx, const ForceArgs& a, const ListTailIn& in, const ListTotals& t, int flags,
+                                const TailSched* pre = nullptr)
 {
     const long long step = in.c_step + 1;
     for (int k = 0; k < 3; ++k) {
@@ -2945,10 +2962,11 @@ __device__ void list_tail_apply(DevCtx* ctx, const ForceArgs& a, const ListTailI
     if (flags & kLFlagSched) {
         const int sf = (int)in.s_flags;
         const double dt = in.s_dt;
-        if (sf & 1) ctx->time = time = (double)step * dt;
+        const TailSched s = pre ? *pre : list_tail_sched(in);
+        if (sf & 1) ctx->time = time = s.time;
         if (sf & 2) {
-            ctx->cs = cs = 1.0 - (1.0 - in.s_cs0) * exp(-(time / in.s_csTau));
-            ctx->bs = 1.0 - (1.0 - in.s_bs0) * exp(-(time / in.s_bsTau));
+            ctx->cs = cs = s.cs;
+            ctx->bs = s.bs;
         }
         if (sf & 4) {
             for (int k = 0; k < 3; ++k) {
@@ -4337,7 +4355,11 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
             if (dbs && tid == 64) dbs[12] = wall_clock64();
         } else {
             ListTailIn tin;
-            if (tid == 0) tin = list_tail_load(&s_ctx, a);  // (the tail's inputs that do not need the totals)
+            TailSched tsc;
+            if (tid == 0) {  // the tail's inputs and the schedule's closed forms: they need no totals
+                tin = list_tail_load(&s_ctx, a);
+                tsc = list_tail_sched(tin);
+            }
             pget_image<R>(half, n, G, n, n + G * kPTotRecs<R>, lane, 64, tag, s_pos, s_pfx, s_pfy, s_pfz, s_tot,
                           &s_stall, [] {}, dbs && tid == 0 ? dbs + 4 : nullptr);
             // the step's totals, in a fixed order (the same totals in every workgroup, bitwise): lane 8 c + p sums
@@ -4362,7 +4384,7 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
             for (int c = 0; c < 6; ++c) t.bb[c] = 0.f;
             t.drift = 0.0;
             if (tid == 0) {
-                list_tail_apply(&s_ctx, a, tin, t, flags | (k == steps - 1 ? kLFlagStats : 0));
+                list_tail_apply(&s_ctx, a, tin, t, flags | (k == steps - 1 ? kLFlagStats : 0), &tsc);
                 if (dbs) dbs[6] = wall_clock64();
             }
         }
