@@ -257,9 +257,9 @@ struct gcs_engine {
     int* list = nullptr;
     int* lcount = nullptr;
     int4* lbase = nullptr;
-    int* ltile = nullptr;  // ListTile16 tile table (ForceArgs::ltile)
-    int* lstage = nullptr;  // ListTile16 image sources (ForceArgs::lstage)
-    unsigned* psync = nullptr;  // the persistent small-system step's barrier counter and accumulator sets
+    unsigned* psync = nullptr;  // the persistent small-system step's hand-off halves
+    int* pstall = nullptr;      // its stall word (ForceArgs::pstall)
+    DevCtx* pkeep = nullptr;    // the context at the start of the current k_pstep launch (k_pstep_guard)
     int small_opt = 1;          // GCS_OPT_SMALL_STEP
     bool fused_explicit = false;  // GCS_OPT_FUSED_STEP was set: the step shape it names, never the small step
     float4* psort[2] = {nullptr, nullptr};
@@ -277,8 +277,8 @@ struct gcs_engine {
     int list_every_opt = 0;     // GCS_OPT_LIST_EVERY: rebuild period in steps (0: from the noise amplitude)
     int list_every = 1;         // the period of the current run
     int list_waves = 4;         // GCS_OPT_LIST_WAVES: waves per tile (2: more tiles resident, for replica runs)
-    int list_fmt_opt = 0;       // GCS_OPT_LIST_FORMAT: 0 tile-staged 16-bit (default), 1 plane-relative 16-bit, 2 absolute
-                                // 32-bit, 3 the slot entries of round 4 (absolute 16-bit up to 65,536, plane-relative beyond)
+    int list_fmt_opt = 0;       // GCS_OPT_LIST_FORMAT: 0 (default) 16-bit slots (absolute up to 65,536 particles,
+                                // plane-relative beyond), 1 plane-relative 16-bit, 2 absolute 32-bit
     long long list_deal_opt = -1;  // GCS_OPT_LIST_DEAL: chunk -> wave pattern of the list build (-1: the default for
                                    // list_waves, 0: round robin)
     bool l_need_build = true;   // the next list step must rebuild (run start without continuity)
@@ -761,7 +761,7 @@ void enqueue_cell_order(gcs_engine* e, bool lists = false, int* islot = nullptr)
         if (lists)
             launch_cell_sort(e->stream, e->ctx, e->dpos[0], e->dpos[1], e->dkmu, e->n, e->tmp, e->cell_of, e->cstart,
                              e->sidx, e->scell, e->spos, e->sb, mix, e->ptype, e->dpsort[0], e->dpsort[1], e->dskmu,
-                             e->sbrow, boff, islot);
+                             e->sbrow, boff, islot, e->psort[0], e->psort[1]);
         else
             launch_cell_sort(e->stream, e->ctx, e->dpos[0], e->dpos[1], e->dkmu, e->n, e->tmp, e->cell_of, e->cstart,
                              e->sidx, e->scell, e->spos, e->sb, mix);
@@ -860,21 +860,15 @@ int skin_level(const gcs_engine* e, int64_t st)
     return std::max(50, (int)std::lround(s1 * u / 10.0) * 10);
 }
 
-// the list entry format (GCS_OPT_LIST_FORMAT): 16-bit indices into the step tile's LDS image of its partner rows
-// (kernels.hip ListTile16, the default), or the slot entries the option names: absolute 16-bit slots up to 65,536
-// particles and plane-relative 16-bit slots beyond (ListRel16), or absolute 32-bit slots.  Every format holds the
-// same pairs in the same order: the trajectories are bitwise the same
+// the list entry format (GCS_OPT_LIST_FORMAT): 0 (default) absolute 16-bit slots up to 65,536 particles and
+// plane-relative 16-bit slots beyond (kernels.hip ListRel16), 1 plane-relative at any size, 2 absolute 32-bit slots.
+// Every format holds the same pairs in the same order: the trajectories are bitwise the same
 int list_format(const gcs_engine* e)
 {
     if (e->list_fmt_opt == 2) return kListFmtInt;
     if (e->list_fmt_opt == 1) return kListFmtRel16;
-    // 3: the tile-staged entries (an experiment: slower than the slot entries at C2 and C5 on MI355X, DESIGN.md §4
-    // "List entry formats"; its LDS class table holds kTileTypes classes; undecomposed runs only)
-    if (e->list_fmt_opt == 3 && e->ntypes <= kTileTypes && !e->dom) return kListFmtTile16;
     return e->n <= 65536 ? kListFmtAbs16 : kListFmtRel16;
 }
-// window-table entries: one per step workgroup (64 slots)
-size_t ltile_entries(const gcs_engine* e) { return (size_t)force_blocks(e->n); }
 
 // the list build's chunk deal (kernels.hip deal_nth): the option, or the default for the waves per tile
 unsigned long long list_deal(const gcs_engine* e)
@@ -920,11 +914,8 @@ ForceArgs list_args(const gcs_engine* e)
     a.list_waves = e->list_waves;
     a.list_fmt = list_format(e);
     a.lbase = e->lbase;
-    a.ltile = e->ltile;
-    a.lstage = e->lstage;
     // the non-temporal hint beyond 16-bit absolute lists that the L2s keep (kernels.hip k_lstep)
-    a.list_nt = (a.list_fmt == kListFmtRel16 || a.list_fmt == kListFmtInt || (a.list_fmt == kListFmtTile16 && e->n > 65536))
-                    ? 1 : 0;
+    a.list_nt = (a.list_fmt == kListFmtRel16 || a.list_fmt == kListFmtInt) ? 1 : 0;
     a.list_deal = list_deal(e);
     a.par_hint = -1;
     return a;
@@ -938,8 +929,6 @@ int ensure_list(gcs_engine* e)
     dfree(e->list);
     dfree(e->lcount);
     dfree(e->lbase);
-    dfree(e->ltile);
-    dfree(e->lstage);
     dfree(e->psort[0]);
     dfree(e->psort[1]);
     dfree(e->skmu);
@@ -950,12 +939,11 @@ int ensure_list(gcs_engine* e)
     e->list_alloc = 0;
     int rc;
     if ((rc = dalloc(&e->list, need)) || (rc = dalloc(&e->lcount, stride * kMaxListWaves)) ||
-        (rc = dalloc(&e->lbase, stride)) || (rc = dalloc(&e->sbrow, stride)) ||
-        (rc = dalloc(&e->ltile, ltile_entries(e) * kListTileWords)) ||
-        (rc = dalloc(&e->lstage, ltile_entries(e) * (size_t)stage_capacity(e->prec))))
+        (rc = dalloc(&e->lbase, stride)) || (rc = dalloc(&e->sbrow, stride)))
         return rc;
-    if (e->prec == 64) {  // the slot-ordered copies in the engine's precision only
-        if ((rc = dalloc(&e->dpsort[0], stride)) || (rc = dalloc(&e->dpsort[1], stride)) || (rc = dalloc(&e->dskmu, stride)))
+    if (e->prec == 64) {  // the slot-ordered copies in the engine's precision, + fp64: the prefilter copies (psort)
+        if ((rc = dalloc(&e->dpsort[0], stride)) || (rc = dalloc(&e->dpsort[1], stride)) ||
+            (rc = dalloc(&e->dskmu, stride)) || (rc = dalloc(&e->psort[0], stride)) || (rc = dalloc(&e->psort[1], stride)))
             return rc;
     } else {
         if ((rc = dalloc(&e->psort[0], stride)) || (rc = dalloc(&e->psort[1], stride)) || (rc = dalloc(&e->skmu, stride)))
@@ -1583,9 +1571,9 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->list);
     dfree(e->lcount);
     dfree(e->lbase);
-    dfree(e->ltile);
-    dfree(e->lstage);
     dfree(e->psync);
+    dfree(e->pstall);
+    dfree(e->pkeep);
     dfree(e->psort[0]);
     dfree(e->psort[1]);
     dfree(e->skmu);
@@ -1858,15 +1846,34 @@ int gcs_engine_set_positions(gcs_engine* e, const double* xyz, int64_t n)
     return GCS_OK;
 }
 
+// A cell scan whose look-back gave up waiting (kernels.hip lookback_sum, counted in DevCtx::scan_stall) leaves wrong
+// cell lists behind: the synchronising reads (positions, samples, context) enqueue the count's copy before their
+// synchronisation and fail once it is non-zero, so a run that went through such a scan is never read as valid
+namespace {
+void enqueue_stall_read(gcs_engine* e, int* dst)
+{
+    (void)hipMemcpyAsync(dst, (const char*)e->ctx + offsetof(DevCtx, scan_stall), sizeof(int), hipMemcpyDeviceToHost,
+                         e->stream);
+}
+int stall_failure()
+{
+    return fail(GCS_ESTATE, "a multi-block cell scan's look-back stalled (DevCtx::scan_stall): the cell lists, and the "
+                            "run that used them, are void");
+}
+}  // namespace
+
 int gcs_engine_get_positions(gcs_engine* e, double* xyz, int64_t n)
 {
     if (!e || !xyz) return fail(GCS_EINVAL, "null argument");
     if (n != e->n) return fail(GCS_EINVAL, "position count does not match the particle count");
     HIPCHK(hipSetDevice(e->device));
+    int stalls = 0;
+    enqueue_stall_read(e, &stalls);
     if (e->prec == 64) {
         std::vector<double4> h(n);
         HIPCHK(hipMemcpyAsync(h.data(), e->dpos[e->parity], n * sizeof(double4), hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
+        if (stalls) return stall_failure();
         for (int64_t i = 0; i < n; ++i) {
             xyz[3 * i] = h[i].x;
             xyz[3 * i + 1] = h[i].y;
@@ -1877,6 +1884,7 @@ int gcs_engine_get_positions(gcs_engine* e, double* xyz, int64_t n)
     std::vector<float4> h(n);
     HIPCHK(hipMemcpyAsync(h.data(), e->pos[e->parity], n * sizeof(float4), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
+    if (stalls) return stall_failure();
     for (int64_t i = 0; i < n; ++i) {
         xyz[3 * i] = h[i].x;
         xyz[3 * i + 1] = h[i].y;
@@ -1892,6 +1900,7 @@ int gcs_engine_get_context(gcs_engine* e, gcs_context* c)
     DevCtx d;
     HIPCHK(hipMemcpyAsync(&d, e->ctx, sizeof(d), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
+    if (d.scan_stall) return stall_failure();
     c->step = d.step;
     c->time = d.time;
     c->core_scale = d.cs;
@@ -2004,8 +2013,20 @@ int run_small(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64
     if ((rc = flush_contacts(e))) return rc;
     if ((rc = begin_run(e, cfg, first_step))) return rc;
     if (!e->psync && (rc = dalloc(&e->psync, kPSyncWords))) return rc;
+    if (!e->pstall) {
+        if ((rc = dalloc(&e->pstall, 1)) || (rc = dalloc(&e->pkeep, 1))) return rc;
+        HIPCHK(hipMemsetAsync(e->pstall, 0, sizeof(int), e->stream));
+    }
     ForceArgs a = e->fa;
     a.psync = e->psync;
+    a.pstall = e->pstall;
+    a.pstep_skip = -1;
+    // GCS_DEBUG_PSTEP_SKIP=<workgroup>:<step> (tests): that workgroup does not publish its hand-off of that step of
+    // the run's first launch, so every workgroup stalls -- the run must fail, with the context and positions as before
+    if (const char* sk = std::getenv("GCS_DEBUG_PSTEP_SKIP")) {
+        int wg = -1, st = -1;
+        if (std::sscanf(sk, "%d:%d", &wg, &st) == 2 && wg >= 0 && st >= 0 && st < 65536) a.pstep_skip = (wg << 16) | st;
+    }
     // GCS_DEBUG_PSTEP=<file>: workgroup 0's phase stamps of the first 64 steps of the call's first launch
     const char* dbg_path = std::getenv("GCS_DEBUG_PSTEP");
     unsigned long long* dbg = nullptr;
@@ -2028,13 +2049,29 @@ int run_small(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, int64
     for (int64_t done = 0; done < steps;) {
         const int len = (int)std::min<int64_t>(kPChunk, steps - done);
         HIPCHK(hipMemsetAsync(e->psync, 0, kPSyncWords * sizeof(unsigned), e->stream));
+        launch_pstep_guard(e->stream, e->ctx, e->pkeep, e->pstall, 0);
         if (launch_pstep(e->stream, e->ctx, a, len, e->sched_flags != 0 ? 1 : 0))
             return fail(GCS_EHIP, "the persistent small-system step could not be launched cooperatively");
         e->rstats.eager_steps += len;
         done += len;
         a.dbg_times = nullptr;
+        a.pstep_skip = -1;
     }
+    // a stalled hand-off fails the run: the context goes back to the failing launch's start (its positions are
+    // intact: a launch writes only the other parity), the stall word is cleared for the next run
+    launch_pstep_guard(e->stream, e->ctx, e->pkeep, e->pstall, 1);
+    int stalled = 0;
     HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(&stalled, e->pstall, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (stalled) {
+        HIPCHK(hipMemsetAsync(e->pstall, 0, sizeof(int), e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        e->chain_valid = false;
+        if (dbg) (void)hipFree(dbg);
+        return fail(GCS_ESTATE, "the persistent small-system step stalled: a workgroup's hand-off did not arrive "
+                                "(the run is void; the context and positions are those before the failing launch)");
+    }
     if (dbg) {
         std::vector<unsigned long long> h(kPDebugWords);
         HIPCHK(hipMemcpyAsync(h.data(), dbg, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost, e->stream));
@@ -2442,8 +2479,11 @@ int gcs_engine_sample_positions(gcs_engine* e, float* xyz, int64_t n, int32_t fr
     else
         launch_quantize(e->stream, e->pos[e->parity], e->q_out, e->n, fraction_bits);
     HIPCHK(hipGetLastError());
+    int stalls = 0;
+    enqueue_stall_read(e, &stalls);
     HIPCHK(hipMemcpyAsync(e->q_host, e->q_out, 3 * (size_t)n * sizeof(float), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
+    if (stalls) return stall_failure();
     std::memcpy(xyz, e->q_host, 3 * (size_t)n * sizeof(float));
     return GCS_OK;
 }
@@ -3326,9 +3366,9 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         return GCS_OK;
     }
     if (option == GCS_OPT_LIST_FORMAT) {
-        if (value < 0 || value > 3)
-            return fail(GCS_EINVAL, "list format must be 0 (tile-staged, default), 1 (plane-relative 16-bit), 2 (32-bit) or "
-                                    "3 (16-bit slots: absolute up to 65,536 particles, plane-relative beyond)");
+        if (value < 0 || value > 2)
+            return fail(GCS_EINVAL, "list format must be 0 (default: 16-bit slots, absolute up to 65,536 particles, "
+                                    "plane-relative beyond), 1 (plane-relative 16-bit) or 2 (32-bit)");
         e->list_fmt_opt = (int)value;
         e->l_need_build = true;
         drop_graph(e);

@@ -297,14 +297,14 @@ struct ForceArgs {
     int list_stride;        // >= N
     float list_skin;        // > 0 only in the list path's own argument block
     int list_waves;         // waves per tile (list segments): 4, or 2 (GCS_OPT_LIST_WAVES)
-    int list_fmt;           // list entries: kListFmtTile16 / kListFmtAbs16 / kListFmtInt / kListFmtRel16 (list_format)
+    int list_fmt;           // list entries: kListFmtAbs16 / kListFmtInt / kListFmtRel16 (list_format)
     int list_nt;            // read the list words with the non-temporal hint (lists far beyond the L2s)
-    // kListFmtTile16 (kernels.hip ListTile16): per step window (64 slots) kListTileWords ints written by the build,
-    // the staged rows of its (up to two) row parts (layout: kernels.hip stage_slot)
-    int* ltile;
-    int* lstage;  // per window stage_capacity(prec) ints: the slot of each record of the step's LDS image
-    // the persistent small-system step (kernels.hip k_pstep): [0] the grid-barrier counter, then three accumulator sets
+    // the persistent small-system step (kernels.hip k_pstep): the hand-off halves (zeroed before every launch)
     unsigned* psync;
+    // k_pstep's stall word (device, zeroed by the engine): a workgroup whose hand-off poll gives up adds 1 and stops
+    // integrating, every other workgroup stops at its next poll; the host fails the run (engine.hip run_small)
+    int* pstall;
+    int pstep_skip;  // GCS_DEBUG_PSTEP_SKIP (tests): workgroup << 16 | step that does not publish its hand-off; -1: none
     unsigned long long list_deal;  // list build: candidate chunk -> wave segment pattern (GCS_OPT_LIST_DEAL; 0: round robin)
     int par_hint;           // >= 0: ctx->parity of this launch, known to the host at enqueue (the slot loads need not
                             // wait for the context); -1: read it
@@ -354,6 +354,7 @@ template <> struct St<float> {
     __host__ __device__ static const float* noise(const ForceArgs& a) { return a.noise; }
     __host__ __device__ static float4* force(const ForceArgs& a) { return a.force_out; }
     __host__ __device__ static const FieldPrm<float>& prm(const ForceArgs& a) { return a.pf; }
+    __host__ __device__ static float4* fsort(const ForceArgs&, int) { return nullptr; }
 };
 template <> struct St<double> {
     __host__ __device__ static double4* pos(const ForceArgs& a, int par) { return par ? a.dpos1 : a.dpos0; }
@@ -367,7 +368,21 @@ template <> struct St<double> {
     __host__ __device__ static const double* noise(const ForceArgs& a) { return a.dnoise; }
     __host__ __device__ static double4* force(const ForceArgs& a) { return a.dforce_out; }
     __host__ __device__ static const FieldPrm<double>& prm(const ForceArgs& a) { return a.pd; }
+    // the fp64 list step's prefilter copy: the fp32 roundings of psort's positions (slot order, .w unused), in the
+    // fp32 slot-order buffers an fp64 engine does not otherwise use; nullptr outside the list path
+    __host__ __device__ static float4* fsort(const ForceArgs& a, int par) { return par ? a.psort1 : a.psort0; }
 };
+// a slot's new position into the slot-order buffer of parity par and, fp64, into its prefilter copy (every writer of
+// psort goes through here, so the copy is the rounding of psort at every step)
+template <typename R>
+__device__ __forceinline__ void put_slot(const ForceArgs& a, int par, int s, const real4<R>& q)
+{
+    St<R>::psort(a, par)[s] = q;
+    if constexpr (sizeof(R) == 8) {
+        float4* const f = St<R>::fsort(a, par);
+        if (f) f[s] = make_float4((float)q.x, (float)q.y, (float)q.z, 0.f);
+    }
+}
 
 // list step launch accumulators behind the arrival counters in ForceArgs::lticket (unsigned words, 128 B per slot):
 // per group of workgroups (b % 8) kListAccSlots slots + one overflow flag (kernels.hip list_accumulate)
@@ -394,16 +409,9 @@ constexpr int kListIndexBits = 24;      // particle index bits of a list entry
 constexpr int kListFmtAbs16 = 0;
 constexpr int kListFmtInt = 1;
 constexpr int kListFmtRel16 = 2;
-// 16-bit indices into the step tile's LDS image of its partners (kernels.hip ListTile16: the default at any size)
-constexpr int kListFmtTile16 = 3;
 constexpr int kPMax = 1536;         // particles of the persistent small-system step (kernels.hip k_pstep: LDS images)
 constexpr int kPHalfBytes = kPMax * 48 + 256 * 144;  // its hand-off buffer (psync): two halves (kernels.hip k_pstep)
 constexpr int kPSyncWords = 2 * kPHalfBytes / 4;
-constexpr int kListTileWords = 128;  // ints per window-table entry (kernels.hip stage_slot_w: 73 used)
-constexpr int kTileTypes = 64;
-// records of the ListTile16 step's LDS image (kernels.hip k_lstep: 33,792 B; fp64 28 B per record in three arrays, fp32
-// whole 16-B records)
-__host__ __device__ constexpr int stage_capacity(int prec) { return prec == 64 ? 1152 : 2112; }      // pair-factor classes of the ListTile16 step (its LDS class table; more: slot entries)
 constexpr int kListCountMask = (1 << 30) - 1;
 constexpr int kListOverflow = 1 << 30;
 
@@ -429,8 +437,8 @@ __device__ __forceinline__ void dom_unpack_records(const ForceArgs& a, const rea
             const int sl = slots ? a.islot[i] : -1;
             if (sl >= 0) {
                 const R4 q = mk4<R>(r.x, r.y, r.z, wpack<R>(i | (a.ptype[i] << kListIndexBits)));
-                St<R>::psort(a, 0)[sl] = q;
-                St<R>::psort(a, 1)[sl] = q;
+                put_slot<R>(a, 0, sl, q);
+                put_slot<R>(a, 1, sl, q);
             }
         }
     }
@@ -488,7 +496,8 @@ void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const double4* pos0, con
                       int n, const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell,
                       float4* spos, float* sb, int pair_mix, const int* ptype = nullptr, double4* psort0 = nullptr,
                       double4* psort1 = nullptr, double4* skmu = nullptr, int2* sbrow = nullptr,
-                      const int* boff = nullptr, int* islot = nullptr);
+                      const int* boff = nullptr, int* islot = nullptr, float4* fsort0 = nullptr,
+                      float4* fsort1 = nullptr);
 // list step: build the neighbour lists on the current cell list (grid rc = cutoff + skin); one step from them
 void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a);
 // flags: 1 apply the schedule, 2 the next step rebuilds (bounding box -> grid), 4 neighbour-count statistics,
@@ -514,6 +523,8 @@ int list_step_grid(const ForceArgs& a);
 // the persistent small-system step: `steps` steps of n <= kPMax particles in ONE cooperative launch (a.psync zeroed
 // by the caller first); flags: kernels.hip kLFlagSched when the schedule applies
 int launch_pstep(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int steps, int flags);
+// k_pstep_guard: restore 0 keeps *ctx in *keep unless *stall; restore 1 puts *keep back into *ctx if *stall
+void launch_pstep_guard(hipStream_t s, DevCtx* ctx, DevCtx* keep, const int* stall, int restore);
 void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceArgs& a, bool fused);
 // fp64 force / energy evaluation on the current cell list (one thread per sorted slot; kernels.hip k_eval64):
 // kModeForce -> a.dforce_out + partial rows a.dpart [blocks][8] (reactions in[3], out[3], max mu|F|, neighbours),

@@ -712,7 +712,7 @@ __device__ __forceinline__ void tail_body(DevCtx* ctx, const ForceArgs& a, int f
 constexpr int kMbThreads = 256;
 constexpr int kMbSeg = 8;
 constexpr int kMbCells = kMbThreads * kMbSeg;
-constexpr unsigned kMbSpinCap = 1u << 22;  // look-back polls before giving up (counted in ctx->scan_stall)
+constexpr unsigned kMbSpinCap = 1u << 22;  // look-back polls before giving up (ctx->scan_stall: the host's reads fail)
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
@@ -1228,7 +1228,8 @@ __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ct
                                                    const int* __restrict__ ptype, real4<R>* __restrict__ psort0,
                                                    real4<R>* __restrict__ psort1, real4<R>* __restrict__ skmu,
                                                    int2* __restrict__ sbrow, const int* __restrict__ boff,
-                                                   int* __restrict__ islot)
+                                                   int* __restrict__ islot, float4* __restrict__ fsort0,
+                                                   float4* __restrict__ fsort1)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n || s >= cstart[ctx->grid.ncell]) return;  // binned particles only (all of them, undecomposed)
@@ -1249,6 +1250,8 @@ __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ct
     if (psort0) {  // list path: the current positions in slot order, .w = particle | class << 24; the slot's
                    // constants and bond CSR row (the list step reads them by slot, not behind the particle index)
         (ctx->parity ? psort1 : psort0)[d] = mk4<R>(p.x, p.y, p.z, wpack<R>(i | (ptype[i] << kListIndexBits)));
+        if (fsort0)  // fp64: the list step's prefilter copy (put_slot)
+            (ctx->parity ? fsort1 : fsort0)[d] = make_float4((float)p.x, (float)p.y, (float)p.z, 0.f);
         skmu[d] = k;
         sbrow[d] = boff ? make_int2(boff[i], boff[i + 1]) : make_int2(0, 0);
         if (islot) islot[i] = d;
@@ -1420,18 +1423,21 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
     if (a.sw_n > 0) {
         // the droplet (simulation_driver_forcefield.cpp:164-185: softwell among the nucleolar targets, cut off at
         // apply_cutoff): every target interacts with every other; a wave holding a target loads all targets' positions
-        // once (lane t: target t) and walks them by shuffles, in target order
+        // once (lane t: target t) and walks them by shuffles, in target order.  With nq lanes per particle lane lq
+        // takes targets lq, lq + nq, ...; every lane runs the same trip count, so each shuffle's source lane is still
+        // in the loop (lanes leaving after different counts read targets from lanes that had left)
         const bool tgt = km.w != R(0);
         if (__ballot(tgt)) {
             const int m = a.sw_n;
             const int jt = (__lane_id() < m) ? a.sw_idx[__lane_id()] : 0;
             const real4<R> pt = posc[jt];
-            for (int t = lq; t < m; t += nq) {
+            for (int t0 = 0; t0 < m; t0 += nq) {
+                const int t = min(t0 + lq, 63);
                 const int j = __shfl(jt, t);
                 const R px = __shfl(pt.x, t), py = __shfl(pt.y, t), pz = __shfl(pt.z, t);
                 const R rx = xi - px, ry = yi - py, rz = zi - pz;
                 const R r2 = r_fma(rz, rz, r_fma(ry, ry, rx * rx));
-                if (tgt && j != i && r2 < P.sw_la) {
+                if (tgt && t0 + lq < m && j != i && r2 < P.sw_la) {
                     const R u6 = r2 * P.sw_kb;
                     const R den = R(1) + u6 * u6 * u6;
                     const R c = R(-6) * P.sw_ka * u6 * u6 * P.sw_kb / (den * den);
@@ -1811,59 +1817,14 @@ __device__ __forceinline__ size_t list_at(int w, int cap, int k, int s, size_t s
 struct ListRel16 {
     unsigned short v;
 };
-// ListTile16 (kListFmtTile16, the default): 16-bit indices into the step tile's LDS image of its partner rows.  The
-// list build and the step share their tiles (<= 64 consecutive slots of one cell row, k_cell_scan's tile table); a
-// tile's partners lie in 9 stencil rows, each a contiguous slot range [cell (x_first - fx), cell (x_last + fx)] of
-// rows y - 1 .. y + 1 in planes z - 1 .. z + 1 at the build.  The build concatenates those ranges (the staged rows,
-// kStageRow order: the tile's own row first, corner rows last) and an entry is the partner's position in that
-// concatenation; the step copies the ranges' CURRENT positions into LDS with LDS-DMA (coalesced rows), so a list entry
-// costs an LDS read instead of an L2/HBM gather.  Slots are fixed between builds, so the same index holds across the
-// period.  Entries beyond the LDS image (tiles whose staged rows exceed kStageBytes) are gathered from global memory
-// through the same row table.  The entry order, hence every sum, is that of the slot formats: bitwise the same.
-struct ListTile16 {
-    unsigned short v;
-};
 template <typename LE>
 struct ListFmt {
     static constexpr bool rel = false;
-    static constexpr bool tile = false;
 };
 template <>
 struct ListFmt<ListRel16> {
     static constexpr bool rel = true;
-    static constexpr bool tile = false;
 };
-template <>
-struct ListFmt<ListTile16> {
-    static constexpr bool rel = false;
-    static constexpr bool tile = true;
-};
-// the staged rows in order: stencil row q = (dz + 1) * 3 + (dy + 1) of staged position k (the tile's own row first,
-// then the 4 edge-adjacent rows, the corner rows last: what an LDS image too small for all 9 keeps is the rows
-// holding most partners)
-__device__ __forceinline__ int stage_row(int k)
-{
-    return (int)((0x862075314ull >> (4 * k)) & 15ull);  // k = 0..8: rows 4, 1, 3, 5, 7, 0, 2, 6, 8
-}
-// A window's table entry (ForceArgs::ltile, kListTileWords ints): staged row r = 9 p + k (part p < kWinParts of the
-// window, its staged row k) starts at staged index t[r] (non-decreasing in r; rows of absent parts start at the
-// total) and holds the slots from t[36 + r] on; t[72] = the total.  The slot of staged index v < t[72]: that of the
-// last row starting at or before v, found by a binary search over the 36 row starts held one per lane (tw0 = t[lane],
-// tw1 = t[64 + lane]; lane-indexed reads of them are ds_bpermute)
-constexpr int kWinParts = 4;
-__device__ __forceinline__ int stage_slot_w(int v, int tw0, int tw1)
-{
-    int lo = 0;
-#pragma unroll
-    for (int st = 32; st > 0; st >>= 1) {
-        const int c = min(lo + st, 35);
-        const int t = __shfl(tw0, c);
-        lo = (lo + st < 36 && t <= v) ? lo + st : lo;
-    }
-    const int tv = __shfl(tw0, lo);
-    const int j0 = __shfl(tw0, min(36 + lo, 63)), j1 = __shfl(tw1, max(lo - 28, 0));
-    return v - tv + (lo < 28 ? j0 : j1);
-}
 constexpr int kRelBits = 14;
 // the partner slot of a list entry (x: its raw bits)
 template <typename LE>
@@ -1918,7 +1879,7 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                                        int s_begin, int s_end, float4 pi, float bi, float& fx, float& fy, float& fz,
                                        float& acc, int* s_rowV, int* s_rowJ, float4* s_cand, int* s_candj, int& ntot,
                                        int wv, int nwv, int self = -1, bool lvalid = false, int* lcnt = nullptr,
-                                       unsigned long long* lpend = nullptr, int4* plb = nullptr, int* s_tile = nullptr)
+                                       unsigned long long* lpend = nullptr, int4* plb = nullptr)
 {
     // kModeList: phase 2 appends each hit (other than the particle itself) to the lane's list segment wv
     // instead of evaluating the pair force (the lists of the list step, built at the grid's rc = cutoff + skin)
@@ -1970,73 +1931,6 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 b[p] = (z >= 0 && z < nz) ? a.cstart[(z * ny + yb) * nx + xb] : 0;
             }
             *plb = make_int4(b[0], b[1], b[2], 0);
-        }
-        if constexpr (MODE == kModeList && ListFmt<LE>::tile) {
-            // the staged rows of the step windows this tile meets (ListTile16; windows of 64 slots, each in up to
-            // kWinParts row parts), one window at a time: the window's slots' cells (one coalesced load), a ballot of
-            // the row changes = the parts' first slots, then lane p * 16 + k, k < 9, takes staged row k (stencil row
-            // stage_row(k)) of part p.  Outputs: the window's table entry (wave 0; identical from every workgroup
-            // that meets the window: kernels.hip stage_slot_w's layout), s_tile[(4 wi + p) * 9 + q] = staged index -
-            // slot of stencil row q of part p of window wi, s_tile[72 + 2 wi], [73 + 2 wi] = its part-start mask
-            const int nsl = a.cstart[g.ncell];  // binned slots
-            const int wA = s_begin >> 6, wZ = (s_end - 1) >> 6;
-            const int p = lane >> 4, k = lane & 15;
-            for (int wi = 0; wi < 2; ++wi) {
-                const int w = wA + wi;
-                if (w > wZ) break;
-                const int wb = w * kTile, we = min(wb + kTile, nsl);
-                const int cell = wb + lane < we ? a.scell[wb + lane] : -1;
-                const int row = cell >= 0 ? cell / nx : -1;
-                const int rprev = __shfl(row, max(lane - 1, 0));
-                const unsigned long long m = __ballot(cell >= 0 && (lane == 0 || row != rprev));
-                // part p: lanes [f, l] of the window
-                unsigned long long mm = m;
-                for (int q = 0; q < p; ++q) mm &= mm - 1ull;
-                const int f = mm ? __ffsll((long long)mm) - 1 : -1;
-                const unsigned long long mn = mm & (mm - 1ull);
-                const int l = mn ? __ffsll((long long)mn) - 2 : (we - wb) - 1;
-                const int fr = __shfl(row, max(f, 0)), fc = __shfl(cell, max(f, 0)), lc = __shfl(cell, max(l, 0));
-                int tl = 0, tj = 0;
-                if (f >= 0 && k < 9) {
-                    const int q = stage_row(k);
-                    const int x0 = fc % nx, x1 = lc % nx;
-                    const int xlo = max(x0 - gfx, 0), xhi = min(x1 + gfx, nx - 1);
-                    const int y = fr % ny + q % 3 - 1, z = fr / ny + q / 3 - 1;
-                    if (y >= 0 && y < ny && z >= 0 && z < nz) {
-                        const int base = (z * ny + y) * nx;
-                        tj = a.cstart[base + xlo];
-                        tl = a.cstart[base + xhi + 1] - tj;
-                    }
-                }
-                int tincl = tl;
-                GCS_DPP_SCAN(dpp_i, add_i, 0, tincl)
-                const int tv = tincl - tl;  // the row's first staged index (rows in part-major order)
-                if (k < 9) s_tile[(4 * wi + p) * 9 + stage_row(k)] = tv - tj;
-                if (lane == 0) {
-                    s_tile[72 + 2 * wi] = (int)(unsigned)m;
-                    s_tile[73 + 2 * wi] = (int)(unsigned)(m >> 32);
-                }
-                if (wv == 0) {
-                    int* const t = a.ltile + (size_t)w * kListTileWords;
-                    if (k < 9) {
-                        t[p * 9 + k] = tv;
-                        t[36 + p * 9 + k] = tj;
-                    }
-                    if (lane == 63) t[72] = tincl;  // the total
-                    // the slot of every staged record the step's LDS image holds (its LDS-DMA sources; 0 past the
-                    // total: every entry a valid slot), row by row, coalesced
-                    const int ks = stage_capacity(a.prec);
-                    const int total = __shfl(tincl, 63);
-                    int* const ls = a.lstage + (size_t)w * ks;
-                    for (int r = 0; r < 36; ++r) {
-                        const int lr = (r / 9) * 16 + r % 9;
-                        const int rs = __builtin_amdgcn_readlane(tv, lr), rj = __builtin_amdgcn_readlane(tj, lr);
-                        const int rl = min(__builtin_amdgcn_readlane(tl, lr), ks - rs);
-                        for (int u = lane; u < rl; u += 64) ls[rs + u] = rj + u;
-                    }
-                    for (int v = min(total, ks) + lane; v < ks; v += 64) ls[v] = 0;
-                }
-            }
         }
         int incl = len;
         GCS_DPP_SCAN(dpp_i, add_i, 0, incl)
@@ -2091,8 +1985,8 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 for (int step = 8; step > 0; step >>= 1)
                     if (rowV[lo + step] <= v) lo += step;
                 nj[f] = rowJ[lo] + (v - rowV[lo]);
-                // ListRel16: the stencil row's z plane (rows q = 0..8: z = z0 + q / 3 - 1); ListTile16: the row
-                npl[f] = ListFmt<LE>::tile ? lo : lo / 3;
+                // ListRel16: the stencil row's z plane (rows q = 0..8: z = z0 + q / 3 - 1)
+                npl[f] = lo / 3;
                 np[f] = a.spos[nj[f]];
                 nb[f] = a.sb[nj[f]];
             }
@@ -2116,7 +2010,7 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                 P[h8 + 6] = fmaf(pz, pz, fmaf(py, py, px * px));
                 // the partner's slot (< 2^24) and, for ListRel16, its plane in bits 28..29
                 reinterpret_cast<int*>(my_cand)[4 * kSub + i] =
-                    real ? ((ListFmt<LE>::rel || ListFmt<LE>::tile) ? (nj[f] | (npl[f] << 28)) : nj[f]) : -1;
+                    real ? (ListFmt<LE>::rel ? (nj[f] | (npl[f] << 28)) : nj[f]) : -1;
                 continue;
             }
             my_cand[2 * i] = make_float4(-2.f * px, -2.f * py, -2.f * pz, fmaf(pz, pz, fmaf(py, py, px * px)));
@@ -2189,17 +2083,6 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
             constexpr int E = 8 / (int)sizeof(LE);
             constexpr int EB = 8 * (int)sizeof(LE);  // bits per entry
             unsigned long long* const lw = reinterpret_cast<unsigned long long*>(a.list);
-            // ListTile16: the lane's window part -> its rows of s_tile (-1: a part past kWinParts, which has no
-            // staged rows: the lane's list is marked overflowed, the step searches it exactly)
-            int tpart = -1;
-            if constexpr (ListFmt<LE>::tile) {
-                const int wi = (s >> 6) != (s_begin >> 6) ? 1 : 0;
-                const unsigned long long m = (unsigned long long)(unsigned)s_tile[72 + 2 * wi] |
-                                             ((unsigned long long)(unsigned)s_tile[73 + 2 * wi] << 32);
-                const int pos = s & 63;
-                const int pp = __popcll(m & (pos == 63 ? ~0ull : ((2ull << pos) - 1ull))) - 1;
-                tpart = pp < kWinParts ? 4 * wi + pp : -1;
-            }
             for (int t = 0; t < mh; ++t) {
                 unsigned b;
                 asm("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(m));
@@ -2212,11 +2095,7 @@ __device__ inline void pair_forces_sub(const DevCtx* __restrict__ ctx, const For
                         const int kk = *lcnt;
                         unsigned code = (unsigned)e;
                         bool fits = true;
-                        if constexpr (ListFmt<LE>::tile) {
-                            const int x = tpart >= 0 ? e + s_tile[9 * tpart + (int)((unsigned)er >> 28)] : -1;
-                            fits = (unsigned)x < (1u << 16);
-                            code = (unsigned)x;
-                        } else if constexpr (ListFmt<LE>::rel) {
+                        if constexpr (ListFmt<LE>::rel) {
                             const int p = er >> 28;
                             const int u = e - (p == 0 ? plb->x : (p == 1 ? plb->y : plb->z));
                             fits = (unsigned)u < (1u << kRelBits);
@@ -3123,16 +3002,10 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
     __shared__ int s_rowV[kListWaves][4 * 17];
     __shared__ int s_rowJ[kListWaves][4 * 16];
     __shared__ float4 s_cand[kListWaves][GCS_LBUILD_GROUPS * 2 * (32 + 1)];
-    __shared__ int s_ovf[kListWaves][80];  // (ListTile16: the window tables of pair_forces_sub until the tile's end)
+    __shared__ int s_ovf[kListWaves][64];
     const int lane = threadIdx.x & 63;
     const int wave = uniform((int)(threadIdx.x >> 6));
     const int ntiles = ctx->ntiles;
-    if constexpr (ListFmt<LE>::tile) {
-        // windows past the binned slots (a decomposed domain's build) stage nothing
-        const int w0 = (a.cstart[ctx->grid.ncell] + kTile - 1) / kTile, wn = (a.n + kTile - 1) / kTile;
-        for (int w = w0 + (int)blockIdx.x; w < wn; w += gridDim.x)
-            if (threadIdx.x < 37) a.ltile[(size_t)w * kListTileWords + (threadIdx.x < 36 ? threadIdx.x : 72)] = 0;
-    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // read by the list steps that follow (next launches); every block here reads ctx->grid only
         ctx->lgrid = ctx->grid;
@@ -3164,7 +3037,7 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
         int4 lb = make_int4(0, 0, 0, 0);
         pair_forces_sub<kModeList, GCS_LBUILD_GROUPS, LE>(ctx, a, lane, s, s_begin, s_end, pi, bi, fx, fy, fz, acc, s_rowV[wave],
                                       s_rowJ[wave], s_cand[wave], nullptr, ntot, wave, kListWaves, self, valid, &cnt,
-                                      &pend, &lb, s_ovf[wave]);  // (ListTile16 tables: s_ovf's row, free until the tile's end)
+                                      &pend, &lb);
         if (ListFmt<LE>::rel && valid && wave == 0) a.lbase[s] = lb;
         {  // the last, partial word of the lane's segment (its r entries sit in the top r slots: shift them down)
             constexpr int E = 8 / (int)sizeof(LE);
@@ -3231,17 +3104,26 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 // per SIMD either spills (3.74e9 / 1.15e9)
 #define GCS_LIST_UNROLL64 4
 #endif
-// One list step.  A workgroup takes ONE tile (W waves): ListTile16 the build's tile (<= 64 consecutive slots of one
-// cell row) from its table entry, the slot formats 64 consecutive slots.  Phases, with nothing but LDS carried from
-// one to the next (every wave's registers are free for the next phase):
+#ifndef GCS_LIST_PREFILTER
+// the fp64 step's fp32 prefilter (1) or every list entry's fp64 record gathered and tested (0)
+#define GCS_LIST_PREFILTER 1
+#endif
+#ifndef GCS_LIST_PF_BATCH
+#define GCS_LIST_PF_BATCH 8  // fp64 step, prefilter: list entries per fp32 batch
+#endif
+#ifndef GCS_LIST_PF_HITS
+#define GCS_LIST_PF_HITS 2  // fp64 step, prefilter: hits whose fp64 records are gathered per round
+#endif
+constexpr int kPfRing = 16;  // per lane: queued prefilter hits (a power of two >= GCS_LIST_PF_BATCH + GCS_LIST_PF_HITS)
+static_assert(kPfRing >= GCS_LIST_PF_BATCH + GCS_LIST_PF_HITS && (kPfRing & (kPfRing - 1)) == 0, "the hit ring");
+// One list step.  A workgroup takes 64 consecutive slots (W waves).  Phases, with nothing but LDS carried from one to
+// the next (every wave's registers are free for the next phase):
 //   1. slot loads: current position (.w = particle | class << 24), build position, list count, the first kU
 //      entries of the wave's segment; the local-terms wave (W - 1) also the slot's constants and bond row.
-//      ListTile16: first the staged rows' current positions into the LDS image (LDS-DMA)
 //   2. wave W - 1: the particle-local terms (bond CSR, droplet, bending, tethers, point sources, walls) -> LDS
-//   3. every wave: its list segment, kU entries per batch (ListTile16: partners from the LDS image, the entries of
-//      the next two batches in flight; slot formats: one gather per entry, the next batch's entries in flight), the
-//      exact search for the lanes the lists may not cover; forces + neighbour counts -> LDS.  Wave 1: the Philox
-//      noise -> LDS
+//   3. every wave: its list segment, kU entries per batch (one gather per entry, the next batch's entries in flight),
+//      the exact search for the lanes the lists may not cover; forces + neighbour counts -> LDS.  Wave 1: the
+//      Philox noise -> LDS
 //   4. (barrier) wave 0: sum the waves' forces, integrate, store; the launch statistics it owns (largest
 //      displacement, fallbacks; bbox / neighbour count on flagged launches) into the group's accumulators.
 //      Waves 1.. (in parallel): the wall reactions into the accumulators
@@ -3259,57 +3141,18 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 // List words are read once per step, with the non-temporal hint (ForceArgs::list_nt) when the lists are far beyond the
 // L2s, so they do not displace the partners (same-box A/B, profiles/r04_list_format_ab.txt: C5 fp64 +3-5 %, C2 fp64
 // with 4 trajectories -16 % when applied to its 16-bit lists, which the L2 / Infinity Cache keep).
-#ifndef GCS_STAGE_BYTES
-// ListTile16: bytes of the step window's LDS image of its partner rows (1,056 fp64 / 2,112 fp32 records; the image
-// also holds the waves' force partials after the pair loop).  With the rest of the kernel's LDS (< 7 KB) a workgroup
-// stays within 40 KB: 4 per CU, so C2's 948 windows are resident at once (a second round of workgroups doubles the
-// latency-bound step: profiles/r05b_probe_f0.log)
-#define GCS_STAGE_BYTES 33792
-#endif
-#ifndef GCS_LIST_WAVES_PER_EU_TILE
-#define GCS_LIST_WAVES_PER_EU_TILE 4  // ListTile16: 4 workgroups of 4 waves per CU -> <= 128 VGPRs
-#endif
-#ifndef GCS_LIST_UNROLL_TILE
-#define GCS_LIST_UNROLL_TILE 8  // ListTile16: list entries per batch (partners read from LDS; 2 batches of words ahead)
-#endif
-#ifndef GCS_LIST_UNROLL_TILE64
-#define GCS_LIST_UNROLL_TILE64 4  // the same at fp64
-#endif
-#ifndef GCS_LIST_PREWORDS
-#define GCS_LIST_PREWORDS 8  // ListTile16: list words loaded with the slot loads (8: 32 16-bit entries per segment)
-#endif
-#ifndef GCS_LIST_PREWORDS_CT
-#define GCS_LIST_PREWORDS_CT 2  // the same in the contact step (its unrolled contact probes would spill with 8)
-#endif
 template <typename LE, int W, bool CT, bool DOM = false, typename R = float, bool RLX = false>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(ListFmt<LE>::tile ? GCS_LIST_WAVES_PER_EU_TILE : CT ? GCS_LIST_WAVES_PER_EU_CT : (sizeof(R) == 8 ? GCS_LIST_WAVES_PER_EU64 : GCS_LIST_WAVES_PER_EU)))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int flags)
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS_LIST_WAVES_PER_EU_CT : (sizeof(R) == 8 ? GCS_LIST_WAVES_PER_EU64 : GCS_LIST_WAVES_PER_EU)))) void k_lstep(DevCtx* __restrict__ ctx, ForceArgs a, int flags)
 {
     using R4 = real4<R>;
     using R2 = real2<R>;
-    constexpr bool TL = ListFmt<LE>::tile;
-    // the LDS image: fp32 whole 16-B records (1-KiB LDS-DMA pieces of 64 records); fp64 (kSplit) three arrays, 28 B
-    // per record instead of 32: {x, y} (16 B, pieces of 64), z (8 B, two 4-B lanes per record: pieces of 32) and the
-    // .w word (4 B, pieces of 64).  (An LDS-DMA lane of 12 B lands at lane x 16 B: tools/calib/glds_width.hip)
-    constexpr bool kSplit = TL && sizeof(R) == 8;
-    constexpr int kStageRec = !TL ? 1 : stage_capacity(sizeof(R) == 8 ? 64 : 32);
-    static_assert(!TL || kStageRec == (kSplit ? GCS_STAGE_BYTES / 28 / 64 * 64 : GCS_STAGE_BYTES / (int)sizeof(R4)),
-                  "the build's image capacity");
-    constexpr int kXyBytes = kSplit ? kStageRec * 16 : (int)sizeof(R4) * kStageRec;  // {x, y} / whole records
-    constexpr int kZBytes = kSplit ? kStageRec * 8 : 0;
-    constexpr int kWBytes = kSplit ? kStageRec * 4 : 0;
-    static_assert(!TL || kXyBytes % 1024 == 0, "the image is whole LDS-DMA pieces");
-    static_assert(!TL || kXyBytes + kZBytes + kWBytes <= GCS_STAGE_BYTES, "the image fits its budget");
-    static_assert(!TL || kXyBytes + kZBytes + kWBytes >= W * 4 * kTile * (int)sizeof(R), "the partials fit the image");
-    __shared__ __attribute__((aligned(16))) char s_img[TL ? kXyBytes + kZBytes + kWBytes : 16];
-    R4* const s_stage = reinterpret_cast<R4*>(s_img);  // whole records (fp32)
-    const R2* const s_xy = reinterpret_cast<const R2*>(s_img);                    // (fp64)
-    const R* const s_z = reinterpret_cast<const R*>(s_img + kXyBytes);
-    const int* const s_w = reinterpret_cast<const int*>(s_img + kXyBytes + kZBytes);
-    __shared__ R s_red[TL ? 1 : W][4][TL ? 1 : kTile];
-    // ListTile16: the force partials reuse the image once every wave's pair loop is done (a barrier apart)
-    R(*const red)[4][kTile] = reinterpret_cast<R(*)[4][kTile]>(TL ? (void*)s_img : (void*)s_red);
+    // fp64 (not the contact step): the fp32 prefilter (PF, below); its per-lane rings of hits in LDS
+    constexpr bool PF = sizeof(R) == 8 && !CT && GCS_LIST_PREFILTER;
+    using QT = typename std::conditional<sizeof(LE) == 2, unsigned short, int>::type;
+    __shared__ QT s_hq[PF ? W : 1][PF ? kPfRing : 1][kTile];
+    __shared__ R red[W][4][kTile];
     __shared__ R4 s_locf[kTile], s_noise[kTile];
-    __shared__ R2 s_tab[TL ? kTileTypes : kMaxTypes];
+    __shared__ R2 s_tab[kMaxTypes];
     __shared__ int s_last, s_final;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = uniform(tid >> 6);
@@ -3327,8 +3170,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(ListFmt<
     const R4* __restrict__ qc = St<R>::psort(a, par);  // slot order (pair partners)
     const int cap = a.list_cap;
     const size_t stride = (size_t)a.list_stride;
-    constexpr int kU = TL ? (sizeof(R) == 4 ? GCS_LIST_UNROLL_TILE : GCS_LIST_UNROLL_TILE64)
-                          : (sizeof(R) == 4 ? GCS_LIST_UNROLL : GCS_LIST_UNROLL64);
+    constexpr int kU = sizeof(R) == 4 ? GCS_LIST_UNROLL : GCS_LIST_UNROLL64;
     constexpr int kE = 8 / (int)sizeof(LE);  // entries per 8-byte list word
     constexpr int kW = kU / kE;              // list words per batch
     static_assert(kU % kE == 0, "a batch is whole list words");
@@ -3344,18 +3186,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(ListFmt<
     };
     const uint2* __restrict__ segw = reinterpret_cast<const uint2*>(a.list) + (size_t)wave * (cap / kE) * stride + sl;
 
-    // 1. slot loads (one round trip; ListTile16: the window's table first, then the staged rows' current positions
-    // into the LDS image, LDS-DMA in 1-KiB pieces of consecutive records: a second round trip, under the first)
-    int tw0 = 0, tw1 = 0, T = 0, nst = 0;
-    constexpr int kGW = TL ? (kStageRec / 64 + W - 1) / W : 1;  // image groups of 64 records per wave
-    int gsl[kGW];
-    if constexpr (TL) {
-        tw0 = a.ltile[(size_t)tile * kListTileWords + lane];
-        tw1 = lane < 9 ? a.ltile[(size_t)tile * kListTileWords + 64 + lane] : 0;
-        const int* __restrict__ lst = a.lstage + (size_t)tile * kStageRec;
-#pragma unroll
-        for (int t = 0; t < kGW; ++t) gsl[t] = lst[min((wave + t * W) * 64 + lane, kStageRec - 1)];
-    }
+    // 1. slot loads (one round trip)
     const R2* __restrict__ tab = St<R>::type_ab(a);
     for (int t = tid; t < a.ntypes; t += blockDim.x) s_tab[t] = tab[t];
     const R4 pi = qc[sl];
@@ -3363,45 +3194,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(ListFmt<
     const int cw = a.lcount[(size_t)wave * stride + sl];
     int4 lb = make_int4(0, 0, 0, 0);
     if constexpr (ListFmt<LE>::rel) lb = a.lbase[sl];
-    uint2 e[kW], e1[kW];
-    // ListTile16: the segment's first kPreW words (kPreW * kE entries: a C2 segment whole) in this round trip, so
-    // the pair loop then runs from registers and LDS alone
-    constexpr int kPreW = TL ? (CT ? GCS_LIST_PREWORDS_CT : GCS_LIST_PREWORDS) : 1;
-    uint2 ew[kPreW];
-    if constexpr (!TL) {
+    uint2 e[kW];
 #pragma unroll
-        for (int j = 0; j < kW; ++j) e[j] = word(segw + (size_t)j * stride);  // list_cap >= kU: in bounds
-    }
-    if constexpr (TL) {
-        const int nw = cap / kE;  // the segment's words
-#pragma unroll
-        for (int j = 0; j < kPreW; ++j) ew[j] = word(segw + (size_t)min(j, nw - 1) * stride);
-        T = __builtin_amdgcn_readlane(tw1, 8);
-        nst = min(T, kStageRec);
-        typedef __attribute__((address_space(3))) void* lds_t;
-        // groups of 64 records: lane l's record 64 g + l, its slot from the build's list of the image's sources
-        // (loaded with the slot loads above); fp64: {x, y} and .w by lane, z by two 4-B lanes per record (the slots
-        // of records 64 g + l / 2 and 64 g + 32 + l / 2 by lane-indexed reads); fp32 the whole record
-        const int ng = (nst + 63) / 64;
-#pragma unroll
-        for (int t = 0; t < kGW; ++t) {
-            const int gg = wave + t * W;
-            if (gg >= ng) break;
-            const char* rec = reinterpret_cast<const char*>(qc + gsl[t]);
-            if constexpr (kSplit) {
-                const int sz0 = __shfl(gsl[t], lane >> 1), sz1 = __shfl(gsl[t], 32 + (lane >> 1));
-                __builtin_amdgcn_global_load_lds((const void*)rec, (lds_t)(s_img + gg * 1024), 16, 0, 0);
-                __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const char*>(qc + sz0) + 16 + 4 * (lane & 1)),
-                                                 (lds_t)(s_img + kXyBytes + gg * 512), 4, 0, 0);
-                __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const char*>(qc + sz1) + 16 + 4 * (lane & 1)),
-                                                 (lds_t)(s_img + kXyBytes + gg * 512 + 256), 4, 0, 0);
-                __builtin_amdgcn_global_load_lds((const void*)(rec + 24), (lds_t)(s_img + kXyBytes + kZBytes + gg * 256), 4,
-                                                 0, 0);
-            } else {
-                __builtin_amdgcn_global_load_lds((const void*)rec, (lds_t)(s_stage + gg * 64), 16, 0, 0);
-            }
-        }
-    }
+    for (int j = 0; j < kW; ++j) e[j] = word(segw + (size_t)j * stride);  // list_cap >= kU: in bounds
     const R cs = (R)ctx->cs;
     const float D = ctx->ldisp;
     const float lrc_b = ctx->lrc_b;
@@ -3480,72 +3275,67 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(ListFmt<
     if (a.has_pair) {
         const int cnt = (act && !fb) ? min(cw & kListCountMask, cap) : 0;
         const int kmax = uniform(wave_max_int(cnt));
-        if constexpr (TL) {
-            // partners from the LDS image (an entry past the image: gathered through the row table); the entry
-            // words of the next two batches in flight
-            auto walk = [&](auto spill) {
-                constexpr bool SP = decltype(spill)::value;
-                // one batch of kU entries held as kW words
-                auto batch = [&](const uint2* eb, int k0) {
-                    R4 q[kU];
+        if constexpr (PF) {
+        // fp64: a software pipeline of two gathers per round, issued together (one round trip): the fp32 roundings
+        // (fsort, 16 B) of the next kUF entries, and the fp64 records (32 B) of the kUD oldest hits of the lane's
+        // prefilter queue; then the exact pairs of those hits in R (list_pair) and the fp32 test of the batch, whose
+        // hits join the queue.  A pair within rc in R always passes the test (the margin: k_pstep's), and an entry
+        // that fails it contributes exactly 0 in list_pair, so the forces, the neighbour counts and their order (list
+        // order) are those of gathering every entry in R: bitwise the same.  At the 350 per-mille skin ~41 % of the
+        // entries lie within the cutoff: the fp64 gathers and pair arithmetic of the rest are skipped, and the fp32
+        // batches hold half the registers of fp64 ones per entry in flight
+        constexpr int kUF = GCS_LIST_PF_BATCH, kUD = GCS_LIST_PF_HITS;
+        constexpr int kWF = kUF / kE;
+        static_assert(kUF % kE == 0 && kUF % kU == 0, "a prefilter batch is whole list words and list batches");
+        const float4* __restrict__ fq = St<R>::fsort(a, par);
+        const float pxf = (float)pi.x, pyf = (float)pi.y, pzf = (float)pi.z;
+        const float mag = fmaxf(fabsf(pxf), fmaxf(fabsf(pyf), fabsf(pzf)));
+        const float thr = (float)rc2 * 1.001f + 1.0e-4f * rcf + 1.0e-6f * rcf * (mag + rcf);
+        const int klastF = (cap / kUF - 1) * kUF;  // the segment's last prefilter batch (list_cap: whole batches of 8)
+        QT* const hq = &s_hq[wave][0][lane];
+        uint2 ef[kWF];
 #pragma unroll
-                    for (int u = 0; u < kU; ++u) {
-                        const int x = (k0 + u < cnt) ? list_entry<LE>(eb, u) : 0;
-                        auto img = [&](int v) -> R4 {
-                            if constexpr (kSplit) {
-                                const R2 xy = s_xy[v];
-                                return mk4<R>(xy.x, xy.y, s_z[v], wpack<R>(s_w[v]));
-                            } else
-                                return s_stage[v];
-                        };
-                        if constexpr (SP) {
-                            const int xs = stage_slot_w(x, tw0, tw1);  // (every lane: lane-indexed reads)
-                            q[u] = x < nst ? img(x) : qc[xs];
-                        } else
-                            q[u] = img(x);
-                    }
+        for (int j = 0; j < kWF; ++j) ef[j] = j < kW ? e[j] : word(segw + (size_t)j * stride);
+        int qh = 0, qt = 0;  // this lane's hits consumed / queued
+        for (int k0 = 0;;) {
+            const int take = min(qt - qh, kUD);
+            if (k0 >= kmax && !__any(qt > qh)) break;
+            R4 d[kUD];
 #pragma unroll
-                    for (int u = 0; u < kU; ++u)
-                        list_pair<R>(pi.x, pi.y, pi.z, q[u], s_tab[(unsigned)wbits(q[u].w) >> kListIndexBits], ahi, bhi,
-                                     kA, kB, k2a, k2b, rc2, k0 + u < cnt, fx, fy, fz, nbr);
-                    if constexpr (CT) {
+            for (int u = 0; u < kUD; ++u)
+                d[u] = qc[u < take ? list_slot<LE>((int)hq[((qh + u) & (kPfRing - 1)) * kTile], lb) : sl];
+            const bool pre = k0 < kmax && uniform(wave_max_int(qt - qh - take)) + kUF <= kPfRing;
+            float4 f[kUF];
+            uint2 ec[kWF];  // this batch's entry words (ef then takes the next batch's)
+            if (pre) {
 #pragma unroll
-                        for (int u = 0; u < kU; ++u)
-                            if (!fbc && k0 + u < cnt) list_contact<R>(a, cd2, pi, q[u], i, wbits(q[u].w) & kIdx);
-                    }
-                };
-                // the preloaded words
+                for (int j = 0; j < kWF; ++j) ec[j] = ef[j];
 #pragma unroll
-                for (int b = 0; b < kPreW / kW; ++b) {
-                    if (b * kU >= kmax) break;
-                    batch(ew + b * kW, b * kU);
-                }
-                // the rest (long segments), the entry words of the next two batches in flight
-                constexpr int kPre = (kPreW / kW) * kU;
-                if (kmax > kPre) {
+                for (int u = 0; u < kUF; ++u)
+                    f[u] = fq[(k0 + u < cnt) ? list_slot<LE>(list_entry<LE>(ec, u), lb) : sl];
+                const int kn = min(k0 + kUF, klastF);
 #pragma unroll
-                    for (int j = 0; j < kW; ++j) {
-                        e[j] = word(segw + (size_t)(min(kPre, klast) / kE + j) * stride);
-                        e1[j] = word(segw + (size_t)(min(kPre + kU, klast) / kE + j) * stride);
-                    }
-                    for (int k0 = kPre; k0 < kmax; k0 += kU) {
-                        uint2 e2[kW];
-                        const int kn = min(k0 + 2 * kU, klast);
+                for (int j = 0; j < kWF; ++j) ef[j] = word(segw + (size_t)(kn / kE + j) * stride);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // every gather of the round in flight before the arithmetic
 #pragma unroll
-                        for (int j = 0; j < kW; ++j) e2[j] = word(segw + (size_t)(kn / kE + j) * stride);
-                        batch(e, k0);
+            for (int u = 0; u < kUD; ++u)
+                list_pair<R>(pi.x, pi.y, pi.z, d[u], s_tab[(unsigned)wbits(d[u].w) >> kListIndexBits], ahi, bhi, kA,
+                             kB, k2a, k2b, rc2, u < take, fx, fy, fz, nbr);
+            qh += take;
+            if (pre) {
 #pragma unroll
-                        for (int j = 0; j < kW; ++j) {
-                            e[j] = e1[j];
-                            e1[j] = e2[j];
-                        }
+                for (int u = 0; u < kUF; ++u) {
+                    const float dx = f[u].x - pxf, dy = f[u].y - pyf, dz = f[u].z - pzf;
+                    const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                    if (k0 + u < cnt && r2 < thr) {
+                        hq[(qt & (kPfRing - 1)) * kTile] = (QT)list_entry<LE>(ec, u);
+                        ++qt;
                     }
                 }
-            };
-            if (T <= kStageRec)
-                walk(std::false_type{});
-            else
-                walk(std::true_type{});
+                k0 += kUF;
+            }
+        }
         } else {
         // batches of kU entries: the partners' gathers are issued first, then the next batch's entry words (they
         // return right behind the gathers, so each batch costs one round trip), then the pair forces (and contacts)
@@ -3648,7 +3438,6 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(ListFmt<
         noise3<R>(a, ctx, i, n0, n1, n2);
         s_noise[lane] = mk4<R>(n0, n1, n2, R(0));
     }
-    if constexpr (TL) __syncthreads();  // every wave is done with the image: the partials may take its place
     red[wave][0][lane] = fx;
     red[wave][1][lane] = fy;
     red[wave][2][lane] = fz;
@@ -3869,7 +3658,7 @@ __global__ __launch_bounds__(kLUpdateBlock) void k_lupdate(DevCtx* __restrict__ 
     const R nzp = pi.z + mdt * f.z + amp * n2;
     if (valid) {
         St<R>::pos(a, par ^ 1)[i] = mk4<R>(nxp, nyp, nzp, R(0));
-        St<R>::psort(a, par ^ 1)[s] = mk4<R>(nxp, nyp, nzp, pi.w);
+        put_slot<R>(a, par ^ 1, s, mk4<R>(nxp, nyp, nzp, pi.w));
     }
     // the list bookkeeping in fp32 (as k_lstep's): displacement from the build, bbox of the roundings
     const float fnx = (float)nxp, fny = (float)nyp, fnz = (float)nzp;
@@ -3925,26 +3714,33 @@ __global__ __launch_bounds__(kLUpdateBlock) void k_lupdate(DevCtx* __restrict__ 
 // The persistent small-system step (the mitotic stages: 586 / 1,172 particles; any system of <= kPMax particles).
 // At these sizes a step of the list step is ~10-19 workgroups and its cost is latency: a launch, a chain of dependent
 // round trips, a cross-workgroup tail (~16 us per step).  Here ONE cooperative launch runs a chunk
-// of steps with one workgroup per 64 particles (all resident, each on a CU of its own), and every workgroup holds the
-// WHOLE system's positions in LDS:
-//   * pairs: all N candidates per particle, a fp32 prefilter on the LDS image with a margin (every pair within the
-//     cutoff in R passes), then the exact pair in R (list_pair, the list step's arithmetic: the same pair set).  No
+// of steps with one workgroup per kPP = 16 particles (4 waves; a wave's 64 lanes are 16 particles x 4 candidate
+// segments; all workgroups resident, one per CU by their LDS), and every workgroup holds the WHOLE system's
+// positions in LDS:
+//   * pairs: all N candidates per particle, a fp32 prefilter on the LDS image (r^2 against rc^2 with a margin that
+//     grows with the coordinates' magnitude: every pair within the cutoff in R passes), the hits listed per lane in
+//     LDS, then the exact pair in R over the list (list_pair, the list step's arithmetic: the same pair set).  No
 //     cell list, no neighbour lists, no rebuilds, no skin: exact at every step by construction;
-//   * particle-local terms on the LDS image (local_terms with the image as its positions);
-//   * one grid barrier per step: each workgroup stores its particles' new positions write-through (sc1), drains,
-//     and ONE lane adds to a counter; the workgroups poll it (sc1 loads), then load the new positions with sc1
-//     loads into LDS (MI355X_MICROARCH.md "inter-workgroup visibility", the counter row of the valid forms: sc1
-//     stores and loads, one workgroup per CU);
+//   * particle-local terms on the LDS image (local_terms with the image as its positions), on the last wave;
+//   * the hand-off, no grid barrier: wave 0 stores each particle's new position as tagged 8-byte granules {data
+//     word, tag = step + 1} (16-B sc1 stores, two halves by step parity) together with the workgroup's partial totals
+//     (6 wall reactions, the neighbour count); every workgroup loads every granule with sc1 loads and re-polls those
+//     whose tag is not yet the step's (MI355X_MICROARCH.md, the tagged-granule hand-off: no fence, no counter).  A
+//     half is rewritten two steps later, only after every workgroup has read it;
 //   * the tail (reactions -> wall ODE, schedule, step / parity / noise cursor) computed REDUNDANTLY by every
-//     workgroup from the step's accumulator set (fixed-point integer sums: order-free, so every copy is the same)
-//     on its own LDS copy of the context; workgroup 0 writes the context back at the end.  Accumulator sets rotate
-//     over three (step k accumulates into set k % 3, workgroup 0 clears set (k + 1) % 3 during step k: every
-//     workgroup read it after barrier k - 2, before arriving at barrier k - 1).
-// The force on a particle sums its partners in index order (wave w takes candidates [w N / 4, (w + 1) N / 4)):
+//     workgroup from the totals summed in a fixed workgroup order (every copy the same bits) on its own LDS copy of
+//     the context; workgroup 0 writes the context back at the end.
+//   * a poll that gives up (pget_image) stops every workgroup and fails the run (ForceArgs::pstall, run_small).
+// The force on a particle sums its partners in index order, its lane groups' and waves' sums in a fixed order:
 // bitwise reproducible, and independent of how a run is chunked.  The sum order differs from the list step's, so
 // the two agree to rounding (tests: both within the oracle's bound).
 #ifndef GCS_PSTEP_SPIN
-#define GCS_PSTEP_SPIN (1 << 22)  // grid-barrier polls before a workgroup gives up (DevCtx::scan_stall; the host fails)
+#define GCS_PSTEP_SPIN (1 << 22)  // hand-off polls before a workgroup gives up (ForceArgs::pstall; the host fails the run)
+#endif
+#ifndef GCS_PSTEP_STALL_TICKS
+// ... or wall-clock ticks (100 MHz: 0.25 s) without the granules arriving, whichever comes first.  A step takes ~6 us
+// and every workgroup of the cooperative launch is resident, so only a lost hand-off waits that long
+#define GCS_PSTEP_STALL_TICKS 25000000ull
 #endif
 constexpr int kPWaves = 4;
 #ifndef GCS_PSTEP_PP
@@ -4008,17 +3804,18 @@ __device__ __forceinline__ double pchunk_double(const int4& v)
 
 // the image of step tag and the G workgroups' partial totals: units u < n are the records, u in [n, n + G TR) the
 // totals records (record kPMax + u - n); thread t of T walks u = ub + t, ub + t + T, ... < ue, a batch's loads issued
-// together, polls
-// until every granule carries the tag (a stall after GCS_PSTEP_SPIN polls: counted, the host fails); records into
-// s_pos and the fp32 coordinate arrays s_pfx / s_pfy / s_pfz, totals chunks (one double each) into s_tot
+// together, polls until every granule carries the tag; records into s_pos and the fp32 coordinate arrays s_pfx /
+// s_pfy / s_pfz, totals chunks (one double each) into s_tot.  A stall -- GCS_PSTEP_SPIN polls or
+// GCS_PSTEP_STALL_TICKS of wall clock without the granules, or the global stall word set by another workgroup (read
+// every 64 polls) -- sets the workgroup's stall flag (its step loop then stops) and adds 1 to the global word (the
+// other workgroups stop at their next poll; engine.hip run_small fails the run and restores the context)
 template <typename R, typename Mid>
 __device__ __forceinline__ void pget_image(char* half, int n, int G, int ub, int ue, int t, int T, unsigned tag, real4<R>* s_pos,
                                            float* s_pfx, float* s_pfy, float* s_pfz, double* s_tot,
-                                           volatile int* stall, Mid&& mid, unsigned long long* dbg = nullptr)
+                                           volatile int* stall, int* gstall, Mid&& mid, unsigned long long* dbg = nullptr)
 {
     // mid(): work of the caller's that runs while the first batch's loads are in flight
     constexpr int C = sizeof(R) == 8 ? 3 : 2, RB = sizeof(R) == 8 ? 4 : 6, RBY = kPRecBytes<R>;
-    const int nu = n + G * kPTotRecs<R>;
     const auto rp = phalf_rsrc(half, kPHalfBytes);
     auto rec = [&](int u) { return u < n ? u : kPMax + (u - n); };
     for (int u0 = ub; u0 < ue; u0 += RB * T) {
@@ -4030,6 +3827,7 @@ __device__ __forceinline__ void pget_image(char* half, int n, int G, int ub, int
             for (int c = 0; c < C; ++c) v[r][c] = u < ue ? ld_sc1_i4(rp, rec(u) * RBY + 16 * c) : int4{};
         }
         if (u0 == ub) mid();
+        unsigned long long t0 = 0ull;
         for (int spin = 0;; ++spin) {
             bool ok = true;
 #pragma unroll
@@ -4041,9 +3839,19 @@ __device__ __forceinline__ void pget_image(char* half, int n, int G, int ub, int
                 dbg[1] = spin;
             }
             if (ok) break;
-            if (*stall || spin >= GCS_PSTEP_SPIN) {
-                *stall = 1;
-                break;
+            if (*stall) break;
+            if ((spin & 63) == 0) {
+                const unsigned long long now = wall_clock64();
+                if (spin == 0) t0 = now;
+                if (__hip_atomic_load(gstall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                    *stall = 1;
+                    break;
+                }
+                if (spin >= GCS_PSTEP_SPIN || now - t0 > GCS_PSTEP_STALL_TICKS) {
+                    *stall = 1;
+                    atomicAdd(gstall, 1);
+                    break;
+                }
             }
             __builtin_amdgcn_s_sleep(1);  // (longer backoffs measured slower: 2 / 4 / 8 x 64 clocks)
 #pragma unroll
@@ -4110,7 +3918,8 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
     unsigned* const sync = a.psync;  // the hand-off halves
     if (tid == 0) {
         s_pad[0] = 0;
-        s_stall = 0;
+        // an earlier launch of the run stalled: do nothing (the host restores the context of that launch's start)
+        s_stall = __hip_atomic_load(a.pstall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ? 1 : 0;
     }
     const FieldPrm<R>& P = St<R>::prm(a);
     const R4* __restrict__ kmu = St<R>::kmu(a);
@@ -4168,6 +3977,7 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
 
     for (int k = 0; k < steps; ++k) {
         __syncthreads();  // s_pos / s_pf* of this step, s_ctx
+        if (s_stall) break;  // a hand-off stalled (this workgroup or another): stop integrating
         const unsigned tag = (unsigned)k + 1u;  // step k's hand-off: half k & 1, tag k + 1
         char* const half = reinterpret_cast<char*>(sync) + (k & 1) * kPHalfBytes;
         // debug stamps (GCS_DEBUG_PSTEP): workgroup 0's phases of the first 64 steps ([16 k ...]), every workgroup's
@@ -4224,8 +4034,11 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
         R fx = 0, fy = 0, fz = 0, nbr = 0;
         if (a.has_pair) {
             const float pxf = (float)pi.x, pyf = (float)pi.y, pzf = (float)pi.z;
-            // margin: the fp32 roundings of the coordinates (|x| < ~400) move r^2 by far less than this
-            const float thr = (float)rc2 * 1.001f + 1.0e-4f * (float)rc;
+            // margin against the fp32 roundings: a coordinate's rounding is <= 2^-24 |x|, so for a pair within rc
+            // (|x_j| <= |x_i| + rc) r^2 moves by <= ~4.2e-7 rc (mag + rc), mag = the particle's largest |coordinate|;
+            // the margin keeps 2x that on top of 0.1 % of rc^2 (the fixed margin held to |x| ~ 400 only)
+            const float mag = fmaxf(fabsf(pxf), fmaxf(fabsf(pyf), fabsf(pzf)));
+            const float thr = (float)rc2 * 1.001f + 1.0e-4f * (float)rc + 1.0e-6f * (float)rc * (mag + (float)rc);
             typedef float f2 __attribute__((ext_vector_type(2)));
             const f2 PX = {pxf, pxf}, PY = {pyf, pyf}, PZ = {pzf, pzf};
             unsigned short* const hl = &s_hit[wave][0][0];
@@ -4317,7 +4130,8 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
             // the workgroup's totals out first (wave 0 of every workgroup waits on them before its tail), then the
             // records
             const R nt = wave_sum_r(lead ? ns : R(0));
-            if (lane < kPTotChunks<R>)  // reactions, neighbours (the unused chunks tagged too: all are polled)
+            const bool pub = a.pstep_skip < 0 || a.pstep_skip != (int)((blockIdx.x << 16) | (unsigned)k);  // (tests)
+            if (pub && lane < kPTotChunks<R>)  // reactions, neighbours (the unused chunks tagged too: all are polled)
                 pput_double(half, kPTotOff<R> + blockIdx.x * kPTotBytes<R> + 16 * lane,
                             lane < 6 ? s_react[min(lane, 5)] : lane == 6 ? (double)nt : 0.0, tag);
             const R4 lf = s_locf[pl];
@@ -4331,7 +4145,7 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
             const R mdt = mu * dt;
             const R4 np = mk4<R>(pi.x + mdt * fsx + amp * xi.x, pi.y + mdt * fsy + amp * xi.y,
                                  pi.z + mdt * fsz + amp * xi.z, R(0));
-            if (lead) {
+            if (lead && pub) {
                 pput_record<R>(half, i, np, tag);
                 if (k == steps - 1) St<R>::pos(a, par ^ 1)[i] = np;  // the launch's result (the launch end orders it)
             }
@@ -4345,7 +4159,7 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
         // while its first loads are in flight
         if (wave > 0) {
             pget_image<R>(half, n, G, 0, n, tid - 64, 64 * (W - 1), tag, s_pos, s_pfx, s_pfy, s_pfz, s_tot, &s_stall,
-                          [&]() {
+                          a.pstall, [&]() {
                 if (wave == 1 && k + 1 < steps) {
                     R n0, n1, n2;
                     noise3_at<R>(a, c_step + 1, c_cursor + 1, il, n0, n1, n2);
@@ -4361,7 +4175,7 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
                 tsc = list_tail_sched(tin);
             }
             pget_image<R>(half, n, G, n, n + G * kPTotRecs<R>, lane, 64, tag, s_pos, s_pfx, s_pfy, s_pfz, s_tot,
-                          &s_stall, [] {}, dbs && tid == 0 ? dbs + 4 : nullptr);
+                          &s_stall, a.pstall, [] {}, dbs && tid == 0 ? dbs + 4 : nullptr);
             // the step's totals, in a fixed order (the same totals in every workgroup, bitwise): lane 8 c + p sums
             // quantity c over workgroups p, p + 8, ..., then the 8 lanes of c pairwise (this wave's own LDS writes)
             const int tc = lane >> 3, tp = lane & 7;
@@ -4391,14 +4205,29 @@ __global__ __launch_bounds__(64 * kPWaves) void k_pstep(DevCtx* __restrict__ ctx
         par ^= 1;
     }
     __syncthreads();
-    if (tid == 0 && s_stall) s_ctx.scan_stall += 1;
     if (a.dbg_times && tid < kPDbgSteps) {  // the stamps: workgroup 0's phases, every workgroup's hand-off
         if (blockIdx.x == 0)
             for (int c = 0; c < 16; ++c) a.dbg_times[16 * tid + c] = tid < steps ? s_dbg[tid][c] : 0ull;
         if (blockIdx.x < 128) a.dbg_times[1024 + 128 * tid + blockIdx.x] = tid < steps ? s_dbw[tid] : 0ull;
     }
     __syncthreads();
-    if (blockIdx.x == 0 && tid == 0) *ctx = s_ctx;
+    // the context of a stalled launch is not written back (the host fails the run either way)
+    if (blockIdx.x == 0 && tid == 0 && !s_stall) *ctx = s_ctx;
+}
+
+// run_small's guard around each k_pstep launch: before it (save) the context is kept unless a launch of the run has
+// stalled already; after the run (restore) a stalled run gets back the context of its failing launch's start (whose
+// position buffer that launch never writes: it writes the other parity)
+__global__ void k_pstep_guard(DevCtx* __restrict__ ctx, DevCtx* __restrict__ keep, const int* __restrict__ stall,
+                              int restore)
+{
+    constexpr int kWords = (int)(sizeof(DevCtx) / sizeof(int));
+    static_assert(sizeof(DevCtx) % sizeof(int) == 0, "DevCtx in words");
+    const bool stalled = *stall != 0;
+    int* const dst = reinterpret_cast<int*>(restore ? ctx : keep);
+    const int* const src = reinterpret_cast<const int*>(restore ? keep : ctx);
+    if (restore ? stalled : !stalled)
+        for (int w = threadIdx.x; w < kWords; w += blockDim.x) dst[w] = src[w];
 }
 
 // The decomposed list step's tail (one workgroup, after the allreduce of every domain's k_lstep<..., DOM> reduction):
@@ -4459,8 +4288,8 @@ __device__ __forceinline__ void ldom_tail_body(DevCtx* __restrict__ ctx, const F
         const int sl = a.islot[i];
         if (sl >= 0) {
             const real4<R> q = mk4<R>(x, y, z, wpack<R>((i & kIdx) | (a.ptype[i] << kListIndexBits)));
-            St<R>::psort(a, 0)[sl] = q;
-            St<R>::psort(a, 1)[sl] = q;
+            put_slot<R>(a, 0, sl, q);
+            put_slot<R>(a, 1, sl, q);
         }
     }
     if (bands)
@@ -4802,16 +4631,18 @@ void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, cons
                       int2* sbrow, const int* boff, int* islot)
 {
     hipLaunchKernelGGL(k_cell_sort<float>, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, kmu, n, tmp,
-                       cell_of, cstart, sidx, scell, spos, sb, pair_mix, ptype, psort0, psort1, skmu, sbrow, boff, islot);
+                       cell_of, cstart, sidx, scell, spos, sb, pair_mix, ptype, psort0, psort1, skmu, sbrow, boff, islot,
+                       (float4*)nullptr, (float4*)nullptr);
 }
 
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const double4* pos0, const double4* pos1, const double4* kmu,
                       int n, const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell, float4* spos,
                       float* sb, int pair_mix, const int* ptype, double4* psort0, double4* psort1, double4* skmu,
-                      int2* sbrow, const int* boff, int* islot)
+                      int2* sbrow, const int* boff, int* islot, float4* fsort0, float4* fsort1)
 {
     hipLaunchKernelGGL(k_cell_sort<double>, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, kmu, n, tmp,
-                       cell_of, cstart, sidx, scell, spos, sb, pair_mix, ptype, psort0, psort1, skmu, sbrow, boff, islot);
+                       cell_of, cstart, sidx, scell, spos, sb, pair_mix, ptype, psort0, psort1, skmu, sbrow, boff, islot,
+                       fsort0, fsort1);
 }
 
 template <int MODE, bool FUSED>
@@ -4847,16 +4678,14 @@ void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceAr
     }
 }
 
-// the list step's launch: one workgroup per 64 consecutive slots (ListTile16: per window of the table)
+// the list step's launch: one workgroup per 64 consecutive slots
 int list_step_grid(const ForceArgs& a) { return force_blocks(a.n); }
 
 // the entry type of the launch's list format (ForceArgs::list_fmt), handed to fn as a value of that type
 template <typename Fn>
 static void with_list_entry(const ForceArgs& a, Fn&& fn)
 {
-    if (a.list_fmt == kListFmtTile16)
-        fn(ListTile16{});
-    else if (a.list_fmt == kListFmtAbs16)
+    if (a.list_fmt == kListFmtAbs16)
         fn((unsigned short)0);
     else if (a.list_fmt == kListFmtRel16)
         fn(ListRel16{});
@@ -4916,6 +4745,11 @@ static void launch_list_relax_r(hipStream_t s, DevCtx* ctx, const ForceArgs& a, 
 void launch_dom_grid(hipStream_t s, DevCtx* ctx, const ForceArgs& a)
 {
     hipLaunchKernelGGL(k_dom_grid, dim3(1), dim3(1), 0, s, ctx, a);
+}
+
+void launch_pstep_guard(hipStream_t s, DevCtx* ctx, DevCtx* keep, const int* stall, int restore)
+{
+    hipLaunchKernelGGL(k_pstep_guard, dim3(1), dim3(64), 0, s, ctx, keep, stall, restore);
 }
 
 int launch_pstep(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int steps, int flags)

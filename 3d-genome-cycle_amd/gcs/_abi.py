@@ -44,7 +44,7 @@ OPT_LIST_CAP = 12
 OPT_LIST_WAVES = 13
 OPT_DENSE_NEIGHBORS = 15
 OPT_LIST_DEAL = 16
-OPT_LIST_FORMAT = 17  # 0 default (16-bit slots, plane-relative beyond 65,536), 1 plane-relative, 2 32-bit, 3 tile-staged
+OPT_LIST_FORMAT = 17  # 0 default (16-bit slots, plane-relative beyond 65,536), 1 plane-relative, 2 32-bit
 OPT_SMALL_STEP = 18  # 1 default: the persistent all-pairs step for <= 2,048 particles; 0 off
 
 

@@ -69,7 +69,8 @@ extern "C" {
  * 3: gcs_system_desc.reserved became .precision (0 = fp64); gcs_run_stats lost the small-path counters and
  *    gained density_probes; gcs_list_stats gained deal; GCS_OPT_SMALL_PATH and GCS_OPT_FUSED_STEP 1 are gone;
  *    later in 3 (additive, no layout change): GCS_OPT_LIST_FORMAT; the default list skin follows the core scale;
- *    GCS_OPT_LIST_FORMAT 3, GCS_OPT_SMALL_STEP */
+ *    GCS_OPT_SMALL_STEP; GCS_ESTATE also reports a stalled cross-workgroup hand-off (round 6: GCS_OPT_LIST_FORMAT 3,
+ *    an experiment, was removed) */
 #define GCS_ABI_VERSION 3
 
 /* arithmetic precision of an engine (gcs_system_desc.precision) */
@@ -389,11 +390,8 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
                                      the particle-local terms); the pair set and the results do not */
 #define GCS_OPT_LIST_FORMAT 17    /* list entries: 0 (default) 16-bit absolute slots up to 65,536 particles, the relative
                                      form beyond; 1 16-bit slots relative to the particle's cell planes (an entry out of
-                                     their range sends the particle to the exact search); 2 32-bit absolute slots; 3
-                                     16-bit indices into the step workgroup's LDS image of its partner rows (the partners
-                                     read from LDS; undecomposed runs with <= 64 pair classes, else the default).  Every
-                                     form holds the same pairs in the same order: the results do not change, but for the
-                                     rare particle the tile-staged form searches exactly */
+                                     their range sends the particle to the exact search); 2 32-bit absolute slots.  Every
+                                     form holds the same pairs in the same order: the results do not change */
 #define GCS_OPT_SMALL_STEP 18     /* systems of <= 1,536 particles (the mitotic stages): 1 (default) one cooperative launch
                                      per chunk of steps, every workgroup holding the whole system in LDS (all pairs; the
                                      new positions handed between workgroups as tagged granules every step), unless

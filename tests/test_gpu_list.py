@@ -554,12 +554,11 @@ def _format_run(design, cfg, prec, fmt, steps, ctx=LATE, seed=11, **opts):
 
 
 @precisions
-@pytest.mark.parametrize("fmt", [1, 2, 3])
+@pytest.mark.parametrize("fmt", [1, 2])
 def test_list_formats_bitwise_c1(c1_design, prec, fmt):
-    """GCS_OPT_LIST_FORMAT: plane-relative 16-bit slots (1, kernels.hip ListRel16), 32-bit slots (2) and the
-    tile-staged entries (3, ListTile16: indices into the step tile's LDS image) hold the same pairs in the same order
-    as the default absolute 16-bit slots (0): the trajectory (list rebuilds included) is bitwise the same, with the
-    same particles searched exactly"""
+    """GCS_OPT_LIST_FORMAT: plane-relative 16-bit slots (1, kernels.hip ListRel16) and 32-bit slots (2) hold the same
+    pairs in the same order as the default absolute 16-bit slots (0): the trajectory (list rebuilds included) is
+    bitwise the same, with the same particles searched exactly"""
     cfg = InterphaseConfig()
     x0, s0 = _format_run(c1_design, cfg, prec, 0, 60)
     x1, s1 = _format_run(c1_design, cfg, prec, fmt, 60)
@@ -572,8 +571,7 @@ def test_list_formats_bitwise_c1(c1_design, prec, fmt):
 def test_relative_entries_c5_bitwise(prec):
     """N > 65,536 (C5, 606,248 particles, its dense synthetic start): the plane-relative 16-bit slots (the default
     there) against 32-bit slots -- every partner within the plane span (no escape to the exact search), so bitwise
-    the same; the tile-staged entries (format 3: many windows' partner rows exceed the LDS image there, those entries
-    are gathered through the window table) within the precision's bound of them"""
+    the same"""
     cfg = resolution_scaled(InterphaseConfig(), 10.0)
     design = synthetic.make_c5()
     ctx = {"step": 0, "time": 0.0, "core_scale": 1.0, "bond_scale": 1.0, "wall_semiaxes": LATE["wall_semiaxes"]}
@@ -581,12 +579,6 @@ def test_relative_entries_c5_bitwise(prec):
     x1, s1 = _format_run(design, cfg, prec, 1, 20, ctx=ctx)
     assert s1["fallback_particle_steps"] == s2["fallback_particle_steps"], (s1, s2)
     assert np.array_equal(x1, x2)
-    # the tile-staged entries: the same pairs, except that the rare particle in a 5th+ cell-row part of its
-    # 64-slot window (kernels.hip kWinParts) is searched exactly (its sum in another order): within the bound
-    x0, s0 = _format_run(design, cfg, prec, 3, 20, ctx=ctx)
-    extra = s0["fallback_particle_steps"] - s2["fallback_particle_steps"]
-    assert 0 <= extra < 1e-4 * design.n * 20, (s0, s2)
-    assert np.abs(x0 - x2).max() <= TOL_X[prec]
 
 
 @precisions
@@ -614,33 +606,6 @@ def test_relative_entries_escape_to_exact_search(prec):
     st = sysd["e"].list_stats()
     assert st["active"] == 1 and st["fallback_particle_steps"] > 0, st
     assert np.abs(sysd["e"].get_positions() - sysd["o"].get_positions()).max() <= TOL_X[prec]
-
-
-@precisions
-def test_tile_entries_beyond_the_lds_image(prec):
-    """The tile-staged entries (format 3, ListTile16) on a dense rod (100,000 particles, 4 x 0.13 x 0.13, ~400-560
-    list entries each) whose tiles' partner rows exceed the LDS image (GCS_STAGE_BYTES) in ~98 % of the tiles at
-    either precision (tools estimate: staged rows ~1,900 fp64 / ~3,000 fp32 records per tile against 1,248 / 2,496):
-    the entries past the image are gathered through the tile's row table.  The same particles searched exactly as
-    with 32-bit slots, bitwise the same trajectory, and the same bound vs the oracle"""
-    n = 100000
-    rng = np.random.default_rng(7)
-    x = np.column_stack([rng.uniform(0, 4, n), rng.uniform(0, 0.13, n), rng.uniform(0, 0.13, n)])
-    runs = {}
-    for name, cls, fmt in (("t", Engine, 3), ("i", Engine, 2), ("o", oracle.OracleSystem, None)):
-        s = cls(n, precision=prec)
-        s.add_neighbor_softcore(2.5, 0.03, 2.5, 0.024, 0.03, mix=False, scaled=False)
-        s.set_positions(x)
-        if fmt is not None:
-            s.set_option(A.OPT_FUSED_STEP, 3)
-            s.set_option(A.OPT_DENSE_NEIGHBORS, 0)
-            s.set_option(A.OPT_LIST_FORMAT, fmt)
-        s.run(5, seed=3, timestep=1e-7)
-        runs[name] = s
-    st = runs["t"].list_stats()
-    assert st["active"] == 1 and st["fallback_particle_steps"] == runs["i"].list_stats()["fallback_particle_steps"], st
-    assert np.array_equal(runs["t"].get_positions(), runs["i"].get_positions())
-    assert np.abs(runs["t"].get_positions() - runs["o"].get_positions()).max() <= TOL_X[prec]
 
 
 @precisions
@@ -706,18 +671,3 @@ def test_many_pair_classes_take_the_cell_list_step(prec):
         s.run(25, seed=9, timestep=1e-5, temperature=1.0)
     assert e.list_stats()["active"] == 0
     assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[prec]
-
-
-@precisions
-def test_pair_classes_beyond_the_tile_table(prec):
-    """65-256 pair classes (100 here): format 3 (the tile-staged entries, whose LDS class table holds 64) falls back
-    to the 16-bit slot entries: bitwise the default, and within the bound of the oracle"""
-    n = 1500
-    runs = [_classes_system(Engine, n, 100, prec, fused_step=3, dense_neighbors=0, list_format=f) for f in (0, 3)]
-    o = _classes_system(oracle.OracleSystem, n, 100, prec)
-    for s in runs + [o]:
-        s.run(25, seed=9, timestep=1e-5, temperature=1.0)
-    st = runs[0].list_stats()
-    assert st["active"] == 1 and st["pair_classes"] == 100
-    assert np.array_equal(runs[0].get_positions(), runs[1].get_positions())
-    assert np.abs(runs[0].get_positions() - o.get_positions()).max() <= TOL_X[prec]

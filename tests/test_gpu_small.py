@@ -1,10 +1,12 @@
-"""GPU: the persistent small-system step (kernels.hip k_pstep, GCS_OPT_SMALL_STEP: the default for <= 2,048
+"""GPU: the persistent small-system step (kernels.hip k_pstep, GCS_OPT_SMALL_STEP: the default for <= 1,536
 particles, i.e. the mitotic stages of C3 and the C1 chain): one cooperative launch per chunk of steps, every
-workgroup holding the whole system in LDS, all pairs through a fp32 prefilter and the exact pair in R, one grid
-barrier per step, the tail computed by every workgroup.  Checked at both precisions against the fp64 oracle (the
+workgroup holding the whole system in LDS, all pairs through a fp32 prefilter and the exact pair in R, a tagged
+hand-off of the new positions per step, the tail computed by every workgroup.  Checked at both precisions against the fp64 oracle (the
 precision's bound, tests/tolerances.py), against the list step (the same pair set, the sum in another order: within
 the same bound), chunk-invariant bit for bit (also across the kernel's 2,048-step launches), and the C3 stage sizes.
 The mitotic drivers' own parity tests (test_gpu_parity.py C3) run through this path too."""
+import time
+
 import numpy as np
 import pytest
 
@@ -49,7 +51,7 @@ def test_small_step_c1_vs_oracle(c1_design, interphase_cfg, prec, ctx):
     ce, co = e.get_context(), o.get_context()
     assert np.allclose(ce["wall_semiaxes"], co["wall_semiaxes"], rtol=WALL_REL[prec])
     assert ce["step"] == first + 60
-    assert e.list_stats()["sync_stalls"] == 0  # no grid-barrier timeout
+    assert e.list_stats()["sync_stalls"] == 0  # no cell-scan look-back timeout (a hand-off stall fails the run)
 
 
 @precisions
@@ -117,3 +119,54 @@ def test_small_step_anatelophase_both_paths(prec):
         xs.append(s.get_positions())
     assert np.abs(xs[0] - xs[2]).max() <= X[prec]
     assert np.abs(xs[1] - xs[2]).max() <= X[prec]
+
+
+@precisions
+def test_small_step_droplet_many_targets(prec):
+    """a droplet of 40 targets (> 16: k_pstep strides a particle's targets over its 4 lanes, whose loop
+    trip counts then differ by lane) -- the small step within the precision's bound of the oracle and of the list
+    step (GCS_OPT_SMALL_STEP 0), the droplet's attraction included (targets packed within its cutoff)"""
+    n = 400
+    rng = np.random.default_rng(12)
+    x = rng.uniform(-0.45, 0.45, (n, 3))
+    tg = np.arange(0, n, 10)
+    x[tg] = rng.uniform(-0.15, 0.15, (tg.size, 3))
+    xs = []
+    for cls, small in ((Engine, 1), (Engine, 0), (oracle.OracleSystem, None)):
+        s = cls(n, precision=prec)
+        s.add_neighbor_softcore(2.5, 0.1, neighbor_distance=0.1, mix=False, scaled=False)
+        s.add_neighbor_softwell(energy=3.0, decay_distance=0.2, cutoff=0.4, targets=tg)
+        s.set_positions(x)
+        if small is not None:
+            s.set_option(A.OPT_SMALL_STEP, small)
+        s.run(40, seed=4, timestep=1e-5, temperature=1.0)
+        xs.append(s.get_positions())
+        if small == 1:
+            assert s.run_stats()["eager_steps"] >= 40  # (the small step: one cooperative launch, no graphs)
+    assert np.abs(xs[0] - xs[2]).max() <= X[prec]
+    assert np.abs(xs[1] - xs[2]).max() <= X[prec]
+    # the droplet moved the targets more than the noise alone would at this timestep
+    assert np.abs(xs[2][tg] - x[tg]).max() > 0
+
+
+@precisions
+def test_small_step_stall_fails_the_run(c1_design, interphase_cfg, prec, monkeypatch):
+    """a workgroup that does not publish its hand-off (GCS_DEBUG_PSTEP_SKIP = workgroup 5, step
+    3 of the run's first launch) stalls every workgroup; gcs_engine_run fails with GCS_ESTATE within a second, the
+    positions and the context are those before the run, and the engine runs on afterwards"""
+    cfg = interphase_cfg
+    e, _ = _pair(c1_design, cfg, prec)
+    x0, c0 = e.get_positions(), e.get_context()
+    monkeypatch.setenv("GCS_DEBUG_PSTEP_SKIP", "5:3")
+    t0 = time.perf_counter()
+    with pytest.raises(A.GcsError) as err:
+        e.run(500, temperature=cfg.temperature, timestep=cfg.timestep, seed=8)
+    dt = time.perf_counter() - t0
+    monkeypatch.delenv("GCS_DEBUG_PSTEP_SKIP")
+    assert err.value.code == A.GCS_ESTATE and "stalled" in str(err.value), err.value
+    assert dt < 1.0, dt
+    assert np.array_equal(e.get_positions(), x0)
+    assert e.get_context() == c0
+    e.run(20, temperature=cfg.temperature, timestep=cfg.timestep, seed=8)
+    assert e.get_context()["step"] == c0["step"] + 20
+    assert not np.array_equal(e.get_positions(), x0)
