@@ -759,6 +759,7 @@ def replica_main(args):
     rank_finite = gather_over_ranks(dist, 1.0 if finite else 0.0)
     rank_sums = gather_over_ranks(dist, float(np.asarray(engines[0].get_positions(), dtype=np.float64).sum()))
     at = after + args.profile_steps
+    rank_steps = gather_over_ranks(dist, float(at))  # the step each rank's checksum was taken at
 
     contacts_ms, contacts_distinct = None, None
     start_rate = None
@@ -817,8 +818,8 @@ def replica_main(args):
         if args.cycle_scale > 0:
             cycle = cycle_leg(local, args.cycle_scale)
 
-    cpu = None
-    if world == 1 and args.cpu_budget > 0 and state is not None and args.config == "c2":
+    cpu = None  # (rank 0 at any world size: the line of an 8-GPU run carries its CPU leg too)
+    if args.cpu_budget > 0 and state is not None and args.config == "c2":
         cpu = cpu_baseline(args.cpu_budget, args.cpu_procs)
 
     value = whole_job_value(n * R, steps, world, el_max)
@@ -845,6 +846,8 @@ def replica_main(args):
         "per_rank_seeds": rank_seeds,
         "per_rank_finite": rank_finite,
         "per_rank_checksums": rank_sums,
+        "per_rank_checksum_steps": rank_steps,
+        "window_start": window,
         "config": {"workload": f"{args.config.upper()} interphase BD step, {n} particles, {R} independent "
                                f"trajectories per GPU, window from step {window} "
                                f"(core_scale {ctx['core_scale']:.4f})",
