@@ -141,6 +141,13 @@ struct gcs_engine {
     int2* bent = nullptr;
     float4* bval = nullptr;
     int* sw_idx = nullptr;  // droplet targets (<= 64)
+    int nbent = 0;          // bond CSR entries
+    int* bslot = nullptr;   // list step: the slot of each bond CSR entry's partner (ForceArgs::bslot)
+    int* swslot = nullptr;  // list step: the slot of each droplet target
+    int bslot_cap = 0;
+    int* brev = nullptr;    // per bond CSR entry: its reverse entry (the partner's entry pointing back)
+    bool brev_ok = false;
+    int* swt = nullptr;     // per particle: its droplet target index, -1 none
     float* bend_eps = nullptr;
     int* toff = nullptr;
     Tether* tent = nullptr;
@@ -522,10 +529,17 @@ int compile(gcs_engine* e)
         if (f64) hkd[t].w = 1.0;
     }
     dfree(e->sw_idx);
+    dfree(e->swt);
     if (a.sw_n > 0) {
         int rc;
         if ((rc = dalloc(&e->sw_idx, 64))) return rc;
         HIPCHK(hipMemcpyAsync(e->sw_idx, sw_idx.data(), sw_idx.size() * sizeof(int), hipMemcpyHostToDevice, e->stream));
+        // particle -> its droplet target index (-1: none): k_cell_sort files a target's slot (slot_bonds)
+        std::vector<int> swt(n, -1);
+        for (size_t t = 0; t < sw_idx.size(); ++t) swt[sw_idx[t]] = (int)t;
+        if ((rc = dalloc(&e->swt, n))) return rc;
+        HIPCHK(hipMemcpyAsync(e->swt, swt.data(), n * sizeof(int), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
     }
     a.sw_idx = e->sw_idx;
     HIPCHK(hipMemcpyAsync(e->kmu, hk.data(), n * sizeof(float4), hipMemcpyHostToDevice, e->stream));
@@ -621,7 +635,36 @@ int compile(gcs_engine* e)
         HIPCHK(hipMemcpyAsync(e->bval, val.data(), val.size() * sizeof(float4), hipMemcpyHostToDevice, e->stream));
         if (f64)
             HIPCHK(hipMemcpyAsync(e->dbval, vald.data(), vald.size() * sizeof(double4), hipMemcpyHostToDevice, e->stream));
-        HIPCHK(hipStreamSynchronize(e->stream));  // val / ent die at the end of this block
+        // the reverse of every entry (j's entry pointing back at i; the k-th such entry for the k-th duplicate):
+        // k_cell_sort then tells each partner's entry its particle's slot (slot_bonds).  Every pairwise field is
+        // entered in both directions; an entry without its reverse turns the slot-indexed partners off
+        std::vector<int> rev(ent.size(), -1);
+        bool rev_ok = true;
+        for (int i = 0; i < n && rev_ok; ++i)
+            for (int q = off[i]; q < off[i + 1]; ++q) {
+                const int j = ent[q].x;
+                int k = 0;  // this is the k-th entry of row i pointing at j
+                for (int r = off[i]; r < q; ++r) k += ent[r].x == j ? 1 : 0;
+                int found = -1;
+                for (int r = off[j]; r < off[j + 1]; ++r)
+                    if (ent[r].x == i && k-- == 0) {
+                        found = r;
+                        break;
+                    }
+                if (found < 0) {
+                    rev_ok = false;
+                    break;
+                }
+                rev[q] = found;
+            }
+        e->brev_ok = rev_ok;
+        dfree(e->brev);
+        if (rev_ok) {
+            if ((rc = dalloc(&e->brev, rev.size()))) return rc;
+            HIPCHK(hipMemcpyAsync(e->brev, rev.data(), rev.size() * sizeof(int), hipMemcpyHostToDevice, e->stream));
+        }
+        HIPCHK(hipStreamSynchronize(e->stream));  // val / ent / rev die at the end of this block
+        e->nbent = (int)ent.size();
         a.has_bonds = 1;
     }
     bool any_bend = false;
@@ -753,15 +796,23 @@ void enqueue_bin(gcs_engine* e)
 
 // order each (scattered) cell by particle index: the cell-sorted copies the pair loop reads; lists: also the
 // slot-ordered positions, constants and bond rows of the list step (islot: a decomposed build's particle -> slot)
+bool slot_bonds(const gcs_engine* e);
 void enqueue_cell_order(gcs_engine* e, bool lists = false, int* islot = nullptr)
 {
+    // slot-indexed partners (undecomposed lists): particle -> slot, each partner's entry and droplet target slot
+    const bool sbm = lists && !islot && slot_bonds(e);
+    const int* sb_rev = sbm && e->fa.has_bonds ? e->brev : nullptr;
+    int* sb_slot = sbm && e->fa.has_bonds ? e->bslot : nullptr;
+    const int* sb_swt = sbm && e->fa.sw_n > 0 ? e->swt : nullptr;
+    int* sb_swslot = sbm && e->fa.sw_n > 0 ? e->swslot : nullptr;
+    if (sbm) islot = e->islot;
     const int mix = e->fa.has_pair ? e->fa.pair_mix : 1;
     const int* boff = e->fa.has_bonds ? e->boff : nullptr;
     if (e->prec == 64) {
         if (lists)
             launch_cell_sort(e->stream, e->ctx, e->dpos[0], e->dpos[1], e->dkmu, e->n, e->tmp, e->cell_of, e->cstart,
                              e->sidx, e->scell, e->spos, e->sb, mix, e->ptype, e->dpsort[0], e->dpsort[1], e->dskmu,
-                             e->sbrow, boff, islot, e->psort[0], e->psort[1]);
+                             e->sbrow, boff, islot, e->psort[0], e->psort[1], sb_rev, sb_slot, sb_swt, sb_swslot);
         else
             launch_cell_sort(e->stream, e->ctx, e->dpos[0], e->dpos[1], e->dkmu, e->n, e->tmp, e->cell_of, e->cstart,
                              e->sidx, e->scell, e->spos, e->sb, mix);
@@ -769,7 +820,7 @@ void enqueue_cell_order(gcs_engine* e, bool lists = false, int* islot = nullptr)
         if (lists)
             launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, e->n, e->tmp, e->cell_of, e->cstart,
                              e->sidx, e->scell, e->spos, e->sb, mix, e->ptype, e->psort[0], e->psort[1], e->skmu,
-                             e->sbrow, boff, islot);
+                             e->sbrow, boff, islot, sb_rev, sb_slot, sb_swt, sb_swslot);
         else
             launch_cell_sort(e->stream, e->ctx, e->pos[0], e->pos[1], e->kmu, e->n, e->tmp, e->cell_of, e->cstart,
                              e->sidx, e->scell, e->spos, e->sb, mix);
@@ -918,13 +969,41 @@ ForceArgs list_args(const gcs_engine* e)
     a.list_nt = (a.list_fmt == kListFmtRel16 || a.list_fmt == kListFmtInt) ? 1 : 0;
     a.list_deal = list_deal(e);
     a.par_hint = -1;
+    if (slot_bonds(e)) {
+        a.bslot = e->bslot;
+        a.swslot = e->swslot;
+    }
     return a;
+}
+
+#ifndef GCS_LIST_SLOT_BONDS
+#define GCS_LIST_SLOT_BONDS 1  // 1: the list step reads bonded / droplet partners by slot (kernels.hip kLFlagPos)
+#endif
+// the undecomposed list step with slot-indexed partners: every partner of the particle-local terms is a bond CSR
+// entry or a droplet target (no bending triples or kinetochore fibers: those read i +- 1, i +- 2 and poles by
+// particle index -- the mitotic fields, whose stages run the small-system step anyway)
+bool slot_bonds(const gcs_engine* e)
+{
+    return GCS_LIST_SLOT_BONDS && !e->dom && !e->fa.has_bend && !e->fa.has_tether && e->bslot != nullptr &&
+           (!e->fa.has_bonds || e->brev_ok) && (e->fa.sw_n == 0 || e->swt != nullptr);
 }
 
 int ensure_list(gcs_engine* e)
 {
     const size_t stride = (size_t)((e->n + 63) & ~63);
     const size_t need = stride * (size_t)e->list_cap;  // every segment layout fits: waves x (cap / waves)
+    int rc;
+    // slot-indexed partners (slot_bonds): particle -> slot, and the partners' slots (k_lbuild writes them); sized
+    // by the current bond table (a topology change may grow it: graphs holding the old pointer are dropped)
+    if (GCS_LIST_SLOT_BONDS && !e->dom && (!e->bslot || e->nbent > e->bslot_cap)) {
+        dfree(e->bslot);
+        dfree(e->swslot);
+        e->bslot_cap = std::max(1, e->nbent);
+        if ((!e->islot && (rc = dalloc(&e->islot, e->n))) || (rc = dalloc(&e->bslot, e->bslot_cap)) ||
+            (rc = dalloc(&e->swslot, 64)))
+            return rc;
+        drop_graph(e);
+    }
     if (need <= e->list_alloc && e->lcount) return GCS_OK;
     dfree(e->list);
     dfree(e->lcount);
@@ -937,7 +1016,6 @@ int ensure_list(gcs_engine* e)
     dfree(e->dpsort[1]);
     dfree(e->dskmu);
     e->list_alloc = 0;
-    int rc;
     if ((rc = dalloc(&e->list, need)) || (rc = dalloc(&e->lcount, stride * kMaxListWaves)) ||
         (rc = dalloc(&e->lbase, stride)) || (rc = dalloc(&e->sbrow, stride)))
         return rc;
@@ -990,7 +1068,7 @@ int auto_list_every(const gcs_engine* e, double temperature, double timestep)
 int list_flags(const gcs_engine* e, int64_t st)
 {
     const bool next_build = ((st + 1) % e->list_every) == 0;
-    return (e->sched_flags != 0 ? 1 : 0) | (next_build ? 2 | 4 : 0);
+    return (e->sched_flags != 0 ? 1 : 0) | (next_build ? 2 | 4 | 16 : 0);  // 16: kLFlagPos
 }
 
 // one list step: on a rebuild step the cell list at cutoff + skin (ctx->grid, set by the prime or the last
@@ -1617,6 +1695,10 @@ int gcs_engine_destroy(gcs_engine* e)
     dfree(e->noise);
     dfree(e->dom_regions);
     dfree(e->islot);
+    dfree(e->bslot);
+    dfree(e->swslot);
+    dfree(e->brev);
+    dfree(e->swt);
     dfree(e->dom_send);
     dfree(e->dom_recv);
     dfree(e->dom_red);
@@ -2157,7 +2239,8 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
             const gcs_bd_config* rx = spacestep ? cfg : nullptr;  // the relaxation step
             if (e->l_need_build || G == 0) {
                 // a run start's rebuild, or no graphs
-                enqueue_list_step(e, e->l_need_build || phase == 0, list_flags(e, st), ct ? 1.0 : 0.0, par(done), rx);
+                enqueue_list_step(e, e->l_need_build || phase == 0, list_flags(e, st) | 16, ct ? 1.0 : 0.0, par(done),
+                                  rx);  // (16: a stretch's last step writes the particle-order copy, kLFlagPos)
                 e->l_need_build = false;
                 ++done;
                 e->rstats.eager_steps++;
@@ -2174,7 +2257,8 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
             // cache slot: rebuild phase, and whether the first step counts contacts
             rc = cached_graph(e, key, phase | (ct ? 1 << 20 : 0), p0, len, [&]() {
                 for (int k = 0; k < len; ++k)
-                    enqueue_list_step(e, (phase + k) % M == 0, list_flags(e, st + k), (ct && k == 0) ? 1.0 : 0.0,
+                    enqueue_list_step(e, (phase + k) % M == 0, list_flags(e, st + k) | (k == len - 1 ? 16 : 0),
+                                      (ct && k == 0) ? 1.0 : 0.0,
                                       p0 ^ (k & 1), rx);
             }, &x);
             if (rc || (rc = launch_graph(e, x))) return rc;
@@ -3171,7 +3255,7 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
             HIPCHK(hipEventRecord(ev[2 + 5 * k], e->stream));
             ForceArgs lk = la;
             lk.par_hint = e->parity ^ (int)(k & 1);  // as gcs_engine_run launches it
-            launch_list_step(e->stream, e->ctx, lk, list_flags(e, first_step + k) | 4);  // statistics every step
+            launch_list_step(e->stream, e->ctx, lk, list_flags(e, first_step + k) | 4 | (k == steps - 1 ? 16 : 0));
             e->fa.dbg_times = nullptr;
             for (int q = 3; q <= 5; ++q) HIPCHK(hipEventRecord(ev[q + 5 * k], e->stream));
             continue;

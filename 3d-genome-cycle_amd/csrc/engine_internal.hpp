@@ -202,6 +202,12 @@ struct ForceArgs {
     // through the bond CSR; targets carry kmu[i].w = 1
     int sw_n;
     const int* sw_idx;
+    // the list step's slot-indexed partners (engine.hip slot_bonds; nullptr: by particle index): per bond CSR entry q
+    // the slot of its partner bent[q].x, per droplet target t the slot of sw_idx[t] -- filed by k_cell_sort at every
+    // rebuild -- so the particle-local terms read the slot-order positions (psort) and the particle-order copy need be
+    // written only before a rebuild and at the end of a stretch of steps (kLFlagPos)
+    const int* bslot;
+    const int* swslot;
     // bending
     int has_bend;
     const float* bend_eps;
@@ -489,7 +495,8 @@ void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, cons
                       int n, const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell,
                       float4* spos, float* sb, int pair_mix, const int* ptype = nullptr, float4* psort0 = nullptr,
                       float4* psort1 = nullptr, float4* skmu = nullptr, int2* sbrow = nullptr,
-                      const int* boff = nullptr, int* islot = nullptr);
+                      const int* boff = nullptr, int* islot = nullptr, const int* brev = nullptr,
+                      int* bslot = nullptr, const int* swt = nullptr, int* swslot = nullptr);
 // fp64 positions: the fp32 sorted copies (spos / sb, what the list build bins) are their roundings; psort / skmu
 // are the fp64 slot-ordered copies the fp64 list step reads
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const double4* pos0, const double4* pos1, const double4* kmu,
@@ -497,7 +504,8 @@ void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const double4* pos0, con
                       float4* spos, float* sb, int pair_mix, const int* ptype = nullptr, double4* psort0 = nullptr,
                       double4* psort1 = nullptr, double4* skmu = nullptr, int2* sbrow = nullptr,
                       const int* boff = nullptr, int* islot = nullptr, float4* fsort0 = nullptr,
-                      float4* fsort1 = nullptr);
+                      float4* fsort1 = nullptr, const int* brev = nullptr, int* bslot = nullptr,
+                      const int* swt = nullptr, int* swslot = nullptr);
 // list step: build the neighbour lists on the current cell list (grid rc = cutoff + skin); one step from them
 void launch_list_build(hipStream_t s, DevCtx* ctx, const ForceArgs& a);
 // flags: 1 apply the schedule, 2 the next step rebuilds (bounding box -> grid), 4 neighbour-count statistics,

@@ -1229,7 +1229,9 @@ __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ct
                                                    real4<R>* __restrict__ psort1, real4<R>* __restrict__ skmu,
                                                    int2* __restrict__ sbrow, const int* __restrict__ boff,
                                                    int* __restrict__ islot, float4* __restrict__ fsort0,
-                                                   float4* __restrict__ fsort1)
+                                                   float4* __restrict__ fsort1, const int* __restrict__ brev,
+                                                   int* __restrict__ bslot, const int* __restrict__ swt,
+                                                   int* __restrict__ swslot)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n || s >= cstart[ctx->grid.ncell]) return;  // binned particles only (all of them, undecomposed)
@@ -1253,8 +1255,17 @@ __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ct
         if (fsort0)  // fp64: the list step's prefilter copy (put_slot)
             (ctx->parity ? fsort1 : fsort0)[d] = make_float4((float)p.x, (float)p.y, (float)p.z, 0.f);
         skmu[d] = k;
-        sbrow[d] = boff ? make_int2(boff[i], boff[i + 1]) : make_int2(0, 0);
+        const int2 row = boff ? make_int2(boff[i], boff[i + 1]) : make_int2(0, 0);
+        sbrow[d] = row;
         if (islot) islot[i] = d;
+        // the slot-indexed partners (ForceArgs::bslot): every entry pointing at this particle -- the reverse of
+        // each of its own entries (the CSR holds both directions) -- and its droplet target row learn its slot
+        if (bslot)
+            for (int q = row.x; q < row.y; ++q) bslot[brev[q]] = d;
+        if (swslot) {
+            const int t = swt[i];
+            if (t >= 0) swslot[t] = d;
+        }
     }
 }
 
@@ -1364,7 +1375,9 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
     // the step-start positions of the partners: the context's buffer, or posv (PL: k_pstep's LDS image, selected
     // statically so the compiler sees the LDS pointer and reads it with ds_read, not with flat loads that also count
     // against vmcnt)
-    const real4<R>* __restrict__ posc = PL ? posv : St<R>::pos(a, ctx->parity);
+    // (not PL: posv = the slot-order positions when the partners are slot-indexed, a.bslot / a.swslot)
+    const real4<R>* __restrict__ posc = (PL || posv) ? posv : St<R>::pos(a, ctx->parity);
+    const int* __restrict__ bsl = PL ? nullptr : a.bslot;
     const R cs = (R)ctx->cs;
     const R bs = (R)ctx->bs;
     R e_sw = 0, e_bond = 0, e_bend = 0, e_win = 0, e_wout = 0, e_pt = 0, e_kf = 0;
@@ -1411,7 +1424,7 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
               bvb[u] = (q0 + u < ee) ? bval[q0 + u] : mk4<R>(R(0), R(0), R(0), R(0));
           }
 #pragma unroll
-          for (int u = 0; u < BB; ++u) pjb[u] = posc[enb[u].x];
+          for (int u = 0; u < BB; ++u) pjb[u] = posc[bsl ? ((q0 + u < ee) ? bsl[q0 + u] : 0) : enb[u].x];
 #pragma unroll
           for (int u = 0; u < BB; ++u) {
             if (q0 + u >= ee) break;
@@ -1430,7 +1443,7 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
         if (__ballot(tgt)) {
             const int m = a.sw_n;
             const int jt = (__lane_id() < m) ? a.sw_idx[__lane_id()] : 0;
-            const real4<R> pt = posc[jt];
+            const real4<R> pt = posc[(!PL && a.swslot) ? ((__lane_id() < m) ? a.swslot[__lane_id()] : 0) : jt];
             for (int t0 = 0; t0 < m; t0 += nq) {
                 const int t = min(t0 + lq, 63);
                 const int j = __shfl(jt, t);
@@ -2806,6 +2819,10 @@ constexpr int kLFlagSched = 1;  // apply the device schedule (gcs_schedule)
 constexpr int kLFlagBBox = 2;   // the next step rebuilds: reduce the bounding box of the new positions -> its cell grid
 constexpr int kLFlagStats = 4;  // reduce the neighbour count (diagnostics: ctx->neighbors)
 constexpr int kLFlagDomain = 8;  // decomposed (k_lstep<..., DOM>): owned slots only, local reduction -> a.dom_red
+// write the particle-order copy of the new positions (always when the partners are particle-indexed, a.bslot ==
+// nullptr; otherwise the step before a rebuild -- k_cell_count bins it -- and the last step of a stretch, which the
+// host reads or other kernels take up)
+constexpr int kLFlagPos = 16;
 
 // the schedule's closed forms of the next step (time, core and bond scale): they need no totals, so k_pstep
 // evaluates them while the step's totals are still landing and hands them to list_tail_apply (the same expressions)
@@ -3237,7 +3254,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         R rin[3] = {0, 0, 0}, rout[3] = {0, 0, 0};
         local_terms<kModeStep, sizeof(R) == 8 ? GCS_LIST_BOND_BATCH64 : GCS_LIST_BOND_BATCH, R>(ctx, a, i, pi.x, pi.y,
                                                                                              pi.z, km, lfx, lfy, lfz, en, rin, rout,
-                                                       erow);
+                                                       erow, a.bslot ? qc : nullptr);
         if constexpr (DOM) {
             // the fused pack's bond check (k_domain_pack's): a bond of an owned particle longer than the halo (its
             // partner may be a stale ghost); the cut-off droplet and shared particles excepted
@@ -3484,10 +3501,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
         const R nyp = pi.y + mdt * fsy + amp * xi.y;
         const R nzp = pi.z + mdt * fsz + amp * xi.z;
         if (act) {
-            R4* __restrict__ pn = St<R>::pos(a, par ^ 1);  // particle order (bonded partners read ctx->parity's)
+            R4* __restrict__ pn = St<R>::pos(a, par ^ 1);  // particle order (see kLFlagPos)
             R4* __restrict__ qn = St<R>::psort(a, par ^ 1);
-            pn[i] = mk4<R>(nxp, nyp, nzp, R(0));
+            if (!a.bslot || (flags & kLFlagPos)) pn[i] = mk4<R>(nxp, nyp, nzp, R(0));
             qn[s] = mk4<R>(nxp, nyp, nzp, pi.w);
+            if constexpr (sizeof(R) == 8) {  // the prefilter copy (put_slot's)
+                float4* const fn = St<R>::fsort(a, par ^ 1);
+                if (fn) fn[s] = make_float4((float)nxp, (float)nyp, (float)nzp, 0.f);
+            }
         }
         if constexpr (DOM) {
             if (a.dom_bands) {
@@ -4628,21 +4649,23 @@ void launch_cell_scatter(hipStream_t s, int n, const int* cell_of, const int* sl
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const float4* pos0, const float4* pos1, const float4* kmu, int n,
                       const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell, float4* spos,
                       float* sb, int pair_mix, const int* ptype, float4* psort0, float4* psort1, float4* skmu,
-                      int2* sbrow, const int* boff, int* islot)
+                      int2* sbrow, const int* boff, int* islot, const int* brev, int* bslot, const int* swt,
+                      int* swslot)
 {
     hipLaunchKernelGGL(k_cell_sort<float>, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, kmu, n, tmp,
                        cell_of, cstart, sidx, scell, spos, sb, pair_mix, ptype, psort0, psort1, skmu, sbrow, boff, islot,
-                       (float4*)nullptr, (float4*)nullptr);
+                       (float4*)nullptr, (float4*)nullptr, brev, bslot, swt, swslot);
 }
 
 void launch_cell_sort(hipStream_t s, const DevCtx* ctx, const double4* pos0, const double4* pos1, const double4* kmu,
                       int n, const int* tmp, const int* cell_of, const int* cstart, int* sidx, int* scell, float4* spos,
                       float* sb, int pair_mix, const int* ptype, double4* psort0, double4* psort1, double4* skmu,
-                      int2* sbrow, const int* boff, int* islot, float4* fsort0, float4* fsort1)
+                      int2* sbrow, const int* boff, int* islot, float4* fsort0, float4* fsort1, const int* brev,
+                      int* bslot, const int* swt, int* swslot)
 {
     hipLaunchKernelGGL(k_cell_sort<double>, dim3((n + 255) / 256), dim3(256), 0, s, ctx, pos0, pos1, kmu, n, tmp,
                        cell_of, cstart, sidx, scell, spos, sb, pair_mix, ptype, psort0, psort1, skmu, sbrow, boff, islot,
-                       fsort0, fsort1);
+                       fsort0, fsort1, brev, bslot, swt, swslot);
 }
 
 template <int MODE, bool FUSED>

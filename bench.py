@@ -919,8 +919,8 @@ def parse_args(argv=None):
     ap.add_argument("--stub-engine", action="store_true", help=argparse.SUPPRESS)  # CPU tests of the launcher
     ap.add_argument("--no-start-window", action="store_true", help="skip the secondary step-0 window")
     ap.add_argument("--c5-steps", type=int, default=256, help="secondary C5 window per step shape (0 = skip)")
-    ap.add_argument("--cycle-scale", type=int, default=10,
-                    help="secondary C3 cell cycle at the reference step counts / this (0 = skip)")
+    ap.add_argument("--cycle-scale", type=int, default=1,
+                    help="secondary C3 cell cycle at the reference step counts / this (1: as configured; 0 = skip)")
     ap.add_argument("--decomp", type=int, default=0,
                     help="spatial domain decomposition of ONE trajectory: K domains (torchrun: one per rank over "
                          "RCCL; single process: K domains on this GPU, in-process exchange)")

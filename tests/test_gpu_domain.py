@@ -249,6 +249,25 @@ def test_engine_domains_processes_host_staged(tmp_path, config, world, prec):
     assert np.allclose(ctx["wall_semiaxes"], single.get_context()["wall_semiaxes"], rtol=WALL_REL[prec], atol=0)
 
 
+@pytest.mark.parametrize("prec", [64, 32])
+def test_decomposed_run_twice_in_one_process(c1_design, prec):
+    """the round-5 fault came on the SECOND identical 2-domain run of a process (device memory
+    recycled from the first run's engines, so stale contents where the first run saw fresh pages).  The same
+    decomposed case three times in this process, the engines of each run freed before the next: bit for bit the
+    same positions and context every time, the checks clear"""
+    cfg = InterphaseConfig()
+    outs = []
+    for _ in range(3):
+        run, doms, _ = _decomposed(c1_design, cfg, 2, STEPS, prec=prec)
+        run.check()
+        outs.append((domain.gather_positions(run, c1_design.n), doms[0].context()))
+        for d in doms:
+            d.e.close()
+    for x, c in outs[1:]:
+        assert np.array_equal(x, outs[0][0])
+        assert c == outs[0][1]
+
+
 @pytest.mark.parametrize("graph", [None, 4])
 @pytest.mark.parametrize("prec", [64, 32])
 def test_decomposed_skin_follows_core_scale(c1_design, prec, graph):
