@@ -1019,9 +1019,10 @@ int ensure_list(gcs_engine* e)
     if ((rc = dalloc(&e->list, need)) || (rc = dalloc(&e->lcount, stride * kMaxListWaves)) ||
         (rc = dalloc(&e->lbase, stride)) || (rc = dalloc(&e->sbrow, stride)))
         return rc;
-    if (e->prec == 64) {  // the slot-ordered copies in the engine's precision, + fp64: the prefilter copies (psort)
+    if (e->prec == 64) {  // the slot-ordered copies in the engine's precision (+ the prefilter's fp32 copies, psort)
         if ((rc = dalloc(&e->dpsort[0], stride)) || (rc = dalloc(&e->dpsort[1], stride)) ||
-            (rc = dalloc(&e->dskmu, stride)) || (rc = dalloc(&e->psort[0], stride)) || (rc = dalloc(&e->psort[1], stride)))
+            (rc = dalloc(&e->dskmu, stride)) ||
+            (GCS_LIST_PREFILTER && ((rc = dalloc(&e->psort[0], stride)) || (rc = dalloc(&e->psort[1], stride)))))
             return rc;
     } else {
         if ((rc = dalloc(&e->psort[0], stride)) || (rc = dalloc(&e->psort[1], stride)) || (rc = dalloc(&e->skmu, stride)))

@@ -418,6 +418,11 @@ constexpr int kListFmtRel16 = 2;
 constexpr int kPMax = 1536;         // particles of the persistent small-system step (kernels.hip k_pstep: LDS images)
 constexpr int kPHalfBytes = kPMax * 48 + 256 * 144;  // its hand-off buffer (psync): two halves (kernels.hip k_pstep)
 constexpr int kPSyncWords = 2 * kPHalfBytes / 4;
+#ifndef GCS_LIST_PREFILTER
+// the fp64 list step's fp32 prefilter (kernels.hip k_lstep, PF; engine.hip keeps its fp32 slot-order copy): 0 (default:
+// measured slower, DESIGN.md §4 "fp32 prefilter") gathers every list entry's fp64 record, 1 the prefilter pipeline
+#define GCS_LIST_PREFILTER 0
+#endif
 constexpr int kListCountMask = (1 << 30) - 1;
 constexpr int kListOverflow = 1 << 30;
 

@@ -3121,10 +3121,6 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 // per SIMD either spills (3.74e9 / 1.15e9)
 #define GCS_LIST_UNROLL64 4
 #endif
-#ifndef GCS_LIST_PREFILTER
-// the fp64 step's fp32 prefilter (1) or every list entry's fp64 record gathered and tested (0)
-#define GCS_LIST_PREFILTER 1
-#endif
 #ifndef GCS_LIST_PF_BATCH
 #define GCS_LIST_PF_BATCH 8  // fp64 step, prefilter: list entries per fp32 batch
 #endif
