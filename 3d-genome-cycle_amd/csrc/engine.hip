@@ -1039,6 +1039,24 @@ int ensure_list(gcs_engine* e)
         HIPCHK(hipMemcpyAsync(e->lticket, h.data(), h.size() * sizeof(unsigned), hipMemcpyHostToDevice, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
     }
+    // GCS_DEBUG_POISON (tests): the per-slot buffers start as hashed garbage instead of whatever the allocator hands
+    // out (fresh pages are zero, a recycled allocation is not): every read of a slot the current build did not write
+    // then shows up -- the round-5 decomposed fault (k_cell_sort's sentinel records)
+    if (std::getenv("GCS_DEBUG_POISON")) {
+        launch_poison(e->stream, e->lcount, stride * kMaxListWaves * sizeof(int));
+        launch_poison(e->stream, e->lbase, stride * sizeof(int4));
+        launch_poison(e->stream, e->sbrow, stride * sizeof(int2));
+        if (e->prec == 64) {
+            launch_poison(e->stream, e->dpsort[0], stride * sizeof(double4));
+            launch_poison(e->stream, e->dpsort[1], stride * sizeof(double4));
+            launch_poison(e->stream, e->dskmu, stride * sizeof(double4));
+        } else {
+            launch_poison(e->stream, e->psort[0], stride * sizeof(float4));
+            launch_poison(e->stream, e->psort[1], stride * sizeof(float4));
+            launch_poison(e->stream, e->skmu, stride * sizeof(float4));
+        }
+        HIPCHK(hipGetLastError());
+    }
     // entries past a slot's count are read (never gathered): keep them defined
     HIPCHK(hipMemsetAsync(e->list, 0, need * sizeof(int), e->stream));
     e->list_alloc = need;

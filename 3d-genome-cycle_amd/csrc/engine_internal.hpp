@@ -536,6 +536,8 @@ int list_step_grid(const ForceArgs& a);
 // the persistent small-system step: `steps` steps of n <= kPMax particles in ONE cooperative launch (a.psync zeroed
 // by the caller first); flags: kernels.hip kLFlagSched when the schedule applies
 int launch_pstep(hipStream_t s, DevCtx* ctx, const ForceArgs& a, int steps, int flags);
+// GCS_DEBUG_POISON: fill `bytes` (a multiple of 4) with hashed garbage words
+void launch_poison(hipStream_t s, void* p, size_t bytes);
 // k_pstep_guard: restore 0 keeps *ctx in *keep unless *stall; restore 1 puts *keep back into *ctx if *stall
 void launch_pstep_guard(hipStream_t s, DevCtx* ctx, DevCtx* keep, const int* stall, int restore);
 void launch_force(hipStream_t s, int mode, int waves, DevCtx* ctx, const ForceArgs& a, bool fused);

@@ -16,6 +16,7 @@
 #include "engine_internal.hpp"
 
 #include <hipcub/hipcub.hpp>
+#include <algorithm>
 #include <type_traits>
 
 #include "../../include/gcs.h"
@@ -1234,7 +1235,22 @@ __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ct
                                                    int* __restrict__ swslot)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n || s >= cstart[ctx->grid.ncell]) return;  // binned particles only (all of them, undecomposed)
+    if (s >= n) return;
+    if (s >= cstart[ctx->grid.ncell]) {  // binned particles only (all of them, undecomposed)
+        // a decomposed build bins fewer slots than the step launches (n): the step's slot loads still read these
+        // slots' records (only `act` masks what it does with them), so they must hold a harmless record -- not
+        // what the memory held before (a recycled allocation: a bond row of garbage sends the local-terms wave's
+        // gathers anywhere; the round-5 decomposed-test fault).  Particle 0, no bonds, no target
+        if (psort0) {
+            const real4<R> z = mk4<R>(R(0), R(0), R(0), wpack<R>(0));
+            psort0[s] = z;
+            psort1[s] = z;
+            if (fsort0) fsort0[s] = fsort1[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+            skmu[s] = mk4<R>(R(0), R(0), R(0), R(0));
+            sbrow[s] = make_int2(0, 0);
+        }
+        return;
+    }
     const real4<R>* pos = ctx->parity ? p1 : p0;
     const int i = tmp[s];
     const int c = cell_of[i];
@@ -4764,6 +4780,18 @@ static void launch_list_relax_r(hipStream_t s, DevCtx* ctx, const ForceArgs& a, 
 void launch_dom_grid(hipStream_t s, DevCtx* ctx, const ForceArgs& a)
 {
     hipLaunchKernelGGL(k_dom_grid, dim3(1), dim3(1), 0, s, ctx, a);
+}
+
+__global__ void k_poison(unsigned* p, size_t words)
+{
+    for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < words; k += (size_t)gridDim.x * blockDim.x)
+        p[k] = (unsigned)((k + 1) * 2654435761ull) ^ 0x5bd1e995u;
+}
+void launch_poison(hipStream_t s, void* p, size_t bytes)
+{
+    const size_t words = bytes / sizeof(unsigned);
+    hipLaunchKernelGGL(k_poison, dim3((unsigned)std::min<size_t>(1024, (words + 255) / 256 + 1)), dim3(256), 0, s,
+                       (unsigned*)p, words);
 }
 
 void launch_pstep_guard(hipStream_t s, DevCtx* ctx, DevCtx* keep, const int* stall, int restore)

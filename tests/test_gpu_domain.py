@@ -250,14 +250,19 @@ def test_engine_domains_processes_host_staged(tmp_path, config, world, prec):
 
 
 @pytest.mark.parametrize("prec", [64, 32])
-def test_decomposed_run_twice_in_one_process(c1_design, prec):
-    """the round-5 fault came on the SECOND identical 2-domain run of a process (device memory
-    recycled from the first run's engines, so stale contents where the first run saw fresh pages).  The same
-    decomposed case three times in this process, the engines of each run freed before the next: bit for bit the
-    same positions and context every time, the checks clear"""
+def test_decomposed_run_twice_in_one_process(c1_design, prec, monkeypatch):
+    """VERDICT r5 item 1.  The round-5 fault came on the SECOND identical 2-domain run of a process: the decomposed
+    step launches a workgroup per 64 of ALL n slots, but a domain's build writes only its binned slots; the others
+    kept what their allocation held -- zeros on fresh pages, anything on a recycled allocation -- and the local-terms
+    wave (every lane, `act` masks only the results) followed that garbage bond row (kernels.hip k_cell_sort now
+    writes a harmless record there).  The same decomposed case three times in this process, the third with every
+    per-slot list buffer filled with hashed garbage at allocation (GCS_DEBUG_POISON): bit for bit the same positions
+    and context every time, the checks clear"""
     cfg = InterphaseConfig()
     outs = []
-    for _ in range(3):
+    for k in range(3):
+        if k == 2:
+            monkeypatch.setenv("GCS_DEBUG_POISON", "1")
         run, doms, _ = _decomposed(c1_design, cfg, 2, STEPS, prec=prec)
         run.check()
         outs.append((domain.gather_positions(run, c1_design.n), doms[0].context()))
@@ -266,6 +271,22 @@ def test_decomposed_run_twice_in_one_process(c1_design, prec):
     for x, c in outs[1:]:
         assert np.array_equal(x, outs[0][0])
         assert c == outs[0][1]
+
+
+@pytest.mark.parametrize("prec", [64, 32])
+def test_list_step_poisoned_buffers_bitwise(c1_design, prec, monkeypatch):
+    """the undecomposed list step with its per-slot buffers poisoned at allocation (GCS_DEBUG_POISON): every slot is
+    rebuilt before it is read, so the trajectory is bitwise the unpoisoned one"""
+    cfg = InterphaseConfig()
+    xs = []
+    for poison in (False, True):
+        if poison:
+            monkeypatch.setenv("GCS_DEBUG_POISON", "1")
+        e = _engine(c1_design, cfg, 3, prec)
+        e.run(40, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
+        xs.append(e.get_positions())
+        e.close()
+    assert np.array_equal(xs[0], xs[1])
 
 
 @pytest.mark.parametrize("graph", [None, 4])
