@@ -1,5 +1,6 @@
 """A bare run of the persistent small-system step on the anatelophase system (fp64), for profilers:
 usage: python tools/pstep_run.py [steps] [precision]"""
+import os
 import sys
 from pathlib import Path
 
@@ -17,5 +18,8 @@ s, h = mitotic.build_anatelophase(Engine, a, cfg, precision=prec)
 mitotic.AnatelophaseDriver(s, h, a, cfg, log=None).run_initialization()
 s.run(steps, temperature=cfg.temperature, timestep=cfg.timestep, seed=3)
 s.synchronize()
+if os.environ.get("GCS_MAPS_OUT"):  # (diagnostics) the mappings, to symbolise a crash at exit (tools/symbolize_trace.py)
+    with open("/proc/self/maps") as src, open(os.environ["GCS_MAPS_OUT"], "w") as dst:
+        dst.write(src.read())
 s.close()
 print("done", steps, flush=True)
