@@ -283,6 +283,7 @@ struct gcs_engine {
     int skin_level_pm = 0;      // the skin (1/1000 of the pair cutoff) of the current undecomposed list run (skin_level)
     int list_every_opt = 0;     // GCS_OPT_LIST_EVERY: rebuild period in steps (0: from the noise amplitude)
     int list_every = 1;         // the period of the current run
+    int list_phase = 0;         // GCS_OPT_LIST_PHASE: rebuilds at the steps s with (s + list_phase) % list_every == 0
     int list_waves = 4;         // GCS_OPT_LIST_WAVES: waves per tile (2: more tiles resident, for replica runs)
     int list_fmt_opt = 0;       // GCS_OPT_LIST_FORMAT: 0 (default) 16-bit slots (absolute up to 65,536 particles,
                                 // plane-relative beyond), 1 plane-relative 16-bit, 2 absolute 32-bit
@@ -1086,7 +1087,7 @@ int auto_list_every(const gcs_engine* e, double temperature, double timestep)
 // rebuilds (its grid); neighbour-count statistics on those steps too (ctx->neighbors)
 int list_flags(const gcs_engine* e, int64_t st)
 {
-    const bool next_build = ((st + 1) % e->list_every) == 0;
+    const bool next_build = ((st + e->list_phase + 1) % e->list_every) == 0;
     return (e->sched_flags != 0 ? 1 : 0) | (next_build ? 2 | 4 | 16 : 0);  // 16: kLFlagPos
 }
 
@@ -2244,7 +2245,7 @@ int gcs_engine_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_step, 
                 key = run_key(e, cfg, spacestep);
             }
             const int M = e->list_every;
-            const int phase = (int)(((st % M) + M) % M);
+            const int phase = (int)((((st + e->list_phase) % M) + M) % M);
             // the contact update the host asked for after the last step: counted by this stretch's first step, its
             // distance set in the context (so the stretch's graph does not depend on it)
             const bool ct = e->c_pending > 0;
@@ -2769,7 +2770,7 @@ void enqueue_dom_list_step(gcs_engine* e, int64_t st, double* red, bool fused_pa
         a.dom_regions = e->dom_regions;
         a.dom_shared = e->dom_shared_flag;
     }
-    if (e->l_need_build || st % e->list_every == 0) {
+    if (e->l_need_build || (st + e->list_phase) % e->list_every == 0) {
         const DomBox reg = dom_region(e);
         enqueue_count(e, &reg, e->islot);
         enqueue_scan(e, false);
@@ -3084,7 +3085,7 @@ int gcs_engine_domain_run(gcs_engine* e, const gcs_bd_config* cfg, int64_t first
             ++k;
             continue;
         }
-        const int phase = e->dom_list ? (int)(st % M) : 0;
+        const int phase = e->dom_list ? (int)((st + e->list_phase) % M) : 0;
         // (geometry, buffers, communicator and options drop the graph when they change: drop_domain_graph)
         const bool same = e->dgexec && e->dg_steps == G && std::memcmp(&e->dg_cfg, cfg, sizeof(*cfg)) == 0 &&
                           e->dg_version == e->topo_version && e->dg_sched_flags == e->sched_flags &&
@@ -3259,7 +3260,7 @@ int gcs_engine_profile(gcs_engine* e, const gcs_bd_config* cfg, int64_t first_st
         HIPCHK(hipEventRecord(ev[1 + 5 * k], e->stream));
         if (dbg && k == steps - 1) e->fa.dbg_times = dbg;
         if (lst) {
-            const bool build = e->l_need_build || ((first_step + k) % e->list_every) == 0;
+            const bool build = e->l_need_build || ((first_step + k + e->list_phase) % e->list_every) == 0;
             e->l_need_build = false;
             ForceArgs la = list_args(e);
             if (build) {
@@ -3489,6 +3490,13 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         if (value < 0) return fail(GCS_EINVAL, "dense threshold must be >= 0");
         e->dense_opt = (int)value;
         e->chain_valid = e->dense_chain = false;
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_LIST_PHASE) {
+        if (value < 0 || value > 1024) return fail(GCS_EINVAL, "list phase must be in [0, 1024]");
+        e->list_phase = (int)value;
+        e->l_need_build = true;
+        drop_graph(e);
         return GCS_OK;
     }
     if (option == GCS_OPT_SMALL_STEP) {

@@ -643,6 +643,10 @@ def replica_main(args):
             from gcs import _abi as A
             e = make_engine(d, cfg, local, window, state, precision=args.precision)
             opts = [(A.OPT_GRAPH_STEPS, G), (A.OPT_SCAN_BLOCKS, args.scan_mb), (A.OPT_LIST_WAVES, list_waves)]
+            if args.stagger and R > 1:
+                # the replicas' list rebuilds staggered over the period (C2: every 8 steps -> phases 0, 2, 4, 6 at
+                # R = 4), so one replica's short cell kernels and list build overlap the others' step kernels
+                opts.append((A.OPT_LIST_PHASE, (8 * k) // R))
             if args.precision == 32:  # the fp32 engine's tile-step shapes and their options
                 opts += [(A.OPT_WAVES_PER_TILE, args.waves), (A.OPT_CHUNK_ORDER, args.chunk_order),
                          (A.OPT_FUSED_STEP, args.fused), (A.OPT_SPLIT_TILES, args.split),
@@ -905,6 +909,9 @@ def parse_args(argv=None):
     ap.add_argument("--cu-count", type=int, default=256)
     ap.add_argument("--engine-opt", action="append", default=[], metavar="NAME=VALUE",
                     help="extra engine option (gcs._abi OPT_<NAME>), repeatable; for experiments")
+    ap.add_argument("--stagger", action="store_true",
+                    help="several replicas per GPU: stagger their list rebuilds over the period (GCS_OPT_LIST_PHASE; "
+                         "measured no faster, profiles/r06_stagger_ab.txt)")
     ap.add_argument("--list-waves", type=int, default=0,
                     help="list step waves per tile: 2 or 4 (0: 2 with several replicas per GPU, else 4)")
     ap.add_argument("--fused", type=int, default=3,

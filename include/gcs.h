@@ -396,6 +396,11 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
                                      per chunk of steps, every workgroup holding the whole system in LDS (all pairs; the
                                      new positions handed between workgroups as tagged granules every step), unless
                                      GCS_OPT_FUSED_STEP was set; 0 the step shapes above */
+#define GCS_OPT_LIST_PHASE 19     /* list step: rebuild at the steps s with (s + phase) % period == 0 (default 0).  Several
+                                     trajectories sharing a GPU (bench.py's replicas) stagger their rebuilds with it, so
+                                     one's short cell kernels overlap the others' step kernels; a trajectory is bitwise
+                                     reproducible for a given phase (its lists' entry order, hence its sums' order,
+                                     follows the rebuild steps) */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
 
 /* List-step diagnostics (the neighbour lists md::neighbor_searcher keeps between rebuilds; micromd, called at

@@ -545,6 +545,31 @@ def test_list_relaxation_small_and_ragged_sizes(n, prec):
                                                                     rel={64: 1e-10, 32: 1e-4}[prec])
 
 
+@precisions
+def test_list_phase_staggers_rebuilds(c1_design, prec):
+    """GCS_OPT_LIST_PHASE (staggered replicas): rebuilds at steps s with (s + phase) % period == 0 -- another set of
+    rebuild steps, so other list orders and sums (not bitwise), but the same pair set: within the precision's bound of
+    the oracle, chunked runs bitwise equal to one run at the same phase"""
+    cfg = InterphaseConfig()
+    o, _ = interphase.build_interphase(oracle.OracleSystem, c1_design, cfg, precision=prec)
+    o.set_schedule(**interphase.interphase_schedule(cfg))
+    o.set_context(LATE)
+    o.run(48, first_step=LATE["step"], temperature=cfg.temperature, timestep=cfg.timestep, seed=11)
+    xs = {}
+    for phase, chunks in ((0, (48,)), (3, (48,)), (3, (20, 28))):
+        e = _list_engine(c1_design, cfg, prec, list_every=8, list_phase=phase)
+        e.set_schedule(**interphase.interphase_schedule(cfg))
+        e.set_context(LATE)
+        st = LATE["step"]
+        for c in chunks:
+            e.run(c, first_step=st, temperature=cfg.temperature, timestep=cfg.timestep, seed=11)
+            st += c
+        xs[(phase, chunks)] = (e.get_positions(), e.list_stats())
+        assert np.abs(xs[(phase, chunks)][0] - o.get_positions()).max() <= TOL_X[prec]
+    assert np.array_equal(xs[(3, (48,))][0], xs[(3, (20, 28))][0])
+    assert xs[(3, (48,))][1]["builds"] == xs[(3, (20, 28))][1]["builds"]
+
+
 def _format_run(design, cfg, prec, fmt, steps, ctx=LATE, seed=11, **opts):
     e = _list_engine(design, cfg, prec, list_format=fmt, **opts)
     e.set_schedule(**interphase.interphase_schedule(cfg))
