@@ -2469,11 +2469,13 @@ int gcs_engine_contacts_update(gcs_engine* e, double distance)
     if (!e->c_keys) {
         int bits = e->c_bits_opt;
         if (bits <= 0) {
-            // >= 512 slots per particle, at most 2^28 (3 GB): a C2 window of the reference's cadence (10 samples x
-            // 50 updates) holds ~4.1 million distinct pairs, 12 % of C2's 2^25 slots; at 128 per particle (2^23,
-            // 49 % full) the probe chains cost 3 % of the interphase stage (tools/interphase_probe.py, r03d)
+            // >= 256 slots per particle, at most 2^28 (3 GB): a C2 window of the reference's cadence (10 samples x
+            // 50 updates) holds ~2.9 million distinct pairs, 18 % of C2's 2^24 slots.  Round 6, 300,000 steps of
+            // the interphase stage with the contact map (profiles/r06_contact_bits.txt): 2^25 slots 28.97k
+            // steps/s, 2^24 29.45k, 2^23 29.30k -- the table's random atomics stay closer to the caches, and each
+            // window's read compacts a smaller table (9.0 -> 5.8 ms); at 2^23 the probe chains start to cost
             bits = 12;
-            while (bits < 28 && ((int64_t)1 << bits) < 512 * (int64_t)e->n) ++bits;
+            while (bits < 28 && ((int64_t)1 << bits) < 256 * (int64_t)e->n) ++bits;
         }
         const size_t slots = (size_t)1 << bits;
         if ((rc = dalloc(&e->c_keys, slots)) || (rc = dalloc(&e->c_counts, slots)) || (rc = dalloc(&e->c_flags, 2)))

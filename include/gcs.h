@@ -373,7 +373,7 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
 #define GCS_OPT_SUBTILES 7       /* pair-loop stencils per 64-particle tile: 1, 2 or 4 (default 2) */
 #define GCS_OPT_SCAN_BLOCKS 8    /* cell scan: 1 = multi-block look-back scan (default), 0 = one workgroup */
 #define GCS_OPT_TILE_PRIORITY 6  /* n > 0: pair-loop wave priority min(3, tile candidates / n); 0 = off (default 700) */
-#define GCS_OPT_CONTACT_BITS 9   /* contact map: 2^bits hash slots (0 = default, >= 2 N slots sized at first update) */
+#define GCS_OPT_CONTACT_BITS 9   /* contact map: 2^bits hash slots (0 = default: >= 256 N slots, <= 2^28, sized at the first update) */
 #define GCS_OPT_LIST_SKIN 10      /* list step: skin in 1/1000 of the pair cutoff (0 = default: 500 fp32, 350 fp64 at core
                                      scale 1; x core scale (fp32) / sqrt(core scale) (fp64) while a schedule grows it: 250 / 250 at 0.5) */
 #define GCS_OPT_LIST_EVERY 11     /* list step: rebuild period in steps (0 = default: from the noise amplitude) */
