@@ -78,40 +78,79 @@ __global__ __launch_bounds__(256) void k_contact_insert(const DevCtx* __restrict
         }
 }
 
-// occupied slots of the table (one atomic per wave): sizes the compaction's scratch before the compaction
+// Both table scans below add to ONE global counter, so they aggregate per workgroup: one atomic per 4,096 slots.
+// (Per-wave atomics -- 2^24 / 64 = 262k adds to one address at C2's table -- serialised in L2 and took 5.8 ms per
+// output window at C2, 46 ms at C5; profiles/r04s_c5_kernel_stats.csv, profiles/r06_contact_bits.txt.)
+constexpr int kCompactPer = 16;                          // slots per thread per chunk
+constexpr long long kCompactChunk = 256LL * kCompactPer;  // slots per workgroup per chunk
+
+// block-wide sum of v (256 threads), valid in thread 0
+__device__ __forceinline__ int block_sum_256(int v, int* s_wave)
+{
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const int t = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+    __syncthreads();
+    return t;
+}
+
+// occupied slots of the table: sizes the compaction's scratch before the compaction
 __global__ __launch_bounds__(256) void k_contact_occupied(const unsigned long long* __restrict__ keys, long long slots,
                                                           int* __restrict__ total)
 {
-    const int lane = threadIdx.x & 63;
+    __shared__ int s_wave[4];
     int c = 0;
     for (long long h = (long long)blockIdx.x * blockDim.x + threadIdx.x; h < slots;
          h += (long long)gridDim.x * blockDim.x)
         c += keys[h] != kContactEmpty ? 1 : 0;
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-    if (lane == 0 && c) atomicAdd(total, c);
+    const int t = block_sum_256(c, s_wave);
+    if (threadIdx.x == 0 && t) atomicAdd(total, t);
 }
 
-// occupied slots -> (key, count) lists; output order is arbitrary (the sort that follows fixes it)
+// occupied slots -> (key, count) lists; output order is arbitrary (the sort that follows fixes it).  A workgroup
+// takes 4,096 consecutive slots (16 per thread, coalesced loads kept in registers), scans the per-thread occupancy
+// across the workgroup, reserves its run of the output with one atomic and writes each thread's keys in its run.
 __global__ __launch_bounds__(256) void k_contact_compact(const unsigned long long* __restrict__ keys,
                                                          const unsigned* __restrict__ counts, long long slots,
                                                          unsigned long long* __restrict__ out_k,
                                                          unsigned* __restrict__ out_c, int* __restrict__ total)
 {
-    const int lane = threadIdx.x & 63;
-    for (long long h = (long long)blockIdx.x * blockDim.x + threadIdx.x; h < slots;
-         h += (long long)gridDim.x * blockDim.x) {
-        const unsigned long long k = keys[h];
-        const bool occ = k != kContactEmpty;
-        // wave-aggregated append: one atomic per wave
-        const unsigned long long m = __ballot(occ);
-        int base = 0;
-        if (lane == 0 && m) base = atomicAdd(total, __popcll(m));
-        base = __shfl(base, 0);
-        if (occ) {
-            const int o = base + __popcll(m & ((1ull << lane) - 1ull));
-            out_k[o] = k;
-            out_c[o] = counts[h];
+    __shared__ int s_wave[4];
+    __shared__ int s_base;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (long long c0 = (long long)blockIdx.x * kCompactChunk; c0 < slots;
+         c0 += (long long)gridDim.x * kCompactChunk) {
+        unsigned long long k[kCompactPer];
+        int m = 0;
+#pragma unroll
+        for (int u = 0; u < kCompactPer; ++u) {
+            const long long h = c0 + (long long)u * 256 + t;
+            k[u] = h < slots ? keys[h] : kContactEmpty;
+            m += k[u] != kContactEmpty ? 1 : 0;
         }
+        int x = m;  // inclusive scan over the wave
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_wave[w] = x;
+        __syncthreads();
+        if (t == 0) {
+            const int tot = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+            s_base = tot ? atomicAdd(total, tot) : 0;
+        }
+        __syncthreads();
+        int o = s_base + x - m;
+        for (int v = 0; v < w; ++v) o += s_wave[v];
+#pragma unroll
+        for (int u = 0; u < kCompactPer; ++u)
+            if (k[u] != kContactEmpty) {
+                out_k[o] = k[u];
+                out_c[o] = counts[c0 + (long long)u * 256 + t];
+                ++o;
+            }
+        __syncthreads();  // s_wave / s_base are rewritten by the next chunk
     }
 }
 
@@ -168,7 +207,8 @@ void launch_contact_occupied(hipStream_t s, const unsigned long long* keys, long
 void launch_contact_compact(hipStream_t s, const unsigned long long* keys, const unsigned* counts, long long slots,
                             unsigned long long* out_k, unsigned* out_c, int* total)
 {
-    const long long blocks = std::min<long long>((slots + 255) / 256, 4096);
+    const long long chunks = (slots + kCompactChunk - 1) / kCompactChunk;
+    const long long blocks = std::max<long long>(1, std::min<long long>(chunks, 8192));
     hipLaunchKernelGGL(k_contact_compact, dim3((unsigned)blocks), dim3(256), 0, s, keys, counts, slots, out_k, out_c,
                        total);
 }

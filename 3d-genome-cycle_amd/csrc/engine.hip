@@ -87,8 +87,19 @@ int dalloc(T** p, size_t count)
     if (count == 0) count = 1;
     hipError_t e = hipMalloc((void**)p, count * sizeof(T));
     if (e != hipSuccess) return fail(GCS_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    // GCS_DEBUG_POISON=2 (diagnostics): every allocation starts as hashed garbage (what a recycled allocation may
+    // hold), so a read of memory nothing wrote shows up in a fresh process too
+    const char* pv = std::getenv("GCS_DEBUG_POISON");
+    if (pv && std::atoi(pv) >= 2) {
+        launch_poison(nullptr, *p, count * sizeof(T) / 4 * 4);
+        (void)hipDeviceSynchronize();
+    }
     return GCS_OK;
 }
+
+// GCS_DEBUG_SYNC (diagnostics): synchronise after each launch of the decomposed path and report, on stderr, the
+// launch after which the stream first holds an error (the kernel that faulted)
+void dbg_sync(gcs_engine* e, const char* what);
 
 template <class T>
 void dfree(T*& p)
@@ -910,6 +921,15 @@ int skin_level(const gcs_engine* e, int64_t st)
     if (!(cs > 0.0) || cs >= 1.0) return s1;
     const double u = e->prec == 64 ? std::sqrt(cs) : cs;
     return std::max(50, (int)std::lround(s1 * u / 10.0) * 10);
+}
+
+void dbg_sync(gcs_engine* e, const char* what)
+{
+    static const bool on = std::getenv("GCS_DEBUG_SYNC") != nullptr;
+    if (!on) return;
+    hipError_t he = hipStreamSynchronize(e->stream);
+    if (he == hipSuccess) he = hipGetLastError();
+    if (he != hipSuccess) std::fprintf(stderr, "GCS_DEBUG_SYNC: the stream failed after %s: %s\n", what, hipGetErrorString(he));
 }
 
 // the list entry format (GCS_OPT_LIST_FORMAT): 0 (default) absolute 16-bit slots up to 65,536 particles and
@@ -2775,14 +2795,20 @@ void enqueue_dom_list_step(gcs_engine* e, int64_t st, double* red, bool fused_pa
     if (e->l_need_build || (st + e->list_phase) % e->list_every == 0) {
         const DomBox reg = dom_region(e);
         enqueue_count(e, &reg, e->islot);
+        dbg_sync(e, "dom: k_cell_count");
         enqueue_scan(e, false);
+        dbg_sync(e, "dom: cell scan");
         launch_cell_scatter(e->stream, e->n, e->cell_of, e->slot, e->cstart, e->tmp, e->count);
+        dbg_sync(e, "dom: k_cell_scatter");
         enqueue_cell_order(e, true, e->islot);
+        dbg_sync(e, "dom: k_cell_sort");
         launch_list_build(e->stream, e->ctx, a);
+        dbg_sync(e, "dom: k_lbuild");
         e->l_need_build = false;
     }
     e->dom_flags_step = list_flags(e, st) | 8;  // 8: kLFlagDomain
     launch_list_step(e->stream, e->ctx, a, e->dom_flags_step);
+    dbg_sync(e, "dom: k_lstep<DOM>");
     if (!fused_pack) launch_domain_shared_out(e->stream, e->ctx, a, e->dom_shared_idx, e->dom_nshared, red);
 }
 
@@ -2792,6 +2818,7 @@ void enqueue_dom_list_finish(gcs_engine* e, const double* glob, void* bands, int
     // (with the engine's reduction buffer: its shared block is zeroed for the next step's fused pack)
     launch_list_domain_tail(e->stream, e->ctx, domain_args(e, e->dom_red), glob, e->dom_flags_step & ~8,
                             e->dom_shared_idx, e->dom_nshared, bands, npeer, e->dom_cap + 1);
+    dbg_sync(e, "dom: k_ldom_tail");
 }
 }  // namespace
 
@@ -2826,6 +2853,7 @@ static int domain_step_impl(gcs_engine* e, const gcs_bd_config* cfg, int64_t ste
         // the fused pack's starting state: empty send bands, an empty shared block in the reduction buffer
         if (e->dom_send) launch_band_headers_zero(e->stream, e->dom_send, e->dom_npeer, e->dom_cap + 1, e->prec);
         if (e->dom_red) HIPCHK(hipMemsetAsync(e->dom_red, 0, (size_t)e->dom_nred * sizeof(double), e->stream));
+        dbg_sync(e, "dom: run start (prime, copies)");
     }
     e->chain_valid = e->dense_chain = false;
     e->dom_next = step + 1;
@@ -2950,6 +2978,7 @@ void enqueue_band_unpack(gcs_engine* e)
                              reinterpret_cast<const int*>(e->dom_recv), e->dom_npeer, e->dom_cap, stride,
                              stride * (int)(band_record_bytes(e->prec) / sizeof(int)), e->dom_list ? 1 : 0, e->dom_send,
                              e->dom_npeer, stride);
+    dbg_sync(e, "dom: k_domain_unpack");
 }
 
 // one grouped send/recv of every peer's band (the count in its header row)

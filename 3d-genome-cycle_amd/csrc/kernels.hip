@@ -1267,9 +1267,14 @@ __global__ __launch_bounds__(256) void k_cell_sort(const DevCtx* __restrict__ ct
     sb[d] = pair_mix ? (float)k.z : 0.f;
     if (psort0) {  // list path: the current positions in slot order, .w = particle | class << 24; the slot's
                    // constants and bond CSR row (the list step reads them by slot, not behind the particle index)
-        (ctx->parity ? psort1 : psort0)[d] = mk4<R>(p.x, p.y, p.z, wpack<R>(i | (ptype[i] << kListIndexBits)));
+        // both parities: the step writes the next parity of the slots it integrates and the unpack both of the
+        // ghosts it receives, so a decomposed ghost that misses a record (its band over capacity, or it left the
+        // exchange region) keeps this build's record, never what the memory held before
+        const real4<R> rec = mk4<R>(p.x, p.y, p.z, wpack<R>(i | (ptype[i] << kListIndexBits)));
+        psort0[d] = rec;
+        psort1[d] = rec;
         if (fsort0)  // fp64: the list step's prefilter copy (put_slot)
-            (ctx->parity ? fsort1 : fsort0)[d] = make_float4((float)p.x, (float)p.y, (float)p.z, 0.f);
+            fsort0[d] = fsort1[d] = make_float4((float)p.x, (float)p.y, (float)p.z, 0.f);
         skmu[d] = k;
         const int2 row = boff ? make_int2(boff[i], boff[i + 1]) : make_int2(0, 0);
         sbrow[d] = row;
@@ -1436,7 +1441,9 @@ __device__ inline void local_terms(const DevCtx* __restrict__ ctx, const ForceAr
           real4<R> bvb[BB], pjb[BB];
 #pragma unroll
           for (int u = 0; u < BB; ++u) {
-              enb[u] = (q0 + u < ee) ? a.bent[q0 + u] : make_int2(i, kSemispring);
+              // (a batch's padding entries gather particle 0, never used: not `i`, which a lane that integrates
+              // nothing may hold unchecked -- a decomposed ghost's stale record)
+              enb[u] = (q0 + u < ee) ? a.bent[q0 + u] : make_int2(0, kSemispring);
               bvb[u] = (q0 + u < ee) ? bval[q0 + u] : mk4<R>(R(0), R(0), R(0), R(0));
           }
 #pragma unroll
@@ -3240,7 +3247,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     unsigned* const acc = a.lticket + kListAccBase + 32 * kAccWords * g;
 
     const int pk = wbits(pi.w);
-    const int i = pk & kIdx;
+    // (clamped: a decomposed ghost slot that missed its band record -- a band over capacity -- may hold a stale
+    // record of another build in this parity; such a lane integrates nothing, but its local terms index by i)
+    const int i = min(pk & kIdx, n - 1);
     const bool act = DOM ? (valid && s < ctx->lnslots && box_has(a.dom, (float)pi.x, (float)pi.y, (float)pi.z)) : valid;
     const R scale = a.pair_scaled ? cs : R(1);
     const R sa = P.pa_sig * scale, sbb = P.pb_sig * scale;

@@ -115,11 +115,20 @@ def test_motion_beyond_halo_is_reported(c1_design):
         run.check()
 
 
-def test_band_capacity_overflow_is_reported(c1_design):
+@pytest.mark.parametrize("poison", [None, "2"])
+def test_band_capacity_overflow_is_reported(c1_design, poison, monkeypatch):
+    """bands over capacity are flagged (the check raises).  With every allocation poisoned (GCS_DEBUG_POISON=2): the
+    ghosts that miss their records keep their build's record in both parities (kernels.hip k_cell_sort) and a lane
+    that integrates nothing never indexes by its record's particle -- round 6's suite faulted here once memory was
+    recycled (the stale ghost's garbage index gathered by the local terms' batch padding)"""
     cfg = InterphaseConfig()
-    run, _, _ = _decomposed(c1_design, cfg, 2, 2, cap=8)
+    if poison:
+        monkeypatch.setenv("GCS_DEBUG_POISON", poison)
+    run, doms, _ = _decomposed(c1_design, cfg, 2, 4, cap=8)
     with pytest.raises(domain.DomainError):
         run.check()
+    for d in doms:
+        d.e.close()
 
 
 def test_bond_beyond_halo_is_reported(c1_design):
@@ -257,12 +266,12 @@ def test_decomposed_run_twice_in_one_process(c1_design, prec, monkeypatch):
     wave (every lane, `act` masks only the results) followed that garbage bond row (kernels.hip k_cell_sort now
     writes a harmless record there).  The same decomposed case three times in this process, the third with every
     per-slot list buffer filled with hashed garbage at allocation (GCS_DEBUG_POISON): bit for bit the same positions
-    and context every time, the checks clear"""
+    and context every time, the checks clear (the third run with EVERY allocation poisoned, GCS_DEBUG_POISON=2)"""
     cfg = InterphaseConfig()
     outs = []
     for k in range(3):
         if k == 2:
-            monkeypatch.setenv("GCS_DEBUG_POISON", "1")
+            monkeypatch.setenv("GCS_DEBUG_POISON", "2")
         run, doms, _ = _decomposed(c1_design, cfg, 2, STEPS, prec=prec)
         run.check()
         outs.append((domain.gather_positions(run, c1_design.n), doms[0].context()))
