@@ -3021,15 +3021,23 @@ __device__ void list_totals(unsigned* base, int ngroups, ListTotals& t)
 // tile keeps the pair partners an XCD gathers within its own slab: each L2 fetches about 1/8 of the positions
 // instead of all of them.  A bijection of [0, G) (G need not be a multiple of 8); the dispatch order only affects
 // speed, never which tiles are processed.
+// Only for the 16-bit absolute lists (<= 65,536 particles: C1, C2, C4's trajectories): there every L2 would otherwise
+// fetch the whole position array, and the slabs win (same box, C2 fp64 4 trajectories 4.51-4.54 vs 4.39e9, single
+// 1.91 vs 1.83; fp32 6.14 vs 5.95).  Beyond (C5's plane-relative lists) the slabs lose: 1.92 vs 2.12e9 at C5 fp64,
+// k_lstep 223 vs 201 us, although the L2s fetch less (393 vs 508 MB per launch) -- a slab of a non-uniform system
+// is a non-uniform share of the work, and the round-robin dispatch runs at the pace of the XCD with the densest slab
+// (profiles/r06s_c5_l2_*.txt, r06t_xcd_remap_c2.txt)
+template <typename LE>
 __device__ __forceinline__ int xcd_block(int b, int G)
 {
 #if GCS_XCD_REMAP
-    const int x = b & 7, k = b >> 3, q = G >> 3, r = G & 7;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
-#else
+    if constexpr (sizeof(LE) == 2 && !ListFmt<LE>::rel) {
+        const int x = b & 7, k = b >> 3, q = G >> 3, r = G & 7;
+        return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+    }
+#endif
     (void)G;
     return b;
-#endif
 }
 
 #ifndef GCS_LBUILD_WAVES_PER_EU
@@ -3061,7 +3069,7 @@ __global__ __launch_bounds__(64 * kListWaves) __attribute__((amdgpu_waves_per_eu
     bool first = true;
     // the launch has force_grid(n) workgroups, the cell rows need ntiles (device-side): remap over the ones in use
     const int gused = min((int)gridDim.x, ntiles);
-    for (int tile = (int)blockIdx.x < gused ? xcd_block(blockIdx.x, gused) : ntiles; tile < ntiles;
+    for (int tile = (int)blockIdx.x < gused ? xcd_block<LE>(blockIdx.x, gused) : ntiles; tile < ntiles;
          tile += gridDim.x) {
         const int2 tr = a.tile_range[tile];
         const int s_begin = uniform(tr.x), s_end = uniform(tr.y);
@@ -3144,6 +3152,9 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 // per SIMD either spills (3.74e9 / 1.15e9)
 #define GCS_LIST_UNROLL64 4
 #endif
+#ifndef GCS_LIST_STORE_SC1
+#define GCS_LIST_STORE_SC1 0  // (experiment) fp64 step: the slot-order position stores write-through (sc1)
+#endif
 #ifndef GCS_LIST_PF_BATCH
 #define GCS_LIST_PF_BATCH 8  // fp64 step, prefilter: list entries per fp32 batch
 #endif
@@ -3198,7 +3209,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
     if (dbg && tid == 0) dbg[0] = wall_clock64();
     const int n = a.n;
     const FieldPrm<R>& P = St<R>::prm(a);
-    const int tile = xcd_block(blockIdx.x, gridDim.x);
+    const int tile = xcd_block<LE>(blockIdx.x, gridDim.x);
     const int s = tile * kTile + lane;
     const bool valid = s < n;
     const int sl = valid ? s : n - 1;
@@ -3525,6 +3536,15 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
             R4* __restrict__ pn = St<R>::pos(a, par ^ 1);  // particle order (see kLFlagPos)
             R4* __restrict__ qn = St<R>::psort(a, par ^ 1);
             if (!a.bslot || (flags & kLFlagPos)) pn[i] = mk4<R>(nxp, nyp, nzp, R(0));
+#if GCS_LIST_STORE_SC1
+            if constexpr (sizeof(R) == 8) {  // (experiment) write-through stores that do not keep the line in L2
+                typedef double d2v __attribute__((ext_vector_type(2)));
+                const d2v lo = {(double)nxp, (double)nyp}, hi = {(double)nzp, (double)pi.w};
+                double* const p = reinterpret_cast<double*>(qn + s);
+                asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(lo) : "memory");
+                asm volatile("global_store_dwordx4 %0, %1, off offset:16 sc1" ::"v"(p), "v"(hi) : "memory");
+            } else
+#endif
             qn[s] = mk4<R>(nxp, nyp, nzp, pi.w);
             if constexpr (sizeof(R) == 8) {  // the prefilter copy (put_slot's)
                 float4* const fn = St<R>::fsort(a, par ^ 1);
