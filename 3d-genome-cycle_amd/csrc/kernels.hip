@@ -3152,9 +3152,6 @@ __device__ __forceinline__ int lgrid_cell(const Grid& g, int k, float v)
 // per SIMD either spills (3.74e9 / 1.15e9)
 #define GCS_LIST_UNROLL64 4
 #endif
-#ifndef GCS_LIST_STORE_SC1
-#define GCS_LIST_STORE_SC1 0  // (experiment) fp64 step: the slot-order position stores write-through (sc1)
-#endif
 #ifndef GCS_LIST_PF_BATCH
 #define GCS_LIST_PF_BATCH 8  // fp64 step, prefilter: list entries per fp32 batch
 #endif
@@ -3536,15 +3533,6 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(CT ? GCS
             R4* __restrict__ pn = St<R>::pos(a, par ^ 1);  // particle order (see kLFlagPos)
             R4* __restrict__ qn = St<R>::psort(a, par ^ 1);
             if (!a.bslot || (flags & kLFlagPos)) pn[i] = mk4<R>(nxp, nyp, nzp, R(0));
-#if GCS_LIST_STORE_SC1
-            if constexpr (sizeof(R) == 8) {  // (experiment) write-through stores that do not keep the line in L2
-                typedef double d2v __attribute__((ext_vector_type(2)));
-                const d2v lo = {(double)nxp, (double)nyp}, hi = {(double)nzp, (double)pi.w};
-                double* const p = reinterpret_cast<double*>(qn + s);
-                asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(lo) : "memory");
-                asm volatile("global_store_dwordx4 %0, %1, off offset:16 sc1" ::"v"(p), "v"(hi) : "memory");
-            } else
-#endif
             qn[s] = mk4<R>(nxp, nyp, nzp, pi.w);
             if constexpr (sizeof(R) == 8) {  // the prefilter copy (put_slot's)
                 float4* const fn = St<R>::fsort(a, par ^ 1);
