@@ -53,8 +53,11 @@ for contacts, bits in [(True, b) for b in cbits] + [(False, 0)]:
     eng.synchronize()
     t2 = time.perf_counter()
     if contacts:
-        print(f"  contact bits {bits or 'default'}: last window's table {len(drv.last_contacts)} distinct pairs",
-              flush=True)
+        import hashlib
+        import numpy as np
+        digest = hashlib.sha1(np.ascontiguousarray(drv.last_contacts).tobytes()).hexdigest()[:16]
+        print(f"  contact bits {bits or 'default'}: last window's table {len(drv.last_contacts)} distinct pairs "
+              f"(sha1 {digest})", flush=True)
     print(f"contacts={contacts}: relaxation {relax} steps {t1 - t0:.2f} s; simulation {steps} steps {t2 - t1:.2f} s "
           f"= {steps / (t2 - t1):.0f} steps/s ({d.n * steps / (t2 - t1):.3e} bead-updates/s)", flush=True)
     r1 = eng.run_stats()
