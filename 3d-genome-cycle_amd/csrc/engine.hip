@@ -294,6 +294,7 @@ struct gcs_engine {
     int skin_level_pm = 0;      // the skin (1/1000 of the pair cutoff) of the current undecomposed list run (skin_level)
     int list_every_opt = 0;     // GCS_OPT_LIST_EVERY: rebuild period in steps (0: from the noise amplitude)
     int list_every = 1;         // the period of the current run
+    int list_skin_base_pm = 0;  // GCS_OPT_LIST_SKIN_BASE: the core-scale-following default skin's s1 (0: the precision's)
     int list_phase = 0;         // GCS_OPT_LIST_PHASE: rebuilds at the steps s with (s + list_phase) % list_every == 0
     int list_waves = 4;         // GCS_OPT_LIST_WAVES: waves per tile (2: more tiles resident, for replica runs)
     int list_fmt_opt = 0;       // GCS_OPT_LIST_FORMAT: 0 (default) 16-bit slots (absolute up to 65,536 particles,
@@ -877,7 +878,13 @@ bool rebuild_path(const gcs_engine* e, bool spacestep) { return eff_fused(e) == 
 // the precision's default skin at core scale 1.  The fp64 step gathers 32-B partners, so shorter lists pay for more
 // frequent rebuilds sooner than at fp32 (4-replica bench sweeps: fp32 profiles/r03_skin_sweep.txt, 500 per mille / 16
 // steps best; fp64 profiles/r04_skin_sweep_f64*.txt)
-int default_skin_pm(const gcs_engine* e) { return e->prec == 64 ? kListSkinPm64 : kListSkinPm32; }
+// (GCS_OPT_LIST_SKIN_BASE replaces s1: one trajectory alone on a GPU, e.g. a stage CLI, is latency-bound and
+// takes fewer rebuilds for longer lists -- profiles/r06g4_skin.txt)
+int default_skin_pm(const gcs_engine* e)
+{
+    if (e->list_skin_base_pm > 0) return e->list_skin_base_pm;
+    return e->prec == 64 ? kListSkinPm64 : kListSkinPm32;
+}
 
 // the list skin: the option, the current run's level (skin_level), or the default
 float list_skin(const gcs_engine* e)
@@ -3477,6 +3484,16 @@ int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value)
         if (value < 0 || value > 4000)
             return fail(GCS_EINVAL, "list skin must be in [1, 4000] per mille of the cutoff (0: the default)");
         e->list_skin_pm = (int)value;
+        drop_graph(e);
+        return GCS_OK;
+    }
+    if (option == GCS_OPT_LIST_SKIN_BASE) {
+        if (value < 0 || value > 4000)
+            return fail(GCS_EINVAL, "list skin base must be in [1, 4000] per mille of the cutoff (0: the default)");
+        if (e->dom && (int)value != e->list_skin_base_pm)
+            return fail(GCS_ESTATE, "the list skin base sizes a decomposed engine's binning halo: set it before the "
+                                    "domain");
+        e->list_skin_base_pm = (int)value;
         drop_graph(e);
         return GCS_OK;
     }

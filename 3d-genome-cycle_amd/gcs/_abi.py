@@ -47,6 +47,7 @@ OPT_LIST_DEAL = 16
 OPT_LIST_FORMAT = 17  # 0 default (16-bit slots, plane-relative beyond 65,536), 1 plane-relative, 2 32-bit
 OPT_SMALL_STEP = 18  # 1 default: the persistent all-pairs step for <= 1,536 particles; 0 off
 OPT_LIST_PHASE = 19  # list step: rebuild steps s with (s + phase) % period == 0 (staggered replicas)
+OPT_LIST_SKIN_BASE = 20  # list step: s1 of the core-scale-following default skin (0 = the precision's default)
 
 
 def list_deal(pattern: str) -> int:

@@ -90,6 +90,9 @@ def build_interphase(backend_cls, design, cfg: InterphaseConfig, **backend_kw):
     return sys_, handles
 
 
+SINGLE_SKIN_BASE_F64 = 400  # GCS_OPT_LIST_SKIN_BASE of a stage's one trajectory (per mille of the pair cutoff)
+
+
 class InterphaseDriver:
     """run_relaxation + run_simulation with the reference callback order, chunked at interval boundaries."""
 
@@ -103,6 +106,12 @@ class InterphaseDriver:
         self.context = initial_context(cfg)
         self.mean_energy = 0.0
         self._writer = None
+        # one trajectory alone on its GPU is latency-bound: at fp64 it takes longer lists and fewer rebuilds than the
+        # engine's default, which suits several trajectories per GPU (the 700k-step stage 1.1 % faster at s1 = 400
+        # than at 350 per mille, profiles/r06h2_skin_base.txt; trajectories stay bitwise reproducible for a given s1)
+        if getattr(system, "precision", None) == 64 and hasattr(system, "set_option"):
+            from . import _abi
+            system.set_option(_abi.OPT_LIST_SKIN_BASE, SINGLE_SKIN_BASE_F64)
 
     def _out(self):
         """the store's sampling writes, on a background writer for the length of a stage (gcs.store.AsyncWriter)"""

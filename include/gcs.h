@@ -70,7 +70,7 @@ extern "C" {
  *    gained density_probes; gcs_list_stats gained deal; GCS_OPT_SMALL_PATH and GCS_OPT_FUSED_STEP 1 are gone;
  *    later in 3 (additive, no layout change): GCS_OPT_LIST_FORMAT; the default list skin follows the core scale;
  *    GCS_OPT_SMALL_STEP; GCS_ESTATE also reports a stalled cross-workgroup hand-off (round 6: GCS_OPT_LIST_FORMAT 3,
- *    an experiment, was removed) */
+ *    an experiment, was removed; GCS_OPT_LIST_PHASE, GCS_OPT_LIST_SKIN_BASE added) */
 #define GCS_ABI_VERSION 3
 
 /* arithmetic precision of an engine (gcs_system_desc.precision) */
@@ -401,6 +401,11 @@ int gcs_engine_domain_flags(gcs_engine* e, int32_t* flags);
                                      one's short cell kernels overlap the others' step kernels; a trajectory is bitwise
                                      reproducible for a given phase (its lists' entry order, hence its sums' order,
                                      follows the rebuild steps) */
+#define GCS_OPT_LIST_SKIN_BASE 20 /* list step: the skin at core scale 1 that the default skin follows (s1 sqrt(cs) at fp64,
+                                     s1 cs at fp32; 0 = the precision's default, 350 / 500 per mille).  The default
+                                     suits several trajectories per GPU; one trajectory alone (the stage drivers) is
+                                     latency-bound and prefers longer lists and fewer rebuilds.  Set before a
+                                     decomposed engine's domain (it sizes the binning halo) */
 int gcs_engine_set_option(gcs_engine* e, int32_t option, int64_t value);
 
 /* List-step diagnostics (the neighbour lists md::neighbor_searcher keeps between rebuilds; micromd, called at

@@ -570,6 +570,28 @@ def test_list_phase_staggers_rebuilds(c1_design, prec):
     assert xs[(3, (48,))][1]["builds"] == xs[(3, (20, 28))][1]["builds"]
 
 
+def test_list_skin_base(c1_design):
+    """GCS_OPT_LIST_SKIN_BASE (the stage drivers' one-trajectory skin, gcs/interphase.py SINGLE_SKIN_BASE_F64): the
+    default skin follows s1 sqrt(cs) with s1 = 400 instead of 350 per mille (fp64) -- longer lists, fewer rebuilds,
+    the same pair set: within the fp64 bound of the oracle; 0 is the default again"""
+    cfg = InterphaseConfig()
+    o, _ = interphase.build_interphase(oracle.OracleSystem, c1_design, cfg, precision=64)
+    o.set_schedule(**interphase.interphase_schedule(cfg))
+    o.set_context(LATE)
+    o.run(48, first_step=LATE["step"], temperature=cfg.temperature, timestep=cfg.timestep, seed=11)
+    stats = {}
+    for base in (0, 400):
+        e = _list_engine(c1_design, cfg, 64, list_skin_base=base)
+        e.set_schedule(**interphase.interphase_schedule(cfg))
+        e.set_context(LATE)
+        e.run(48, first_step=LATE["step"], temperature=cfg.temperature, timestep=cfg.timestep, seed=11)
+        assert np.abs(e.get_positions() - o.get_positions()).max() <= TOL_X[64]
+        stats[base] = e.list_stats()
+        e.close()
+    assert stats[400]["skin"] == pytest.approx(stats[0]["skin"] * 400 / 350, rel=1e-5)
+    assert stats[400]["rebuild_every"] > stats[0]["rebuild_every"]
+
+
 def _format_run(design, cfg, prec, fmt, steps, ctx=LATE, seed=11, **opts):
     e = _list_engine(design, cfg, prec, list_format=fmt, **opts)
     e.set_schedule(**interphase.interphase_schedule(cfg))

@@ -3,7 +3,7 @@ cadence: contact map every 20 steps, energy + sampled frame every 1,000, contact
 each engine call the driver makes, the run statistics (graph replays / eager steps / captures), and the same stretch
 without the contact map.  No store (the frames' HDF5 writes run on a background writer in the stage CLI anyway).
 
-usage: python tools/interphase_probe.py [steps] [relaxation_steps]"""
+usage: python tools/interphase_probe.py [steps] [relaxation_steps] [contact bits,...] [list skin bases,...]"""
 import sys
 import time
 from collections import defaultdict
@@ -18,6 +18,7 @@ from gcs.engine import Engine  # noqa: E402
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 relax = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
 cbits = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0]  # GCS_OPT_CONTACT_BITS (0: default)
+bases = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [0]  # GCS_OPT_LIST_SKIN_BASE (0: default)
 
 
 def timed(eng, acc):
@@ -36,10 +37,14 @@ def timed(eng, acc):
 
 
 d = synthetic.make_c2(1)
-for contacts, bits in [(True, b) for b in cbits] + [(False, 0)]:
+for contacts, bits, base in [(True, b, bases[0]) for b in cbits] + [(True, cbits[0], b) for b in bases[1:]] + \
+        [(False, 0, bases[0])]:
     cfg = InterphaseConfig()
     eng, _ = interphase.build_interphase(Engine, d, cfg)
     eng.set_option(_abi.OPT_CONTACT_BITS, bits)
+    eng.set_option(_abi.OPT_LIST_SKIN_BASE, base)
+    if base:
+        print(f"  list skin base {base}", flush=True)
     eng.set_option(_abi.OPT_DENSE_NEIGHBORS, 0)  # C2 is list-step territory; the probe upsets rocprofv3 (engine.hip)
     acc = defaultdict(lambda: [0.0, 0])
     timed(eng, acc)
