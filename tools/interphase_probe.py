@@ -18,7 +18,7 @@ from gcs.engine import Engine  # noqa: E402
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 relax = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
 cbits = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0]  # GCS_OPT_CONTACT_BITS (0: default)
-bases = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [0]  # GCS_OPT_LIST_SKIN_BASE (0: default)
+bases = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [0]  # GCS_OPT_LIST_SKIN_BASE (0: the driver's)
 
 
 def timed(eng, acc):
@@ -42,13 +42,14 @@ for contacts, bits, base in [(True, b, bases[0]) for b in cbits] + [(True, cbits
     cfg = InterphaseConfig()
     eng, _ = interphase.build_interphase(Engine, d, cfg)
     eng.set_option(_abi.OPT_CONTACT_BITS, bits)
-    eng.set_option(_abi.OPT_LIST_SKIN_BASE, base)
-    if base:
-        print(f"  list skin base {base}", flush=True)
+
     eng.set_option(_abi.OPT_DENSE_NEIGHBORS, 0)  # C2 is list-step territory; the probe upsets rocprofv3 (engine.hip)
     acc = defaultdict(lambda: [0.0, 0])
     timed(eng, acc)
     drv = interphase.InterphaseDriver(eng, d, cfg, store=None, log=None)
+    if base:  # (after the driver, which sets its own: gcs/interphase.py SINGLE_SKIN_BASE_F64)
+        eng.set_option(_abi.OPT_LIST_SKIN_BASE, base)
+        print(f"  list skin base {base}", flush=True)
     t0 = time.perf_counter()
     drv.run_relaxation(relax)
     eng.synchronize()
