@@ -337,3 +337,17 @@ def test_decomposed_skin_follows_core_scale(c1_design, prec, graph):
     single = eng()
     single.run(70, first_step=0, temperature=cfg.temperature, timestep=cfg.timestep, seed=SEED)
     assert np.abs(single.get_positions() - xd).max() <= X[prec]
+
+
+def test_skin_base_fixed_once_decomposed(c1_design):
+    """GCS_OPT_LIST_SKIN_BASE sizes a decomposed engine's binning halo (engine.hip list_skin_max): once the engine has
+    its domain a change is refused (GCS_ESTATE), setting the value it already has is not"""
+    cfg = InterphaseConfig()
+    run, doms, _ = _decomposed(c1_design, cfg, 2, 2, prec=64)
+    e = doms[0].e
+    e.set_option(A.OPT_LIST_SKIN_BASE, 0)
+    with pytest.raises(A.GcsError):
+        e.set_option(A.OPT_LIST_SKIN_BASE, 400)
+    run.check()
+    for d in doms:
+        d.e.close()
