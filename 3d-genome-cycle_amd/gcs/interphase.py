@@ -94,7 +94,9 @@ SINGLE_SKIN_BASE_F64 = 400  # GCS_OPT_LIST_SKIN_BASE of a stage's one trajectory
 
 
 class InterphaseDriver:
-    """run_relaxation + run_simulation with the reference callback order, chunked at interval boundaries."""
+    """run_relaxation + run_simulation with the reference callback order, chunked at interval boundaries.  On an fp64
+    engine it sets GCS_OPT_LIST_SKIN_BASE to SINGLE_SKIN_BASE_F64 (the stage's one trajectory; set the option again
+    after construction to override)."""
 
     def __init__(self, system, design, cfg: InterphaseConfig, store=None, log=sys.stderr):
         self.sys = system
