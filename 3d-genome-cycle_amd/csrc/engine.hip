@@ -934,6 +934,9 @@ void dbg_sync(gcs_engine* e, const char* what)
 {
     static const bool on = std::getenv("GCS_DEBUG_SYNC") != nullptr;
     if (!on) return;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(e->stream, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone)
+        return;  // (a graph being captured: nothing runs until it is launched)
     hipError_t he = hipStreamSynchronize(e->stream);
     if (he == hipSuccess) he = hipGetLastError();
     if (he != hipSuccess) std::fprintf(stderr, "GCS_DEBUG_SYNC: the stream failed after %s: %s\n", what, hipGetErrorString(he));
